@@ -1,0 +1,330 @@
+"""Generate golden parity vectors by running the REFERENCE implementation (this container only).
+
+Usage (from the repo root, in the build container where /root/reference exists):
+    python tests/golden/gen_golden.py
+
+The reference is imported read-only from /root/reference with the off-path modules stubbed
+(cv2/addict/imageio/skimage/torchvision are only used by data loading,
+camera-matrix decomposition and logging, none of which is on the render path).  Only inputs
+and outputs are written (small .npz files under tests/golden/); weights are rebuilt from seeds
+by tests/golden/weightgen.py.  Nothing here is imported by the product or by the GPU tests.
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import weightgen as wg  # noqa: E402
+
+REF = '/root/reference'
+
+
+def _import_reference():
+    for name in ['cv2', 'addict', 'imageio', 'skimage', 'skimage.transform', 'torchvision',
+                 'torchvision.utils']:
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules['addict'].Dict = dict
+    sys.modules['skimage.transform'].rescale = None
+    sys.modules['skimage'].transform = sys.modules['skimage.transform']
+    sys.path.insert(0, REF)
+    from models.frameworks import neus, volsdf, unisurf  # noqa
+    from models import base, ray_casting  # noqa
+    from utils import rend_util, train_util  # noqa
+    return types.SimpleNamespace(neus=neus, volsdf=volsdf, unisurf=unisurf, base=base,
+                                 ray_casting=ray_casting, rend_util=rend_util, train_util=train_util)
+
+
+SURF = dict(use_siren=False, embed_multires=6, geometric_init=True, D=8, W=256, skips=[4])
+
+
+def _np(d):
+    out = {}
+    for k, v in d.items():
+        if isinstance(v, torch.Tensor):
+            v = v.detach().cpu()
+            out[k] = v.numpy() if v.dtype != torch.bool else v.numpy().astype(np.uint8)
+        else:
+            out[k] = np.asarray(v)
+    return out
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **_np(arrays))
+    print('wrote', path, os.path.getsize(path), 'bytes')
+
+
+def camera_rays(R, key, idx=None):
+    H, W, f, dist = wg.CAMERAS[key]
+    c2w = wg.look_at_c2w(dist)[None]
+    K = wg.intrinsics(f, H, W)[None]
+    rays_o, rays_d, _ = R.rend_util.get_rays(c2w, K, H, W, N_rays=-1)
+    if idx is not None:
+        rays_o, rays_d = rays_o[:, idx], rays_d[:, idx]
+    return rays_o.contiguous(), rays_d.contiguous()
+
+
+def grid_idx(H, W, n=8, lo=0.15, hi=0.85):
+    rows = np.linspace(lo * (H - 1), hi * (H - 1), n).round().astype(np.int64)
+    cols = np.linspace(lo * (W - 1), hi * (W - 1), n).round().astype(np.int64)
+    return torch.tensor((rows[:, None] * W + cols[None, :]).reshape(-1))
+
+
+def gen_components(R):
+    torch.manual_seed(123)
+    # Embedders (A3)
+    x = torch.randn(256, 3) * 1.5
+    x4 = torch.randn(256, 4)
+    e6, _ = R.base.get_embedder(6)
+    e4, _ = R.base.get_embedder(4)
+    e10, _ = R.base.get_embedder(10, input_dim=4)
+    save('embed.npz', x=x, x4=x4, emb6=e6(x), emb4=e4(x), emb10_4d=e10(x4))
+
+    # SDF net (A4-A6) with NeuS config
+    sd = wg.neus_state(seed=11)
+    surf = R.base.ImplicitSurface(W_geo_feat=256, input_ch=3, obj_bounding_size=1.0, radius_init=0.5, **SURF)
+    surf.load_state_dict({k[len('implicit_surface.'):]: v for k, v in sd.items()
+                          if k.startswith('implicit_surface.')})
+    pts = torch.randn(512, 3) * 0.6
+    with torch.no_grad():
+        sdf_ng, h_ng = surf.forward(pts, return_h=True)
+    sdf, nab, h = surf.forward_with_nablas(pts)
+    save('sdf_net.npz', seed=11, pts=pts, sdf_nograd=sdf_ng, sdf=sdf, nablas=nab, h=h[:64], h_nograd=h_ng[:64])
+
+    # Radiance nets (A7): NeuS cfg (view embed 4) and VolSDF cfg (identity embeds)
+    rad_n = R.base.RadianceNet(W_geo_feat=256, embed_multires=-1, embed_multires_view=4, use_view_dirs=True,
+                               D=4, W=256, skips=[])
+    rad_n.load_state_dict({k[len('radiance_net.'):]: v for k, v in sd.items() if k.startswith('radiance_net.')})
+    sdv = wg.volsdf_state(seed=12)
+    rad_v = R.base.RadianceNet(W_geo_feat=256, embed_multires=-1, embed_multires_view=-1, use_view_dirs=True,
+                               D=4, W=256, skips=[])
+    rad_v.load_state_dict({k[len('radiance_net.'):]: v for k, v in sdv.items() if k.startswith('radiance_net.')})
+    P = 256
+    rx = torch.randn(P, 3) * 0.5
+    rv = torch.nn.functional.normalize(torch.randn(P, 3), dim=-1)
+    rn = torch.randn(P, 3)
+    rf = torch.randn(P, 256) * 0.3
+    with torch.no_grad():
+        out_n = rad_n(rx, rv, rn, rf)
+        out_v = rad_v(rx, rv, rn, rf)
+    save('radiance.npz', seed_neus=11, seed_volsdf=12, x=rx, v=rv, n=rn, f=rf, rgb_neus=out_n, rgb_volsdf=out_v)
+
+    # NeRF++ background net (A8)
+    sdo = wg.neus_state(seed=13, use_outside_nerf=True)
+    nerf = R.base.NeRF(input_ch=4, multires=10, multires_view=4, use_view_dirs=True)
+    nerf.load_state_dict({k[len('nerf_outside.'):]: v for k, v in sdo.items() if k.startswith('nerf_outside.')})
+    p = torch.randn(P, 3) * 3.0
+    r = p.norm(dim=-1, keepdim=True)
+    x4 = torch.cat([p / r, 1. / r], dim=-1)
+    with torch.no_grad():
+        sig, rgb = nerf(x4, rv)
+    save('nerf.npz', seed=13, x4=x4, v=rv, sigma=sig, rgb=rgb)
+
+
+def gen_sampling(R):
+    torch.manual_seed(7)
+    ru = R.rend_util
+    # sample_pdf: random weights, plus rows with zeros, one-hot mass, ties in bins
+    Rn, L = 64, 33
+    bins = torch.sort(torch.rand(Rn, L) * 4.0, dim=-1).values
+    bins[3, 5:9] = bins[3, 5]          # repeated bins
+    w = torch.rand(Rn, L - 1)
+    w[0] = 0.0                          # all-zero weights (uniform after +1e-5)
+    w[1] = 0.0; w[1, 7] = 1.0           # one-hot
+    w[2, :16] = 0.0                     # half empty
+    w[4] = 1e-7
+    s16 = ru.sample_pdf(bins, w, 16, det=True)
+    s66 = ru.sample_pdf(bins, w, 66, det=True)
+    u_rand = torch.rand(Rn, 16)
+    # reproduce det=False with an explicit u by monkeypatching torch.rand inside the call
+    orig = torch.rand
+    try:
+        torch.rand = lambda *a, **k: u_rand.clone()
+        s_rand = ru.sample_pdf(bins, w, 16, det=False)
+    finally:
+        torch.rand = orig
+    cdf_in = torch.cumsum(torch.rand(Rn, L - 1), -1)
+    cdf_in = cdf_in / cdf_in[:, -1:]
+    sc = ru.sample_cdf(bins, cdf_in, 24, det=True)
+    # near/far & sphere intersections
+    o = torch.randn(Rn, 3) * 2.0
+    d = torch.nn.functional.normalize(torch.randn(Rn, 3), dim=-1)
+    near, far = ru.near_far_from_sphere(o, d, r=1.0)
+    near4, far4 = ru.near_far_from_sphere(o, d, r=4.0, keepdim=False)
+    n_i, f_i, m_i = ru.get_sphere_intersection(o, d, r=1.0)
+    o_in = torch.nn.functional.normalize(torch.randn(Rn, 3), dim=-1) * 0.9
+    rs = 3.0 / torch.flip(torch.linspace(0, 1, 34)[1:-1], dims=[-1])
+    dv = ru.get_dvals_from_radius(o_in * 2.0, d, rs.expand(Rn, 32))
+    save('sampling.npz', bins=bins, weights=w, s16=s16, s66=s66, u_rand=u_rand, s_rand=s_rand,
+         cdf_in=cdf_in, s_cdf=sc, o=o, d=d, near=near, far=far, near4=near4, far4=far4,
+         si_near=n_i, si_far=f_i, si_mask=m_i, o_in=o_in * 2.0, rs=rs, dvals=dv)
+
+    # get_rays: matrix and quaternion forms, plus random pixel selection
+    H, W = 12, 20
+    c2w = wg.look_at_c2w(2.5)[None]
+    K = wg.intrinsics(25.0, H, W)[None]
+    K[0, 0, 1] = 0.3   # skew
+    ro, rd, si = ru.get_rays(c2w, K, H, W, N_rays=-1)
+    # NOTE: the quaternion branch (rend_util.py:114-119) cannot run: quat_to_rot unpacks two prefix
+    # dims (rend_util.py:77) that get_rays' bmm path cannot accept, so it is not pinned here.
+    torch.manual_seed(5)
+    ror, rdr, sir = ru.get_rays(c2w, K, H, W, N_rays=37)
+    save('get_rays.npz', H=H, W=W, c2w=c2w, K=K, rays_o=ro, rays_d=rd,
+         rays_o_sel=ror, rays_d_sel=rdr, select_inds=sir)
+
+
+def _neus_model(R, sd, use_outside_nerf):
+    m = R.neus.NeuS(variance_init=0.05, speed_factor=10.0, input_ch=3, W_geo_feat=256,
+                    use_outside_nerf=use_outside_nerf, obj_bounding_radius=1.0,
+                    surface_cfg=dict(radius_init=0.5, **SURF),
+                    radiance_cfg=dict(use_siren=False, embed_multires=-1, embed_multires_view=4,
+                                      use_view_dirs=True, D=4, W=256, skips=[]))
+    m.load_state_dict(sd)
+    return m.eval()
+
+
+def gen_neus(R):
+    # config (b): NeuS 64x64 camera, 64-ray sub-grid
+    sd = wg.neus_state(seed=1)
+    model = _neus_model(R, sd, False)
+    H, W, _, _ = wg.CAMERAS['b']
+    idx = grid_idx(H, W)
+    ro, rd = camera_rays(R, 'b', idx)
+    with torch.no_grad():
+        rgb, depth, ex = R.neus.volume_render(
+            ro, rd, model, obj_bounding_radius=1.0, batched=True, calc_normal=True, detailed_output=True,
+            perturb=False, N_samples=64, N_importance=64, N_outside=0, upsample_algo='official_solution',
+            N_upsample_iters=4)
+    save('neus_b.npz', seed=1, rays_o=ro, rays_d=rd, idx=idx, rgb=rgb, depth=depth,
+         mask=ex['mask_volume'], normals=ex['normals_volume'], d_final=ex['d_final'],
+         sdf=ex['implicit_surface'], nablas=ex['implicit_nablas'], radiance=ex['radiance'],
+         alpha=ex['alpha'], cdf=ex['cdf'], weights=ex['visibility_weights'])
+
+    # NeuS direct_use / direct_more upsampling variants (12 rays)
+    sub = slice(20, 32)
+    outs = {}
+    for algo in ['direct_use', 'direct_more']:
+        with torch.no_grad():
+            rgb2, depth2, ex2 = R.neus.volume_render(
+                ro[:, sub], rd[:, sub], model, obj_bounding_radius=1.0, batched=True, calc_normal=True,
+                detailed_output=True, perturb=False, N_samples=64, N_importance=64, upsample_algo=algo,
+                N_nograd_samples=512)
+        outs[algo + '_rgb'] = rgb2
+        outs[algo + '_depth'] = depth2
+        outs[algo + '_d_final'] = ex2['d_final']
+    save('neus_algos.npz', seed=1, rays_o=ro[:, sub], rays_d=rd[:, sub], N_nograd_samples=512, **outs)
+
+    # config (d): NeuS + NeRF++ background, 800x600 camera sub-grid
+    sd = wg.neus_state(seed=4, use_outside_nerf=True)
+    model = _neus_model(R, sd, True)
+    H, W, _, _ = wg.CAMERAS['d']
+    idx = grid_idx(H, W, n=8, lo=0.02, hi=0.98)
+    ro, rd = camera_rays(R, 'd', idx)
+    with torch.no_grad():
+        rgb, depth, ex = R.neus.volume_render(
+            ro, rd, model, obj_bounding_radius=1.0, batched=True, calc_normal=True, detailed_output=True,
+            perturb=False, N_samples=64, N_importance=64, N_outside=32, upsample_algo='official_solution',
+            N_upsample_iters=4)
+    save('neus_d.npz', seed=4, rays_o=ro, rays_d=rd, idx=idx, rgb=rgb, depth=depth,
+         mask=ex['mask_volume'], normals=ex['normals_volume'], d_final=ex['d_final'],
+         sdf=ex['implicit_surface'], nablas=ex['implicit_nablas'], radiance=ex['radiance'],
+         alpha=ex['alpha'], weights=ex['visibility_weights'], sigma_out=ex['sigma_out'],
+         radiance_out=ex['radiance_out'])
+
+
+def _volsdf_model(R, sd, beta_init):
+    m = R.volsdf.VolSDF(beta_init=beta_init, speed_factor=10.0, input_ch=3, W_geo_feat=256,
+                        obj_bounding_radius=3.0, use_nerfplusplus=False,
+                        surface_cfg=dict(radius_init=1.0, **SURF),
+                        radiance_cfg=dict(use_siren=False, embed_multires=-1, embed_multires_view=-1,
+                                          use_view_dirs=True, D=4, W=256, skips=[]))
+    m.load_state_dict(sd)
+    return m.eval()
+
+
+def gen_volsdf(R):
+    # config (a): 16x32 camera, 512 rays, beta 0.1, 64+64
+    sd = wg.volsdf_state(seed=2, beta_init=0.1)
+    model = _volsdf_model(R, sd, 0.1)
+    ro, rd = camera_rays(R, 'a')
+    with torch.no_grad():
+        rgb, depth, ex = R.volsdf.volume_render(
+            ro, rd, model, near=0.0, far=6.0, obj_bounding_radius=3.0, batched=True, calc_normal=True,
+            detailed_output=True, perturb=False, N_samples=64, N_importance=64, max_upsample_steps=6)
+    keep = slice(0, 512, 8)
+    save('volsdf_a.npz', seed=2, beta_init=0.1, rays_o=ro, rays_d=rd, rgb=rgb, depth=depth,
+         mask=ex['mask_volume'], normals=ex['normals_volume'], beta_map=ex['beta_map'],
+         iter_usage=ex['iter_usage'], d_vals=ex['d_vals'][:, keep], sdf=ex['implicit_surface'][:, keep],
+         weights=ex['visibility_weights'][:, keep], radiance=ex['radiance'][:, keep])
+
+    # config (c): 32x64 camera sub-grid, beta 1e-3 (adaptive loop active), 128+128
+    sd = wg.volsdf_state(seed=5, beta_init=1e-3)
+    model = _volsdf_model(R, sd, 1e-3)
+    H, W, _, _ = wg.CAMERAS['c']
+    idx = grid_idx(H, W, n=8, lo=0.05, hi=0.95)
+    ro, rd = camera_rays(R, 'c', idx)
+    with torch.no_grad():
+        rgb, depth, ex = R.volsdf.volume_render(
+            ro, rd, model, near=0.0, far=6.0, obj_bounding_radius=3.0, batched=True, calc_normal=True,
+            detailed_output=True, perturb=False, N_samples=128, N_importance=128, max_upsample_steps=6)
+    save('volsdf_c.npz', seed=5, beta_init=1e-3, rays_o=ro, rays_d=rd, idx=idx, rgb=rgb, depth=depth,
+         mask=ex['mask_volume'], normals=ex['normals_volume'], beta_map=ex['beta_map'],
+         iter_usage=ex['iter_usage'], d_vals=ex['d_vals'], sdf=ex['implicit_surface'],
+         weights=ex['visibility_weights'])
+
+    # error_bound / sdf_to_sigma on a 1-D analytic SDF (debug_tools/test_volsdf_algo.py:73-87 shape)
+    x = torch.linspace(0, 6.0, 128)
+    y1 = -x + 1.65; y2 = x - 1.55; y3 = -x + 2.05
+    sdf1d = torch.where(x < 1.8, torch.where(x < 1.6, y1, y2), y3)
+    beta = 0.003
+    b1 = R.volsdf.error_bound(x, sdf1d, 1. / beta, beta)
+    bplus = float(np.sqrt(36.0 / (4 * 127 * np.log(1.1))))
+    b2 = R.volsdf.error_bound(x, sdf1d, 1. / bplus, bplus)
+    sg = R.volsdf.sdf_to_sigma(sdf1d, 1. / beta, beta)
+    save('volsdf_1d.npz', x=x, sdf=sdf1d, beta=beta, bplus=bplus, bounds_net=b1, bounds_plus=b2, sigma=sg)
+
+
+def gen_unisurf(R):
+    sd = wg.unisurf_state(seed=3)
+    m = R.unisurf.UNISURF(W_geo_feat=256, surface_cfg=dict(radius_init=1.0, **SURF),
+                          radiance_cfg=dict(use_siren=False, embed_multires=-1, embed_multires_view=-1,
+                                            use_view_dirs=True, D=4, W=256, skips=[]))
+    m.load_state_dict(sd)
+    m.eval()
+    H, W, _, _ = wg.CAMERAS['e']
+    idx = grid_idx(H, W, n=8, lo=0.1, hi=0.9)
+    ro, rd = camera_rays(R, 'e', idx)
+    logit_tau = R.unisurf.UNISURF.get_surface_from_opacity(0.5)
+    res = {}
+    for tag, nc in [('', 1048576), ('_nc1000', 1000)]:
+        with torch.no_grad():
+            rgb, depth, ex = R.unisurf.volume_render(
+                ro, rd, m, batched=True, calc_normal=True, detailed_output=True, perturb=False,
+                logit_tau=logit_tau, radius_of_interest=4.0, interval=1.0, N_query=64, N_freespace=32,
+                netchunk=nc)
+        res.update({'rgb' + tag: rgb, 'depth' + tag: depth, 'mask' + tag: ex['mask_volume'],
+                    'normals' + tag: ex['normals_volume']})
+        if tag == '':
+            res.update(dict(depth_surface=ex['depth_surface'], mask_surface=ex['mask_surface'],
+                            surface_points=ex['surface_points'], sdf=ex['implicit_surface'],
+                            nablas=ex['implicit_nablas'], radiance=ex['radiance'],
+                            weights=ex['visibility_weights']))
+    save('unisurf_e.npz', seed=3, logit_tau=float(logit_tau), rays_o=ro, rays_d=rd, idx=idx, **res)
+
+
+def main():
+    torch.set_num_threads(8)
+    R = _import_reference()
+    gen_components(R)
+    gen_sampling(R)
+    gen_neus(R)
+    gen_volsdf(R)
+    gen_unisurf(R)
+
+
+if __name__ == '__main__':
+    main()

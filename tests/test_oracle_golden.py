@@ -1,0 +1,165 @@
+"""Pin the oracle (CPU restatement) against golden vectors produced by the real reference.
+
+CPU-only.  The oracle runs the same fp32 torch CPU kernels as the reference, so agreement is at
+rounding level; tolerances below are written per quantity.
+"""
+import numpy as np
+import pytest
+import torch
+
+import weightgen as wg
+from oracle import nets, rays
+from oracle.neus import NeuSOracle, sdf_to_alpha, alpha_to_w
+from oracle.volsdf import VolSDFOracle, error_bound, sdf_to_sigma
+from oracle.unisurf import UNISURFOracle
+
+T = lambda a: torch.from_numpy(np.asarray(a))
+
+
+def close(a, b, rtol=1e-5, atol=1e-6):
+    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+    np.testing.assert_allclose(a, np.asarray(b), rtol=rtol, atol=atol)
+
+
+def test_embed(golden):
+    g = golden('embed')
+    close(nets.embed(T(g['x']), 6), g['emb6'], 0, 0)
+    close(nets.embed(T(g['x']), 4), g['emb4'], 0, 0)
+    close(nets.embed(T(g['x4']), 10), g['emb10_4d'], 0, 0)
+
+
+def test_sdf_net(golden):
+    g = golden('sdf_net')
+    net = nets.SDFNet(wg.neus_state(seed=int(g['seed'])))
+    s, h = net.forward(T(g['pts']))
+    close(s, g['sdf_nograd'], 1e-6, 1e-7)
+    close(h[:64], g['h_nograd'], 1e-6, 1e-7)
+    s, n, h = net.forward_with_nablas(T(g['pts']))
+    close(s, g['sdf'], 1e-6, 1e-7)
+    close(n, g['nablas'], 1e-5, 1e-6)
+
+
+def test_radiance_nets(golden):
+    g = golden('radiance')
+    rn = nets.RadianceNet(wg.neus_state(seed=int(g['seed_neus'])), multires_view=4)
+    rv = nets.RadianceNet(wg.volsdf_state(seed=int(g['seed_volsdf'])), multires_view=-1)
+    args = [T(g[k]) for k in ('x', 'v', 'n', 'f')]
+    close(rn.forward(*args), g['rgb_neus'], 1e-6, 1e-7)
+    close(rv.forward(*args), g['rgb_volsdf'], 1e-6, 1e-7)
+
+
+def test_nerf(golden):
+    g = golden('nerf')
+    net = nets.NeRFNet(wg.neus_state(seed=int(g['seed']), use_outside_nerf=True))
+    s, c = net.forward(T(g['x4']), T(g['v']))
+    close(s, g['sigma'], 1e-6, 1e-6)
+    close(c, g['rgb'], 1e-6, 1e-7)
+
+
+def test_sampling(golden):
+    g = golden('sampling')
+    bins, w = T(g['bins']), T(g['weights'])
+    close(rays.sample_pdf(bins, w, 16, det=True), g['s16'], 0, 0)
+    close(rays.sample_pdf(bins, w, 66, det=True), g['s66'], 0, 0)
+    close(rays.sample_pdf(bins, w, 16, det=False, u=T(g['u_rand'])), g['s_rand'], 0, 0)
+    close(rays.sample_cdf(bins, T(g['cdf_in']), 24, det=True), g['s_cdf'], 0, 0)
+    o, d = T(g['o']), T(g['d'])
+    n, f = rays.near_far_from_sphere(o, d, 1.0)
+    close(n, g['near'], 0, 0); close(f, g['far'], 0, 0)
+    n, f = rays.near_far_from_sphere(o, d, 4.0, keepdim=False)
+    close(n, g['near4'], 0, 0); close(f, g['far4'], 0, 0)
+    n, f, m = rays.sphere_intersection(o, d, 1.0)
+    close(n, g['si_near'], 0, 0); close(f, g['si_far'], 0, 0); close(m.numpy().astype(np.uint8), g['si_mask'], 0, 0)
+    close(rays.dvals_from_radius(T(g['o_in']), d, T(g['rs']).expand(o.shape[0], -1)), g['dvals'], 0, 0)
+
+
+def test_get_rays(golden):
+    g = golden('get_rays')
+    H, W = int(g['H']), int(g['W'])
+    ro, rd, _ = rays.get_rays(T(g['c2w']), T(g['K']), H, W)
+    close(ro, g['rays_o'], 0, 0)
+    close(rd, g['rays_d'], 1e-6, 1e-7)
+    ro, rd, _ = rays.get_rays(T(g['c2w']), T(g['K']), H, W, select_inds=T(g['select_inds']))
+    close(rd, g['rays_d_sel'], 1e-6, 1e-7)
+
+
+def test_neus_b(golden):
+    g = golden('neus_b')
+    orc = NeuSOracle(wg.neus_state(seed=int(g['seed'])))
+    with torch.no_grad():
+        out = orc.render(T(g['rays_o']), T(g['rays_d']))
+    close(out['d_final'], g['d_final'], 1e-6, 1e-6)
+    close(out['implicit_surface'], g['sdf'], 1e-5, 1e-6)
+    close(out['implicit_nablas'], g['nablas'], 1e-5, 1e-6)
+    close(out['radiance'], g['radiance'], 1e-5, 1e-6)
+    close(out['visibility_weights'], g['weights'], 1e-5, 1e-6)
+    close(out['rgb'], g['rgb'], 1e-5, 1e-6)
+    close(out['depth_volume'], g['depth'], 1e-5, 1e-6)
+    close(out['mask_volume'], g['mask'], 1e-5, 1e-6)
+    close(out['normals_volume'], g['normals'], 1e-5, 1e-6)
+
+
+def test_neus_upsample_variants(golden):
+    g = golden('neus_algos')
+    orc = NeuSOracle(wg.neus_state(seed=int(g['seed'])))
+    for algo in ['direct_use', 'direct_more']:
+        with torch.no_grad():
+            out = orc.render(T(g['rays_o']), T(g['rays_d']), upsample_algo=algo,
+                             N_nograd_samples=int(g['N_nograd_samples']))
+        close(out['d_final'], g[algo + '_d_final'], 1e-6, 1e-6)
+        close(out['rgb'], g[algo + '_rgb'], 1e-5, 1e-6)
+        close(out['depth_volume'], g[algo + '_depth'], 1e-5, 1e-6)
+
+
+def test_neus_d_nerfpp(golden):
+    g = golden('neus_d')
+    orc = NeuSOracle(wg.neus_state(seed=int(g['seed']), use_outside_nerf=True), use_outside_nerf=True)
+    with torch.no_grad():
+        out = orc.render(T(g['rays_o']), T(g['rays_d']), N_outside=32)
+    close(out['d_final'], g['d_final'], 1e-6, 1e-6)
+    close(out['sigma_out'], g['sigma_out'], 1e-5, 1e-5)
+    close(out['radiance_out'], g['radiance_out'], 1e-5, 1e-6)
+    close(out['rgb'], g['rgb'], 1e-5, 1e-6)
+    close(out['depth_volume'], g['depth'], 1e-5, 1e-6)
+    close(out['normals_volume'], g['normals'], 1e-5, 1e-6)
+
+
+def test_volsdf_1d(golden):
+    g = golden('volsdf_1d')
+    x, s, beta, bp = T(g['x']), T(g['sdf']), float(g['beta']), float(g['bplus'])
+    close(error_bound(x, s, 1. / beta, beta), g['bounds_net'], 1e-6, 0)
+    close(error_bound(x, s, 1. / bp, bp), g['bounds_plus'], 1e-6, 0)
+    close(sdf_to_sigma(s, 1. / beta, beta), g['sigma'], 0, 0)
+
+
+@pytest.mark.parametrize('name,N_samples,N_importance', [('volsdf_a', 64, 64), ('volsdf_c', 128, 128)])
+def test_volsdf(golden, name, N_samples, N_importance):
+    g = golden(name)
+    orc = VolSDFOracle(wg.volsdf_state(seed=int(g['seed']), beta_init=float(g['beta_init'])))
+    with torch.no_grad():
+        out = orc.render(T(g['rays_o']), T(g['rays_d']), N_samples=N_samples, N_importance=N_importance,
+                         max_upsample_steps=6)
+    close(out['iter_usage'], g['iter_usage'], 0, 0)
+    close(out['beta_map'], g['beta_map'], 1e-6, 0)
+    keep = slice(None) if name == 'volsdf_c' else slice(0, 512, 8)
+    close(out['d_vals'][:, keep], g['d_vals'], 1e-6, 1e-6)
+    close(out['rgb'], g['rgb'], 1e-5, 1e-6)
+    close(out['depth_volume'], g['depth'], 1e-5, 1e-6)
+    close(out['mask_volume'], g['mask'], 1e-5, 1e-6)
+    close(out['normals_volume'], g['normals'], 1e-5, 1e-6)
+
+
+def test_unisurf(golden):
+    g = golden('unisurf_e')
+    orc = UNISURFOracle(wg.unisurf_state(seed=int(g['seed'])))
+    for tag, nc in [('', 1048576), ('_nc1000', 1000)]:
+        with torch.no_grad():
+            out = orc.render(T(g['rays_o']), T(g['rays_d']), logit_tau=float(g['logit_tau']), netchunk=nc)
+        if tag == '':
+            close(out['mask_surface'].numpy().astype(np.uint8), g['mask_surface'], 0, 0)
+            close(out['depth_surface'], g['depth_surface'], 1e-6, 1e-6)
+            close(out['implicit_surface'], g['sdf'], 1e-5, 1e-6)
+            close(out['radiance'], g['radiance'], 1e-5, 1e-6)
+        close(out['rgb'], g['rgb' + tag], 1e-5, 1e-6)
+        close(out['depth_volume'], g['depth' + tag], 1e-5, 1e-6)
+        close(out['normals_volume'], g['normals' + tag], 1e-5, 1e-6)
