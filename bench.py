@@ -1,0 +1,171 @@
+"""Benchmark: NeuS volume rendering, 4096 rays x 128 samples, 8x256 SDF MLP (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL)
+
+A step = one `volume_render` call (render mode: torch.no_grad, perturb=False, calc_normal=True,
+detailed_output=False) over one 4096-ray batch of the synthetic config-(b) camera (64x64 pixels,
+f=160, camera at distance 3 looking at a radius-0.5 geometric-init sphere; random-init weights of
+the configs/neus.yaml architecture -- no datasets offline).  Rays are already resident in HBM.
+Multi-GPU: every rank renders its own 4096-ray batch (weak scaling, no data-path collective);
+value = all ranks' rays / max-over-ranks time.  Prints one JSON line on rank 0.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X dense fp32 matrix (MI355X_MICROARCH.md)
+MAC_SDF_FWD = 524_544             # SURVEY §8(a) A5 (incl. the 257-row last layer)
+MAC_SDF_BWD = 459_008             # SURVEY §8(a) A6 (reverse pass for the nablas)
+MAC_RAD = 271_360                 # SURVEY §8(a) A7, NeuS radiance input 289
+RAY_FLOP = 704.8e6                # 128 no-grad SDF + 255 SDF-with-nabla + 127 radiance
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--rays', type=int, default=4096)
+    ap.add_argument('--precision', default=os.environ.get('NR_PRECISION', 'fp32'))
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-rays', type=int, default=1024)
+    return ap.parse_args()
+
+
+def make_model(device, precision):
+    from neurecon_amd.frameworks.neus import NeuS
+    torch.manual_seed(0)
+    surf = dict(use_siren=False, embed_multires=6, radius_init=0.5, geometric_init=True, D=8, W=256, skips=[4],
+                precision=precision)
+    rad = dict(use_siren=False, embed_multires=-1, embed_multires_view=4, use_view_dirs=True, D=4, W=256, skips=[],
+               precision=precision)
+    m = NeuS(variance_init=0.05, speed_factor=10.0, W_geo_feat=256, use_outside_nerf=False, obj_bounding_radius=1.0,
+             surface_cfg=surf, radiance_cfg=rad)
+    return m.to(device).eval()
+
+
+def camera(device):
+    """config (b): c2w = look_at((0,0,-3) -> origin, up (0,-1,0)), K = [[160,0,32],[0,160,32],[0,0,1]]"""
+    import numpy as np
+    cam = np.array([0.0, 0.0, -3.0])
+    fwd = -cam / np.linalg.norm(cam)
+    x = np.cross([0.0, -1.0, 0.0], fwd); x /= np.linalg.norm(x)
+    y = np.cross(fwd, x)
+    c2w = np.eye(4); c2w[:3, 0], c2w[:3, 1], c2w[:3, 2], c2w[:3, 3] = x, y, fwd, cam
+    K = np.eye(4); K[0, 0] = K[1, 1] = 160.0; K[0, 2] = K[1, 2] = 32.0
+    return (torch.tensor(c2w, dtype=torch.float32, device=device)[None],
+            torch.tensor(K, dtype=torch.float32, device=device)[None])
+
+
+def render_kwargs():
+    return dict(obj_bounding_radius=1.0, batched=True, calc_normal=True, detailed_output=False, perturb=False,
+                N_samples=64, N_importance=64, N_outside=0, upsample_algo='official_solution', N_upsample_iters=4)
+
+
+def cpu_baseline(n_rays):
+    """Oracle (clean-room CPU restatement, parity-pinned to the reference) timed on the host cores."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, 'tests', 'golden'))
+    from oracle.neus import NeuSOracle
+    from oracle import rays as orays
+    threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    m = make_model('cpu', 'fp32')
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    orc = NeuSOracle(sd)
+    c2w, K = camera('cpu')
+    ro, rd, _ = orays.get_rays(c2w, K, 64, 64)
+    idx = torch.linspace(0, 4095, n_rays).round().long()
+    ro, rd = ro[:, idx], rd[:, idx]
+    with torch.no_grad():
+        orc.render(ro[:, :32], rd[:, :32])  # warm-up
+        t = time.perf_counter()
+        orc.render(ro, rd)
+        dt = time.perf_counter() - t
+    return {'value': round(n_rays / dt, 2), 'unit': 'rays/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{n_rays} of the 4096 config-(b) rays (evenly spaced), oracle/neus.py, '
+                      f'torch {torch.__version__} CPU fp32, {threads} threads, {dt:.1f} s'}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group('nccl')
+    dev = torch.device('cuda', local)
+    from neurecon_amd import rend_util
+    from neurecon_amd.frameworks.neus import volume_render
+    model = make_model(dev, args.precision)
+    c2w, K = camera(dev)
+    ro, rd, _ = rend_util.get_rays(c2w, K, 64, 64)
+    if args.rays != 4096:
+        reps = math.ceil(args.rays / 4096)
+        ro = ro.repeat(1, reps, 1)[:, :args.rays].contiguous()
+        rd = rd.repeat(1, reps, 1)[:, :args.rays].contiguous()
+    kw = render_kwargs()
+
+    def step():
+        with torch.no_grad():
+            return volume_render(ro, rd, model, **kw)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+    n_rays = ro.shape[1]
+    total_rays = n_rays * args.steps * world
+    value = total_rays / dt
+    if rank == 0:
+        ms = dt / args.steps * 1e3
+        achieved = RAY_FLOP * n_rays / (dt / args.steps) / 1e12
+        out = {
+            'metric': 'rays/sec (4096 rays x 128 samples, 8-layer x256 SDF MLP)',
+            'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'f32' if args.precision == 'fp32' else args.precision,
+            'data': 'synthetic (config-(b) camera rays, seeded geometric-init weights)',
+            'config': {'workload': 'NeuS render, configs/neus.yaml architecture, 64x64 camera = 4096 rays x '
+                                   '(64 coarse + 4x16 upsampled) samples, render mode',
+                       'rays_per_gpu': n_rays, 'samples_per_ray': 128, 'precision': args.precision,
+                       'parallelism': f'ray-sharded x{world}'},
+            'roofline': {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': FP32_MFMA_PEAK_TFLOPS,
+                         'unit': 'TFLOP/s', 'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': None,
+                         'scope': 'whole render step (per-kernel events pending)'},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out['cpu_baseline'] = cpu_baseline(args.cpu_rays)
+        print(json.dumps(out), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,154 @@
+/*
+ * neurecon_hip.h — C-ABI of the MI355X (gfx950) render library `libnrhip.so`.
+ *
+ * Drop-in boundary for neurecon's ray-marched SDF volume renderer.  The reference is pure
+ * Python/PyTorch (no FFI), so each entry point below replaces a Python-level operator of the
+ * reference (file:line cited per function, paths relative to SuwoongHeo/neurecon):
+ *
+ *   nr_sdf_forward          ImplicitSurface.forward / forward_with_nablas   models/base.py:243-282
+ *   nr_radiance_forward     RadianceNet.forward                              models/base.py:372-391
+ *   nr_nerf_forward         NeRF.forward (NeRF++ background)                models/base.py:426-453
+ *   nr_neus_render          neus.volume_render (one ray chunk, render mode) models/frameworks/neus.py:118-397
+ *   nr_sample_pdf           rend_util.sample_pdf                             utils/rend_util.py:255-292
+ *   nr_get_rays             rend_util.get_rays (+ lift)                      utils/rend_util.py:95-164
+ *
+ * Conventions
+ *   - all pointers are DEVICE pointers (fp32 unless stated) owned by the caller;
+ *   - `stream` is a hipStream_t (PyTorch's current stream) passed as void*;
+ *   - no hidden allocation: scratch lives in a caller-provided workspace whose size is given by
+ *     the matching *_workspace_bytes() query;
+ *   - weights are passed as *effective* fp32 matrices (weight_norm folded: W = g * v / ||v||,
+ *     models/base.py:226-227) and packed once by *_pack() into the kernels' tile layout;
+ *   - every call returns 0 on success or a negative NR_ERR_* code; nr_last_error() gives text.
+ *   - no global mutable state besides the thread-local error string: entry points are reentrant.
+ */
+#ifndef NEURECON_HIP_H
+#define NEURECON_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NR_OK 0
+#define NR_ERR_ARG (-1)
+#define NR_ERR_UNSUPPORTED (-2)
+#define NR_ERR_HIP (-3)
+#define NR_ERR_WORKSPACE (-4)
+
+/* arithmetic mode of the MLP GEMMs (fp32 accumulate in both) */
+#define NR_PREC_FP32 0  /* v_mfma_f32_16x16x4_f32: exact fp32 products                        */
+#define NR_PREC_F16X3 1 /* split-fp16 x3 on v_mfma_f32_16x16x32_f16 (hi*hi + hi*lo + lo*hi)     */
+
+int nr_version(void);
+const char* nr_last_error(void);
+
+/* ------------------------------------------------------------------------------------------
+ * SDF MLP  (ImplicitSurface, models/base.py:131-282)
+ * D+1 weight-normed linear layers, Softplus(beta=100) hidden activation, skip connection
+ * cat([h, embed(x)]) / sqrt(2) before layer `skip`; output row 0 = sdf, rows 1..W_geo_feat =
+ * geometry feature.  Supported: D=8, W=256, skip=4, multires in [1,10], W_geo_feat=256.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  int D;          /* 8   */
+  int W;          /* 256 */
+  int skip;       /* 4   */
+  int multires;   /* 6   */
+  int W_geo_feat; /* 256 */
+  int precision;  /* NR_PREC_* */
+} NrSdfDesc;
+
+size_t nr_sdf_packed_bytes(const NrSdfDesc* d);
+/* W[l]: [out_l, in_l] row-major effective weights, b[l]: [out_l], l = 0..D (device pointers) */
+int nr_sdf_pack(const NrSdfDesc* d, const float* const* W, const float* const* b, void* packed, void* stream);
+size_t nr_mlp_workspace_bytes(int with_backward);
+/* pts [P,3] -> sdf [P]; nabla [P,3] (= d sdf / d x, NULL to skip the backward pass);
+ * feature [P, W_geo_feat] (NULL to skip).  Replaces base.py:243-263 / :265-282. */
+int nr_sdf_forward(const NrSdfDesc* d, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,
+                   float* feature, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Radiance MLP (RadianceNet, models/base.py:312-391)
+ * input cat([embed(x), embed_view(v), normals, feature]) -> D x (Linear+ReLU, W) -> Linear(3)+Sigmoid.
+ * Supported: D=4, W=256, multires=-1 (identity on x), view_multires in {-1..10}, W_geo_feat=256.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  int D;             /* 4   */
+  int W;             /* 256 */
+  int multires;      /* -1  */
+  int multires_view; /* 4 (NeuS) or -1 (VolSDF/UNISURF) */
+  int W_geo_feat;    /* 256 */
+  int precision;
+} NrRadDesc;
+
+size_t nr_radiance_packed_bytes(const NrRadDesc* d);
+int nr_radiance_pack(const NrRadDesc* d, const float* const* W, const float* const* b, void* packed, void* stream);
+/* x [P,3], view dirs: vdir[(p / vdir_div) * 3 + c] (vdir_div = samples per ray, or 1),
+ * normals [P,3], feature [P,W_geo_feat] -> rgb [P,3] */
+int nr_radiance_forward(const NrRadDesc* d, const void* packed, const float* x, const float* vdir, int64_t vdir_div,
+                        const float* normals, const float* feature, int64_t P, float* rgb, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * NeuS render, one ray chunk, render mode (neus.py:118-397 with perturb=False,
+ * upsample_algo='official_solution').  Rays are [n_rays, 3]; rays_d need not be normalized.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  const float* rays_o;
+  const float* rays_d;
+  int64_t n_rays;
+  const NrSdfDesc* sdf;
+  const void* sdf_packed;
+  const NrRadDesc* rad;
+  const void* rad_packed;
+  float s;                   /* exp(ln_s * speed_factor)  (neus.py:108-109)        */
+  float obj_bounding_radius; /* near/far sphere radius    (rend_util.py:167-185)   */
+  float near_bypass;         /* NaN = unused (neus.py:185-188) */
+  float far_bypass;          /* NaN = unused */
+  int N_samples;             /* coarse samples, <= 64+... (N_samples + N_importance <= 256) */
+  int N_importance;
+  int N_upsample_iters;
+  int calc_normal;
+  int white_bkgd;
+  const float* t_coarse; /* torch.linspace(0,1,N_samples) as computed by the host        */
+  const float* u_fine;   /* torch.linspace(0,1,N_importance/N_upsample_iters)              */
+  /* outputs [n_rays]-major */
+  float* rgb;     /* [n_rays,3] */
+  float* depth;   /* [n_rays]   */
+  float* acc;     /* [n_rays]   */
+  float* normals; /* [n_rays,3] (if calc_normal) */
+  /* optional per-sample outputs (NULL to skip), ray-major; S = N_samples+N_importance */
+  float* d_final;     /* [n_rays, S-1] */
+  float* sdf_out;     /* [n_rays, S]   */
+  float* nablas_out;  /* [n_rays, S, 3] */
+  float* radiance_out;/* [n_rays, S-1, 3] */
+  float* alpha_out;   /* [n_rays, S-1] */
+  float* cdf_out;     /* [n_rays, S]   */
+  float* weights_out; /* [n_rays, S-1] */
+  void* workspace;
+  size_t workspace_bytes;
+} NrNeusArgs;
+
+size_t nr_neus_workspace_bytes(const NrNeusArgs* a);
+int nr_neus_render(const NrNeusArgs* a, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Inverse-CDF sampling (rend_util.sample_pdf, det=True or caller-provided u):
+ * bins [R, L], weights [R, L-1], u [N] (shared) -> samples [R, N].
+ * ------------------------------------------------------------------------------------------ */
+int nr_sample_pdf(const float* bins, const float* weights, int64_t R, int L, const float* u, int N, float* out,
+                  void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Pixel -> ray (rend_util.get_rays, pose-matrix form): c2w [B,4,4], K [B,4,4] (row-major),
+ * select_inds [B,N] int64 pixel indices (row*W+col) or NULL for all N = H*W pixels in order.
+ * rays_o, rays_d [B,N,3]; rays_d is NOT normalized (rend_util.py:159-162).
+ * ------------------------------------------------------------------------------------------ */
+int nr_get_rays(const float* c2w, const float* K, int B, int H, int W, const int64_t* select_inds, int64_t N,
+                float* rays_o, float* rays_d, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NEURECON_HIP_H */

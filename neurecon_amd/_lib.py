@@ -1,0 +1,111 @@
+"""ctypes binding of libnrhip.so (include/neurecon_hip.h).
+
+The library is the product: there is no fallback.  `lib()` raises if the shared object is
+missing or cannot be loaded, and every wrapper raises on a non-zero status code.
+"""
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (loads the HIP runtime that libnrhip.so binds to by SONAME)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('NR_LIB', os.path.join(HERE, 'libnrhip.so'))
+
+PREC_FP32 = 0
+PREC_F16X3 = 1
+
+_c_p = ctypes.c_void_p
+_c_i = ctypes.c_int
+_c_i64 = ctypes.c_int64
+_c_f = ctypes.c_float
+_c_sz = ctypes.c_size_t
+
+
+class NrSdfDesc(ctypes.Structure):
+    _fields_ = [('D', _c_i), ('W', _c_i), ('skip', _c_i), ('multires', _c_i), ('W_geo_feat', _c_i),
+                ('precision', _c_i)]
+
+
+class NrRadDesc(ctypes.Structure):
+    _fields_ = [('D', _c_i), ('W', _c_i), ('multires', _c_i), ('multires_view', _c_i), ('W_geo_feat', _c_i),
+                ('precision', _c_i)]
+
+
+class NrNeusArgs(ctypes.Structure):
+    _fields_ = [
+        ('rays_o', _c_p), ('rays_d', _c_p), ('n_rays', _c_i64),
+        ('sdf', ctypes.POINTER(NrSdfDesc)), ('sdf_packed', _c_p),
+        ('rad', ctypes.POINTER(NrRadDesc)), ('rad_packed', _c_p),
+        ('s', _c_f), ('obj_bounding_radius', _c_f), ('near_bypass', _c_f), ('far_bypass', _c_f),
+        ('N_samples', _c_i), ('N_importance', _c_i), ('N_upsample_iters', _c_i), ('calc_normal', _c_i),
+        ('white_bkgd', _c_i),
+        ('t_coarse', _c_p), ('u_fine', _c_p),
+        ('rgb', _c_p), ('depth', _c_p), ('acc', _c_p), ('normals', _c_p),
+        ('d_final', _c_p), ('sdf_out', _c_p), ('nablas_out', _c_p), ('radiance_out', _c_p),
+        ('alpha_out', _c_p), ('cdf_out', _c_p), ('weights_out', _c_p),
+        ('workspace', _c_p), ('workspace_bytes', _c_sz),
+    ]
+
+
+_SIGS = {
+    'nr_version': (_c_i, []),
+    'nr_last_error': (ctypes.c_char_p, []),
+    'nr_sdf_packed_bytes': (_c_sz, [ctypes.POINTER(NrSdfDesc)]),
+    'nr_sdf_pack': (_c_i, [ctypes.POINTER(NrSdfDesc), ctypes.POINTER(_c_p), ctypes.POINTER(_c_p), _c_p, _c_p]),
+    'nr_mlp_workspace_bytes': (_c_sz, [_c_i]),
+    'nr_sdf_forward': (_c_i, [ctypes.POINTER(NrSdfDesc), _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
+    'nr_radiance_packed_bytes': (_c_sz, [ctypes.POINTER(NrRadDesc)]),
+    'nr_radiance_pack': (_c_i, [ctypes.POINTER(NrRadDesc), ctypes.POINTER(_c_p), ctypes.POINTER(_c_p), _c_p, _c_p]),
+    'nr_radiance_forward': (_c_i, [ctypes.POINTER(NrRadDesc), _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_i64, _c_p,
+                                   _c_p]),
+    'nr_neus_workspace_bytes': (_c_sz, [ctypes.POINTER(NrNeusArgs)]),
+    'nr_neus_render': (_c_i, [ctypes.POINTER(NrNeusArgs), _c_p]),
+    'nr_sample_pdf': (_c_i, [_c_p, _c_p, _c_i64, _c_i, _c_p, _c_i, _c_p, _c_p]),
+    'nr_get_rays': (_c_i, [_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lock = threading.Lock()
+_lib = None
+
+
+class NrError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libnrhip.so (raises if absent: the HIP path is the only path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(f'neurecon_amd: {LIB_PATH} not found; build it with `python -m neurecon_amd.build`')
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        raise NrError(f'libnrhip error {rc}: {lib().nr_last_error().decode()}')
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_gpu(t, what='input'):
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        raise RuntimeError(f'neurecon_amd: {what} must be a GPU (ROCm) tensor; the render path is HIP-only')

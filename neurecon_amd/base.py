@@ -1,0 +1,299 @@
+"""Network modules of the render path, state_dict-compatible with the reference (models/base.py).
+
+Parameters keep the reference's names and shapes so reference checkpoints load unchanged
+(weight_norm'ed layers store `weight_g [out,1]`, `weight_v [out,in]`, `bias [out]`;
+ImplicitSurface has the `obj_bounding_size` buffer).  Forward passes run on the HIP kernels of
+libnrhip.so (render mode, no autograd graph); there is no PyTorch/CPU compute fallback.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+
+
+# ---------------------------------------------------------------------------------------------
+# positional encoding (models/base.py:14-81) -- API object; the kernels fuse it themselves
+# ---------------------------------------------------------------------------------------------
+class Embedder(nn.Module):
+    def __init__(self, input_dim, max_freq_log2, N_freqs, log_sampling=True, include_input=True,
+                 periodic_fns=(torch.sin, torch.cos)):
+        super().__init__()
+        self.input_dim = input_dim
+        self.include_input = include_input
+        self.periodic_fns = periodic_fns
+        self.out_dim = (input_dim if include_input else 0) + input_dim * N_freqs * len(periodic_fns)
+        bands = 2. ** torch.linspace(0., max_freq_log2, N_freqs) if log_sampling else \
+            torch.linspace(2. ** 0., 2. ** max_freq_log2, N_freqs)
+        self.freq_bands = bands.numpy().tolist()
+
+    def forward(self, x):
+        assert x.shape[-1] == self.input_dim
+        parts = [x] if self.include_input else []
+        for f in self.freq_bands:
+            parts.extend(fn(x * f) for fn in self.periodic_fns)
+        return torch.cat(parts, dim=-1)
+
+
+def get_embedder(multires, input_dim=3):
+    if multires < 0:
+        return nn.Identity(), input_dim
+    e = Embedder(input_dim, multires - 1, multires)
+    return e, e.out_dim
+
+
+# ---------------------------------------------------------------------------------------------
+# layers
+# ---------------------------------------------------------------------------------------------
+class WNLinear(nn.Module):
+    """Linear layer under nn.utils.weight_norm(dim=0): W = g * v / ||v||_row (base.py:226-227).
+    Stores exactly the parameters weight_norm leaves on the module: weight_g, weight_v, bias."""
+
+    def __init__(self, in_dim, out_dim, weight=None, bias=None):
+        super().__init__()
+        self.in_features, self.out_features = in_dim, out_dim
+        if weight is None:  # nn.Linear's default init
+            weight = torch.empty(out_dim, in_dim)
+            nn.init.kaiming_uniform_(weight, a=math.sqrt(5))
+        if bias is None:
+            k = 1.0 / math.sqrt(in_dim)
+            bias = torch.empty(out_dim).uniform_(-k, k)
+        self.weight_v = nn.Parameter(weight.clone())
+        self.weight_g = nn.Parameter(torch.norm_except_dim(weight, 2, 0).clone())
+        self.bias = nn.Parameter(bias.clone())
+
+    def effective_weight(self):
+        return torch._weight_norm(self.weight_v, self.weight_g, 0)
+
+
+def _wn_params(layers):
+    Ws, bs = [], []
+    for layer in layers:
+        Ws.append(layer.effective_weight().detach().float().contiguous())
+        bs.append(layer.bias.detach().float().contiguous())
+    return Ws, bs
+
+
+def _version_key(module, precision, device):
+    return (str(device), precision) + tuple((p.data_ptr(), p._version) for p in module.parameters())
+
+
+def _ptr_array(ts):
+    arr = (ctypes_void_p * len(ts))(*[t.data_ptr() for t in ts])
+    return arr
+
+
+import ctypes  # noqa: E402
+ctypes_void_p = ctypes.c_void_p
+
+
+def _no_training(*tensors_or_modules):
+    if torch.is_grad_enabled():
+        for m in tensors_or_modules:
+            ps = m.parameters() if isinstance(m, nn.Module) else [m]
+            if any(getattr(p, 'requires_grad', False) for p in ps):
+                raise NotImplementedError(
+                    'neurecon_amd: the native HIP path implements render mode (no autograd graph); wrap the call '
+                    'in torch.no_grad() -- the training backward is the next milestone (SURVEY.md §8f)')
+
+
+# ---------------------------------------------------------------------------------------------
+# ImplicitSurface (models/base.py:131-282)
+# ---------------------------------------------------------------------------------------------
+class ImplicitSurface(nn.Module):
+    def __init__(self, W=256, D=8, skips=[4], W_geo_feat=256, input_ch=3, radius_init=1.0, obj_bounding_size=2.0,
+                 geometric_init=True, embed_multires=6, weight_norm=True, use_siren=False, precision='fp32'):
+        super().__init__()
+        if use_siren or not weight_norm:
+            raise NotImplementedError('neurecon_amd: SIREN / non-weight-normed surface nets are out of scope')
+        self.radius_init = radius_init
+        self.register_buffer('obj_bounding_size', torch.tensor([obj_bounding_size]).float())
+        self.geometric_init = geometric_init
+        self.D, self.W, self.W_geo_feat, self.skips = D, W, W_geo_feat, list(skips)
+        self.use_siren = False
+        self.embed_multires = embed_multires
+        self.embed_fn, in_ch = get_embedder(embed_multires)
+        self.input_ch = in_ch
+        self.precision = precision
+        layers = []
+        for l in range(D + 1):
+            if l == D:
+                out_dim = 1 + W_geo_feat if W_geo_feat > 0 else 1
+            elif (l + 1) in self.skips:
+                out_dim = W - in_ch
+            else:
+                out_dim = W
+            in_dim = in_ch if l == 0 else W
+            w = torch.empty(out_dim, in_dim)
+            b = torch.empty(out_dim)
+            if geometric_init:  # SAL / IDR sphere init (base.py:207-224)
+                if l == D:
+                    nn.init.normal_(w, mean=np.sqrt(np.pi) / np.sqrt(in_dim), std=0.0001)
+                    nn.init.constant_(b, -radius_init)
+                elif embed_multires > 0 and l == 0:
+                    nn.init.constant_(b, 0.0)
+                    nn.init.constant_(w[:, 3:], 0.0)
+                    nn.init.normal_(w[:, :3], 0.0, np.sqrt(2) / np.sqrt(out_dim))
+                elif embed_multires > 0 and l in self.skips:
+                    nn.init.constant_(b, 0.0)
+                    nn.init.normal_(w, 0.0, np.sqrt(2) / np.sqrt(out_dim))
+                    nn.init.constant_(w[:, -(in_ch - 3):], 0.0)
+                else:
+                    nn.init.constant_(b, 0.0)
+                    nn.init.normal_(w, 0.0, np.sqrt(2) / np.sqrt(out_dim))
+                layers.append(WNLinear(in_dim, out_dim, w, b))
+            else:
+                layers.append(WNLinear(in_dim, out_dim))
+        self.surface_fc_layers = nn.ModuleList(layers)
+        self._nr_cache = None
+
+    # -- native plumbing ----------------------------------------------------------------------
+    def nr_desc(self):
+        if len(self.skips) != 1:
+            raise NotImplementedError('neurecon_amd: SDF nets with exactly one skip layer are supported')
+        return L.NrSdfDesc(self.D, self.W, self.skips[0], self.embed_multires, self.W_geo_feat,
+                           L.PREC_FP32 if self.precision == 'fp32' else L.PREC_F16X3)
+
+    def nr_packed(self, device):
+        """Effective weights folded (weight_norm) and packed into the kernel layout; cached until a
+        parameter changes (tensor version counter)."""
+        key = _version_key(self, self.precision, device)
+        if self._nr_cache is not None and self._nr_cache[0] == key:
+            return self._nr_cache[1], self._nr_cache[2]
+        lib = L.lib()
+        desc = self.nr_desc()
+        nbytes = lib.nr_sdf_packed_bytes(ctypes.byref(desc))
+        if nbytes == 0:
+            raise NotImplementedError('neurecon_amd: ' + lib.nr_last_error().decode())
+        with torch.no_grad():
+            Ws, bs = _wn_params(self.surface_fc_layers)
+            Ws = [w.to(device) for w in Ws]
+            bs = [b.to(device) for b in bs]
+            packed = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            L.check(lib.nr_sdf_pack(ctypes.byref(desc), _ptr_array(Ws), _ptr_array(bs), L.ptr(packed),
+                                    L.stream_of(device)))
+        self._nr_cache = (key, desc, packed, Ws, bs)  # keep sources alive until the pack ran
+        return desc, packed
+
+    def _run(self, x, nabla, feature):
+        L.require_gpu(x, 'points')
+        _no_training(self)
+        shape = x.shape[:-1]
+        pts = x.reshape(-1, 3).float().contiguous()
+        P = pts.shape[0]
+        dev = pts.device
+        desc, packed = self.nr_packed(dev)
+        sdf = torch.empty(P, device=dev)
+        nab = torch.empty(P, 3, device=dev) if nabla else None
+        feat = torch.empty(P, self.W_geo_feat, device=dev) if feature else None
+        lib = L.lib()
+        ws_bytes = lib.nr_mlp_workspace_bytes(1 if nabla else 0)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        L.check(lib.nr_sdf_forward(ctypes.byref(desc), L.ptr(packed), L.ptr(pts), P, L.ptr(sdf), L.ptr(nab),
+                                   L.ptr(feat), L.ptr(ws), ws_bytes, L.stream_of(dev)))
+        out = [sdf.reshape(shape)]
+        out.append(None if nab is None else nab.reshape(*shape, 3))
+        out.append(None if feat is None else feat.reshape(*shape, self.W_geo_feat))
+        return out
+
+    # -- reference API ------------------------------------------------------------------------
+    def forward(self, x, return_h=False):
+        """base.py:243-263 (render mode)."""
+        sdf, _, h = self._run(x, nabla=False, feature=return_h)
+        return (sdf, h) if return_h else sdf
+
+    def forward_with_nablas(self, x, has_grad_bypass=None):
+        """base.py:265-282: (sdf, d sdf/d x, geometry feature); no graph is built."""
+        sdf, nab, h = self._run(x, nabla=True, feature=True)
+        return sdf, nab, h
+
+    def pretrain_hook(self, configs={}):
+        return False
+
+
+# ---------------------------------------------------------------------------------------------
+# RadianceNet (models/base.py:312-391)
+# ---------------------------------------------------------------------------------------------
+class RadianceNet(nn.Module):
+    def __init__(self, D=4, W=256, skips=[], W_geo_feat=256, embed_multires=6, embed_multires_view=4,
+                 use_view_dirs=True, weight_norm=True, use_siren=False, precision='fp32'):
+        super().__init__()
+        if use_siren or not weight_norm or skips or not use_view_dirs:
+            raise NotImplementedError('neurecon_amd: RadianceNet needs weight_norm, view dirs, no skips, no SIREN')
+        self.D, self.W, self.skips, self.use_view_dirs = D, W, list(skips), use_view_dirs
+        self.embed_multires, self.embed_multires_view, self.W_geo_feat = embed_multires, embed_multires_view, W_geo_feat
+        self.embed_fn, ch_pts = get_embedder(embed_multires)
+        self.embed_fn_view, ch_view = get_embedder(embed_multires_view)
+        in0 = ch_pts + ch_view + 3 + W_geo_feat
+        self.precision = precision
+        self.layers = nn.ModuleList([WNLinear(in0 if l == 0 else W, 3 if l == D else W) for l in range(D + 1)])
+        self._nr_cache = None
+
+    def nr_desc(self):
+        return L.NrRadDesc(self.D, self.W, self.embed_multires, self.embed_multires_view, self.W_geo_feat,
+                           L.PREC_FP32 if self.precision == 'fp32' else L.PREC_F16X3)
+
+    def nr_packed(self, device):
+        key = _version_key(self, self.precision, device)
+        if self._nr_cache is not None and self._nr_cache[0] == key:
+            return self._nr_cache[1], self._nr_cache[2]
+        lib = L.lib()
+        desc = self.nr_desc()
+        nbytes = lib.nr_radiance_packed_bytes(ctypes.byref(desc))
+        if nbytes == 0:
+            raise NotImplementedError('neurecon_amd: ' + lib.nr_last_error().decode())
+        with torch.no_grad():
+            Ws, bs = _wn_params(self.layers)
+            Ws = [w.to(device) for w in Ws]
+            bs = [b.to(device) for b in bs]
+            packed = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            L.check(lib.nr_radiance_pack(ctypes.byref(desc), _ptr_array(Ws), _ptr_array(bs), L.ptr(packed),
+                                         L.stream_of(device)))
+        self._nr_cache = (key, desc, packed, Ws, bs)
+        return desc, packed
+
+    def forward(self, x, view_dirs, normals, geometry_feature):
+        """base.py:372-391 (render mode)."""
+        L.require_gpu(x, 'points')
+        _no_training(self)
+        shape = x.shape[:-1]
+        dev = x.device
+        xs = x.reshape(-1, 3).float().contiguous()
+        P = xs.shape[0]
+        v = view_dirs.reshape(-1, 3).float().contiguous()
+        if v.shape[0] != P:
+            raise ValueError('view_dirs must have one direction per point')
+        n = normals.reshape(-1, 3).float().contiguous()
+        f = geometry_feature.reshape(-1, self.W_geo_feat).float().contiguous()
+        desc, packed = self.nr_packed(dev)
+        rgb = torch.empty(P, 3, device=dev)
+        L.check(L.lib().nr_radiance_forward(ctypes.byref(desc), L.ptr(packed), L.ptr(xs), L.ptr(v), 1, L.ptr(n),
+                                            L.ptr(f), P, L.ptr(rgb), L.stream_of(dev)))
+        return rgb.reshape(*shape, 3)
+
+
+# ---------------------------------------------------------------------------------------------
+# NeRF++ background (models/base.py:395-453): parameters only in this round (state_dict compat)
+# ---------------------------------------------------------------------------------------------
+class NeRF(nn.Module):
+    def __init__(self, D=8, W=256, input_ch=3, input_ch_view=3, multires=-1, multires_view=-1, output_ch=4,
+                 skips=[4], use_view_dirs=False):
+        super().__init__()
+        self.D, self.W, self.skips, self.use_view_dirs = D, W, list(skips), use_view_dirs
+        self.multires, self.multires_view = multires, multires_view
+        self.embed_fn, input_ch = get_embedder(multires, input_dim=input_ch)
+        self.embed_fn_view, input_ch_view = get_embedder(multires_view, input_dim=input_ch_view)
+        self.pts_linears = nn.ModuleList(
+            [nn.Linear(input_ch, W)] + [nn.Linear(W + input_ch if i in self.skips else W, W) for i in range(D - 1)])
+        self.views_linears = nn.ModuleList([nn.Linear(input_ch_view + W, W // 2)])
+        if use_view_dirs:
+            self.feature_linear = nn.Linear(W, W)
+            self.alpha_linear = nn.Linear(W, 1)
+            self.rgb_linear = nn.Linear(W // 2, 3)
+        else:
+            self.output_linear = nn.Linear(W, output_ch)
+
+    def forward(self, input_pts, input_views):
+        raise NotImplementedError('neurecon_amd: the NeRF++ background kernel lands with config (d)')

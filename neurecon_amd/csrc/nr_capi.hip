@@ -1,0 +1,288 @@
+// neurecon_amd — C-ABI entry points (include/neurecon_hip.h): argument checking, packed-weight
+// layouts, and the host-side orchestration of one NeuS ray chunk.
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "nr_common.h"
+#include "nr_mlp.h"
+#include "nr_neus.h"
+
+namespace nr {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// ---------------------------------------------------------------------------------------------
+// descriptors
+// ---------------------------------------------------------------------------------------------
+int check_sdf_desc(const NrSdfDesc* d) {
+  NR_REQUIRE(d, NR_ERR_ARG, "null NrSdfDesc");
+  NR_REQUIRE(d->D == 8 && d->W == 256 && d->skip == 4 && d->multires == 6 && d->W_geo_feat == 256,
+             NR_ERR_UNSUPPORTED,
+             "SDF net: only D=8, W=256, skips=[4], embed_multires=6, W_geo_feat=256 are implemented");
+  NR_REQUIRE(d->precision == NR_PREC_FP32, NR_ERR_UNSUPPORTED, "SDF net: precision mode not implemented");
+  return NR_OK;
+}
+
+int check_rad_desc(const NrRadDesc* d) {
+  NR_REQUIRE(d, NR_ERR_ARG, "null NrRadDesc");
+  NR_REQUIRE(d->D == 4 && d->W == 256 && d->multires < 0 && d->W_geo_feat == 256 && d->multires_view <= 7,
+             NR_ERR_UNSUPPORTED,
+             "radiance net: only D=4, W=256, embed_multires=-1, embed_multires_view<=7, W_geo_feat=256");
+  NR_REQUIRE(d->precision == NR_PREC_FP32, NR_ERR_UNSUPPORTED, "radiance net: precision mode not implemented");
+  return NR_OK;
+}
+
+// (input blocks, output blocks) of each SDF GEMM op, stream order F0..F8, B7..B0
+static const int kSdfKB[kSdfOps] = {4, 16, 16, 16, 18, 16, 16, 16, 16, 16, 16, 16, 16, 14, 16, 16, 16};
+static const int kSdfNBO[kSdfOps] = {16, 16, 16, 14, 16, 16, 16, 16, 16, 16, 16, 16, 18, 16, 16, 16, 4};
+
+SdfLayout sdf_layout(const NrSdfDesc&) {
+  SdfLayout L{};
+  size_t off = 0;
+  for (int i = 0; i < kSdfOps; ++i) {
+    L.op_bytes[i] = (2 * kSdfKB[i] + 1) * 1024;
+    L.op_off[i] = (uint32_t)off;
+    off += (size_t)(kSdfNBO[i] / 2) * L.op_bytes[i];
+  }
+  L.w8row0_off = (uint32_t)off;
+  off = align256(off + 256 * 4);
+  L.misc_off = (uint32_t)off;
+  off = align256(off + 16);
+  L.total = (uint32_t)off;
+  return L;
+}
+
+static int rad_small(const NrRadDesc& d) { return 3 + (d.multires_view < 0 ? 3 : 3 + 6 * d.multires_view) + 3; }
+
+RadLayout rad_layout(const NrRadDesc& d) {
+  RadLayout L{};
+  L.n_small = rad_small(d);
+  L.kbs = L.n_small <= 32 ? 2 : 4;
+  size_t off = 0;
+  for (int i = 0; i < 4; ++i) {
+    const int kb = i == 0 ? 16 + L.kbs : 16;
+    L.op_bytes[i] = (2 * kb + 1) * 1024;
+    L.op_off[i] = (uint32_t)off;
+    off += 8 * (size_t)L.op_bytes[i];
+  }
+  L.head_off = (uint32_t)off;
+  off = align256(off + (3 * 256 + 4) * 4);
+  L.total = (uint32_t)off;
+  return L;
+}
+
+static PackSeg seg(int nblk, int off, int nvalid) { return PackSeg{nblk, off, nvalid}; }
+static PackSeg none() { return PackSeg{0, 0, 0}; }
+
+static size_t scratch_bytes() {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  return (size_t)cus * kScratchPerWG;
+}
+
+// ---------------------------------------------------------------------------------------------
+// NeuS chunk orchestration
+// ---------------------------------------------------------------------------------------------
+static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int R, hipStream_t st) {
+  char* ws = (char*)a.workspace;
+  const int n_up = a.N_upsample_iters > 0 ? a.N_importance / a.N_upsample_iters : 0;
+  NeusChunk c{};
+  c.R = R;
+  c.N_samples = a.N_samples;
+  c.n_up = n_up;
+  c.n_iters = a.N_upsample_iters;
+  c.S = a.N_samples + a.N_upsample_iters * n_up;
+  auto F = [&](size_t o) { return (float*)(ws + o); };
+  c.ro = F(pl.o_ro); c.rd = F(pl.o_rd); c.near = F(pl.o_near); c.far = F(pl.o_far);
+  c.dv = F(pl.o_dv); c.sv = F(pl.o_sv); c.wtmp = F(pl.o_wtmp); c.dnew = F(pl.o_dnew); c.snew = F(pl.o_snew);
+  c.pts = F(pl.o_pts); c.mids = F(pl.o_mids); c.dmid = F(pl.o_dmid);
+  c.sdf_f = F(pl.o_sdf_f); c.nab_f = F(pl.o_nab_f);
+  c.sdf_m = F(pl.o_sdf_m); c.nab_m = F(pl.o_nab_m); c.feat_m = F(pl.o_feat_m); c.rad_m = F(pl.o_rad_m);
+  void* mlp_ws = ws + pl.o_mlp;
+  const size_t mlp_bytes = a.workspace_bytes - pl.o_mlp;
+  const SdfLayout SL = sdf_layout(*a.sdf);
+  const RadLayout RL = rad_layout(*a.rad);
+  const dim3 blk(256), grd((R + 255) / 256);
+  int rc;
+
+  hipLaunchKernelGGL(neus_prologue, grd, blk, 0, st, c, a.rays_o + ray0 * 3, a.rays_d + ray0 * 3, a.t_coarse,
+                     a.obj_bounding_radius, a.near_bypass, a.far_bypass);
+  NR_HIP_CHECK(hipGetLastError());
+  // coarse SDF (no grad, neus.py:251)
+  if ((rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)a.N_samples * R, c.sv, nullptr, nullptr, a.sdf->multires,
+                       nullptr, 0, st)))
+    return rc;
+  for (int it = 0; it < a.N_upsample_iters; ++it) {
+    hipLaunchKernelGGL(neus_upsample, grd, blk, 0, st, c, it, a.u_fine);
+    NR_HIP_CHECK(hipGetLastError());
+    if ((rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)n_up * R, c.snew, nullptr, nullptr, a.sdf->multires,
+                         nullptr, 0, st)))
+      return rc;
+  }
+  hipLaunchKernelGGL(neus_points, grd, blk, 0, st, c);
+  NR_HIP_CHECK(hipGetLastError());
+  // SDF + nablas at the samples (neus.py:294)
+  if ((rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)c.S * R, c.sdf_f, c.nab_f, nullptr, a.sdf->multires, mlp_ws,
+                       mlp_bytes, st)))
+    return rc;
+  // SDF + nablas + geometry feature at the mid-points, then the radiance net (neus.py:103-106, :298)
+  if ((rc = launch_sdf(SL, a.sdf_packed, c.mids, (int64_t)(c.S - 1) * R, c.sdf_m, c.nab_m, c.feat_m,
+                       a.sdf->multires, mlp_ws, mlp_bytes, st)))
+    return rc;
+  if ((rc = launch_radiance(RL, a.rad_packed, c.mids, c.rd, 1, R, c.nab_m, c.feat_m, (int64_t)(c.S - 1) * R, c.rad_m,
+                            a.rad->multires_view, st)))
+    return rc;
+  NeusOut o{ray0, a.rgb, a.depth, a.acc, a.normals, a.d_final, a.sdf_out, a.nablas_out,
+            a.radiance_out, a.alpha_out, a.cdf_out, a.weights_out};
+  hipLaunchKernelGGL(neus_composite, grd, blk, 0, st, c, o, a.s, a.calc_normal, a.white_bkgd);
+  NR_HIP_CHECK(hipGetLastError());
+  return NR_OK;
+}
+
+static int64_t neus_chunk_rays(const NrNeusArgs* a) {
+  const int64_t cap = 16384;
+  return a->n_rays < cap ? (a->n_rays > 0 ? a->n_rays : 1) : cap;
+}
+
+}  // namespace nr
+
+using namespace nr;
+
+extern "C" {
+
+int nr_version(void) { return 1; }
+const char* nr_last_error(void) { return g_err.c_str(); }
+
+size_t nr_sdf_packed_bytes(const NrSdfDesc* d) {
+  if (check_sdf_desc(d)) return 0;
+  return sdf_layout(*d).total;
+}
+
+int nr_sdf_pack(const NrSdfDesc* d, const float* const* W, const float* const* b, void* packed, void* stream) {
+  int rc = check_sdf_desc(d);
+  if (rc) return rc;
+  NR_REQUIRE(W && b && packed, NR_ERR_ARG, "nr_sdf_pack: null argument");
+  for (int l = 0; l <= 8; ++l) NR_REQUIRE(W[l] && b[l], NR_ERR_ARG, "nr_sdf_pack: null layer pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const SdfLayout L = sdf_layout(*d);
+  char* P = (char*)packed;
+  const int in0 = 39, n3 = 217;
+  const float isq2 = 1.0f / 1.41421356237309504880f;
+  PackOp ops[kSdfOps];
+  // forward
+  ops[F0] = PackOp{W[0], b[0], in0, 0, {seg(16, 0, 256), none()}, {seg(4, 0, in0), none()}, 1.0f};
+  ops[F1] = PackOp{W[1], b[1], 256, 0, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  ops[F2] = PackOp{W[2], b[2], 256, 0, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  ops[F3] = PackOp{W[3], b[3], 256, 0, {seg(14, 0, n3), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  ops[F4] = PackOp{W[4], b[4], 256, 0, {seg(16, 0, 256), none()}, {seg(14, 0, n3), seg(4, n3, in0)}, isq2};
+  ops[F5] = PackOp{W[5], b[5], 256, 0, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  ops[F6] = PackOp{W[6], b[6], 256, 0, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  ops[F7] = PackOp{W[7], b[7], 256, 0, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  ops[F8] = PackOp{W[8], b[8], 256, 0, {seg(16, 1, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  // backward (transposed)
+  ops[B7] = PackOp{W[7], nullptr, 256, 1, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  ops[B6] = PackOp{W[6], nullptr, 256, 1, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  ops[B5] = PackOp{W[5], nullptr, 256, 1, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  ops[B4] = PackOp{W[4], nullptr, 256, 1, {seg(14, 0, n3), seg(4, n3, in0)}, {seg(16, 0, 256), none()}, isq2};
+  ops[B3] = PackOp{W[3], nullptr, 256, 1, {seg(16, 0, 256), none()}, {seg(14, 0, n3), none()}, 1.0f};
+  ops[B2] = PackOp{W[2], nullptr, 256, 1, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  ops[B1] = PackOp{W[1], nullptr, 256, 1, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  ops[B0] = PackOp{W[0], nullptr, in0, 1, {seg(4, 0, in0), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  for (int i = 0; i < kSdfOps; ++i)
+    if ((rc = launch_pack_op(ops[i], P + L.op_off[i], st))) return rc;
+  if ((rc = launch_pack_vec(W[8], 0, 256, 256, P + L.w8row0_off, st))) return rc;
+  if ((rc = launch_pack_vec(b[8], 0, 1, 4, P + L.misc_off, st))) return rc;
+  return NR_OK;
+}
+
+size_t nr_mlp_workspace_bytes(int with_backward) { return with_backward ? scratch_bytes() : 0; }
+
+int nr_sdf_forward(const NrSdfDesc* d, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,
+                   float* feature, void* workspace, size_t workspace_bytes, void* stream) {
+  int rc = check_sdf_desc(d);
+  if (rc) return rc;
+  NR_REQUIRE(packed && pts && sdf && P >= 0, NR_ERR_ARG, "nr_sdf_forward: null argument");
+  return launch_sdf(sdf_layout(*d), packed, pts, P, sdf, nabla, feature, d->multires, workspace, workspace_bytes,
+                    (hipStream_t)stream);
+}
+
+size_t nr_radiance_packed_bytes(const NrRadDesc* d) {
+  if (check_rad_desc(d)) return 0;
+  return rad_layout(*d).total;
+}
+
+int nr_radiance_pack(const NrRadDesc* d, const float* const* W, const float* const* b, void* packed, void* stream) {
+  int rc = check_rad_desc(d);
+  if (rc) return rc;
+  NR_REQUIRE(W && b && packed, NR_ERR_ARG, "nr_radiance_pack: null argument");
+  for (int l = 0; l <= 4; ++l) NR_REQUIRE(W[l] && b[l], NR_ERR_ARG, "nr_radiance_pack: null layer pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const RadLayout L = rad_layout(*d);
+  char* P = (char*)packed;
+  const int ns = L.n_small, ld0 = ns + 256;
+  PackOp ops[4];
+  ops[0] = PackOp{W[0], b[0], ld0, 0, {seg(16, 0, 256), none()}, {seg(16, ns, 256), seg(L.kbs, 0, ns)}, 1.0f};
+  for (int i = 1; i < 4; ++i) ops[i] = PackOp{W[i], b[i], 256, 0, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  for (int i = 0; i < 4; ++i) {
+    if ((rc = launch_pack_op(ops[i], P + L.op_off[i], st))) return rc;
+  }
+  if ((rc = launch_pack_vec(W[4], 0, 768, 768, P + L.head_off, st))) return rc;
+  if ((rc = launch_pack_vec(b[4], 0, 3, 4, P + L.head_off + 768 * 4, st))) return rc;
+  return NR_OK;
+}
+
+int nr_radiance_forward(const NrRadDesc* d, const void* packed, const float* x, const float* vdir, int64_t vdir_div,
+                        const float* normals, const float* feature, int64_t P, float* rgb, void* stream) {
+  int rc = check_rad_desc(d);
+  if (rc) return rc;
+  NR_REQUIRE(packed && x && vdir && normals && feature && rgb && vdir_div > 0, NR_ERR_ARG,
+             "nr_radiance_forward: bad argument");
+  return launch_radiance(rad_layout(*d), packed, x, vdir, vdir_div, INT64_MAX, normals, feature, P, rgb,
+                         d->multires_view, (hipStream_t)stream);
+}
+
+size_t nr_neus_workspace_bytes(const NrNeusArgs* a) {
+  if (!a) return 0;
+  return neus_plan(*a, neus_chunk_rays(a)).total;
+}
+
+int nr_neus_render(const NrNeusArgs* a, void* stream) {
+  NR_REQUIRE(a, NR_ERR_ARG, "nr_neus_render: null args");
+  int rc = check_sdf_desc(a->sdf);
+  if (rc) return rc;
+  if ((rc = check_rad_desc(a->rad))) return rc;
+  NR_REQUIRE(a->rays_o && a->rays_d && a->sdf_packed && a->rad_packed && a->t_coarse && a->rgb && a->depth && a->acc,
+             NR_ERR_ARG, "nr_neus_render: null argument");
+  NR_REQUIRE(a->N_samples >= 2, NR_ERR_ARG, "nr_neus_render: N_samples must be >= 2");
+  NR_REQUIRE(!a->calc_normal || a->normals, NR_ERR_ARG, "nr_neus_render: calc_normal needs normals output");
+  if (a->N_upsample_iters > 0) {
+    const int n_up = a->N_importance / a->N_upsample_iters;
+    NR_REQUIRE(n_up >= 1 && n_up <= kMaxUp && a->u_fine, NR_ERR_UNSUPPORTED,
+               "nr_neus_render: N_importance/N_upsample_iters must be in [1, 32]");
+  }
+  if (a->n_rays <= 0) return NR_OK;
+  const int64_t Rc = neus_chunk_rays(a);
+  const NeusPlan pl = neus_plan(*a, Rc);
+  NR_REQUIRE(a->workspace && a->workspace_bytes >= pl.total, NR_ERR_WORKSPACE, "nr_neus_render: workspace too small");
+  for (int64_t r0 = 0; r0 < a->n_rays; r0 += Rc) {
+    const int R = (int)((a->n_rays - r0) < Rc ? (a->n_rays - r0) : Rc);
+    if ((rc = neus_chunk(*a, pl, r0, R, (hipStream_t)stream))) return rc;
+  }
+  return NR_OK;
+}
+
+int nr_sample_pdf(const float* bins, const float* weights, int64_t R, int L, const float* u, int N, float* out,
+                  void* stream) {
+  NR_REQUIRE(bins && weights && u && out && L >= 2 && N >= 1, NR_ERR_ARG, "nr_sample_pdf: bad argument");
+  if (R <= 0) return NR_OK;
+  hipLaunchKernelGGL(sample_pdf_kernel, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, (hipStream_t)stream, bins,
+                     weights, R, L, u, N, out);
+  NR_HIP_CHECK(hipGetLastError());
+  return NR_OK;
+}
+
+}  // extern "C"

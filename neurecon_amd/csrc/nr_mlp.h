@@ -1,0 +1,63 @@
+// neurecon_amd — MLP kernel constants, packed-weight layouts and launchers (internal header).
+#pragma once
+#include "nr_common.h"
+
+namespace nr {
+
+constexpr int kWaves = 8;                       // waves per workgroup (2 per SIMD)
+constexpr int kThreads = 64 * kWaves;           // 512
+constexpr int kTile = 16;                       // points per wave (MFMA N dimension)
+constexpr int kPointsPerWG = kTile * kWaves;    // 128
+constexpr int kMaxChunkBytes = 48 * 1024;       // LDS chunk: 2 output blocks x <=24 input blocks x 1 KB
+constexpr size_t kScratchPerWG = (size_t)kWaves * 8 * 16 * 64 * 16;  // exp(100z) slabs, 1 MiB
+
+// SDF GEMM ops in stream order (forward F*, feature F8, backward B*)
+enum SdfOp { F0, F1, F2, F3, F4, F5, F6, F7, F8, B7, B6, B5, B4, B3, B2, B1, B0, kSdfOps };
+
+struct SdfLayout {
+  uint32_t op_off[kSdfOps];
+  uint32_t op_bytes[kSdfOps];  // bytes of one chunk of the op
+  uint32_t w8row0_off;         // sdf row of the last layer [256]
+  uint32_t misc_off;           // [0] = sdf bias
+  uint32_t total;
+};
+
+struct RadLayout {
+  uint32_t op_off[4];
+  uint32_t op_bytes[4];
+  uint32_t head_off;  // [3][256] weights, then [3] bias
+  uint32_t total;
+  int kbs;            // small-input blocks (even)
+  int n_small;        // 3 + view-embedding + 3
+};
+
+struct PackSeg {
+  int nblk;    // 16-feature blocks
+  int off;     // first source index
+  int nvalid;  // valid source indices (rest zero-padded)
+};
+
+struct PackOp {
+  const float* W;
+  const float* bias;  // per output row (same row mapping as W), or null
+  int ld;
+  int transpose;  // 1: value = W[in][out] (Wᵀ)
+  PackSeg out[2];
+  PackSeg in[2];
+  float scale;
+};
+
+int launch_pack_op(const PackOp& op, char* dst, hipStream_t stream);
+int launch_pack_vec(const float* src, int off, int nvalid, int n, char* dst, hipStream_t stream);
+int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,
+               float* feature, int nfreq, void* ws, size_t ws_bytes, hipStream_t stream);
+int launch_radiance(const RadLayout& L, const void* packed, const float* x, const float* vdir, int64_t vdiv,
+                    int64_t vmod, const float* normals, const float* feature, int64_t P, float* rgb, int nfreq_view,
+                    hipStream_t stream);
+
+SdfLayout sdf_layout(const NrSdfDesc& d);
+RadLayout rad_layout(const NrRadDesc& d);
+int check_sdf_desc(const NrSdfDesc* d);
+int check_rad_desc(const NrRadDesc* d);
+
+}  // namespace nr

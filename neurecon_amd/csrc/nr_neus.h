@@ -1,0 +1,47 @@
+// neurecon_amd — NeuS render path internals.
+#pragma once
+#include "nr_common.h"
+
+namespace nr {
+
+constexpr int kMaxUp = 32;  // max new samples per upsampling round
+
+// device views of one ray chunk's workspace (sample-major [s][r] arrays)
+struct NeusChunk {
+  int R;          // rays in this chunk
+  int N_samples;  // coarse samples
+  int n_up;       // new samples per round
+  int n_iters;    // upsampling rounds
+  int S;          // total samples = N_samples + n_iters * n_up
+  float* ro; float* rd; float* near; float* far;
+  float* dv; float* sv; float* wtmp; float* dnew; float* snew;
+  float* pts; float* mids; float* dmid;
+  float* sdf_f; float* nab_f;
+  float* sdf_m; float* nab_m; float* feat_m; float* rad_m;
+};
+
+// outputs (ray-major); ray0 = index of the chunk's first ray in the full batch
+struct NeusOut {
+  int64_t ray0;
+  float* rgb; float* depth; float* acc; float* normals;
+  float* d_final; float* sdf; float* nablas; float* radiance; float* alpha; float* cdf; float* weights;
+};
+
+struct NeusPlan {
+  int64_t Rc;
+  size_t o_ro, o_rd, o_near, o_far, o_dv, o_sv, o_wtmp, o_dnew, o_snew, o_pts, o_mids, o_dmid;
+  size_t o_sdf_f, o_nab_f, o_sdf_m, o_nab_m, o_feat_m, o_rad_m, o_mlp;
+  size_t total;
+};
+
+NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc);
+
+__global__ void neus_prologue(NeusChunk c, const float* rays_o, const float* rays_d, const float* t_coarse,
+                              float r_obj, float near_bypass, float far_bypass);
+__global__ void neus_upsample(NeusChunk c, int it, const float* u);
+__global__ void neus_points(NeusChunk c);
+__global__ void neus_composite(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd);
+__global__ void sample_pdf_kernel(const float* bins, const float* weights, int64_t R, int L, const float* u, int N,
+                                  float* out);
+
+}  // namespace nr

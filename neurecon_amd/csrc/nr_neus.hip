@@ -1,0 +1,319 @@
+// neurecon_amd — NeuS render path for gfx950: per-ray sampling / compositing kernels and the
+// orchestration of one ray chunk (models/frameworks/neus.py:118-397, render mode).
+//
+// Per-ray state is stored sample-major ([sample][ray]) so the one-thread-per-ray kernels read
+// and write coalesced lines; the MLP kernels see a flat point list p = sample * Rc + ray.
+// Scans (cumsum / cumprod) accumulate in fp64 exactly like ATen's CPU kernels
+// (acc_type<float, is_cuda=false> = double), each prefix rounded to fp32.
+#include "nr_common.h"
+#include "nr_mlp.h"
+#include "nr_neus.h"
+
+namespace nr {
+
+__device__ __forceinline__ float4 load3(const float* p) { return make_float4(p[0], p[1], p[2], 0.f); }
+
+// F.normalize(v, dim=-1): v / max(||v||_2, 1e-12)
+__device__ __forceinline__ void normalize3(float& x, float& y, float& z) {
+  const float n = sqrtf(fadd(fadd(fmul(x, x), fmul(y, y)), fmul(z, z)));
+  const float d = fmaxf(n, 1e-12f);
+  x = fdiv(x, d);
+  y = fdiv(y, d);
+  z = fdiv(z, d);
+}
+
+// ---------------------------------------------------------------------------------------------
+// prologue: normalize rays_d (neus.py:169-172), near/far (rend_util.py:167-185), coarse depths
+// (neus.py:209-210) and their points (neus.py:251)
+// ---------------------------------------------------------------------------------------------
+__global__ void neus_prologue(NeusChunk c, const float* __restrict__ rays_o, const float* __restrict__ rays_d,
+                              const float* __restrict__ t_coarse, float r_obj, float near_bypass, float far_bypass) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= c.R) return;
+  const float ox = rays_o[r * 3 + 0], oy = rays_o[r * 3 + 1], oz = rays_o[r * 3 + 2];
+  float dx = rays_d[r * 3 + 0], dy = rays_d[r * 3 + 1], dz = rays_d[r * 3 + 2];
+  normalize3(dx, dy, dz);
+  c.ro[r * 3 + 0] = ox; c.ro[r * 3 + 1] = oy; c.ro[r * 3 + 2] = oz;
+  c.rd[r * 3 + 0] = dx; c.rd[r * 3 + 1] = dy; c.rd[r * 3 + 2] = dz;
+  const float mid = -fadd(fadd(fmul(ox, dx), fmul(oy, dy)), fmul(oz, dz));
+  float nr = fmaxf(fsub(mid, r_obj), 0.0f);
+  float fr = fmaxf(fadd(mid, r_obj), r_obj);
+  if (!__builtin_isnan(near_bypass)) nr = near_bypass;
+  if (!__builtin_isnan(far_bypass)) fr = far_bypass;
+  c.near[r] = nr;
+  c.far[r] = fr;
+  for (int s = 0; s < c.N_samples; ++s) {
+    const float t = t_coarse[s];
+    const float d = fadd(fmul(nr, fsub(1.0f, t)), fmul(fr, t));
+    const int64_t q = (int64_t)s * c.R + r;
+    c.dv[q] = d;
+    c.pts[q * 3 + 0] = fadd(ox, fmul(dx, d));
+    c.pts[q * 3 + 1] = fadd(oy, fmul(dy, d));
+    c.pts[q * 3 + 2] = fadd(oz, fmul(dz, d));
+  }
+}
+
+// merge the sorted list (dv,sv)[0..L) with the n_up new samples (dnew,snew), in place
+__device__ void merge_new(const NeusChunk& c, int r, int L) {
+  float dn[kMaxUp], sn[kMaxUp];
+  const int n = c.n_up;
+  for (int k = 0; k < n; ++k) {
+    dn[k] = c.dnew[(int64_t)k * c.R + r];
+    sn[k] = c.snew[(int64_t)k * c.R + r];
+  }
+  for (int k = 1; k < n; ++k) {  // insertion sort (new samples are sorted up to rounding)
+    const float d = dn[k], s = sn[k];
+    int m = k - 1;
+    while (m >= 0 && dn[m] > d) { dn[m + 1] = dn[m]; sn[m + 1] = sn[m]; --m; }
+    dn[m + 1] = d;
+    sn[m + 1] = s;
+  }
+  int i = L - 1, j = n - 1;
+  for (int k = L + n - 1; k >= 0 && j >= 0; --k) {
+    const int64_t qk = (int64_t)k * c.R + r;
+    const float di = i >= 0 ? c.dv[(int64_t)i * c.R + r] : 0.f;
+    if (i >= 0 && di > dn[j]) {
+      c.dv[qk] = di;
+      c.sv[qk] = c.sv[(int64_t)i * c.R + r];
+      --i;
+    } else {
+      c.dv[qk] = dn[j];
+      c.sv[qk] = sn[j];
+      --j;
+    }
+  }
+}
+
+// inverse-CDF sample for one u (rend_util.py:284-290)
+__device__ __forceinline__ float invert_one(float u, float c0, float c1, float b0, float b1) {
+  float denom = fsub(c1, c0);
+  if (denom < 1e-5f) denom = 1.0f;
+  const float t = fdiv(fsub(u, c0), denom);
+  return fadd(b0, fmul(t, fsub(b1, b0)));
+}
+
+// sample_pdf(bins=dv[0..L), weights=wtmp[0..L-1) (already +1e-5), N=n, u) -> out[k*R + r]
+// total = sum of the (+1e-5) weights.  rend_util.py:255-292.
+__device__ void sample_pdf_ray(const float* __restrict__ bins, const float* __restrict__ w, int64_t stride, int L,
+                               float total, const float* __restrict__ u, int n, float* __restrict__ out,
+                               int64_t out_stride) {
+  // w[i] are the raw weights; the +1e-5 of rend_util.py:259 is applied on the fly
+  int k = 0;
+  const float b_first = bins[0];
+  while (k < n && u[k] <= 0.0f) {  // searchsorted -> 0: below = above = 0
+    out[k * out_stride] = invert_one(u[k], 0.0f, 0.0f, b_first, b_first);
+    ++k;
+  }
+  double acc = 0.0;
+  float c_prev = 0.0f, b_prev = b_first;
+  for (int i = 0; i < L - 1 && k < n; ++i) {
+    acc += (double)fdiv(fadd(w[i * stride], 1e-5f), total);
+    const float c_next = (float)acc;
+    const float b_next = bins[(i + 1) * stride];
+    while (k < n && u[k] <= c_next) {
+      out[k * out_stride] = invert_one(u[k], c_prev, c_next, b_prev, b_next);
+      ++k;
+    }
+    c_prev = c_next;
+    b_prev = b_next;
+  }
+  // u above every cdf value: searchsorted -> L, below = above = L-1 (c_prev = cdf[L-1] here)
+  for (; k < n; ++k) out[k * out_stride] = invert_one(u[k], c_prev, c_prev, b_prev, b_prev);
+}
+
+// one "official_solution" upsampling round (neus.py:252-276) for rays of this chunk:
+// merge last round's samples, then draw n_up new depths and write their points.
+__global__ void neus_upsample(NeusChunk c, int it, const float* __restrict__ u) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= c.R) return;
+  int L = c.N_samples + it * c.n_up;
+  if (it > 0) merge_new(c, r, L - c.n_up);
+  const int64_t R = c.R;
+  const float S = (float)(64 << it);  // 64 * 2**i
+  float prev_slope = 0.0f;
+  double T = 1.0;
+  double total = 0.0;
+  float s0 = c.sv[r], z0 = c.dv[r];
+  for (int i = 0; i < L - 1; ++i) {
+    const float s1 = c.sv[(i + 1) * R + r], z1 = c.dv[(i + 1) * R + r];
+    const float mid = fmul(fadd(s0, s1), 0.5f);
+    const float slope = fdiv(fsub(s1, s0), fadd(fsub(z1, z0), 1e-5f));
+    float m = fminf(prev_slope, slope);
+    prev_slope = slope;
+    m = fminf(fmaxf(m, -10.0f), 0.0f);
+    const float dist = fsub(z1, z0);
+    const float md = fmul(fmul(m, dist), 0.5f);
+    const float c0 = sigmoidf_ref(fmul(fsub(mid, md), S));
+    const float c1 = sigmoidf_ref(fmul(fadd(mid, md), S));
+    const float alpha = fdiv(fadd(fsub(c0, c1), 1e-5f), fadd(c0, 1e-5f));
+    const float w = fmul(alpha, (float)T);
+    T *= (double)fadd(fsub(1.0f, alpha), 1e-10f);
+    c.wtmp[i * R + r] = w;
+    total += (double)fadd(w, 1e-5f);
+    s0 = s1;
+    z0 = z1;
+  }
+  sample_pdf_ray(c.dv + r, c.wtmp + r, R, L, (float)total, u, c.n_up, c.dnew + r, R);
+  const float ox = c.ro[r * 3], oy = c.ro[r * 3 + 1], oz = c.ro[r * 3 + 2];
+  const float dx = c.rd[r * 3], dy = c.rd[r * 3 + 1], dz = c.rd[r * 3 + 2];
+  for (int k = 0; k < c.n_up; ++k) {
+    const int64_t q = k * R + r;
+    const float d = c.dnew[q];
+    c.pts[q * 3 + 0] = fadd(ox, fmul(dx, d));
+    c.pts[q * 3 + 1] = fadd(oy, fmul(dy, d));
+    c.pts[q * 3 + 2] = fadd(oz, fmul(dz, d));
+  }
+}
+
+// final merge; points at the S sorted depths (neus.py:284) and at the S-1 mid-points (:287-288)
+__global__ void neus_points(NeusChunk c) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= c.R) return;
+  const int S = c.S;
+  if (c.n_iters > 0) merge_new(c, r, S - c.n_up);
+  const int64_t R = c.R;
+  const float ox = c.ro[r * 3], oy = c.ro[r * 3 + 1], oz = c.ro[r * 3 + 2];
+  const float dx = c.rd[r * 3], dy = c.rd[r * 3 + 1], dz = c.rd[r * 3 + 2];
+  float dprev = 0.f;
+  for (int s = 0; s < S; ++s) {
+    const int64_t q = s * R + r;
+    const float d = c.dv[q];
+    c.pts[q * 3 + 0] = fadd(ox, fmul(dx, d));
+    c.pts[q * 3 + 1] = fadd(oy, fmul(dy, d));
+    c.pts[q * 3 + 2] = fadd(oz, fmul(dz, d));
+    if (s > 0) {
+      const float dm = fmul(0.5f, fadd(d, dprev));
+      const int64_t qm = (s - 1) * R + r;
+      c.dmid[qm] = dm;
+      c.mids[qm * 3 + 0] = fadd(ox, fmul(dx, dm));
+      c.mids[qm * 3 + 1] = fadd(oy, fmul(dy, dm));
+      c.mids[qm * 3 + 2] = fadd(oz, fmul(dz, dm));
+    }
+    dprev = d;
+  }
+}
+
+// compositing (neus.py:296, :346-380)
+__global__ void neus_composite(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= c.R) return;
+  const int S = c.S;
+  const int64_t R = c.R;
+  const int64_t ro = o.ray0 + r;  // global ray index for outputs
+  double T = 1.0, acc = 0.0, rgb0 = 0.0, rgb1 = 0.0, rgb2 = 0.0, n0 = 0.0, n1 = 0.0, n2 = 0.0;
+  float cprev = sigmoidf_ref(fmul(c.sdf_f[r], s_inv));
+  if (o.cdf) o.cdf[ro * S] = cprev;
+  for (int i = 0; i < S - 1; ++i) {
+    const float cn = sigmoidf_ref(fmul(c.sdf_f[(i + 1) * R + r], s_inv));
+    const float alpha = fmaxf(fdiv(fsub(cprev, cn), fadd(cprev, 1e-10f)), 0.0f);
+    const float w = fmul(alpha, (float)T);
+    T *= (double)fadd(fsub(1.0f, alpha), 1e-10f);
+    const int64_t q = i * R + r;
+    rgb0 += (double)fmul(w, c.rad_m[q * 3 + 0]);
+    rgb1 += (double)fmul(w, c.rad_m[q * 3 + 1]);
+    rgb2 += (double)fmul(w, c.rad_m[q * 3 + 2]);
+    acc += (double)w;
+    if (calc_normal) {
+      float x = c.nab_f[q * 3 + 0], y = c.nab_f[q * 3 + 1], z = c.nab_f[q * 3 + 2];
+      normalize3(x, y, z);
+      n0 += (double)fmul(x, w);
+      n1 += (double)fmul(y, w);
+      n2 += (double)fmul(z, w);
+    }
+    c.wtmp[q] = w;
+    if (o.cdf) o.cdf[ro * S + i + 1] = cn;
+    if (o.alpha) o.alpha[ro * (S - 1) + i] = alpha;
+    if (o.weights) o.weights[ro * (S - 1) + i] = w;
+    cprev = cn;
+  }
+  const float accf = (float)acc;
+  const float denom = fadd(accf, 1e-10f);
+  double depth = 0.0;
+  for (int i = 0; i < S - 1; ++i) {
+    const int64_t q = i * R + r;
+    depth += (double)fmul(fdiv(c.wtmp[q], denom), c.dmid[q]);
+  }
+  float r0 = (float)rgb0, r1 = (float)rgb1, r2 = (float)rgb2;
+  if (white_bkgd) {
+    const float bg = fsub(1.0f, accf);
+    r0 = fadd(r0, bg); r1 = fadd(r1, bg); r2 = fadd(r2, bg);
+  }
+  o.rgb[ro * 3 + 0] = r0;
+  o.rgb[ro * 3 + 1] = r1;
+  o.rgb[ro * 3 + 2] = r2;
+  o.depth[ro] = (float)depth;
+  o.acc[ro] = accf;
+  if (calc_normal && o.normals) {
+    o.normals[ro * 3 + 0] = (float)n0;
+    o.normals[ro * 3 + 1] = (float)n1;
+    o.normals[ro * 3 + 2] = (float)n2;
+  }
+  // detailed per-sample outputs, ray-major
+  for (int i = 0; i < S; ++i) {
+    const int64_t q = i * R + r;
+    if (o.sdf) o.sdf[ro * S + i] = c.sdf_f[q];
+    if (o.nablas) {
+      o.nablas[(ro * S + i) * 3 + 0] = c.nab_f[q * 3 + 0];
+      o.nablas[(ro * S + i) * 3 + 1] = c.nab_f[q * 3 + 1];
+      o.nablas[(ro * S + i) * 3 + 2] = c.nab_f[q * 3 + 2];
+    }
+    if (i < S - 1) {
+      if (o.d_final) o.d_final[ro * (S - 1) + i] = c.dmid[q];
+      if (o.radiance) {
+        o.radiance[(ro * (S - 1) + i) * 3 + 0] = c.rad_m[q * 3 + 0];
+        o.radiance[(ro * (S - 1) + i) * 3 + 1] = c.rad_m[q * 3 + 1];
+        o.radiance[(ro * (S - 1) + i) * 3 + 2] = c.rad_m[q * 3 + 2];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// generic sample_pdf entry (rend_util.py:255-292), bins/weights ray-major [R][L], u [N]
+// ---------------------------------------------------------------------------------------------
+__global__ void sample_pdf_kernel(const float* __restrict__ bins, const float* __restrict__ weights, int64_t R, int L,
+                                  const float* __restrict__ u, int N, float* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  double total = 0.0;
+  for (int i = 0; i < L - 1; ++i) total += (double)fadd(weights[r * (L - 1) + i], 1e-5f);
+  sample_pdf_ray(bins + r * L, weights + r * (L - 1), 1, L, (float)total, u, N, out + r * N, 1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// host orchestration
+// ---------------------------------------------------------------------------------------------
+static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc) {
+  NeusPlan p{};
+  const int n_up0 = a.N_upsample_iters > 0 ? a.N_importance / a.N_upsample_iters : 0;
+  const int S = a.N_samples + a.N_upsample_iters * n_up0;
+  p.Rc = Rc;
+  size_t off = 0;
+  auto take = [&](size_t floats) { size_t o = off; off = align_up(off + floats * 4); return o; };
+  p.o_ro = take(Rc * 3);
+  p.o_rd = take(Rc * 3);
+  p.o_near = take(Rc);
+  p.o_far = take(Rc);
+  p.o_dv = take((size_t)S * Rc);
+  p.o_sv = take((size_t)S * Rc);
+  p.o_wtmp = take((size_t)S * Rc);
+  const int n_up = a.N_upsample_iters > 0 ? a.N_importance / a.N_upsample_iters : 0;
+  p.o_dnew = take((size_t)(n_up > 0 ? n_up : 1) * Rc);
+  p.o_snew = take((size_t)(n_up > 0 ? n_up : 1) * Rc);
+  p.o_pts = take((size_t)S * Rc * 3);
+  p.o_mids = take((size_t)(S - 1) * Rc * 3);
+  p.o_dmid = take((size_t)(S - 1) * Rc);
+  p.o_sdf_f = take((size_t)S * Rc);
+  p.o_nab_f = take((size_t)S * Rc * 3);
+  p.o_sdf_m = take((size_t)(S - 1) * Rc);
+  p.o_nab_m = take((size_t)(S - 1) * Rc * 3);
+  p.o_feat_m = take((size_t)(S - 1) * Rc * 256);
+  p.o_rad_m = take((size_t)(S - 1) * Rc * 3);
+  p.o_mlp = off;
+  p.total = off + nr_mlp_workspace_bytes(1);
+  return p;
+}
+
+}  // namespace nr

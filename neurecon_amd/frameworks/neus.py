@@ -1,0 +1,229 @@
+"""NeuS framework: same API as the reference's models/frameworks/neus.py, render path on HIP.
+
+`volume_render(rays_o, rays_d, model, **kw) -> (rgb, depth, extras)` keeps the reference's
+signature, argument meaning, output shapes and extras keys (neus.py:118-397); the whole ray
+chunk (near/far, coarse samples, 4-round 'official_solution' upsampling, SDF + nablas, radiance,
+alpha compositing) runs in libnrhip.so (`nr_neus_render`).
+"""
+import copy
+import ctypes
+import math
+from collections import OrderedDict
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .. import _lib as L
+from ..base import ImplicitSurface, NeRF, RadianceNet, _no_training
+from .. import rend_util
+
+
+class NeuS(nn.Module):
+    """neus.py:72-115 (parameter tree and names identical: ln_s, implicit_surface.*, radiance_net.*,
+    nerf_outside.*)."""
+
+    def __init__(self, variance_init=0.05, speed_factor=1.0, input_ch=3, W_geo_feat=-1, use_outside_nerf=False,
+                 obj_bounding_radius=1.0, surface_cfg=dict(), radiance_cfg=dict()):
+        super().__init__()
+        self.ln_s = nn.Parameter(data=torch.Tensor([-np.log(variance_init) / speed_factor]), requires_grad=True)
+        self.speed_factor = speed_factor
+        self.implicit_surface = ImplicitSurface(W_geo_feat=W_geo_feat, input_ch=input_ch,
+                                                obj_bounding_size=obj_bounding_radius, **surface_cfg)
+        if W_geo_feat < 0:
+            W_geo_feat = self.implicit_surface.W
+        self.radiance_net = RadianceNet(W_geo_feat=W_geo_feat, **radiance_cfg)
+        if use_outside_nerf:
+            self.nerf_outside = NeRF(input_ch=4, multires=10, multires_view=4, use_view_dirs=True)
+
+    def forward_radiance(self, x, view_dirs):
+        _, nablas, geometry_feature = self.implicit_surface.forward_with_nablas(x)
+        return self.radiance_net.forward(x, view_dirs, nablas, geometry_feature)
+
+    def forward_s(self):
+        return torch.exp(self.ln_s * self.speed_factor)
+
+    def forward(self, x, view_dirs):
+        sdf, nablas, geometry_feature = self.implicit_surface.forward_with_nablas(x)
+        radiances = self.radiance_net.forward(x, view_dirs, nablas, geometry_feature)
+        return radiances, sdf, nablas
+
+
+_TABLES = {}
+
+
+def _linspace_table(n, device):
+    """torch.linspace(0, 1, n) computed on the CPU exactly as the reference does, uploaded once."""
+    key = (n, str(device))
+    t = _TABLES.get(key)
+    if t is None:
+        t = torch.linspace(0, 1, n).float().to(device)
+        _TABLES[key] = t
+    return t
+
+
+def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False, batched_info={},
+                  calc_normal=False, use_view_dirs=True, rayschunk=65536, netchunk=1048576, white_bkgd=False,
+                  near_bypass=None, far_bypass=None, detailed_output=True, show_progress=False, perturb=False,
+                  fixed_s_recp=1 / 64., N_samples=64, N_importance=64, N_outside=0,
+                  upsample_algo='official_solution', N_nograd_samples=2048, N_upsample_iters=4, **dummy_kwargs):
+    """neus.py:118-397, render mode.  rays_o/rays_d: [(B,) N_rays, 3]; rays_d need not be normalized."""
+    L.require_gpu(rays_o, 'rays_o')
+    _no_training(model)
+    if perturb:
+        raise NotImplementedError('neurecon_amd: stratified (perturb=True) sampling is a training feature')
+    if upsample_algo != 'official_solution':
+        raise NotImplementedError(f'neurecon_amd: upsample_algo={upsample_algo!r} not native yet')
+    if N_outside > 0:
+        raise NotImplementedError('neurecon_amd: NeRF++ background (N_outside>0) not native yet')
+    if not use_view_dirs:
+        raise NotImplementedError('neurecon_amd: use_view_dirs=False not supported')
+    dev = rays_o.device
+    if batched:
+        B = rays_d.shape[0]
+        prefix = [B, -1]
+    else:
+        prefix = [-1]
+    ro = rays_o.reshape(-1, 3).float().contiguous()
+    rd = rays_d.reshape(-1, 3).float().contiguous()
+    n = ro.shape[0]
+    n_up = N_importance // N_upsample_iters if N_upsample_iters > 0 else 0
+    S = N_samples + N_upsample_iters * n_up
+
+    sdf_desc, sdf_packed = model.implicit_surface.nr_packed(dev)
+    rad_desc, rad_packed = model.radiance_net.nr_packed(dev)
+    s = float(model.forward_s().detach().float().reshape(-1)[0].item())
+    t_coarse = _linspace_table(N_samples, dev)
+    u_fine = _linspace_table(max(n_up, 1), dev)
+
+    rgb = torch.empty(n, 3, device=dev)
+    depth = torch.empty(n, device=dev)
+    acc = torch.empty(n, device=dev)
+    normals = torch.empty(n, 3, device=dev) if calc_normal else None
+    det = {}
+    if detailed_output:
+        det = dict(implicit_nablas=torch.empty(n, S, 3, device=dev), implicit_surface=torch.empty(n, S, device=dev),
+                   radiance=torch.empty(n, S - 1, 3, device=dev), alpha=torch.empty(n, S - 1, device=dev),
+                   cdf=torch.empty(n, S, device=dev), visibility_weights=torch.empty(n, S - 1, device=dev),
+                   d_final=torch.empty(n, S - 1, device=dev))
+    a = L.NrNeusArgs()
+    a.rays_o, a.rays_d, a.n_rays = L.ptr(ro), L.ptr(rd), n
+    a.sdf, a.sdf_packed = ctypes.pointer(sdf_desc), L.ptr(sdf_packed)
+    a.rad, a.rad_packed = ctypes.pointer(rad_desc), L.ptr(rad_packed)
+    a.s = s
+    a.obj_bounding_radius = float(obj_bounding_radius)
+    a.near_bypass = float('nan') if near_bypass is None else float(near_bypass)
+    a.far_bypass = float('nan') if far_bypass is None else float(far_bypass)
+    a.N_samples, a.N_importance, a.N_upsample_iters = N_samples, N_importance, N_upsample_iters
+    a.calc_normal, a.white_bkgd = int(bool(calc_normal)), int(bool(white_bkgd))
+    a.t_coarse, a.u_fine = L.ptr(t_coarse), L.ptr(u_fine)
+    a.rgb, a.depth, a.acc, a.normals = L.ptr(rgb), L.ptr(depth), L.ptr(acc), L.ptr(normals)
+    a.d_final = L.ptr(det.get('d_final'))
+    a.sdf_out = L.ptr(det.get('implicit_surface'))
+    a.nablas_out = L.ptr(det.get('implicit_nablas'))
+    a.radiance_out = L.ptr(det.get('radiance'))
+    a.alpha_out = L.ptr(det.get('alpha'))
+    a.cdf_out = L.ptr(det.get('cdf'))
+    a.weights_out = L.ptr(det.get('visibility_weights'))
+    lib = L.lib()
+    ws_bytes = lib.nr_neus_workspace_bytes(ctypes.byref(a))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    a.workspace, a.workspace_bytes = L.ptr(ws), ws_bytes
+    L.check(lib.nr_neus_render(ctypes.byref(a), L.stream_of(dev)))
+
+    ret = OrderedDict([('rgb', rgb.reshape(*prefix, 3)), ('depth_volume', depth.reshape(prefix)),
+                       ('mask_volume', acc.reshape(prefix))])
+    if calc_normal:
+        ret['normals_volume'] = normals.reshape(*prefix, 3)
+    if detailed_output:
+        ret['implicit_nablas'] = det['implicit_nablas'].reshape(*prefix, S, 3)
+        ret['implicit_surface'] = det['implicit_surface'].reshape(*prefix, S)
+        ret['radiance'] = det['radiance'].reshape(*prefix, S - 1, 3)
+        ret['alpha'] = det['alpha'].reshape(*prefix, S - 1)
+        ret['cdf'] = det['cdf'].reshape(*prefix, S)
+        ret['visibility_weights'] = det['visibility_weights'].reshape(*prefix, S - 1)
+        ret['d_final'] = det['d_final'].reshape(*prefix, S - 1)
+    return ret['rgb'], ret['depth_volume'], ret
+
+
+class SingleRenderer(nn.Module):
+    """neus.py:399-405 -- an nn.Module so nn.DataParallel can scatter rays over dim 1."""
+
+    def __init__(self, model):
+        super().__init__()
+        self.model = model
+
+    def forward(self, rays_o, rays_d, **kwargs):
+        return volume_render(rays_o, rays_d, self.model, **kwargs)
+
+
+class Trainer(nn.Module):
+    """neus.py:408-485.  The training step needs the backward of the render kernels (next milestone,
+    SURVEY.md §8f); forward() therefore raises from the render call while grad is enabled."""
+
+    def __init__(self, model, device_ids=[0], batched=True):
+        super().__init__()
+        self.model = model
+        self.renderer = SingleRenderer(model)
+        if len(device_ids) > 1:
+            self.renderer = nn.DataParallel(self.renderer, device_ids=device_ids, dim=1 if batched else 0)
+        self.device = device_ids[0]
+
+    def forward(self, args, indices, model_input, ground_truth, render_kwargs_train, it, device='cuda'):
+        intrinsics = model_input['intrinsics'].to(device)
+        c2w = model_input['c2w'].to(device)
+        rays_o, rays_d, select_inds = rend_util.get_rays(c2w, intrinsics, render_kwargs_train['H'],
+                                                         render_kwargs_train['W'], N_rays=args.data.N_rays)
+        return self.renderer(rays_o, rays_d, detailed_output=True, **render_kwargs_train)
+
+
+def get_model(args):
+    """neus.py:488-546 (same config keys and defaults)."""
+    from ..config import as_cfg
+    args = as_cfg(args)
+    if not args.training.with_mask:
+        assert 'N_outside' in args.model.keys() and args.model.N_outside > 0, \
+            'Please specify a positive model:N_outside for neus with nerf++'
+    model_config = {
+        'obj_bounding_radius': args.model.obj_bounding_radius,
+        'W_geo_feat': args.model.setdefault('W_geometry_feature', 256),
+        'use_outside_nerf': not args.training.with_mask,
+        'speed_factor': args.training.setdefault('speed_factor', 1.0),
+        'variance_init': args.model.setdefault('variance_init', 0.05),
+    }
+    surface_cfg = {
+        'use_siren': args.model.surface.setdefault('use_siren', args.model.setdefault('use_siren', False)),
+        'embed_multires': args.model.surface.setdefault('embed_multires', 6),
+        'radius_init': args.model.surface.setdefault('radius_init', 1.0),
+        'geometric_init': args.model.surface.setdefault('geometric_init', True),
+        'D': args.model.surface.setdefault('D', 8),
+        'W': args.model.surface.setdefault('W', 256),
+        'skips': args.model.surface.setdefault('skips', [4]),
+    }
+    radiance_cfg = {
+        'use_siren': args.model.radiance.setdefault('use_siren', args.model.setdefault('use_siren', False)),
+        'embed_multires': args.model.radiance.setdefault('embed_multires', -1),
+        'embed_multires_view': args.model.radiance.setdefault('embed_multires_view', -1),
+        'use_view_dirs': args.model.radiance.setdefault('use_view_dirs', True),
+        'D': args.model.radiance.setdefault('D', 4),
+        'W': args.model.radiance.setdefault('W', 256),
+        'skips': args.model.radiance.setdefault('skips', []),
+    }
+    model_config['surface_cfg'] = surface_cfg
+    model_config['radiance_cfg'] = radiance_cfg
+    model = NeuS(**model_config)
+    render_kwargs_train = {
+        'upsample_algo': args.model.setdefault('upsample_algo', 'official_solution'),
+        'N_nograd_samples': args.model.setdefault('N_nograd_samples', 2048),
+        'N_upsample_iters': args.model.setdefault('N_upsample_iters', 4),
+        'N_outside': args.model.setdefault('N_outside', 0),
+        'obj_bounding_radius': args.data.setdefault('obj_bounding_radius', 1.0),
+        'batched': args.data.batch_size is not None,
+        'perturb': args.model.setdefault('perturb', True),
+        'white_bkgd': args.model.setdefault('white_bkgd', False),
+    }
+    render_kwargs_test = copy.deepcopy(render_kwargs_train)
+    render_kwargs_test['rayschunk'] = args.data.val_rayschunk
+    render_kwargs_test['perturb'] = False
+    trainer = Trainer(model, device_ids=args.device_ids, batched=render_kwargs_train['batched'])
+    return model, trainer, render_kwargs_train, render_kwargs_test, trainer.renderer

@@ -1,0 +1,72 @@
+"""Ray utilities with the reference's signatures (utils/rend_util.py); compute on libnrhip.so."""
+import ctypes
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import _lib as L
+
+
+def get_rays(c2w, intrinsics, H, W, N_rays=-1):
+    """rend_util.py:112-164 (pose-matrix form).  Random pixel selection draws
+    randint(H)*W + randint(W) with torch's generator exactly like the reference."""
+    L.require_gpu(c2w, 'c2w')
+    if c2w.shape[-1] == 7:
+        raise NotImplementedError('quaternion camera poses (rend_util.py:114-119) are not supported')
+    dev = c2w.device
+    prefix = c2w.shape[:-2]
+    B = int(np.prod(prefix)) if len(prefix) else 1
+    m = c2w.reshape(B, 4, 4).float().contiguous()
+    K = intrinsics.to(dev).reshape(-1, 4, 4).float().expand(B, 4, 4).contiguous()
+    if N_rays > 0:
+        N_rays = min(N_rays, H * W)
+        hs = torch.randint(0, H, size=[N_rays]).to(dev)
+        ws = torch.randint(0, W, size=[N_rays]).to(dev)
+        select_inds = (hs * W + ws).expand([*prefix, N_rays])
+        sel = select_inds.reshape(B, N_rays).contiguous()
+        N = N_rays
+    else:
+        N = H * W
+        select_inds = torch.arange(N, device=dev).expand([*prefix, N])
+        sel = None
+    ro = torch.empty(B, N, 3, device=dev)
+    rd = torch.empty(B, N, 3, device=dev)
+    L.check(L.lib().nr_get_rays(L.ptr(m), L.ptr(K), B, H, W, L.ptr(sel), N, L.ptr(ro), L.ptr(rd),
+                                L.stream_of(dev)))
+    return ro.reshape(*prefix, N, 3), rd.reshape(*prefix, N, 3), select_inds
+
+
+def near_far_from_sphere(ray_origins, ray_directions, r=1.0, keepdim=True):
+    """rend_util.py:167-185 (the render kernels compute this in-kernel; kept for API users)."""
+    mid = -torch.sum(ray_origins * ray_directions, dim=-1, keepdim=keepdim)
+    return (mid - r).clamp_min(0.0), (mid + r).clamp_min(r)
+
+
+def sample_pdf(bins, weights, N_importance, det=False, eps=1e-5):
+    """rend_util.py:255-292 on the HIP kernel (det=True)."""
+    if not det:
+        raise NotImplementedError('neurecon_amd.sample_pdf: stochastic sampling is a training feature')
+    L.require_gpu(bins, 'bins')
+    shape = bins.shape[:-1]
+    Lb = bins.shape[-1]
+    b = bins.reshape(-1, Lb).float().contiguous()
+    w = weights.reshape(-1, Lb - 1).float().contiguous()
+    u = torch.linspace(0.0, 1.0, steps=N_importance).float().to(bins.device)
+    out = torch.empty(b.shape[0], N_importance, device=bins.device)
+    L.check(L.lib().nr_sample_pdf(L.ptr(b), L.ptr(w), b.shape[0], Lb, L.ptr(u), N_importance, L.ptr(out),
+                                  L.stream_of(bins.device)))
+    return out.reshape(*shape, N_importance)
+
+
+def lin2img(tensor, H, W, batched=False, B=None):
+    """rend_util.py:237-247."""
+    *_, num_samples, channels = tensor.shape
+    assert num_samples == H * W
+    if batched:
+        if B is None:
+            B = tensor.shape[0]
+        else:
+            tensor = tensor.view([B, num_samples // B, channels])
+        return tensor.permute(0, 2, 1).view([B, channels, H, W])
+    return tensor.permute(1, 0).view([channels, H, W])

@@ -1,0 +1,134 @@
+"""GPU parity: HIP path (libnrhip.so via neurecon_amd) vs the reference's golden vectors and the
+oracle.  Run on the MI355X box: `pytest -m gpu`.
+
+Tolerance (north star): |gpu - ref| <= 1e-4 * |ref| + 1e-6 for rendered rgb / depth / mask /
+normals (fp32).  Per-sample quantities behind a discrete decision (sample_pdf's `denom < eps`
+switch, searchsorted ties) can legitimately move a sample when the SDF differs by rounding; those
+are reported as per-ray pass rates, with rgb/depth held to the bar per ray.
+"""
+import numpy as np
+import pytest
+import torch
+
+import weightgen as wg
+from helpers import neus_model, report, to_gpu
+
+pytestmark = pytest.mark.gpu
+
+RT, AT = 1e-4, 1e-6
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from neurecon_amd import _lib
+    _lib.lib()  # must load: no fallback exists
+
+
+def test_sdf_net_vs_golden(golden):
+    g = golden('sdf_net')
+    m = neus_model(wg.neus_state(seed=int(g['seed'])))
+    pts = to_gpu(g['pts'])
+    with torch.no_grad():
+        s, h = m.implicit_surface.forward(pts, return_h=True)
+        s2, n, h2 = m.implicit_surface.forward_with_nablas(pts)
+    assert report('sdf (no grad)', s, g['sdf_nograd'], 1e-5, 1e-6)[0].all()
+    assert report('h (no grad)', h[:64], g['h_nograd'], 1e-5, 1e-6)[0].all()
+    assert report('sdf (with nablas)', s2, g['sdf'], 1e-5, 1e-6)[0].all()
+    assert report('nablas', n, g['nablas'], RT, AT)[0].all()
+    assert report('h (with nablas)', h2[:64], g['h'], 1e-5, 1e-6)[0].all()
+
+
+def test_sdf_net_ragged_sizes():
+    """P not a multiple of the 128-point workgroup tile, and P = 1, match the oracle."""
+    from oracle.nets import SDFNet
+    sd = wg.neus_state(seed=11)
+    m = neus_model(sd)
+    orc = SDFNet(sd)
+    torch.manual_seed(0)
+    for P in (1, 17, 129, 1000):
+        x = torch.randn(P, 3) * 0.7
+        ref_s, ref_n, ref_h = orc.forward_with_nablas(x)
+        with torch.no_grad():
+            s, n, h = m.implicit_surface.forward_with_nablas(x.cuda())
+        assert report(f'sdf P={P}', s, ref_s, 1e-5, 1e-6)[0].all()
+        assert report(f'nabla P={P}', n, ref_n, RT, AT)[0].all()
+        assert report(f'h P={P}', h, ref_h, 1e-5, 1e-6)[0].all()
+
+
+def test_radiance_vs_golden(golden):
+    g = golden('radiance')
+    m = neus_model(wg.neus_state(seed=int(g['seed_neus'])))
+    with torch.no_grad():
+        rgb = m.radiance_net.forward(to_gpu(g['x']), to_gpu(g['v']), to_gpu(g['n']), to_gpu(g['f']))
+    assert report('radiance (NeuS cfg)', rgb, g['rgb_neus'], 1e-5, 1e-6)[0].all()
+
+
+def test_sample_pdf_vs_golden(golden):
+    from neurecon_amd import rend_util
+    g = golden('sampling')
+    s16 = rend_util.sample_pdf(to_gpu(g['bins']), to_gpu(g['weights']), 16, det=True)
+    s66 = rend_util.sample_pdf(to_gpu(g['bins']), to_gpu(g['weights']), 66, det=True)
+    assert report('sample_pdf N=16', s16, g['s16'], 1e-6, 1e-6)[0].all()
+    assert report('sample_pdf N=66', s66, g['s66'], 1e-6, 1e-6)[0].all()
+
+
+def test_get_rays_vs_golden(golden):
+    from neurecon_amd import rend_util
+    g = golden('get_rays')
+    H, W = int(g['H']), int(g['W'])
+    ro, rd, _ = rend_util.get_rays(to_gpu(g['c2w']), to_gpu(g['K']), H, W)
+    assert report('rays_o', ro, g['rays_o'], 0, 0)[0].all()
+    assert report('rays_d', rd, g['rays_d'], 1e-6, 1e-7)[0].all()
+
+
+def _neus_render(m, ro, rd, **kw):
+    from neurecon_amd.frameworks.neus import volume_render
+    with torch.no_grad():
+        return volume_render(ro, rd, m, obj_bounding_radius=1.0, batched=True, calc_normal=True,
+                             detailed_output=True, perturb=False, N_samples=64, N_importance=64,
+                             upsample_algo='official_solution', N_upsample_iters=4, **kw)
+
+
+def test_neus_render_vs_golden(golden):
+    g = golden('neus_b')
+    m = neus_model(wg.neus_state(seed=int(g['seed'])))
+    rgb, depth, ex = _neus_render(m, to_gpu(g['rays_o']), to_gpu(g['rays_d']))
+    ok_d, _ = report('d_final', ex['d_final'], g['d_final'], 1e-5, 1e-6)
+    report('sdf', ex['implicit_surface'], g['sdf'], 1e-4, 1e-6)
+    report('nablas', ex['implicit_nablas'], g['nablas'], 1e-4, 1e-6)
+    report('radiance', ex['radiance'], g['radiance'], 1e-4, 1e-6)
+    report('weights', ex['visibility_weights'], g['weights'], 1e-4, 1e-6)
+    assert report('rgb', rgb, g['rgb'], RT, AT)[0].all()
+    assert report('depth', depth, g['depth'], RT, AT)[0].all()
+    assert report('mask', ex['mask_volume'], g['mask'], RT, AT)[0].all()
+    assert report('normals', ex['normals_volume'], g['normals'], RT, AT)[0].all()
+    # samples: every ray whose sampling did not flip a discrete decision matches per sample
+    assert ok_d.all(axis=-1).mean() >= 0.95
+
+
+def test_neus_full_config_b_vs_oracle():
+    """4096 rays (the BASELINE config) vs the oracle; per-ray pass rate at the 1e-4 bar."""
+    from oracle.neus import NeuSOracle
+    from oracle import rays as orays
+    H, W, f, dist = wg.CAMERAS['b']
+    c2w = wg.look_at_c2w(dist)[None]
+    K = wg.intrinsics(f, H, W)[None]
+    ro, rd, _ = orays.get_rays(c2w, K, H, W)
+    sd = wg.neus_state(seed=1)
+    torch.set_num_threads(8)
+    with torch.no_grad():
+        ref = NeuSOracle(sd).render(ro, rd)
+    m = neus_model(sd)
+    rgb, depth, ex = _neus_render(m, ro.cuda(), rd.cuda())
+    ok_rgb, _ = report('rgb', rgb, ref['rgb'], RT, AT)
+    ok_dep, _ = report('depth', depth, ref['depth_volume'], RT, AT)
+    ok_n, _ = report('normals', ex['normals_volume'], ref['normals_volume'], RT, AT)
+    ray_ok = ok_rgb.all(-1) & ok_dep
+    d_same = (np.abs(ex['d_final'].cpu().numpy() - ref['d_final'].numpy()) <= 1e-5).all(-1)
+    print(f'per-ray rgb+depth pass: {ray_ok.mean() * 100:.3f}%  rays with identical samples: '
+          f'{d_same.mean() * 100:.3f}%  failing rays with identical samples: {(~ray_ok & d_same).sum()}')
+    # a ray may only miss the bar if a discrete sampling decision flipped on it
+    assert (~ray_ok & d_same).sum() == 0
+    assert ray_ok.mean() >= 0.995
