@@ -97,6 +97,33 @@ def cpu_baseline(n_rays):
                       f'torch {torch.__version__} CPU fp32, {threads} threads, {dt:.1f} s'}
 
 
+# algorithmic MACs per unit (point) of each library kernel, SURVEY.md §8(a)
+KERNEL_MAC = {'sdf_fwd': MAC_SDF_FWD, 'sdf_feat': MAC_SDF_FWD, 'sdf_nabla': MAC_SDF_FWD + MAC_SDF_BWD,
+              'sdf_nabla_feat': MAC_SDF_FWD + MAC_SDF_BWD, 'radiance': MAC_RAD}
+
+
+def roofline(kstats, precision):
+    """Dominant kernel (largest device time): algorithmic FLOPs per launch / mean launch duration."""
+    # the two sdf_kernel<nabla> launches (samples, mid-points) are one kernel
+    merged = {}
+    for name, (n, ms, units) in kstats.items():
+        key = 'sdf_nabla' if name.startswith('sdf_nabla') else name
+        a = merged.setdefault(key, [0, 0.0, 0.0])
+        a[0] += n; a[1] += ms; a[2] += units * 2.0 * KERNEL_MAC.get(name, 0)
+    total_ms = sum(v[1] for v in merged.values())
+    for name, (n, ms, fl) in sorted(merged.items(), key=lambda kv: -kv[1][1]):
+        print(f'[bench] {name:16s} launches {n:5d}  {ms:9.3f} ms ({100 * ms / max(total_ms, 1e-9):5.1f}%)  '
+              f'{fl / max(ms, 1e-9) / 1e9:8.2f} TFLOP/s', file=sys.stderr)
+    dom, (n, ms, fl) = max(merged.items(), key=lambda kv: kv[1][1])
+    per_launch_ms = ms / n
+    achieved = fl / n / (per_launch_ms * 1e-3) / 1e12
+    peak = FP32_MFMA_PEAK_TFLOPS
+    return {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': peak, 'unit': 'TFLOP/s',
+            'frac': round(achieved / peak, 4), 'traffic': None, 'kernel': dom,
+            'avg_launch_ms': round(per_launch_ms, 4), 'launches': n,
+            'flop_per_launch': fl / n, 'share_of_device_time': round(ms / total_ms, 4)}
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -129,6 +156,9 @@ def main():
     if dist:
         tdist.barrier()
     torch.cuda.synchronize()
+    from neurecon_amd import _lib as L
+    L.profile_read()           # drop warm-up records
+    L.profile_enable(True)     # per-kernel HIP events on the launch stream, inside the timed region
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -136,6 +166,8 @@ def main():
     if dist:
         tdist.barrier()
     dt = time.perf_counter() - t0
+    L.profile_enable(False)
+    kstats = L.profile_read()
     if dist:
         t = torch.tensor([dt], device=dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -145,7 +177,7 @@ def main():
     value = total_rays / dt
     if rank == 0:
         ms = dt / args.steps * 1e3
-        achieved = RAY_FLOP * n_rays / (dt / args.steps) / 1e12
+        roof = roofline(kstats, args.precision)
         out = {
             'metric': 'rays/sec (4096 rays x 128 samples, 8-layer x256 SDF MLP)',
             'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
@@ -156,9 +188,8 @@ def main():
                                    '(64 coarse + 4x16 upsampled) samples, render mode',
                        'rays_per_gpu': n_rays, 'samples_per_ray': 128, 'precision': args.precision,
                        'parallelism': f'ray-sharded x{world}'},
-            'roofline': {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': FP32_MFMA_PEAK_TFLOPS,
-                         'unit': 'TFLOP/s', 'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': None,
-                         'scope': 'whole render step (per-kernel events pending)'},
+            'roofline': roof,
+            'step_tflops': round(RAY_FLOP * n_rays / (dt / args.steps) / 1e12, 2),
         }
         if not args.no_cpu_baseline and world == 1:
             out['cpu_baseline'] = cpu_baseline(args.cpu_rays)

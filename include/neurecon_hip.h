@@ -148,6 +148,21 @@ int nr_sample_pdf(const float* bins, const float* weights, int64_t R, int L, con
 int nr_get_rays(const float* c2w, const float* K, int B, int H, int W, const int64_t* select_inds, int64_t N,
                 float* rays_o, float* rays_d, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Opt-in kernel timing (diagnostics / bench roofline).  While enabled, every kernel launch of
+ * the library is bracketed by hipEvents on its stream; nr_profile_read() waits for them and
+ * returns per-kernel totals (launches, milliseconds, work units: points or rays), then clears.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  char name[32];
+  int64_t launches;
+  double ms;
+  double units;
+} NrKernelStat;
+
+int nr_profile_enable(int on);
+int nr_profile_read(NrKernelStat* out, int max, int* n_out);
+
 #ifdef __cplusplus
 }
 #endif

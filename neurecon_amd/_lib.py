@@ -48,6 +48,11 @@ class NrNeusArgs(ctypes.Structure):
     ]
 
 
+class NrKernelStat(ctypes.Structure):
+    _fields_ = [('name', ctypes.c_char * 32), ('launches', _c_i64), ('ms', ctypes.c_double),
+                ('units', ctypes.c_double)]
+
+
 _SIGS = {
     'nr_version': (_c_i, []),
     'nr_last_error': (ctypes.c_char_p, []),
@@ -63,6 +68,8 @@ _SIGS = {
     'nr_neus_render': (_c_i, [ctypes.POINTER(NrNeusArgs), _c_p]),
     'nr_sample_pdf': (_c_i, [_c_p, _c_p, _c_i64, _c_i, _c_p, _c_i, _c_p, _c_p]),
     'nr_get_rays': (_c_i, [_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p]),
+    'nr_profile_enable': (_c_i, [_c_i]),
+    'nr_profile_read': (_c_i, [ctypes.POINTER(NrKernelStat), _c_i, ctypes.POINTER(_c_i)]),
 }
 
 EXPORTED = tuple(_SIGS)
@@ -104,6 +111,18 @@ def ptr(t):
 
 def stream_of(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def profile_enable(on=True):
+    check(lib().nr_profile_enable(1 if on else 0))
+
+
+def profile_read():
+    """{kernel: (launches, total_ms, total_units)} since the last read (waits for the events)."""
+    buf = (NrKernelStat * 64)()
+    n = ctypes.c_int(0)
+    check(lib().nr_profile_read(buf, 64, ctypes.byref(n)))
+    return {buf[i].name.decode(): (buf[i].launches, buf[i].ms, buf[i].units) for i in range(n.value)}
 
 
 def require_gpu(t, what='input'):

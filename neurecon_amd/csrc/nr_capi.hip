@@ -109,21 +109,30 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   const dim3 blk(256), grd((R + 255) / 256);
   int rc;
 
+  {
+  ProfScope prof("neus_prologue", (double)R, st);
   hipLaunchKernelGGL(neus_prologue, grd, blk, 0, st, c, a.rays_o + ray0 * 3, a.rays_d + ray0 * 3, a.t_coarse,
                      a.obj_bounding_radius, a.near_bypass, a.far_bypass);
+  }
   NR_HIP_CHECK(hipGetLastError());
   // coarse SDF (no grad, neus.py:251)
   if ((rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)a.N_samples * R, c.sv, nullptr, nullptr, a.sdf->multires,
                        nullptr, 0, st)))
     return rc;
   for (int it = 0; it < a.N_upsample_iters; ++it) {
-    hipLaunchKernelGGL(neus_upsample, grd, blk, 0, st, c, it, a.u_fine);
+    {
+      ProfScope prof("neus_upsample", (double)R, st);
+      hipLaunchKernelGGL(neus_upsample, grd, blk, 0, st, c, it, a.u_fine);
+    }
     NR_HIP_CHECK(hipGetLastError());
     if ((rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)n_up * R, c.snew, nullptr, nullptr, a.sdf->multires,
                          nullptr, 0, st)))
       return rc;
   }
-  hipLaunchKernelGGL(neus_points, grd, blk, 0, st, c);
+  {
+    ProfScope prof("neus_points", (double)R, st);
+    hipLaunchKernelGGL(neus_points, grd, blk, 0, st, c);
+  }
   NR_HIP_CHECK(hipGetLastError());
   // SDF + nablas at the samples (neus.py:294)
   if ((rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)c.S * R, c.sdf_f, c.nab_f, nullptr, a.sdf->multires, mlp_ws,
@@ -138,7 +147,10 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
     return rc;
   NeusOut o{ray0, a.rgb, a.depth, a.acc, a.normals, a.d_final, a.sdf_out, a.nablas_out,
             a.radiance_out, a.alpha_out, a.cdf_out, a.weights_out};
-  hipLaunchKernelGGL(neus_composite, grd, blk, 0, st, c, o, a.s, a.calc_normal, a.white_bkgd);
+  {
+    ProfScope prof("neus_composite", (double)R, st);
+    hipLaunchKernelGGL(neus_composite, grd, blk, 0, st, c, o, a.s, a.calc_normal, a.white_bkgd);
+  }
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;
 }

@@ -33,6 +33,19 @@ void set_error(const std::string& msg);
     }                                                                                   \
   } while (0)
 
+// opt-in kernel timing (nr_profile.hip): brackets a launch with events on its stream
+bool prof_on();
+class ProfScope {
+ public:
+  ProfScope(const char* name, double units, hipStream_t st);
+  ~ProfScope();
+
+ private:
+  hipStream_t st_;
+  bool on_;
+  size_t idx_ = 0;
+};
+
 // ---------------------------------------------------------------------------------------------
 // Exact-rounding fp32 arithmetic.  The reference runs eager fp32 PyTorch ops, i.e. every
 // mul/add is rounded separately; hipcc would otherwise contract a*b+c into one FMA.
@@ -41,6 +54,78 @@ __device__ __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b)
 __device__ __forceinline__ float fadd(float a, float b) { return __fadd_rn(a, b); }
 __device__ __forceinline__ float fsub(float a, float b) { return __fsub_rn(a, b); }
 __device__ __forceinline__ float fdiv(float a, float b) { return __fdiv_rn(a, b); }
+
+// ATen's CPU float sum of one contiguous row (cascade_sum -> vectorized_inner_sum, or row_sum for
+// rows shorter than a vector), reproduced operation for operation so that normalisers feeding a
+// discrete decision (sample_pdf's `denom < eps`, searchsorted) round exactly like the reference.
+// Vector width 8 and the 4-way ILP / 4-level cascade were verified against torch.sum (2.10, x86).
+template <class Load>
+__device__ float aten_row_sum(int n, Load ld) {
+  constexpr int V = 8;
+  if (n < V) {
+    float p[4] = {0.f, 0.f, 0.f, 0.f};
+    const int si = n / 4;
+    for (int i = 0; i < si; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) p[k] = __fadd_rn(p[k], ld(4 * i + k));
+    for (int t = si * 4; t < n; ++t) p[0] = __fadd_rn(p[0], ld(t));
+    return __fadd_rn(__fadd_rn(__fadd_rn(p[0], p[1]), p[2]), p[3]);
+  }
+  const int vec_size = n / V, size_ilp = vec_size / 4;
+  float acc[4][4][V];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int l = 0; l < V; ++l) acc[j][k][l] = 0.f;
+  int cl2 = 1;
+  if (size_ilp > 2) { cl2 = 0; while ((1 << cl2) < size_ilp) ++cl2; }
+  const int lp = (cl2 / 4) > 4 ? (cl2 / 4) : 4;
+  const int step = 1 << lp, mask = step - 1;
+  int i = 0;
+  while (i + step <= size_ilp) {
+    for (int j = 0; j < step; ++j, ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int l = 0; l < V; ++l) acc[0][k][l] = __fadd_rn(acc[0][k][l], ld((4 * i + k) * V + l));
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int l = 0; l < V; ++l) {
+          acc[j][k][l] = __fadd_rn(acc[j][k][l], acc[j - 1][k][l]);
+          acc[j - 1][k][l] = 0.f;
+        }
+      if ((i & (mask << (j * lp))) != 0) break;
+    }
+  }
+  for (; i < size_ilp; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int l = 0; l < V; ++l) acc[0][k][l] = __fadd_rn(acc[0][k][l], ld((4 * i + k) * V + l));
+#pragma unroll
+  for (int j = 1; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int l = 0; l < V; ++l) acc[0][k][l] = __fadd_rn(acc[0][k][l], acc[j][k][l]);
+  for (int t = size_ilp * 4; t < vec_size; ++t)
+#pragma unroll
+    for (int l = 0; l < V; ++l) acc[0][0][l] = __fadd_rn(acc[0][0][l], ld(t * V + l));
+#pragma unroll
+  for (int k = 1; k < 4; ++k)
+#pragma unroll
+    for (int l = 0; l < V; ++l) acc[0][0][l] = __fadd_rn(acc[0][0][l], acc[0][k][l]);
+  float fa = 0.f;
+  for (int t = vec_size * V; t < n; ++t) fa = __fadd_rn(fa, ld(t));
+#pragma unroll
+  for (int l = 0; l < V; ++l) fa = __fadd_rn(fa, acc[0][0][l]);
+  return fa;
+}
 
 // torch.sigmoid(x) = 1 / (1 + exp(-x))
 __device__ __forceinline__ float sigmoidf_ref(float x) { return fdiv(1.0f, fadd(1.0f, expf(-x))); }

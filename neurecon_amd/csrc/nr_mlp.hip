@@ -579,6 +579,8 @@ int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t
   if (P <= 0) return NR_OK;
   const int grid = grid_for(P);
   SdfKArgs a{(const char*)packed, L, pts, P, sdf, nabla, feature, (float4*)ws, nfreq};
+  ProfScope prof(nabla ? (feature ? "sdf_nabla_feat" : "sdf_nabla") : (feature ? "sdf_feat" : "sdf_fwd"), (double)P,
+                 stream);
   if (nabla) {
     const size_t need = (size_t)grid * kScratchPerWG;
     NR_REQUIRE(ws && ws_bytes >= need, NR_ERR_WORKSPACE, "sdf nabla workspace too small");
@@ -596,6 +598,7 @@ int launch_radiance(const RadLayout& L, const void* packed, const float* x, cons
   if (P <= 0) return NR_OK;
   const int grid = grid_for(P);
   RadKArgs a{(const char*)packed, L, x, vdir, vdiv, vmod, normals, feature, P, rgb, nfreq_view};
+  ProfScope prof("radiance", (double)P, stream);
   switch (L.kbs) {
     case 2: hipLaunchKernelGGL(radiance_kernel<2>, dim3(grid), dim3(kThreads), 0, stream, a); break;
     case 4: hipLaunchKernelGGL(radiance_kernel<4>, dim3(grid), dim3(kThreads), 0, stream, a); break;

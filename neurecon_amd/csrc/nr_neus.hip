@@ -132,7 +132,6 @@ __global__ void neus_upsample(NeusChunk c, int it, const float* __restrict__ u) 
   const float S = (float)(64 << it);  // 64 * 2**i
   float prev_slope = 0.0f;
   double T = 1.0;
-  double total = 0.0;
   float s0 = c.sv[r], z0 = c.dv[r];
   for (int i = 0; i < L - 1; ++i) {
     const float s1 = c.sv[(i + 1) * R + r], z1 = c.dv[(i + 1) * R + r];
@@ -149,11 +148,12 @@ __global__ void neus_upsample(NeusChunk c, int it, const float* __restrict__ u) 
     const float w = fmul(alpha, (float)T);
     T *= (double)fadd(fsub(1.0f, alpha), 1e-10f);
     c.wtmp[i * R + r] = w;
-    total += (double)fadd(w, 1e-5f);
     s0 = s1;
     z0 = z1;
   }
-  sample_pdf_ray(c.dv + r, c.wtmp + r, R, L, (float)total, u, c.n_up, c.dnew + r, R);
+  const float* wr = c.wtmp + r;
+  const float total = aten_row_sum(L - 1, [&](int i) { return fadd(wr[i * R], 1e-5f); });
+  sample_pdf_ray(c.dv + r, wr, R, L, total, u, c.n_up, c.dnew + r, R);
   const float ox = c.ro[r * 3], oy = c.ro[r * 3 + 1], oz = c.ro[r * 3 + 2];
   const float dx = c.rd[r * 3], dy = c.rd[r * 3 + 1], dz = c.rd[r * 3 + 2];
   for (int k = 0; k < c.n_up; ++k) {
@@ -275,9 +275,9 @@ __global__ void sample_pdf_kernel(const float* __restrict__ bins, const float* _
                                   const float* __restrict__ u, int N, float* __restrict__ out) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
-  double total = 0.0;
-  for (int i = 0; i < L - 1; ++i) total += (double)fadd(weights[r * (L - 1) + i], 1e-5f);
-  sample_pdf_ray(bins + r * L, weights + r * (L - 1), 1, L, (float)total, u, N, out + r * N, 1);
+  const float* wr = weights + r * (L - 1);
+  const float total = aten_row_sum(L - 1, [&](int i) { return fadd(wr[i], 1e-5f); });
+  sample_pdf_ray(bins + r * L, wr, 1, L, total, u, N, out + r * N, 1);
 }
 
 // ---------------------------------------------------------------------------------------------

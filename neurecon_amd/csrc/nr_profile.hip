@@ -1,0 +1,76 @@
+// neurecon_amd — opt-in per-kernel timing with HIP events (bench.py roofline numbers).
+// Disabled by default; when enabled each library kernel launch is bracketed by two events on its
+// own stream, so the measured duration is that kernel's, not the surrounding step's.
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "nr_common.h"
+
+namespace nr {
+
+struct ProfRec {
+  const char* name;
+  double units;
+  hipEvent_t a, b;
+};
+static std::mutex g_mu;
+static std::vector<ProfRec> g_recs;
+static bool g_on = false;
+
+bool prof_on() { return g_on; }
+
+ProfScope::ProfScope(const char* name, double units, hipStream_t st) : st_(st), on_(g_on) {
+  if (!on_) return;
+  ProfRec r{name, units, nullptr, nullptr};
+  if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) { on_ = false; return; }
+  (void)hipEventRecord(r.a, st);
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_recs.push_back(r);
+  idx_ = g_recs.size() - 1;
+}
+
+ProfScope::~ProfScope() {
+  if (!on_) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  (void)hipEventRecord(g_recs[idx_].b, st_);
+}
+
+}  // namespace nr
+
+using namespace nr;
+
+extern "C" int nr_profile_enable(int on) {
+  g_on = on != 0;
+  return NR_OK;
+}
+
+extern "C" int nr_profile_read(NrKernelStat* out, int max, int* n_out) {
+  NR_REQUIRE(n_out, NR_ERR_ARG, "nr_profile_read: null n_out");
+  std::lock_guard<std::mutex> lk(g_mu);
+  std::vector<NrKernelStat> acc;
+  for (auto& r : g_recs) {
+    float ms = 0.f;
+    if (hipEventSynchronize(r.b) == hipSuccess) (void)hipEventElapsedTime(&ms, r.a, r.b);
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+    NrKernelStat* s = nullptr;
+    for (auto& x : acc)
+      if (std::string(x.name) == r.name) s = &x;
+    if (!s) {
+      NrKernelStat z{};
+      snprintf(z.name, sizeof(z.name), "%s", r.name);
+      acc.push_back(z);
+      s = &acc.back();
+    }
+    s->launches += 1;
+    s->ms += ms;
+    s->units += r.units;
+  }
+  g_recs.clear();
+  int n = 0;
+  for (auto& x : acc)
+    if (n < max && out) out[n++] = x;
+  *n_out = n;
+  return NR_OK;
+}
