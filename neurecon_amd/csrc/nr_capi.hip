@@ -23,7 +23,8 @@ int check_sdf_desc(const NrSdfDesc* d) {
   NR_REQUIRE(d->D == 8 && d->W == 256 && d->skip == 4 && d->multires == 6 && d->W_geo_feat == 256,
              NR_ERR_UNSUPPORTED,
              "SDF net: only D=8, W=256, skips=[4], embed_multires=6, W_geo_feat=256 are implemented");
-  NR_REQUIRE(d->precision == NR_PREC_FP32, NR_ERR_UNSUPPORTED, "SDF net: precision mode not implemented");
+  NR_REQUIRE(d->precision == NR_PREC_FP32 || d->precision == NR_PREC_F16X3, NR_ERR_UNSUPPORTED,
+             "SDF net: unknown precision mode");
   return NR_OK;
 }
 
@@ -32,7 +33,8 @@ int check_rad_desc(const NrRadDesc* d) {
   NR_REQUIRE(d->D == 4 && d->W == 256 && d->multires < 0 && d->W_geo_feat == 256 && d->multires_view <= 7,
              NR_ERR_UNSUPPORTED,
              "radiance net: only D=4, W=256, embed_multires=-1, embed_multires_view<=7, W_geo_feat=256");
-  NR_REQUIRE(d->precision == NR_PREC_FP32, NR_ERR_UNSUPPORTED, "radiance net: precision mode not implemented");
+  NR_REQUIRE(d->precision == NR_PREC_FP32 || d->precision == NR_PREC_F16X3, NR_ERR_UNSUPPORTED,
+             "radiance net: unknown precision mode");
   return NR_OK;
 }
 
@@ -40,14 +42,17 @@ int check_rad_desc(const NrRadDesc* d) {
 static const int kSdfKB[kSdfOps] = {4, 16, 16, 16, 18, 16, 16, 16, 16, 16, 16, 16, 16, 14, 16, 16, 16};
 static const int kSdfNBO[kSdfOps] = {16, 16, 16, 14, 16, 16, 16, 16, 16, 16, 16, 16, 18, 16, 16, 16, 4};
 
-SdfLayout sdf_layout(const NrSdfDesc&) {
+SdfLayout sdf_layout(const NrSdfDesc& d) {
   SdfLayout L{};
+  L.prec = d.precision;
   size_t off = 0;
   for (int i = 0; i < kSdfOps; ++i) {
     L.op_bytes[i] = (2 * kSdfKB[i] + 1) * 1024;
     L.op_off[i] = (uint32_t)off;
     off += (size_t)(kSdfNBO[i] / 2) * L.op_bytes[i];
   }
+  L.scale_off = (uint32_t)off;
+  off = align256(off + kSdfOps * 4);
   L.w8row0_off = (uint32_t)off;
   off = align256(off + 256 * 4);
   L.misc_off = (uint32_t)off;
@@ -60,6 +65,7 @@ static int rad_small(const NrRadDesc& d) { return 3 + (d.multires_view < 0 ? 3 :
 
 RadLayout rad_layout(const NrRadDesc& d) {
   RadLayout L{};
+  L.prec = d.precision;
   L.n_small = rad_small(d);
   L.kbs = L.n_small <= 32 ? 2 : 4;
   size_t off = 0;
@@ -69,6 +75,8 @@ RadLayout rad_layout(const NrRadDesc& d) {
     L.op_off[i] = (uint32_t)off;
     off += 8 * (size_t)L.op_bytes[i];
   }
+  L.scale_off = (uint32_t)off;
+  off = align256(off + 4 * 4);
   L.head_off = (uint32_t)off;
   off = align256(off + (3 * 256 + 4) * 4);
   L.total = (uint32_t)off;
@@ -76,6 +84,14 @@ RadLayout rad_layout(const NrRadDesc& d) {
 }
 
 static PackSeg seg(int nblk, int off, int nvalid) { return PackSeg{nblk, off, nvalid}; }
+static PackOp mkop(const float* W, const float* bias, int rows, int ld, int tr, PackSeg o0, PackSeg o1, PackSeg i0,
+                   PackSeg i1, float scale, int prec, float* wmax) {
+  PackOp op{};
+  op.W = W; op.bias = bias; op.wn = (int64_t)rows * ld; op.ld = ld; op.transpose = tr;
+  op.out[0] = o0; op.out[1] = o1; op.in[0] = i0; op.in[1] = i1;
+  op.scale = scale; op.prec = prec; op.wmax = wmax;
+  return op;
+}
 static PackSeg none() { return PackSeg{0, 0, 0}; }
 
 static size_t scratch_bytes() {
@@ -184,26 +200,29 @@ int nr_sdf_pack(const NrSdfDesc* d, const float* const* W, const float* const* b
   char* P = (char*)packed;
   const int in0 = 39, n3 = 217;
   const float isq2 = 1.0f / 1.41421356237309504880f;
+  const int prec = d->precision;
+  float* wmax = (float*)(P + L.scale_off);
+  auto ROWS = [&](int l) { return l == 3 ? n3 : (l == 8 ? 257 : 256); };
   PackOp ops[kSdfOps];
   // forward
-  ops[F0] = PackOp{W[0], b[0], in0, 0, {seg(16, 0, 256), none()}, {seg(4, 0, in0), none()}, 1.0f};
-  ops[F1] = PackOp{W[1], b[1], 256, 0, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
-  ops[F2] = PackOp{W[2], b[2], 256, 0, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
-  ops[F3] = PackOp{W[3], b[3], 256, 0, {seg(14, 0, n3), none()}, {seg(16, 0, 256), none()}, 1.0f};
-  ops[F4] = PackOp{W[4], b[4], 256, 0, {seg(16, 0, 256), none()}, {seg(14, 0, n3), seg(4, n3, in0)}, isq2};
-  ops[F5] = PackOp{W[5], b[5], 256, 0, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
-  ops[F6] = PackOp{W[6], b[6], 256, 0, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
-  ops[F7] = PackOp{W[7], b[7], 256, 0, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
-  ops[F8] = PackOp{W[8], b[8], 256, 0, {seg(16, 1, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  ops[F0] = mkop(W[0], b[0], ROWS(0), in0, 0, seg(16, 0, 256), none(), seg(4, 0, in0), none(), 1.0f, prec, wmax + F0);
+  ops[F1] = mkop(W[1], b[1], ROWS(1), 256, 0, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + F1);
+  ops[F2] = mkop(W[2], b[2], ROWS(2), 256, 0, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + F2);
+  ops[F3] = mkop(W[3], b[3], ROWS(3), 256, 0, seg(14, 0, n3), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + F3);
+  ops[F4] = mkop(W[4], b[4], ROWS(4), 256, 0, seg(16, 0, 256), none(), seg(14, 0, n3), seg(4, n3, in0), isq2, prec, wmax + F4);
+  ops[F5] = mkop(W[5], b[5], ROWS(5), 256, 0, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + F5);
+  ops[F6] = mkop(W[6], b[6], ROWS(6), 256, 0, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + F6);
+  ops[F7] = mkop(W[7], b[7], ROWS(7), 256, 0, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + F7);
+  ops[F8] = mkop(W[8], b[8], ROWS(8), 256, 0, seg(16, 1, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + F8);
   // backward (transposed)
-  ops[B7] = PackOp{W[7], nullptr, 256, 1, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
-  ops[B6] = PackOp{W[6], nullptr, 256, 1, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
-  ops[B5] = PackOp{W[5], nullptr, 256, 1, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
-  ops[B4] = PackOp{W[4], nullptr, 256, 1, {seg(14, 0, n3), seg(4, n3, in0)}, {seg(16, 0, 256), none()}, isq2};
-  ops[B3] = PackOp{W[3], nullptr, 256, 1, {seg(16, 0, 256), none()}, {seg(14, 0, n3), none()}, 1.0f};
-  ops[B2] = PackOp{W[2], nullptr, 256, 1, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
-  ops[B1] = PackOp{W[1], nullptr, 256, 1, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
-  ops[B0] = PackOp{W[0], nullptr, in0, 1, {seg(4, 0, in0), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  ops[B7] = mkop(W[7], nullptr, ROWS(7), 256, 1, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + B7);
+  ops[B6] = mkop(W[6], nullptr, ROWS(6), 256, 1, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + B6);
+  ops[B5] = mkop(W[5], nullptr, ROWS(5), 256, 1, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + B5);
+  ops[B4] = mkop(W[4], nullptr, ROWS(4), 256, 1, seg(14, 0, n3), seg(4, n3, in0), seg(16, 0, 256), none(), isq2, prec, wmax + B4);
+  ops[B3] = mkop(W[3], nullptr, ROWS(3), 256, 1, seg(16, 0, 256), none(), seg(14, 0, n3), none(), 1.0f, prec, wmax + B3);
+  ops[B2] = mkop(W[2], nullptr, ROWS(2), 256, 1, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + B2);
+  ops[B1] = mkop(W[1], nullptr, ROWS(1), 256, 1, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + B1);
+  ops[B0] = mkop(W[0], nullptr, ROWS(0), in0, 1, seg(4, 0, in0), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + B0);
   for (int i = 0; i < kSdfOps; ++i)
     if ((rc = launch_pack_op(ops[i], P + L.op_off[i], st))) return rc;
   if ((rc = launch_pack_vec(W[8], 0, 256, 256, P + L.w8row0_off, st))) return rc;
@@ -237,8 +256,11 @@ int nr_radiance_pack(const NrRadDesc* d, const float* const* W, const float* con
   char* P = (char*)packed;
   const int ns = L.n_small, ld0 = ns + 256;
   PackOp ops[4];
-  ops[0] = PackOp{W[0], b[0], ld0, 0, {seg(16, 0, 256), none()}, {seg(16, ns, 256), seg(L.kbs, 0, ns)}, 1.0f};
-  for (int i = 1; i < 4; ++i) ops[i] = PackOp{W[i], b[i], 256, 0, {seg(16, 0, 256), none()}, {seg(16, 0, 256), none()}, 1.0f};
+  const int prec = d->precision;
+  float* wmax = (float*)(P + L.scale_off);
+  ops[0] = mkop(W[0], b[0], 256, ld0, 0, seg(16, 0, 256), none(), seg(16, ns, 256), seg(L.kbs, 0, ns), 1.0f, prec, wmax);
+  for (int i = 1; i < 4; ++i)
+    ops[i] = mkop(W[i], b[i], 256, 256, 0, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + i);
   for (int i = 0; i < 4; ++i) {
     if ((rc = launch_pack_op(ops[i], P + L.op_off[i], st))) return rc;
   }

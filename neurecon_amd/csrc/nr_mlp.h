@@ -17,16 +17,20 @@ enum SdfOp { F0, F1, F2, F3, F4, F5, F6, F7, F8, B7, B6, B5, B4, B3, B2, B1, B0,
 struct SdfLayout {
   uint32_t op_off[kSdfOps];
   uint32_t op_bytes[kSdfOps];  // bytes of one chunk of the op
+  uint32_t scale_off;          // [kSdfOps] max |W| per op (f16x3 weight scaling)
   uint32_t w8row0_off;         // sdf row of the last layer [256]
   uint32_t misc_off;           // [0] = sdf bias
   uint32_t total;
+  int prec;
 };
 
 struct RadLayout {
   uint32_t op_off[4];
   uint32_t op_bytes[4];
   uint32_t head_off;  // [3][256] weights, then [3] bias
+  uint32_t scale_off; // [4] max |W| per op
   uint32_t total;
+  int prec;
   int kbs;            // small-input blocks (even)
   int n_small;        // 3 + view-embedding + 3
 };
@@ -40,11 +44,14 @@ struct PackSeg {
 struct PackOp {
   const float* W;
   const float* bias;  // per output row (same row mapping as W), or null
+  int64_t wn;         // elements of W (for the max-|W| scan)
   int ld;
   int transpose;  // 1: value = W[in][out] (Wᵀ)
   PackSeg out[2];
   PackSeg in[2];
   float scale;
+  int prec;            // NR_PREC_*
+  float* wmax;         // device word receiving max |W * scale| (f16x3 scaling)
 };
 
 int launch_pack_op(const PackOp& op, char* dst, hipStream_t stream);

@@ -26,19 +26,37 @@ using lds_ptr = __attribute__((address_space(3))) void*;
 // ---------------------------------------------------------------------------------------------
 // LDS weight stream: 2 buffers of kMaxChunkBytes, filled by LDS-DMA (global_load_lds, 16 B/lane)
 // ---------------------------------------------------------------------------------------------
+// The DMA is issued from inline asm so that hipcc does not treat it as a pending LDS store:
+// with the builtin, hipcc puts `s_waitcnt vmcnt(0)` in front of the next ds_read, i.e. every chunk
+// would wait for the *next* chunk's weights before computing (no overlap).  Completion is
+// counted by hand: vmcnt(0) + barrier in flip(), one chunk after the issue.
+__device__ __forceinline__ void glds16(const char* gsrc, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+
 struct WStream {
   char* lds;
   int cur;
   __device__ __forceinline__ void issue(const char* gsrc, int bytes) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    char* dst = lds + (cur ^ 1) * kMaxChunkBytes;
-    for (int off = wave * 1024; off < bytes; off += kThreads * 16) {
-      __builtin_amdgcn_global_load_lds((const void*)(gsrc + off + lane * 16), (lds_ptr)(dst + off), 16, 0, 0);
-    }
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t base = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)lds) +
+                          (uint32_t)((cur ^ 1) * kMaxChunkBytes);
+    for (int off = wave * 1024; off < bytes; off += kThreads * 16)
+      glds16(gsrc + off + lane * 16, __builtin_amdgcn_readfirstlane(base + off));
   }
   __device__ __forceinline__ const float4* buf() const { return (const float4*)(lds + cur * kMaxChunkBytes); }
   __device__ __forceinline__ void flip() {
-    __syncthreads();  // drains the LDS-DMA (vmcnt) and orders it for every wave
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA for the next chunk landed
+    __syncthreads();                                   // ... and every other wave's
     cur ^= 1;
   }
 };
@@ -105,25 +123,103 @@ __device__ __forceinline__ void push2cat(float4 (&Y)[16], float4 (&Z)[4], float4
 // Softplus(beta=100, threshold=20): y = (100 z > 20) ? z : log1p(exp(100 z)) / 100.
 // e = exp(100 z) is kept for the backward (softplus_backward: g * e / (e + 1)); +inf marks the
 // linear branch (gradient passes through unchanged).
+//  P = NR_PREC_FP32 : libm-accurate expf/log1pf and IEEE division, op order of the reference.
+//  P = NR_PREC_F16X3: hardware v_exp_f32 / v_log_f32 / v_rcp_f32 (~1e-6 rel), for the fast mode.
+template <int P>
 __device__ __forceinline__ void softplus_fwd(float z, float& y, float& e) {
   const float t = fmul(z, 100.0f);
-  const float ex = expf(t);
   const bool lin = t > 20.0f;
-  y = lin ? z : fdiv(log1pf(ex), 100.0f);
-  e = lin ? __builtin_inff() : ex;
+  if constexpr (P == NR_PREC_FP32) {
+    const float ex = expf(t);
+    y = lin ? z : fdiv(log1pf(ex), 100.0f);
+    e = lin ? __builtin_inff() : ex;
+  } else {
+    const float ex = __builtin_amdgcn_exp2f(t * 1.44269504088896341f);
+    y = lin ? z : __builtin_amdgcn_logf(1.0f + ex) * (0.693147180559945309f * 0.01f);
+    e = lin ? __builtin_inff() : ex;
+  }
 }
+template <int P>
 __device__ __forceinline__ float softplus_bwd(float g, float e) {
-  return __builtin_isinf(e) ? g : fdiv(fmul(g, e), fadd(e, 1.0f));
+  if constexpr (P == NR_PREC_FP32) return __builtin_isinf(e) ? g : fdiv(fmul(g, e), fadd(e, 1.0f));
+  else return __builtin_isinf(e) ? g : g * e * __builtin_amdgcn_rcpf(e + 1.0f);
 }
 
 enum { ACT_NONE = 0, ACT_SOFTPLUS = 1, ACT_RELU = 2 };
 
-// chunk = [A: 2*KB KB][bias slot: 32 floats (2 output blocks), padded to 1 KB]
+// chunk = [A: 2*KB KB][bias slot: 32 floats (2 output blocks), [32] = 1/weight-scale; 1 KB]
 __host__ __device__ constexpr int chunk_bytes(int KB) { return (2 * KB + 1) * 1024; }
+
+// ---------------------------------------------------------------------------------------------
+// split-fp16 x3 operands: v = (hi + lo) * 2^-k with hi = f16(v 2^k), lo = f16(v 2^k - hi).
+// One power-of-two scale per point (column of the B operand) keeps |hi| < 2^13 and lo normal.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ f32x4 mfma16h(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f16x8 as_h8(float4 v) { return __builtin_bit_cast(f16x8, v); }
+
+__device__ __forceinline__ float amax4(float4 v) {
+  return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
+// 2^(13 - e) with m = f 2^e, f in [0.5, 1): m * scale < 2^13
+__device__ __forceinline__ float pow2_scale(float m) {
+  if (!(m > 0.0f) || __builtin_isinf(m)) return 1.0f;
+  return __builtin_ldexpf(1.0f, 13 - __builtin_amdgcn_frexp_expf(m));
+}
+__device__ __forceinline__ void split8(float4 lo4, float4 hi4, float sc, f16x8& h, f16x8& l) {
+  const float v[8] = {lo4.x * sc, lo4.y * sc, lo4.z * sc, lo4.w * sc, hi4.x * sc, hi4.y * sc, hi4.z * sc, hi4.w * sc};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const _Float16 hh = (_Float16)v[e];
+    h[e] = hh;
+    l[e] = (_Float16)(v[e] - (float)hh);
+  }
+}
+// B operand of a layer whose input is [X[0..KBX) ; E[0..KBE)] (16-feature blocks, acc layout):
+// k-step s pairs blocks 2s, 2s+1.  Returns 1/scale of this lane's point.
+template <int KBX, int KBE>
+__device__ __forceinline__ float make_b16(const float4 (&X)[16], const float4 (&E)[4], f16x8 (&bh)[12],
+                                          f16x8 (&bl)[12]) {
+  constexpr int KB = KBX + KBE;
+  static_assert(KB % 2 == 0 && KB <= 24, "bad block count");
+  float m = 0.0f;
+#pragma unroll
+  for (int b = 0; b < KBX; ++b) m = fmaxf(m, amax4(X[b]));
+#pragma unroll
+  for (int b = 0; b < KBE; ++b) m = fmaxf(m, amax4(E[b]));
+  m = fmaxf(m, __shfl_xor(m, 16));
+  m = fmaxf(m, __shfl_xor(m, 32));
+  const float sc = pow2_scale(m);
+#pragma unroll
+  for (int s = 0; s < KB / 2; ++s) {
+    const int b0 = 2 * s, b1 = 2 * s + 1;
+    const float4 v0 = b0 < KBX ? X[b0 < KBX ? b0 : 0] : E[b0 < KBX ? 0 : b0 - KBX];
+    const float4 v1 = b1 < KBX ? X[b1 < KBX ? b1 : 0] : E[b1 < KBX ? 0 : b1 - KBX];
+    split8(v0, v1, sc, bh[s], bl[s]);
+  }
+  return 1.0f / sc;
+}
+// A layout (f16x3): [obl(2)][s(NS)][hl(2)][lane(64)] x 16 B (8 halves)
+template <int NS>
+__device__ __forceinline__ void mma_chunk_h3(const float4* __restrict__ A, const f16x8 (&bh)[12],
+                                             const f16x8 (&bl)[12], f32x4& acc0, f32x4& acc1, int lane) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const f16x8 h0 = as_h8(A[(s * 2) * 64 + lane]), l0 = as_h8(A[(s * 2 + 1) * 64 + lane]);
+    const f16x8 h1 = as_h8(A[((NS + s) * 2) * 64 + lane]), l1 = as_h8(A[((NS + s) * 2 + 1) * 64 + lane]);
+    acc0 = mfma16h(l0, bh[s], acc0);
+    acc1 = mfma16h(l1, bh[s], acc1);
+    acc0 = mfma16h(h0, bl[s], acc0);
+    acc1 = mfma16h(h1, bl[s], acc1);
+    acc0 = mfma16h(h0, bh[s], acc0);
+    acc1 = mfma16h(h1, bh[s], acc1);
+  }
+}
 
 // Forward GEMM layer: Y[0..NBO) = act(W · [X[0..KBX) ; E[0..KBE)] + bias).
 // `op` chunks are consumed from the stream; `nxt/nxt_bytes` is the chunk that follows this op.
-template <int KBX, int KBE, int NBO, int ACT>
+template <int P, int KBX, int KBE, int NBO, int ACT>
 __device__ __forceinline__ void gemm_fwd(WStream& ws, const char* __restrict__ op, const char* nxt, int nxt_bytes,
                                          const float4 (&X)[16], const float4 (&E)[4], float4 (&Y)[16],
                                          float4* __restrict__ e_out, float* __restrict__ feat_out, bool feat_ok,
@@ -131,45 +227,76 @@ __device__ __forceinline__ void gemm_fwd(WStream& ws, const char* __restrict__ o
   constexpr int KB = KBX + KBE;
   constexpr int CB = chunk_bytes(KB);
   const int g = lane >> 4;
+  f16x8 bh[12], bl[12];
+  float xinv = 1.0f;
+  if constexpr (P == NR_PREC_F16X3) xinv = make_b16<KBX, KBE>(X, E, bh, bl);
+  // global stores of chunk c are issued at the start of chunk c+1, *before* that chunk's DMA, so
+  // the vmcnt(0) in flip() waits for a store that had a whole chunk to retire, not a fresh one
+  float4 p0 = make_float4(0, 0, 0, 0), p1 = p0;
+  int pc = -1;
+  auto drain = [&]() {
+    if (pc >= 0) {
+      if constexpr (ACT == ACT_SOFTPLUS) {
+        if (e_out) {
+          e_out[(2 * pc) * 64 + lane] = p0;
+          e_out[(2 * pc + 1) * 64 + lane] = p1;
+        }
+      } else {
+        if (feat_out && feat_ok) {  // row-major [P][256] feature rows of that chunk
+          *(float4*)(feat_out + (2 * pc) * 16 + g * 4) = p0;
+          *(float4*)(feat_out + (2 * pc + 1) * 16 + g * 4) = p1;
+        }
+      }
+    }
+    pc = -1;
+  };
 #pragma unroll 1
   for (int c = 0; c < NBO / 2; ++c) {
+    drain();
     if (c + 1 < NBO / 2) ws.issue(op + (c + 1) * CB, CB);
     else if (nxt) ws.issue(nxt, nxt_bytes);
     const float4* A = ws.buf();
-    f32x4 acc0 = tof(A[2 * KB * 64 + g]);
-    f32x4 acc1 = tof(A[2 * KB * 64 + 4 + g]);
-    mma_chunk<KBX, KBE>(A, X, E, acc0, acc1, lane);
+    const f32x4 b0 = tof(A[2 * KB * 64 + g]), b1 = tof(A[2 * KB * 64 + 4 + g]);
+    f32x4 acc0, acc1;
+    if constexpr (P == NR_PREC_FP32) {
+      acc0 = b0;
+      acc1 = b1;
+      mma_chunk<KBX, KBE>(A, X, E, acc0, acc1, lane);
+    } else {
+      acc0 = f32x4{0, 0, 0, 0};
+      acc1 = f32x4{0, 0, 0, 0};
+      mma_chunk_h3<KB / 2>(A, bh, bl, acc0, acc1, lane);
+      const float inv = xinv * A[2 * KB * 64 + 8].x;  // 1/(x scale * w scale), exact powers of two
+      acc0 = acc0 * inv + b0;
+      acc1 = acc1 * inv + b1;
+    }
     float4 y0, y1;
     if constexpr (ACT == ACT_SOFTPLUS) {
-      float4 e0, e1;
-      softplus_fwd(acc0[0], y0.x, e0.x); softplus_fwd(acc0[1], y0.y, e0.y);
-      softplus_fwd(acc0[2], y0.z, e0.z); softplus_fwd(acc0[3], y0.w, e0.w);
-      softplus_fwd(acc1[0], y1.x, e1.x); softplus_fwd(acc1[1], y1.y, e1.y);
-      softplus_fwd(acc1[2], y1.z, e1.z); softplus_fwd(acc1[3], y1.w, e1.w);
-      if (e_out) {
-        e_out[(2 * c) * 64 + lane] = e0;
-        e_out[(2 * c + 1) * 64 + lane] = e1;
-      }
+      softplus_fwd<P>(acc0[0], y0.x, p0.x); softplus_fwd<P>(acc0[1], y0.y, p0.y);
+      softplus_fwd<P>(acc0[2], y0.z, p0.z); softplus_fwd<P>(acc0[3], y0.w, p0.w);
+      softplus_fwd<P>(acc1[0], y1.x, p1.x); softplus_fwd<P>(acc1[1], y1.y, p1.y);
+      softplus_fwd<P>(acc1[2], y1.z, p1.z); softplus_fwd<P>(acc1[3], y1.w, p1.w);
+      pc = c;
     } else if constexpr (ACT == ACT_RELU) {
       y0 = make_float4(fmaxf(acc0[0], 0.f), fmaxf(acc0[1], 0.f), fmaxf(acc0[2], 0.f), fmaxf(acc0[3], 0.f));
       y1 = make_float4(fmaxf(acc1[0], 0.f), fmaxf(acc1[1], 0.f), fmaxf(acc1[2], 0.f), fmaxf(acc1[3], 0.f));
     } else {
       y0 = fromf(acc0);
       y1 = fromf(acc1);
-    }
-    if (feat_out && feat_ok) {  // row-major [P][256] feature rows of this chunk
-      *(float4*)(feat_out + (2 * c) * 16 + g * 4) = y0;
-      *(float4*)(feat_out + (2 * c + 1) * 16 + g * 4) = y1;
+      p0 = y0;
+      p1 = y1;
+      pc = c;
     }
     push2<NBO>(Y, y0, y1);
     ws.flip();
   }
+  drain();
 }
 
 // Backward GEMM layer: out = Wᵀ · G (no bias).  The first NBO1 output blocks are scaled by
 // softplus'(z) of the previous layer (e_prev) and rotated into Y; the remaining NBO2 blocks are
 // gradients w.r.t. the positional encoding and are handed to `emb(block, value)` as produced.
-template <int KBG, int NBO1, int NBO2, class EmbFn>
+template <int P, int KBG, int NBO1, int NBO2, class EmbFn>
 __device__ __forceinline__ void gemm_bwd(WStream& ws, const char* __restrict__ op, const char* nxt, int nxt_bytes,
                                          const float4 (&G)[16], float4 (&Y)[16], const float4* __restrict__ e_prev,
                                          int lane, EmbFn&& emb) {
@@ -177,6 +304,9 @@ __device__ __forceinline__ void gemm_bwd(WStream& ws, const char* __restrict__ o
   static_assert(NBO1 % 2 == 0 && NBO2 % 2 == 0, "output segments must be chunk aligned");
   constexpr int CB = chunk_bytes(KBG);
   const float4 dummy[4] = {};
+  f16x8 bh[12], bl[12];
+  float ginv = 1.0f;
+  if constexpr (P == NR_PREC_F16X3) ginv = make_b16<KBG, 0>(G, dummy, bh, bl);
 #pragma unroll 1
   for (int c = 0; c < NBO / 2; ++c) {
     if (c + 1 < NBO / 2) ws.issue(op + (c + 1) * CB, CB);
@@ -187,15 +317,23 @@ __device__ __forceinline__ void gemm_bwd(WStream& ws, const char* __restrict__ o
       e0 = e_prev[(2 * c) * 64 + lane];
       e1 = e_prev[(2 * c + 1) * 64 + lane];
     }
+    const float4* A = ws.buf();
     f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
-    mma_chunk<KBG, 0>(ws.buf(), G, dummy, acc0, acc1, lane);
+    if constexpr (P == NR_PREC_FP32) {
+      mma_chunk<KBG, 0>(A, G, dummy, acc0, acc1, lane);
+    } else {
+      mma_chunk_h3<KBG / 2>(A, bh, bl, acc0, acc1, lane);
+      const float inv = ginv * A[2 * KBG * 64 + 8].x;
+      acc0 = acc0 * inv;
+      acc1 = acc1 * inv;
+    }
     float4 y0 = fromf(acc0), y1 = fromf(acc1);
     if (main) {
       if (e_prev) {
-        y0 = make_float4(softplus_bwd(y0.x, e0.x), softplus_bwd(y0.y, e0.y), softplus_bwd(y0.z, e0.z),
-                         softplus_bwd(y0.w, e0.w));
-        y1 = make_float4(softplus_bwd(y1.x, e1.x), softplus_bwd(y1.y, e1.y), softplus_bwd(y1.z, e1.z),
-                         softplus_bwd(y1.w, e1.w));
+        y0 = make_float4(softplus_bwd<P>(y0.x, e0.x), softplus_bwd<P>(y0.y, e0.y), softplus_bwd<P>(y0.z, e0.z),
+                         softplus_bwd<P>(y0.w, e0.w));
+        y1 = make_float4(softplus_bwd<P>(y1.x, e1.x), softplus_bwd<P>(y1.y, e1.y), softplus_bwd<P>(y1.z, e1.z),
+                         softplus_bwd<P>(y1.w, e1.w));
       }
       if constexpr (NBO1 > 0) push2<NBO1>(Y, y0, y1);
     } else {
@@ -265,7 +403,7 @@ struct SdfKArgs {
   int nfreq;
 };
 
-template <bool NABLA>
+template <int P, bool NABLA>
 __global__ __launch_bounds__(kThreads) void sdf_kernel(SdfKArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kMaxChunkBytes];
   WStream ws{smem, 1};
@@ -304,17 +442,17 @@ __global__ __launch_bounds__(kThreads) void sdf_kernel(SdfKArgs a) {
     for (int l = 0; l < 8; ++l) e_l[l] = NABLA ? escr + l * 16 * 64 : nullptr;
 
     // ---- forward (base.py:243-257) -----------------------------------------------------------
-    gemm_fwd<0, 4, 16, ACT_SOFTPLUS>(ws, OP(F0), OP(F1), OPB(F1), X, E, Y, e_l[0], nullptr, false, lane);
-    gemm_fwd<16, 0, 16, ACT_SOFTPLUS>(ws, OP(F1), OP(F2), OPB(F2), Y, E, X, e_l[1], nullptr, false, lane);
-    gemm_fwd<16, 0, 16, ACT_SOFTPLUS>(ws, OP(F2), OP(F3), OPB(F3), X, E, Y, e_l[2], nullptr, false, lane);
-    gemm_fwd<16, 0, 14, ACT_SOFTPLUS>(ws, OP(F3), OP(F4), OPB(F4), Y, E, X, e_l[3], nullptr, false, lane);
-    gemm_fwd<14, 4, 16, ACT_SOFTPLUS>(ws, OP(F4), OP(F5), OPB(F5), X, E, Y, e_l[4], nullptr, false, lane);
-    gemm_fwd<16, 0, 16, ACT_SOFTPLUS>(ws, OP(F5), OP(F6), OPB(F6), Y, E, X, e_l[5], nullptr, false, lane);
-    gemm_fwd<16, 0, 16, ACT_SOFTPLUS>(ws, OP(F6), OP(F7), OPB(F7), X, E, Y, e_l[6], nullptr, false, lane);
+    gemm_fwd<P, 0, 4, 16, ACT_SOFTPLUS>(ws, OP(F0), OP(F1), OPB(F1), X, E, Y, e_l[0], nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_SOFTPLUS>(ws, OP(F1), OP(F2), OPB(F2), Y, E, X, e_l[1], nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_SOFTPLUS>(ws, OP(F2), OP(F3), OPB(F3), X, E, Y, e_l[2], nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 14, ACT_SOFTPLUS>(ws, OP(F3), OP(F4), OPB(F4), Y, E, X, e_l[3], nullptr, false, lane);
+    gemm_fwd<P, 14, 4, 16, ACT_SOFTPLUS>(ws, OP(F4), OP(F5), OPB(F5), X, E, Y, e_l[4], nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_SOFTPLUS>(ws, OP(F5), OP(F6), OPB(F6), Y, E, X, e_l[5], nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_SOFTPLUS>(ws, OP(F6), OP(F7), OPB(F7), X, E, Y, e_l[6], nullptr, false, lane);
     {
       const char* n = want_feat ? OP(F8) : (NABLA ? OP(B7) : (has_next ? OP(F0) : nullptr));
       const int nb = want_feat ? OPB(F8) : (NABLA ? OPB(B7) : OPB(F0));
-      gemm_fwd<16, 0, 16, ACT_SOFTPLUS>(ws, OP(F7), n, nb, Y, E, X, e_l[7], nullptr, false, lane);
+      gemm_fwd<P, 16, 0, 16, ACT_SOFTPLUS>(ws, OP(F7), n, nb, Y, E, X, e_l[7], nullptr, false, lane);
     }
     // ---- last layer, row 0 = sdf (VALU dot product) ---------------------------------------------
     float part = 0.0f;
@@ -332,7 +470,7 @@ __global__ __launch_bounds__(kThreads) void sdf_kernel(SdfKArgs a) {
     if (want_feat) {
       const char* n = NABLA ? OP(B7) : (has_next ? OP(F0) : nullptr);
       const int nb = NABLA ? OPB(B7) : OPB(F0);
-      gemm_fwd<16, 0, 16, ACT_NONE>(ws, OP(F8), n, nb, X, E, Y, nullptr, a.feature + pc * 256, valid,
+      gemm_fwd<P, 16, 0, 16, ACT_NONE>(ws, OP(F8), n, nb, X, E, Y, nullptr, a.feature + pc * 256, valid,
                                     lane);
     }
     if constexpr (NABLA) {
@@ -342,8 +480,8 @@ __global__ __launch_bounds__(kThreads) void sdf_kernel(SdfKArgs a) {
       for (int b = 0; b < 16; ++b) {
         const float4 w = *(const float4*)(w8 + 16 * b + 4 * g);
         const float4 e = e_l[7][b * 64 + lane];
-        X[b] = make_float4(softplus_bwd(w.x, e.x), softplus_bwd(w.y, e.y), softplus_bwd(w.z, e.z),
-                           softplus_bwd(w.w, e.w));
+        X[b] = make_float4(softplus_bwd<P>(w.x, e.x), softplus_bwd<P>(w.y, e.y), softplus_bwd<P>(w.z, e.z),
+                           softplus_bwd<P>(w.w, e.w));
       }
       // gradients w.r.t. the positional encoding (skip layer + first layer) are parked in the
       // (already consumed) layer-7 slab and folded into the nabla after the GEMM chain
@@ -351,15 +489,15 @@ __global__ __launch_bounds__(kThreads) void sdf_kernel(SdfKArgs a) {
       auto emb_skip = [&](int eb, float4 gv) { park[eb * 64 + lane] = gv; };
       auto emb_first = [&](int eb, float4 gv) { park[(4 + eb) * 64 + lane] = gv; };
       auto noemb = [](int, float4) {};
-      gemm_bwd<16, 16, 0>(ws, OP(B7), OP(B6), OPB(B6), X, Y, e_l[6], lane, noemb);
-      gemm_bwd<16, 16, 0>(ws, OP(B6), OP(B5), OPB(B5), Y, X, e_l[5], lane, noemb);
-      gemm_bwd<16, 16, 0>(ws, OP(B5), OP(B4), OPB(B4), X, Y, e_l[4], lane, noemb);
+      gemm_bwd<P, 16, 16, 0>(ws, OP(B7), OP(B6), OPB(B6), X, Y, e_l[6], lane, noemb);
+      gemm_bwd<P, 16, 16, 0>(ws, OP(B6), OP(B5), OPB(B5), Y, X, e_l[5], lane, noemb);
+      gemm_bwd<P, 16, 16, 0>(ws, OP(B5), OP(B4), OPB(B4), X, Y, e_l[4], lane, noemb);
       // skip layer: rows 0..216 -> h3 (scaled by softplus'(z3)), rows 217..255 -> embedding
-      gemm_bwd<16, 14, 4>(ws, OP(B4), OP(B3), OPB(B3), Y, X, e_l[3], lane, emb_skip);
-      gemm_bwd<14, 16, 0>(ws, OP(B3), OP(B2), OPB(B2), X, Y, e_l[2], lane, noemb);
-      gemm_bwd<16, 16, 0>(ws, OP(B2), OP(B1), OPB(B1), Y, X, e_l[1], lane, noemb);
-      gemm_bwd<16, 16, 0>(ws, OP(B1), OP(B0), OPB(B0), X, Y, e_l[0], lane, noemb);
-      gemm_bwd<16, 0, 4>(ws, OP(B0), has_next ? OP(F0) : nullptr, OPB(F0), Y, X, nullptr, lane, emb_first);
+      gemm_bwd<P, 16, 14, 4>(ws, OP(B4), OP(B3), OPB(B3), Y, X, e_l[3], lane, emb_skip);
+      gemm_bwd<P, 14, 16, 0>(ws, OP(B3), OP(B2), OPB(B2), X, Y, e_l[2], lane, noemb);
+      gemm_bwd<P, 16, 16, 0>(ws, OP(B2), OP(B1), OPB(B1), Y, X, e_l[1], lane, noemb);
+      gemm_bwd<P, 16, 16, 0>(ws, OP(B1), OP(B0), OPB(B0), X, Y, e_l[0], lane, noemb);
+      gemm_bwd<P, 16, 0, 4>(ws, OP(B0), has_next ? OP(F0) : nullptr, OPB(F0), Y, X, nullptr, lane, emb_first);
       // chain rule through the positional encoding (autograd sums both uses of embed(x))
       float n0 = 0.f, n1 = 0.f, n2 = 0.f;
 #pragma unroll
@@ -412,7 +550,7 @@ __device__ __forceinline__ float rad_small_feature(int f, const float (&x)[3], c
   return 0.0f;
 }
 
-template <int KBS>
+template <int P, int KBS>
 __global__ __launch_bounds__(kThreads) void radiance_kernel(RadKArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kMaxChunkBytes];
   WStream ws{smem, 1};
@@ -453,10 +591,10 @@ __global__ __launch_bounds__(kThreads) void radiance_kernel(RadKArgs a) {
 #pragma unroll
     for (int b = 0; b < 16; ++b) X[b] = *(const float4*)(a.feature + pc * 256 + 16 * b + 4 * g);
 
-    gemm_fwd<16, KBS, 16, ACT_RELU>(ws, OP(0), OP(1), OPB(1), X, S, Y, nullptr, nullptr, false, lane);
-    gemm_fwd<16, 0, 16, ACT_RELU>(ws, OP(1), OP(2), OPB(2), Y, S, X, nullptr, nullptr, false, lane);
-    gemm_fwd<16, 0, 16, ACT_RELU>(ws, OP(2), OP(3), OPB(3), X, S, Y, nullptr, nullptr, false, lane);
-    gemm_fwd<16, 0, 16, ACT_RELU>(ws, OP(3), has_next ? OP(0) : nullptr, OPB(0), Y, S, X, nullptr,
+    gemm_fwd<P, 16, KBS, 16, ACT_RELU>(ws, OP(0), OP(1), OPB(1), X, S, Y, nullptr, nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_RELU>(ws, OP(1), OP(2), OPB(2), Y, S, X, nullptr, nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_RELU>(ws, OP(2), OP(3), OPB(3), X, S, Y, nullptr, nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_RELU>(ws, OP(3), has_next ? OP(0) : nullptr, OPB(0), Y, S, X, nullptr,
                                   nullptr, false, lane);
     // head: Linear(256 -> 3) + sigmoid  (VALU dot products)
     float r[3];
@@ -484,16 +622,50 @@ __global__ __launch_bounds__(kThreads) void radiance_kernel(RadKArgs a) {
 // =============================================================================================
 // weight packing (device): effective W [rows][ld] -> chunk layout of one GEMM op
 // =============================================================================================
-__global__ void pack_op_kernel(PackOp op, float* __restrict__ dst, int64_t n) {
+// source element (W * scale) of A-element (ob, b, fi) of an op, or 0 for padding
+__device__ __forceinline__ float pack_src(const PackOp& op, int ob, int i, int b, int fi) {
+  int row = -1, col = -1;
+  int ob_loc = ob;
+  for (int s = 0; s < 2; ++s) {
+    if (ob_loc < op.out[s].nblk) {
+      const int rl = 16 * ob_loc + i;
+      if (rl < op.out[s].nvalid) row = op.out[s].off + rl;
+      break;
+    }
+    ob_loc -= op.out[s].nblk;
+  }
+  int b_loc = b;
+  for (int s = 0; s < 2; ++s) {
+    if (b_loc < op.in[s].nblk) {
+      const int cl = 16 * b_loc + fi;
+      if (cl < op.in[s].nvalid) col = op.in[s].off + cl;
+      break;
+    }
+    b_loc -= op.in[s].nblk;
+  }
+  if (row < 0 || col < 0) return 0.0f;
+  return (op.transpose ? op.W[(int64_t)col * op.ld + row] : op.W[(int64_t)row * op.ld + col]) * op.scale;
+}
+
+// weight scale 2^(13 - e) for max |W| = f 2^e (f16x3), 1 for fp32
+__device__ __forceinline__ float wscale(const PackOp& op) {
+  if (op.prec != NR_PREC_F16X3) return 1.0f;
+  const float m = *op.wmax;
+  if (!(m > 0.0f)) return 1.0f;
+  return __builtin_ldexpf(1.0f, 13 - __builtin_amdgcn_frexp_expf(m));
+}
+
+// one thread per 32-bit word of the packed op
+__global__ void pack_op_kernel(PackOp op, uint32_t* __restrict__ dst, int64_t n) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   const int KB = op.in[0].nblk + op.in[1].nblk;
-  const int per_chunk = (2 * KB + 1) * 256;  // floats
+  const int per_chunk = (2 * KB + 1) * 256;  // words
   const int c = (int)(e / per_chunk);
   const int w = (int)(e - (int64_t)c * per_chunk);
-  float v = 0.0f;
-  if (w >= 2 * KB * 256) {  // bias slot: 2 blocks x 16 rows, then padding
+  if (w >= 2 * KB * 256) {  // bias slot: 2 blocks x 16 rows, [32] = 1 / weight scale
     const int idx = w - 2 * KB * 256;
+    float v = 0.0f;
     if (idx < 32 && op.bias) {
       int ob_loc = 2 * c + idx / 16;
       for (int s = 0; s < 2; ++s) {
@@ -504,43 +676,42 @@ __global__ void pack_op_kernel(PackOp op, float* __restrict__ dst, int64_t n) {
         }
         ob_loc -= op.out[s].nblk;
       }
+    } else if (idx == 32) {
+      v = 1.0f / wscale(op);
     }
-    dst[e] = v;
+    dst[e] = __float_as_uint(v);
     return;
   }
-  const int r = w & 3;
-  const int lane = (w >> 2) & 63;
-  const int t = w >> 8;
-  const int b = t % KB;
-  const int obl = t / KB;
-  const int ob = 2 * c + obl;
-  const int i = lane & 15, gg = lane >> 4;
-  int row = -1;
-  {
-    int ob_loc = ob;
-    for (int s = 0; s < 2; ++s) {
-      if (ob_loc < op.out[s].nblk) {
-        const int rl = 16 * ob_loc + i;
-        if (rl < op.out[s].nvalid) row = op.out[s].off + rl;
-        break;
-      }
-      ob_loc -= op.out[s].nblk;
+  if (op.prec == NR_PREC_FP32) {  // [obl][b][lane][r] floats
+    const int r = w & 3, lane = (w >> 2) & 63, t = w >> 8;
+    const int b = t % KB, obl = t / KB;
+    dst[e] = __float_as_uint(pack_src(op, 2 * c + obl, lane & 15, b, 4 * (lane >> 4) + r));
+  } else {  // [obl][s][hl][lane][8 halves]; word = halves (2q, 2q+1)
+    const int q = w & 3, lane = (w >> 2) & 63, hl = (w >> 8) & 1, t = w >> 9;
+    const int NS = KB / 2, s = t % NS, obl = t / NS;
+    const float sc = wscale(op);
+    uint32_t word = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int el = 2 * q + h;
+      const int b = 2 * s + (el >> 2), fi = 4 * (lane >> 4) + (el & 3);
+      const float v = pack_src(op, 2 * c + obl, lane & 15, b, fi) * sc;
+      const _Float16 hi = (_Float16)v;
+      const _Float16 lo = (_Float16)(v - (float)hi);
+      const _Float16 out = hl ? lo : hi;
+      word |= (uint32_t)__builtin_bit_cast(uint16_t, out) << (16 * h);
     }
+    dst[e] = word;
   }
-  int col = -1;
-  {
-    int b_loc = b;
-    for (int s = 0; s < 2; ++s) {
-      if (b_loc < op.in[s].nblk) {
-        const int cl = 16 * b_loc + 4 * gg + r;
-        if (cl < op.in[s].nvalid) col = op.in[s].off + cl;
-        break;
-      }
-      b_loc -= op.in[s].nblk;
-    }
-  }
-  if (row >= 0 && col >= 0) v = (op.transpose ? op.W[(int64_t)col * op.ld + row] : op.W[(int64_t)row * op.ld + col]) * op.scale;
-  dst[e] = v;
+}
+
+// max |W * scale| into *out (out zeroed beforehand; non-negative floats order like their bits)
+__global__ void maxabs_kernel(const float* __restrict__ W, int64_t n, float scale, unsigned* __restrict__ out) {
+  float m = 0.0f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(W[i] * scale));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
 }
 
 __global__ void pack_vec_kernel(const float* __restrict__ src, int off, int nvalid, int n, float* __restrict__ dst) {
@@ -555,8 +726,14 @@ __global__ void pack_vec_kernel(const float* __restrict__ src, int off, int nval
 int launch_pack_op(const PackOp& op, char* dst, hipStream_t stream) {
   const int KB = op.in[0].nblk + op.in[1].nblk;
   const int NBO = op.out[0].nblk + op.out[1].nblk;
+  if (op.prec == NR_PREC_F16X3) {
+    NR_REQUIRE(op.wmax, NR_ERR_ARG, "pack: f16x3 needs a max-|W| word");
+    NR_HIP_CHECK(hipMemsetAsync(op.wmax, 0, sizeof(float), stream));
+    hipLaunchKernelGGL(maxabs_kernel, dim3(64), dim3(256), 0, stream, op.W, op.wn, op.scale, (unsigned*)op.wmax);
+    NR_HIP_CHECK(hipGetLastError());
+  }
   const int64_t n = (int64_t)(NBO / 2) * (2 * KB + 1) * 256;
-  hipLaunchKernelGGL(pack_op_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, op, (float*)dst, n);
+  hipLaunchKernelGGL(pack_op_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, op, (uint32_t*)dst, n);
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;
 }
@@ -584,9 +761,11 @@ int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t
   if (nabla) {
     const size_t need = (size_t)grid * kScratchPerWG;
     NR_REQUIRE(ws && ws_bytes >= need, NR_ERR_WORKSPACE, "sdf nabla workspace too small");
-    hipLaunchKernelGGL(sdf_kernel<true>, dim3(grid), dim3(kThreads), 0, stream, a);
+    if (L.prec == NR_PREC_F16X3) hipLaunchKernelGGL((sdf_kernel<NR_PREC_F16X3, true>), dim3(grid), dim3(kThreads), 0, stream, a);
+    else hipLaunchKernelGGL((sdf_kernel<NR_PREC_FP32, true>), dim3(grid), dim3(kThreads), 0, stream, a);
   } else {
-    hipLaunchKernelGGL(sdf_kernel<false>, dim3(grid), dim3(kThreads), 0, stream, a);
+    if (L.prec == NR_PREC_F16X3) hipLaunchKernelGGL((sdf_kernel<NR_PREC_F16X3, false>), dim3(grid), dim3(kThreads), 0, stream, a);
+    else hipLaunchKernelGGL((sdf_kernel<NR_PREC_FP32, false>), dim3(grid), dim3(kThreads), 0, stream, a);
   }
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;
@@ -599,9 +778,16 @@ int launch_radiance(const RadLayout& L, const void* packed, const float* x, cons
   const int grid = grid_for(P);
   RadKArgs a{(const char*)packed, L, x, vdir, vdiv, vmod, normals, feature, P, rgb, nfreq_view};
   ProfScope prof("radiance", (double)P, stream);
+  const bool h3 = L.prec == NR_PREC_F16X3;
   switch (L.kbs) {
-    case 2: hipLaunchKernelGGL(radiance_kernel<2>, dim3(grid), dim3(kThreads), 0, stream, a); break;
-    case 4: hipLaunchKernelGGL(radiance_kernel<4>, dim3(grid), dim3(kThreads), 0, stream, a); break;
+    case 2:
+      if (h3) hipLaunchKernelGGL((radiance_kernel<NR_PREC_F16X3, 2>), dim3(grid), dim3(kThreads), 0, stream, a);
+      else hipLaunchKernelGGL((radiance_kernel<NR_PREC_FP32, 2>), dim3(grid), dim3(kThreads), 0, stream, a);
+      break;
+    case 4:
+      if (h3) hipLaunchKernelGGL((radiance_kernel<NR_PREC_F16X3, 4>), dim3(grid), dim3(kThreads), 0, stream, a);
+      else hipLaunchKernelGGL((radiance_kernel<NR_PREC_FP32, 4>), dim3(grid), dim3(kThreads), 0, stream, a);
+      break;
     default: set_error("radiance: unsupported small-input block count"); return NR_ERR_UNSUPPORTED;
   }
   NR_HIP_CHECK(hipGetLastError());

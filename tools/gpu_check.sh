@@ -2,7 +2,7 @@
 # GPU-box check: parity tests, then (unless a test run crashed) a short bench.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-timeout -k 10 ${T_TEST:-900} python -m pytest tests -m gpu -x -q -s ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 ${T_TEST:-900} python -m pytest tests -m gpu -q -s ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping: pytest crashed/timed out"; exit $rc; fi
