@@ -23,6 +23,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X dense fp32 matrix (MI355X_MICROARCH.md)
+F16_MFMA_PEAK_TFLOPS = 2500.0     # MI355X dense fp16/bf16 matrix (MI355X_MICROARCH.md; sparsity excluded)
+# f16x3 spends 3 fp16 MFMA products (hi*hi + hi*lo + lo*hi) per algorithmic fp32 MAC
+F16X3_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / 3
 MAC_SDF_FWD = 524_544             # SURVEY §8(a) A5 (incl. the 257-row last layer)
 MAC_SDF_BWD = 459_008             # SURVEY §8(a) A6 (reverse pass for the nablas)
 MAC_RAD = 271_360                 # SURVEY §8(a) A7, NeuS radiance input 289
@@ -35,7 +38,7 @@ def parse():
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--rays', type=int, default=4096)
-    ap.add_argument('--precision', default=os.environ.get('NR_PRECISION', 'fp32'))
+    ap.add_argument('--precision', default=os.environ.get('NR_PRECISION', 'f16x3'), choices=['f16x3', 'fp32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-rays', type=int, default=1024)
     return ap.parse_args()
@@ -117,7 +120,7 @@ def roofline(kstats, precision):
     dom, (n, ms, fl) = max(merged.items(), key=lambda kv: kv[1][1])
     per_launch_ms = ms / n
     achieved = fl / n / (per_launch_ms * 1e-3) / 1e12
-    peak = FP32_MFMA_PEAK_TFLOPS
+    peak = FP32_MFMA_PEAK_TFLOPS if precision == 'fp32' else F16X3_PEAK_TFLOPS
     return {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': peak, 'unit': 'TFLOP/s',
             'frac': round(achieved / peak, 4), 'traffic': None, 'kernel': dom,
             'avg_launch_ms': round(per_launch_ms, 4), 'launches': n,

@@ -68,6 +68,20 @@ class WNLinear(nn.Module):
         return torch._weight_norm(self.weight_v, self.weight_g, 0)
 
 
+PRECISIONS = ('f16x3', 'fp32')
+
+
+def default_precision():
+    """GEMM arithmetic of the MLP kernels: 'f16x3' (default; split-fp16 x3 on fp16 MFMA, per-point
+    power-of-two scaling -- measured at fp32-level error on the parity suite) or 'fp32' (fp32 MFMA).
+    Override with NR_PRECISION or the modules' `precision=` argument."""
+    import os
+    p = os.environ.get('NR_PRECISION', 'f16x3')
+    if p not in PRECISIONS:
+        raise ValueError(f'NR_PRECISION must be one of {PRECISIONS}')
+    return p
+
+
 def _wn_params(layers):
     Ws, bs = [], []
     for layer in layers:
@@ -104,7 +118,7 @@ def _no_training(*tensors_or_modules):
 # ---------------------------------------------------------------------------------------------
 class ImplicitSurface(nn.Module):
     def __init__(self, W=256, D=8, skips=[4], W_geo_feat=256, input_ch=3, radius_init=1.0, obj_bounding_size=2.0,
-                 geometric_init=True, embed_multires=6, weight_norm=True, use_siren=False, precision='fp32'):
+                 geometric_init=True, embed_multires=6, weight_norm=True, use_siren=False, precision=None):
         super().__init__()
         if use_siren or not weight_norm:
             raise NotImplementedError('neurecon_amd: SIREN / non-weight-normed surface nets are out of scope')
@@ -116,7 +130,7 @@ class ImplicitSurface(nn.Module):
         self.embed_multires = embed_multires
         self.embed_fn, in_ch = get_embedder(embed_multires)
         self.input_ch = in_ch
-        self.precision = precision
+        self.precision = default_precision() if precision is None else precision
         layers = []
         for l in range(D + 1):
             if l == D:
@@ -218,7 +232,7 @@ class ImplicitSurface(nn.Module):
 # ---------------------------------------------------------------------------------------------
 class RadianceNet(nn.Module):
     def __init__(self, D=4, W=256, skips=[], W_geo_feat=256, embed_multires=6, embed_multires_view=4,
-                 use_view_dirs=True, weight_norm=True, use_siren=False, precision='fp32'):
+                 use_view_dirs=True, weight_norm=True, use_siren=False, precision=None):
         super().__init__()
         if use_siren or not weight_norm or skips or not use_view_dirs:
             raise NotImplementedError('neurecon_amd: RadianceNet needs weight_norm, view dirs, no skips, no SIREN')
@@ -227,7 +241,7 @@ class RadianceNet(nn.Module):
         self.embed_fn, ch_pts = get_embedder(embed_multires)
         self.embed_fn_view, ch_view = get_embedder(embed_multires_view)
         in0 = ch_pts + ch_view + 3 + W_geo_feat
-        self.precision = precision
+        self.precision = default_precision() if precision is None else precision
         self.layers = nn.ModuleList([WNLinear(in0 if l == 0 else W, 3 if l == D else W) for l in range(D + 1)])
         self._nr_cache = None
 
