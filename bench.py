@@ -30,6 +30,11 @@ MAC_SDF_FWD = 524_544             # SURVEY §8(a) A5 (incl. the 257-row last lay
 MAC_SDF_BWD = 459_008             # SURVEY §8(a) A6 (reverse pass for the nablas)
 MAC_RAD = 271_360                 # SURVEY §8(a) A7, NeuS radiance input 289
 RAY_FLOP = 704.8e6                # 128 no-grad SDF + 255 SDF-with-nabla + 127 radiance
+# HBM-side bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc passes of this bench,
+# tools/gpu_pmc.sh); counters cannot be read live, so the latest committed summary is reported.
+PMC_SUMMARY = {'f16x3': 'profiles/r01/f16x3_pmc_summary.json'}
+PMC_KERNEL = {('sdf_nabla', 'f16x3'): 'void nr::sdf_kernel<1, true>(nr::SdfKArgs)',
+              ('sdf_nabla', 'fp32'): 'void nr::sdf_kernel<0, true>(nr::SdfKArgs)'}
 
 
 def parse():
@@ -105,6 +110,16 @@ KERNEL_MAC = {'sdf_fwd': MAC_SDF_FWD, 'sdf_feat': MAC_SDF_FWD, 'sdf_nabla': MAC_
               'sdf_nabla_feat': MAC_SDF_FWD + MAC_SDF_BWD, 'radiance': MAC_RAD}
 
 
+def pmc_traffic(kernel, precision):
+    path = os.path.join(ROOT, PMC_SUMMARY.get(precision, '-'))
+    name = PMC_KERNEL.get((kernel, precision))
+    if not name or not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        rec = json.load(f).get(name)
+    return (rec['hbm_bytes_per_launch'], PMC_SUMMARY[precision]) if rec else (None, None)
+
+
 def roofline(kstats, precision):
     """Dominant kernel (largest device time): algorithmic FLOPs per launch / mean launch duration."""
     # the two sdf_kernel<nabla> launches (samples, mid-points) are one kernel
@@ -121,8 +136,10 @@ def roofline(kstats, precision):
     per_launch_ms = ms / n
     achieved = fl / n / (per_launch_ms * 1e-3) / 1e12
     peak = FP32_MFMA_PEAK_TFLOPS if precision == 'fp32' else F16X3_PEAK_TFLOPS
+    traffic, src = pmc_traffic(dom, precision)
     return {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': peak, 'unit': 'TFLOP/s',
-            'frac': round(achieved / peak, 4), 'traffic': None, 'kernel': dom,
+            'frac': round(achieved / peak, 4), 'traffic': traffic, 'traffic_unit': 'bytes/launch',
+            'traffic_source': src, 'kernel': dom,
             'avg_launch_ms': round(per_launch_ms, 4), 'launches': n,
             'flop_per_launch': fl / n, 'share_of_device_time': round(ms / total_ms, 4)}
 
