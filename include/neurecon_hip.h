@@ -9,6 +9,7 @@
  *   nr_radiance_forward     RadianceNet.forward                              models/base.py:372-391
  *   nr_nerf_forward         NeRF.forward (NeRF++ background)                models/base.py:426-453
  *   nr_neus_render          neus.volume_render (one ray chunk, render mode) models/frameworks/neus.py:118-397
+ *   nr_volsdf_render        volsdf.volume_render (render mode)             models/frameworks/volsdf.py:16-551
  *   nr_sample_pdf           rend_util.sample_pdf                             utils/rend_util.py:255-292
  *   nr_get_rays             rend_util.get_rays (+ lift)                      utils/rend_util.py:95-164
  *
@@ -132,6 +133,55 @@ typedef struct {
 
 size_t nr_neus_workspace_bytes(const NrNeusArgs* a);
 int nr_neus_render(const NrNeusArgs* a, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * VolSDF rendering (models/frameworks/volsdf.py:377-551, render mode: perturb=False, builtin
+ * background sphere).  Error-bounded sampling (volsdf.py:77-272) over 4*N_samples initial depths,
+ * up to max_upsample_steps rounds of 4*N_samples new depths with max_bisection_steps bisection
+ * steps on beta+, then N_importance final depths merged with N_samples uniform ones.
+ * Outputs are ray-major; detailed outputs (NULL to skip) have S = N_samples + N_importance
+ * samples (S-1 for alpha / p_i / weights).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  const float* rays_o; /* [n_rays, 3] */
+  const float* rays_d; /* [n_rays, 3], normalised inside (volsdf.py:388) */
+  int64_t n_rays;
+  const NrSdfDesc* sdf;
+  const void* sdf_packed;
+  const NrRadDesc* rad;
+  const void* rad_packed;
+  float alpha_net, beta_net; /* VolSDF.forward_ab() (volsdf.py:306-308) */
+  float beta_plus_init;      /* sqrt(far^2 / (4 (4 N_samples - 1) log(1 + eps))) (volsdf.py:128) */
+  float eps;                 /* epsilon, compared in fp32 like the reference */
+  float near, far;           /* constant near / far (volsdf.py:408-413) */
+  float obj_bounding_radius; /* background sphere radius (volsdf.py:310-325) */
+  int use_sphere_bg;
+  int N_samples, N_importance, max_upsample_steps, max_bisection_steps;
+  int calc_normal, white_bkgd;
+  const float* t_coarse; /* torch.linspace(0, 1, N_samples)     (CPU values) */
+  const float* t_init;   /* torch.linspace(0, 1, 4 N_samples)   */
+  const float* u_up;     /* torch.linspace(0, 1, 4 N_samples + 2) */
+  const float* u_fine;   /* torch.linspace(0, 1, N_importance)  */
+  float* rgb;            /* [n_rays, 3] */
+  float* depth;          /* [n_rays]    */
+  float* acc;            /* [n_rays]    */
+  float* normals;        /* [n_rays, 3] (calc_normal) */
+  float* d_vals;         /* [n_rays, S]   */
+  float* sdf_out;        /* [n_rays, S]   implicit_surface */
+  float* nablas_out;     /* [n_rays, S, 3] */
+  float* radiance_out;   /* [n_rays, S, 3] */
+  float* alpha_out;      /* [n_rays, S-1] */
+  float* p_out;          /* [n_rays, S-1] p_i */
+  float* weights_out;    /* [n_rays, S-1] visibility_weights */
+  float* sigma_out;      /* [n_rays, S]   */
+  float* beta_map;       /* [n_rays]      */
+  float* iter_usage;     /* [n_rays]      */
+  void* workspace;
+  size_t workspace_bytes;
+} NrVolsdfArgs;
+
+size_t nr_volsdf_workspace_bytes(const NrVolsdfArgs* a);
+int nr_volsdf_render(const NrVolsdfArgs* a, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Inverse-CDF sampling (rend_util.sample_pdf, det=True or caller-provided u):

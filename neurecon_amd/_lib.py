@@ -48,6 +48,24 @@ class NrNeusArgs(ctypes.Structure):
     ]
 
 
+class NrVolsdfArgs(ctypes.Structure):
+    _fields_ = [
+        ('rays_o', _c_p), ('rays_d', _c_p), ('n_rays', _c_i64),
+        ('sdf', ctypes.POINTER(NrSdfDesc)), ('sdf_packed', _c_p),
+        ('rad', ctypes.POINTER(NrRadDesc)), ('rad_packed', _c_p),
+        ('alpha_net', _c_f), ('beta_net', _c_f), ('beta_plus_init', _c_f), ('eps', _c_f),
+        ('near', _c_f), ('far', _c_f), ('obj_bounding_radius', _c_f), ('use_sphere_bg', _c_i),
+        ('N_samples', _c_i), ('N_importance', _c_i), ('max_upsample_steps', _c_i), ('max_bisection_steps', _c_i),
+        ('calc_normal', _c_i), ('white_bkgd', _c_i),
+        ('t_coarse', _c_p), ('t_init', _c_p), ('u_up', _c_p), ('u_fine', _c_p),
+        ('rgb', _c_p), ('depth', _c_p), ('acc', _c_p), ('normals', _c_p),
+        ('d_vals', _c_p), ('sdf_out', _c_p), ('nablas_out', _c_p), ('radiance_out', _c_p),
+        ('alpha_out', _c_p), ('p_out', _c_p), ('weights_out', _c_p), ('sigma_out', _c_p),
+        ('beta_map', _c_p), ('iter_usage', _c_p),
+        ('workspace', _c_p), ('workspace_bytes', _c_sz),
+    ]
+
+
 class NrKernelStat(ctypes.Structure):
     _fields_ = [('name', ctypes.c_char * 32), ('launches', _c_i64), ('ms', ctypes.c_double),
                 ('units', ctypes.c_double)]
@@ -66,6 +84,8 @@ _SIGS = {
                                    _c_p]),
     'nr_neus_workspace_bytes': (_c_sz, [ctypes.POINTER(NrNeusArgs)]),
     'nr_neus_render': (_c_i, [ctypes.POINTER(NrNeusArgs), _c_p]),
+    'nr_volsdf_workspace_bytes': (_c_sz, [ctypes.POINTER(NrVolsdfArgs)]),
+    'nr_volsdf_render': (_c_i, [ctypes.POINTER(NrVolsdfArgs), _c_p]),
     'nr_sample_pdf': (_c_i, [_c_p, _c_p, _c_i64, _c_i, _c_p, _c_i, _c_p, _c_p]),
     'nr_get_rays': (_c_i, [_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p]),
     'nr_profile_enable': (_c_i, [_c_i]),

@@ -7,6 +7,7 @@
 #include "nr_common.h"
 #include "nr_mlp.h"
 #include "nr_neus.h"
+#include "nr_volsdf.h"
 
 namespace nr {
 
@@ -96,7 +97,7 @@ static PackSeg none() { return PackSeg{0, 0, 0}; }
 
 static size_t scratch_bytes() {
   int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   return (size_t)cus * kScratchPerWG;
 }
 
@@ -174,6 +175,116 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
 static int64_t neus_chunk_rays(const NrNeusArgs* a) {
   const int64_t cap = 16384;
   return a->n_rays < cap ? (a->n_rays > 0 ? a->n_rays : 1) : cap;
+}
+
+// ---------------------------------------------------------------------------------------------
+// VolSDF chunk orchestration (volsdf.py:394-551): prologue -> SDF(4 N_samples) -> first check ->
+// [SDF(active x N_up, device count) -> round it] x max_iter -> points -> SDF+nablas+feature ->
+// radiance -> composite.  No host synchronisation inside a chunk.
+// ---------------------------------------------------------------------------------------------
+static int volsdf_chunk(const NrVolsdfArgs& a, const VolPlan& pl, int64_t ray0, int R, hipStream_t st) {
+  char* ws = (char*)a.workspace;
+  auto F = [&](size_t o) { return (float*)(ws + o); };
+  VolChunk c{};
+  c.R = R;
+  c.N0 = 4 * a.N_samples;
+  c.N_up = 4 * a.N_samples;
+  c.cap = c.N0 + a.max_upsample_steps * c.N_up;
+  c.N_samples = a.N_samples;
+  c.N_imp = a.N_importance;
+  c.S = a.N_samples + a.N_importance;
+  c.max_iter = a.max_upsample_steps;
+  c.max_bisect = a.max_bisection_steps;
+  c.alpha_net = a.alpha_net;
+  c.beta_net = a.beta_net;
+  c.beta_plus0 = a.beta_plus_init;
+  c.eps = a.eps;
+  c.near = a.near;
+  c.far = a.far;
+  c.r_bg = a.obj_bounding_radius;
+  c.use_bg = a.use_sphere_bg;
+  c.ro = F(pl.o_ro); c.rd = F(pl.o_rd);
+  c.Ld[0] = F(pl.o_Ld0); c.Ld[1] = F(pl.o_Ld1); c.Ls[0] = F(pl.o_Ls0); c.Ls[1] = F(pl.o_Ls1);
+  c.dnew[0] = F(pl.o_dn0); c.dnew[1] = F(pl.o_dn1);
+  c.pts = F(pl.o_pts); c.sraw = F(pl.o_sraw);
+  c.act[0] = (int*)(ws + pl.o_act0); c.act[1] = (int*)(ws + pl.o_act1); c.cnt = (int*)(ws + pl.o_cnt);
+  c.beta = F(pl.o_beta); c.fine = F(pl.o_fine); c.usage = F(pl.o_usage); c.bmap = F(pl.o_bmap);
+  c.d_all = F(pl.o_dall); c.pts_f = F(pl.o_ptsf); c.sdf_f = F(pl.o_sdff); c.nab_f = F(pl.o_nabf);
+  c.feat_f = F(pl.o_featf); c.rad_f = F(pl.o_radf);
+  c.t_coarse = a.t_coarse; c.t_init = a.t_init; c.u_up = a.u_up; c.u_fine = a.u_fine;
+  void* mlp_ws = ws + pl.o_mlp;
+  const size_t mlp_bytes = a.workspace_bytes - pl.o_mlp;
+  const SdfLayout SL = sdf_layout(*a.sdf);
+  const RadLayout RL = rad_layout(*a.rad);
+  const unsigned lds = (unsigned)pl.lds_bytes;
+  const dim3 blk(64), grd((unsigned)R);
+  int rc;
+  NR_HIP_CHECK(hipMemsetAsync(c.cnt, 0, sizeof(int) * (a.max_upsample_steps + 1), st));
+  {
+    ProfScope prof("volsdf_prologue", (double)R, st);
+    hipLaunchKernelGGL(volsdf_prologue, grd, blk, 0, st, c, a.rays_o + ray0 * 3, a.rays_d + ray0 * 3);
+  }
+  NR_HIP_CHECK(hipGetLastError());
+  if ((rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)c.N0 * R, c.sraw, nullptr, nullptr, a.sdf->multires,
+                       nullptr, 0, st)))
+    return rc;
+  {
+    ProfScope prof("volsdf_first", (double)R, st);
+    hipLaunchKernelGGL(volsdf_first, grd, blk, lds, st, c);
+  }
+  NR_HIP_CHECK(hipGetLastError());
+  for (int it = 1; it <= a.max_upsample_steps; ++it) {
+    if ((rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)c.N_up * R, c.sraw, nullptr, nullptr, a.sdf->multires,
+                         nullptr, 0, st, c.cnt + (it - 1), c.N_up)))
+      return rc;
+    {
+      ProfScope prof("volsdf_iter", (double)R, st);
+      hipLaunchKernelGGL(volsdf_iter, grd, blk, lds, st, c, it);
+    }
+    NR_HIP_CHECK(hipGetLastError());
+  }
+  {
+    ProfScope prof("volsdf_points", (double)R, st);
+    hipLaunchKernelGGL(volsdf_points, grd, blk, lds, st, c);
+  }
+  NR_HIP_CHECK(hipGetLastError());
+  const int64_t P = (int64_t)c.S * R;
+  if ((rc = launch_sdf(SL, a.sdf_packed, c.pts_f, P, c.sdf_f, c.nab_f, c.feat_f, a.sdf->multires, mlp_ws, mlp_bytes,
+                       st)))
+    return rc;
+  if ((rc = launch_radiance(RL, a.rad_packed, c.pts_f, c.rd, c.S, INT64_MAX, c.nab_f, c.feat_f, P, c.rad_f,
+                            a.rad->multires_view, st)))
+    return rc;
+  VolOut o{ray0, a.rgb, a.depth, a.acc, a.normals, a.d_vals, a.sdf_out, a.nablas_out, a.radiance_out,
+           a.alpha_out, a.p_out, a.weights_out, a.sigma_out, a.beta_map, a.iter_usage};
+  {
+    ProfScope prof("volsdf_composite", (double)R, st);
+    hipLaunchKernelGGL(volsdf_composite, grd, blk, lds, st, c, o, a.calc_normal, a.white_bkgd);
+  }
+  NR_HIP_CHECK(hipGetLastError());
+  return NR_OK;
+}
+
+static int64_t volsdf_chunk_rays(const NrVolsdfArgs* a) {
+  const int64_t cap = 16384;
+  return a->n_rays < cap ? (a->n_rays > 0 ? a->n_rays : 1) : cap;
+}
+
+static int check_volsdf(const NrVolsdfArgs* a) {
+  NR_REQUIRE(a, NR_ERR_ARG, "nr_volsdf_render: null args");
+  int rc = check_sdf_desc(a->sdf);
+  if (rc) return rc;
+  if ((rc = check_rad_desc(a->rad))) return rc;
+  NR_REQUIRE(a->rays_o && a->rays_d && a->sdf_packed && a->rad_packed && a->t_coarse && a->t_init && a->u_up &&
+                 a->u_fine && a->rgb && a->depth && a->acc,
+             NR_ERR_ARG, "nr_volsdf_render: null argument");
+  NR_REQUIRE(!a->calc_normal || a->normals, NR_ERR_ARG, "nr_volsdf_render: calc_normal needs normals output");
+  NR_REQUIRE(a->N_samples >= 1 && a->N_importance >= 1 && a->max_upsample_steps >= 0 && a->max_bisection_steps >= 0,
+             NR_ERR_ARG, "nr_volsdf_render: bad sample counts");
+  NR_REQUIRE(4 * a->N_samples <= 1024 && a->N_importance <= 1024, NR_ERR_UNSUPPORTED,
+             "nr_volsdf_render: 4*N_samples and N_importance must be <= 1024");
+  NR_REQUIRE(a->beta_net > 0.f && a->beta_plus_init > 0.f, NR_ERR_ARG, "nr_volsdf_render: beta must be positive");
+  return NR_OK;
 }
 
 }  // namespace nr
@@ -305,6 +416,31 @@ int nr_neus_render(const NrNeusArgs* a, void* stream) {
   for (int64_t r0 = 0; r0 < a->n_rays; r0 += Rc) {
     const int R = (int)((a->n_rays - r0) < Rc ? (a->n_rays - r0) : Rc);
     if ((rc = neus_chunk(*a, pl, r0, R, (hipStream_t)stream))) return rc;
+  }
+  return NR_OK;
+}
+
+size_t nr_volsdf_workspace_bytes(const NrVolsdfArgs* a) {
+  if (!a || check_volsdf(a)) return 0;
+  return volsdf_plan(*a, volsdf_chunk_rays(a)).total;
+}
+
+int nr_volsdf_render(const NrVolsdfArgs* a, void* stream) {
+  int rc = check_volsdf(a);
+  if (rc) return rc;
+  if (a->n_rays <= 0) return NR_OK;
+  const int64_t Rc = volsdf_chunk_rays(a);
+  const VolPlan pl = volsdf_plan(*a, Rc);
+  NR_REQUIRE(a->workspace && a->workspace_bytes >= pl.total, NR_ERR_WORKSPACE,
+             "nr_volsdf_render: workspace too small");
+  int dev = 0, lds_max = 65536;
+  NR_HIP_CHECK(hipGetDevice(&dev));
+  NR_HIP_CHECK(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
+  NR_REQUIRE(pl.lds_bytes <= (size_t)lds_max, NR_ERR_UNSUPPORTED,
+             "nr_volsdf_render: per-ray sample list does not fit in LDS (reduce N_samples or max_upsample_steps)");
+  for (int64_t r0 = 0; r0 < a->n_rays; r0 += Rc) {
+    const int R = (int)((a->n_rays - r0) < Rc ? (a->n_rays - r0) : Rc);
+    if ((rc = volsdf_chunk(*a, pl, r0, R, (hipStream_t)stream))) return rc;
   }
   return NR_OK;
 }

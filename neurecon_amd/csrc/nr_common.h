@@ -127,6 +127,14 @@ __device__ float aten_row_sum(int n, Load ld) {
   return fa;
 }
 
+// inverse-CDF sample for one u (rend_util.py:284-290)
+__device__ __forceinline__ float invert_one(float u, float c0, float c1, float b0, float b1) {
+  float denom = fsub(c1, c0);
+  if (denom < 1e-5f) denom = 1.0f;
+  const float t = fdiv(fsub(u, c0), denom);
+  return fadd(b0, fmul(t, fsub(b1, b0)));
+}
+
 // torch.sigmoid(x) = 1 / (1 + exp(-x))
 __device__ __forceinline__ float sigmoidf_ref(float x) { return fdiv(1.0f, fadd(1.0f, expf(-x))); }
 

@@ -57,7 +57,8 @@ struct PackOp {
 int launch_pack_op(const PackOp& op, char* dst, hipStream_t stream);
 int launch_pack_vec(const float* src, int off, int nvalid, int n, char* dst, hipStream_t stream);
 int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,
-               float* feature, int nfreq, void* ws, size_t ws_bytes, hipStream_t stream);
+               float* feature, int nfreq, void* ws, size_t ws_bytes, hipStream_t stream,
+               const int* P_dev = nullptr, int P_mult = 0);  // P_dev: device count, P_eff = min(P, *P_dev * P_mult)
 int launch_radiance(const RadLayout& L, const void* packed, const float* x, const float* vdir, int64_t vdiv,
                     int64_t vmod, const float* normals, const float* feature, int64_t P, float* rgb, int nfreq_view,
                     hipStream_t stream);

@@ -401,6 +401,8 @@ struct SdfKArgs {
   float* feature;
   float4* scratch;  // [grid*8 waves][8 layers][16 blocks][64 lanes] float4
   int nfreq;
+  const int* P_dev;  // optional device-side point count (x P_mult), bounded by P
+  int P_mult;
 };
 
 template <int P, bool NABLA>
@@ -422,11 +424,12 @@ __global__ __launch_bounds__(kThreads) void sdf_kernel(SdfKArgs a) {
   ws.issue(OP(F0), OPB(F0));
   ws.flip();
 
-  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < a.P; base += (int64_t)gridDim.x * kPointsPerWG) {
-    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < a.P;
+  const int64_t Pn = a.P_dev ? min(a.P, (int64_t)(*a.P_dev) * a.P_mult) : a.P;
+  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < Pn; base += (int64_t)gridDim.x * kPointsPerWG) {
+    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < Pn;
     const int64_t p = base + wave * kTile + j;
-    const bool valid = p < a.P;
-    const int64_t pc = valid ? p : a.P - 1;
+    const bool valid = p < Pn;
+    const int64_t pc = valid ? p : Pn - 1;
     const float x0 = a.pts[pc * 3 + 0], x1 = a.pts[pc * 3 + 1], x2 = a.pts[pc * 3 + 2];
 
     float4 E[4];
@@ -746,16 +749,17 @@ int launch_pack_vec(const float* src, int off, int nvalid, int n, char* dst, hip
 
 static int grid_for(int64_t P) {
   int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t need = (P + kPointsPerWG - 1) / kPointsPerWG;
   return (int)(need < cus ? (need > 0 ? need : 1) : cus);
 }
 
 int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,
-               float* feature, int nfreq, void* ws, size_t ws_bytes, hipStream_t stream) {
+               float* feature, int nfreq, void* ws, size_t ws_bytes, hipStream_t stream, const int* P_dev,
+               int P_mult) {
   if (P <= 0) return NR_OK;
   const int grid = grid_for(P);
-  SdfKArgs a{(const char*)packed, L, pts, P, sdf, nabla, feature, (float4*)ws, nfreq};
+  SdfKArgs a{(const char*)packed, L, pts, P, sdf, nabla, feature, (float4*)ws, nfreq, P_dev, P_mult};
   ProfScope prof(nabla ? (feature ? "sdf_nabla_feat" : "sdf_nabla") : (feature ? "sdf_feat" : "sdf_fwd"), (double)P,
                  stream);
   if (nabla) {

@@ -84,14 +84,6 @@ __device__ void merge_new(const NeusChunk& c, int r, int L) {
   }
 }
 
-// inverse-CDF sample for one u (rend_util.py:284-290)
-__device__ __forceinline__ float invert_one(float u, float c0, float c1, float b0, float b1) {
-  float denom = fsub(c1, c0);
-  if (denom < 1e-5f) denom = 1.0f;
-  const float t = fdiv(fsub(u, c0), denom);
-  return fadd(b0, fmul(t, fsub(b1, b0)));
-}
-
 // sample_pdf(bins=dv[0..L), weights=wtmp[0..L-1) (already +1e-5), N=n, u) -> out[k*R + r]
 // total = sum of the (+1e-5) weights.  rend_util.py:255-292.
 __device__ void sample_pdf_ray(const float* __restrict__ bins, const float* __restrict__ w, int64_t stride, int L,

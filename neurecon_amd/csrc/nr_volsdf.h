@@ -1,0 +1,60 @@
+// neurecon_amd — VolSDF render path internals (models/frameworks/volsdf.py, render mode).
+#pragma once
+#include "nr_common.h"
+
+namespace nr {
+
+// Device views of one ray chunk.  Per-ray sample lists are ray-major ([ray][cap]) and are
+// processed one wave (= one 64-thread workgroup) per ray; the MLP kernels see flat point lists.
+struct VolChunk {
+  int R;          // rays in this chunk
+  int N0;         // initial samples of the error-bounded sampler (4 * N_samples)
+  int N_up;       // samples added per round (4 * N_samples)
+  int cap;        // list capacity = N0 + max_iter * N_up
+  int N_samples;  // coarse samples (final pass)
+  int N_imp;      // fine samples (final pass)
+  int S;          // N_samples + N_imp
+  int max_iter, max_bisect;
+  float alpha_net, beta_net, beta_plus0, eps;
+  float near, far, r_bg;
+  int use_bg;
+  float* ro; float* rd;            // [R][3] (rd normalised)
+  float* Ld[2]; float* Ls[2];      // ping-pong sample lists [R][cap]
+  float* dnew[2];                  // ping-pong new samples [R][N_up] (by active slot)
+  float* pts;                      // MLP input, flat
+  float* sraw;                     // MLP output, flat
+  int* act[2];                     // ping-pong active ray lists
+  int* cnt;                        // [max_iter + 1] active counts (zeroed per chunk)
+  float* beta;                     // [R] current beta+
+  float* fine;                     // [R][N_imp] final fine depths
+  float* usage;                    // [R] iter_usage
+  float* bmap;                     // [R] beta_map
+  // final pass (ray-major [R][S])
+  float* d_all; float* pts_f; float* sdf_f; float* nab_f; float* feat_f; float* rad_f;
+  const float* t_coarse; const float* t_init; const float* u_up; const float* u_fine;
+};
+
+struct VolOut {
+  int64_t ray0;
+  float* rgb; float* depth; float* acc; float* normals;
+  float* d_vals; float* sdf; float* nablas; float* radiance; float* alpha; float* p_i; float* weights;
+  float* sigma; float* beta_map; float* iter_usage;
+};
+
+struct VolPlan {
+  int64_t Rc;
+  size_t o_ro, o_rd, o_Ld0, o_Ld1, o_Ls0, o_Ls1, o_dn0, o_dn1, o_pts, o_sraw, o_act0, o_act1, o_cnt;
+  size_t o_beta, o_fine, o_usage, o_bmap, o_dall, o_ptsf, o_sdff, o_nabf, o_featf, o_radf, o_mlp;
+  size_t total;
+  size_t lds_bytes;  // dynamic LDS of the per-ray kernels
+};
+
+VolPlan volsdf_plan(const NrVolsdfArgs& a, int64_t Rc);
+
+__global__ void volsdf_prologue(VolChunk c, const float* rays_o, const float* rays_d);
+__global__ void volsdf_first(VolChunk c);
+__global__ void volsdf_iter(VolChunk c, int it);
+__global__ void volsdf_points(VolChunk c);
+__global__ void volsdf_composite(VolChunk c, VolOut o, int calc_normal, int white_bkgd);
+
+}  // namespace nr

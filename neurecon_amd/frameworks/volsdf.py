@@ -1,0 +1,252 @@
+"""VolSDF framework: same API as the reference's models/frameworks/volsdf.py, render path on HIP.
+
+`volume_render(rays_o, rays_d, model, **kw) -> (rgb, depth, extras)` keeps the reference's
+signature, argument meaning, output shapes and extras keys (volsdf.py:377-551).  The whole path
+(error-bounded sampling with bisection on beta+, final SDF + nablas + radiance, Laplace-CDF density
+compositing, builtin background sphere) runs in libnrhip.so (`nr_volsdf_render`).
+"""
+import copy
+import ctypes
+from collections import OrderedDict
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .. import _lib as L
+from .. import rend_util
+from ..base import ImplicitSurface, NeRF, RadianceNet, _no_training
+from .neus import _linspace_table
+
+
+class VolSDF(nn.Module):
+    """volsdf.py:276-327 (parameter tree and names identical: ln_beta, implicit_surface.*,
+    radiance_net.*, nerf_outside.*)."""
+
+    def __init__(self, beta_init=0.1, speed_factor=1.0, input_ch=3, W_geo_feat=-1, obj_bounding_radius=3.0,
+                 use_nerfplusplus=False, surface_cfg=dict(), radiance_cfg=dict()):
+        super().__init__()
+        self.speed_factor = speed_factor
+        ln_beta_init = np.log(beta_init) / self.speed_factor
+        self.ln_beta = nn.Parameter(data=torch.Tensor([ln_beta_init]), requires_grad=True)
+        self.use_sphere_bg = not use_nerfplusplus
+        self.obj_bounding_radius = obj_bounding_radius
+        self.implicit_surface = ImplicitSurface(W_geo_feat=W_geo_feat, input_ch=input_ch,
+                                                obj_bounding_size=obj_bounding_radius, **surface_cfg)
+        if W_geo_feat < 0:
+            W_geo_feat = self.implicit_surface.W
+        self.radiance_net = RadianceNet(W_geo_feat=W_geo_feat, **radiance_cfg)
+        if use_nerfplusplus:
+            self.nerf_outside = NeRF(input_ch=4, multires=10, multires_view=4, use_view_dirs=True)
+
+    def forward_ab(self):
+        beta = torch.exp(self.ln_beta * self.speed_factor)
+        return 1. / beta, beta
+
+    def forward_surface(self, x):
+        """volsdf.py:310-315: min(sdf, r - |x|) with the builtin background sphere."""
+        sdf = self.implicit_surface.forward(x)
+        if self.use_sphere_bg:
+            return torch.min(sdf, self.obj_bounding_radius - x.norm(dim=-1))
+        return sdf
+
+    def forward_surface_with_nablas(self, x):
+        """volsdf.py:317-325 (nablas of the network, sdf replaced outside the background sphere)."""
+        sdf, nablas, h = self.implicit_surface.forward_with_nablas(x)
+        if self.use_sphere_bg:
+            d_bg = self.obj_bounding_radius - x.norm(dim=-1)
+            outside = d_bg < sdf
+            sdf[outside] = d_bg[outside]
+        return sdf, nablas, h
+
+    def forward(self, x, view_dirs):
+        sdf, nablas, geometry_feature = self.forward_surface_with_nablas(x)
+        radiances = self.radiance_net.forward(x, view_dirs, nablas, geometry_feature)
+        return radiances, sdf, nablas
+
+
+def _host_ab(model):
+    """forward_ab() evaluated exactly as the reference's CPU run (fp32 exp, fp32 reciprocal)."""
+    with torch.no_grad():
+        beta = torch.exp(model.ln_beta.detach().float().cpu() * model.speed_factor)
+        alpha = 1. / beta
+    return float(alpha.reshape(-1)[0]), float(beta.reshape(-1)[0])
+
+
+def _beta_plus_init(far, n_init, eps):
+    """volsdf.py:127-129: sqrt(far^2 / (4 (N-1) log(1+eps))) in fp32 on the CPU."""
+    far_t = far * torch.ones([1])
+    return float(torch.sqrt((far_t ** 2) / (4 * (n_init - 1) * np.log(1 + eps))).reshape(-1)[0])
+
+
+def volume_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=3.0, batched=False,
+                  batched_info={}, calc_normal=False, use_view_dirs=True, rayschunk=65536, netchunk=1048576,
+                  white_bkgd=False, use_nerfplusplus=False, detailed_output=True, show_progress=False,
+                  perturb=False, N_samples=128, N_importance=64, N_outside=32, max_upsample_steps=5,
+                  max_bisection_steps=10, epsilon=0.1, **dummy_kwargs):
+    """volsdf.py:377-551, render mode.  rays_o/rays_d: [(B,) N_rays, 3]."""
+    L.require_gpu(rays_o, 'rays_o')
+    _no_training(model)
+    if perturb:
+        raise NotImplementedError('neurecon_amd: stratified (perturb=True) sampling is a training feature')
+    if use_nerfplusplus:
+        raise NotImplementedError('neurecon_amd: VolSDF with the NeRF++ background is not native yet')
+    if not use_view_dirs:
+        raise NotImplementedError('neurecon_amd: use_view_dirs=False not supported')
+    dev = rays_o.device
+    prefix = [rays_d.shape[0], -1] if batched else [-1]
+    ro = rays_o.reshape(-1, 3).float().contiguous()
+    rd = rays_d.reshape(-1, 3).float().contiguous()
+    n = ro.shape[0]
+    S = N_samples + N_importance
+    N0 = 4 * N_samples
+
+    sdf_desc, sdf_packed = model.implicit_surface.nr_packed(dev)
+    rad_desc, rad_packed = model.radiance_net.nr_packed(dev)
+    alpha_net, beta_net = _host_ab(model)
+    t_coarse = _linspace_table(N_samples, dev)
+    t_init = _linspace_table(N0, dev)
+    u_up = _linspace_table(N0 + 2, dev)
+    u_fine = _linspace_table(N_importance, dev)
+
+    rgb = torch.empty(n, 3, device=dev)
+    depth = torch.empty(n, device=dev)
+    acc = torch.empty(n, device=dev)
+    normals = torch.empty(n, 3, device=dev) if calc_normal else None
+    det = {}
+    if detailed_output:
+        det = dict(implicit_surface=torch.empty(n, S, device=dev), implicit_nablas=torch.empty(n, S, 3, device=dev),
+                   radiance=torch.empty(n, S, 3, device=dev), alpha=torch.empty(n, S - 1, device=dev),
+                   p_i=torch.empty(n, S - 1, device=dev), visibility_weights=torch.empty(n, S - 1, device=dev),
+                   d_vals=torch.empty(n, S, device=dev), sigma=torch.empty(n, S, device=dev),
+                   beta_map=torch.empty(n, device=dev), iter_usage=torch.empty(n, device=dev))
+    a = L.NrVolsdfArgs()
+    a.rays_o, a.rays_d, a.n_rays = L.ptr(ro), L.ptr(rd), n
+    a.sdf, a.sdf_packed = ctypes.pointer(sdf_desc), L.ptr(sdf_packed)
+    a.rad, a.rad_packed = ctypes.pointer(rad_desc), L.ptr(rad_packed)
+    a.alpha_net, a.beta_net = alpha_net, beta_net
+    a.beta_plus_init = _beta_plus_init(far, N0, epsilon)
+    a.eps = float(epsilon)
+    a.near, a.far = float(near), float(far)
+    a.obj_bounding_radius = float(model.obj_bounding_radius)
+    a.use_sphere_bg = int(bool(model.use_sphere_bg))
+    a.N_samples, a.N_importance = N_samples, N_importance
+    a.max_upsample_steps, a.max_bisection_steps = max_upsample_steps, max_bisection_steps
+    a.calc_normal, a.white_bkgd = int(bool(calc_normal)), int(bool(white_bkgd))
+    a.t_coarse, a.t_init, a.u_up, a.u_fine = L.ptr(t_coarse), L.ptr(t_init), L.ptr(u_up), L.ptr(u_fine)
+    a.rgb, a.depth, a.acc, a.normals = L.ptr(rgb), L.ptr(depth), L.ptr(acc), L.ptr(normals)
+    a.d_vals = L.ptr(det.get('d_vals'))
+    a.sdf_out = L.ptr(det.get('implicit_surface'))
+    a.nablas_out = L.ptr(det.get('implicit_nablas'))
+    a.radiance_out = L.ptr(det.get('radiance'))
+    a.alpha_out = L.ptr(det.get('alpha'))
+    a.p_out = L.ptr(det.get('p_i'))
+    a.weights_out = L.ptr(det.get('visibility_weights'))
+    a.sigma_out = L.ptr(det.get('sigma'))
+    a.beta_map = L.ptr(det.get('beta_map'))
+    a.iter_usage = L.ptr(det.get('iter_usage'))
+    lib = L.lib()
+    ws_bytes = lib.nr_volsdf_workspace_bytes(ctypes.byref(a))
+    if ws_bytes == 0:
+        raise NotImplementedError('neurecon_amd: ' + lib.nr_last_error().decode())
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    a.workspace, a.workspace_bytes = L.ptr(ws), ws_bytes
+    L.check(lib.nr_volsdf_render(ctypes.byref(a), L.stream_of(dev)))
+
+    ret = OrderedDict([('rgb', rgb.reshape(*prefix, 3)), ('depth_volume', depth.reshape(prefix)),
+                       ('mask_volume', acc.reshape(prefix))])
+    if calc_normal:
+        ret['normals_volume'] = normals.reshape(*prefix, 3)
+    if detailed_output:
+        ret['implicit_surface'] = det['implicit_surface'].reshape(*prefix, S)
+        ret['implicit_nablas'] = det['implicit_nablas'].reshape(*prefix, S, 3)
+        ret['radiance'] = det['radiance'].reshape(*prefix, S, 3)
+        ret['alpha'] = det['alpha'].reshape(*prefix, S - 1)
+        ret['p_i'] = det['p_i'].reshape(*prefix, S - 1)
+        ret['visibility_weights'] = det['visibility_weights'].reshape(*prefix, S - 1)
+        ret['d_vals'] = det['d_vals'].reshape(*prefix, S)
+        ret['sigma'] = det['sigma'].reshape(*prefix, S)
+        ret['beta_map'] = det['beta_map'].reshape(*prefix, 1)
+        ret['iter_usage'] = det['iter_usage'].reshape(prefix)
+    return ret['rgb'], ret['depth_volume'], ret
+
+
+class SingleRenderer(nn.Module):
+    """volsdf.py:555-561."""
+
+    def __init__(self, model):
+        super().__init__()
+        self.model = model
+
+    def forward(self, rays_o, rays_d, **kwargs):
+        return volume_render(rays_o, rays_d, self.model, **kwargs)
+
+
+class Trainer(nn.Module):
+    """volsdf.py:564-640.  The training step needs the backward of the render kernels;
+    the render call raises while grad is enabled."""
+
+    def __init__(self, model, device_ids=[0], batched=True):
+        super().__init__()
+        self.model = model
+        self.renderer = SingleRenderer(model)
+        if len(device_ids) > 1:
+            self.renderer = nn.DataParallel(self.renderer, device_ids=device_ids, dim=1 if batched else 0)
+        self.device = device_ids[0]
+
+    def forward(self, args, indices, model_input, ground_truth, render_kwargs_train, it):
+        device = self.device
+        intrinsics = model_input['intrinsics'].to(device)
+        c2w = model_input['c2w'].to(device)
+        rays_o, rays_d, select_inds = rend_util.get_rays(c2w, intrinsics, render_kwargs_train['H'],
+                                                         render_kwargs_train['W'], N_rays=args.data.N_rays)
+        return self.renderer(rays_o, rays_d, detailed_output=True, **render_kwargs_train)
+
+
+def get_model(args):
+    """volsdf.py:685-750 (same config keys and defaults)."""
+    from ..config import as_cfg
+    args = as_cfg(args)
+    model_config = {
+        'use_nerfplusplus': args.model.setdefault('outside_scene', 'builtin') == 'nerf++',
+        'obj_bounding_radius': args.model.obj_bounding_radius,
+        'W_geo_feat': args.model.setdefault('W_geometry_feature', 256),
+        'speed_factor': args.training.setdefault('speed_factor', 1.0),
+        'beta_init': args.training.setdefault('beta_init', 0.1),
+    }
+    surface_cfg = {
+        'use_siren': args.model.surface.setdefault('use_siren', args.model.setdefault('use_siren', False)),
+        'embed_multires': args.model.surface.setdefault('embed_multires', 6),
+        'radius_init': args.model.surface.setdefault('radius_init', 1.0),
+        'geometric_init': args.model.surface.setdefault('geometric_init', True),
+        'D': args.model.surface.setdefault('D', 8),
+        'W': args.model.surface.setdefault('W', 256),
+        'skips': args.model.surface.setdefault('skips', [4]),
+    }
+    radiance_cfg = {
+        'use_siren': args.model.radiance.setdefault('use_siren', args.model.setdefault('use_siren', False)),
+        'embed_multires': args.model.radiance.setdefault('embed_multires', -1),
+        'embed_multires_view': args.model.radiance.setdefault('embed_multires_view', -1),
+        'use_view_dirs': args.model.radiance.setdefault('use_view_dirs', True),
+        'D': args.model.radiance.setdefault('D', 4),
+        'W': args.model.radiance.setdefault('W', 256),
+        'skips': args.model.radiance.setdefault('skips', []),
+    }
+    model_config['surface_cfg'] = surface_cfg
+    model_config['radiance_cfg'] = radiance_cfg
+    model = VolSDF(**model_config)
+    render_kwargs_train = {
+        'near': args.data.near,
+        'far': args.data.far,
+        'batched': True,
+        'perturb': args.model.setdefault('perturb', True),
+        'white_bkgd': args.model.setdefault('white_bkgd', False),
+        'max_upsample_steps': args.model.setdefault('max_upsample_iter', 5),
+        'use_nerfplusplus': model_config['use_nerfplusplus'],
+        'obj_bounding_radius': args.model.obj_bounding_radius,
+    }
+    render_kwargs_test = copy.deepcopy(render_kwargs_train)
+    render_kwargs_test['rayschunk'] = args.data.val_rayschunk
+    render_kwargs_test['perturb'] = False
+    trainer = Trainer(model, device_ids=args.device_ids, batched=render_kwargs_train['batched'])
+    return model, trainer, render_kwargs_train, render_kwargs_test, trainer.renderer
