@@ -10,6 +10,8 @@
  *   nr_nerf_forward         NeRF.forward (NeRF++ background)                models/base.py:426-453
  *   nr_neus_render          neus.volume_render (one ray chunk, render mode) models/frameworks/neus.py:118-397
  *   nr_volsdf_render        volsdf.volume_render (render mode)             models/frameworks/volsdf.py:16-551
+ *   nr_unisurf_render       unisurf.volume_render (render mode)            models/frameworks/unisurf.py:62-283,
+ *                           + root_finding_surface_points (secant)         models/ray_casting.py:11-160
  *   nr_sample_pdf           rend_util.sample_pdf                             utils/rend_util.py:255-292
  *   nr_get_rays             rend_util.get_rays (+ lift)                      utils/rend_util.py:95-164
  *
@@ -45,6 +47,29 @@ extern "C" {
 
 int nr_version(void);
 const char* nr_last_error(void);
+
+/* ------------------------------------------------------------------------------------------
+ * NeRF++ background MLP (NeRF, models/base.py:395-453) as used by NeuS / VolSDF outside scenes:
+ * input_ch=4 ([x/r, 1/r]), multires=10, multires_view=4, use_view_dirs=True, D=8, W=256,
+ * skips=[4]; plain nn.Linear layers (no weight norm).  Output: raw sigma and sigmoid rgb.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  int D;             /* 8   */
+  int W;             /* 256 */
+  int skip;          /* 4   */
+  int input_ch;      /* 4   */
+  int multires;      /* 10  */
+  int multires_view; /* 4   */
+  int precision;     /* NR_PREC_* */
+} NrNerfDesc;
+
+size_t nr_nerf_packed_bytes(const NrNerfDesc* d);
+/* W/b: pts_linears[0..7], feature_linear, views_linears[0], alpha_linear, rgb_linear (12 layers,
+ * PyTorch [out, in] row-major weights, device pointers) */
+int nr_nerf_pack(const NrNerfDesc* d, const float* const* W, const float* const* b, void* packed, void* stream);
+/* x4 [P, 4], view dirs [P / vdir_div, 3] -> sigma [P], rgb [P, 3].  Replaces base.py:426-453. */
+int nr_nerf_forward(const NrNerfDesc* d, const void* packed, const float* x4, const float* vdir, int64_t vdir_div,
+                    int64_t P, float* sigma, float* rgb, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * SDF MLP  (ImplicitSurface, models/base.py:131-282)
@@ -127,6 +152,15 @@ typedef struct {
   float* alpha_out;   /* [n_rays, S-1] */
   float* cdf_out;     /* [n_rays, S]   */
   float* weights_out; /* [n_rays, S-1] */
+  /* NeRF++ background (neus.py:303-343), N_outside = 0 disables it.  With N_outside > 0 the
+   * per-sample outputs d_final / radiance_out / alpha_out / weights_out have M = S-1+N_outside
+   * entries per ray (mid-points then the inverted-sphere samples). */
+  const NrNerfDesc* nerf;
+  const void* nerf_packed;
+  int N_outside;
+  const float* t_outside; /* torch.linspace(0, 1, N_outside + 2) */
+  float* sigma_out;       /* [n_rays, M]    raw NeRF sigma ('sigma_out')      */
+  float* radiance_bg_out; /* [n_rays, M, 3] NeRF radiance  ('radiance_out')  */
   void* workspace;
   size_t workspace_bytes;
 } NrNeusArgs;
@@ -182,6 +216,54 @@ typedef struct {
 
 size_t nr_volsdf_workspace_bytes(const NrVolsdfArgs* a);
 int nr_volsdf_render(const NrVolsdfArgs* a, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * UNISURF rendering (models/frameworks/unisurf.py:62-283, render mode: perturb=False, secant
+ * root finding of ray_casting.py:11-160).  P = N_query + N_freespace samples per ray.
+ * normal_mode selects what the reference's F.normalize(nablas) (default dim=1, unisurf.py:36)
+ * normalises over: 0 = the xyz components of each point (unbatched call, [chunk, 3] tensors),
+ * 1 = each component over a batchify_query window of `netchunk` points of one batch row's
+ * ray chunk of `rayschunk` rays (batched call, [B, chunk, 3] tensors).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  const float* rays_o; /* [n_rays, 3] */
+  const float* rays_d; /* [n_rays, 3], normalised inside (unisurf.py:112) */
+  int64_t n_rays;
+  int64_t rays_per_batch; /* rays of one batch row (n_rays = B * rays_per_batch); <= 0: n_rays */
+  const NrSdfDesc* sdf;
+  const void* sdf_packed;
+  const NrRadDesc* rad;
+  const void* rad_packed;
+  float logit_tau;
+  float radius_of_interest;
+  float interval;
+  float too_close_threshold;
+  float near_bypass, far_bypass; /* NaN = none */
+  int N_steps, N_secant_steps, N_query, N_freespace;
+  int normal_mode;
+  int64_t rayschunk, netchunk;
+  int calc_normal, white_bkgd;
+  const float* t_march; /* torch.linspace(0, 1, N_steps)     (CPU values) */
+  const float* t_query; /* torch.linspace(0, 1, N_query)     */
+  const float* t_free;  /* torch.linspace(0, 1, N_freespace) */
+  float* rgb;            /* [n_rays, 3] */
+  float* depth;          /* [n_rays]    */
+  float* acc;            /* [n_rays]    */
+  float* normals;        /* [n_rays, 3] (calc_normal) */
+  float* surface_points; /* [n_rays, 3] */
+  uint8_t* mask_surface; /* [n_rays] (bool) */
+  float* depth_surface;  /* [n_rays]    */
+  float* radiance_out;   /* [n_rays, P, 3] */
+  float* sdf_out;        /* [n_rays, P] implicit_surface (logits) */
+  float* nablas_out;     /* [n_rays, P, 3] */
+  float* alpha_out;      /* [n_rays, P] */
+  float* weights_out;    /* [n_rays, P] visibility_weights */
+  void* workspace;
+  size_t workspace_bytes;
+} NrUnisurfArgs;
+
+size_t nr_unisurf_workspace_bytes(const NrUnisurfArgs* a);
+int nr_unisurf_render(const NrUnisurfArgs* a, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Inverse-CDF sampling (rend_util.sample_pdf, det=True or caller-provided u):

@@ -32,6 +32,11 @@ class NrRadDesc(ctypes.Structure):
                 ('precision', _c_i)]
 
 
+class NrNerfDesc(ctypes.Structure):
+    _fields_ = [('D', _c_i), ('W', _c_i), ('skip', _c_i), ('input_ch', _c_i), ('multires', _c_i),
+                ('multires_view', _c_i), ('precision', _c_i)]
+
+
 class NrNeusArgs(ctypes.Structure):
     _fields_ = [
         ('rays_o', _c_p), ('rays_d', _c_p), ('n_rays', _c_i64),
@@ -44,6 +49,8 @@ class NrNeusArgs(ctypes.Structure):
         ('rgb', _c_p), ('depth', _c_p), ('acc', _c_p), ('normals', _c_p),
         ('d_final', _c_p), ('sdf_out', _c_p), ('nablas_out', _c_p), ('radiance_out', _c_p),
         ('alpha_out', _c_p), ('cdf_out', _c_p), ('weights_out', _c_p),
+        ('nerf', ctypes.POINTER(NrNerfDesc)), ('nerf_packed', _c_p), ('N_outside', _c_i), ('t_outside', _c_p),
+        ('sigma_out', _c_p), ('radiance_bg_out', _c_p),
         ('workspace', _c_p), ('workspace_bytes', _c_sz),
     ]
 
@@ -66,6 +73,24 @@ class NrVolsdfArgs(ctypes.Structure):
     ]
 
 
+class NrUnisurfArgs(ctypes.Structure):
+    _fields_ = [
+        ('rays_o', _c_p), ('rays_d', _c_p), ('n_rays', _c_i64), ('rays_per_batch', _c_i64),
+        ('sdf', ctypes.POINTER(NrSdfDesc)), ('sdf_packed', _c_p),
+        ('rad', ctypes.POINTER(NrRadDesc)), ('rad_packed', _c_p),
+        ('logit_tau', _c_f), ('radius_of_interest', _c_f), ('interval', _c_f), ('too_close_threshold', _c_f),
+        ('near_bypass', _c_f), ('far_bypass', _c_f),
+        ('N_steps', _c_i), ('N_secant_steps', _c_i), ('N_query', _c_i), ('N_freespace', _c_i),
+        ('normal_mode', _c_i), ('rayschunk', _c_i64), ('netchunk', _c_i64),
+        ('calc_normal', _c_i), ('white_bkgd', _c_i),
+        ('t_march', _c_p), ('t_query', _c_p), ('t_free', _c_p),
+        ('rgb', _c_p), ('depth', _c_p), ('acc', _c_p), ('normals', _c_p),
+        ('surface_points', _c_p), ('mask_surface', _c_p), ('depth_surface', _c_p),
+        ('radiance_out', _c_p), ('sdf_out', _c_p), ('nablas_out', _c_p), ('alpha_out', _c_p), ('weights_out', _c_p),
+        ('workspace', _c_p), ('workspace_bytes', _c_sz),
+    ]
+
+
 class NrKernelStat(ctypes.Structure):
     _fields_ = [('name', ctypes.c_char * 32), ('launches', _c_i64), ('ms', ctypes.c_double),
                 ('units', ctypes.c_double)]
@@ -82,10 +107,15 @@ _SIGS = {
     'nr_radiance_pack': (_c_i, [ctypes.POINTER(NrRadDesc), ctypes.POINTER(_c_p), ctypes.POINTER(_c_p), _c_p, _c_p]),
     'nr_radiance_forward': (_c_i, [ctypes.POINTER(NrRadDesc), _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_i64, _c_p,
                                    _c_p]),
+    'nr_nerf_packed_bytes': (_c_sz, [ctypes.POINTER(NrNerfDesc)]),
+    'nr_nerf_pack': (_c_i, [ctypes.POINTER(NrNerfDesc), ctypes.POINTER(_c_p), ctypes.POINTER(_c_p), _c_p, _c_p]),
+    'nr_nerf_forward': (_c_i, [ctypes.POINTER(NrNerfDesc), _c_p, _c_p, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_p]),
     'nr_neus_workspace_bytes': (_c_sz, [ctypes.POINTER(NrNeusArgs)]),
     'nr_neus_render': (_c_i, [ctypes.POINTER(NrNeusArgs), _c_p]),
     'nr_volsdf_workspace_bytes': (_c_sz, [ctypes.POINTER(NrVolsdfArgs)]),
     'nr_volsdf_render': (_c_i, [ctypes.POINTER(NrVolsdfArgs), _c_p]),
+    'nr_unisurf_workspace_bytes': (_c_sz, [ctypes.POINTER(NrUnisurfArgs)]),
+    'nr_unisurf_render': (_c_i, [ctypes.POINTER(NrUnisurfArgs), _c_p]),
     'nr_sample_pdf': (_c_i, [_c_p, _c_p, _c_i64, _c_i, _c_p, _c_i, _c_p, _c_p]),
     'nr_get_rays': (_c_i, [_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p]),
     'nr_profile_enable': (_c_i, [_c_i]),

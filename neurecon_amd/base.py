@@ -289,14 +289,14 @@ class RadianceNet(nn.Module):
 
 
 # ---------------------------------------------------------------------------------------------
-# NeRF++ background (models/base.py:395-453): parameters only in this round (state_dict compat)
+# NeRF++ background (models/base.py:395-453)
 # ---------------------------------------------------------------------------------------------
 class NeRF(nn.Module):
     def __init__(self, D=8, W=256, input_ch=3, input_ch_view=3, multires=-1, multires_view=-1, output_ch=4,
-                 skips=[4], use_view_dirs=False):
+                 skips=[4], use_view_dirs=False, precision=None):
         super().__init__()
         self.D, self.W, self.skips, self.use_view_dirs = D, W, list(skips), use_view_dirs
-        self.multires, self.multires_view = multires, multires_view
+        self.multires, self.multires_view, self.input_ch_raw = multires, multires_view, input_ch
         self.embed_fn, input_ch = get_embedder(multires, input_dim=input_ch)
         self.embed_fn_view, input_ch_view = get_embedder(multires_view, input_dim=input_ch_view)
         self.pts_linears = nn.ModuleList(
@@ -308,6 +308,49 @@ class NeRF(nn.Module):
             self.rgb_linear = nn.Linear(W // 2, 3)
         else:
             self.output_linear = nn.Linear(W, output_ch)
+        self.precision = default_precision() if precision is None else precision
+        self._nr_cache = None
+
+    def nr_desc(self):
+        if not self.use_view_dirs or len(self.skips) != 1:
+            raise NotImplementedError('neurecon_amd: only the NeRF++ background configuration is native')
+        return L.NrNerfDesc(self.D, self.W, self.skips[0], self.input_ch_raw, self.multires, self.multires_view,
+                            L.PREC_FP32 if self.precision == 'fp32' else L.PREC_F16X3)
+
+    def nr_packed(self, device):
+        key = _version_key(self, self.precision, device)
+        if self._nr_cache is not None and self._nr_cache[0] == key:
+            return self._nr_cache[1], self._nr_cache[2]
+        lib = L.lib()
+        desc = self.nr_desc()
+        nbytes = lib.nr_nerf_packed_bytes(ctypes.byref(desc))
+        if nbytes == 0:
+            raise NotImplementedError('neurecon_amd: ' + lib.nr_last_error().decode())
+        layers = list(self.pts_linears) + [self.feature_linear, self.views_linears[0], self.alpha_linear,
+                                           self.rgb_linear]
+        with torch.no_grad():
+            Ws = [l.weight.detach().float().contiguous().to(device) for l in layers]
+            bs = [l.bias.detach().float().contiguous().to(device) for l in layers]
+            packed = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            L.check(lib.nr_nerf_pack(ctypes.byref(desc), _ptr_array(Ws), _ptr_array(bs), L.ptr(packed),
+                                     L.stream_of(device)))
+        self._nr_cache = (key, desc, packed, Ws, bs)
+        return desc, packed
 
     def forward(self, input_pts, input_views):
-        raise NotImplementedError('neurecon_amd: the NeRF++ background kernel lands with config (d)')
+        """base.py:426-453 (render mode): returns (sigma [...], rgb [..., 3])."""
+        L.require_gpu(input_pts, 'points')
+        _no_training(self)
+        shape = input_pts.shape[:-1]
+        dev = input_pts.device
+        x = input_pts.reshape(-1, 4).float().contiguous()
+        P = x.shape[0]
+        v = input_views.reshape(-1, 3).float().contiguous()
+        if v.shape[0] != P:
+            raise ValueError('input_views must have one direction per point')
+        desc, packed = self.nr_packed(dev)
+        sigma = torch.empty(P, device=dev)
+        rgb = torch.empty(P, 3, device=dev)
+        L.check(L.lib().nr_nerf_forward(ctypes.byref(desc), L.ptr(packed), L.ptr(x), L.ptr(v), 1, P, L.ptr(sigma),
+                                        L.ptr(rgb), L.stream_of(dev)))
+        return sigma.reshape(shape), rgb.reshape(*shape, 3)

@@ -8,6 +8,7 @@
 #include "nr_mlp.h"
 #include "nr_neus.h"
 #include "nr_volsdf.h"
+#include "nr_unisurf.h"
 
 namespace nr {
 
@@ -84,6 +85,41 @@ RadLayout rad_layout(const NrRadDesc& d) {
   return L;
 }
 
+int check_nerf_desc(const NrNerfDesc* d) {
+  NR_REQUIRE(d, NR_ERR_ARG, "null NrNerfDesc");
+  NR_REQUIRE(d->D == 8 && d->W == 256 && d->skip == 4 && d->input_ch == 4 && d->multires == 10 &&
+                 d->multires_view == 4,
+             NR_ERR_UNSUPPORTED,
+             "NeRF net: only the NeRF++ background configuration (D=8, W=256, skips=[4], input_ch=4, "
+             "multires=10, multires_view=4, use_view_dirs) is implemented");
+  NR_REQUIRE(d->precision == NR_PREC_FP32 || d->precision == NR_PREC_F16X3, NR_ERR_UNSUPPORTED,
+             "NeRF net: unknown precision mode");
+  return NR_OK;
+}
+
+// (input blocks, output blocks) of each NeRF GEMM op: N0..N7, feature, views
+static const int kNerfKB[kNerfOps] = {6, 16, 16, 16, 16, 22, 16, 16, 16, 18};
+static const int kNerfNBO[kNerfOps] = {16, 16, 16, 16, 16, 16, 16, 16, 16, 8};
+
+NerfLayout nerf_layout(const NrNerfDesc& d) {
+  NerfLayout L{};
+  L.prec = d.precision;
+  size_t off = 0;
+  for (int i = 0; i < kNerfOps; ++i) {
+    L.op_bytes[i] = (2 * kNerfKB[i] + 1) * 1024;
+    L.op_off[i] = (uint32_t)off;
+    off += (size_t)(kNerfNBO[i] / 2) * L.op_bytes[i];
+  }
+  L.scale_off = (uint32_t)off;
+  off = align256(off + kNerfOps * 4);
+  L.alpha_off = (uint32_t)off;
+  off = align256(off + 257 * 4);
+  L.rgb_off = (uint32_t)off;
+  off = align256(off + (3 * 128 + 3) * 4);
+  L.total = (uint32_t)off;
+  return L;
+}
+
 static PackSeg seg(int nblk, int off, int nvalid) { return PackSeg{nblk, off, nvalid}; }
 static PackOp mkop(const float* W, const float* bias, int rows, int ld, int tr, PackSeg o0, PackSeg o1, PackSeg i0,
                    PackSeg i1, float scale, int prec, float* wmax) {
@@ -119,6 +155,10 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   c.pts = F(pl.o_pts); c.mids = F(pl.o_mids); c.dmid = F(pl.o_dmid);
   c.sdf_f = F(pl.o_sdf_f); c.nab_f = F(pl.o_nab_f);
   c.sdf_m = F(pl.o_sdf_m); c.nab_m = F(pl.o_nab_m); c.feat_m = F(pl.o_feat_m); c.rad_m = F(pl.o_rad_m);
+  c.N_out = a.N_outside;
+  c.r_obj = a.obj_bounding_radius;
+  c.t_out = a.t_outside;
+  c.d_out = F(pl.o_dout); c.x4 = F(pl.o_x4); c.sig_o = F(pl.o_sigo); c.rad_o = F(pl.o_rado);
   void* mlp_ws = ws + pl.o_mlp;
   const size_t mlp_bytes = a.workspace_bytes - pl.o_mlp;
   const SdfLayout SL = sdf_layout(*a.sdf);
@@ -163,8 +203,16 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
                             a.rad->multires_view, st)))
     return rc;
   NeusOut o{ray0, a.rgb, a.depth, a.acc, a.normals, a.d_final, a.sdf_out, a.nablas_out,
-            a.radiance_out, a.alpha_out, a.cdf_out, a.weights_out};
-  {
+            a.radiance_out, a.alpha_out, a.cdf_out, a.weights_out, a.sigma_out, a.radiance_bg_out};
+  if (a.N_outside > 0) {  // NeRF++ background on [mid-points ; inverted-sphere samples]
+    hipLaunchKernelGGL(neus_outside_points, grd, blk, 0, st, c);
+    NR_HIP_CHECK(hipGetLastError());
+    const int64_t Po = (int64_t)(c.S - 1 + a.N_outside) * R;
+    if ((rc = launch_nerf(nerf_layout(*a.nerf), a.nerf_packed, c.x4, c.rd, 1, R, Po, c.sig_o, c.rad_o, st)))
+      return rc;
+    ProfScope prof("neus_composite", (double)R, st);
+    hipLaunchKernelGGL(neus_composite_outside, grd, blk, 0, st, c, o, a.s, a.calc_normal, a.white_bkgd);
+  } else {
     ProfScope prof("neus_composite", (double)R, st);
     hipLaunchKernelGGL(neus_composite, grd, blk, 0, st, c, o, a.s, a.calc_normal, a.white_bkgd);
   }
@@ -287,6 +335,101 @@ static int check_volsdf(const NrVolsdfArgs* a) {
   return NR_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// UNISURF chunk orchestration (unisurf.py:118-244): prologue -> SDF(march) -> root -> [SDF(secant
+// point) -> secant] x N_secant_steps -> samples -> SDF+nablas+feature -> F.normalize -> radiance
+// -> composite.
+// ---------------------------------------------------------------------------------------------
+static int unisurf_chunk(const NrUnisurfArgs& a, const UniPlan& pl, int64_t ray0, int R, hipStream_t st) {
+  char* ws = (char*)a.workspace;
+  auto F = [&](size_t o) { return (float*)(ws + o); };
+  UniChunk c{};
+  c.R = R;
+  c.N_steps = a.N_steps;
+  c.N_query = a.N_query;
+  c.N_free = a.N_freespace;
+  c.P = a.N_query + a.N_freespace;
+  c.logit_tau = a.logit_tau;
+  c.interval = a.interval;
+  c.too_close = a.too_close_threshold;
+  c.near_bypass = a.near_bypass;
+  c.far_bypass = a.far_bypass;
+  c.r_interest = a.radius_of_interest;
+  c.ro = F(pl.o_ro); c.rd = F(pl.o_rd); c.near = F(pl.o_near); c.far = F(pl.o_far); c.thr = F(pl.o_thr);
+  c.pts_m = F(pl.o_ptsm); c.sm = F(pl.o_sm); c.sec = F(pl.o_sec); c.pts_s = F(pl.o_ptss); c.ss = F(pl.o_ss);
+  c.d_all = F(pl.o_dall); c.pts_f = F(pl.o_ptsf); c.sdf_f = F(pl.o_sdff); c.nab_f = F(pl.o_nabf);
+  c.feat_f = F(pl.o_featf); c.nrm_f = F(pl.o_nrmf); c.rad_f = F(pl.o_radf); c.wss = (double*)(ws + pl.o_wss);
+  c.netchunk = a.netchunk;
+  c.t_march = a.t_march; c.t_query = a.t_query; c.t_free = a.t_free;
+  void* mlp_ws = ws + pl.o_mlp;
+  const size_t mlp_bytes = a.workspace_bytes - pl.o_mlp;
+  const SdfLayout SL = sdf_layout(*a.sdf);
+  const RadLayout RL = rad_layout(*a.rad);
+  const dim3 blk(256), grd((R + 255) / 256);
+  const int64_t P = (int64_t)c.P * R;
+  int rc;
+  {
+    ProfScope prof("unisurf_prologue", (double)R, st);
+    hipLaunchKernelGGL(uni_prologue, grd, blk, 0, st, c, a.rays_o + ray0 * 3, a.rays_d + ray0 * 3);
+  }
+  NR_HIP_CHECK(hipGetLastError());
+  if ((rc = launch_sdf(SL, a.sdf_packed, c.pts_m, (int64_t)a.N_steps * R, c.sm, nullptr, nullptr, a.sdf->multires,
+                       nullptr, 0, st)))
+    return rc;
+  hipLaunchKernelGGL(uni_root, grd, blk, 0, st, c);
+  NR_HIP_CHECK(hipGetLastError());
+  for (int i = 0; i < a.N_secant_steps; ++i) {
+    if ((rc = launch_sdf(SL, a.sdf_packed, c.pts_s, R, c.ss, nullptr, nullptr, a.sdf->multires, nullptr, 0, st)))
+      return rc;
+    hipLaunchKernelGGL(uni_secant, grd, blk, 0, st, c, (int)(i == a.N_secant_steps - 1));
+    NR_HIP_CHECK(hipGetLastError());
+  }
+  UniOut o{ray0, a.rgb, a.depth, a.acc, a.normals, a.surface_points, a.mask_surface, a.depth_surface,
+           a.radiance_out, a.sdf_out, a.nablas_out, a.alpha_out, a.weights_out};
+  hipLaunchKernelGGL(uni_samples, grd, blk, 0, st, c, o);
+  NR_HIP_CHECK(hipGetLastError());
+  if ((rc = launch_sdf(SL, a.sdf_packed, c.pts_f, P, c.sdf_f, c.nab_f, c.feat_f, a.sdf->multires, mlp_ws, mlp_bytes,
+                       st)))
+    return rc;
+  if (a.normal_mode == 1) {
+    const int64_t nw = (P + a.netchunk - 1) / a.netchunk;
+    hipLaunchKernelGGL(uni_window_ss, dim3((unsigned)nw), dim3(256), 0, st, c);
+    NR_HIP_CHECK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(uni_normalize, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, c, a.normal_mode);
+  NR_HIP_CHECK(hipGetLastError());
+  if ((rc = launch_radiance(RL, a.rad_packed, c.pts_f, c.rd, 1, R, c.nrm_f, c.feat_f, P, c.rad_f,
+                            a.rad->multires_view, st)))
+    return rc;
+  {
+    ProfScope prof("unisurf_composite", (double)R, st);
+    hipLaunchKernelGGL(uni_composite, grd, blk, 0, st, c, o, a.calc_normal, a.white_bkgd);
+  }
+  NR_HIP_CHECK(hipGetLastError());
+  return NR_OK;
+}
+
+static int check_unisurf(const NrUnisurfArgs* a) {
+  NR_REQUIRE(a, NR_ERR_ARG, "nr_unisurf_render: null args");
+  int rc = check_sdf_desc(a->sdf);
+  if (rc) return rc;
+  if ((rc = check_rad_desc(a->rad))) return rc;
+  NR_REQUIRE(a->rays_o && a->rays_d && a->sdf_packed && a->rad_packed && a->t_march && a->t_query && a->t_free &&
+                 a->rgb && a->depth && a->acc,
+             NR_ERR_ARG, "nr_unisurf_render: null argument");
+  NR_REQUIRE(!a->calc_normal || a->normals, NR_ERR_ARG, "nr_unisurf_render: calc_normal needs normals output");
+  NR_REQUIRE(a->N_steps >= 2 && a->N_secant_steps >= 0 && a->N_query >= 1 && a->N_freespace >= 1, NR_ERR_ARG,
+             "nr_unisurf_render: bad sample counts");
+  NR_REQUIRE(a->normal_mode == 0 || a->normal_mode == 1, NR_ERR_ARG, "nr_unisurf_render: normal_mode must be 0|1");
+  NR_REQUIRE(a->normal_mode == 0 || (a->rayschunk > 0 && a->netchunk > 0), NR_ERR_ARG,
+             "nr_unisurf_render: rayschunk/netchunk must be positive");
+  if (a->rays_per_batch > 0)
+    NR_REQUIRE(a->n_rays % a->rays_per_batch == 0, NR_ERR_ARG, "nr_unisurf_render: n_rays % rays_per_batch != 0");
+  NR_REQUIRE(unisurf_chunk_rays(*a) > 0, NR_ERR_UNSUPPORTED,
+             "nr_unisurf_render: rayschunk too large for windowed normalisation unless netchunk % P == 0");
+  return NR_OK;
+}
+
 }  // namespace nr
 
 using namespace nr;
@@ -352,6 +495,52 @@ int nr_sdf_forward(const NrSdfDesc* d, const void* packed, const float* pts, int
                     (hipStream_t)stream);
 }
 
+size_t nr_nerf_packed_bytes(const NrNerfDesc* d) {
+  if (check_nerf_desc(d)) return 0;
+  return nerf_layout(*d).total;
+}
+
+int nr_nerf_pack(const NrNerfDesc* d, const float* const* W, const float* const* b, void* packed, void* stream) {
+  int rc = check_nerf_desc(d);
+  if (rc) return rc;
+  NR_REQUIRE(W && b && packed, NR_ERR_ARG, "nr_nerf_pack: null argument");
+  for (int l = 0; l < 12; ++l) NR_REQUIRE(W[l] && b[l], NR_ERR_ARG, "nr_nerf_pack: null layer pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const NerfLayout L = nerf_layout(*d);
+  char* P = (char*)packed;
+  const int prec = d->precision;
+  float* wmax = (float*)(P + L.scale_off);
+  const int in0 = 84, inv = 27;
+  PackOp ops[kNerfOps];
+  ops[N0] = mkop(W[0], b[0], 256, in0, 0, seg(16, 0, 256), none(), seg(6, 0, in0), none(), 1.0f, prec, wmax + N0);
+  for (int i = 1; i < 8; ++i) {
+    if (i == 5)  // Linear(W + input_ch, W): columns [input_pts(84) | h(256)] -> K blocks [h ; input_pts]
+      ops[i] = mkop(W[i], b[i], 256, 256 + in0, 0, seg(16, 0, 256), none(), seg(16, in0, 256), seg(6, 0, in0), 1.0f,
+                    prec, wmax + i);
+    else
+      ops[i] = mkop(W[i], b[i], 256, 256, 0, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + i);
+  }
+  ops[NF] = mkop(W[8], b[8], 256, 256, 0, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + NF);
+  ops[NV] = mkop(W[9], b[9], 128, 256 + inv, 0, seg(8, 0, 128), none(), seg(16, 0, 256), seg(2, 256, inv), 1.0f, prec,
+                 wmax + NV);
+  for (int i = 0; i < kNerfOps; ++i)
+    if ((rc = launch_pack_op(ops[i], P + L.op_off[i], st))) return rc;
+  if ((rc = launch_pack_vec(W[10], 0, 256, 256, P + L.alpha_off, st))) return rc;
+  if ((rc = launch_pack_vec(b[10], 0, 1, 1, P + L.alpha_off + 256 * 4, st))) return rc;
+  if ((rc = launch_pack_vec(W[11], 0, 384, 384, P + L.rgb_off, st))) return rc;
+  if ((rc = launch_pack_vec(b[11], 0, 3, 3, P + L.rgb_off + 384 * 4, st))) return rc;
+  return NR_OK;
+}
+
+int nr_nerf_forward(const NrNerfDesc* d, const void* packed, const float* x4, const float* vdir, int64_t vdir_div,
+                    int64_t P, float* sigma, float* rgb, void* stream) {
+  int rc = check_nerf_desc(d);
+  if (rc) return rc;
+  NR_REQUIRE(packed && x4 && vdir && sigma && rgb && vdir_div > 0 && P >= 0, NR_ERR_ARG,
+             "nr_nerf_forward: bad argument");
+  return launch_nerf(nerf_layout(*d), packed, x4, vdir, vdir_div, INT64_MAX, P, sigma, rgb, (hipStream_t)stream);
+}
+
 size_t nr_radiance_packed_bytes(const NrRadDesc* d) {
   if (check_rad_desc(d)) return 0;
   return rad_layout(*d).total;
@@ -404,6 +593,11 @@ int nr_neus_render(const NrNeusArgs* a, void* stream) {
              NR_ERR_ARG, "nr_neus_render: null argument");
   NR_REQUIRE(a->N_samples >= 2, NR_ERR_ARG, "nr_neus_render: N_samples must be >= 2");
   NR_REQUIRE(!a->calc_normal || a->normals, NR_ERR_ARG, "nr_neus_render: calc_normal needs normals output");
+  NR_REQUIRE(a->N_outside >= 0, NR_ERR_ARG, "nr_neus_render: N_outside must be >= 0");
+  if (a->N_outside > 0) {
+    if ((rc = check_nerf_desc(a->nerf))) return rc;
+    NR_REQUIRE(a->nerf_packed && a->t_outside, NR_ERR_ARG, "nr_neus_render: N_outside > 0 needs the NeRF++ net");
+  }
   if (a->N_upsample_iters > 0) {
     const int n_up = a->N_importance / a->N_upsample_iters;
     NR_REQUIRE(n_up >= 1 && n_up <= kMaxUp && a->u_fine, NR_ERR_UNSUPPORTED,
@@ -441,6 +635,35 @@ int nr_volsdf_render(const NrVolsdfArgs* a, void* stream) {
   for (int64_t r0 = 0; r0 < a->n_rays; r0 += Rc) {
     const int R = (int)((a->n_rays - r0) < Rc ? (a->n_rays - r0) : Rc);
     if ((rc = volsdf_chunk(*a, pl, r0, R, (hipStream_t)stream))) return rc;
+  }
+  return NR_OK;
+}
+
+size_t nr_unisurf_workspace_bytes(const NrUnisurfArgs* a) {
+  if (!a || check_unisurf(a)) return 0;
+  return unisurf_plan(*a, unisurf_chunk_rays(*a)).total;
+}
+
+int nr_unisurf_render(const NrUnisurfArgs* a, void* stream) {
+  int rc = check_unisurf(a);
+  if (rc) return rc;
+  if (a->n_rays <= 0) return NR_OK;
+  const int64_t Rc = unisurf_chunk_rays(*a);
+  const UniPlan pl = unisurf_plan(*a, Rc);
+  NR_REQUIRE(a->workspace && a->workspace_bytes >= pl.total, NR_ERR_WORKSPACE,
+             "nr_unisurf_render: workspace too small");
+  const int64_t per_b = (a->normal_mode == 1 && a->rays_per_batch > 0) ? a->rays_per_batch : a->n_rays;
+  // window mode: chunks restart at every batch row and at every reference ray chunk
+  const int64_t span = a->normal_mode == 1 ? (a->rayschunk < per_b ? a->rayschunk : per_b) : per_b;
+  for (int64_t b0 = 0; b0 < a->n_rays; b0 += per_b) {
+    const int64_t b1 = b0 + per_b < a->n_rays ? b0 + per_b : a->n_rays;
+    for (int64_t c0 = b0; c0 < b1; c0 += span) {
+      const int64_t c1 = c0 + span < b1 ? c0 + span : b1;
+      for (int64_t r0 = c0; r0 < c1; r0 += Rc) {
+        const int R = (int)((c1 - r0) < Rc ? (c1 - r0) : Rc);
+        if ((rc = unisurf_chunk(*a, pl, r0, R, (hipStream_t)stream))) return rc;
+      }
+    }
   }
   return NR_OK;
 }

@@ -135,6 +135,13 @@ __device__ __forceinline__ float invert_one(float u, float c0, float c1, float b
   return fadd(b0, fmul(t, fsub(b1, b0)));
 }
 
+// torch CPU x.norm(dim=-1) of a 3-vector (and F.normalize's denominator): the reduction loop
+// accumulates with fused multiply-adds, sqrt(fma(z, z, fma(y, y, x*x))) -- verified bit-exact vs
+// torch.norm on the host (tests/test_sum_order.py)
+__device__ __forceinline__ float norm3_ref(float x, float y, float z) {
+  return sqrtf(__fmaf_rn(z, z, __fmaf_rn(y, y, fmul(x, x))));
+}
+
 // torch.sigmoid(x) = 1 / (1 + exp(-x))
 __device__ __forceinline__ float sigmoidf_ref(float x) { return fdiv(1.0f, fadd(1.0f, expf(-x))); }
 

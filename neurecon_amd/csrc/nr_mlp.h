@@ -35,6 +35,20 @@ struct RadLayout {
   int n_small;        // 3 + view-embedding + 3
 };
 
+// NeRF++ background MLP (models/base.py:395-453): 8 x (Linear+ReLU) with the input re-injected
+// after layer 4, sigma head, feature Linear, view branch Linear(256+27 -> 128)+ReLU, rgb head.
+enum NerfOp { N0, N1, N2, N3, N4, N5, N6, N7, NF, NV, kNerfOps };
+
+struct NerfLayout {
+  uint32_t op_off[kNerfOps];
+  uint32_t op_bytes[kNerfOps];
+  uint32_t scale_off;  // [kNerfOps] max |W| per op
+  uint32_t alpha_off;  // [256] weights, [256] = bias
+  uint32_t rgb_off;    // [3][128] weights, then [3] bias
+  uint32_t total;
+  int prec;
+};
+
 struct PackSeg {
   int nblk;    // 16-feature blocks
   int off;     // first source index
@@ -59,6 +73,8 @@ int launch_pack_vec(const float* src, int off, int nvalid, int n, char* dst, hip
 int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,
                float* feature, int nfreq, void* ws, size_t ws_bytes, hipStream_t stream,
                const int* P_dev = nullptr, int P_mult = 0);  // P_dev: device count, P_eff = min(P, *P_dev * P_mult)
+int launch_nerf(const NerfLayout& L, const void* packed, const float* x4, const float* vdir, int64_t vdiv,
+                int64_t vmod, int64_t P, float* sigma, float* rgb, hipStream_t stream);
 int launch_radiance(const RadLayout& L, const void* packed, const float* x, const float* vdir, int64_t vdiv,
                     int64_t vmod, const float* normals, const float* feature, int64_t P, float* rgb, int nfreq_view,
                     hipStream_t stream);

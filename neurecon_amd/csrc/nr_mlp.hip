@@ -71,8 +71,8 @@ __device__ __forceinline__ float4 fromf(f32x4 v) { return make_float4(v[0], v[1]
 // Software-pipelined one input block deep: the A fragments of block b+1 are read from LDS while
 // block b's 8 MFMAs issue; sched_barrier stops hipcc from hoisting every LDS read of the chunk
 // (which would cost ~128 VGPRs and force spills at 2 waves/SIMD).
-template <int KBX, int KBE>
-__device__ __forceinline__ void mma_chunk(const float4* __restrict__ A, const float4 (&X)[16], const float4 (&E)[4],
+template <int KBX, int KBE, int NE>
+__device__ __forceinline__ void mma_chunk(const float4* __restrict__ A, const float4 (&X)[16], const float4 (&E)[NE],
                                           f32x4& acc0, f32x4& acc1, int lane) {
   constexpr int KB = KBX + KBE;
   float4 n0 = A[lane], n1 = A[KB * 64 + lane];
@@ -178,8 +178,8 @@ __device__ __forceinline__ void split8(float4 lo4, float4 hi4, float sc, f16x8& 
 }
 // B operand of a layer whose input is [X[0..KBX) ; E[0..KBE)] (16-feature blocks, acc layout):
 // k-step s pairs blocks 2s, 2s+1.  Returns 1/scale of this lane's point.
-template <int KBX, int KBE>
-__device__ __forceinline__ float make_b16(const float4 (&X)[16], const float4 (&E)[4], f16x8 (&bh)[12],
+template <int KBX, int KBE, int NE>
+__device__ __forceinline__ float make_b16(const float4 (&X)[16], const float4 (&E)[NE], f16x8 (&bh)[12],
                                           f16x8 (&bl)[12]) {
   constexpr int KB = KBX + KBE;
   static_assert(KB % 2 == 0 && KB <= 24, "bad block count");
@@ -219,9 +219,9 @@ __device__ __forceinline__ void mma_chunk_h3(const float4* __restrict__ A, const
 
 // Forward GEMM layer: Y[0..NBO) = act(W · [X[0..KBX) ; E[0..KBE)] + bias).
 // `op` chunks are consumed from the stream; `nxt/nxt_bytes` is the chunk that follows this op.
-template <int P, int KBX, int KBE, int NBO, int ACT>
+template <int P, int KBX, int KBE, int NBO, int ACT, int NE>
 __device__ __forceinline__ void gemm_fwd(WStream& ws, const char* __restrict__ op, const char* nxt, int nxt_bytes,
-                                         const float4 (&X)[16], const float4 (&E)[4], float4 (&Y)[16],
+                                         const float4 (&X)[16], const float4 (&E)[NE], float4 (&Y)[16],
                                          float4* __restrict__ e_out, float* __restrict__ feat_out, bool feat_ok,
                                          int lane) {
   constexpr int KB = KBX + KBE;
@@ -229,7 +229,7 @@ __device__ __forceinline__ void gemm_fwd(WStream& ws, const char* __restrict__ o
   const int g = lane >> 4;
   f16x8 bh[12], bl[12];
   float xinv = 1.0f;
-  if constexpr (P == NR_PREC_F16X3) xinv = make_b16<KBX, KBE>(X, E, bh, bl);
+  if constexpr (P == NR_PREC_F16X3) xinv = make_b16<KBX, KBE, NE>(X, E, bh, bl);
   // global stores of chunk c are issued at the start of chunk c+1, *before* that chunk's DMA, so
   // the vmcnt(0) in flip() waits for a store that had a whole chunk to retire, not a fresh one
   float4 p0 = make_float4(0, 0, 0, 0), p1 = p0;
@@ -261,7 +261,7 @@ __device__ __forceinline__ void gemm_fwd(WStream& ws, const char* __restrict__ o
     if constexpr (P == NR_PREC_FP32) {
       acc0 = b0;
       acc1 = b1;
-      mma_chunk<KBX, KBE>(A, X, E, acc0, acc1, lane);
+      mma_chunk<KBX, KBE, NE>(A, X, E, acc0, acc1, lane);
     } else {
       acc0 = f32x4{0, 0, 0, 0};
       acc1 = f32x4{0, 0, 0, 0};
@@ -306,7 +306,7 @@ __device__ __forceinline__ void gemm_bwd(WStream& ws, const char* __restrict__ o
   const float4 dummy[4] = {};
   f16x8 bh[12], bl[12];
   float ginv = 1.0f;
-  if constexpr (P == NR_PREC_F16X3) ginv = make_b16<KBG, 0>(G, dummy, bh, bl);
+  if constexpr (P == NR_PREC_F16X3) ginv = make_b16<KBG, 0, 4>(G, dummy, bh, bl);
 #pragma unroll 1
   for (int c = 0; c < NBO / 2; ++c) {
     if (c + 1 < NBO / 2) ws.issue(op + (c + 1) * CB, CB);
@@ -320,7 +320,7 @@ __device__ __forceinline__ void gemm_bwd(WStream& ws, const char* __restrict__ o
     const float4* A = ws.buf();
     f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
     if constexpr (P == NR_PREC_FP32) {
-      mma_chunk<KBG, 0>(A, G, dummy, acc0, acc1, lane);
+      mma_chunk<KBG, 0, 4>(A, G, dummy, acc0, acc1, lane);
     } else {
       mma_chunk_h3<KBG / 2>(A, bh, bl, acc0, acc1, lane);
       const float inv = ginv * A[2 * KBG * 64 + 8].x;
@@ -623,6 +623,119 @@ __global__ __launch_bounds__(kThreads) void radiance_kernel(RadKArgs a) {
 }
 
 // =============================================================================================
+// NeRF++ background kernel (models/base.py:395-453, use_view_dirs=True, multires 10 on the 4-D
+// inverted-sphere input [x/r, 1/r], multires_view 4).  Plain nn.Linear layers, ReLU.
+// =============================================================================================
+struct NerfKArgs {
+  const char* packed;
+  NerfLayout L;
+  const float* x4;    // [P][4]
+  const float* vdir;  // view direction of point p: vdir[((p / vdiv) % vmod) * 3]
+  int64_t vdiv;
+  int64_t vmod;
+  int64_t P;
+  float* sigma;       // [P]
+  float* rgb;         // [P][3]
+};
+
+// Embedder(input_dim=4, multires=10): [x, sin(x 2^0), cos(x 2^0), ..., sin(x 2^9), cos(x 2^9)]
+__device__ __noinline__ float nerf_embed4(int f, float x0, float x1, float x2, float x3) {
+  auto comp = [&](int c) { return c == 0 ? x0 : (c == 1 ? x1 : (c == 2 ? x2 : x3)); };
+  if (f < 4) return comp(f);
+  const int fp = f - 4;
+  if (fp >= 80) return 0.0f;
+  const int band = fp >> 3, m = fp & 7;
+  const float v = fmul(comp(m & 3), (float)(1 << band));
+  return m < 4 ? sinf(v) : cosf(v);
+}
+
+template <int P>
+__global__ __launch_bounds__(kThreads) void nerf_kernel(NerfKArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kMaxChunkBytes];
+  WStream ws{smem, 1};
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  const NerfLayout& L = a.L;
+  const char* W = a.packed;
+  auto OP = [&](int i) { return W + L.op_off[i]; };
+  auto OPB = [&](int i) { return (int)L.op_bytes[i]; };
+  const float* wa = (const float*)(W + L.alpha_off);
+  const float* wr = (const float*)(W + L.rgb_off);
+
+  ws.issue(OP(N0), OPB(N0));
+  ws.flip();
+  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < a.P; base += (int64_t)gridDim.x * kPointsPerWG) {
+    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < a.P;
+    const int64_t p = base + wave * kTile + j;
+    const bool valid = p < a.P;
+    const int64_t pc = valid ? p : a.P - 1;
+    const float4 xin = *(const float4*)(a.x4 + pc * 4);
+    const int64_t pv = (pc / a.vdiv) % a.vmod;
+    const float v0 = a.vdir[pv * 3 + 0], v1 = a.vdir[pv * 3 + 1], v2 = a.vdir[pv * 3 + 2];
+    float4 E[6], V[2];
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const int f = 16 * b + 4 * g;
+      E[b] = make_float4(nerf_embed4(f + 0, xin.x, xin.y, xin.z, xin.w), nerf_embed4(f + 1, xin.x, xin.y, xin.z, xin.w),
+                         nerf_embed4(f + 2, xin.x, xin.y, xin.z, xin.w), nerf_embed4(f + 3, xin.x, xin.y, xin.z, xin.w));
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int f = 16 * b + 4 * g;
+      V[b] = make_float4(f + 0 < 27 ? embed_feature(f + 0, v0, v1, v2, 4) : 0.0f,
+                         f + 1 < 27 ? embed_feature(f + 1, v0, v1, v2, 4) : 0.0f,
+                         f + 2 < 27 ? embed_feature(f + 2, v0, v1, v2, 4) : 0.0f,
+                         f + 3 < 27 ? embed_feature(f + 3, v0, v1, v2, 4) : 0.0f);
+    }
+    float4 X[16], Y[16];
+    gemm_fwd<P, 0, 6, 16, ACT_RELU>(ws, OP(N0), OP(N1), OPB(N1), X, E, Y, nullptr, nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_RELU>(ws, OP(N1), OP(N2), OPB(N2), Y, E, X, nullptr, nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_RELU>(ws, OP(N2), OP(N3), OPB(N3), X, E, Y, nullptr, nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_RELU>(ws, OP(N3), OP(N4), OPB(N4), Y, E, X, nullptr, nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_RELU>(ws, OP(N4), OP(N5), OPB(N5), X, E, Y, nullptr, nullptr, false, lane);
+    // skip: cat([input_pts, h]) (base.py:431-432); K blocks packed as [h ; embedding]
+    gemm_fwd<P, 16, 6, 16, ACT_RELU>(ws, OP(N5), OP(N6), OPB(N6), Y, E, X, nullptr, nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_RELU>(ws, OP(N6), OP(N7), OPB(N7), X, E, Y, nullptr, nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_RELU>(ws, OP(N7), OP(NF), OPB(NF), Y, E, X, nullptr, nullptr, false, lane);
+    // sigma = alpha_linear(h) (no activation)
+    float part = 0.f;
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const float4 w = *(const float4*)(wa + 16 * b + 4 * g);
+      part = fmaf(X[b].x, w.x, part);
+      part = fmaf(X[b].y, w.y, part);
+      part = fmaf(X[b].z, w.z, part);
+      part = fmaf(X[b].w, w.w, part);
+    }
+    const float sigma = wave_sum4(part) + wa[256];
+    // feature = feature_linear(h); h = relu(views_linears[0](cat([feature, embed_view(v)])))
+    gemm_fwd<P, 16, 0, 16, ACT_NONE>(ws, OP(NF), OP(NV), OPB(NV), X, E, Y, nullptr, nullptr, false, lane);
+    gemm_fwd<P, 16, 2, 8, ACT_RELU>(ws, OP(NV), has_next ? OP(N0) : nullptr, OPB(N0), Y, V, X, nullptr, nullptr,
+                                    false, lane);
+    float r[3];
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      float q = 0.f;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const float4 w = *(const float4*)(wr + o * 128 + 16 * b + 4 * g);
+        q = fmaf(X[b].x, w.x, q);
+        q = fmaf(X[b].y, w.y, q);
+        q = fmaf(X[b].z, w.z, q);
+        q = fmaf(X[b].w, w.w, q);
+      }
+      r[o] = sigmoidf_ref(wave_sum4(q) + wr[3 * 128 + o]);
+    }
+    if (valid && g == 0) {
+      a.sigma[p] = sigma;
+      a.rgb[p * 3 + 0] = r[0];
+      a.rgb[p * 3 + 1] = r[1];
+      a.rgb[p * 3 + 2] = r[2];
+    }
+  }
+}
+
+// =============================================================================================
 // weight packing (device): effective W [rows][ld] -> chunk layout of one GEMM op
 // =============================================================================================
 // source element (W * scale) of A-element (ob, b, fi) of an op, or 0 for padding
@@ -771,6 +884,18 @@ int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t
     if (L.prec == NR_PREC_F16X3) hipLaunchKernelGGL((sdf_kernel<NR_PREC_F16X3, false>), dim3(grid), dim3(kThreads), 0, stream, a);
     else hipLaunchKernelGGL((sdf_kernel<NR_PREC_FP32, false>), dim3(grid), dim3(kThreads), 0, stream, a);
   }
+  NR_HIP_CHECK(hipGetLastError());
+  return NR_OK;
+}
+
+int launch_nerf(const NerfLayout& L, const void* packed, const float* x4, const float* vdir, int64_t vdiv,
+                int64_t vmod, int64_t P, float* sigma, float* rgb, hipStream_t stream) {
+  if (P <= 0) return NR_OK;
+  const int grid = grid_for(P);
+  NerfKArgs a{(const char*)packed, L, x4, vdir, vdiv, vmod, P, sigma, rgb};
+  ProfScope prof("nerf", (double)P, stream);
+  if (L.prec == NR_PREC_F16X3) hipLaunchKernelGGL((nerf_kernel<NR_PREC_F16X3>), dim3(grid), dim3(kThreads), 0, stream, a);
+  else hipLaunchKernelGGL((nerf_kernel<NR_PREC_FP32>), dim3(grid), dim3(kThreads), 0, stream, a);
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;
 }

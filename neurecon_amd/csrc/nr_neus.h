@@ -18,6 +18,11 @@ struct NeusChunk {
   float* pts; float* mids; float* dmid;
   float* sdf_f; float* nab_f;
   float* sdf_m; float* nab_m; float* feat_m; float* rad_m;
+  // NeRF++ background (N_out = 0: none); M = S-1+N_out samples, sample-major
+  int N_out;
+  float r_obj;
+  const float* t_out;
+  float* d_out; float* x4; float* sig_o; float* rad_o;
 };
 
 // outputs (ray-major); ray0 = index of the chunk's first ray in the full batch
@@ -25,12 +30,13 @@ struct NeusOut {
   int64_t ray0;
   float* rgb; float* depth; float* acc; float* normals;
   float* d_final; float* sdf; float* nablas; float* radiance; float* alpha; float* cdf; float* weights;
+  float* sigma_out; float* radiance_bg;
 };
 
 struct NeusPlan {
   int64_t Rc;
   size_t o_ro, o_rd, o_near, o_far, o_dv, o_sv, o_wtmp, o_dnew, o_snew, o_pts, o_mids, o_dmid;
-  size_t o_sdf_f, o_nab_f, o_sdf_m, o_nab_m, o_feat_m, o_rad_m, o_mlp;
+  size_t o_sdf_f, o_nab_f, o_sdf_m, o_nab_m, o_feat_m, o_rad_m, o_dout, o_x4, o_sigo, o_rado, o_mlp;
   size_t total;
 };
 
@@ -41,6 +47,8 @@ __global__ void neus_prologue(NeusChunk c, const float* rays_o, const float* ray
 __global__ void neus_upsample(NeusChunk c, int it, const float* u);
 __global__ void neus_points(NeusChunk c);
 __global__ void neus_composite(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd);
+__global__ void neus_outside_points(NeusChunk c);
+__global__ void neus_composite_outside(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd);
 __global__ void sample_pdf_kernel(const float* bins, const float* weights, int64_t R, int L, const float* u, int N,
                                   float* out);
 

@@ -15,7 +15,7 @@ __device__ __forceinline__ float4 load3(const float* p) { return make_float4(p[0
 
 // F.normalize(v, dim=-1): v / max(||v||_2, 1e-12)
 __device__ __forceinline__ void normalize3(float& x, float& y, float& z) {
-  const float n = sqrtf(fadd(fadd(fmul(x, x), fmul(y, y)), fmul(z, z)));
+  const float n = norm3_ref(x, y, z);
   const float d = fmaxf(n, 1e-12f);
   x = fdiv(x, d);
   y = fdiv(y, d);
@@ -261,6 +261,131 @@ __global__ void neus_composite(NeusChunk c, NeusOut o, float s_inv, int calc_nor
 }
 
 // ---------------------------------------------------------------------------------------------
+// NeRF++ background (neus.py:303-343)
+// ---------------------------------------------------------------------------------------------
+// d_vals_out = cat([d_mid, far / flip(linspace(0,1,N_out+2)[1:-1])]); x_out = [p / |p|, 1 / |p|]
+__global__ void neus_outside_points(NeusChunk c) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= c.R) return;
+  const int64_t R = c.R;
+  const int S1 = c.S - 1, M = S1 + c.N_out;
+  const float ox = c.ro[r * 3], oy = c.ro[r * 3 + 1], oz = c.ro[r * 3 + 2];
+  const float dx = c.rd[r * 3], dy = c.rd[r * 3 + 1], dz = c.rd[r * 3 + 2];
+  const float fr = c.far[r];
+  for (int k = 0; k < M; ++k) {
+    const float d = k < S1 ? c.dmid[(int64_t)k * R + r] : fdiv(fr, c.t_out[c.N_out - (k - S1)]);
+    const int64_t q = (int64_t)k * R + r;
+    c.d_out[q] = d;
+    const float px = fadd(ox, fmul(dx, d)), py = fadd(oy, fmul(dy, d)), pz = fadd(oz, fmul(dz, d));
+    const float rr = norm3_ref(px, py, pz);
+    *(float4*)(c.x4 + q * 4) = make_float4(fdiv(px, rr), fdiv(py, rr), fdiv(pz, rr), fdiv(1.0f, rr));
+  }
+}
+
+// F.softplus (beta 1, threshold 20)
+__device__ __forceinline__ float softplus1(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
+
+// compositing with the background merged in (neus.py:325-343, :346-380)
+__global__ void neus_composite_outside(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= c.R) return;
+  const int S = c.S, S1 = S - 1, M = S1 + c.N_out;
+  const int64_t R = c.R;
+  const int64_t ro = o.ray0 + r;
+  const float ox = c.ro[r * 3], oy = c.ro[r * 3 + 1], oz = c.ro[r * 3 + 2];
+  const float dx = c.rd[r * 3], dy = c.rd[r * 3 + 1], dz = c.rd[r * 3 + 2];
+  double T = 1.0, acc = 0.0, rgb0 = 0.0, rgb1 = 0.0, rgb2 = 0.0, n0 = 0.0, n1 = 0.0, n2 = 0.0;
+  float cprev = sigmoidf_ref(fmul(c.sdf_f[r], s_inv));
+  if (o.cdf) o.cdf[ro * S] = cprev;
+  const int Nn = M < S ? M : S;  // normals use min(#weights, #nablas) samples (neus.py:364-366)
+  for (int k = 0; k < M; ++k) {
+    const int64_t q = (int64_t)k * R + r;
+    const float dk = c.d_out[q];
+    const float dist = k + 1 < M ? fsub(c.d_out[q + R], dk) : 1e10f;
+    const float a_out = fsub(1.0f, expf(fmul(-softplus1(c.sig_o[q]), dist)));
+    float alpha, r0, r1, r2;
+    bool inside = false;
+    float a_in = 0.f;
+    if (k < S1) {
+      const float cn = sigmoidf_ref(fmul(c.sdf_f[(int64_t)(k + 1) * R + r], s_inv));
+      a_in = fmaxf(fdiv(fsub(cprev, cn), fadd(cprev, 1e-10f)), 0.0f);
+      if (o.cdf) o.cdf[ro * S + k + 1] = cn;
+      cprev = cn;
+      const float dm = c.dmid[q];
+      const float px = fadd(ox, fmul(dx, dm)), py = fadd(oy, fmul(dy, dm)), pz = fadd(oz, fmul(dz, dm));
+      inside = norm3_ref(px, py, pz) <= c.r_obj;
+    }
+    if (inside) {
+      alpha = a_in;
+      r0 = c.rad_m[q * 3 + 0]; r1 = c.rad_m[q * 3 + 1]; r2 = c.rad_m[q * 3 + 2];
+    } else {
+      alpha = a_out;
+      r0 = c.rad_o[q * 3 + 0]; r1 = c.rad_o[q * 3 + 1]; r2 = c.rad_o[q * 3 + 2];
+    }
+    const float w = fmul(alpha, (float)T);
+    T *= (double)fadd(fsub(1.0f, alpha), 1e-10f);
+    rgb0 += (double)fmul(w, r0);
+    rgb1 += (double)fmul(w, r1);
+    rgb2 += (double)fmul(w, r2);
+    acc += (double)w;
+    if (calc_normal && k < Nn) {
+      float x = c.nab_f[(int64_t)k * R * 3 + r * 3 + 0], y = c.nab_f[(int64_t)k * R * 3 + r * 3 + 1],
+            z = c.nab_f[(int64_t)k * R * 3 + r * 3 + 2];
+      normalize3(x, y, z);
+      n0 += (double)fmul(x, w);
+      n1 += (double)fmul(y, w);
+      n2 += (double)fmul(z, w);
+    }
+    c.wtmp[q] = w;
+    if (o.alpha) o.alpha[ro * M + k] = alpha;
+    if (o.weights) o.weights[ro * M + k] = w;
+    if (o.d_final) o.d_final[ro * M + k] = dk;
+    if (o.radiance) {
+      o.radiance[(ro * M + k) * 3 + 0] = r0;
+      o.radiance[(ro * M + k) * 3 + 1] = r1;
+      o.radiance[(ro * M + k) * 3 + 2] = r2;
+    }
+    if (o.sigma_out) o.sigma_out[ro * M + k] = c.sig_o[q];
+    if (o.radiance_bg) {
+      o.radiance_bg[(ro * M + k) * 3 + 0] = c.rad_o[q * 3 + 0];
+      o.radiance_bg[(ro * M + k) * 3 + 1] = c.rad_o[q * 3 + 1];
+      o.radiance_bg[(ro * M + k) * 3 + 2] = c.rad_o[q * 3 + 2];
+    }
+  }
+  const float accf = (float)acc;
+  const float denom = fadd(accf, 1e-10f);
+  double depth = 0.0;
+  for (int k = 0; k < M; ++k) {
+    const int64_t q = (int64_t)k * R + r;
+    depth += (double)fmul(fdiv(c.wtmp[q], denom), c.d_out[q]);
+  }
+  float q0 = (float)rgb0, q1 = (float)rgb1, q2 = (float)rgb2;
+  if (white_bkgd) {
+    const float bg = fsub(1.0f, accf);
+    q0 = fadd(q0, bg); q1 = fadd(q1, bg); q2 = fadd(q2, bg);
+  }
+  o.rgb[ro * 3 + 0] = q0;
+  o.rgb[ro * 3 + 1] = q1;
+  o.rgb[ro * 3 + 2] = q2;
+  o.depth[ro] = (float)depth;
+  o.acc[ro] = accf;
+  if (calc_normal && o.normals) {
+    o.normals[ro * 3 + 0] = (float)n0;
+    o.normals[ro * 3 + 1] = (float)n1;
+    o.normals[ro * 3 + 2] = (float)n2;
+  }
+  for (int i = 0; i < S; ++i) {
+    const int64_t q = (int64_t)i * R + r;
+    if (o.sdf) o.sdf[ro * S + i] = c.sdf_f[q];
+    if (o.nablas) {
+      o.nablas[(ro * S + i) * 3 + 0] = c.nab_f[q * 3 + 0];
+      o.nablas[(ro * S + i) * 3 + 1] = c.nab_f[q * 3 + 1];
+      o.nablas[(ro * S + i) * 3 + 2] = c.nab_f[q * 3 + 2];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // generic sample_pdf entry (rend_util.py:255-292), bins/weights ray-major [R][L], u [N]
 // ---------------------------------------------------------------------------------------------
 __global__ void sample_pdf_kernel(const float* __restrict__ bins, const float* __restrict__ weights, int64_t R, int L,
@@ -303,6 +428,12 @@ NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc) {
   p.o_nab_m = take((size_t)(S - 1) * Rc * 3);
   p.o_feat_m = take((size_t)(S - 1) * Rc * 256);
   p.o_rad_m = take((size_t)(S - 1) * Rc * 3);
+  const int M = S - 1 + a.N_outside;
+  p.o_wtmp = a.N_outside > 0 ? take((size_t)M * Rc) : p.o_wtmp;  // weights of all M samples
+  p.o_dout = take((size_t)(a.N_outside > 0 ? M : 1) * Rc);
+  p.o_x4 = take((size_t)(a.N_outside > 0 ? M : 1) * Rc * 4);
+  p.o_sigo = take((size_t)(a.N_outside > 0 ? M : 1) * Rc);
+  p.o_rado = take((size_t)(a.N_outside > 0 ? M : 1) * Rc * 3);
   p.o_mlp = off;
   p.total = off + nr_mlp_workspace_bytes(1);
   return p;

@@ -1,0 +1,366 @@
+// neurecon_amd — UNISURF render path for gfx950 (models/frameworks/unisurf.py:62-283 and
+// models/ray_casting.py:11-160, render mode: perturb=False, secant root finding).
+//
+// One thread per ray for the march / secant / sampling / compositing steps (sample-major state,
+// coalesced); the SDF and radiance MLPs run in the fused MFMA kernels.  The reference feeds
+// F.normalize(nablas) with torch's default dim=1 to the radiance net (unisurf.py:36): for batched
+// renders that normalises each gradient component over a whole batchify_query chunk of points
+// (train_util.py:23-71), which is reproduced here with a per-window fp64 reduction.
+#include "nr_common.h"
+#include "nr_mlp.h"
+#include "nr_unisurf.h"
+
+namespace nr {
+namespace {
+
+__device__ __forceinline__ float norm3f(float x, float y, float z) {
+  return norm3_ref(x, y, z);
+}
+
+// d_proposal = near * (1 - t) + far * t (ray_casting.py:79)
+__device__ __forceinline__ float lerp_ref(float a, float b, float t) { return fadd(fmul(a, fsub(1.0f, t)), fmul(b, t)); }
+
+// d_pred = -f_low * (d_high - d_low) / (f_high - f_low) + d_low (ray_casting.py:15, :29)
+__device__ __forceinline__ float secant(float d_lo, float f_lo, float d_hi, float f_hi) {
+  return fadd(fdiv(fmul(-f_lo, fsub(d_hi, d_lo)), fsub(f_hi, f_lo)), d_lo);
+}
+
+enum { kDLo, kFLo, kDHi, kFHi, kDPred, kHit, kCross, kFree, kSec };
+
+}  // namespace
+
+// normalised directions, near/far on the sphere of interest (rend_util.py:167-185), the too-close
+// threshold (unisurf.py:128) and the N_steps march points (ray_casting.py:74-83)
+__global__ void uni_prologue(UniChunk c, const float* __restrict__ rays_o, const float* __restrict__ rays_d) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= c.R) return;
+  const float ox = rays_o[r * 3 + 0], oy = rays_o[r * 3 + 1], oz = rays_o[r * 3 + 2];
+  float dx = rays_d[r * 3 + 0], dy = rays_d[r * 3 + 1], dz = rays_d[r * 3 + 2];
+  const float nn = fmaxf(norm3f(dx, dy, dz), 1e-12f);
+  dx = fdiv(dx, nn);
+  dy = fdiv(dy, nn);
+  dz = fdiv(dz, nn);
+  c.ro[r * 3 + 0] = ox; c.ro[r * 3 + 1] = oy; c.ro[r * 3 + 2] = oz;
+  c.rd[r * 3 + 0] = dx; c.rd[r * 3 + 1] = dy; c.rd[r * 3 + 2] = dz;
+  const float mid = -fadd(fadd(fmul(ox, dx), fmul(oy, dy)), fmul(oz, dz));
+  float nr = fmaxf(fsub(mid, c.r_interest), 0.0f);
+  float fr = fmaxf(fadd(mid, c.r_interest), c.r_interest);
+  if (!__builtin_isnan(c.near_bypass)) nr = c.near_bypass;
+  if (!__builtin_isnan(c.far_bypass)) fr = c.far_bypass;
+  c.near[r] = nr;
+  c.far[r] = fr;
+  c.thr[r] = fadd(nr, fmul(fsub(fr, nr), c.too_close));
+  for (int i = 0; i < c.N_steps; ++i) {
+    const float d = lerp_ref(nr, fr, c.t_march[i]);
+    const int64_t q = (int64_t)i * c.R + r;
+    c.pts_m[q * 3 + 0] = fadd(ox, fmul(d, dx));
+    c.pts_m[q * 3 + 1] = fadd(oy, fmul(d, dy));
+    c.pts_m[q * 3 + 2] = fadd(oz, fmul(d, dz));
+  }
+}
+
+// first sign change of the march (ray_casting.py:89-131) and the first secant estimate
+__global__ void uni_root(UniChunk c) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= c.R) return;
+  const int N = c.N_steps;
+  const float tau = c.logit_tau;
+  float v0 = fsub(c.sm[r], tau);
+  const bool first_free = v0 > 0.0f;
+  int idx = -1;
+  float vi = v0, vn = 0.0f;
+  for (int i = 0; i + 1 < N; ++i) {
+    vn = fsub(c.sm[(int64_t)(i + 1) * c.R + r], tau);
+    if (fmul(vi, vn) < 0.0f) {  // torch.sign(v_i * v_{i+1}) == -1: the earliest one wins the min
+      idx = i;
+      break;
+    }
+    vi = vn;
+  }
+  const bool crossing = idx >= 0;
+  const bool hit = crossing && vi > 0.0f && first_free;
+  float* s = c.sec + (int64_t)r * kSec;
+  s[kHit] = hit ? 1.0f : 0.0f;
+  s[kCross] = crossing ? 1.0f : 0.0f;
+  s[kFree] = first_free ? 1.0f : 0.0f;
+  float dp = 1.0f;
+  if (hit) {
+    const float nr = c.near[r], fr = c.far[r];
+    const int i1 = idx + 1 < N ? idx + 1 : N - 1;
+    const float d_hi = lerp_ref(nr, fr, c.t_march[idx]), f_hi = vi;
+    const float d_lo = lerp_ref(nr, fr, c.t_march[i1]), f_lo = vn;
+    s[kDLo] = d_lo; s[kFLo] = f_lo; s[kDHi] = d_hi; s[kFHi] = f_hi;
+    dp = secant(d_lo, f_lo, d_hi, f_hi);
+  }
+  s[kDPred] = dp;
+  c.pts_s[r * 3 + 0] = fadd(c.ro[r * 3 + 0], fmul(dp, c.rd[r * 3 + 0]));
+  c.pts_s[r * 3 + 1] = fadd(c.ro[r * 3 + 1], fmul(dp, c.rd[r * 3 + 1]));
+  c.pts_s[r * 3 + 2] = fadd(c.ro[r * 3 + 2], fmul(dp, c.rd[r * 3 + 2]));
+}
+
+// one secant step (ray_casting.py:17-29) given f at the current estimate
+__global__ void uni_secant(UniChunk c, int last) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= c.R) return;
+  float* s = c.sec + (int64_t)r * kSec;
+  if (s[kHit] == 0.0f) return;
+  const float dp = s[kDPred];
+  const float fm = fsub(c.ss[r], c.logit_tau);
+  if (fm < 0.0f) {
+    s[kDLo] = dp;
+    s[kFLo] = fm;
+  } else {
+    s[kDHi] = dp;
+    s[kFHi] = fm;
+  }
+  const float dn = secant(s[kDLo], s[kFLo], s[kDHi], s[kFHi]);
+  s[kDPred] = dn;
+  if (!last) {
+    c.pts_s[r * 3 + 0] = fadd(c.ro[r * 3 + 0], fmul(dn, c.rd[r * 3 + 0]));
+    c.pts_s[r * 3 + 1] = fadd(c.ro[r * 3 + 1], fmul(dn, c.rd[r * 3 + 1]));
+    c.pts_s[r * 3 + 2] = fadd(c.ro[r * 3 + 2], fmul(dn, c.rd[r * 3 + 2]));
+  }
+}
+
+// surface outputs, interval + free-space samples, sorted (unisurf.py:135-203)
+__global__ void uni_samples(UniChunk c, UniOut o) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= c.R) return;
+  const float* s = c.sec + (int64_t)r * kSec;
+  const bool hit = s[kHit] != 0.0f, crossing = s[kCross] != 0.0f, first_free = s[kFree] != 0.0f;
+  const float dpred = s[kDPred];
+  const float nr = c.near[r], fr = c.far[r];
+  const float ox = c.ro[r * 3], oy = c.ro[r * 3 + 1], oz = c.ro[r * 3 + 2];
+  const float dx = c.rd[r * 3], dy = c.rd[r * 3 + 1], dz = c.rd[r * 3 + 2];
+  float dout = hit ? dpred : fr;  // fill_inf=False (unisurf.py:143)
+  if (!first_free) dout = 0.0f;
+  const int64_t rg = o.ray0 + r;
+  if (o.surface_points) {
+    o.surface_points[rg * 3 + 0] = hit ? fadd(ox, fmul(dpred, dx)) : 1.0f;
+    o.surface_points[rg * 3 + 1] = hit ? fadd(oy, fmul(dpred, dy)) : 1.0f;
+    o.surface_points[rg * 3 + 2] = hit ? fadd(oz, fmul(dpred, dz)) : 1.0f;
+  }
+  if (o.mask_surface) o.mask_surface[rg] = hit ? 1 : 0;
+  const float dc = fmaxf(fminf(dout, fr), nr);
+  if (o.depth_surface) o.depth_surface[rg] = dc;
+  const float d_up = fminf(fadd(dc, c.interval), fr);
+  const float d_lo = fmaxf(fsub(dc, c.interval), nr);
+  float d_lo2 = fmaxf(d_lo, c.thr[r]);
+  if (!crossing) d_lo2 = fr;
+  if (d_lo2 < 1e-10f) d_lo2 = fr;
+  // merge the two (ascending) runs; an insertion pass below repairs rounding-level disorder
+  const int nf = c.N_free, nq = c.N_query, P = c.P;
+  const int64_t R = c.R;
+  float* da = c.d_all + r;
+  int jf = 0, jq = 0;
+  float vf = nf > 0 ? lerp_ref(nr, d_lo2, c.t_free[0]) : 0.0f;
+  float vq = nq > 0 ? lerp_ref(d_lo, d_up, c.t_query[0]) : 0.0f;
+  for (int k = 0; k < P; ++k) {
+    const bool take_f = jq >= nq || (jf < nf && vf <= vq);
+    if (take_f) {
+      da[k * R] = vf;
+      ++jf;
+      if (jf < nf) vf = lerp_ref(nr, d_lo2, c.t_free[jf]);
+    } else {
+      da[k * R] = vq;
+      ++jq;
+      if (jq < nq) vq = lerp_ref(d_lo, d_up, c.t_query[jq]);
+    }
+  }
+  for (int k = 1; k < P; ++k) {
+    const float v = da[k * R];
+    int j = k - 1;
+    while (j >= 0 && da[j * R] > v) {
+      da[(j + 1) * R] = da[j * R];
+      --j;
+    }
+    da[(j + 1) * R] = v;
+  }
+  for (int k = 0; k < P; ++k) {
+    const float d = da[k * R];
+    const int64_t q = k * R + r;
+    c.pts_f[q * 3 + 0] = fadd(ox, fmul(dx, d));
+    c.pts_f[q * 3 + 1] = fadd(oy, fmul(dy, d));
+    c.pts_f[q * 3 + 2] = fadd(oz, fmul(dz, d));
+  }
+}
+
+// sum of squares of every nabla component over each F.normalize window (one block per window):
+// window w = points q in [w*netchunk, (w+1)*netchunk) of the chunk's ray-major flat order q = r*P+s
+__global__ void uni_window_ss(UniChunk c) {
+  __shared__ double red[3][256];
+  const int64_t w = blockIdx.x, t = threadIdx.x;
+  const int64_t n = (int64_t)c.R * c.P;
+  const int64_t q0 = w * c.netchunk, q1 = min(n, q0 + c.netchunk);
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  for (int64_t q = q0 + t; q < q1; q += blockDim.x) {
+    const int64_t r = q / c.P, s = q % c.P;
+    const int64_t p = s * c.R + r;
+    const double x = c.nab_f[p * 3 + 0], y = c.nab_f[p * 3 + 1], z = c.nab_f[p * 3 + 2];
+    a0 += x * x;
+    a1 += y * y;
+    a2 += z * z;
+  }
+  red[0][t] = a0;
+  red[1][t] = a1;
+  red[2][t] = a2;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if (t < o) {
+      red[0][t] += red[0][t + o];
+      red[1][t] += red[1][t + o];
+      red[2][t] += red[2][t + o];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    c.wss[w * 3 + 0] = red[0][0];
+    c.wss[w * 3 + 1] = red[1][0];
+    c.wss[w * 3 + 2] = red[2][0];
+  }
+}
+
+// normals fed to the radiance net: F.normalize(nablas) (unisurf.py:36). mode 0: per point (an
+// unbatched call normalises over the xyz dim); mode 1: per window and component.
+__global__ void uni_normalize(UniChunk c, int mode) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = (int64_t)c.R * c.P;
+  if (p >= n) return;
+  const float x = c.nab_f[p * 3 + 0], y = c.nab_f[p * 3 + 1], z = c.nab_f[p * 3 + 2];
+  if (mode == 0) {
+    const float d = fmaxf(norm3f(x, y, z), 1e-12f);
+    c.nrm_f[p * 3 + 0] = fdiv(x, d);
+    c.nrm_f[p * 3 + 1] = fdiv(y, d);
+    c.nrm_f[p * 3 + 2] = fdiv(z, d);
+  } else {
+    const int64_t r = p % c.R, s = p / c.R;
+    const int64_t w = (r * c.P + s) / c.netchunk;
+    c.nrm_f[p * 3 + 0] = fdiv(x, fmaxf((float)sqrt(c.wss[w * 3 + 0]), 1e-12f));
+    c.nrm_f[p * 3 + 1] = fdiv(y, fmaxf((float)sqrt(c.wss[w * 3 + 1]), 1e-12f));
+    c.nrm_f[p * 3 + 2] = fdiv(z, fmaxf((float)sqrt(c.wss[w * 3 + 2]), 1e-12f));
+  }
+}
+
+// occupancy-logit alpha compositing (unisurf.py:53-62, :206-244)
+__global__ void uni_composite(UniChunk c, UniOut o, int calc_normal, int white_bkgd) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= c.R) return;
+  const int P = c.P;
+  const int64_t R = c.R;
+  const int64_t rg = o.ray0 + r;
+  double T = 1.0, a_acc = 0.0, a0 = 0.0, a1 = 0.0, a2 = 0.0, n0 = 0.0, n1 = 0.0, n2 = 0.0;
+  for (int i = 0; i < P; ++i) {
+    const int64_t q = i * R + r;
+    const float lg = c.sdf_f[q];
+    const float odds = expf(-lg);
+    const float alpha = fdiv(odds, fadd(1.0f, odds));
+    const float w = fmul(alpha, (float)T);
+    T *= (double)fadd(fsub(1.0f, alpha), 1e-10f);
+    a0 += (double)fmul(w, c.rad_f[q * 3 + 0]);
+    a1 += (double)fmul(w, c.rad_f[q * 3 + 1]);
+    a2 += (double)fmul(w, c.rad_f[q * 3 + 2]);
+    a_acc += (double)w;
+    const float nx = c.nab_f[q * 3 + 0], ny = c.nab_f[q * 3 + 1], nz = c.nab_f[q * 3 + 2];
+    if (calc_normal) {
+      const float d = fmaxf(norm3f(nx, ny, nz), 1e-12f);
+      n0 += (double)fmul(fdiv(nx, d), w);
+      n1 += (double)fmul(fdiv(ny, d), w);
+      n2 += (double)fmul(fdiv(nz, d), w);
+    }
+    if (o.alpha) o.alpha[rg * P + i] = alpha;
+    if (o.weights) o.weights[rg * P + i] = w;
+    if (o.sdf) o.sdf[rg * P + i] = lg;
+    if (o.nablas) {
+      o.nablas[(rg * P + i) * 3 + 0] = nx;
+      o.nablas[(rg * P + i) * 3 + 1] = ny;
+      o.nablas[(rg * P + i) * 3 + 2] = nz;
+    }
+    if (o.radiance) {
+      o.radiance[(rg * P + i) * 3 + 0] = c.rad_f[q * 3 + 0];
+      o.radiance[(rg * P + i) * 3 + 1] = c.rad_f[q * 3 + 1];
+      o.radiance[(rg * P + i) * 3 + 2] = c.rad_f[q * 3 + 2];
+    }
+  }
+  const float accf = (float)a_acc;
+  const float denom = fadd(accf, 1e-10f);
+  double dep = 0.0;
+  T = 1.0;
+  for (int i = 0; i < P; ++i) {  // second pass: weights normalised by their float sum
+    const int64_t q = i * R + r;
+    const float odds = expf(-c.sdf_f[q]);
+    const float alpha = fdiv(odds, fadd(1.0f, odds));
+    const float w = fmul(alpha, (float)T);
+    T *= (double)fadd(fsub(1.0f, alpha), 1e-10f);
+    dep += (double)fmul(fdiv(w, denom), c.d_all[q]);
+  }
+  float q0 = (float)a0, q1 = (float)a1, q2 = (float)a2;
+  if (white_bkgd) {
+    const float bg = fsub(1.0f, accf);
+    q0 = fadd(q0, bg); q1 = fadd(q1, bg); q2 = fadd(q2, bg);
+  }
+  o.rgb[rg * 3 + 0] = q0;
+  o.rgb[rg * 3 + 1] = q1;
+  o.rgb[rg * 3 + 2] = q2;
+  o.depth[rg] = (float)dep;
+  o.acc[rg] = accf;
+  if (calc_normal && o.normals) {
+    o.normals[rg * 3 + 0] = (float)n0;
+    o.normals[rg * 3 + 1] = (float)n1;
+    o.normals[rg * 3 + 2] = (float)n2;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// workspace plan and chunking
+// ---------------------------------------------------------------------------------------------
+static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static constexpr int64_t kUniMaxChunk = 65536;
+
+// rays per internal chunk: in window mode (batched call) a chunk never straddles a normalisation
+// window, i.e. it is the reference's ray chunk (rayschunk) or a whole number of windows of it
+int64_t unisurf_chunk_rays(const NrUnisurfArgs& a) {
+  const int64_t P = a.N_query + a.N_freespace;
+  const int64_t per_b = a.rays_per_batch > 0 ? a.rays_per_batch : a.n_rays;
+  if (a.normal_mode == 1) {
+    const int64_t rc = a.rayschunk < per_b ? a.rayschunk : per_b;
+    if (rc <= kUniMaxChunk) return rc > 0 ? rc : 1;
+    if (a.netchunk % P != 0) return -1;
+    const int64_t rw = a.netchunk / P;  // rays per window
+    const int64_t k = kUniMaxChunk / rw;
+    return k > 0 ? k * rw : -1;
+  }
+  return a.n_rays < kUniMaxChunk ? (a.n_rays > 0 ? a.n_rays : 1) : kUniMaxChunk;
+}
+
+UniPlan unisurf_plan(const NrUnisurfArgs& a, int64_t Rc) {
+  UniPlan p{};
+  const int P = a.N_query + a.N_freespace;
+  p.Rc = Rc;
+  p.max_windows = a.normal_mode == 1 ? (Rc * P + a.netchunk - 1) / a.netchunk : 1;
+  size_t off = 0;
+  auto take = [&](size_t words) { size_t o = off; off = align_up(off + words * 4); return o; };
+  p.o_ro = take(Rc * 3);
+  p.o_rd = take(Rc * 3);
+  p.o_near = take(Rc);
+  p.o_far = take(Rc);
+  p.o_thr = take(Rc);
+  p.o_ptsm = take((size_t)a.N_steps * Rc * 3);
+  p.o_sm = take((size_t)a.N_steps * Rc);
+  p.o_sec = take((size_t)Rc * 9);
+  p.o_ptss = take(Rc * 3);
+  p.o_ss = take(Rc);
+  p.o_dall = take((size_t)P * Rc);
+  p.o_ptsf = take((size_t)P * Rc * 3);
+  p.o_sdff = take((size_t)P * Rc);
+  p.o_nabf = take((size_t)P * Rc * 3);
+  p.o_featf = take((size_t)P * Rc * 256);
+  p.o_nrmf = take((size_t)P * Rc * 3);
+  p.o_radf = take((size_t)P * Rc * 3);
+  p.o_wss = take((size_t)p.max_windows * 6);
+  p.o_mlp = off;
+  p.total = off + nr_mlp_workspace_bytes(1);
+  return p;
+}
+
+}  // namespace nr

@@ -90,7 +90,7 @@ __device__ __forceinline__ void point_at(const VolChunk& c, int r, float d, floa
 }
 
 __device__ __forceinline__ float norm3(float x, float y, float z) {
-  return sqrtf(fadd(fadd(fmul(x, x), fmul(y, y)), fmul(z, z)));
+  return norm3_ref(x, y, z);
 }
 
 // VolSDF.forward_surface (volsdf.py:310-315): min(sdf, r_bg - |x|) with the builtin background

@@ -74,8 +74,6 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
         raise NotImplementedError('neurecon_amd: stratified (perturb=True) sampling is a training feature')
     if upsample_algo != 'official_solution':
         raise NotImplementedError(f'neurecon_amd: upsample_algo={upsample_algo!r} not native yet')
-    if N_outside > 0:
-        raise NotImplementedError('neurecon_amd: NeRF++ background (N_outside>0) not native yet')
     if not use_view_dirs:
         raise NotImplementedError('neurecon_amd: use_view_dirs=False not supported')
     dev = rays_o.device
@@ -89,6 +87,7 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     n = ro.shape[0]
     n_up = N_importance // N_upsample_iters if N_upsample_iters > 0 else 0
     S = N_samples + N_upsample_iters * n_up
+    M = S - 1 + N_outside  # samples after the NeRF++ merge (neus.py:325-343)
 
     sdf_desc, sdf_packed = model.implicit_surface.nr_packed(dev)
     rad_desc, rad_packed = model.radiance_net.nr_packed(dev)
@@ -103,9 +102,12 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     det = {}
     if detailed_output:
         det = dict(implicit_nablas=torch.empty(n, S, 3, device=dev), implicit_surface=torch.empty(n, S, device=dev),
-                   radiance=torch.empty(n, S - 1, 3, device=dev), alpha=torch.empty(n, S - 1, device=dev),
-                   cdf=torch.empty(n, S, device=dev), visibility_weights=torch.empty(n, S - 1, device=dev),
-                   d_final=torch.empty(n, S - 1, device=dev))
+                   radiance=torch.empty(n, M, 3, device=dev), alpha=torch.empty(n, M, device=dev),
+                   cdf=torch.empty(n, S, device=dev), visibility_weights=torch.empty(n, M, device=dev),
+                   d_final=torch.empty(n, M, device=dev))
+        if N_outside > 0:
+            det['sigma_out'] = torch.empty(n, M, device=dev)
+            det['radiance_out'] = torch.empty(n, M, 3, device=dev)
     a = L.NrNeusArgs()
     a.rays_o, a.rays_d, a.n_rays = L.ptr(ro), L.ptr(rd), n
     a.sdf, a.sdf_packed = ctypes.pointer(sdf_desc), L.ptr(sdf_packed)
@@ -125,6 +127,14 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     a.alpha_out = L.ptr(det.get('alpha'))
     a.cdf_out = L.ptr(det.get('cdf'))
     a.weights_out = L.ptr(det.get('visibility_weights'))
+    if N_outside > 0:
+        if not hasattr(model, 'nerf_outside'):
+            raise ValueError('N_outside > 0 needs a model built with use_outside_nerf=True')
+        nerf_desc, nerf_packed = model.nerf_outside.nr_packed(dev)
+        t_out = _linspace_table(N_outside + 2, dev)
+        a.nerf, a.nerf_packed = ctypes.pointer(nerf_desc), L.ptr(nerf_packed)
+        a.N_outside, a.t_outside = N_outside, L.ptr(t_out)
+        a.sigma_out, a.radiance_bg_out = L.ptr(det.get('sigma_out')), L.ptr(det.get('radiance_out'))
     lib = L.lib()
     ws_bytes = lib.nr_neus_workspace_bytes(ctypes.byref(a))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
@@ -138,11 +148,14 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     if detailed_output:
         ret['implicit_nablas'] = det['implicit_nablas'].reshape(*prefix, S, 3)
         ret['implicit_surface'] = det['implicit_surface'].reshape(*prefix, S)
-        ret['radiance'] = det['radiance'].reshape(*prefix, S - 1, 3)
-        ret['alpha'] = det['alpha'].reshape(*prefix, S - 1)
+        ret['radiance'] = det['radiance'].reshape(*prefix, M, 3)
+        ret['alpha'] = det['alpha'].reshape(*prefix, M)
         ret['cdf'] = det['cdf'].reshape(*prefix, S)
-        ret['visibility_weights'] = det['visibility_weights'].reshape(*prefix, S - 1)
-        ret['d_final'] = det['d_final'].reshape(*prefix, S - 1)
+        ret['visibility_weights'] = det['visibility_weights'].reshape(*prefix, M)
+        ret['d_final'] = det['d_final'].reshape(*prefix, M)
+        if N_outside > 0:
+            ret['sigma_out'] = det['sigma_out'].reshape(*prefix, M)
+            ret['radiance_out'] = det['radiance_out'].reshape(*prefix, M, 3)
     return ret['rgb'], ret['depth_volume'], ret
 
 

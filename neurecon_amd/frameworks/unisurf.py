@@ -1,0 +1,223 @@
+"""UNISURF framework: same API as the reference's models/frameworks/unisurf.py, render path on HIP.
+
+`volume_render(rays_o, rays_d, model, **kw) -> (rgb, depth, extras)` keeps the reference's
+signature, argument meaning, output shapes and extras keys (unisurf.py:62-283).  The whole path
+(256-step march + secant root finding, interval / free-space sampling, occupancy MLP with nablas,
+F.normalize'd normals into the radiance net, alpha compositing) runs in libnrhip.so
+(`nr_unisurf_render`).
+"""
+import copy
+import ctypes
+from collections import OrderedDict
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _lib as L
+from .. import rend_util
+from ..base import ImplicitSurface, RadianceNet, _no_training
+from .neus import _linspace_table
+
+N_STEPS = 256        # ray_casting.py:49 (root_finding_surface_points default)
+N_SECANT_STEPS = 8   # ray_casting.py:52
+
+
+class UNISURF(nn.Module):
+    """unisurf.py:16-62 (parameter tree and names identical: implicit_surface.*, radiance_net.*)."""
+
+    def __init__(self, input_ch=3, W_geo_feat=-1, surface_cfg=dict(), radiance_cfg=dict()):
+        super().__init__()
+        self.implicit_surface = ImplicitSurface(input_ch=input_ch, W_geo_feat=W_geo_feat, **surface_cfg)
+        if W_geo_feat < 0:
+            W_geo_feat = self.implicit_surface.W
+        self.radiance_net = RadianceNet(W_geo_feat=W_geo_feat, **radiance_cfg)
+
+    def forward(self, x, view_dirs):
+        occ, nablas, geometry_feature = self.implicit_surface.forward_with_nablas(x)
+        normals = F.normalize(nablas)  # default dim=1, exactly as unisurf.py:36
+        radiances = self.radiance_net.forward(x, view_dirs, normals, geometry_feature)
+        return radiances, occ, nablas
+
+    @staticmethod
+    def get_surface_from_opacity(opacity, eps=1e-4):
+        if isinstance(opacity, torch.Tensor):
+            opacity = torch.clamp(opacity, min=eps, max=1 - eps)
+            imp_surface = torch.log(opacity / (1 - opacity))
+        else:
+            opacity = np.clip(opacity, a_min=eps, a_max=1 - eps)
+            imp_surface = np.log(opacity / (1 - opacity))
+        return (-1.) * imp_surface
+
+    @staticmethod
+    def get_opacity_from_surface(imp_surface):
+        if isinstance(imp_surface, torch.Tensor):
+            odds = torch.exp(-1. * imp_surface)
+        else:
+            odds = np.exp(-1. * imp_surface)
+        return odds / (1 + odds)
+
+
+def volume_render(rays_o, rays_d, model, batched=False, batched_info={}, calc_normal=False, logit_tau=0.0,
+                  use_view_dirs=True, method='secant', rayschunk=65536, netchunk=1048576, white_bkgd=False,
+                  near_bypass=None, far_bypass=None, detailed_output=True, show_progress=False,
+                  radius_of_interest=4.0, perturb=False, interval=1.0, too_close_threshold=0.1, N_query=64,
+                  N_freespace=32, **dummy_kwargs):
+    """unisurf.py:62-283, render mode.  rays_o/rays_d: [(B,) N_rays, 3]."""
+    L.require_gpu(rays_o, 'rays_o')
+    _no_training(model)
+    if perturb:
+        raise NotImplementedError('neurecon_amd: stratified (perturb=True) sampling is a training feature')
+    if method != 'secant':
+        raise NotImplementedError(f'neurecon_amd: root finding method={method!r} not native')
+    if not use_view_dirs:
+        raise NotImplementedError('neurecon_amd: use_view_dirs=False not supported')
+    dev = rays_o.device
+    if batched:
+        B, N = rays_d.shape[0], rays_d.reshape(rays_d.shape[0], -1, 3).shape[1]
+        prefix = [B, -1]
+    else:
+        N = rays_d.reshape(-1, 3).shape[0]
+        prefix = [-1]
+    ro = rays_o.reshape(-1, 3).float().contiguous()
+    rd = rays_d.reshape(-1, 3).float().contiguous()
+    n = ro.shape[0]
+    P = N_query + N_freespace
+
+    sdf_desc, sdf_packed = model.implicit_surface.nr_packed(dev)
+    rad_desc, rad_packed = model.radiance_net.nr_packed(dev)
+    t_march = _linspace_table(N_STEPS, dev)
+    t_query = _linspace_table(N_query, dev)
+    t_free = _linspace_table(N_freespace, dev)
+
+    rgb = torch.empty(n, 3, device=dev)
+    depth = torch.empty(n, device=dev)
+    acc = torch.empty(n, device=dev)
+    normals = torch.empty(n, 3, device=dev) if calc_normal else None
+    det = {}
+    if detailed_output:
+        det = dict(surface_points=torch.empty(n, 3, device=dev), mask_surface=torch.empty(n, dtype=torch.bool,
+                                                                                           device=dev),
+                   depth_surface=torch.empty(n, device=dev), radiance=torch.empty(n, P, 3, device=dev),
+                   implicit_surface=torch.empty(n, P, device=dev), implicit_nablas=torch.empty(n, P, 3, device=dev),
+                   alpha=torch.empty(n, P, device=dev), visibility_weights=torch.empty(n, P, device=dev))
+    a = L.NrUnisurfArgs()
+    a.rays_o, a.rays_d, a.n_rays, a.rays_per_batch = L.ptr(ro), L.ptr(rd), n, N
+    a.sdf, a.sdf_packed = ctypes.pointer(sdf_desc), L.ptr(sdf_packed)
+    a.rad, a.rad_packed = ctypes.pointer(rad_desc), L.ptr(rad_packed)
+    a.logit_tau = float(logit_tau)
+    a.radius_of_interest, a.interval = float(radius_of_interest), float(interval)
+    a.too_close_threshold = float(too_close_threshold)
+    a.near_bypass = float('nan') if near_bypass is None else float(near_bypass)
+    a.far_bypass = float('nan') if far_bypass is None else float(far_bypass)
+    a.N_steps, a.N_secant_steps, a.N_query, a.N_freespace = N_STEPS, N_SECANT_STEPS, N_query, N_freespace
+    # F.normalize(nablas) with dim=1: per point for [chunk, 3] inputs, per window for [B, chunk, 3]
+    a.normal_mode = 1 if batched else 0
+    a.rayschunk, a.netchunk = int(rayschunk), int(netchunk)
+    a.calc_normal, a.white_bkgd = int(bool(calc_normal)), int(bool(white_bkgd))
+    a.t_march, a.t_query, a.t_free = L.ptr(t_march), L.ptr(t_query), L.ptr(t_free)
+    a.rgb, a.depth, a.acc, a.normals = L.ptr(rgb), L.ptr(depth), L.ptr(acc), L.ptr(normals)
+    a.surface_points = L.ptr(det.get('surface_points'))
+    a.mask_surface = L.ptr(det.get('mask_surface'))
+    a.depth_surface = L.ptr(det.get('depth_surface'))
+    a.radiance_out = L.ptr(det.get('radiance'))
+    a.sdf_out = L.ptr(det.get('implicit_surface'))
+    a.nablas_out = L.ptr(det.get('implicit_nablas'))
+    a.alpha_out = L.ptr(det.get('alpha'))
+    a.weights_out = L.ptr(det.get('visibility_weights'))
+    lib = L.lib()
+    ws_bytes = lib.nr_unisurf_workspace_bytes(ctypes.byref(a))
+    if ws_bytes == 0:
+        raise NotImplementedError('neurecon_amd: ' + lib.nr_last_error().decode())
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    a.workspace, a.workspace_bytes = L.ptr(ws), ws_bytes
+    L.check(lib.nr_unisurf_render(ctypes.byref(a), L.stream_of(dev)))
+
+    ret = OrderedDict([('rgb', rgb.reshape(*prefix, 3)), ('depth_volume', depth.reshape(prefix)),
+                       ('mask_volume', acc.reshape(prefix))])
+    if calc_normal:
+        ret['normals_volume'] = normals.reshape(*prefix, 3)
+    if detailed_output:
+        ret['surface_points'] = det['surface_points'].reshape(*prefix, 3)
+        ret['mask_surface'] = det['mask_surface'].reshape(prefix)
+        ret['depth_surface'] = det['depth_surface'].reshape(prefix)
+        ret['radiance'] = det['radiance'].reshape(*prefix, P, 3)
+        ret['implicit_surface'] = det['implicit_surface'].reshape(*prefix, P)
+        ret['implicit_nablas'] = det['implicit_nablas'].reshape(*prefix, P, 3)
+        ret['alpha'] = det['alpha'].reshape(*prefix, P)
+        ret['visibility_weights'] = det['visibility_weights'].reshape(*prefix, P)
+    return ret['rgb'], ret['depth_volume'], ret
+
+
+class SingleRenderer(nn.Module):
+    """unisurf.py:286-291."""
+
+    def __init__(self, model):
+        super().__init__()
+        self.model = model
+
+    def forward(self, rays_o, rays_d, **kwargs):
+        return volume_render(rays_o, rays_d, self.model, **kwargs)
+
+
+class Trainer(nn.Module):
+    """unisurf.py:294-351.  Training needs the backward of the render kernels; the
+    render call raises while grad is enabled."""
+
+    def __init__(self, model, device_ids=[0], batched=True):
+        super().__init__()
+        self.model = model
+        self.renderer = SingleRenderer(model)
+        if len(device_ids) > 1:
+            self.renderer = nn.DataParallel(self.renderer, device_ids=device_ids, dim=1 if batched else 0)
+        self.device = device_ids[0]
+
+    def forward(self, args, indices, model_input, ground_truth, render_kwargs_train, it, device='cuda'):
+        intrinsics = model_input['intrinsics'].to(device)
+        c2w = model_input['c2w'].to(device)
+        rays_o, rays_d, select_inds = rend_util.get_rays(c2w, intrinsics, render_kwargs_train['H'],
+                                                         render_kwargs_train['W'], N_rays=args.data.N_rays)
+        interval = max(args.training.delta_max * np.exp(-it * args.training.delta_beta), args.training.delta_min)
+        return self.renderer(rays_o, rays_d, interval=interval, detailed_output=True, **render_kwargs_train)
+
+
+def get_model(args):
+    """unisurf.py:354-404 (same config keys and defaults)."""
+    from ..config import as_cfg
+    args = as_cfg(args)
+    model_config = {'W_geo_feat': args.model.setdefault('W_geometry_feature', 256)}
+    surface_cfg = {
+        'use_siren': args.model.surface.setdefault('use_siren', args.model.setdefault('use_siren', False)),
+        'embed_multires': args.model.surface.setdefault('embed_multires', 6),
+        'radius_init': args.model.surface.setdefault('radius_init', 1.0),
+        'geometric_init': args.model.surface.setdefault('geometric_init', True),
+        'D': args.model.surface.setdefault('D', 8),
+        'W': args.model.surface.setdefault('W', 256),
+        'skips': args.model.surface.setdefault('skips', [4]),
+    }
+    radiance_cfg = {
+        'use_siren': args.model.radiance.setdefault('use_siren', args.model.setdefault('use_siren', False)),
+        'embed_multires': args.model.radiance.setdefault('embed_multires', -1),
+        'embed_multires_view': args.model.radiance.setdefault('embed_multires_view', -1),
+        'use_view_dirs': args.model.radiance.setdefault('use_view_dirs', True),
+        'D': args.model.radiance.setdefault('D', 4),
+        'W': args.model.radiance.setdefault('W', 256),
+        'skips': args.model.radiance.setdefault('skips', []),
+    }
+    model_config['surface_cfg'] = surface_cfg
+    model_config['radiance_cfg'] = radiance_cfg
+    model = UNISURF(**model_config)
+    render_kwargs_train = {
+        'batched': True,
+        'tau': args.model.tau,
+        'perturb': args.model.get('perturb', True),
+        'white_bkgd': args.model.get('white_bkgd', False),
+        'logit_tau': model.get_surface_from_opacity(args.model.tau),
+        'radius_of_interest': args.model.obj_bounding_radius,
+    }
+    render_kwargs_test = copy.deepcopy(render_kwargs_train)
+    render_kwargs_test['rayschunk'] = args.data.val_rayschunk
+    render_kwargs_test['perturb'] = False
+    trainer = Trainer(model, device_ids=args.device_ids, batched=render_kwargs_train['batched'])
+    return model, trainer, render_kwargs_train, render_kwargs_test, trainer.renderer

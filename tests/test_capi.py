@@ -53,10 +53,9 @@ def test_descriptor_validation_without_gpu(lib):
 
 def test_struct_sizes(lib):
     from neurecon_amd import _lib
-    # NrNeusArgs: 7 pointers+i64, 4 floats, 5 ints (+pad), 2 table ptrs, 11 output ptrs, ws ptr + size
     assert ctypes.sizeof(_lib.NrSdfDesc) == 24
     assert ctypes.sizeof(_lib.NrRadDesc) == 24
-    assert ctypes.sizeof(_lib.NrNeusArgs) == 7 * 8 + 4 * 4 + 5 * 4 + 4 + 2 * 8 + 11 * 8 + 2 * 8
+    assert ctypes.sizeof(_lib.NrNerfDesc) == 28
 
 
 def test_cpu_tensors_are_rejected():
@@ -67,3 +66,27 @@ def test_cpu_tensors_are_rejected():
     from neurecon_amd.frameworks.neus import NeuS
     with pytest.raises(RuntimeError, match='GPU'):
         volume_render(torch.zeros(1, 4, 3), torch.ones(1, 4, 3), None)
+
+
+def test_struct_layouts_match_the_c_compiler(tmp_path):
+    """Every ctypes mirror struct has the size and field offsets gcc computes from the header."""
+    import subprocess
+    from neurecon_amd import _lib
+    structs = [getattr(_lib, n) for n in dir(_lib) if n.startswith('Nr') and isinstance(getattr(_lib, n), type)
+               and issubclass(getattr(_lib, n), ctypes.Structure)]
+    assert len(structs) >= 7  # 3 descriptors, 3 render-argument blocks, kernel stats
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "neurecon_hip.h"', 'int main(void) {']
+    for S in structs:
+        lines.append(f'printf("{S.__name__} %zu\\n", sizeof({S.__name__}));')
+        for f, _ in S._fields_:
+            lines.append(f'printf("{S.__name__}.{f} %zu\\n", offsetof({S.__name__}, {f}));')
+    lines.append('return 0; }')
+    src = tmp_path / 'layout.c'
+    src.write_text('\n'.join(lines))
+    exe = tmp_path / 'layout'
+    subprocess.check_call(['gcc', '-I', os.path.join(ROOT, 'include'), str(src), '-o', str(exe)])
+    got = dict(l.split() for l in subprocess.check_output([str(exe)]).decode().splitlines())
+    for S in structs:
+        assert int(got[S.__name__]) == ctypes.sizeof(S), S.__name__
+        for f, _ in S._fields_:
+            assert int(got[f'{S.__name__}.{f}']) == getattr(S, f).offset, (S.__name__, f)

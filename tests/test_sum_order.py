@@ -69,3 +69,15 @@ def test_row_sum_order_matches_torch():
                 x[rng.randint(n)] = 1.0
             ref = torch.sum(torch.from_numpy(x).reshape(1, n), -1, keepdim=True).numpy()[0, 0]
             assert aten_row_sum(x) == ref, (n, trial)
+
+
+def test_norm3_matches_torch_fma_order():
+    """nr_common.h norm3_ref: torch's CPU x.norm(dim=-1) of 3-vectors == sqrt(fma(z,z,fma(y,y,x*x)))."""
+    torch.manual_seed(0)
+    x = (torch.randn(200000, 3) * 3).float()
+    ref = x.norm(dim=-1).numpy()
+    d = x.numpy().astype(np.float64)
+    fma = lambda p, q, r: (p * q + r).astype(np.float32).astype(np.float64)  # exact product, one rounding
+    sq = (d[:, 0] * d[:, 0]).astype(np.float32).astype(np.float64)
+    got = np.sqrt(fma(d[:, 2], d[:, 2], fma(d[:, 1], d[:, 1], sq))).astype(np.float32)
+    assert (got == ref).all()

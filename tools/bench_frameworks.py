@@ -1,0 +1,73 @@
+"""Timing of the VolSDF and UNISURF render paths (secondary §8 rows) on the config-(b) camera:
+4096 rays, seeded random-init weights, render mode.  Prints per-kernel device time (HIP events)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'tests'))
+sys.path.insert(0, os.path.join(ROOT, 'tests', 'golden'))
+
+
+def rays(dev):
+    import weightgen as wg
+    from neurecon_amd import rend_util
+    H, W, f, dist = wg.CAMERAS['b']
+    c2w = wg.look_at_c2w(dist)[None].to(dev)
+    K = wg.intrinsics(f, H, W)[None].to(dev)
+    ro, rd, _ = rend_util.get_rays(c2w, K, H, W)
+    return ro, rd
+
+
+def timeit(fn, steps, warmup):
+    from neurecon_amd import _lib as L
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    L.profile_read()
+    L.profile_enable(True)
+    t = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t) / steps
+    L.profile_enable(False)
+    return dt, L.profile_read()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--precision', default='f16x3')
+    args = ap.parse_args()
+    import weightgen as wg
+    from helpers import unisurf_model, volsdf_model
+    dev = torch.device('cuda')
+    ro, rd = rays(dev)
+    out = {}
+    from neurecon_amd.frameworks import unisurf, volsdf
+    mv = volsdf_model(wg.volsdf_state(seed=2, beta_init=0.1), 0.1, precision=args.precision)
+    kw = dict(near=0.0, far=6.0, batched=True, calc_normal=True, detailed_output=False, N_samples=128,
+              N_importance=64, max_upsample_steps=6)
+    with torch.no_grad():
+        dt, ks = timeit(lambda: volsdf.volume_render(ro, rd, mv, **kw), args.steps, args.warmup)
+        _, _, ex = volsdf.volume_render(ro, rd, mv, **dict(kw, detailed_output=True))
+    it = ex['iter_usage'].flatten()
+    out['volsdf'] = {'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3, 'kernels': ks,
+                     'iter_usage': {str(k): int((it == k).sum()) for k in it.unique().tolist()}}
+    mu = unisurf_model(wg.unisurf_state(seed=3), precision=args.precision)
+    with torch.no_grad():
+        dt, ks = timeit(lambda: unisurf.volume_render(ro, rd, mu, batched=True, calc_normal=True,
+                                                      detailed_output=False, logit_tau=0.0), args.steps, args.warmup)
+    out['unisurf'] = {'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3, 'kernels': ks}
+    print(json.dumps(out, default=str))
+
+
+if __name__ == '__main__':
+    main()
