@@ -45,6 +45,11 @@ extern "C" {
 #define NR_PREC_FP32 0  /* v_mfma_f32_16x16x4_f32: exact fp32 products                        */
 #define NR_PREC_F16X3 1 /* split-fp16 x3 on v_mfma_f32_16x16x32_f16 (hi*hi + hi*lo + lo*hi)     */
 
+/* NeuS upsampling algorithms (models/frameworks/neus.py:213-279) */
+#define NR_UPSAMPLE_OFFICIAL 0
+#define NR_UPSAMPLE_DIRECT_USE 1
+#define NR_UPSAMPLE_DIRECT_MORE 2
+
 int nr_version(void);
 const char* nr_last_error(void);
 
@@ -161,6 +166,14 @@ typedef struct {
   const float* t_outside; /* torch.linspace(0, 1, N_outside + 2) */
   float* sigma_out;       /* [n_rays, M]    raw NeRF sigma ('sigma_out')      */
   float* radiance_bg_out; /* [n_rays, M, 3] NeRF radiance  ('radiance_out')  */
+  /* upsampling algorithm (neus.py:213-279): NR_UPSAMPLE_OFFICIAL (N_upsample_iters rounds of
+   * N_importance/N_upsample_iters, u_fine = linspace(0,1,N_importance/N_upsample_iters)), or
+   * DIRECT_USE / DIRECT_MORE (one sample_pdf of N_importance over the coarse / N_nograd_samples
+   * uniform depths with s = 1/fixed_s_recp, u_fine = linspace(0,1,N_importance)) */
+  int upsample_algo;
+  float fixed_s;          /* 1 / fixed_s_recp (direct algorithms)     */
+  int N_nograd_samples;   /* direct_more                               */
+  const float* t_nograd;  /* torch.linspace(0, 1, N_nograd_samples)  */
   void* workspace;
   size_t workspace_bytes;
 } NrNeusArgs;

@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get('NR_LIB', os.path.join(HERE, 'libnrhip.so'))
 
 PREC_FP32 = 0
 PREC_F16X3 = 1
+UPSAMPLE = {'official_solution': 0, 'direct_use': 1, 'direct_more': 2}
 
 _c_p = ctypes.c_void_p
 _c_i = ctypes.c_int
@@ -51,6 +52,7 @@ class NrNeusArgs(ctypes.Structure):
         ('alpha_out', _c_p), ('cdf_out', _c_p), ('weights_out', _c_p),
         ('nerf', ctypes.POINTER(NrNerfDesc)), ('nerf_packed', _c_p), ('N_outside', _c_i), ('t_outside', _c_p),
         ('sigma_out', _c_p), ('radiance_bg_out', _c_p),
+        ('upsample_algo', _c_i), ('fixed_s', _c_f), ('N_nograd_samples', _c_i), ('t_nograd', _c_p),
         ('workspace', _c_p), ('workspace_bytes', _c_sz),
     ]
 

@@ -142,13 +142,18 @@ static size_t scratch_bytes() {
 // ---------------------------------------------------------------------------------------------
 static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int R, hipStream_t st) {
   char* ws = (char*)a.workspace;
-  const int n_up = a.N_upsample_iters > 0 ? a.N_importance / a.N_upsample_iters : 0;
+  const bool direct = a.upsample_algo != NR_UPSAMPLE_OFFICIAL;
+  const int n_up = direct ? 0 : (a.N_upsample_iters > 0 ? a.N_importance / a.N_upsample_iters : 0);
   NeusChunk c{};
   c.R = R;
   c.N_samples = a.N_samples;
   c.n_up = n_up;
-  c.n_iters = a.N_upsample_iters;
-  c.S = a.N_samples + a.N_upsample_iters * n_up;
+  c.n_iters = direct ? 0 : a.N_upsample_iters;
+  c.S = direct ? a.N_samples + a.N_importance : a.N_samples + a.N_upsample_iters * n_up;
+  c.n_imp = a.N_importance;
+  c.n_nog = a.upsample_algo == NR_UPSAMPLE_DIRECT_MORE ? a.N_nograd_samples : 0;
+  c.fixed_s = a.fixed_s;
+  c.t_nog = a.t_nograd;
   auto F = [&](size_t o) { return (float*)(ws + o); };
   c.ro = F(pl.o_ro); c.rd = F(pl.o_rd); c.near = F(pl.o_near); c.far = F(pl.o_far);
   c.dv = F(pl.o_dv); c.sv = F(pl.o_sv); c.wtmp = F(pl.o_wtmp); c.dnew = F(pl.o_dnew); c.snew = F(pl.o_snew);
@@ -159,6 +164,7 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   c.r_obj = a.obj_bounding_radius;
   c.t_out = a.t_outside;
   c.d_out = F(pl.o_dout); c.x4 = F(pl.o_x4); c.sig_o = F(pl.o_sigo); c.rad_o = F(pl.o_rado);
+  c.pts_nog = F(pl.o_ptsn); c.s_nog = F(pl.o_sn);
   void* mlp_ws = ws + pl.o_mlp;
   const size_t mlp_bytes = a.workspace_bytes - pl.o_mlp;
   const SdfLayout SL = sdf_layout(*a.sdf);
@@ -172,11 +178,25 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
                      a.obj_bounding_radius, a.near_bypass, a.far_bypass);
   }
   NR_HIP_CHECK(hipGetLastError());
-  // coarse SDF (no grad, neus.py:251)
-  if ((rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)a.N_samples * R, c.sv, nullptr, nullptr, a.sdf->multires,
+  // coarse SDF (no grad, neus.py:220 / :251); direct_more uses its own uniform depths instead
+  if (a.upsample_algo != NR_UPSAMPLE_DIRECT_MORE &&
+      (rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)a.N_samples * R, c.sv, nullptr, nullptr, a.sdf->multires,
                        nullptr, 0, st)))
     return rc;
-  for (int it = 0; it < a.N_upsample_iters; ++it) {
+  if (a.upsample_algo == NR_UPSAMPLE_DIRECT_MORE) {  // SDF at N_nograd_samples uniform depths
+    hipLaunchKernelGGL(neus_nograd_points, grd, blk, 0, st, c);
+    NR_HIP_CHECK(hipGetLastError());
+    if ((rc = launch_sdf(SL, a.sdf_packed, c.pts_nog, (int64_t)c.n_nog * R, c.s_nog, nullptr, nullptr,
+                         a.sdf->multires, nullptr, 0, st)))
+      return rc;
+  }
+  if (direct) {
+    ProfScope prof("neus_upsample", (double)R, st);
+    hipLaunchKernelGGL(neus_direct_upsample, grd, blk, 0, st, c, (int)(a.upsample_algo == NR_UPSAMPLE_DIRECT_MORE),
+                       a.u_fine);
+  }
+  NR_HIP_CHECK(hipGetLastError());
+  for (int it = 0; it < c.n_iters; ++it) {
     {
       ProfScope prof("neus_upsample", (double)R, st);
       hipLaunchKernelGGL(neus_upsample, grd, blk, 0, st, c, it, a.u_fine);
@@ -598,7 +618,14 @@ int nr_neus_render(const NrNeusArgs* a, void* stream) {
     if ((rc = check_nerf_desc(a->nerf))) return rc;
     NR_REQUIRE(a->nerf_packed && a->t_outside, NR_ERR_ARG, "nr_neus_render: N_outside > 0 needs the NeRF++ net");
   }
-  if (a->N_upsample_iters > 0) {
+  NR_REQUIRE(a->upsample_algo >= NR_UPSAMPLE_OFFICIAL && a->upsample_algo <= NR_UPSAMPLE_DIRECT_MORE, NR_ERR_ARG,
+             "nr_neus_render: unknown upsample_algo");
+  if (a->upsample_algo != NR_UPSAMPLE_OFFICIAL) {
+    NR_REQUIRE(a->N_importance >= 1 && a->u_fine && a->fixed_s > 0.f, NR_ERR_ARG,
+               "nr_neus_render: direct upsampling needs N_importance >= 1, u_fine and fixed_s > 0");
+    NR_REQUIRE(a->upsample_algo != NR_UPSAMPLE_DIRECT_MORE || (a->N_nograd_samples >= 2 && a->t_nograd), NR_ERR_ARG,
+               "nr_neus_render: direct_more needs N_nograd_samples >= 2 and t_nograd");
+  } else if (a->N_upsample_iters > 0) {
     const int n_up = a->N_importance / a->N_upsample_iters;
     NR_REQUIRE(n_up >= 1 && n_up <= kMaxUp && a->u_fine, NR_ERR_UNSUPPORTED,
                "nr_neus_render: N_importance/N_upsample_iters must be in [1, 32]");

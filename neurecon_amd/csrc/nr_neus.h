@@ -23,6 +23,12 @@ struct NeusChunk {
   float r_obj;
   const float* t_out;
   float* d_out; float* x4; float* sig_o; float* rad_o;
+  // direct_use / direct_more upsampling
+  int n_imp;      // N_importance drawn in one sample_pdf
+  int n_nog;      // N_nograd_samples (direct_more)
+  float fixed_s;
+  const float* t_nog;
+  float* pts_nog; float* s_nog;
 };
 
 // outputs (ray-major); ray0 = index of the chunk's first ray in the full batch
@@ -36,7 +42,7 @@ struct NeusOut {
 struct NeusPlan {
   int64_t Rc;
   size_t o_ro, o_rd, o_near, o_far, o_dv, o_sv, o_wtmp, o_dnew, o_snew, o_pts, o_mids, o_dmid;
-  size_t o_sdf_f, o_nab_f, o_sdf_m, o_nab_m, o_feat_m, o_rad_m, o_dout, o_x4, o_sigo, o_rado, o_mlp;
+  size_t o_sdf_f, o_nab_f, o_sdf_m, o_nab_m, o_feat_m, o_rad_m, o_dout, o_x4, o_sigo, o_rado, o_ptsn, o_sn, o_mlp;
   size_t total;
 };
 
@@ -48,6 +54,8 @@ __global__ void neus_upsample(NeusChunk c, int it, const float* u);
 __global__ void neus_points(NeusChunk c);
 __global__ void neus_composite(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd);
 __global__ void neus_outside_points(NeusChunk c);
+__global__ void neus_nograd_points(NeusChunk c);
+__global__ void neus_direct_upsample(NeusChunk c, int more, const float* u);
 __global__ void neus_composite_outside(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd);
 __global__ void sample_pdf_kernel(const float* bins, const float* weights, int64_t R, int L, const float* u, int N,
                                   float* out);

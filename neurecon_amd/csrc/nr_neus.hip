@@ -261,6 +261,82 @@ __global__ void neus_composite(NeusChunk c, NeusOut o, float s_inv, int calc_nor
 }
 
 // ---------------------------------------------------------------------------------------------
+// 'direct_use' / 'direct_more' upsampling (neus.py:215-243): one sample_pdf of N_importance over
+// the visibility weights of the coarse (or N_nograd_samples uniform) depths, s = 1/fixed_s_recp
+// ---------------------------------------------------------------------------------------------
+__global__ void neus_nograd_points(NeusChunk c) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= c.R) return;
+  const int64_t R = c.R;
+  const float ox = c.ro[r * 3], oy = c.ro[r * 3 + 1], oz = c.ro[r * 3 + 2];
+  const float dx = c.rd[r * 3], dy = c.rd[r * 3 + 1], dz = c.rd[r * 3 + 2];
+  const float nr = c.near[r], fr = c.far[r];
+  for (int k = 0; k < c.n_nog; ++k) {
+    const float t = c.t_nog[k];
+    const float d = fadd(fmul(nr, fsub(1.0f, t)), fmul(fr, t));
+    const int64_t q = (int64_t)k * R + r;
+    c.pts_nog[q * 3 + 0] = fadd(ox, fmul(d, dx));
+    c.pts_nog[q * 3 + 1] = fadd(oy, fmul(d, dy));
+    c.pts_nog[q * 3 + 2] = fadd(oz, fmul(d, dz));
+  }
+}
+
+__global__ void neus_direct_upsample(NeusChunk c, int more, const float* __restrict__ u) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= c.R) return;
+  const int64_t R = c.R;
+  const int L = more ? c.n_nog : c.N_samples;
+  const float nr = c.near[r], fr = c.far[r];
+  // bins: the coarse depths (dv) or the nograd depths (recomputed, never stored)
+  float* bins = c.dv + r;
+  if (more) {
+    bins = c.d_out + r;  // scratch column of >= n_nog floats
+    for (int k = 0; k < L; ++k) {
+      const float t = c.t_nog[k];
+      bins[(int64_t)k * R] = fadd(fmul(nr, fsub(1.0f, t)), fmul(fr, t));
+    }
+  }
+  const float* sdf = more ? c.s_nog + r : c.sv + r;
+  // sdf_to_w (neus.py:37-70): logistic cdf, alpha = max((c_i - c_i+1)/(c_i + 1e-10), 0), cumprod
+  double T = 1.0;
+  float cprev = sigmoidf_ref(fmul(sdf[0], c.fixed_s));
+  for (int i = 0; i < L - 1; ++i) {
+    const float cn = sigmoidf_ref(fmul(sdf[(int64_t)(i + 1) * R], c.fixed_s));
+    const float alpha = fmaxf(fdiv(fsub(cprev, cn), fadd(cprev, 1e-10f)), 0.0f);
+    c.wtmp[(int64_t)i * R + r] = fmul(alpha, (float)T);
+    T *= (double)fadd(fsub(1.0f, alpha), 1e-10f);
+    cprev = cn;
+  }
+  const float* wr = c.wtmp + r;
+  const float total = aten_row_sum(L - 1, [&](int i) { return fadd(wr[(int64_t)i * R], 1e-5f); });
+  float* dn = c.dnew + r;
+  sample_pdf_ray(bins, wr, R, L, total, u, c.n_imp, dn, R);
+  // sort(cat([d_coarse, d_fine])) (neus.py:227-228): insertion-sort the new column, merge in place
+  const int n = c.n_imp;
+  for (int k = 1; k < n; ++k) {
+    const float v = dn[(int64_t)k * R];
+    int j = k - 1;
+    while (j >= 0 && dn[(int64_t)j * R] > v) {
+      dn[(int64_t)(j + 1) * R] = dn[(int64_t)j * R];
+      --j;
+    }
+    dn[(int64_t)(j + 1) * R] = v;
+  }
+  int i = c.N_samples - 1, j = n - 1;
+  for (int k = c.N_samples + n - 1; k >= 0 && j >= 0; --k) {
+    const float di = i >= 0 ? c.dv[(int64_t)i * R + r] : 0.f;
+    const float dj = dn[(int64_t)j * R];
+    if (i >= 0 && di > dj) {
+      c.dv[(int64_t)k * R + r] = di;
+      --i;
+    } else {
+      c.dv[(int64_t)k * R + r] = dj;
+      --j;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // NeRF++ background (neus.py:303-343)
 // ---------------------------------------------------------------------------------------------
 // d_vals_out = cat([d_mid, far / flip(linspace(0,1,N_out+2)[1:-1])]); x_out = [p / |p|, 1 / |p|]
@@ -404,8 +480,10 @@ static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc) {
   NeusPlan p{};
+  const bool direct = a.upsample_algo != NR_UPSAMPLE_OFFICIAL;
   const int n_up0 = a.N_upsample_iters > 0 ? a.N_importance / a.N_upsample_iters : 0;
-  const int S = a.N_samples + a.N_upsample_iters * n_up0;
+  const int S = direct ? a.N_samples + a.N_importance : a.N_samples + a.N_upsample_iters * n_up0;
+  const int n_nog = a.upsample_algo == NR_UPSAMPLE_DIRECT_MORE ? a.N_nograd_samples : 0;
   p.Rc = Rc;
   size_t off = 0;
   auto take = [&](size_t floats) { size_t o = off; off = align_up(off + floats * 4); return o; };
@@ -415,8 +493,8 @@ NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc) {
   p.o_far = take(Rc);
   p.o_dv = take((size_t)S * Rc);
   p.o_sv = take((size_t)S * Rc);
-  p.o_wtmp = take((size_t)S * Rc);
-  const int n_up = a.N_upsample_iters > 0 ? a.N_importance / a.N_upsample_iters : 0;
+  p.o_wtmp = take((size_t)(S > n_nog ? S : n_nog) * Rc);
+  const int n_up = direct ? a.N_importance : (a.N_upsample_iters > 0 ? a.N_importance / a.N_upsample_iters : 0);
   p.o_dnew = take((size_t)(n_up > 0 ? n_up : 1) * Rc);
   p.o_snew = take((size_t)(n_up > 0 ? n_up : 1) * Rc);
   p.o_pts = take((size_t)S * Rc * 3);
@@ -430,10 +508,12 @@ NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc) {
   p.o_rad_m = take((size_t)(S - 1) * Rc * 3);
   const int M = S - 1 + a.N_outside;
   p.o_wtmp = a.N_outside > 0 ? take((size_t)M * Rc) : p.o_wtmp;  // weights of all M samples
-  p.o_dout = take((size_t)(a.N_outside > 0 ? M : 1) * Rc);
+  p.o_dout = take((size_t)(a.N_outside > 0 ? (M > n_nog ? M : n_nog) : (n_nog > 0 ? n_nog : 1)) * Rc);
   p.o_x4 = take((size_t)(a.N_outside > 0 ? M : 1) * Rc * 4);
   p.o_sigo = take((size_t)(a.N_outside > 0 ? M : 1) * Rc);
   p.o_rado = take((size_t)(a.N_outside > 0 ? M : 1) * Rc * 3);
+  p.o_ptsn = take((size_t)(n_nog > 0 ? n_nog : 1) * Rc * 3);
+  p.o_sn = take((size_t)(n_nog > 0 ? n_nog : 1) * Rc);
   p.o_mlp = off;
   p.total = off + nr_mlp_workspace_bytes(1);
   return p;

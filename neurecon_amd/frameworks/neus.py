@@ -72,8 +72,9 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     _no_training(model)
     if perturb:
         raise NotImplementedError('neurecon_amd: stratified (perturb=True) sampling is a training feature')
-    if upsample_algo != 'official_solution':
-        raise NotImplementedError(f'neurecon_amd: upsample_algo={upsample_algo!r} not native yet')
+    if upsample_algo not in L.UPSAMPLE:
+        raise NotImplementedError(upsample_algo)
+    direct = upsample_algo != 'official_solution'
     if not use_view_dirs:
         raise NotImplementedError('neurecon_amd: use_view_dirs=False not supported')
     dev = rays_o.device
@@ -85,8 +86,12 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     ro = rays_o.reshape(-1, 3).float().contiguous()
     rd = rays_d.reshape(-1, 3).float().contiguous()
     n = ro.shape[0]
-    n_up = N_importance // N_upsample_iters if N_upsample_iters > 0 else 0
-    S = N_samples + N_upsample_iters * n_up
+    if direct:  # one sample_pdf of N_importance (neus.py:215-243)
+        n_up = N_importance
+        S = N_samples + N_importance
+    else:
+        n_up = N_importance // N_upsample_iters if N_upsample_iters > 0 else 0
+        S = N_samples + N_upsample_iters * n_up
     M = S - 1 + N_outside  # samples after the NeRF++ merge (neus.py:325-343)
 
     sdf_desc, sdf_packed = model.implicit_surface.nr_packed(dev)
@@ -119,6 +124,11 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     a.N_samples, a.N_importance, a.N_upsample_iters = N_samples, N_importance, N_upsample_iters
     a.calc_normal, a.white_bkgd = int(bool(calc_normal)), int(bool(white_bkgd))
     a.t_coarse, a.u_fine = L.ptr(t_coarse), L.ptr(u_fine)
+    a.upsample_algo = L.UPSAMPLE[upsample_algo]
+    a.fixed_s = 1. / fixed_s_recp
+    if upsample_algo == 'direct_more':
+        t_nograd = _linspace_table(N_nograd_samples, dev)
+        a.N_nograd_samples, a.t_nograd = N_nograd_samples, L.ptr(t_nograd)
     a.rgb, a.depth, a.acc, a.normals = L.ptr(rgb), L.ptr(depth), L.ptr(acc), L.ptr(normals)
     a.d_final = L.ptr(det.get('d_final'))
     a.sdf_out = L.ptr(det.get('implicit_surface'))
