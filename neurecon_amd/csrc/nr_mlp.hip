@@ -24,12 +24,17 @@ namespace nr {
 using lds_ptr = __attribute__((address_space(3))) void*;
 
 // ---------------------------------------------------------------------------------------------
-// LDS weight stream: 2 buffers of kMaxChunkBytes, filled by LDS-DMA (global_load_lds, 16 B/lane)
+// LDS weight stream: a ring of kRing chunk buffers filled by LDS-DMA (global_load_lds, 16 B/lane),
+// issued kRing-1 = 2 chunks ahead of the chunk being computed
 // ---------------------------------------------------------------------------------------------
-// The DMA is issued from inline asm so that hipcc does not treat it as a pending LDS store:
-// with the builtin, hipcc puts `s_waitcnt vmcnt(0)` in front of the next ds_read, i.e. every chunk
-// would wait for the *next* chunk's weights before computing (no overlap).  Completion is
-// counted by hand: vmcnt(0) + barrier in flip(), one chunk after the issue.
+// The DMA is issued from inline asm so that hipcc does not treat it as a pending LDS store
+// (with the builtin it puts `s_waitcnt vmcnt(0)` in front of the next ds_read, i.e. every chunk
+// would wait for the newest DMA).  Completion is counted by hand: at the end of chunk c, flip()
+// waits until only the DMA instructions of chunk c+2 (issued last) may still be outstanding --
+// vmcnt retires in issue order on gfx9 -- then barriers, so chunk c+1 has landed for all waves.
+// Everything a chunk needs from global memory besides the weights (the softplus' slab of the
+// reverse pass) also travels by LDS-DMA, so no compiler-visible load is ever waited on behind
+// an in-flight weight DMA.
 __device__ __forceinline__ void glds16(const char* gsrc, uint32_t lds_addr) {
   unsigned keep;
   asm volatile(
@@ -43,21 +48,110 @@ __device__ __forceinline__ void glds16(const char* gsrc, uint32_t lds_addr) {
       : "memory");
 }
 
-struct WStream {
-  char* lds;
-  int cur;
-  __device__ __forceinline__ void issue(const char* gsrc, int bytes) {
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint32_t base = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)lds) +
-                          (uint32_t)((cur ^ 1) * kMaxChunkBytes);
-    for (int off = wave * 1024; off < bytes; off += kThreads * 16)
-      glds16(gsrc + off + lane * 16, __builtin_amdgcn_readfirstlane(base + off));
+// LDS-DMA with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane offset: keeps address
+// math out of the (full) VGPR file -- a spilled address would be reloaded with a vmcnt(0) that
+// also waits for every in-flight weight DMA
+__device__ __forceinline__ void glds16s(const char* sbase, uint32_t voff, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds_addr)
+      : "memory");
+}
+
+// a pointer every lane of the wave agrees on, forced into SGPRs
+template <class T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (T*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
+// s_waitcnt vmcnt(n) for a runtime n (the immediate must be a constant)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
   }
-  __device__ __forceinline__ const float4* buf() const { return (const float4*)(lds + cur * kMaxChunkBytes); }
+}
+
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)p);
+}
+
+constexpr int kRing = 3;
+constexpr int kSlabChunk = kWaves * 2 * 64 * 16;  // softplus' of 2 blocks for every wave: 16 KB
+
+template <int CBMAX>
+struct WStream {
+  char* lds;   // kRing x CBMAX weight buffers
+  char* slab;  // 2 x kSlabChunk staged softplus' values (reverse pass), or null
+  int cur;     // ring slot of the chunk being computed
+  int pend;    // DMA instructions of the newest issued chunk (this wave)
+  int ecur;    // slab slot of the chunk being computed
+  __device__ __forceinline__ static int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+  __device__ __forceinline__ int dma(const char* gsrc, int bytes, int slot) {
+#ifdef NR_EXP_NO_DMA  // timing experiment only: weights are not streamed (results are garbage)
+    return 0;
+#endif
+    const int wave = wave_id();
+    const uint32_t voff = (threadIdx.x & 63) * 16;
+    const char* g = uniform_ptr(gsrc);
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_u32(lds) + (uint32_t)(slot * CBMAX));
+    int n = 0;
+    for (int off = wave * 1024; off < bytes; off += kThreads * 16, ++n) glds16s(g + off, voff, base + off);
+    return n;
+  }
+  // chunks 0 and 1 of the stream; returns once chunk 0 is in LDS for every wave
+  __device__ __forceinline__ void start(const char* g0, int b0, const char* g1, int b1) {
+    cur = 0;
+    ecur = 0;
+    dma(g0, b0, 0);
+    pend = dma(g1, b1, 1);
+    wait_vmcnt(pend);
+    __syncthreads();
+  }
+  // the chunk two ahead of the current one: the last VMEM of a chunk
+  __device__ __forceinline__ void issue(const char* gsrc, int bytes) { pend = dma(gsrc, bytes, (cur + 2) % kRing); }
+  __device__ __forceinline__ void none() { pend = 0; }
+  // softplus' blocks (b, b+1) of this wave's slab for the NEXT chunk (before issue())
+  __device__ __forceinline__ void slab_next(const float4* e, int b) {
+#ifndef NR_EXP_NO_ELOAD
+    const int wave = wave_id();
+    const uint32_t voff = (threadIdx.x & 63) * 16;
+    const char* g = (const char*)uniform_ptr(e + b * 64);
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_u32(slab) + (uint32_t)((ecur ^ 1) * kSlabChunk + wave * 2048));
+    glds16s(g, voff, base);
+    glds16s(g + 1024, voff, base + 1024);
+#endif
+  }
+  // ... or for the CURRENT chunk, waiting for it (once per tile, before the first reverse op)
+  __device__ __forceinline__ void slab_now(const float4* e, int b) {
+    ecur ^= 1;
+    slab_next(e, b);
+    ecur ^= 1;
+    wait_vmcnt(0);
+  }
+  __device__ __forceinline__ const float4* slab_cur() const {
+    return (const float4*)(slab + ecur * kSlabChunk + wave_id() * 2048);
+  }
+  __device__ __forceinline__ const float4* buf() const { return (const float4*)(lds + cur * CBMAX); }
   __device__ __forceinline__ void flip() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA for the next chunk landed
-    __syncthreads();                                   // ... and every other wave's
-    cur ^= 1;
+    wait_vmcnt(pend);  // everything older than the newest chunk's DMA has landed (this wave)
+    __syncthreads();   // ... for every wave
+    cur = (cur + 1) % kRing;
+    ecur ^= 1;
   }
 };
 
@@ -92,6 +186,8 @@ __device__ __forceinline__ void mma_chunk(const float4* __restrict__ A, const fl
     acc1 = mfma4(a1.z, x.z, acc1);
     acc0 = mfma4(a0.w, x.w, acc0);
     acc1 = mfma4(a1.w, x.w, acc1);
+    if (b + 1 < KB) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // next block's reads first
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -162,6 +258,13 @@ __device__ __forceinline__ f16x8 as_h8(float4 v) { return __builtin_bit_cast(f16
 __device__ __forceinline__ float amax4(float4 v) {
   return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
 }
+// max over the 4 lane groups of a point (lanes l, l^16, l^32, l^48) without ds_bpermute: no
+// address VGPRs to keep live (they would be spilled and reloaded behind the in-flight DMA)
+__device__ __forceinline__ float max4_groups(float m) {
+  m = fmaxf(m, __uint_as_float(__builtin_amdgcn_ds_swizzle(__float_as_uint(m), 0x401F)));  // lane ^ 16
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));                              // lane ^ 32
+}
 // 2^(13 - e) with m = f 2^e, f in [0.5, 1): m * scale < 2^13
 __device__ __forceinline__ float pow2_scale(float m) {
   if (!(m > 0.0f) || __builtin_isinf(m)) return 1.0f;
@@ -188,8 +291,7 @@ __device__ __forceinline__ float make_b16(const float4 (&X)[16], const float4 (&
   for (int b = 0; b < KBX; ++b) m = fmaxf(m, amax4(X[b]));
 #pragma unroll
   for (int b = 0; b < KBE; ++b) m = fmaxf(m, amax4(E[b]));
-  m = fmaxf(m, __shfl_xor(m, 16));
-  m = fmaxf(m, __shfl_xor(m, 32));
+  m = max4_groups(m);
   const float sc = pow2_scale(m);
 #pragma unroll
   for (int s = 0; s < KB / 2; ++s) {
@@ -197,50 +299,72 @@ __device__ __forceinline__ float make_b16(const float4 (&X)[16], const float4 (&
     const float4 v0 = b0 < KBX ? X[b0 < KBX ? b0 : 0] : E[b0 < KBX ? 0 : b0 - KBX];
     const float4 v1 = b1 < KBX ? X[b1 < KBX ? b1 : 0] : E[b1 < KBX ? 0 : b1 - KBX];
     split8(v0, v1, sc, bh[s], bl[s]);
+    // opaque to the optimiser: otherwise hipcc keeps X live and re-splits it inside every chunk
+    // of the layer (~200 VALU per chunk) to save the 8 extra VGPRs the halves need over X
+    asm volatile("" : "+v"(bh[s]), "+v"(bl[s]));
   }
   return 1.0f / sc;
 }
-// A layout (f16x3): [obl(2)][s(NS)][hl(2)][lane(64)] x 16 B (8 halves)
+// A layout (f16x3): [obl(2)][s(NS)][hl(2)][lane(64)] x 16 B (8 halves).
+// Software-pipelined one k-step deep (the 4 A fragments of step s+1 are read while step s's 6
+// MFMAs issue); sched_barrier keeps hipcc from re-serialising each read behind an lgkmcnt(0).
 template <int NS>
 __device__ __forceinline__ void mma_chunk_h3(const float4* __restrict__ A, const f16x8 (&bh)[12],
                                              const f16x8 (&bl)[12], f32x4& acc0, f32x4& acc1, int lane) {
+  f16x8 nh0 = as_h8(A[0 * 64 + lane]), nl0 = as_h8(A[1 * 64 + lane]);
+  f16x8 nh1 = as_h8(A[(NS * 2) * 64 + lane]), nl1 = as_h8(A[(NS * 2 + 1) * 64 + lane]);
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const f16x8 h0 = as_h8(A[(s * 2) * 64 + lane]), l0 = as_h8(A[(s * 2 + 1) * 64 + lane]);
-    const f16x8 h1 = as_h8(A[((NS + s) * 2) * 64 + lane]), l1 = as_h8(A[((NS + s) * 2 + 1) * 64 + lane]);
+    const f16x8 h0 = nh0, l0 = nl0, h1 = nh1, l1 = nl1;
+    if (s + 1 < NS) {
+      nh0 = as_h8(A[((s + 1) * 2) * 64 + lane]);
+      nl0 = as_h8(A[((s + 1) * 2 + 1) * 64 + lane]);
+      nh1 = as_h8(A[((NS + s + 1) * 2) * 64 + lane]);
+      nl1 = as_h8(A[((NS + s + 1) * 2 + 1) * 64 + lane]);
+    }
     acc0 = mfma16h(l0, bh[s], acc0);
     acc1 = mfma16h(l1, bh[s], acc1);
     acc0 = mfma16h(h0, bl[s], acc0);
     acc1 = mfma16h(h1, bl[s], acc1);
     acc0 = mfma16h(h0, bh[s], acc0);
     acc1 = mfma16h(h1, bh[s], acc1);
+    // issue order: the next step's LDS reads first, then this step's MFMAs
+    if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
 // Forward GEMM layer: Y[0..NBO) = act(W · [X[0..KBX) ; E[0..KBE)] + bias).
-// `op` chunks are consumed from the stream; `nxt/nxt_bytes` is the chunk that follows this op.
-template <int P, int KBX, int KBE, int NBO, int ACT, int NE>
-__device__ __forceinline__ void gemm_fwd(WStream& ws, const char* __restrict__ op, const char* nxt, int nxt_bytes,
+// `op` chunks are consumed from the stream; `nxt` (chunks of nxt_bytes) is the op that follows.
+template <int P, int KBX, int KBE, int NBO, int ACT, int NE, class WS>
+__device__ __forceinline__ void gemm_fwd(WS& ws, const char* __restrict__ op, const char* nxt, int nxt_bytes,
                                          const float4 (&X)[16], const float4 (&E)[NE], float4 (&Y)[16],
                                          float4* __restrict__ e_out, float* __restrict__ feat_out, bool feat_ok,
                                          int lane) {
   constexpr int KB = KBX + KBE;
   constexpr int CB = chunk_bytes(KB);
+  constexpr int NCH = NBO / 2;
+  static_assert(NCH >= 2, "the 2-ahead stream needs >= 2 chunks per op");
   const int g = lane >> 4;
   f16x8 bh[12], bl[12];
   float xinv = 1.0f;
   if constexpr (P == NR_PREC_F16X3) xinv = make_b16<KBX, KBE, NE>(X, E, bh, bl);
   // global stores of chunk c are issued at the start of chunk c+1, *before* that chunk's DMA, so
-  // the vmcnt(0) in flip() waits for a store that had a whole chunk to retire, not a fresh one
+  // flip()'s wait never stands behind a store younger than the weights it waits for
   float4 p0 = make_float4(0, 0, 0, 0), p1 = p0;
   int pc = -1;
   auto drain = [&]() {
     if (pc >= 0) {
       if constexpr (ACT == ACT_SOFTPLUS) {
-        if (e_out) {
-          e_out[(2 * pc) * 64 + lane] = p0;
-          e_out[(2 * pc + 1) * 64 + lane] = p1;
+#ifndef NR_EXP_NO_ESTORE  // timing experiment: skip the e-slab stores
+        if (e_out) {  // streamed: non-temporal so the slab does not evict the weights from L2
+          using gf4 = __attribute__((address_space(1))) f32x4;
+          gf4* eb = (gf4*)uniform_ptr(e_out + (2 * pc) * 64);
+          __builtin_nontemporal_store(tof(p0), eb + lane);
+          __builtin_nontemporal_store(tof(p1), eb + 64 + lane);
         }
+#endif
       } else {
         if (feat_out && feat_ok) {  // row-major [P][256] feature rows of that chunk
           *(float4*)(feat_out + (2 * pc) * 16 + g * 4) = p0;
@@ -251,10 +375,11 @@ __device__ __forceinline__ void gemm_fwd(WStream& ws, const char* __restrict__ o
     pc = -1;
   };
 #pragma unroll 1
-  for (int c = 0; c < NBO / 2; ++c) {
+  for (int c = 0; c < NCH; ++c) {
     drain();
-    if (c + 1 < NBO / 2) ws.issue(op + (c + 1) * CB, CB);
-    else if (nxt) ws.issue(nxt, nxt_bytes);
+    if (c + 2 < NCH) ws.issue(op + (c + 2) * CB, CB);
+    else if (nxt) ws.issue(nxt + (c + 2 - NCH) * nxt_bytes, nxt_bytes);
+    else ws.none();
     const float4* A = ws.buf();
     const f32x4 b0 = tof(A[2 * KB * 64 + g]), b1 = tof(A[2 * KB * 64 + 4 + g]);
     f32x4 acc0, acc1;
@@ -294,29 +419,33 @@ __device__ __forceinline__ void gemm_fwd(WStream& ws, const char* __restrict__ o
 }
 
 // Backward GEMM layer: out = Wᵀ · G (no bias).  The first NBO1 output blocks are scaled by
-// softplus'(z) of the previous layer (e_prev) and rotated into Y; the remaining NBO2 blocks are
-// gradients w.r.t. the positional encoding and are handed to `emb(block, value)` as produced.
-template <int P, int KBG, int NBO1, int NBO2, class EmbFn>
-__device__ __forceinline__ void gemm_bwd(WStream& ws, const char* __restrict__ op, const char* nxt, int nxt_bytes,
-                                         const float4 (&G)[16], float4 (&Y)[16], const float4* __restrict__ e_prev,
-                                         int lane, EmbFn&& emb) {
+// softplus'(z) of the previous layer (slab e_cur, staged into LDS one chunk ahead) and rotated
+// into Y; the remaining NBO2 blocks are gradients w.r.t. the positional encoding and are handed to
+// `emb(block, value)` as produced.  The last chunk stages e_next blocks 0,1 for the next op.
+template <int P, int KBG, int NBO1, int NBO2, class WS, class EmbFn>
+__device__ __forceinline__ void gemm_bwd(WS& ws, const char* __restrict__ op, const char* nxt, int nxt_bytes,
+                                         const float4 (&G)[16], float4 (&Y)[16], const float4* __restrict__ e_cur,
+                                         const float4* __restrict__ e_next, int lane, EmbFn&& emb) {
   constexpr int NBO = NBO1 + NBO2;
+  constexpr int NCH = NBO / 2;
   static_assert(NBO1 % 2 == 0 && NBO2 % 2 == 0, "output segments must be chunk aligned");
+  static_assert(NCH >= 2, "the 2-ahead stream needs >= 2 chunks per op");
   constexpr int CB = chunk_bytes(KBG);
   const float4 dummy[4] = {};
   f16x8 bh[12], bl[12];
   float ginv = 1.0f;
   if constexpr (P == NR_PREC_F16X3) ginv = make_b16<KBG, 0, 4>(G, dummy, bh, bl);
 #pragma unroll 1
-  for (int c = 0; c < NBO / 2; ++c) {
-    if (c + 1 < NBO / 2) ws.issue(op + (c + 1) * CB, CB);
-    else if (nxt) ws.issue(nxt, nxt_bytes);
+  for (int c = 0; c < NCH; ++c) {
     const bool main = 2 * c < NBO1;
-    float4 e0 = make_float4(0, 0, 0, 0), e1 = e0;
-    if (main && e_prev) {
-      e0 = e_prev[(2 * c) * 64 + lane];
-      e1 = e_prev[(2 * c + 1) * 64 + lane];
+    if (2 * c + 2 < NBO1) {
+      if (e_cur) ws.slab_next(e_cur, 2 * c + 2);
+    } else if (c + 1 == NCH && e_next) {
+      ws.slab_next(e_next, 0);
     }
+    if (c + 2 < NCH) ws.issue(op + (c + 2) * CB, CB);
+    else if (nxt) ws.issue(nxt + (c + 2 - NCH) * nxt_bytes, nxt_bytes);
+    else ws.none();
     const float4* A = ws.buf();
     f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
     if constexpr (P == NR_PREC_FP32) {
@@ -329,7 +458,13 @@ __device__ __forceinline__ void gemm_bwd(WStream& ws, const char* __restrict__ o
     }
     float4 y0 = fromf(acc0), y1 = fromf(acc1);
     if (main) {
-      if (e_prev) {
+      if (e_cur) {
+        const float4* eb = ws.slab_cur();
+#ifdef NR_EXP_NO_ELOAD
+        const float4 e0 = make_float4(1.f, 1.f, 1.f, 1.f), e1 = e0;
+#else
+        const float4 e0 = eb[lane], e1 = eb[64 + lane];
+#endif
         y0 = make_float4(softplus_bwd<P>(y0.x, e0.x), softplus_bwd<P>(y0.y, e0.y), softplus_bwd<P>(y0.z, e0.z),
                          softplus_bwd<P>(y0.w, e0.w));
         y1 = make_float4(softplus_bwd<P>(y1.x, e1.x), softplus_bwd<P>(y1.y, e1.y), softplus_bwd<P>(y1.z, e1.z),
@@ -407,8 +542,9 @@ struct SdfKArgs {
 
 template <int P, bool NABLA>
 __global__ __launch_bounds__(kThreads) void sdf_kernel(SdfKArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * kMaxChunkBytes];
-  WStream ws{smem, 1};
+  constexpr int CB = chunk_bytes(18);  // largest SDF op chunk (F4: 14 + 4 input blocks)
+  __shared__ __attribute__((aligned(16))) char smem[kRing * CB + (NABLA ? 2 * kSlabChunk : 0)];
+  WStream<CB> ws{smem, NABLA ? smem + kRing * CB : nullptr, 0, 0, 0};
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int j = lane & 15, g = lane >> 4;
   const SdfLayout& L = a.L;
@@ -417,12 +553,10 @@ __global__ __launch_bounds__(kThreads) void sdf_kernel(SdfKArgs a) {
   auto OPB = [&](int i) { return (int)L.op_bytes[i]; };
   const float* w8 = (const float*)(W + L.w8row0_off);
   const float b8 = *(const float*)(W + L.misc_off);
-  float4* escr = a.scratch + (size_t)(blockIdx.x * kWaves + wave) * (8 * 16 * 64);
+  float4* escr = uniform_ptr(a.scratch + (size_t)(blockIdx.x * kWaves + wave) * (8 * 16 * 64));
   const bool want_feat = a.feature != nullptr;
 
-  // first chunk of the stream
-  ws.issue(OP(F0), OPB(F0));
-  ws.flip();
+  ws.start(OP(F0), OPB(F0), OP(F0) + OPB(F0), OPB(F0));
 
   const int64_t Pn = a.P_dev ? min(a.P, (int64_t)(*a.P_dev) * a.P_mult) : a.P;
   for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < Pn; base += (int64_t)gridDim.x * kPointsPerWG) {
@@ -492,15 +626,17 @@ __global__ __launch_bounds__(kThreads) void sdf_kernel(SdfKArgs a) {
       auto emb_skip = [&](int eb, float4 gv) { park[eb * 64 + lane] = gv; };
       auto emb_first = [&](int eb, float4 gv) { park[(4 + eb) * 64 + lane] = gv; };
       auto noemb = [](int, float4) {};
-      gemm_bwd<P, 16, 16, 0>(ws, OP(B7), OP(B6), OPB(B6), X, Y, e_l[6], lane, noemb);
-      gemm_bwd<P, 16, 16, 0>(ws, OP(B6), OP(B5), OPB(B5), Y, X, e_l[5], lane, noemb);
-      gemm_bwd<P, 16, 16, 0>(ws, OP(B5), OP(B4), OPB(B4), X, Y, e_l[4], lane, noemb);
+      ws.slab_now(e_l[6], 0);  // softplus'(z6) blocks 0,1 for B7's first chunk
+      gemm_bwd<P, 16, 16, 0>(ws, OP(B7), OP(B6), OPB(B6), X, Y, e_l[6], e_l[5], lane, noemb);
+      gemm_bwd<P, 16, 16, 0>(ws, OP(B6), OP(B5), OPB(B5), Y, X, e_l[5], e_l[4], lane, noemb);
+      gemm_bwd<P, 16, 16, 0>(ws, OP(B5), OP(B4), OPB(B4), X, Y, e_l[4], e_l[3], lane, noemb);
       // skip layer: rows 0..216 -> h3 (scaled by softplus'(z3)), rows 217..255 -> embedding
-      gemm_bwd<P, 16, 14, 4>(ws, OP(B4), OP(B3), OPB(B3), Y, X, e_l[3], lane, emb_skip);
-      gemm_bwd<P, 14, 16, 0>(ws, OP(B3), OP(B2), OPB(B2), X, Y, e_l[2], lane, noemb);
-      gemm_bwd<P, 16, 16, 0>(ws, OP(B2), OP(B1), OPB(B1), Y, X, e_l[1], lane, noemb);
-      gemm_bwd<P, 16, 16, 0>(ws, OP(B1), OP(B0), OPB(B0), X, Y, e_l[0], lane, noemb);
-      gemm_bwd<P, 16, 0, 4>(ws, OP(B0), has_next ? OP(F0) : nullptr, OPB(F0), Y, X, nullptr, lane, emb_first);
+      gemm_bwd<P, 16, 14, 4>(ws, OP(B4), OP(B3), OPB(B3), Y, X, e_l[3], e_l[2], lane, emb_skip);
+      gemm_bwd<P, 14, 16, 0>(ws, OP(B3), OP(B2), OPB(B2), X, Y, e_l[2], e_l[1], lane, noemb);
+      gemm_bwd<P, 16, 16, 0>(ws, OP(B2), OP(B1), OPB(B1), Y, X, e_l[1], e_l[0], lane, noemb);
+      gemm_bwd<P, 16, 16, 0>(ws, OP(B1), OP(B0), OPB(B0), X, Y, e_l[0], nullptr, lane, noemb);
+      gemm_bwd<P, 16, 0, 4>(ws, OP(B0), has_next ? OP(F0) : nullptr, OPB(F0), Y, X, nullptr, nullptr, lane,
+                            emb_first);
       // chain rule through the positional encoding (autograd sums both uses of embed(x))
       float n0 = 0.f, n1 = 0.f, n2 = 0.f;
 #pragma unroll
@@ -522,6 +658,7 @@ __global__ __launch_bounds__(kThreads) void sdf_kernel(SdfKArgs a) {
       }
     }
   }
+  wait_vmcnt(0);  // a block without tiles still has the prologue's second chunk in flight
 }
 
 // =============================================================================================
@@ -555,8 +692,9 @@ __device__ __forceinline__ float rad_small_feature(int f, const float (&x)[3], c
 
 template <int P, int KBS>
 __global__ __launch_bounds__(kThreads) void radiance_kernel(RadKArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * kMaxChunkBytes];
-  WStream ws{smem, 1};
+  constexpr int CB = chunk_bytes(16 + KBS);
+  __shared__ __attribute__((aligned(16))) char smem[kRing * CB];
+  WStream<CB> ws{smem, nullptr, 0, 0, 0};
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int j = lane & 15, g = lane >> 4;
   const RadLayout& L = a.L;
@@ -565,8 +703,7 @@ __global__ __launch_bounds__(kThreads) void radiance_kernel(RadKArgs a) {
   auto OPB = [&](int i) { return (int)L.op_bytes[i]; };
   const float* head = (const float*)(W + L.head_off);  // [3][256] weights then [3] bias
 
-  ws.issue(OP(0), OPB(0));
-  ws.flip();
+  ws.start(OP(0), OPB(0), OP(0) + OPB(0), OPB(0));
   for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < a.P; base += (int64_t)gridDim.x * kPointsPerWG) {
     const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < a.P;
     const int64_t p = base + wave * kTile + j;
@@ -620,6 +757,7 @@ __global__ __launch_bounds__(kThreads) void radiance_kernel(RadKArgs a) {
       a.rgb[p * 3 + 2] = r[2];
     }
   }
+  wait_vmcnt(0);
 }
 
 // =============================================================================================
@@ -651,8 +789,9 @@ __device__ __noinline__ float nerf_embed4(int f, float x0, float x1, float x2, f
 
 template <int P>
 __global__ __launch_bounds__(kThreads) void nerf_kernel(NerfKArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * kMaxChunkBytes];
-  WStream ws{smem, 1};
+  constexpr int CB = chunk_bytes(22);  // N5: 16 + 6 input blocks
+  __shared__ __attribute__((aligned(16))) char smem[kRing * CB];
+  WStream<CB> ws{smem, nullptr, 0, 0, 0};
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int j = lane & 15, g = lane >> 4;
   const NerfLayout& L = a.L;
@@ -662,8 +801,7 @@ __global__ __launch_bounds__(kThreads) void nerf_kernel(NerfKArgs a) {
   const float* wa = (const float*)(W + L.alpha_off);
   const float* wr = (const float*)(W + L.rgb_off);
 
-  ws.issue(OP(N0), OPB(N0));
-  ws.flip();
+  ws.start(OP(N0), OPB(N0), OP(N0) + OPB(N0), OPB(N0));
   for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < a.P; base += (int64_t)gridDim.x * kPointsPerWG) {
     const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < a.P;
     const int64_t p = base + wave * kTile + j;
@@ -733,6 +871,7 @@ __global__ __launch_bounds__(kThreads) void nerf_kernel(NerfKArgs a) {
       a.rgb[p * 3 + 2] = r[2];
     }
   }
+  wait_vmcnt(0);
 }
 
 // =============================================================================================

@@ -1,0 +1,74 @@
+"""World-size-2 gloo run of the ray-sharded render driver (neurecon_amd/dist.py) on the CPU.
+
+The render function here is a stand-in with the frameworks' calling convention (the HIP render
+needs a GPU); what is checked is the sharding, the chunk alignment and the all-gather, i.e. that
+a sharded render reassembles bit-for-bit into the single-process result."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from neurecon_amd import dist as nd
+
+
+def _fake_render(ro, rd, model, batched=True, **kw):
+    # per-ray, order-independent function of the ray, same output structure as volume_render
+    rgb = torch.stack([ro.sum(-1), rd.sum(-1), (ro * rd).sum(-1)], -1)
+    depth = ro.norm(dim=-1)
+    return rgb, depth, {'rgb': rgb, 'depth_volume': depth, 'mask_volume': rd.norm(dim=-1),
+                        'implicit_surface': ro[..., :1].expand(*ro.shape[:-1], 5).contiguous(), 'scalar': 3}
+
+
+def _worker(rank, ws, port, q, align):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=ws)
+    try:
+        g = torch.Generator().manual_seed(0)
+        ro = torch.randn(1, 37, 3, generator=g)
+        rd = torch.randn(1, 37, 3, generator=g)
+        rgb, depth, ex = nd.render_sharded(_fake_render, ro, rd, None, batched=True, align=align)
+        ref = _fake_render(ro, rd, None)
+        ok = (torch.equal(rgb, ref[0]) and torch.equal(depth, ref[1]) and
+              torch.equal(ex['implicit_surface'], ref[2]['implicit_surface']) and ex['scalar'] == 3)
+        lo, hi = nd.shard_bounds(37, rank, ws, align)
+        q.put((rank, ok, lo, hi))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize('align', [1, 8])
+def test_sharded_render_reassembles_world2(align):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, align)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _, _ in res)
+    (_, _, lo0, hi0), (_, _, lo1, hi1) = res
+    assert lo0 == 0 and hi0 == lo1 and hi1 == 37
+    assert hi0 % align == 0
+
+
+def test_shard_bounds_cover_and_align():
+    for n in (1, 5, 64, 4096, 4097):
+        for ws in (1, 2, 3, 8):
+            for align in (1, 16, 1000):
+                b = [nd.shard_bounds(n, r, ws, align) for r in range(ws)]
+                assert b[0][0] == 0 and b[-1][1] == n
+                assert all(b[i][1] == b[i + 1][0] for i in range(ws - 1))
+                assert all(lo % align == 0 for lo, _ in b if lo < n)

@@ -1,0 +1,46 @@
+"""Minimal driver for profiling the fused SDF MLP kernels: ImplicitSurface.forward_with_nablas on
+P points (default 524288 = one config-(b) step's samples), N launches.  Used under rocprofv3."""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--points', type=int, default=524288)
+    ap.add_argument('--iters', type=int, default=5)
+    ap.add_argument('--precision', default='f16x3')
+    ap.add_argument('--mode', default='nabla', choices=['nabla', 'fwd', 'radiance'])
+    a = ap.parse_args()
+    from neurecon_amd.base import ImplicitSurface, RadianceNet
+    torch.manual_seed(0)
+    s = ImplicitSurface(W=256, D=8, skips=[4], W_geo_feat=256, radius_init=0.5, embed_multires=6,
+                        precision=a.precision).cuda().eval()
+    x = (torch.rand(a.points, 3, device='cuda') * 2 - 1) * 0.9
+    with torch.no_grad():
+        if a.mode == 'radiance':
+            r = RadianceNet(D=4, W=256, W_geo_feat=256, embed_multires=-1, embed_multires_view=4,
+                            precision=a.precision).cuda().eval()
+            _, n, h = s.forward_with_nablas(x)
+            fn = lambda: r.forward(x, x, n, h)
+        elif a.mode == 'fwd':
+            fn = lambda: s.forward(x)
+        else:
+            fn = lambda: s.forward_with_nablas(x)
+        fn()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(a.iters):
+            fn()
+        torch.cuda.synchronize()
+    dt = (time.perf_counter() - t) / a.iters
+    print(f'{a.mode} {a.precision}: {a.points} points, {dt * 1e3:.3f} ms/launch-set')
+
+
+if __name__ == '__main__':
+    main()
