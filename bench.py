@@ -105,6 +105,38 @@ def cpu_baseline(n_rays):
                       f'torch {torch.__version__} CPU fp32, {threads} threads, {dt:.1f} s'}
 
 
+def eager_gpu_baseline(dev, n_rays, reps=3):
+    """The same oracle (op-for-op the reference's eager PyTorch sequence, fp32) run on the GPU with
+    PyTorch-ROCm: the north star's "reference single-GPU PyTorch-ROCm" denominator,
+    since the reference itself cannot travel to the box.  Part of the baseline leg, never the product."""
+    from oracle.neus import NeuSOracle
+    from neurecon_amd import rend_util
+    m = make_model(dev, 'fp32')
+    sd = {k: v.detach() for k, v in m.state_dict().items()}
+    c2w, K = camera(dev)
+    ro, rd, _ = rend_util.get_rays(c2w, K, 64, 64)
+    ro, rd = ro[:, :n_rays].contiguous(), rd[:, :n_rays].contiguous()
+    prev = torch.get_default_device()
+    torch.set_default_device(dev)   # the oracle's linspace/ones tables follow the rays' device
+    try:
+        orc = NeuSOracle(sd)
+        times = []
+        with torch.no_grad():
+            orc.render(ro, rd)  # warm-up
+            for _ in range(reps):
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                orc.render(ro, rd)
+                torch.cuda.synchronize()
+                times.append(time.perf_counter() - t)
+    finally:
+        torch.set_default_device(prev)
+    dt = sorted(times)[len(times) // 2]
+    return {'value': round(n_rays / dt, 1), 'unit': 'rays/s', 'kind': 'port', 'device': torch.cuda.get_device_name(dev),
+            'sample': f'{n_rays} config-(b) rays in one chunk, oracle/neus.py eager fp32 on 1 GPU, median of {reps}, '
+                      f'{dt * 1e3:.1f} ms'}
+
+
 # algorithmic MACs per unit (point) of each library kernel, SURVEY.md §8(a)
 KERNEL_MAC = {'sdf_fwd': MAC_SDF_FWD, 'sdf_feat': MAC_SDF_FWD, 'sdf_nabla': MAC_SDF_FWD + MAC_SDF_BWD,
               'sdf_nabla_feat': MAC_SDF_FWD + MAC_SDF_BWD, 'radiance': MAC_RAD}
@@ -213,6 +245,9 @@ def main():
         }
         if not args.no_cpu_baseline and world == 1:
             out['cpu_baseline'] = cpu_baseline(args.cpu_rays)
+            eg = eager_gpu_baseline(dev, n_rays)
+            eg['speedup'] = round(value / eg['value'], 2)
+            out['cpu_baseline']['eager_gpu_reference'] = eg
         print(json.dumps(out), flush=True)
     if dist:
         tdist.destroy_process_group()

@@ -7,7 +7,7 @@ import torch.nn.functional as F
 
 def freq_bands(n_freqs):
     # models/base.py:38-44: 2**linspace(0, F-1, F), cast to python floats
-    return (2. ** torch.linspace(0., n_freqs - 1, n_freqs)).numpy().tolist()
+    return (2. ** torch.linspace(0., n_freqs - 1, n_freqs, device='cpu')).numpy().tolist()
 
 
 def embed(x, n_freqs):
