@@ -40,9 +40,6 @@ int check_rad_desc(const NrRadDesc* d) {
   return NR_OK;
 }
 
-// (input blocks, output blocks) of each SDF GEMM op, stream order F0..F8, B7..B0
-static const int kSdfKB[kSdfOps] = {4, 16, 16, 16, 18, 16, 16, 16, 16, 16, 16, 16, 16, 14, 16, 16, 16};
-static const int kSdfNBO[kSdfOps] = {16, 16, 16, 14, 16, 16, 16, 16, 16, 16, 16, 16, 18, 16, 16, 16, 4};
 
 SdfLayout sdf_layout(const NrSdfDesc& d) {
   SdfLayout L{};
@@ -53,8 +50,11 @@ SdfLayout sdf_layout(const NrSdfDesc& d) {
     L.op_off[i] = (uint32_t)off;
     off += (size_t)(kSdfNBO[i] / 2) * L.op_bytes[i];
   }
+  static_assert(sdf_op_off(kSdfOps - 1) + (kSdfNBO[kSdfOps - 1] / 2) * (2 * kSdfKB[kSdfOps - 1] + 1) * 1024 > 0, "");
   L.scale_off = (uint32_t)off;
   off = align256(off + kSdfOps * 4);
+  L.bound_off = (uint32_t)off;
+  off = align256(off + kSdfOps * 8);
   L.w8row0_off = (uint32_t)off;
   off = align256(off + 256 * 4);
   L.misc_off = (uint32_t)off;
@@ -497,6 +497,9 @@ int nr_sdf_pack(const NrSdfDesc* d, const float* const* W, const float* const* b
   ops[B2] = mkop(W[2], nullptr, ROWS(2), 256, 1, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + B2);
   ops[B1] = mkop(W[1], nullptr, ROWS(1), 256, 1, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + B1);
   ops[B0] = mkop(W[0], nullptr, ROWS(0), in0, 1, seg(4, 0, in0), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + B0);
+  float* bound = (float*)(P + L.bound_off);
+  for (int i = 0; i < kSdfOps; ++i) ops[i].bound = bound + 2 * i;
+  ops[F7].aux = W[8];  // sdf row W8[0, :] rides with F7's chunks (v2 pipeline's running dot product)
   for (int i = 0; i < kSdfOps; ++i)
     if ((rc = launch_pack_op(ops[i], P + L.op_off[i], st))) return rc;
   if ((rc = launch_pack_vec(W[8], 0, 256, 256, P + L.w8row0_off, st))) return rc;

@@ -14,10 +14,21 @@ constexpr size_t kScratchPerWG = (size_t)kWaves * 8 * 16 * 64 * 16;  // exp(100z
 // SDF GEMM ops in stream order (forward F*, feature F8, backward B*)
 enum SdfOp { F0, F1, F2, F3, F4, F5, F6, F7, F8, B7, B6, B5, B4, B3, B2, B1, B0, kSdfOps };
 
+// (input blocks, output blocks) of each SDF GEMM op, stream order F0..F8, B7..B0; ops are packed
+// back to back in this order, chunk = 2 output blocks x KB input blocks + a 1 KB bias slot
+constexpr int kSdfKB[kSdfOps] = {4, 16, 16, 16, 18, 16, 16, 16, 16, 16, 16, 16, 16, 14, 16, 16, 16};
+constexpr int kSdfNBO[kSdfOps] = {16, 16, 16, 14, 16, 16, 16, 16, 16, 16, 16, 16, 18, 16, 16, 16, 4};
+__host__ __device__ constexpr uint32_t sdf_op_off(int i) {
+  uint32_t off = 0;
+  for (int k = 0; k < i; ++k) off += (uint32_t)(kSdfNBO[k] / 2) * (2 * kSdfKB[k] + 1) * 1024;
+  return off;
+}
+
 struct SdfLayout {
   uint32_t op_off[kSdfOps];
   uint32_t op_bytes[kSdfOps];  // bytes of one chunk of the op
   uint32_t scale_off;          // [kSdfOps] max |W| per op (f16x3 weight scaling)
+  uint32_t bound_off;          // [kSdfOps][2] max row L1 norm, max |bias| per op (f16x3 operand scales)
   uint32_t w8row0_off;         // sdf row of the last layer [256]
   uint32_t misc_off;           // [0] = sdf bias
   uint32_t total;
@@ -66,6 +77,8 @@ struct PackOp {
   float scale;
   int prec;            // NR_PREC_*
   float* wmax;         // device word receiving max |W * scale| (f16x3 scaling)
+  const float* aux;    // optional per-output-row vector written to bias-slot floats 64..95 of each chunk
+  float* bound;        // optional [2]: max over output rows of sum |W * scale|, max |bias|
 };
 
 int launch_pack_op(const PackOp& op, char* dst, hipStream_t stream);

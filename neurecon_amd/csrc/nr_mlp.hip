@@ -16,6 +16,7 @@
 //    per-wave scratch slab and applies torch's softplus_backward formula g*e/(e+1).
 //  * Everything per point (embedding, nabla chain rule through sin/cos, sdf row dot product,
 //    sigmoid head) is VALU work in the same kernel.
+#include <type_traits>
 #include "nr_common.h"
 #include "nr_mlp.h"
 
@@ -90,6 +91,13 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
   return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)p);
 }
 
+// chunk loops: rolled (push2 rotates the outputs) unless NR_EXP_UNROLL (experiment)
+#ifdef NR_EXP_UNROLL
+#define NR_CHUNK_UNROLL _Pragma("unroll")
+#else
+#define NR_CHUNK_UNROLL _Pragma("unroll 1")
+#endif
+
 constexpr int kRing = 3;
 constexpr int kSlabChunk = kWaves * 2 * 64 * 16;  // softplus' of 2 blocks for every wave: 16 KB
 
@@ -149,7 +157,9 @@ struct WStream {
   __device__ __forceinline__ const float4* buf() const { return (const float4*)(lds + cur * CBMAX); }
   __device__ __forceinline__ void flip() {
     wait_vmcnt(pend);  // everything older than the newest chunk's DMA has landed (this wave)
+#ifndef NR_EXP_NO_BARRIER  // timing experiment: waves drift apart (results are garbage)
     __syncthreads();   // ... for every wave
+#endif
     cur = (cur + 1) % kRing;
     ecur ^= 1;
   }
@@ -223,6 +233,9 @@ __device__ __forceinline__ void push2cat(float4 (&Y)[16], float4 (&Z)[4], float4
 //  P = NR_PREC_F16X3: hardware v_exp_f32 / v_log_f32 / v_rcp_f32 (~1e-6 rel), for the fast mode.
 template <int P>
 __device__ __forceinline__ void softplus_fwd(float z, float& y, float& e) {
+#ifdef NR_EXP_NO_SOFTPLUS  // timing experiment: activation skipped (results are garbage)
+  y = z; e = z; return;
+#endif
   const float t = fmul(z, 100.0f);
   const bool lin = t > 20.0f;
   if constexpr (P == NR_PREC_FP32) {
@@ -286,6 +299,16 @@ __device__ __forceinline__ float make_b16(const float4 (&X)[16], const float4 (&
                                           f16x8 (&bl)[12]) {
   constexpr int KB = KBX + KBE;
   static_assert(KB % 2 == 0 && KB <= 24, "bad block count");
+#ifdef NR_EXP_NO_SPLIT  // timing experiment: operands reinterpreted, not split (results are garbage)
+#pragma unroll
+  for (int s = 0; s < KB / 2; ++s) {
+    const float4 v0 = 2 * s < KBX ? X[2 * s < KBX ? 2 * s : 0] : E[2 * s < KBX ? 0 : 2 * s - KBX];
+    const float4 v1 = 2 * s + 1 < KBX ? X[2 * s + 1 < KBX ? 2 * s + 1 : 0] : E[2 * s + 1 < KBX ? 0 : 2 * s + 1 - KBX];
+    bh[s] = as_h8(v0);
+    bl[s] = as_h8(v1);
+  }
+  return 1.0f;
+#endif
   float m = 0.0f;
 #pragma unroll
   for (int b = 0; b < KBX; ++b) m = fmaxf(m, amax4(X[b]));
@@ -374,7 +397,7 @@ __device__ __forceinline__ void gemm_fwd(WS& ws, const char* __restrict__ op, co
     }
     pc = -1;
   };
-#pragma unroll 1
+NR_CHUNK_UNROLL
   for (int c = 0; c < NCH; ++c) {
     drain();
     if (c + 2 < NCH) ws.issue(op + (c + 2) * CB, CB);
@@ -435,7 +458,7 @@ __device__ __forceinline__ void gemm_bwd(WS& ws, const char* __restrict__ op, co
   f16x8 bh[12], bl[12];
   float ginv = 1.0f;
   if constexpr (P == NR_PREC_F16X3) ginv = make_b16<KBG, 0, 4>(G, dummy, bh, bl);
-#pragma unroll 1
+NR_CHUNK_UNROLL
   for (int c = 0; c < NCH; ++c) {
     const bool main = 2 * c < NBO1;
     if (2 * c + 2 < NBO1) {
@@ -658,6 +681,711 @@ __global__ __launch_bounds__(kThreads) void sdf_kernel(SdfKArgs a) {
       }
     }
   }
+  wait_vmcnt(0);  // a block without tiles still has the prologue's second chunk in flight
+}
+
+// =============================================================================================
+// f16x3 SDF pipeline v2 (sdf3_kernel)
+// =============================================================================================
+// What changes against sdf_kernel<F16X3>:
+//  * The B operand of op l+1 is split into f16 hi/lo fragments by op l's epilogue, one k-step per
+//    chunk (chunk c of op l produces exactly k-step c of op l+1), instead of in one burst of
+//    ~300 VALU per layer in which every wave of the workgroup idles its matrix core.  The per-point
+//    power-of-two scale this needs is fixed *before* op l runs, from a bound on its outputs:
+//    |out| <= R_l * max|in| + B_l (R_l = max row L1 norm of the op's effective matrix, B_l = max
+//    |bias|, both computed at pack time; softplus(z) <= max(z, 0) + ln2/100; the backward factor
+//    softplus' <= 1).  The scale puts the bound at 2^14 < f16 max, so hi never overflows, and the
+//    bound is loose by ~10-50x in practice, leaving the outputs near 2^9..2^10 where hi + lo still
+//    carry 22 significant bits (lo turns subnormal only 2^-17 below the bound).
+//  * No fp32 copy of the activations is kept, chunk loops are fully unrolled (no register
+//    rotation), and every DMA count / vmcnt is a compile-time constant.
+//  * Ping-pong wave groups: waves 0-3 (one per SIMD) run [MFMA(c) -> epilogue(c)] per chunk,
+//    waves 4-7 run [epilogue(c-1) -> MFMA(c)], so each SIMD's matrix core is fed by one wave
+//    while the other does its VALU epilogue (activation, slab I/O, operand split).
+//  * The reverse pass stores softplus'(z) = sigmoid(100 z) itself (1 on torch's linear branch),
+//    so the backward epilogue is one multiply.
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t cvt_pk_h(float a, float b) {  // v_cvt_pk_f16_f32 (RNE)
+  const h2v h = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(uint32_t, h);
+}
+// 8 values of one k-step (block 2s: a, block 2s+1: b), scaled by sc, into f16 hi / lo fragments
+__device__ __forceinline__ void split8s(float4 a, float4 b, float sc, f16x8& h, f16x8& l) {
+  const f2v s2 = {sc, sc};
+  const f2v v[4] = {f2v{a.x, a.y} * s2, f2v{a.z, a.w} * s2, f2v{b.x, b.y} * s2, f2v{b.z, b.w} * s2};
+  uint32_t hw[4], lw[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint32_t hh = cvt_pk_h(v[i].x, v[i].y);
+    asm volatile("" : "+v"(hh));  // widen the packed halves back (not a second pair of converts)
+    const h2v hv = __builtin_bit_cast(h2v, hh);
+    const f2v r = v[i] - f2v{(float)hv.x, (float)hv.y};
+    hw[i] = hh;
+    lw[i] = cvt_pk_h(r.x, r.y);
+  }
+  h = __builtin_bit_cast(f16x8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
+  l = __builtin_bit_cast(f16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
+}
+// ... parked in AGPRs: B operands are read only by MFMAs, which take AGPR sources directly
+__device__ __forceinline__ void split8a(float4 a, float4 b, float sc, f16x8& h, f16x8& l) {
+  split8s(a, b, sc, h, l);
+  asm volatile("" : "+a"(h), "+a"(l));
+}
+__device__ __forceinline__ float max3abs(float m, float a, float b) {
+  return __builtin_fmaxf(m, __builtin_fmaxf(fabsf(a), fabsf(b)));  // -> v_max3_f32 with |.| modifiers
+}
+__device__ __forceinline__ float amax8(float m, float4 a, float4 b) {
+  m = max3abs(m, a.x, a.y);
+  m = max3abs(m, a.z, a.w);
+  m = max3abs(m, b.x, b.y);
+  return max3abs(m, b.z, b.w);
+}
+// power-of-two scale putting a bound M at < 2^14 (1 for M = 0, inf or NaN)
+__device__ __forceinline__ float bound_scale(float M) {
+  if (!(M > 0.0f) || __builtin_isinf(M)) return 1.0f;
+  return __builtin_ldexpf(1.0f, 14 - __builtin_amdgcn_frexp_expf(M));
+}
+// softplus(beta=100, threshold=20) (base.py:202) and its derivative sigmoid(100 z) (1 on the linear
+// branch, as torch's softplus_backward passes the gradient through there)
+template <bool DERIV>
+__device__ __forceinline__ void softplus3(float z, float& y, float& s) {
+  const float t = z * 100.0f;
+  const bool lin = t > 20.0f;
+  const float ex = __builtin_amdgcn_exp2f(t * 1.44269504088896341f);
+  const float u = 1.0f + ex;
+  const float yy = __builtin_amdgcn_logf(u) * (0.693147180559945309f * 0.01f);
+  y = lin ? z : yy;
+  if constexpr (DERIV) s = lin ? 1.0f : ex * __builtin_amdgcn_rcpf(u);
+}
+__device__ __forceinline__ float4 fma4s(f32x4 a, float m, float4 b) {
+  const f2v m2 = {m, m};
+  const f2v lo = __builtin_elementwise_fma(f2v{a[0], a[1]}, m2, f2v{b.x, b.y});
+  const f2v hi = __builtin_elementwise_fma(f2v{a[2], a[3]}, m2, f2v{b.z, b.w});
+  return make_float4(lo.x, lo.y, hi.x, hi.y);
+}
+
+using gf4 = __attribute__((address_space(1))) f32x4;
+
+// =============================================================================================
+// f16x3 SDF pipeline v3 (sdf4_kernel): one wave per SIMD, 32 points per wave
+// =============================================================================================
+// * 4 waves x 32 points (two 16-point MFMA column tiles per wave) = the same 128-point tile; each
+//   A (weight) fragment read from LDS feeds both columns, and a wave may hold 512 registers, so
+//   the B operands of the op being computed AND of the op being produced stay in registers.
+// * Chunk c's epilogue (bias, activation, slab I/O, per-chunk operand split) is issued in the same
+//   basic block as chunk c+1's MFMAs, so the wave's VALU work fills the matrix core's issue gaps.
+// * The operand split uses per-point power-of-two scales fixed before the op runs, from a bound on
+//   its outputs (see the v2 notes above: split8s / bound_scale / softplus3).
+constexpr int kW4 = 4;          // waves per workgroup (one per SIMD)
+constexpr int kT4 = 64 * kW4;   // 256 threads
+constexpr int kSlab4 = kW4 * 4096;  // one chunk's softplus' values (2 blocks x 2 columns) per wave: 16 KB
+
+// Deferred stores of one chunk (up to 4 x 16 B per lane), issued at the start of the next chunk
+// before its weight DMA, so flip()'s counted wait never stands behind a store younger than the
+// weights it waits for.  Wave-uniform base (SGPR) + per-lane 32-bit float4 offsets.
+struct Pend4 {
+  float4* base;  // null: nothing pending
+  uint32_t o[4];
+  float4 v[4];
+  int n;
+  bool nt;
+  // global_store_dwordx4 with an SGPR base and a 32-bit VGPR byte offset (saddr form), from asm:
+  // compiler-built 64-bit per-lane addresses get hoisted out of the tile loop and spilled
+  __device__ __forceinline__ void flush() {
+    if (base) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i < n) {
+          const uint32_t off = o[i] * 16u;
+          const f32x4 d = tof(v[i]);
+          // s_nop: the store-data hazard (a VALU may not overwrite a >8-byte store's data VGPRs in
+          // the next cycle) is not tracked through inline asm
+          if (nt) asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" : : "v"(off), "v"(d), "s"(base) : "memory");
+          else asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" : : "v"(off), "v"(d), "s"(base) : "memory");
+        }
+      }
+      base = nullptr;
+    }
+  }
+  __device__ __forceinline__ void put(float4* b, int cnt, bool nontemporal) {
+    base = b;
+    n = cnt;
+    nt = nontemporal;
+  }
+};
+
+template <int CBMAX>
+struct WStream4 {
+  char* lds;
+  char* slab;  // 2 x kSlab4
+  int cur;     // ring slot of the chunk being computed
+  int es;      // slab slot staged in this chunk's iteration (read in the next one)
+  __device__ __forceinline__ static int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+  // BYTES/1 KB pieces; every wave issues ceil(pieces/kW4) (a wave past the end repeats the last
+  // piece: identical bytes to the same LDS address) so the count is one constant in every wave
+  template <int BYTES>
+  __device__ __forceinline__ static constexpr int pieces() { return (BYTES / 1024 + kW4 - 1) / kW4; }
+  template <int BYTES>
+  __device__ __forceinline__ void dma(const char* gsrc, int slot) {
+    const int wave = wave_id();
+    const uint32_t voff = (threadIdx.x & 63) * 16;
+    const char* g = uniform_ptr(gsrc);
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_u32(lds) + (uint32_t)(slot * CBMAX));
+#pragma unroll
+    for (int i = 0; i < pieces<BYTES>(); ++i) {
+      int off = (wave + i * kW4) * 1024;
+      if (i == pieces<BYTES>() - 1 && off > BYTES - 1024) off = BYTES - 1024;
+      off = __builtin_amdgcn_readfirstlane(off);
+      glds16s(g + off, voff, base + off);
+    }
+  }
+  template <int B0, int B1>
+  __device__ __forceinline__ void start(const char* g0, const char* g1) {
+    cur = 0;
+    es = 0;
+    dma<B0>(g0, 0);
+    dma<B1>(g1, 1);
+    wait_vmcnt(pieces<B1>());
+    __syncthreads();
+  }
+  template <int BYTES>
+  __device__ __forceinline__ void issue(const char* gsrc) { dma<BYTES>(gsrc, (cur + 2) % kRing); }
+  // this wave's softplus' of chunk c (blocks 2c, 2c+1, both columns: 4 KB contiguous) -> slab slot es
+  __device__ __forceinline__ void stage_slab(const float4* e, int c) {
+    const uint32_t voff = (threadIdx.x & 63) * 16;
+    const char* g = (const char*)uniform_ptr(e + 4 * c * 64);
+    const uint32_t base =
+        __builtin_amdgcn_readfirstlane(lds_u32(slab) + (uint32_t)(es * kSlab4 + wave_id() * 4096));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16s(g + i * 1024, voff, base + i * 1024);
+  }
+  // the slab staged in the previous iteration (the chunk whose epilogue runs now)
+  __device__ __forceinline__ const float4* slab_prev() const {
+    uint32_t off = (es ^ 1) * kSlab4 + wave_id() * 4096;
+    asm volatile("" : "+s"(off));
+    return (const float4*)(slab + off);
+  }
+  __device__ __forceinline__ const float4* buf() const {
+    uint32_t off = cur * CBMAX;
+    asm volatile("" : "+s"(off));
+    return (const float4*)(lds + off);
+  }
+  template <int PEND>
+  __device__ __forceinline__ void flip() {
+    wait_vmcnt(PEND);
+    __syncthreads();
+    cur = (cur + 1) % kRing;
+    es ^= 1;
+  }
+};
+
+// one k-step pair of output blocks x two point columns: 12 MFMAs per k-step
+// Software-pipelined one k-step deep (step s+1's 4 fragments are read while step s's 12 MFMAs
+// issue).  stage(s) is VALU work of the previous chunk's epilogue placed in k-step s's scheduling
+// region, so it fills the matrix core's issue gaps instead of running before or after the MFMAs.
+template <int NS, class Stage>
+__device__ __forceinline__ void mma4(const float4* __restrict__ A, const f16x8 (&bh)[2][12], const f16x8 (&bl)[2][12],
+                                     f32x4 (&acc)[2][2], int lane, Stage&& stage) {
+  f16x8 nh0 = as_h8(A[0 * 64 + lane]), nl0 = as_h8(A[1 * 64 + lane]);
+  f16x8 nh1 = as_h8(A[(NS * 2) * 64 + lane]), nl1 = as_h8(A[(NS * 2 + 1) * 64 + lane]);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const f16x8 h0 = nh0, l0 = nl0, h1 = nh1, l1 = nl1;
+    if (s + 1 < NS) {
+      nh0 = as_h8(A[((s + 1) * 2) * 64 + lane]);
+      nl0 = as_h8(A[((s + 1) * 2 + 1) * 64 + lane]);
+      nh1 = as_h8(A[((NS + s + 1) * 2) * 64 + lane]);
+      nl1 = as_h8(A[((NS + s + 1) * 2 + 1) * 64 + lane]);
+    }
+    stage(s);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      acc[q][0] = mfma16h(l0, bh[q][s], acc[q][0]);
+      acc[q][1] = mfma16h(l1, bh[q][s], acc[q][1]);
+      acc[q][0] = mfma16h(h0, bl[q][s], acc[q][0]);
+      acc[q][1] = mfma16h(h1, bl[q][s], acc[q][1]);
+      acc[q][0] = mfma16h(h0, bh[q][s], acc[q][0]);
+      acc[q][1] = mfma16h(h1, bh[q][s], acc[q][1]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Pre-activations of one chunk: z[q][o] = column q, output block 2c+o; aux[o] = the op's per-row
+// vector (bias-slot floats 64..95) for block o
+struct Z4 {
+  float4 z[2][2];
+  float4 aux[2];
+};
+
+// One GEMM op: out = W · B (+ bias), NBO/2 chunks, fully unrolled; chunk c's epilogue runs in chunk
+// c+1's iteration (after its DMA issue, beside its MFMAs).
+//  pre(c): first thing in chunk c's iteration (slab staging of chunk c for its epilogue)
+template <int KB, int NBO, int NXT_CB, bool AUX, class WS, class Pre, class Epi>
+__device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const char* nxt, const f16x8 (&bh)[2][12],
+                                    const f16x8 (&bl)[2][12], const float (&xinv)[2], Pend4& pd, Pre&& pre,
+                                    Epi&& epi, int lane) {
+  constexpr int CB = chunk_bytes(KB);
+  constexpr int NCH = NBO / 2;
+  static_assert(NCH >= 2, "the 2-ahead stream needs >= 2 chunks per op");
+  const int g = lane >> 4;
+  Z4 zq{};
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    pd.flush();
+    pre(c);
+    // opaque per chunk: keeps the scheduler from computing every chunk's address up front
+    const char* opc = op;
+    const char* nxc = nxt;
+    asm volatile("" : "+s"(opc), "+s"(nxc));
+    if (c + 2 < NCH) ws.template issue<CB>(opc + (c + 2) * CB);
+    else if (nxc) ws.template issue<NXT_CB>(nxc + (c + 2 - NCH) * NXT_CB);
+    const float4* A = ws.buf();
+    f32x4 acc[2][2] = {};
+    // the previous chunk's epilogue, 8 stages spread over this chunk's KB/2 k-steps
+    mma4<KB / 2>(A, bh, bl, acc, lane, [&](int st) {
+      if (c > 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (e * (KB / 2) / 8 == st) epi(c - 1, zq, e);
+      }
+    });
+    const float wi = A[2 * KB * 64 + 8].x;
+    const float4 b0 = A[2 * KB * 64 + g], b1 = A[2 * KB * 64 + 4 + g];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float inv = xinv[q] * wi;
+      zq.z[q][0] = fma4s(acc[q][0], inv, b0);
+      zq.z[q][1] = fma4s(acc[q][1], inv, b1);
+    }
+    if constexpr (AUX) {
+      zq.aux[0] = A[2 * KB * 64 + 16 + g];
+      zq.aux[1] = A[2 * KB * 64 + 20 + g];
+    }
+    if (c + 2 < NCH) ws.template flip<WS::template pieces<CB>()>();
+    else if (nxt) ws.template flip<WS::template pieces<NXT_CB>()>();
+    else ws.template flip<0>();
+  }
+  pd.flush();  // chunk NCH-2's stores, put by its epilogue in the last iteration
+#pragma unroll
+  for (int e = 0; e < 8; ++e) epi(NCH - 1, zq, e);
+}
+
+// ---- staged epilogues: operator()(c, z, st) does stage st (0..7) of chunk c's epilogue; stages
+// 4q..4q+3 handle column q (two values each, the fourth also splits the column's 8 outputs) ----
+template <bool NABLA>
+__device__ __forceinline__ void sp_pair(const Z4& zz, int q, int k, float4 (&y)[2], float4& s0, float4& s1) {
+  const int o = k >> 1;
+  const float4 z = zz.z[q][o];
+  float4& s = o ? s1 : s0;
+  if ((k & 1) == 0) {
+    softplus3<NABLA>(z.x, y[o].x, s.x);
+    softplus3<NABLA>(z.y, y[o].y, s.y);
+  } else {
+    softplus3<NABLA>(z.z, y[o].z, s.z);
+    softplus3<NABLA>(z.w, y[o].w, s.w);
+  }
+}
+__device__ __forceinline__ float4 mul4(float4 a, float4 b) { return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w); }
+// slab layout [block][column][lane]: the chunk's blocks 2c, 2c+1 of both columns = 4 KB
+__device__ __forceinline__ uint32_t opaque_lane(int lane) {  // not hoistable: offsets built at use
+  uint32_t l = (uint32_t)lane;
+  asm volatile("" : "+v"(l));
+  return l;
+}
+__device__ __forceinline__ void pend_chunk(Pend4& pd, float4* base, int first_blk, float4 c0b0, float4 c1b0,
+                                           float4 c0b1, float4 c1b1, int lane, bool nt) {
+  pd.v[0] = c0b0; pd.v[1] = c1b0; pd.v[2] = c0b1; pd.v[3] = c1b1;
+  const uint32_t l = opaque_lane(lane);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) pd.o[i] = (2 * first_blk + i) * 64 + l;
+  pd.put(base, 4, nt);
+}
+
+// forward softplus op: out -> next operand (k-step c of oh/ol), slab <- softplus'
+template <bool NABLA>
+struct FwdEpi4 {
+  f16x8 (&oh)[2][12];
+  f16x8 (&ol)[2][12];
+  const float (&sc)[2];
+  float4* sl;
+  float (&mrun)[2];
+  Pend4& pd;
+  int lane;
+  float4 y[2][2];
+  __device__ __forceinline__ void operator()(int c, const Z4& zz, int st) {
+    const int q = st >> 2, k = st & 3;
+    // softplus' goes straight into the pending-store slots ([block][column] order; the previous
+    // chunk's stores were flushed at the start of this iteration)
+    sp_pair<NABLA>(zz, q, k, y[q], pd.v[q], pd.v[2 + q]);
+    if (k == 3) {
+      mrun[q] = amax8(mrun[q], y[q][0], y[q][1]);
+      split8a(y[q][0], y[q][1], sc[q], oh[q][c], ol[q][c]);
+    }
+    if constexpr (NABLA)
+      if (st == 7) pend_chunk(pd, sl, 2 * c, pd.v[0], pd.v[1], pd.v[2], pd.v[3], lane, true);
+  }
+};
+
+// F7: softplus, sdf row (aux = W8[0, :]) as a running dot product, d sdf / d z7 parked in slab 7,
+// h7 split for F8 when the geometry feature is wanted
+template <bool NABLA, bool FEAT>
+struct F7Epi4 {
+  f16x8 (&oh)[2][12];
+  f16x8 (&ol)[2][12];
+  const float (&sc)[2];
+  float4* g7;
+  float (&mrun)[2];
+  float (&sdf_part)[2];
+  Pend4& pd;
+  int lane;
+  float4 y[2][2], s[2][2];
+  __device__ __forceinline__ void operator()(int c, const Z4& zz, int st) {
+    const int q = st >> 2, k = st & 3;
+    sp_pair<NABLA>(zz, q, k, y[q], s[q][0], s[q][1]);
+    if (k == 3) {
+      const float4 w0 = zz.aux[0], w1 = zz.aux[1];
+      float sp = sdf_part[q];
+      sp = fmaf(y[q][0].x, w0.x, sp); sp = fmaf(y[q][0].y, w0.y, sp);
+      sp = fmaf(y[q][0].z, w0.z, sp); sp = fmaf(y[q][0].w, w0.w, sp);
+      sp = fmaf(y[q][1].x, w1.x, sp); sp = fmaf(y[q][1].y, w1.y, sp);
+      sp = fmaf(y[q][1].z, w1.z, sp); sp = fmaf(y[q][1].w, w1.w, sp);
+      sdf_part[q] = sp;
+      if constexpr (NABLA) {
+        pd.v[q] = mul4(w0, s[q][0]);
+        pd.v[2 + q] = mul4(w1, s[q][1]);
+      }
+      if constexpr (FEAT) {
+        mrun[q] = amax8(mrun[q], y[q][0], y[q][1]);
+        split8a(y[q][0], y[q][1], sc[q], oh[q][c], ol[q][c]);
+      }
+    }
+    if constexpr (NABLA)
+      if (st == 7) pend_chunk(pd, g7, 2 * c, pd.v[0], pd.v[1], pd.v[2], pd.v[3], lane, false);
+  }
+};
+
+// backward op: out = Wᵀ G scaled by softplus'(z) of the layer below (slab staged into LDS in the
+// chunk's own iteration, read here, one iteration later); chunks >= NMAIN/2 are embedding
+// gradients, parked in fp32 from block park_blk on
+template <int NMAIN, class WS>
+struct BwdEpi4 {
+  f16x8 (&oh)[2][12];
+  f16x8 (&ol)[2][12];
+  const float (&sc)[2];
+  WS& ws;
+  float4* park;
+  int park_blk;
+  float (&mrun)[2];
+  Pend4& pd;
+  int lane;
+  float4 y[2][2];
+  __device__ __forceinline__ void operator()(int c, const Z4& zz, int st) {
+    if (2 * c < NMAIN) {
+      const int q = st >> 2, k = st & 3;
+      if (k < 2) {
+        const float4 sv = ws.slab_prev()[(2 * k + q) * 64 + lane];
+        y[q][k] = mul4(zz.z[q][k], sv);
+      } else if (k == 2) {
+        mrun[q] = amax8(mrun[q], y[q][0], y[q][1]);
+      } else {
+        split8a(y[q][0], y[q][1], sc[q], oh[q][c], ol[q][c]);
+      }
+    } else if (st == 7) {
+      pend_chunk(pd, park, park_blk + 2 * c - NMAIN, zz.z[0][0], zz.z[1][0], zz.z[0][1], zz.z[1][1], lane, false);
+    }
+  }
+};
+
+struct NoPre4 {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
+template <bool NABLA, bool FEAT>
+__global__ __attribute__((amdgpu_flat_work_group_size(kT4, kT4), amdgpu_waves_per_eu(1, 1)))
+void sdf4_kernel(SdfKArgs a) {
+  constexpr int CB = chunk_bytes(18);  // largest SDF op chunk (F4: 14 + 4 input blocks)
+  constexpr int C16 = chunk_bytes(16), C4 = chunk_bytes(4), C14 = chunk_bytes(14), C18 = chunk_bytes(18);
+  __shared__ __attribute__((aligned(16))) char smem[kRing * CB + (NABLA ? 2 * kSlab4 : 0)];
+  WStream4<CB> ws{smem, NABLA ? smem + kRing * CB : nullptr, 0, 0};
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  const char* W = a.packed;
+  // addresses are rebuilt from an opaque base at each use: hoisted out of the tile loop, the ~50
+  // chunk / slab addresses would pin (and spill) registers for the whole kernel
+  auto OP = [&](int i) {  // ops packed back to back (nr_mlp.h)
+    const char* w = W;
+    asm volatile("" : "+s"(w));
+    return w + sdf_op_off(i);
+  };
+  const float b8 = *(const float*)(W + a.L.misc_off);
+  // this wave's slabs: [layer 8][block 16][column 2][lane 64] float4 (256 KB)
+  float4* escr = uniform_ptr(a.scratch + (size_t)(blockIdx.x * kW4 + wave) * (8 * 16 * 2 * 64));
+  auto slab = [&](int l) {
+    float4* e = escr;
+    asm volatile("" : "+s"(e));
+    return e + l * 16 * 2 * 64;
+  };
+
+  ws.template start<C4, C4>(OP(F0), OP(F0) + C4);
+  Pend4 pd{};
+  NoPre4 nopre;
+  const float kSpSlack = 0.0070f;  // softplus(z) <= max(z, 0) + ln2/100
+
+  const int64_t Pn = a.P_dev ? min(a.P, (int64_t)(*a.P_dev) * a.P_mult) : a.P;
+  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < Pn; base += (int64_t)gridDim.x * kPointsPerWG) {
+    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < Pn;
+    const int64_t p0 = base + wave * 32;  // this wave's first point
+    int64_t pq[2];
+    bool valid[2];
+    float xs[2][3];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int64_t p = p0 + 16 * q + j;
+      valid[q] = p < Pn;
+      pq[q] = valid[q] ? p : Pn - 1;
+      xs[q][0] = a.pts[pq[q] * 3 + 0];
+      xs[q][1] = a.pts[pq[q] * 3 + 1];
+      xs[q][2] = a.pts[pq[q] * 3 + 2];
+    }
+    float4 E[2][4];
+    float mE[2], xinv[2];
+    f16x8 Uh[2][12], Ul[2][12], Vh[2][12], Vl[2][12];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int f = 16 * b + 4 * g;
+        E[q][b] = make_float4(embed_feature(f + 0, xs[q][0], xs[q][1], xs[q][2], a.nfreq),
+                              embed_feature(f + 1, xs[q][0], xs[q][1], xs[q][2], a.nfreq),
+                              embed_feature(f + 2, xs[q][0], xs[q][1], xs[q][2], a.nfreq),
+                              embed_feature(f + 3, xs[q][0], xs[q][1], xs[q][2], a.nfreq));
+      }
+      mE[q] = max4_groups(amax8(amax8(0.0f, E[q][0], E[q][1]), E[q][2], E[q][3]));
+      const float sE = bound_scale(mE[q]);  // exact-max scale for the embedding operand of F0
+      split8a(E[q][0], E[q][1], sE, Uh[q][0], Ul[q][0]);
+      split8a(E[q][2], E[q][3], sE, Uh[q][1], Ul[q][1]);
+      xinv[q] = 1.0f / sE;
+    }
+    // F4 (skip layer) needs the embedding again, split at F3's output scale: with a slab workspace
+    // it waits there (slab 7, blocks 12-15, free until F7) instead of in 32 registers
+    float4* epark = slab(7);
+    if constexpr (NABLA) {
+      const uint32_t l = opaque_lane(lane);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const uint32_t off = (((12 + b) * 2 + q) * 64 + l) * 16u;
+          const f32x4 d = tof(E[q][b]);
+          asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" : : "v"(off), "v"(d), "s"(epark) : "memory");
+        }
+    }
+    float mrun[2] = {0.0f, 0.0f};  // running max |output| of the op being computed (lane's values)
+    float m_in[2] = {mE[0], mE[1]};  // max |input| of the op being computed (per point)
+    // (R, B) of the op about to run ride in its chunks' bias slot (floats 33, 34); its chunk 0 is
+    // the current ring slot when it starts
+    auto next_scales = [&](int kb, float extra, const float (&floor_max)[2], float (&sc)[2]) {
+      const float4 v = ws.buf()[2 * kb * 64 + 8];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) sc[q] = bound_scale(fmaxf(fmaf(v.y, m_in[q], v.z) + extra, floor_max[q]));
+    };
+    auto finish = [&](const float (&sc)[2]) {  // end of an op: its output becomes the next operand
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        m_in[q] = max4_groups(mrun[q]);
+        mrun[q] = 0.0f;
+        xinv[q] = 1.0f / sc[q];
+      }
+    };
+    const float zero2[2] = {0.0f, 0.0f};
+    auto fwd_epi = [&](f16x8(&oh)[2][12], f16x8(&ol)[2][12], const float (&sc)[2], float4* sl) {
+      return FwdEpi4<NABLA>{oh, ol, sc, sl, mrun, pd, lane};
+    };
+
+    // ---- forward (base.py:243-257) -------------------------------------------------------------
+    {
+      float sc[2];
+      next_scales(4, kSpSlack, zero2, sc);
+      op4<4, 16, C16, false>(ws, OP(F0), OP(F1), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(0)), lane);
+      finish(sc);
+    }
+    {
+      float sc[2];
+      next_scales(16, kSpSlack, zero2, sc);
+      op4<16, 16, C16, false>(ws, OP(F1), OP(F2), Vh, Vl, xinv, pd, nopre, fwd_epi(Uh, Ul, sc, slab(1)), lane);
+      finish(sc);
+    }
+    {
+      float sc[2];
+      next_scales(16, kSpSlack, zero2, sc);
+      op4<16, 16, C16, false>(ws, OP(F2), OP(F3), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(2)), lane);
+      finish(sc);
+    }
+    {
+      // F3's outputs (h3: 217 rows in 14 blocks) and the embedding form F4's operand: one scale
+      float sc[2];
+      next_scales(16, kSpSlack, mE, sc);
+      op4<16, 14, C18, false>(ws, OP(F3), OP(F4), Vh, Vl, xinv, pd, nopre, fwd_epi(Uh, Ul, sc, slab(3)), lane);
+      if constexpr (NABLA) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) E[q][b] = fromf(*((const gf4*)epark + ((12 + b) * 2 + q) * 64 + lane));
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        split8a(E[q][0], E[q][1], sc[q], Uh[q][7], Ul[q][7]);
+        split8a(E[q][2], E[q][3], sc[q], Uh[q][8], Ul[q][8]);
+        mrun[q] = fmaxf(mrun[q], mE[q]);
+      }
+      finish(sc);
+    }
+    {
+      float sc[2];
+      next_scales(18, kSpSlack, zero2, sc);
+      op4<18, 16, C16, false>(ws, OP(F4), OP(F5), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(4)), lane);
+      finish(sc);
+    }
+    {
+      float sc[2];
+      next_scales(16, kSpSlack, zero2, sc);
+      op4<16, 16, C16, false>(ws, OP(F5), OP(F6), Vh, Vl, xinv, pd, nopre, fwd_epi(Uh, Ul, sc, slab(5)), lane);
+      finish(sc);
+    }
+    {
+      float sc[2];
+      next_scales(16, kSpSlack, zero2, sc);
+      op4<16, 16, C16, false>(ws, OP(F6), OP(F7), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(6)), lane);
+      finish(sc);
+    }
+    // F7: softplus, sdf row (aux = W8[0, :]) as a running dot product, d sdf / d z7 parked in slab 7,
+    // h7 split for F8 when the geometry feature is wanted
+    float sdf_part[2] = {0.0f, 0.0f};
+    {
+      float sc[2];
+      next_scales(16, kSpSlack, zero2, sc);
+      F7Epi4<NABLA, FEAT> epi{Uh, Ul, sc, slab(7), mrun, sdf_part, pd, lane};
+      constexpr int NXT = (NABLA || FEAT) ? C16 : C4;
+      const char* n = FEAT ? OP(F8) : (NABLA ? OP(B7) : (has_next ? OP(F0) : nullptr));
+      op4<16, 16, NXT, true>(ws, OP(F7), n, Vh, Vl, xinv, pd, nopre, epi, lane);
+      finish(sc);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float sdf = wave_sum4(sdf_part[q]) + b8;
+      if (valid[q] && g == 0) a.sdf[p0 + 16 * q + j] = sdf;
+    }
+    // ---- geometry feature rows 1..256 (no activation) ------------------------------------------
+    if constexpr (FEAT) {
+      const int64_t pf = p0 < Pn ? p0 : Pn - 1;
+      float4* fb = uniform_ptr((float4*)(a.feature + pf * 256));
+      // clamped lanes (past the end) rewrite the last point's row with that point's own values
+      uint32_t frow[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) frow[q] = (uint32_t)(pq[q] - pf);
+      auto epi = [&](int c, const Z4& zz, int st) {
+        if (st != 7) return;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          pd.v[2 * q] = zz.z[q][0];
+          pd.v[2 * q + 1] = zz.z[q][1];
+          const uint32_t r = opaque_lane(frow[q] * 64 + g);
+          pd.o[2 * q] = r + (2 * c) * 4;
+          pd.o[2 * q + 1] = r + (2 * c + 1) * 4;
+        }
+        pd.put(fb, 4, false);
+      };
+      constexpr int NXT = NABLA ? C16 : C4;
+      const char* n = NABLA ? OP(B7) : (has_next ? OP(F0) : nullptr);
+      op4<16, 16, NXT, false>(ws, OP(F8), n, Uh, Ul, xinv, pd, nopre, epi, lane);
+    }
+    if constexpr (NABLA) {
+      // ---- reverse pass (autograd.grad of sdf w.r.t. x, base.py:265-282) ------------------------
+      pd.flush();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      float4* g7 = slab(7);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {  // d sdf / d z7 from slab 7, split with the exact max scale
+        float4 G[16];
+#pragma unroll
+        for (int b = 0; b < 16; ++b) G[b] = fromf(*((const gf4*)g7 + (2 * b + q) * 64 + lane));
+        float m = 0.0f;
+#pragma unroll
+        for (int b = 0; b < 16; b += 2) m = amax8(m, G[b], G[b + 1]);
+        m_in[q] = max4_groups(m);
+        const float sc = bound_scale(m_in[q]);
+#pragma unroll
+        for (int s = 0; s < 8; ++s) split8a(G[2 * s], G[2 * s + 1], sc, Uh[q][s], Ul[q][s]);
+        xinv[q] = 1.0f / sc;
+      }
+      float4* park = slab(7);  // embedding gradients [block 8][column 2][lane]: skip layer 0-3, first layer 4-7
+      // backward op: out = Wᵀ G, scaled by softplus'(z) of the layer below (its slab, staged into
+      // LDS in the chunk's own iteration, read by its epilogue in the next); output chunks >=
+      // NMAIN/2 are embedding gradients, parked in fp32
+      auto bwd = [&](auto kb_tag, auto nbo_tag, auto nmain_tag, auto nxt_tag, int opi, const char* nxt,
+                     f16x8(&ih)[2][12], f16x8(&il)[2][12], f16x8(&oh)[2][12], f16x8(&ol)[2][12], int lcur,
+                     int park_blk) {
+        constexpr int KBo = decltype(kb_tag)::value, NBOo = decltype(nbo_tag)::value;
+        constexpr int NMAIN = decltype(nmain_tag)::value, NXC = decltype(nxt_tag)::value;
+        float sc[2];
+        next_scales(KBo, 0.0f, zero2, sc);
+        auto pre = [&](int c) {
+          if (2 * c < NMAIN) ws.stage_slab(slab(lcur), c);
+        };
+        BwdEpi4<NMAIN, WStream4<CB>> epi{oh, ol, sc, ws, park, park_blk, mrun, pd, lane};
+        op4<KBo, NBOo, NXC, false>(ws, OP(opi), nxt, ih, il, xinv, pd, pre, epi, lane);
+        finish(sc);
+      };
+      using I0 = std::integral_constant<int, 0>;
+      using I4 = std::integral_constant<int, 4>;
+      using I14 = std::integral_constant<int, 14>;
+      using I16 = std::integral_constant<int, 16>;
+      using I18 = std::integral_constant<int, 18>;
+      using IC16 = std::integral_constant<int, C16>;
+      using IC14 = std::integral_constant<int, C14>;
+      using IC4 = std::integral_constant<int, C4>;
+      bwd(I16{}, I16{}, I16{}, IC16{}, B7, OP(B6), Uh, Ul, Vh, Vl, 6, 0);
+      bwd(I16{}, I16{}, I16{}, IC16{}, B6, OP(B5), Vh, Vl, Uh, Ul, 5, 0);
+      bwd(I16{}, I16{}, I16{}, IC16{}, B5, OP(B4), Uh, Ul, Vh, Vl, 4, 0);
+      // skip layer: rows 0..216 -> h3 (scaled by softplus'(z3)), rows 217..255 -> embedding
+      bwd(I16{}, I18{}, I14{}, IC14{}, B4, OP(B3), Vh, Vl, Uh, Ul, 3, 0);
+      bwd(I14{}, I16{}, I16{}, IC16{}, B3, OP(B2), Uh, Ul, Vh, Vl, 2, 0);
+      bwd(I16{}, I16{}, I16{}, IC16{}, B2, OP(B1), Vh, Vl, Uh, Ul, 1, 0);
+      bwd(I16{}, I16{}, I16{}, IC16{}, B1, OP(B0), Uh, Ul, Vh, Vl, 0, 0);
+      bwd(I16{}, I4{}, I0{}, IC4{}, B0, has_next ? OP(F0) : nullptr, Vh, Vl, Uh, Ul, 0, 4);
+      pd.flush();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // chain rule through the positional encoding (autograd sums both uses of embed(x))
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        float n0 = 0.f, n1 = 0.f, n2 = 0.f;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const float4 u = fromf(*((const gf4*)park + (2 * b + q) * 64 + lane));
+          const float4 v = fromf(*((const gf4*)park + (2 * (4 + b) + q) * 64 + lane));
+          const int f = 16 * b + 4 * g;
+          embed_backward(f + 0, fadd(v.x, u.x), xs[q][0], xs[q][1], xs[q][2], a.nfreq, n0, n1, n2);
+          embed_backward(f + 1, fadd(v.y, u.y), xs[q][0], xs[q][1], xs[q][2], a.nfreq, n0, n1, n2);
+          embed_backward(f + 2, fadd(v.z, u.z), xs[q][0], xs[q][1], xs[q][2], a.nfreq, n0, n1, n2);
+          embed_backward(f + 3, fadd(v.w, u.w), xs[q][0], xs[q][1], xs[q][2], a.nfreq, n0, n1, n2);
+        }
+        n0 = wave_sum4(n0);
+        n1 = wave_sum4(n1);
+        n2 = wave_sum4(n2);
+        if (valid[q] && g == 0) {
+          const int64_t p = p0 + 16 * q + j;
+          a.nabla[p * 3 + 0] = n0;
+          a.nabla[p * 3 + 1] = n1;
+          a.nabla[p * 3 + 2] = n2;
+        }
+      }
+    }
+  }
+  pd.flush();
   wait_vmcnt(0);  // a block without tiles still has the prologue's second chunk in flight
 }
 
@@ -933,6 +1661,18 @@ __global__ void pack_op_kernel(PackOp op, uint32_t* __restrict__ dst, int64_t n)
       }
     } else if (idx == 32) {
       v = 1.0f / wscale(op);
+    } else if ((idx == 33 || idx == 34) && op.bound) {
+      v = op.bound[idx - 33];
+    } else if (idx >= 64 && idx < 96 && op.aux) {
+      int ob_loc = 2 * c + (idx - 64) / 16;
+      for (int s = 0; s < 2; ++s) {
+        if (ob_loc < op.out[s].nblk) {
+          const int rl = 16 * ob_loc + (idx & 15);
+          if (rl < op.out[s].nvalid) v = op.aux[op.out[s].off + rl];
+          break;
+        }
+        ob_loc -= op.out[s].nblk;
+      }
     }
     dst[e] = __float_as_uint(v);
     return;
@@ -969,6 +1709,33 @@ __global__ void maxabs_kernel(const float* __restrict__ W, int64_t n, float scal
   if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
 }
 
+// bound[0] = max over packed output rows of sum_k |W * scale| (row L1 norm of the op's effective
+// matrix), bound[1] = max |bias|; one thread per output row (bound zeroed beforehand)
+__global__ void bound_kernel(PackOp op, unsigned* __restrict__ bound) {
+  const int KB = op.in[0].nblk + op.in[1].nblk;
+  const int NBO = op.out[0].nblk + op.out[1].nblk;
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= NBO * 16) return;
+  const int ob = r >> 4, i = r & 15;
+  float s = 0.0f;
+  for (int b = 0; b < KB; ++b)
+    for (int fi = 0; fi < 16; ++fi) s += fabsf(pack_src(op, ob, i, b, fi));
+  float bb = 0.0f;
+  if (op.bias) {
+    int ob_loc = ob;
+    for (int q = 0; q < 2; ++q) {
+      if (ob_loc < op.out[q].nblk) {
+        const int rl = 16 * ob_loc + i;
+        if (rl < op.out[q].nvalid) bb = fabsf(op.bias[op.out[q].off + rl]);
+        break;
+      }
+      ob_loc -= op.out[q].nblk;
+    }
+  }
+  atomicMax(bound, __float_as_uint(s * 1.0001f));  // margin for the summation's rounding
+  atomicMax(bound + 1, __float_as_uint(bb));
+}
+
 __global__ void pack_vec_kernel(const float* __restrict__ src, int off, int nvalid, int n, float* __restrict__ dst) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
@@ -985,6 +1752,11 @@ int launch_pack_op(const PackOp& op, char* dst, hipStream_t stream) {
     NR_REQUIRE(op.wmax, NR_ERR_ARG, "pack: f16x3 needs a max-|W| word");
     NR_HIP_CHECK(hipMemsetAsync(op.wmax, 0, sizeof(float), stream));
     hipLaunchKernelGGL(maxabs_kernel, dim3(64), dim3(256), 0, stream, op.W, op.wn, op.scale, (unsigned*)op.wmax);
+    NR_HIP_CHECK(hipGetLastError());
+  }
+  if (op.bound) {
+    NR_HIP_CHECK(hipMemsetAsync(op.bound, 0, 2 * sizeof(float), stream));
+    hipLaunchKernelGGL(bound_kernel, dim3((NBO * 16 + 63) / 64), dim3(64), 0, stream, op, (unsigned*)op.bound);
     NR_HIP_CHECK(hipGetLastError());
   }
   const int64_t n = (int64_t)(NBO / 2) * (2 * KB + 1) * 256;
@@ -1017,10 +1789,16 @@ int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t
   if (nabla) {
     const size_t need = (size_t)grid * kScratchPerWG;
     NR_REQUIRE(ws && ws_bytes >= need, NR_ERR_WORKSPACE, "sdf nabla workspace too small");
-    if (L.prec == NR_PREC_F16X3) hipLaunchKernelGGL((sdf_kernel<NR_PREC_F16X3, true>), dim3(grid), dim3(kThreads), 0, stream, a);
+    if (L.prec == NR_PREC_F16X3) {
+      if (feature) hipLaunchKernelGGL((sdf4_kernel<true, true>), dim3(grid), dim3(kT4), 0, stream, a);
+      else hipLaunchKernelGGL((sdf4_kernel<true, false>), dim3(grid), dim3(kT4), 0, stream, a);
+    }
     else hipLaunchKernelGGL((sdf_kernel<NR_PREC_FP32, true>), dim3(grid), dim3(kThreads), 0, stream, a);
   } else {
-    if (L.prec == NR_PREC_F16X3) hipLaunchKernelGGL((sdf_kernel<NR_PREC_F16X3, false>), dim3(grid), dim3(kThreads), 0, stream, a);
+    if (L.prec == NR_PREC_F16X3) {
+      if (feature) hipLaunchKernelGGL((sdf4_kernel<false, true>), dim3(grid), dim3(kT4), 0, stream, a);
+      else hipLaunchKernelGGL((sdf4_kernel<false, false>), dim3(grid), dim3(kT4), 0, stream, a);
+    }
     else hipLaunchKernelGGL((sdf_kernel<NR_PREC_FP32, false>), dim3(grid), dim3(kThreads), 0, stream, a);
   }
   NR_HIP_CHECK(hipGetLastError());

@@ -15,21 +15,34 @@ VARIANTS = {
     'noestore': ['-DNR_EXP_NO_ESTORE'],
     'noeload': ['-DNR_EXP_NO_ELOAD'],
     'noslab': ['-DNR_EXP_NO_ESTORE', '-DNR_EXP_NO_ELOAD'],
+    'nosoftplus': ['-DNR_EXP_NO_SOFTPLUS'],
+    'nosplit': ['-DNR_EXP_NO_SPLIT'],
+    'nobarrier': ['-DNR_EXP_NO_BARRIER'],
+    'novalu': ['-DNR_EXP_NO_SOFTPLUS', '-DNR_EXP_NO_SPLIT'],
+    'unroll': ['-DNR_EXP_UNROLL'],
+    'nopp': ['-DNR_EXP_NO_PINGPONG'],
+    'unroll_nosplit': ['-DNR_EXP_UNROLL', '-DNR_EXP_NO_SPLIT'],
 }
 
 
-def main(names):
+def one(name):
     out_dir = os.path.join(ROOT, 'neurecon_amd', '_exp')
-    os.makedirs(out_dir, exist_ok=True)
-    for name in names:
-        objs = []
-        for src in B._sources():
-            obj = os.path.join(out_dir, f'{name}_{os.path.basename(src)}.o')
-            subprocess.check_call([B.HIPCC] + B.FLAGS + VARIANTS[name] + ['-c', src, '-o', obj])
-            objs.append(obj)
-        lib = os.path.join(out_dir, f'libnrhip_{name}.so')
-        subprocess.check_call([B.HIPCC, '-shared', '-fPIC', f'--offload-arch={B.ARCH}', '-o', lib] + objs)
-        print(lib)
+    objs = []
+    for src in B._sources():
+        obj = os.path.join(out_dir, f'{name}_{os.path.basename(src)}.o')
+        subprocess.check_call([B.HIPCC] + B.FLAGS + VARIANTS[name] + ['-c', src, '-o', obj])
+        objs.append(obj)
+    lib = os.path.join(out_dir, f'libnrhip_{name}.so')
+    subprocess.check_call([B.HIPCC, '-shared', '-fPIC', f'--offload-arch={B.ARCH}', '-o', lib] + objs)
+    return lib
+
+
+def main(names):
+    import concurrent.futures as cf
+    os.makedirs(os.path.join(ROOT, 'neurecon_amd', '_exp'), exist_ok=True)
+    with cf.ThreadPoolExecutor(4) as ex:
+        for lib in ex.map(one, names):
+            print(lib)
 
 
 if __name__ == '__main__':
