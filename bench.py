@@ -32,8 +32,8 @@ MAC_RAD = 271_360                 # SURVEY §8(a) A7, NeuS radiance input 289
 RAY_FLOP = 704.8e6                # 128 no-grad SDF + 255 SDF-with-nabla + 127 radiance
 # HBM-side bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc passes of this bench,
 # tools/gpu_pmc.sh); counters cannot be read live, so the latest committed summary is reported.
-PMC_SUMMARY = {'f16x3': 'profiles/r01/f16x3_pmc_summary.json'}
-PMC_KERNEL = {('sdf_nabla', 'f16x3'): 'void nr::sdf_kernel<1, true>(nr::SdfKArgs)',
+PMC_SUMMARY = {'f16x3': 'profiles/r01/f16x3_pmc_summary.json'}  # refreshed with tools/gpu_pmc.sh
+PMC_KERNEL = {('sdf_nabla', 'f16x3'): 'void nr::sdf4_kernel<true, false>(nr::SdfKArgs)',
               ('sdf_nabla', 'fp32'): 'void nr::sdf_kernel<0, true>(nr::SdfKArgs)'}
 
 
@@ -45,7 +45,7 @@ def parse():
     ap.add_argument('--rays', type=int, default=4096)
     ap.add_argument('--precision', default=os.environ.get('NR_PRECISION', 'f16x3'), choices=['f16x3', 'fp32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-rays', type=int, default=1024)
+    ap.add_argument('--cpu-rays', type=int, default=4096)
     return ap.parse_args()
 
 
@@ -93,15 +93,16 @@ def cpu_baseline(n_rays):
     orc = NeuSOracle(sd)
     c2w, K = camera('cpu')
     ro, rd, _ = orays.get_rays(c2w, K, 64, 64)
-    idx = torch.linspace(0, 4095, n_rays).round().long()
-    ro, rd = ro[:, idx], rd[:, idx]
+    if n_rays < 4096:
+        idx = torch.linspace(0, 4095, n_rays).round().long()
+        ro, rd = ro[:, idx], rd[:, idx]
     with torch.no_grad():
         orc.render(ro[:, :32], rd[:, :32])  # warm-up
         t = time.perf_counter()
         orc.render(ro, rd)
         dt = time.perf_counter() - t
     return {'value': round(n_rays / dt, 2), 'unit': 'rays/s', 'cores': threads, 'kind': 'port',
-            'sample': f'{n_rays} of the 4096 config-(b) rays (evenly spaced), oracle/neus.py, '
+            'sample': f'{n_rays} of the 4096 config-(b) rays, oracle/neus.py, '
                       f'torch {torch.__version__} CPU fp32, {threads} threads, {dt:.1f} s'}
 
 

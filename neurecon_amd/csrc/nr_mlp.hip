@@ -65,6 +65,18 @@ __device__ __forceinline__ void glds16s(const char* sbase, uint32_t voff, uint32
       : "memory");
 }
 
+// ... with M0 declared clobbered instead of saved and restored around every piece (the v3 kernel
+// issues ~9 pieces per chunk per wave; the compiler re-materialises M0 where it needs it)
+__device__ __forceinline__ void glds16m(const char* sbase, uint32_t voff, uint32_t lds_addr) {
+  asm volatile(
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, %1"
+      :
+      : "v"(voff), "s"(sbase), "s"(lds_addr)
+      : "memory", "m0");
+}
+
 // a pointer every lane of the wave agrees on, forced into SGPRs
 template <class T>
 __device__ __forceinline__ T* uniform_ptr(T* p) {
@@ -728,9 +740,25 @@ __device__ __forceinline__ void split8s(float4 a, float4 b, float sc, f16x8& h, 
   h = __builtin_bit_cast(f16x8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
   l = __builtin_bit_cast(f16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
 }
-// ... parked in AGPRs: B operands are read only by MFMAs, which take AGPR sources directly
+// ... with the lo halves from v_fma_mix (f16(v*sc - hi) fused, written straight into the packed
+// halves), parked in AGPRs: B operands are read only by MFMAs, which take AGPR sources directly
 __device__ __forceinline__ void split8a(float4 a, float4 b, float sc, f16x8& h, f16x8& l) {
-  split8s(a, b, sc, h, l);
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint32_t hw[4], lw[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f2v p = f2v{v[2 * i], v[2 * i + 1]} * f2v{sc, sc};
+    const uint32_t hh = cvt_pk_h(p.x, p.y);
+    uint32_t lo;
+    asm volatile("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(lo) : "v"(v[2 * i]), "v"(sc), "v"(hh));
+    asm volatile("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+                 : "+v"(lo)
+                 : "v"(v[2 * i + 1]), "v"(sc), "v"(hh));
+    hw[i] = hh;
+    lw[i] = lo;
+  }
+  h = __builtin_bit_cast(f16x8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
+  l = __builtin_bit_cast(f16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
   asm volatile("" : "+a"(h), "+a"(l));
 }
 __device__ __forceinline__ float max3abs(float m, float a, float b) {
@@ -758,6 +786,26 @@ __device__ __forceinline__ void softplus3(float z, float& y, float& s) {
   const float yy = __builtin_amdgcn_logf(u) * (0.693147180559945309f * 0.01f);
   y = lin ? z : yy;
   if constexpr (DERIV) s = lin ? 1.0f : ex * __builtin_amdgcn_rcpf(u);
+}
+// the same on a pair, with packed fp32 arithmetic and 100 log2(e) folded into one multiply
+// (the linear-branch test t > 20 becomes t log2(e) > 20 log2(e); differs from softplus3 by
+// rounding only)
+template <bool DERIV>
+__device__ __forceinline__ void softplus_pk(float z0, float z1, float& y0, float& y1, float& s0, float& s1) {
+  const f2v z = {z0, z1};
+  const f2v t = z * f2v{144.269504088896341f, 144.269504088896341f};
+  const f2v ex = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+  const f2v u = ex + f2v{1.0f, 1.0f};
+  const f2v yy = f2v{__builtin_amdgcn_logf(u.x), __builtin_amdgcn_logf(u.y)} *
+                 f2v{0.693147180559945309f * 0.01f, 0.693147180559945309f * 0.01f};
+  const bool l0 = t.x > 28.8539008f, l1 = t.y > 28.8539008f;
+  y0 = l0 ? z0 : yy.x;
+  y1 = l1 ? z1 : yy.y;
+  if constexpr (DERIV) {
+    const f2v sv = ex * f2v{__builtin_amdgcn_rcpf(u.x), __builtin_amdgcn_rcpf(u.y)};
+    s0 = l0 ? 1.0f : sv.x;
+    s1 = l1 ? 1.0f : sv.y;
+  }
 }
 __device__ __forceinline__ float4 fma4s(f32x4 a, float m, float4 b) {
   const f2v m2 = {m, m};
@@ -829,6 +877,9 @@ struct WStream4 {
   __device__ __forceinline__ static constexpr int pieces() { return (BYTES / 1024 + kW4 - 1) / kW4; }
   template <int BYTES>
   __device__ __forceinline__ void dma(const char* gsrc, int slot) {
+#ifdef NR_EXP_NO_DMA
+    return;
+#endif
     const int wave = wave_id();
     const uint32_t voff = (threadIdx.x & 63) * 16;
     const char* g = uniform_ptr(gsrc);
@@ -838,7 +889,7 @@ struct WStream4 {
       int off = (wave + i * kW4) * 1024;
       if (i == pieces<BYTES>() - 1 && off > BYTES - 1024) off = BYTES - 1024;
       off = __builtin_amdgcn_readfirstlane(off);
-      glds16s(g + off, voff, base + off);
+      glds16m(g + off, voff, base + off);
     }
   }
   template <int B0, int B1>
@@ -859,7 +910,7 @@ struct WStream4 {
     const uint32_t base =
         __builtin_amdgcn_readfirstlane(lds_u32(slab) + (uint32_t)(es * kSlab4 + wave_id() * 4096));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds16s(g + i * 1024, voff, base + i * 1024);
+    for (int i = 0; i < 4; ++i) glds16m(g + i * 1024, voff, base + i * 1024);
   }
   // the slab staged in the previous iteration (the chunk whose epilogue runs now)
   __device__ __forceinline__ const float4* slab_prev() const {
@@ -875,7 +926,9 @@ struct WStream4 {
   template <int PEND>
   __device__ __forceinline__ void flip() {
     wait_vmcnt(PEND);
+#ifndef NR_EXP_NO_BARRIER
     __syncthreads();
+#endif
     cur = (cur + 1) % kRing;
     es ^= 1;
   }
@@ -946,6 +999,10 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
     f32x4 acc[2][2] = {};
     // the previous chunk's epilogue, 8 stages spread over this chunk's KB/2 k-steps
     mma4<KB / 2>(A, bh, bl, acc, lane, [&](int st) {
+#ifdef NR_EXP_NO_EPI
+      if (c > 0 && st == 7) epi(c - 1, zq, 7);
+      return;
+#endif
       if (c > 0) {
 #pragma unroll
         for (int e = 0; e < 8; ++e)
@@ -980,13 +1037,8 @@ __device__ __forceinline__ void sp_pair(const Z4& zz, int q, int k, float4 (&y)[
   const int o = k >> 1;
   const float4 z = zz.z[q][o];
   float4& s = o ? s1 : s0;
-  if ((k & 1) == 0) {
-    softplus3<NABLA>(z.x, y[o].x, s.x);
-    softplus3<NABLA>(z.y, y[o].y, s.y);
-  } else {
-    softplus3<NABLA>(z.z, y[o].z, s.z);
-    softplus3<NABLA>(z.w, y[o].w, s.w);
-  }
+  if ((k & 1) == 0) softplus_pk<NABLA>(z.x, z.y, y[o].x, y[o].y, s.x, s.y);
+  else softplus_pk<NABLA>(z.z, z.w, y[o].z, y[o].w, s.z, s.w);
 }
 __device__ __forceinline__ float4 mul4(float4 a, float4 b) { return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w); }
 // slab layout [block][column][lane]: the chunk's blocks 2c, 2c+1 of both columns = 4 KB

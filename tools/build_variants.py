@@ -21,6 +21,10 @@ VARIANTS = {
     'novalu': ['-DNR_EXP_NO_SOFTPLUS', '-DNR_EXP_NO_SPLIT'],
     'unroll': ['-DNR_EXP_UNROLL'],
     'nopp': ['-DNR_EXP_NO_PINGPONG'],
+    'v3nodma': ['-DNR_EXP_NO_DMA'],
+    'v3nobar': ['-DNR_EXP_NO_BARRIER'],
+    'v3noepi': ['-DNR_EXP_NO_EPI'],
+    'v3noslab': ['-DNR_EXP_NO_ESTORE', '-DNR_EXP_NO_ELOAD'],
     'unroll_nosplit': ['-DNR_EXP_UNROLL', '-DNR_EXP_NO_SPLIT'],
 }
 
