@@ -95,7 +95,15 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
     case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;  // callers stay <= 15
   }
 }
 
@@ -697,9 +705,10 @@ __global__ __launch_bounds__(kThreads) void sdf_kernel(SdfKArgs a) {
 }
 
 // =============================================================================================
-// f16x3 SDF pipeline v2 (sdf3_kernel)
+// f16x3 operand helpers of the v3 SDF pipeline (sdf4_kernel, below)
 // =============================================================================================
-// What changes against sdf_kernel<F16X3>:
+// What changes against sdf_kernel<F16X3> (which stays the reference design for the radiance and
+// NeRF++ kernels):
 //  * The B operand of op l+1 is split into f16 hi/lo fragments by op l's epilogue, one k-step per
 //    chunk (chunk c of op l produces exactly k-step c of op l+1), instead of in one burst of
 //    ~300 VALU per layer in which every wave of the workgroup idles its matrix core.  The per-point
@@ -710,10 +719,7 @@ __global__ __launch_bounds__(kThreads) void sdf_kernel(SdfKArgs a) {
 //    bound is loose by ~10-50x in practice, leaving the outputs near 2^9..2^10 where hi + lo still
 //    carry 22 significant bits (lo turns subnormal only 2^-17 below the bound).
 //  * No fp32 copy of the activations is kept, chunk loops are fully unrolled (no register
-//    rotation), and every DMA count / vmcnt is a compile-time constant.
-//  * Ping-pong wave groups: waves 0-3 (one per SIMD) run [MFMA(c) -> epilogue(c)] per chunk,
-//    waves 4-7 run [epilogue(c-1) -> MFMA(c)], so each SIMD's matrix core is fed by one wave
-//    while the other does its VALU epilogue (activation, slab I/O, operand split).
+//    rotation), and every DMA count is a compile-time constant.
 //  * The reverse pass stores softplus'(z) = sigmoid(100 z) itself (1 on torch's linear branch),
 //    so the backward epilogue is one multiply.
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -841,8 +847,10 @@ struct Pend4 {
   bool nt;
   // global_store_dwordx4 with an SGPR base and a 32-bit VGPR byte offset (saddr form), from asm:
   // compiler-built 64-bit per-lane addresses get hoisted out of the tile loop and spilled
-  __device__ __forceinline__ void flush() {
+  __device__ __forceinline__ int flush() {
+    int issued = 0;
     if (base) {
+      issued = n;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if (i < n) {
@@ -856,6 +864,7 @@ struct Pend4 {
       }
       base = nullptr;
     }
+    return issued;
   }
   __device__ __forceinline__ void put(float4* b, int cnt, bool nontemporal) {
     base = b;
@@ -923,9 +932,13 @@ struct WStream4 {
     asm volatile("" : "+s"(off));
     return (const float4*)(lds + off);
   }
+  // PEND: the newest chunk's DMA pieces; extra: stores issued after them in this iteration
+  // (vmcnt retires in issue order, so they are simply not waited for)
   template <int PEND>
-  __device__ __forceinline__ void flip() {
-    wait_vmcnt(PEND);
+  __device__ __forceinline__ void flip(int extra = 0) {
+    static_assert(PEND + 4 <= 15, "vmcnt switch covers 0..15");
+    if (extra == 4) wait_vmcnt(PEND + 4);
+    else wait_vmcnt(PEND);
 #ifndef NR_EXP_NO_BARRIER
     __syncthreads();
 #endif
@@ -962,6 +975,10 @@ __device__ __forceinline__ void mma4(const float4* __restrict__ A, const f16x8 (
       acc[q][0] = mfma16h(h0, bh[q][s], acc[q][0]);
       acc[q][1] = mfma16h(h1, bh[q][s], acc[q][1]);
     }
+    // the next step's 4 fragment reads ahead of this step's MFMAs (a whole region of prefetch
+    // distance); the epilogue VALU is left to the scheduler
+    if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -987,7 +1004,6 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
   Z4 zq{};
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    pd.flush();
     pre(c);
     // opaque per chunk: keeps the scheduler from computing every chunk's address up front
     const char* opc = op;
@@ -995,6 +1011,9 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
     asm volatile("" : "+s"(opc), "+s"(nxc));
     if (c + 2 < NCH) ws.template issue<CB>(opc + (c + 2) * CB);
     else if (nxc) ws.template issue<NXT_CB>(nxc + (c + 2 - NCH) * NXT_CB);
+    // the previous chunk's stores go out after this chunk's weight DMA: this chunk's flip does not
+    // wait for them (the next one does, two chunk-times after issue)
+    const int nst = pd.flush();
     const float4* A = ws.buf();
     f32x4 acc[2][2] = {};
     // the previous chunk's epilogue, 8 stages spread over this chunk's KB/2 k-steps
@@ -1021,9 +1040,9 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
       zq.aux[0] = A[2 * KB * 64 + 16 + g];
       zq.aux[1] = A[2 * KB * 64 + 20 + g];
     }
-    if (c + 2 < NCH) ws.template flip<WS::template pieces<CB>()>();
-    else if (nxt) ws.template flip<WS::template pieces<NXT_CB>()>();
-    else ws.template flip<0>();
+    if (c + 2 < NCH) ws.template flip<WS::template pieces<CB>()>(nst);
+    else if (nxt) ws.template flip<WS::template pieces<NXT_CB>()>(nst);
+    else ws.template flip<0>(0);
   }
   pd.flush();  // chunk NCH-2's stores, put by its epilogue in the last iteration
 #pragma unroll

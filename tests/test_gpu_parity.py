@@ -214,3 +214,29 @@ def test_neus_direct_upsampling_vs_golden(golden, algo):
     ray_ok = (ok_rgb.all(-1) & ok_dep).reshape(-1)
     assert ray_ok[same].all()
     assert same.mean() >= 0.5 and ray_ok.mean() >= 0.9
+
+
+@pytest.mark.parametrize('gain', [1.0, 1.6])
+def test_f16x3_sdf_net_ragged_and_scaled(gain):
+    """f16x3 operand scales come from per-layer bounds (nr_mlp.hip, v3 pipeline): ragged sizes,
+    far / near-origin points and weights scaled up (activations growing layer to layer) must stay
+    within the f16x3 bar against the oracle -- no overflow, no lost precision."""
+    from oracle.nets import SDFNet
+    sd = wg.neus_state(seed=5)
+    sd = {k: (v * gain if k.endswith('weight_g') else v) for k, v in sd.items()}
+    m = neus_model(sd, precision='f16x3')
+    orc = SDFNet(sd)
+    torch.manual_seed(1)
+    for P in (1, 17, 129, 1000, 5000):
+        x = torch.randn(P, 3) * 0.7
+        x[: P // 3] *= 4.0    # far points (large embedding arguments, large activations)
+        x[-(P // 3):] *= 1e-3  # near the origin
+        ref_s, ref_n, ref_h = orc.forward_with_nablas(x)
+        with torch.no_grad():
+            s, n, h = m.implicit_surface.forward_with_nablas(x.cuda())
+            s0 = m.implicit_surface.forward(x.cuda())
+        scale = float(ref_s.abs().max())
+        assert report(f'f16x3 sdf P={P} gain={gain}', s, ref_s, 1e-4, 1e-6 * scale)[0].all()
+        assert report(f'f16x3 sdf(no grad) P={P}', s0, ref_s, 1e-4, 1e-6 * scale)[0].all()
+        assert report(f'f16x3 nabla P={P}', n, ref_n, 1e-3, 1e-3 * float(ref_n.abs().max()))[0].all()
+        assert report(f'f16x3 h P={P}', h, ref_h, 1e-4, 1e-5 * float(ref_h.abs().max()))[0].all()
