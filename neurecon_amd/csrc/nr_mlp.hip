@@ -884,21 +884,54 @@ struct WStream4 {
   // piece: identical bytes to the same LDS address) so the count is one constant in every wave
   template <int BYTES>
   __device__ __forceinline__ static constexpr int pieces() { return (BYTES / 1024 + kW4 - 1) / kW4; }
+  // Each wave moves a contiguous run of NPW pieces (the last wave's run is shifted back to end at
+  // the chunk's end; overlapping pieces are identical bytes to the same LDS address), up to 4 per
+  // M0 setting: the instruction offset steps the global and the LDS address together.
   template <int BYTES>
   __device__ __forceinline__ void dma(const char* gsrc, int slot) {
 #ifdef NR_EXP_NO_DMA
     return;
 #endif
+    constexpr int NB = BYTES / 1024, NPW = pieces<BYTES>();
     const int wave = wave_id();
     const uint32_t voff = (threadIdx.x & 63) * 16;
-    const char* g = uniform_ptr(gsrc);
-    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_u32(lds) + (uint32_t)(slot * CBMAX));
+    const int first = __builtin_amdgcn_readfirstlane(min(wave * NPW, NB - NPW));
+    const char* g = uniform_ptr(gsrc) + first * 1024;
+    const uint32_t base =
+        __builtin_amdgcn_readfirstlane(lds_u32(lds) + (uint32_t)(slot * CBMAX) + (uint32_t)(first * 1024));
 #pragma unroll
-    for (int i = 0; i < pieces<BYTES>(); ++i) {
-      int off = (wave + i * kW4) * 1024;
-      if (i == pieces<BYTES>() - 1 && off > BYTES - 1024) off = BYTES - 1024;
-      off = __builtin_amdgcn_readfirstlane(off);
-      glds16m(g + off, voff, base + off);
+    for (int j = 0; j < NPW; j += 4) {
+      const char* gj = g + j * 1024;
+      const uint32_t mj = base + j * 1024;
+      if (NPW - j >= 4)
+        asm volatile(
+            "s_mov_b32 m0, %2\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %0, %1\n\t"
+            "global_load_lds_dwordx4 %0, %1 offset:1024\n\t"
+            "global_load_lds_dwordx4 %0, %1 offset:2048\n\t"
+            "global_load_lds_dwordx4 %0, %1 offset:3072"
+            :
+            : "v"(voff), "s"(gj), "s"(mj)
+            : "memory", "m0");
+      else if (NPW - j == 3)
+        asm volatile(
+            "s_mov_b32 m0, %2\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %0, %1\n\t"
+            "global_load_lds_dwordx4 %0, %1 offset:1024\n\t"
+            "global_load_lds_dwordx4 %0, %1 offset:2048"
+            :
+            : "v"(voff), "s"(gj), "s"(mj)
+            : "memory", "m0");
+      else if (NPW - j == 2)
+        asm volatile(
+            "s_mov_b32 m0, %2\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %0, %1\n\t"
+            "global_load_lds_dwordx4 %0, %1 offset:1024"
+            :
+            : "v"(voff), "s"(gj), "s"(mj)
+            : "memory", "m0");
+      else
+        glds16m(gj, voff, mj);
     }
   }
   template <int B0, int B1>
@@ -1075,7 +1108,15 @@ __device__ __forceinline__ void pend_chunk(Pend4& pd, float4* base, int first_bl
   pd.put(base, 4, nt);
 }
 
-// forward softplus op: out -> next operand (k-step c of oh/ol), slab <- softplus'
+// forward softplus op: out -> next operand (k-step c of oh/ol), slab <- softplus'.
+// Staged by operation, not by value: each stage applies one step of the softplus to all 16 values
+// of the chunk (2 columns x 2 blocks x 4), so the ~24 VALU a k-step region receives are
+// independent of each other and issue back to back between its MFMAs (a value-by-value chain
+// would stall the single wave on every transcendental's latency).
+//   y = max(log2(1 + 2^t) ln2/100, z), t = min(100 log2(e) z, 126); s = 2^t / (1 + 2^t)
+// equals torch's softplus(beta=100, threshold=20) / softplus_backward up to ~1e-10 relative: on
+// the linear branch (100 z > 20) the log path exceeds z by log1p(e^-100z)/100 < 2e-11, and where
+// the clamp bites (z > 0.873) the max returns z itself; s there is 1 - 2^-126.
 template <bool NABLA>
 struct FwdEpi4 {
   f16x8 (&oh)[2][12];
@@ -1085,18 +1126,72 @@ struct FwdEpi4 {
   float (&mrun)[2];
   Pend4& pd;
   int lane;
-  float4 y[2][2];
+  float e[16], w[16], y[16];  // value i = (2q + o) * 4 + r: column q, block o, register r
+  __device__ __forceinline__ static float zval(const Z4& zz, int i) {
+    const float4 v = zz.z[i >> 3][(i >> 2) & 1];
+    const int r = i & 3;
+    return r == 0 ? v.x : (r == 1 ? v.y : (r == 2 ? v.z : v.w));
+  }
   __device__ __forceinline__ void operator()(int c, const Z4& zz, int st) {
-    const int q = st >> 2, k = st & 3;
-    // softplus' goes straight into the pending-store slots ([block][column] order; the previous
-    // chunk's stores were flushed at the start of this iteration)
-    sp_pair<NABLA>(zz, q, k, y[q], pd.v[q], pd.v[2 + q]);
-    if (k == 3) {
-      mrun[q] = amax8(mrun[q], y[q][0], y[q][1]);
-      split8a(y[q][0], y[q][1], sc[q], oh[q][c], ol[q][c]);
+    constexpr float K = 144.269504088896341f, C = 0.693147180559945309f * 0.01f;
+    if (st == 0) {
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        const f2v t = f2v{zval(zz, i), zval(zz, i + 1)} * f2v{K, K};
+        e[i] = fminf(t.x, 126.0f);
+        e[i + 1] = fminf(t.y, 126.0f);
+      }
+    } else if (st == 1) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) e[i] = __builtin_amdgcn_exp2f(e[i]);
+    } else if (st == 2) {
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        const f2v u = f2v{e[i], e[i + 1]} + f2v{1.0f, 1.0f};
+        w[i] = u.x;
+        w[i + 1] = u.y;
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) y[i] = __builtin_amdgcn_logf(w[i]);
+    } else if (st == 3) {
+      if constexpr (NABLA) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_rcpf(w[i]);
+      }
+    } else if (st == 4) {
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        const f2v v = f2v{y[i], y[i + 1]} * f2v{C, C};
+        y[i] = fmaxf(v.x, zval(zz, i));
+        y[i + 1] = fmaxf(v.y, zval(zz, i + 1));
+      }
+    } else if (st == 5) {
+      if constexpr (NABLA) {  // softplus' straight into the pending-store slots ([block][column])
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int o = 0; o < 2; ++o) {
+            const int i = (2 * q + o) * 4;
+            const f2v s01 = f2v{e[i], e[i + 1]} * f2v{w[i], w[i + 1]};
+            const f2v s23 = f2v{e[i + 2], e[i + 3]} * f2v{w[i + 2], w[i + 3]};
+            pd.v[2 * o + q] = make_float4(s01.x, s01.y, s23.x, s23.y);
+          }
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int i = 8 * q;
+        mrun[q] = amax8(mrun[q], make_float4(y[i], y[i + 1], y[i + 2], y[i + 3]),
+                        make_float4(y[i + 4], y[i + 5], y[i + 6], y[i + 7]));
+      }
+    } else if (st == 6) {
+      const int q = 0;
+      split8a(make_float4(y[0], y[1], y[2], y[3]), make_float4(y[4], y[5], y[6], y[7]), sc[q], oh[q][c], ol[q][c]);
+    } else {
+      const int q = 1;
+      split8a(make_float4(y[8], y[9], y[10], y[11]), make_float4(y[12], y[13], y[14], y[15]), sc[q], oh[q][c],
+              ol[q][c]);
+      if constexpr (NABLA) pend_chunk(pd, sl, 2 * c, pd.v[0], pd.v[1], pd.v[2], pd.v[3], lane, true);
     }
-    if constexpr (NABLA)
-      if (st == 7) pend_chunk(pd, sl, 2 * c, pd.v[0], pd.v[1], pd.v[2], pd.v[3], lane, true);
   }
 };
 
