@@ -999,6 +999,10 @@ __device__ __forceinline__ void mma4(const float4* __restrict__ A, const f16x8 (
       nl1 = as_h8(A[((NS + s + 1) * 2 + 1) * 64 + lane]);
     }
     stage(s);
+#ifdef NR_EXP_NO_MFMA  // timing experiment: fragments read, no matrix work (results are garbage)
+    asm volatile("" : : "v"(h0), "v"(l0), "v"(h1), "v"(l1));
+    continue;
+#endif
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       acc[q][0] = mfma16h(l0, bh[q][s], acc[q][0]);

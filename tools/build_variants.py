@@ -24,6 +24,7 @@ VARIANTS = {
     'v3nodma': ['-DNR_EXP_NO_DMA'],
     'v3nobar': ['-DNR_EXP_NO_BARRIER'],
     'v3noepi': ['-DNR_EXP_NO_EPI'],
+    'v3nomfma': ['-DNR_EXP_NO_MFMA'],
     'v3noslab': ['-DNR_EXP_NO_ESTORE', '-DNR_EXP_NO_ELOAD'],
     'unroll_nosplit': ['-DNR_EXP_UNROLL', '-DNR_EXP_NO_SPLIT'],
 }
