@@ -294,6 +294,34 @@ int nr_get_rays(const float* c2w, const float* K, int B, int H, int W, const int
                 float* rays_o, float* rays_d, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Surface rendering (models/ray_casting.py:163-263).
+ * nr_sphere_trace replaces `sphere_tracing_surface_points` (ray_casting.py:163-182): from d = near,
+ * n_iters times d += sdf(o + d*dir) on rays still inside [0, far]; rays_d as given (surface_render
+ * normalizes first, ray_casting.py:209).  Outputs d_pred [R], pts [R,3] (= o + d*dir), mask [R]
+ * (u8).  Only still-active rays are evaluated (compacted on device).  Workspace:
+ * nr_sphere_trace_workspace_bytes(R).
+ * nr_normalize3: F.normalize(v, dim=-1) of [n,3] (ray_casting.py:209).
+ * nr_surface_finish: surface_render's tail (ray_casting.py:226, 255-258): rgb[~mask] = 0 in place;
+ * normals (optional) = F.normalize(nablas) with normals[~mask] = 0.
+ * ------------------------------------------------------------------------------------------ */
+size_t nr_sphere_trace_workspace_bytes(int64_t n_rays);
+int nr_sphere_trace(const NrSdfDesc* d, const void* packed, const float* rays_o, const float* rays_d, int64_t n_rays,
+                    float near, float far, int n_iters, float* d_pred, float* pts, uint8_t* mask, void* workspace,
+                    size_t workspace_bytes, void* stream);
+int nr_normalize3(const float* v, int64_t n, float* out, void* stream);
+int nr_surface_finish(float* rgb, const float* nablas, const uint8_t* mask, int64_t n, float* normals, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Mesh-extraction SDF grid (utils/mesh_util.py:82-112 `extract_mesh`): points
+ * [i0, i0+n) of the N^3 voxel grid of edge `volume_size` centred at the origin, generated on the
+ * device with the reference's float64 formula (:87-100, including its true divisions), then the
+ * forward SDF (ImplicitSurface.forward) -> sdf [n].  Workspace: nr_sdf_grid_workspace_bytes(n).
+ * ------------------------------------------------------------------------------------------ */
+size_t nr_sdf_grid_workspace_bytes(int64_t n_points);
+int nr_sdf_grid(const NrSdfDesc* d, const void* packed, double volume_size, int64_t N, int64_t i0, int64_t n,
+                float* sdf, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Opt-in kernel timing (diagnostics / bench roofline).  While enabled, every kernel launch of
  * the library is bracketed by hipEvents on its stream; nr_profile_read() waits for them and
  * returns per-kernel totals (launches, milliseconds, work units: points or rays), then clears.

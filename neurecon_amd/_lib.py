@@ -120,6 +120,14 @@ _SIGS = {
     'nr_unisurf_render': (_c_i, [ctypes.POINTER(NrUnisurfArgs), _c_p]),
     'nr_sample_pdf': (_c_i, [_c_p, _c_p, _c_i64, _c_i, _c_p, _c_i, _c_p, _c_p]),
     'nr_get_rays': (_c_i, [_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p]),
+    'nr_sphere_trace_workspace_bytes': (_c_sz, [_c_i64]),
+    'nr_sphere_trace': (_c_i, [ctypes.POINTER(NrSdfDesc), _c_p, _c_p, _c_p, _c_i64, ctypes.c_float, ctypes.c_float,
+                               _c_i, _c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
+    'nr_normalize3': (_c_i, [_c_p, _c_i64, _c_p, _c_p]),
+    'nr_surface_finish': (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_p, _c_p]),
+    'nr_sdf_grid_workspace_bytes': (_c_sz, [_c_i64]),
+    'nr_sdf_grid': (_c_i, [ctypes.POINTER(NrSdfDesc), _c_p, ctypes.c_double, _c_i64, _c_i64, _c_i64, _c_p, _c_p,
+                           _c_sz, _c_p]),
     'nr_profile_enable': (_c_i, [_c_i]),
     'nr_profile_read': (_c_i, [ctypes.POINTER(NrKernelStat), _c_i, ctypes.POINTER(_c_i)]),
 }

@@ -1,0 +1,102 @@
+"""Surface rendering: drop-in for models/ray_casting.py:163-263.
+
+`sphere_tracing_surface_points` runs entirely in libnrhip (`nr_sphere_trace`: compacted active-ray
+lists on the device, the SDF MLP launched with a device-side count each iteration), and
+`surface_render` chains it with the framework's own native `model.forward` (SDF + nablas +
+radiance kernels) and a finish kernel (`nr_surface_finish`).  Called by tools/render_view.py
+(`--use_surface_render sphere_tracing`, render_view.py:236-239).
+"""
+import ctypes
+from collections import OrderedDict
+
+import torch
+
+from . import _lib as L
+from .base import _no_training
+
+
+def _normalize3(v):
+    """F.normalize(v, dim=-1) on the device (ray_casting.py:209)."""
+    L.require_gpu(v, 'vectors')
+    src = v.reshape(-1, 3).float().contiguous()
+    out = torch.empty_like(src)
+    L.check(L.lib().nr_normalize3(L.ptr(src), src.shape[0], L.ptr(out), L.stream_of(src.device)))
+    return out.reshape(v.shape)
+
+
+def sphere_tracing_surface_points(implicit_surface, rays_o, rays_d, near=0.0, far=6.0, batched=True,
+                                  batched_info={}, N_iters=20):
+    """ray_casting.py:163-182 -> (d_preds [...], pts [..., 3], mask [...] bool)."""
+    L.require_gpu(rays_o, 'rays_o')
+    _no_training(implicit_surface)
+    shape = rays_o.shape[:-1]
+    ro = rays_o.reshape(-1, 3).float().contiguous()
+    rd = rays_d.reshape(-1, 3).float().contiguous()
+    n = ro.shape[0]
+    dev = ro.device
+    desc, packed = implicit_surface.nr_packed(dev)
+    lib = L.lib()
+    d = torch.empty(n, device=dev)
+    pts = torch.empty(n, 3, device=dev)
+    mask = torch.empty(n, dtype=torch.uint8, device=dev)
+    ws_bytes = lib.nr_sphere_trace_workspace_bytes(n)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    L.check(lib.nr_sphere_trace(ctypes.byref(desc), L.ptr(packed), L.ptr(ro), L.ptr(rd), n, ctypes.c_float(near),
+                                ctypes.c_float(far), int(N_iters), L.ptr(d), L.ptr(pts), L.ptr(mask), L.ptr(ws),
+                                ws_bytes, L.stream_of(dev)))
+    return d.reshape(shape), pts.reshape(*shape, 3), mask.view(torch.bool).reshape(shape)
+
+
+def root_finding_surface_points(*args, **kwargs):
+    raise NotImplementedError('neurecon_amd: root_finding_surface_points runs inside the native UNISURF renderer '
+                              '(frameworks.unisurf.volume_render); standalone surface_render root finding is not '
+                              'exposed yet')
+
+
+def _couples_rays(model):
+    """UNISURF's forward normalizes nablas over the points axis (unisurf.py:36): results depend on
+    the chunk, so the reference's rayschunk split must be kept.  Other frameworks are per point."""
+    from .frameworks.unisurf import UNISURF
+    return isinstance(model, UNISURF)
+
+
+def surface_render(rays_o, rays_d, model, calc_normal=True, rayschunk=8192, netchunk=1048576, batched=True,
+                   use_view_dirs=True, show_progress=False, ray_casting_algo='', ray_casting_cfgs={},
+                   **not_used_kwargs):
+    """ray_casting.py:185-263 -> (colors, depths, extras{implicit_nablas, mask_surface[, normals_surface]})."""
+    if ray_casting_algo == 'root_finding':
+        root_finding_surface_points()
+    if ray_casting_algo != 'sphere_tracing':
+        raise NotImplementedError(ray_casting_algo)
+    if not use_view_dirs:
+        raise NotImplementedError('neurecon_amd: use_view_dirs=False not supported')
+    L.require_gpu(rays_o, 'rays_o')
+    with torch.no_grad():
+        if batched:
+            DIM = 1
+            flat = [rays_d.shape[0], -1, 3]
+        else:
+            DIM = 0
+            flat = [-1, 3]
+        ro = rays_o.reshape(flat).float().contiguous()
+        rd = _normalize3(rays_d.reshape(flat).float())
+        # sphere tracing is per ray: one launch sequence over every ray
+        d_pred, pt_pred, mask = sphere_tracing_surface_points(model.implicit_surface, ro, rd, batched=batched,
+                                                              **ray_casting_cfgs)
+        n = ro.shape[DIM]
+        step = rayschunk if _couples_rays(model) else max(rayschunk, 1 << 18)
+        colors, nablas = [], []
+        for i in range(0, n, step):
+            c, _, nb = model.forward(pt_pred.narrow(DIM, i, min(step, n - i)), rd.narrow(DIM, i, min(step, n - i)))
+            colors.append(c)
+            nablas.append(nb)
+        colors = torch.cat(colors, DIM).contiguous()
+        nablas = torch.cat(nablas, DIM).contiguous()
+        normals = torch.empty_like(nablas) if calc_normal else None
+        m8 = mask.contiguous().view(torch.uint8)
+        L.check(L.lib().nr_surface_finish(L.ptr(colors), L.ptr(nablas), L.ptr(m8), m8.numel(), L.ptr(normals),
+                                          L.stream_of(colors.device)))
+        extras = OrderedDict([('implicit_nablas', nablas), ('mask_surface', mask)])
+        if calc_normal:
+            extras['normals_surface'] = normals
+        return colors, d_pred, extras

@@ -316,14 +316,57 @@ def gen_unisurf(R):
     save('unisurf_e.npz', seed=3, logit_tau=float(logit_tau), rays_o=ro, rays_d=rd, idx=idx, **res)
 
 
+def gen_surface(R):
+    """surface_render / sphere tracing (ray_casting.py:163-263) and extract_mesh's SDF grid
+    (mesh_util.py:82-112) on NeuS weights (seed 1), 256 rays of the config-(b) camera."""
+    sd = wg.neus_state(seed=1)
+    model = _neus_model(R, sd, False)
+    H, W, _, _ = wg.CAMERAS['b']
+    idx = grid_idx(H, W, n=16, lo=0.0, hi=1.0)
+    ro, rd = camera_rays(R, 'b', idx)
+    with torch.no_grad():
+        rgb, depth, ex = R.ray_casting.surface_render(ro, rd, model, calc_normal=True, rayschunk=8192, batched=True,
+                                                      ray_casting_algo='sphere_tracing')
+        rdn = torch.nn.functional.normalize(rd, dim=-1)
+        d5, p5, m5 = R.ray_casting.sphere_tracing_surface_points(model.implicit_surface, ro, rdn, near=0.5, far=4.0,
+                                                                 N_iters=5)
+    # extract_mesh runs as shipped except for what this image lacks: numpy>=1.24 has no np.int
+    # (mesh_util.py:87), there is no GPU (`.cuda()`, :104) and no scikit-image/plyfile (the
+    # marching-cubes writer is replaced by a capture of the SDF volume it receives).
+    for name in ['plyfile', 'skimage.measure']:
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules['skimage'].measure = sys.modules['skimage.measure']
+    from utils import mesh_util
+    grids = {}
+    np_int = getattr(np, 'int', None)
+    cuda = torch.Tensor.cuda
+    np.int = int
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    saved = mesh_util.convert_sigma_samples_to_ply
+    try:
+        for N, s in [(16, 2.0), (24, 1.5)]:
+            mesh_util.convert_sigma_samples_to_ply = lambda out, *a, _N=N, **k: grids.__setitem__(_N, out.copy())
+            with torch.no_grad():
+                mesh_util.extract_mesh(model.implicit_surface, volume_size=s, N=N, show_progress=False, chunk=1000)
+    finally:
+        mesh_util.convert_sigma_samples_to_ply = saved
+        torch.Tensor.cuda = cuda
+        if np_int is None:
+            del np.int
+    save('surface.npz', seed=1, rays_o=ro, rays_d=rd, idx=idx, rgb=rgb, depth=depth,
+         nablas=ex['implicit_nablas'], mask=ex['mask_surface'], normals=ex['normals_surface'],
+         st5_d=d5, st5_pts=p5, st5_mask=m5, grid16=grids[16], grid24=grids[24])
+
+
 def main():
     torch.set_num_threads(8)
     R = _import_reference()
-    gen_components(R)
-    gen_sampling(R)
-    gen_neus(R)
-    gen_volsdf(R)
-    gen_unisurf(R)
+    only = sys.argv[1:]
+    gens = dict(components=gen_components, sampling=gen_sampling, neus=gen_neus, volsdf=gen_volsdf,
+                unisurf=gen_unisurf, surface=gen_surface)
+    for name, fn in gens.items():
+        if not only or name in only:
+            fn(R)
 
 
 if __name__ == '__main__':

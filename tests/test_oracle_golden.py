@@ -163,3 +163,24 @@ def test_unisurf(golden):
         close(out['rgb'], g['rgb' + tag], 1e-5, 1e-6)
         close(out['depth_volume'], g['depth' + tag], 1e-5, 1e-6)
         close(out['normals_volume'], g['normals' + tag], 1e-5, 1e-6)
+
+
+def test_surface_render_and_grid(golden):
+    """oracle/surface.py vs ray_casting.surface_render / sphere tracing / extract_mesh's grid."""
+    from oracle import surface
+    g = golden('surface')
+    orc = NeuSOracle(wg.neus_state(seed=int(g['seed'])))
+    with torch.no_grad():
+        out = surface.surface_render_neus(orc, T(g['rays_o']), T(g['rays_d']))
+        np.testing.assert_array_equal(out['mask'].numpy(), g['mask'].astype(bool))
+        close(out['depth'], g['depth'], 1e-6, 1e-6)
+        close(out['rgb'], g['rgb'], 1e-5, 1e-6)
+        close(out['nablas'], g['nablas'], 1e-5, 1e-6)
+        close(out['normals'], g['normals'], 1e-5, 1e-6)
+        d = torch.nn.functional.normalize(T(g['rays_d']), dim=-1)
+        d5, p5, m5 = surface.sphere_trace(orc.sdf_net.sdf, T(g['rays_o']), d, near=0.5, far=4.0, N_iters=5)
+        np.testing.assert_array_equal(m5.numpy(), g['st5_mask'].astype(bool))
+        close(d5, g['st5_d'], 1e-6, 1e-6)
+        close(p5, g['st5_pts'], 1e-6, 1e-6)
+        for N, s in [(16, 2.0), (24, 1.5)]:
+            close(surface.sdf_grid(orc.sdf_net.sdf, N, s), g[f'grid{N}'], 1e-6, 1e-7)
