@@ -183,7 +183,7 @@ int nr_neus_render(const NrNeusArgs* a, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * VolSDF rendering (models/frameworks/volsdf.py:377-551, render mode: perturb=False, builtin
- * background sphere).  Error-bounded sampling (volsdf.py:77-272) over 4*N_samples initial depths,
+ * background sphere or NeRF++ background).  Error-bounded sampling (volsdf.py:77-272) over 4*N_samples initial depths,
  * up to max_upsample_steps rounds of 4*N_samples new depths with max_bisection_steps bisection
  * steps on beta+, then N_importance final depths merged with N_samples uniform ones.
  * Outputs are ray-major; detailed outputs (NULL to skip) have S = N_samples + N_importance
@@ -225,6 +225,19 @@ typedef struct {
   float* iter_usage;     /* [n_rays]      */
   void* workspace;
   size_t workspace_bytes;
+  /* NeRF++ background (volsdf.py:400-405, 451-469), N_outside > 0 (requires use_sphere_bg = 0):
+   * far per ray = exit of the sphere of radius obj_bounding_radius (rend_util.py:188-210; `far`
+   * above is then unused), beta+ init per ray = sqrt(far^2 / beta_plus_k) (volsdf.py:127-129),
+   * N_outside background samples on the spheres of radii rs_out (rend_util.py:213-234) through the
+   * NeRF MLP, composited after the S inside samples.  With N_outside > 0 the detailed outputs
+   * d_vals / sigma_out / radiance_out hold M = S + N_outside samples and alpha / p / weights M-1. */
+  int N_outside;
+  const NrNerfDesc* nerf;
+  const void* nerf_packed;
+  const float* rs_out;   /* [N_outside] obj_bounding_radius / flip(linspace(0,1,N_outside+2)[1:-1]) (CPU values) */
+  float beta_plus_k;     /* float32(4 (4 N_samples - 1) log(1 + eps)) */
+  float* sigma_bg;       /* [n_rays, N_outside] sigma_out (detailed, NULL to skip) */
+  float* radiance_bg;    /* [n_rays, N_outside, 3] radiance_out (detailed) */
 } NrVolsdfArgs;
 
 size_t nr_volsdf_workspace_bytes(const NrVolsdfArgs* a);

@@ -72,6 +72,8 @@ class NrVolsdfArgs(ctypes.Structure):
         ('alpha_out', _c_p), ('p_out', _c_p), ('weights_out', _c_p), ('sigma_out', _c_p),
         ('beta_map', _c_p), ('iter_usage', _c_p),
         ('workspace', _c_p), ('workspace_bytes', _c_sz),
+        ('N_outside', _c_i), ('nerf', ctypes.POINTER(NrNerfDesc)), ('nerf_packed', _c_p), ('rs_out', _c_p),
+        ('beta_plus_k', _c_f), ('sigma_bg', _c_p), ('radiance_bg', _c_p),
     ]
 
 

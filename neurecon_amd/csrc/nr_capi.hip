@@ -280,6 +280,10 @@ static int volsdf_chunk(const NrVolsdfArgs& a, const VolPlan& pl, int64_t ray0, 
   c.d_all = F(pl.o_dall); c.pts_f = F(pl.o_ptsf); c.sdf_f = F(pl.o_sdff); c.nab_f = F(pl.o_nabf);
   c.feat_f = F(pl.o_featf); c.rad_f = F(pl.o_radf);
   c.t_coarse = a.t_coarse; c.t_init = a.t_init; c.u_up = a.u_up; c.u_fine = a.u_fine;
+  c.N_out = a.N_outside > 0 ? a.N_outside : 0;
+  c.beta_k = a.beta_plus_k;
+  c.farr = F(pl.o_farr); c.bp0 = F(pl.o_bp0); c.rs_out = a.rs_out; c.d_out = F(pl.o_dout);
+  c.x4 = F(pl.o_x4); c.sig_o = F(pl.o_sigo); c.rad_o = F(pl.o_rado);
   void* mlp_ws = ws + pl.o_mlp;
   const size_t mlp_bytes = a.workspace_bytes - pl.o_mlp;
   const SdfLayout SL = sdf_layout(*a.sdf);
@@ -323,8 +327,18 @@ static int volsdf_chunk(const NrVolsdfArgs& a, const VolPlan& pl, int64_t ray0, 
   if ((rc = launch_radiance(RL, a.rad_packed, c.pts_f, c.rd, c.S, INT64_MAX, c.nab_f, c.feat_f, P, c.rad_f,
                             a.rad->multires_view, st)))
     return rc;
+  if (c.N_out > 0) {
+    {
+      ProfScope prof("volsdf_outside", (double)R, st);
+      hipLaunchKernelGGL(volsdf_outside, grd, blk, 0, st, c);
+    }
+    NR_HIP_CHECK(hipGetLastError());
+    if ((rc = launch_nerf(nerf_layout(*a.nerf), a.nerf_packed, c.x4, c.rd, c.N_out, INT64_MAX,
+                          (int64_t)c.N_out * R, c.sig_o, c.rad_o, st)))
+      return rc;
+  }
   VolOut o{ray0, a.rgb, a.depth, a.acc, a.normals, a.d_vals, a.sdf_out, a.nablas_out, a.radiance_out,
-           a.alpha_out, a.p_out, a.weights_out, a.sigma_out, a.beta_map, a.iter_usage};
+           a.alpha_out, a.p_out, a.weights_out, a.sigma_out, a.beta_map, a.iter_usage, a.sigma_bg, a.radiance_bg};
   {
     ProfScope prof("volsdf_composite", (double)R, st);
     hipLaunchKernelGGL(volsdf_composite, grd, blk, lds, st, c, o, a.calc_normal, a.white_bkgd);
@@ -351,7 +365,14 @@ static int check_volsdf(const NrVolsdfArgs* a) {
              NR_ERR_ARG, "nr_volsdf_render: bad sample counts");
   NR_REQUIRE(4 * a->N_samples <= 1024 && a->N_importance <= 1024, NR_ERR_UNSUPPORTED,
              "nr_volsdf_render: 4*N_samples and N_importance must be <= 1024");
-  NR_REQUIRE(a->beta_net > 0.f && a->beta_plus_init > 0.f, NR_ERR_ARG, "nr_volsdf_render: beta must be positive");
+  NR_REQUIRE(a->beta_net > 0.f && (a->N_outside > 0 || a->beta_plus_init > 0.f), NR_ERR_ARG,
+             "nr_volsdf_render: beta must be positive");
+  if (a->N_outside > 0) {
+    NR_REQUIRE(!a->use_sphere_bg, NR_ERR_ARG, "nr_volsdf_render: NeRF++ background excludes the builtin sphere");
+    NR_REQUIRE(a->nerf && a->nerf_packed && a->rs_out && a->beta_plus_k > 0.f, NR_ERR_ARG,
+               "nr_volsdf_render: N_outside > 0 needs nerf, nerf_packed, rs_out and beta_plus_k");
+    if ((rc = check_nerf_desc(a->nerf))) return rc;
+  }
   return NR_OK;
 }
 

@@ -32,6 +32,15 @@ struct VolChunk {
   // final pass (ray-major [R][S])
   float* d_all; float* pts_f; float* sdf_f; float* nab_f; float* feat_f; float* rad_f;
   const float* t_coarse; const float* t_init; const float* u_up; const float* u_fine;
+  // NeRF++ background (N_out > 0): per-ray far (sphere exit) and beta+ init, outside samples
+  int N_out;
+  float beta_k;                    // float32(4 (N0 - 1) log(1 + eps))
+  float* farr;                     // [R] far per ray
+  float* bp0;                      // [R] beta+ init per ray
+  const float* rs_out;             // [N_out] radii of the background spheres
+  float* d_out;                    // [R][N_out] background depths
+  float* x4;                       // [R][N_out][4] NeRF input [p / r, 1 / r]
+  float* sig_o; float* rad_o;      // [R][N_out], [R][N_out][3] NeRF outputs
 };
 
 struct VolOut {
@@ -39,12 +48,14 @@ struct VolOut {
   float* rgb; float* depth; float* acc; float* normals;
   float* d_vals; float* sdf; float* nablas; float* radiance; float* alpha; float* p_i; float* weights;
   float* sigma; float* beta_map; float* iter_usage;
+  float* sigma_bg; float* radiance_bg;
 };
 
 struct VolPlan {
   int64_t Rc;
   size_t o_ro, o_rd, o_Ld0, o_Ld1, o_Ls0, o_Ls1, o_dn0, o_dn1, o_pts, o_sraw, o_act0, o_act1, o_cnt;
   size_t o_beta, o_fine, o_usage, o_bmap, o_dall, o_ptsf, o_sdff, o_nabf, o_featf, o_radf, o_mlp;
+  size_t o_farr, o_bp0, o_dout, o_x4, o_sigo, o_rado;
   size_t total;
   size_t lds_bytes;  // dynamic LDS of the per-ray kernels
 };
@@ -55,6 +66,7 @@ __global__ void volsdf_prologue(VolChunk c, const float* rays_o, const float* ra
 __global__ void volsdf_first(VolChunk c);
 __global__ void volsdf_iter(VolChunk c, int it);
 __global__ void volsdf_points(VolChunk c);
+__global__ void volsdf_outside(VolChunk c);
 __global__ void volsdf_composite(VolChunk c, VolOut o, int calc_normal, int white_bkgd);
 
 }  // namespace nr

@@ -270,7 +270,8 @@ struct Lds {
 
 __device__ __forceinline__ Lds lds_views(const VolChunk& c) {
   extern __shared__ float lds[];
-  const int big = c.cap > c.S ? c.cap : c.S;
+  const int M = c.S + c.N_out;
+  const int big = c.cap > M ? c.cap : M;
   const int small = c.N_up > c.N_imp ? c.N_up : c.N_imp;
   return Lds{lds, lds + big, lds + 2 * big, lds + 2 * big + small, lds + 2 * big + 2 * small};
 }
@@ -291,7 +292,7 @@ __device__ void vs_decide(const VolChunk& c, int r, int it, int n, Lds& s) {
     }
     return;
   }
-  float beta = c.beta_plus0;
+  float beta = c.N_out > 0 ? c.bp0[r] : c.beta_plus0;
   if (it > 0) {  // bisection on beta+ (volsdf.py:228-244)
     float br = c.beta[r], bl = c.beta_net;
     for (int b = 0; b < c.max_bisect; ++b) {
@@ -345,6 +346,11 @@ __device__ void vs_decide(const VolChunk& c, int r, int it, int n, Lds& s) {
 
 }  // namespace
 
+// torch.sum(a * b, dim=-1) of two 3-vectors on the CPU: products rounded, then summed in order
+__device__ __forceinline__ float ray_dot(float ax, float ay, float az, float bx, float by, float bz) {
+  return fadd(fadd(fmul(ax, bx), fmul(ay, by)), fmul(az, bz));
+}
+
 // ---------------------------------------------------------------------------------------------
 // kernels (one 64-thread workgroup = one wave per ray or active slot)
 // ---------------------------------------------------------------------------------------------
@@ -359,6 +365,18 @@ __global__ __launch_bounds__(64) void volsdf_prologue(VolChunk c, const float* _
   dx = fdiv(dx, nn);
   dy = fdiv(dy, nn);
   dz = fdiv(dz, nn);
+  float far = c.far;
+  if (c.N_out > 0) {
+    // rend_util.get_sphere_intersection (rend_util.py:188-210), far end, clamp_min(0); rays that
+    // miss keep far = 0 (the reference asserts they do not occur, volsdf.py:405)
+    const float dot = ray_dot(ox, oy, oz, dx, dy, dz);
+    const float under = fsub(fadd(fmul(dot, dot), fmul(c.r_bg, c.r_bg)), ray_dot(ox, oy, oz, ox, oy, oz));
+    far = under > 0.f ? fmaxf(fsub(sqrtf(under), dot), 0.f) : 0.f;
+    if (l == 0) {
+      c.farr[r] = far;
+      c.bp0[r] = sqrtf(fdiv(fmul(far, far), c.beta_k));  // volsdf.py:129 with a per-ray far
+    }
+  }
   if (l == 0) {
     c.ro[r * 3 + 0] = ox; c.ro[r * 3 + 1] = oy; c.ro[r * 3 + 2] = oz;
     c.rd[r * 3 + 0] = dx; c.rd[r * 3 + 1] = dy; c.rd[r * 3 + 2] = dz;
@@ -367,7 +385,7 @@ __global__ __launch_bounds__(64) void volsdf_prologue(VolChunk c, const float* _
   float* pp = c.pts + (int64_t)r * c.N0 * 3;
   for (int j = l; j < c.N0; j += 64) {
     const float t = c.t_init[j];
-    const float d = fadd(fmul(c.near, fsub(1.0f, t)), fmul(c.far, t));
+    const float d = fadd(fmul(c.near, fsub(1.0f, t)), fmul(far, t));
     gd[j] = d;
     pp[j * 3 + 0] = fadd(ox, fmul(dx, d));
     pp[j * 3 + 1] = fadd(oy, fmul(dy, d));
@@ -423,9 +441,10 @@ __global__ __launch_bounds__(64) void volsdf_iter(VolChunk c, int it) {
 __global__ __launch_bounds__(64) void volsdf_points(VolChunk c) {
   const int r = blockIdx.x, l = threadIdx.x;
   Lds s = lds_views(c);
+  const float far = c.N_out > 0 ? c.farr[r] : c.far;
   for (int j = l; j < c.N_samples; j += 64) {
     const float t = c.t_coarse[j];
-    s.D[j] = fadd(fmul(c.near, fsub(1.0f, t)), fmul(c.far, t));
+    s.D[j] = fadd(fmul(c.near, fsub(1.0f, t)), fmul(far, t));
     s.S[j] = 0.0f;
   }
   const float* fine = c.fine + (int64_t)r * c.N_imp;
@@ -448,17 +467,41 @@ __global__ __launch_bounds__(64) void volsdf_points(VolChunk c) {
   }
 }
 
-// background replacement (volsdf.py:317-325), sigma, p_i, tau_i and the maps (volsdf.py:449-528)
+// NeRF++ background samples (volsdf.py:451-463): d_out = get_dvals_from_radius(o, d, rs)
+// (rend_util.py:213-234, far end), x_out = [p_out / rs, 1 / rs]
+__global__ __launch_bounds__(64) void volsdf_outside(VolChunk c) {
+  const int r = blockIdx.x, l = threadIdx.x;
+  const float ox = c.ro[r * 3], oy = c.ro[r * 3 + 1], oz = c.ro[r * 3 + 2];
+  const float dx = c.rd[r * 3], dy = c.rd[r * 3 + 1], dz = c.rd[r * 3 + 2];
+  const float nsq = ray_dot(ox, oy, oz, ox, oy, oz);
+  const float dot = ray_dot(ox, oy, oz, dx, dy, dz);
+  const float q = fsub(nsq, fmul(dot, dot));
+  for (int k = l; k < c.N_out; k += 64) {
+    const float rs = c.rs_out[k];
+    const float d = fadd(-dot, sqrtf(fsub(fmul(rs, rs), q)));
+    const int64_t i = (int64_t)r * c.N_out + k;
+    c.d_out[i] = d;
+    c.x4[i * 4 + 0] = fdiv(fadd(ox, fmul(dx, d)), rs);
+    c.x4[i * 4 + 1] = fdiv(fadd(oy, fmul(dy, d)), rs);
+    c.x4[i * 4 + 2] = fdiv(fadd(oz, fmul(dz, d)), rs);
+    c.x4[i * 4 + 3] = fdiv(1.0f, rs);
+  }
+}
+
+// background replacement (volsdf.py:317-325), sigma, p_i, tau_i and the maps (volsdf.py:449-528);
+// with NeRF++ the N_out background samples follow the S inside ones (volsdf.py:465-469)
 __global__ __launch_bounds__(64) void volsdf_composite(VolChunk c, VolOut o, int calc_normal, int white_bkgd) {
   const int r = blockIdx.x, l = threadIdx.x;
   Lds s = lds_views(c);
-  const int S = c.S;
+  const int S = c.S, No = c.N_out, M = S + No;
   const int64_t ro = o.ray0 + r;
   const float* da = c.d_all + (int64_t)r * S;
   const float* sf = c.sdf_f + (int64_t)r * S;
   const float* nb = c.nab_f + (int64_t)r * S * 3;
   const float* rad = c.rad_f + (int64_t)r * S * 3;
   const float* pp = c.pts_f + (int64_t)r * S * 3;
+  const float* rado = c.rad_o + (int64_t)r * No * 3;
+  // s.D: depths, s.S: sigma (inside: from the sdf; outside: the NeRF's raw sigma)
   for (int j = l; j < S; j += 64) {
     const float d = da[j];
     float v = sf[j];
@@ -466,32 +509,46 @@ __global__ __launch_bounds__(64) void volsdf_composite(VolChunk c, VolOut o, int
       const float dbg = fsub(c.r_bg, norm3(pp[j * 3], pp[j * 3 + 1], pp[j * 3 + 2]));
       if (dbg < v) v = dbg;
     }
+    const float sg = vs_sigma(v, c.alpha_net, c.beta_net);
     s.D[j] = d;
-    s.S[j] = v;
+    s.S[j] = sg;
     if (o.sdf) o.sdf[ro * S + j] = v;
-    if (o.d_vals) o.d_vals[ro * S + j] = d;
-    if (o.sigma) o.sigma[ro * S + j] = vs_sigma(v, c.alpha_net, c.beta_net);
+    if (o.d_vals) o.d_vals[ro * M + j] = d;
+    if (o.sigma) o.sigma[ro * M + j] = sg;
     if (o.nablas) {
       o.nablas[(ro * S + j) * 3 + 0] = nb[j * 3 + 0];
       o.nablas[(ro * S + j) * 3 + 1] = nb[j * 3 + 1];
       o.nablas[(ro * S + j) * 3 + 2] = nb[j * 3 + 2];
     }
     if (o.radiance) {
-      o.radiance[(ro * S + j) * 3 + 0] = rad[j * 3 + 0];
-      o.radiance[(ro * S + j) * 3 + 1] = rad[j * 3 + 1];
-      o.radiance[(ro * S + j) * 3 + 2] = rad[j * 3 + 2];
+      o.radiance[(ro * M + j) * 3 + 0] = rad[j * 3 + 0];
+      o.radiance[(ro * M + j) * 3 + 1] = rad[j * 3 + 1];
+      o.radiance[(ro * M + j) * 3 + 2] = rad[j * 3 + 2];
+    }
+  }
+  for (int k = l; k < No; k += 64) {
+    const int64_t i = (int64_t)r * No + k;
+    const float d = c.d_out[i], sg = c.sig_o[i];
+    s.D[S + k] = d;
+    s.S[S + k] = sg;
+    if (o.d_vals) o.d_vals[ro * M + S + k] = d;
+    if (o.sigma) o.sigma[ro * M + S + k] = sg;
+    if (o.sigma_bg) o.sigma_bg[ro * No + k] = sg;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      if (o.radiance) o.radiance[(ro * M + S + k) * 3 + q] = rado[k * 3 + q];
+      if (o.radiance_bg) o.radiance_bg[(ro * No + k) * 3 + q] = rado[k * 3 + q];
     }
   }
   __syncthreads();
+  // normals use the first min(#tau, #nablas) samples (volsdf.py:509-511)
+  const int Nn = M - 1 < S ? M - 1 : S;
   double T = 1.0, a_rgb0 = 0.0, a_rgb1 = 0.0, a_rgb2 = 0.0, a_acc = 0.0, a_n0 = 0.0, a_n1 = 0.0, a_n2 = 0.0;
-  for (int base = 0; base < S - 1; base += 64) {
+  for (int base = 0; base < M - 1; base += 64) {
     const int i = base + l;
-    const bool v = i < S - 1;
+    const bool v = i < M - 1;
     float p = 1.0f;
-    if (v) {
-      const float sg = vs_sigma(s.S[i], c.alpha_net, c.beta_net);
-      p = expf(-fmaxf(fmul(sg, fsub(s.D[i + 1], s.D[i])), 0.0f));
-    }
+    if (v) p = expf(-fmaxf(fmul(s.S[i], fsub(s.D[i + 1], s.D[i])), 0.0f));
     const double inc = wave_scan_mul((double)p);
     double ex = __shfl_up(inc, 1);
     if (l == 0) ex = 1.0;
@@ -499,28 +556,29 @@ __global__ __launch_bounds__(64) void volsdf_composite(VolChunk c, VolOut o, int
     T *= __shfl(inc, 63);
     if (v) {
       const float tau = fmul(fadd(fsub(1.0f, p), 1e-10f), Ti);
-      a_rgb0 += (double)fmul(tau, rad[i * 3 + 0]);
-      a_rgb1 += (double)fmul(tau, rad[i * 3 + 1]);
-      a_rgb2 += (double)fmul(tau, rad[i * 3 + 2]);
+      const float* rr = i < S ? rad + i * 3 : rado + (i - S) * 3;
+      a_rgb0 += (double)fmul(tau, rr[0]);
+      a_rgb1 += (double)fmul(tau, rr[1]);
+      a_rgb2 += (double)fmul(tau, rr[2]);
       a_acc += (double)tau;
-      if (calc_normal) {
+      if (calc_normal && i < Nn) {
         float x = nb[i * 3 + 0], y = nb[i * 3 + 1], z = nb[i * 3 + 2];
         const float nn = fmaxf(norm3(x, y, z), 1e-12f);
         a_n0 += (double)fmul(fdiv(x, nn), tau);
         a_n1 += (double)fmul(fdiv(y, nn), tau);
         a_n2 += (double)fmul(fdiv(z, nn), tau);
       }
-      if (o.alpha) o.alpha[ro * (S - 1) + i] = fsub(1.0f, p);
-      if (o.p_i) o.p_i[ro * (S - 1) + i] = p;
-      if (o.weights) o.weights[ro * (S - 1) + i] = tau;
-      s.S[i] = tau;  // sdf of sample i is no longer needed past this block
+      if (o.alpha) o.alpha[ro * (M - 1) + i] = fsub(1.0f, p);
+      if (o.p_i) o.p_i[ro * (M - 1) + i] = p;
+      if (o.weights) o.weights[ro * (M - 1) + i] = tau;
+      s.S[i] = tau;  // sigma of sample i is only read by this lane, above
     }
     __syncthreads();
   }
   const float accf = (float)wave_sum(a_acc);
   const float denom = fadd(accf, 1e-10f);
   double a_dep = 0.0;
-  for (int i = l; i < S - 1; i += 64) a_dep += (double)fmul(fdiv(s.S[i], denom), s.D[i]);
+  for (int i = l; i < M - 1; i += 64) a_dep += (double)fmul(fdiv(s.S[i], denom), s.D[i]);
   const float depth = (float)wave_sum(a_dep);
   const float r0 = (float)wave_sum(a_rgb0), r1 = (float)wave_sum(a_rgb1), r2 = (float)wave_sum(a_rgb2);
   float n0 = 0.f, n1 = 0.f, n2 = 0.f;
@@ -587,9 +645,16 @@ VolPlan volsdf_plan(const NrVolsdfArgs& a, int64_t Rc) {
   p.o_nabf = take((size_t)Rc * S * 3);
   p.o_featf = take((size_t)Rc * S * 256);
   p.o_radf = take((size_t)Rc * S * 3);
+  const int No = a.N_outside > 0 ? a.N_outside : 0;
+  p.o_farr = take(Rc);
+  p.o_bp0 = take(Rc);
+  p.o_dout = take((size_t)Rc * No + 1);
+  p.o_x4 = take((size_t)Rc * No * 4 + 1);
+  p.o_sigo = take((size_t)Rc * No + 1);
+  p.o_rado = take((size_t)Rc * No * 3 + 1);
   p.o_mlp = off;
   p.total = off + nr_mlp_workspace_bytes(1);
-  const int big = cap > S ? cap : S;
+  const int big = cap > S + No ? cap : S + No;
   const int small = N_up > a.N_importance ? N_up : a.N_importance;
   p.lds_bytes = (size_t)(2 * big + 2 * small + 4) * 4;
   return p;

@@ -79,6 +79,12 @@ def _beta_plus_init(far, n_init, eps):
     return float(torch.sqrt((far_t ** 2) / (4 * (n_init - 1) * np.log(1 + eps))).reshape(-1)[0])
 
 
+def _outside_radii(n, r, device):
+    """volsdf.py:452-453: r / flip(linspace(0, 1, n + 2)[1:-1]) on the CPU in fp32, uploaded."""
+    t = torch.linspace(0, 1, n + 2)[..., 1:-1].float()
+    return (r / torch.flip(t, dims=[-1])).contiguous().to(device)
+
+
 def volume_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=3.0, batched=False,
                   batched_info={}, calc_normal=False, use_view_dirs=True, rayschunk=65536, netchunk=1048576,
                   white_bkgd=False, use_nerfplusplus=False, detailed_output=True, show_progress=False,
@@ -89,8 +95,6 @@ def volume_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=
     _no_training(model)
     if perturb:
         raise NotImplementedError('neurecon_amd: stratified (perturb=True) sampling is a training feature')
-    if use_nerfplusplus:
-        raise NotImplementedError('neurecon_amd: VolSDF with the NeRF++ background is not native yet')
     if not use_view_dirs:
         raise NotImplementedError('neurecon_amd: use_view_dirs=False not supported')
     dev = rays_o.device
@@ -100,6 +104,8 @@ def volume_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=
     n = ro.shape[0]
     S = N_samples + N_importance
     N0 = 4 * N_samples
+    No = int(N_outside) if use_nerfplusplus else 0
+    M = S + No  # samples after the NeRF++ merge (volsdf.py:465-469)
 
     sdf_desc, sdf_packed = model.implicit_surface.nr_packed(dev)
     rad_desc, rad_packed = model.radiance_net.nr_packed(dev)
@@ -116,16 +122,26 @@ def volume_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=
     det = {}
     if detailed_output:
         det = dict(implicit_surface=torch.empty(n, S, device=dev), implicit_nablas=torch.empty(n, S, 3, device=dev),
-                   radiance=torch.empty(n, S, 3, device=dev), alpha=torch.empty(n, S - 1, device=dev),
-                   p_i=torch.empty(n, S - 1, device=dev), visibility_weights=torch.empty(n, S - 1, device=dev),
-                   d_vals=torch.empty(n, S, device=dev), sigma=torch.empty(n, S, device=dev),
+                   radiance=torch.empty(n, M, 3, device=dev), alpha=torch.empty(n, M - 1, device=dev),
+                   p_i=torch.empty(n, M - 1, device=dev), visibility_weights=torch.empty(n, M - 1, device=dev),
+                   d_vals=torch.empty(n, M, device=dev), sigma=torch.empty(n, M, device=dev),
                    beta_map=torch.empty(n, device=dev), iter_usage=torch.empty(n, device=dev))
+        if No > 0:
+            det['sigma_out'] = torch.empty(n, No, device=dev)
+            det['radiance_out'] = torch.empty(n, No, 3, device=dev)
     a = L.NrVolsdfArgs()
     a.rays_o, a.rays_d, a.n_rays = L.ptr(ro), L.ptr(rd), n
     a.sdf, a.sdf_packed = ctypes.pointer(sdf_desc), L.ptr(sdf_packed)
     a.rad, a.rad_packed = ctypes.pointer(rad_desc), L.ptr(rad_packed)
     a.alpha_net, a.beta_net = alpha_net, beta_net
-    a.beta_plus_init = _beta_plus_init(far, N0, epsilon)
+    a.beta_plus_init = _beta_plus_init(far, N0, epsilon) if No == 0 else 0.0
+    if No > 0:
+        nerf_desc, nerf_packed = model.nerf_outside.nr_packed(dev)
+        a.N_outside = No
+        a.nerf, a.nerf_packed = ctypes.pointer(nerf_desc), L.ptr(nerf_packed)
+        rs_out = _outside_radii(No, float(obj_bounding_radius), dev)
+        a.rs_out = L.ptr(rs_out)
+        a.beta_plus_k = float(np.float32(4 * (N0 - 1) * np.log(1 + epsilon)))
     a.eps = float(epsilon)
     a.near, a.far = float(near), float(far)
     a.obj_bounding_radius = float(model.obj_bounding_radius)
@@ -145,6 +161,8 @@ def volume_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=
     a.sigma_out = L.ptr(det.get('sigma'))
     a.beta_map = L.ptr(det.get('beta_map'))
     a.iter_usage = L.ptr(det.get('iter_usage'))
+    a.sigma_bg = L.ptr(det.get('sigma_out'))
+    a.radiance_bg = L.ptr(det.get('radiance_out'))
     lib = L.lib()
     ws_bytes = lib.nr_volsdf_workspace_bytes(ctypes.byref(a))
     if ws_bytes == 0:
@@ -160,14 +178,17 @@ def volume_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=
     if detailed_output:
         ret['implicit_surface'] = det['implicit_surface'].reshape(*prefix, S)
         ret['implicit_nablas'] = det['implicit_nablas'].reshape(*prefix, S, 3)
-        ret['radiance'] = det['radiance'].reshape(*prefix, S, 3)
-        ret['alpha'] = det['alpha'].reshape(*prefix, S - 1)
-        ret['p_i'] = det['p_i'].reshape(*prefix, S - 1)
-        ret['visibility_weights'] = det['visibility_weights'].reshape(*prefix, S - 1)
-        ret['d_vals'] = det['d_vals'].reshape(*prefix, S)
-        ret['sigma'] = det['sigma'].reshape(*prefix, S)
+        ret['radiance'] = det['radiance'].reshape(*prefix, M, 3)
+        ret['alpha'] = det['alpha'].reshape(*prefix, M - 1)
+        ret['p_i'] = det['p_i'].reshape(*prefix, M - 1)
+        ret['visibility_weights'] = det['visibility_weights'].reshape(*prefix, M - 1)
+        ret['d_vals'] = det['d_vals'].reshape(*prefix, M)
+        ret['sigma'] = det['sigma'].reshape(*prefix, M)
         ret['beta_map'] = det['beta_map'].reshape(*prefix, 1)
         ret['iter_usage'] = det['iter_usage'].reshape(prefix)
+        if No > 0:
+            ret['sigma_out'] = det['sigma_out'].reshape(*prefix, No)
+            ret['radiance_out'] = det['radiance_out'].reshape(*prefix, No, 3)
     return ret['rgb'], ret['depth_volume'], ret
 
 

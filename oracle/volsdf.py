@@ -1,11 +1,11 @@
 """ORACLE (test infrastructure only): VolSDF rendering restated from models/frameworks/volsdf.py
-(render mode, builtin background sphere, perturb=False)."""
+(render mode, builtin background sphere or NeRF++ background, perturb=False)."""
 import numpy as np
 import torch
 import torch.nn.functional as F
 
 from . import rays as R
-from .nets import SDFNet, RadianceNet
+from .nets import NeRFNet, RadianceNet, SDFNet
 
 
 def sdf_to_sigma(sdf, alpha, beta):
@@ -109,12 +109,13 @@ def fine_sample(sdf_fn, d_init, o, d, alpha_net, beta_net, far, eps=0.1, max_ite
 
 
 class VolSDFOracle:
-    def __init__(self, sd, speed_factor=10.0, obj_bounding_radius=3.0, multires=6):
+    def __init__(self, sd, speed_factor=10.0, obj_bounding_radius=3.0, multires=6, use_nerfplusplus=False):
         self.sd = sd
         self.speed_factor = speed_factor
         self.R = obj_bounding_radius
         self.sdf_net = SDFNet(sd, multires=multires)
         self.rad_net = RadianceNet(sd, multires=-1, multires_view=-1)
+        self.nerf = NeRFNet(sd) if use_nerfplusplus else None  # use_sphere_bg = not use_nerfplusplus
 
     def forward_ab(self):
         # volsdf.py:306-308
@@ -122,16 +123,22 @@ class VolSDFOracle:
         return 1. / beta, beta
 
     def surface(self, x):
-        # volsdf.py:310-315 (builtin background sphere)
+        # volsdf.py:310-315 (builtin background sphere; plain network with NeRF++)
+        if self.nerf is not None:
+            return self.sdf_net.sdf(x)
         return torch.min(self.sdf_net.sdf(x), self.R - x.norm(dim=-1))
 
     def render(self, rays_o, rays_d, near=0.0, far=6.0, calc_normal=True, N_samples=128, N_importance=64,
-               max_upsample_steps=5, max_bisection_steps=10, epsilon=0.1, white_bkgd=False):
+               max_upsample_steps=5, max_bisection_steps=10, epsilon=0.1, white_bkgd=False, N_outside=32):
         o = rays_o.reshape(rays_o.shape[0], -1, 3).float()
         d = F.normalize(rays_d.reshape(rays_d.shape[0], -1, 3).float(), dim=-1)
         B, N = o.shape[:2]
         nears = near * torch.ones([B, N, 1])
-        fars = far * torch.ones([B, N, 1])
+        if self.nerf is not None:                                              # volsdf.py:403-405
+            _, fars, hit = R.sphere_intersection(o, d, r=self.R)
+            assert hit.all()
+        else:
+            fars = far * torch.ones([B, N, 1])
         t = torch.linspace(0, 1, N_samples).float()
         d_coarse = nears * (1 - t) + fars * t                                  # volsdf.py:415-417
         alpha, beta = self.forward_ab()
@@ -145,9 +152,22 @@ class VolSDFOracle:
         d_all = torch.sort(torch.cat([d_coarse, d_fine], -1), -1)[0]
         pts = o[..., None, :] + d[..., None, :] * d_all[..., :, None]
         sdf, nablas, h = self.sdf_net.forward_with_nablas(pts)
-        sdf = torch.min(sdf, self.R - pts.norm(dim=-1))                       # volsdf.py:317-325
+        if self.nerf is None:
+            sdf = torch.min(sdf, self.R - pts.norm(dim=-1))                   # volsdf.py:317-325
         rad = self.rad_net.forward(pts, d.unsqueeze(-2).expand_as(pts), nablas, h)
         sigma = sdf_to_sigma(sdf, alpha, beta)
+        extra = {}
+        if self.nerf is not None:                                              # volsdf.py:451-469
+            t_out = torch.linspace(0, 1, N_outside + 2)[..., 1:-1].float()
+            rs = (self.R / torch.flip(t_out, dims=[-1])).expand([B, N, N_outside])
+            d_out = R.dvals_from_radius(o, d, rs)
+            pts_out = o[..., None, :] + d[..., None, :] * d_out[..., :, None]
+            x_out = torch.cat([pts_out / rs[..., None], 1. / rs[..., None]], dim=-1)
+            sigma_out, rad_out = self.nerf.forward(x_out, d.unsqueeze(-2).expand_as(pts_out))
+            d_all = torch.cat([d_all, d_out], -1)
+            sigma = torch.cat([sigma, sigma_out], -1)
+            rad = torch.cat([rad, rad_out], -2)
+            extra = dict(sigma_out=sigma_out, radiance_out=rad_out)
         delta = d_all[..., 1:] - d_all[..., :-1]                               # volsdf.py:482-499
         p = torch.exp(-F.relu(sigma[..., :-1] * delta))
         tau = (1 - p + 1e-10) * torch.cumprod(torch.cat([torch.ones_like(p[..., :1]), p], -1), -1)[..., :-1]
@@ -158,7 +178,7 @@ class VolSDFOracle:
             rgb = rgb + (1.0 - acc[..., None])
         out = dict(rgb=rgb, depth_volume=depth, mask_volume=acc, implicit_surface=sdf, implicit_nablas=nablas,
                    radiance=rad, alpha=1.0 - p, p_i=p, visibility_weights=tau, d_vals=d_all, sigma=sigma,
-                   beta_map=beta_map, iter_usage=usage)
+                   beta_map=beta_map, iter_usage=usage, **extra)
         if calc_normal:
             nrm = F.normalize(nablas, dim=-1)
             n = min(tau.shape[-1], nrm.shape[-2])

@@ -236,9 +236,9 @@ def gen_neus(R):
          radiance_out=ex['radiance_out'])
 
 
-def _volsdf_model(R, sd, beta_init):
+def _volsdf_model(R, sd, beta_init, use_nerfplusplus=False):
     m = R.volsdf.VolSDF(beta_init=beta_init, speed_factor=10.0, input_ch=3, W_geo_feat=256,
-                        obj_bounding_radius=3.0, use_nerfplusplus=False,
+                        obj_bounding_radius=3.0, use_nerfplusplus=use_nerfplusplus,
                         surface_cfg=dict(radius_init=1.0, **SURF),
                         radiance_cfg=dict(use_siren=False, embed_multires=-1, embed_multires_view=-1,
                                           use_view_dirs=True, D=4, W=256, skips=[]))
@@ -286,6 +286,25 @@ def gen_volsdf(R):
     b2 = R.volsdf.error_bound(x, sdf1d, 1. / bplus, bplus)
     sg = R.volsdf.sdf_to_sigma(sdf1d, 1. / beta, beta)
     save('volsdf_1d.npz', x=x, sdf=sdf1d, beta=beta, bplus=bplus, bounds_net=b1, bounds_plus=b2, sigma=sg)
+
+
+def gen_volsdf_nerfpp(R):
+    """VolSDF with the NeRF++ background (volsdf.py:400-405, 451-469): config-(a) camera (inside
+    the r=3 bounding sphere, so every ray intersects it), 128 rays, 64+64 inside, 32 outside."""
+    sd = wg.volsdf_state(seed=6, beta_init=0.1, use_nerfplusplus=True)
+    model = _volsdf_model(R, sd, 0.1, use_nerfplusplus=True)
+    H, W, _, _ = wg.CAMERAS['a']
+    idx = torch.arange(0, H * W, 4)
+    ro, rd = camera_rays(R, 'a', idx)
+    with torch.no_grad():
+        rgb, depth, ex = R.volsdf.volume_render(
+            ro, rd, model, near=0.0, far=6.0, obj_bounding_radius=3.0, batched=True, calc_normal=True,
+            detailed_output=True, perturb=False, N_samples=64, N_importance=64, N_outside=32,
+            use_nerfplusplus=True, max_upsample_steps=6)
+    save('volsdf_nerfpp.npz', seed=6, beta_init=0.1, rays_o=ro, rays_d=rd, idx=idx, rgb=rgb, depth=depth,
+         mask=ex['mask_volume'], normals=ex['normals_volume'], beta_map=ex['beta_map'],
+         iter_usage=ex['iter_usage'], d_vals=ex['d_vals'], sigma=ex['sigma'], weights=ex['visibility_weights'],
+         sigma_out=ex['sigma_out'], radiance_out=ex['radiance_out'], radiance=ex['radiance'])
 
 
 def gen_unisurf(R):
@@ -363,7 +382,8 @@ def main():
     R = _import_reference()
     only = sys.argv[1:]
     gens = dict(components=gen_components, sampling=gen_sampling, neus=gen_neus, volsdf=gen_volsdf,
-                unisurf=gen_unisurf, surface=gen_surface)
+                unisurf=gen_unisurf, surface=gen_surface,
+                volsdf_nerfpp=gen_volsdf_nerfpp)
     for name, fn in gens.items():
         if not only or name in only:
             fn(R)

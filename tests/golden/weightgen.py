@@ -124,11 +124,14 @@ def neus_state(seed=1, use_outside_nerf=False, variance_init=0.05, speed_factor=
     return sd
 
 
-def volsdf_state(seed=2, beta_init=0.1, speed_factor=10.0, obj_bounding_radius=3.0, radius_init=1.0):
+def volsdf_state(seed=2, beta_init=0.1, speed_factor=10.0, obj_bounding_radius=3.0, radius_init=1.0,
+                 use_nerfplusplus=False):
     rs = np.random.RandomState(seed)
     sd = {'ln_beta': torch.tensor([np.log(beta_init) / speed_factor], dtype=torch.float32)}
     sd.update(surface_state(rs, 'implicit_surface.', radius_init, obj_bounding_radius))
     sd.update(radiance_state(rs, 'radiance_net.', 3 + 3 + 3 + 256))
+    if use_nerfplusplus:
+        sd.update(nerf_state(rs, 'nerf_outside.'))
     return sd
 
 

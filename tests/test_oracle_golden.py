@@ -184,3 +184,19 @@ def test_surface_render_and_grid(golden):
         close(p5, g['st5_pts'], 1e-6, 1e-6)
         for N, s in [(16, 2.0), (24, 1.5)]:
             close(surface.sdf_grid(orc.sdf_net.sdf, N, s), g[f'grid{N}'], 1e-6, 1e-7)
+
+
+def test_volsdf_nerfpp(golden):
+    """VolSDF + NeRF++ background (volsdf.py:400-405, 451-469) vs the reference."""
+    g = golden('volsdf_nerfpp')
+    orc = VolSDFOracle(wg.volsdf_state(seed=int(g['seed']), beta_init=float(g['beta_init']), use_nerfplusplus=True),
+                       use_nerfplusplus=True)
+    with torch.no_grad():
+        out = orc.render(T(g['rays_o']), T(g['rays_d']), N_samples=64, N_importance=64, N_outside=32,
+                         max_upsample_steps=6)
+    np.testing.assert_array_equal(out['iter_usage'].numpy(), g['iter_usage'])
+    close(out['d_vals'], g['d_vals'], 1e-6, 1e-6)
+    close(out['sigma_out'], g['sigma_out'], 1e-5, 1e-6)
+    close(out['radiance_out'], g['radiance_out'], 1e-5, 1e-6)
+    for k, gk in [('rgb', 'rgb'), ('depth_volume', 'depth'), ('mask_volume', 'mask'), ('normals_volume', 'normals')]:
+        close(out[k], g[gk], 1e-5, 1e-6)
