@@ -321,6 +321,17 @@ size_t nr_sphere_trace_workspace_bytes(int64_t n_rays);
 int nr_sphere_trace(const NrSdfDesc* d, const void* packed, const float* rays_o, const float* rays_d, int64_t n_rays,
                     float near, float far, int n_iters, float* d_pred, float* pts, uint8_t* mask, void* workspace,
                     size_t workspace_bytes, void* stream);
+/* nr_root_find replaces `root_finding_surface_points` (ray_casting.py:35-160) with scalar near/far:
+ * N_steps march samples at near*(1-t)+far*t (t_march = torch.linspace(0,1,N_steps), CPU values),
+ * first sign change of sdf - logit_tau, N_secant_steps secant refinements on rays entering the
+ * surface from outside with a free first sample.  Outputs d_pred [R] (inf if fill_inf, else far, on
+ * misses; 0 when the first sample is occupied), pts [R,3] (1 on misses), mask [R], mask_sign_change
+ * [R] (u8, optional).  rays_d as given (already normalised).  Workspace: nr_root_find_workspace_bytes. */
+size_t nr_root_find_workspace_bytes(int64_t n_rays, int N_steps);
+int nr_root_find(const NrSdfDesc* d, const void* packed, const float* rays_o, const float* rays_d, int64_t n_rays,
+                 float near, float far, int N_steps, const float* t_march, int N_secant_steps, float logit_tau,
+                 int fill_inf, float* d_pred, float* pts, uint8_t* mask, uint8_t* mask_sign_change,
+                 void* workspace, size_t workspace_bytes, void* stream);
 int nr_normalize3(const float* v, int64_t n, float* out, void* stream);
 int nr_surface_finish(float* rgb, const float* nablas, const uint8_t* mask, int64_t n, float* normals, void* stream);
 

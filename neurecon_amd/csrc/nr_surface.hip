@@ -3,10 +3,13 @@
 //     active rays compacted between iterations, so the SDF MLP only runs on rays still marching;
 //   * surface_render's per-ray finish (ray_casting.py:219-262: black colour and zero normal off
 //     the surface, F.normalize(nablas));
+//   * root finding (ray_casting.py:35-160 `root_finding_surface_points`): the UNISURF march /
+//     first-crossing / secant kernels driven with constant near / far on caller-normalised rays;
 //   * the mesh-extraction grid (utils/mesh_util.py:82-112 `extract_mesh`): voxel coordinates
 //     generated on the device with the reference's own float64 formula, then the forward SDF.
 #include "nr_common.h"
 #include "nr_mlp.h"
+#include "nr_unisurf.h"
 
 namespace nr {
 
@@ -150,6 +153,32 @@ static TracePlan trace_plan(int64_t R) {
 
 static dim3 grid1(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
+constexpr int64_t kRootChunk = 65536;  // rays per chunk: 16.7 M march points at N_steps = 256
+constexpr int kSecFloats = 8;          // per-ray secant state (nr_unisurf.hip kSec)
+
+struct RootPlan {
+  int64_t Rc;
+  size_t o_ro, o_rd, o_near, o_far, o_ptsm, o_sm, o_sec, o_ptss, o_ss, total;
+};
+
+static RootPlan root_plan(int64_t n_rays, int N_steps) {
+  RootPlan p{};
+  p.Rc = n_rays < kRootChunk ? (n_rays > 0 ? n_rays : 1) : kRootChunk;
+  const size_t R = (size_t)p.Rc;
+  size_t o = 0;
+  p.o_ro = o; o += a256(R * 12);
+  p.o_rd = o; o += a256(R * 12);
+  p.o_near = o; o += a256(R * 4);
+  p.o_far = o; o += a256(R * 4);
+  p.o_ptsm = o; o += a256(R * (size_t)N_steps * 12);
+  p.o_sm = o; o += a256(R * (size_t)N_steps * 4);
+  p.o_sec = o; o += a256(R * kSecFloats * 4);
+  p.o_ptss = o; o += a256(R * 12);
+  p.o_ss = o; o += a256(R * 4);
+  p.total = o;
+  return p;
+}
+
 }  // namespace nr
 
 using namespace nr;
@@ -217,6 +246,57 @@ int nr_surface_finish(float* rgb, const float* nablas, const uint8_t* mask, int6
   NR_REQUIRE(rgb && nablas && mask, NR_ERR_ARG, "nr_surface_finish: null argument");
   hipLaunchKernelGGL(surface_finish, grid1(n), dim3(256), 0, (hipStream_t)stream, rgb, nablas, mask, n, normals);
   NR_HIP_CHECK(hipGetLastError());
+  return NR_OK;
+}
+
+size_t nr_root_find_workspace_bytes(int64_t n_rays, int N_steps) {
+  return N_steps >= 2 ? root_plan(n_rays, N_steps).total : 0;
+}
+
+int nr_root_find(const NrSdfDesc* d, const void* packed, const float* rays_o, const float* rays_d, int64_t n_rays,
+                 float near, float far, int N_steps, const float* t_march, int N_secant_steps, float logit_tau,
+                 int fill_inf, float* d_pred, float* pts, uint8_t* mask, uint8_t* mask_sign_change,
+                 void* workspace, size_t workspace_bytes, void* stream) {
+  int rc = check_sdf_desc(d);
+  if (rc) return rc;
+  NR_REQUIRE(n_rays >= 0 && N_steps >= 2 && N_secant_steps >= 0, NR_ERR_ARG,
+             "nr_root_find: need n_rays >= 0, N_steps >= 2, N_secant_steps >= 0");
+  if (n_rays == 0) return NR_OK;
+  NR_REQUIRE(packed && rays_o && rays_d && t_march && d_pred && pts && mask, NR_ERR_ARG, "nr_root_find: null argument");
+  const RootPlan pl = root_plan(n_rays, N_steps);
+  NR_REQUIRE(workspace && workspace_bytes >= pl.total, NR_ERR_WORKSPACE, "nr_root_find: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  auto F = [&](size_t o) { return (float*)(ws + o); };
+  const SdfLayout SL = sdf_layout(*d);
+  for (int64_t r0 = 0; r0 < n_rays; r0 += pl.Rc) {
+    const int R = (int)((n_rays - r0) < pl.Rc ? (n_rays - r0) : pl.Rc);
+    UniChunk c{};
+    c.R = R;
+    c.N_steps = N_steps;
+    c.logit_tau = logit_tau;
+    c.ro = F(pl.o_ro); c.rd = F(pl.o_rd); c.near = F(pl.o_near); c.far = F(pl.o_far);
+    c.pts_m = F(pl.o_ptsm); c.sm = F(pl.o_sm); c.sec = F(pl.o_sec); c.pts_s = F(pl.o_ptss); c.ss = F(pl.o_ss);
+    c.t_march = t_march;
+    const dim3 blk(256), grd((R + 255) / 256);
+    {
+      ProfScope prof("root_prologue", (double)R, st);
+      hipLaunchKernelGGL(rf_prologue, grd, blk, 0, st, c, rays_o + r0 * 3, rays_d + r0 * 3, near, far);
+    }
+    NR_HIP_CHECK(hipGetLastError());
+    if ((rc = launch_sdf(SL, packed, c.pts_m, (int64_t)N_steps * R, c.sm, nullptr, nullptr, d->multires, nullptr, 0,
+                         st)))
+      return rc;
+    hipLaunchKernelGGL(uni_root, grd, blk, 0, st, c);
+    NR_HIP_CHECK(hipGetLastError());
+    for (int i = 0; i < N_secant_steps; ++i) {
+      if ((rc = launch_sdf(SL, packed, c.pts_s, R, c.ss, nullptr, nullptr, d->multires, nullptr, 0, st))) return rc;
+      hipLaunchKernelGGL(uni_secant, grd, blk, 0, st, c, (int)(i == N_secant_steps - 1));
+      NR_HIP_CHECK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(rf_finish, grd, blk, 0, st, c, r0, d_pred, pts, mask, mask_sign_change, fill_inf);
+    NR_HIP_CHECK(hipGetLastError());
+  }
   return NR_OK;
 }
 

@@ -47,6 +47,9 @@ int64_t unisurf_chunk_rays(const NrUnisurfArgs& a);
 
 __global__ void uni_prologue(UniChunk c, const float* rays_o, const float* rays_d);
 __global__ void uni_root(UniChunk c);
+__global__ void rf_prologue(UniChunk c, const float* rays_o, const float* rays_d, float near, float far);
+__global__ void rf_finish(UniChunk c, int64_t ray0, float* d_out, float* pts, uint8_t* mask, uint8_t* msc,
+                          int fill_inf);
 __global__ void uni_secant(UniChunk c, int last);
 __global__ void uni_samples(UniChunk c, UniOut o);
 __global__ void uni_window_ss(UniChunk c);

@@ -59,6 +59,48 @@ __global__ void uni_prologue(UniChunk c, const float* __restrict__ rays_o, const
   }
 }
 
+// standalone root_finding_surface_points (ray_casting.py:35-160, used by surface_render): rays as
+// given (already normalised by the caller), constant near / far, march points sample-major
+__global__ void rf_prologue(UniChunk c, const float* __restrict__ rays_o, const float* __restrict__ rays_d,
+                            float near, float far) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= c.R) return;
+  const float ox = rays_o[r * 3 + 0], oy = rays_o[r * 3 + 1], oz = rays_o[r * 3 + 2];
+  const float dx = rays_d[r * 3 + 0], dy = rays_d[r * 3 + 1], dz = rays_d[r * 3 + 2];
+  c.ro[r * 3 + 0] = ox; c.ro[r * 3 + 1] = oy; c.ro[r * 3 + 2] = oz;
+  c.rd[r * 3 + 0] = dx; c.rd[r * 3 + 1] = dy; c.rd[r * 3 + 2] = dz;
+  c.near[r] = near;
+  c.far[r] = far;
+  for (int i = 0; i < c.N_steps; ++i) {
+    const float d = lerp_ref(near, far, c.t_march[i]);
+    const int64_t q = (int64_t)i * c.R + r;
+    // p_proposal = rays_o + d_proposal * rays_d (ray_casting.py:82)
+    c.pts_m[q * 3 + 0] = fadd(ox, fmul(d, dx));
+    c.pts_m[q * 3 + 1] = fadd(oy, fmul(d, dy));
+    c.pts_m[q * 3 + 2] = fadd(oz, fmul(d, dz));
+  }
+}
+
+// outputs of root_finding_surface_points (ray_casting.py:142-160): d = secant estimate on hits,
+// inf (fill_inf) or far elsewhere, 0 when the first sample is occupied; points o + d*dir on hits, 1
+// elsewhere; mask = hit; mask_sign_change = any crossing
+__global__ void rf_finish(UniChunk c, int64_t ray0, float* __restrict__ d_out, float* __restrict__ pts,
+                          uint8_t* __restrict__ mask, uint8_t* __restrict__ msc, int fill_inf) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= c.R) return;
+  const float* s = c.sec + (int64_t)r * kSec;
+  const bool hit = s[kHit] != 0.0f;
+  const float dp = s[kDPred];
+  float d = hit ? dp : (fill_inf ? __builtin_inff() : c.far[r]);
+  if (s[kFree] == 0.0f) d = 0.0f;
+  const int64_t o = ray0 + r;
+  d_out[o] = d;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) pts[o * 3 + k] = hit ? fadd(c.ro[r * 3 + k], fmul(dp, c.rd[r * 3 + k])) : 1.0f;
+  mask[o] = hit ? 1 : 0;
+  if (msc) msc[o] = s[kCross] != 0.0f ? 1 : 0;
+}
+
 // first sign change of the march (ray_casting.py:89-131) and the first secant estimate
 __global__ void uni_root(UniChunk c) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;

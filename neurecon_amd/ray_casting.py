@@ -1,8 +1,9 @@
 """Surface rendering: drop-in for models/ray_casting.py:163-263.
 
 `sphere_tracing_surface_points` runs entirely in libnrhip (`nr_sphere_trace`: compacted active-ray
-lists on the device, the SDF MLP launched with a device-side count each iteration), and
-`surface_render` chains it with the framework's own native `model.forward` (SDF + nablas +
+lists on the device, the SDF MLP launched with a device-side count each iteration), as does
+`root_finding_surface_points` (`nr_root_find`: march, first crossing, secant steps); `surface_render`
+chains either with the framework's own native `model.forward` (SDF + nablas +
 radiance kernels) and a finish kernel (`nr_surface_finish`).  Called by tools/render_view.py
 (`--use_surface_render sphere_tracing`, render_view.py:236-239).
 """
@@ -47,10 +48,40 @@ def sphere_tracing_surface_points(implicit_surface, rays_o, rays_d, near=0.0, fa
     return d.reshape(shape), pts.reshape(*shape, 3), mask.view(torch.bool).reshape(shape)
 
 
-def root_finding_surface_points(*args, **kwargs):
-    raise NotImplementedError('neurecon_amd: root_finding_surface_points runs inside the native UNISURF renderer '
-                              '(frameworks.unisurf.volume_render); standalone surface_render root finding is not '
-                              'exposed yet')
+def root_finding_surface_points(surface_query_fn, rays_o, rays_d, near=0.0, far=6.0, batched=True, batched_info={},
+                                N_steps=256, logit_tau=0.0, method='secant', N_secant_steps=8, fill_inf=True):
+    """ray_casting.py:35-160 -> (d_pred_out, pt_pred, mask, mask_sign_change); rays_d already
+    normalised.  `surface_query_fn` must be a neurecon_amd ImplicitSurface (its forward SDF runs in
+    the library); near / far are scalars."""
+    from .frameworks.neus import _linspace_table
+    if not hasattr(surface_query_fn, 'nr_packed'):
+        raise NotImplementedError('neurecon_amd: root finding needs a neurecon_amd ImplicitSurface as surface_query_fn')
+    if isinstance(near, torch.Tensor) or isinstance(far, torch.Tensor):
+        raise NotImplementedError('neurecon_amd: per-ray near/far tensors are not supported by nr_root_find')
+    if method != 'secant':
+        raise NotImplementedError(method)
+    L.require_gpu(rays_o, 'rays_o')
+    _no_training(surface_query_fn)
+    shape = rays_o.shape[:-1]
+    ro = rays_o.reshape(-1, 3).float().contiguous()
+    rd = rays_d.reshape(-1, 3).float().contiguous()
+    n = ro.shape[0]
+    dev = ro.device
+    desc, packed = surface_query_fn.nr_packed(dev)
+    lib = L.lib()
+    t = _linspace_table(int(N_steps), dev)
+    d = torch.empty(n, device=dev)
+    pts = torch.empty(n, 3, device=dev)
+    mask = torch.empty(n, dtype=torch.uint8, device=dev)
+    msc = torch.empty(n, dtype=torch.uint8, device=dev)
+    ws_bytes = lib.nr_root_find_workspace_bytes(n, int(N_steps))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    L.check(lib.nr_root_find(ctypes.byref(desc), L.ptr(packed), L.ptr(ro), L.ptr(rd), n, ctypes.c_float(near),
+                             ctypes.c_float(far), int(N_steps), L.ptr(t), int(N_secant_steps), ctypes.c_float(logit_tau),
+                             int(bool(fill_inf)), L.ptr(d), L.ptr(pts), L.ptr(mask), L.ptr(msc), L.ptr(ws), ws_bytes,
+                             L.stream_of(dev)))
+    return (d.reshape(shape), pts.reshape(*shape, 3), mask.view(torch.bool).reshape(shape),
+            msc.view(torch.bool).reshape(shape))
 
 
 def _couples_rays(model):
@@ -64,9 +95,7 @@ def surface_render(rays_o, rays_d, model, calc_normal=True, rayschunk=8192, netc
                    use_view_dirs=True, show_progress=False, ray_casting_algo='', ray_casting_cfgs={},
                    **not_used_kwargs):
     """ray_casting.py:185-263 -> (colors, depths, extras{implicit_nablas, mask_surface[, normals_surface]})."""
-    if ray_casting_algo == 'root_finding':
-        root_finding_surface_points()
-    if ray_casting_algo != 'sphere_tracing':
+    if ray_casting_algo not in ('root_finding', 'sphere_tracing'):
         raise NotImplementedError(ray_casting_algo)
     if not use_view_dirs:
         raise NotImplementedError('neurecon_amd: use_view_dirs=False not supported')
@@ -80,9 +109,13 @@ def surface_render(rays_o, rays_d, model, calc_normal=True, rayschunk=8192, netc
             flat = [-1, 3]
         ro = rays_o.reshape(flat).float().contiguous()
         rd = _normalize3(rays_d.reshape(flat).float())
-        # sphere tracing is per ray: one launch sequence over every ray
-        d_pred, pt_pred, mask = sphere_tracing_surface_points(model.implicit_surface, ro, rd, batched=batched,
-                                                              **ray_casting_cfgs)
+        # ray casting is per ray: one launch sequence over every ray
+        if ray_casting_algo == 'root_finding':
+            d_pred, pt_pred, mask, _ = root_finding_surface_points(model.implicit_surface, ro, rd, batched=batched,
+                                                                   **ray_casting_cfgs)
+        else:
+            d_pred, pt_pred, mask = sphere_tracing_surface_points(model.implicit_surface, ro, rd, batched=batched,
+                                                                  **ray_casting_cfgs)
         n = ro.shape[DIM]
         step = rayschunk if _couples_rays(model) else max(rayschunk, 1 << 18)
         colors, nablas = [], []

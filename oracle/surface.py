@@ -23,11 +23,21 @@ def sphere_trace(sdf_fn, rays_o, rays_d, near=0.0, far=6.0, N_iters=20):
     return d, rays_o + rays_d * d[..., :, None], mask
 
 
-def surface_render_neus(oracle, rays_o, rays_d, calc_normal=True, **cfgs):
+def root_find(sdf_fn, o, d, near=0.0, far=6.0, **cfgs):
+    """ray_casting.py:35-160 with scalar near / far (restated in oracle/unisurf.py:root_find)."""
+    from .unisurf import root_find as rf
+    cfgs.setdefault('fill_inf', True)
+    return rf(sdf_fn, o, d, near * torch.ones(o.shape[:-1]), far * torch.ones(o.shape[:-1]), **cfgs)
+
+
+def surface_render_neus(oracle, rays_o, rays_d, calc_normal=True, algo='sphere_tracing', **cfgs):
     """ray_casting.py:185-263 with a NeuS model (model.forward = neus.py:111-115), batched [B, N, 3]."""
     o = rays_o.reshape(rays_o.shape[0], -1, 3).float()
     d = F.normalize(rays_d.reshape(rays_d.shape[0], -1, 3).float(), dim=-1)
-    dp, pts, mask = sphere_trace(oracle.sdf_net.sdf, o, d, **cfgs)
+    if algo == 'root_finding':
+        dp, pts, mask, _ = root_find(oracle.sdf_net.sdf, o, d, **cfgs)
+    else:
+        dp, pts, mask = sphere_trace(oracle.sdf_net.sdf, o, d, **cfgs)
     _, nab, h = oracle.sdf_net.forward_with_nablas(pts)
     color = oracle.rad_net.forward(pts, d, nab, h)
     color[~mask] = 0

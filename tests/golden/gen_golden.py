@@ -349,6 +349,11 @@ def gen_surface(R):
         rdn = torch.nn.functional.normalize(rd, dim=-1)
         d5, p5, m5 = R.ray_casting.sphere_tracing_surface_points(model.implicit_surface, ro, rdn, near=0.5, far=4.0,
                                                                  N_iters=5)
+        rgb_rf, depth_rf, ex_rf = R.ray_casting.surface_render(ro, rd, model, calc_normal=True, rayschunk=8192,
+                                                               batched=True, ray_casting_algo='root_finding')
+        rf = R.ray_casting.root_finding_surface_points(model.implicit_surface, ro.clone(), rdn.clone(), near=0.5,
+                                                       far=4.0, N_steps=64, N_secant_steps=4, logit_tau=0.01,
+                                                       fill_inf=False)
     # extract_mesh runs as shipped except for what this image lacks: numpy>=1.24 has no np.int
     # (mesh_util.py:87), there is no GPU (`.cuda()`, :104) and no scikit-image/plyfile (the
     # marching-cubes writer is replaced by a capture of the SDF volume it receives).
@@ -374,7 +379,9 @@ def gen_surface(R):
             del np.int
     save('surface.npz', seed=1, rays_o=ro, rays_d=rd, idx=idx, rgb=rgb, depth=depth,
          nablas=ex['implicit_nablas'], mask=ex['mask_surface'], normals=ex['normals_surface'],
-         st5_d=d5, st5_pts=p5, st5_mask=m5, grid16=grids[16], grid24=grids[24])
+         st5_d=d5, st5_pts=p5, st5_mask=m5, grid16=grids[16], grid24=grids[24],
+         rf_rgb=rgb_rf, rf_depth=depth_rf, rf_nablas=ex_rf['implicit_nablas'], rf_mask=ex_rf['mask_surface'],
+         rf_normals=ex_rf['normals_surface'], rf2_d=rf[0], rf2_pts=rf[1], rf2_mask=rf[2], rf2_msc=rf[3])
 
 
 def main():

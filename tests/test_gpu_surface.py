@@ -144,3 +144,57 @@ def test_sdf_grid_512_consistency():
         got = out[torch.from_numpy(i).cuda()]
         print(f'grid512: exact on {(got == ref).float().mean().item() * 100:.2f}% of sampled voxels')
         assert report('grid512', got, ref.cpu(), RT, 1e-6)[0].all()
+
+
+@pytest.mark.parametrize('precision', ['f16x3', 'fp32'])
+def test_surface_render_root_finding_vs_golden(golden, precision):
+    """surface_render(ray_casting_algo='root_finding') (ray_casting.py:35-160, 219-221): 256-step march,
+    first outside->inside crossing, 8 secant steps.  Masks identical, depth within the bar on hits
+    (inf on misses), shading at the traced points vs the oracle as for sphere tracing."""
+    from oracle.nets import RadianceNet, SDFNet
+    from neurecon_amd.ray_casting import _normalize3, root_finding_surface_points, surface_render
+    g = golden('surface')
+    sd = wg.neus_state(seed=int(g['seed']))
+    m = neus_model(sd, precision=precision)
+    ro = to_gpu(g['rays_o'])
+    rgb, depth, ex = surface_render(ro, to_gpu(g['rays_d']), m, calc_normal=True, batched=True,
+                                    ray_casting_algo='root_finding')
+    torch.cuda.synchronize()
+    mask = ex['mask_surface'].cpu().numpy()
+    print(f'hit rays: {mask.sum()} / {mask.size}')
+    assert (mask == g['rf_mask'].astype(bool)).all()
+    dep = depth.cpu().numpy()
+    assert (np.isinf(dep) == np.isinf(g['rf_depth'])).all()
+    assert report('depth (hits)', dep[mask], g['rf_depth'][mask], RT, AT)[0].all()
+    assert report('rgb (end to end)', rgb, g['rf_rgb'], RT, AT)[0].mean() >= 0.99
+    with torch.no_grad():
+        rdn = _normalize3(to_gpu(g['rays_d']))
+        _, pts, _, _ = root_finding_surface_points(m.implicit_surface, ro, rdn)
+        p, v = pts.cpu(), rdn.cpu()
+        _, nab_ref, h = SDFNet(sd).forward_with_nablas(p)
+        c_ref = RadianceNet(sd).forward(p, v, nab_ref, h)
+    mk = torch.from_numpy(mask)
+    c_ref[~mk] = 0
+    n_ref = torch.nn.functional.normalize(nab_ref, dim=-1)
+    n_ref[~mk] = 0
+    assert report('rgb (at traced points)', rgb, c_ref, RT, AT)[0].all()
+    assert report('normals (at traced points)', ex['normals_surface'], n_ref, RT, 1e-4)[0].all()
+
+
+def test_root_finding_cfgs_vs_golden(golden):
+    """root_finding_surface_points with near/far, N_steps=64, N_secant_steps=4, logit_tau=0.01,
+    fill_inf=False (misses get far, occupied first samples 0)."""
+    from neurecon_amd.ray_casting import root_finding_surface_points
+    g = golden('surface')
+    m = neus_model(wg.neus_state(seed=int(g['seed'])), precision='f16x3')
+    rd = torch.nn.functional.normalize(torch.from_numpy(g['rays_d']), dim=-1)
+    with torch.no_grad():
+        d, p, mask, msc = root_finding_surface_points(m.implicit_surface, to_gpu(g['rays_o']), rd.cuda(), near=0.5,
+                                                      far=4.0, N_steps=64, N_secant_steps=4, logit_tau=0.01,
+                                                      fill_inf=False)
+    mask = mask.cpu().numpy()
+    assert (mask == g['rf2_mask'].astype(bool)).all()
+    assert (msc.cpu().numpy() == g['rf2_msc'].astype(bool)).all()
+    assert report('d', d, g['rf2_d'], RT, AT)[0].all()
+    err = np.abs(p.cpu().numpy() - g['rf2_pts']).max(-1)
+    assert (err <= RT * np.abs(g['rf2_d']) + AT).all(), err.max()

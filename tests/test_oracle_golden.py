@@ -200,3 +200,24 @@ def test_volsdf_nerfpp(golden):
     close(out['radiance_out'], g['radiance_out'], 1e-5, 1e-6)
     for k, gk in [('rgb', 'rgb'), ('depth_volume', 'depth'), ('mask_volume', 'mask'), ('normals_volume', 'normals')]:
         close(out[k], g[gk], 1e-5, 1e-6)
+
+
+def test_surface_render_root_finding(golden):
+    """oracle root finding vs ray_casting.surface_render(ray_casting_algo='root_finding') and
+    root_finding_surface_points with non-default cfgs (fill_inf=False, logit_tau, short march)."""
+    from oracle import surface
+    g = golden('surface')
+    orc = NeuSOracle(wg.neus_state(seed=int(g['seed'])))
+    with torch.no_grad():
+        out = surface.surface_render_neus(orc, T(g['rays_o']), T(g['rays_d']), algo='root_finding')
+        np.testing.assert_array_equal(out['mask'].numpy(), g['rf_mask'].astype(bool))
+        close(out['depth'], g['rf_depth'], 1e-6, 1e-6)
+        close(out['rgb'], g['rf_rgb'], 1e-5, 1e-6)
+        close(out['normals'], g['rf_normals'], 1e-5, 1e-6)
+        d = torch.nn.functional.normalize(T(g['rays_d']), dim=-1)
+        dp, p, m, msc = surface.root_find(orc.sdf_net.sdf, T(g['rays_o']), d, near=0.5, far=4.0, N_steps=64,
+                                          N_secant_steps=4, logit_tau=0.01, fill_inf=False)
+        np.testing.assert_array_equal(m.numpy(), g['rf2_mask'].astype(bool))
+        np.testing.assert_array_equal(msc.numpy(), g['rf2_msc'].astype(bool))
+        close(dp, g['rf2_d'], 1e-6, 1e-6)
+        close(p, g['rf2_pts'], 1e-6, 1e-6)
