@@ -3,6 +3,8 @@
 The render path has no data-path exchange: rays are independent (NeuS / VolSDF), so each rank
 renders a contiguous slice of the rays and, when the caller wants the whole frame on every rank,
 the per-ray maps are all-gathered once (RCCL over xGMI with backend 'nccl', gloo on CPU).
+The same driver shards surface_render (sphere tracing / root finding are per ray) and
+`sdf_grid_sharded` splits extract_mesh's voxel grid by contiguous index ranges.
 UNISURF's F.normalize(nablas) couples the points of one `rayschunk` (unisurf.py:36,
 train_util.py:23-71); `align` keeps shard boundaries on those chunk boundaries so the result is
 identical to a single-process render.
@@ -62,7 +64,32 @@ def render_sharded(render_fn, rays_o, rays_d, model, gather=True, align=1, **kw)
     rgb, depth, extras = render_fn(ro, rd, model, **kw)
     if not gather:
         return rgb, depth, extras
+    g = lambda v: gather_rays(v, n, dim=dim, align=align)
+    rgb_all, depth_all = g(rgb), g(depth)
     out = {}
     for k, v in extras.items():
-        out[k] = gather_rays(v, n, dim=dim, align=align) if isinstance(v, torch.Tensor) and v.dim() > dim else v
-    return out['rgb'], out['depth_volume'], out
+        if v is rgb:
+            out[k] = rgb_all
+        elif v is depth:
+            out[k] = depth_all
+        else:
+            out[k] = g(v) if isinstance(v, torch.Tensor) and v.dim() > dim else v
+    return rgb_all, depth_all, out
+
+
+def sdf_grid_sharded(implicit_surface, volume_size=2.0, N=512, gather=True, grid_fn=None):
+    """extract_mesh's N^3 SDF grid (mesh_util.py:82-108) split into contiguous voxel ranges, one per
+    rank (`nr_sdf_grid` evaluates any [i0, i0+n) sub-range with the same coordinates as the whole
+    grid); with gather=True one all_gather assembles the [N, N, N] volume on every rank, else the
+    rank's flat slice and its range are returned.  `grid_fn(i0, n)` overrides the evaluator (tests)."""
+    from .mesh_util import sdf_grid_range
+    rank, ws = world()
+    total = int(N) ** 3
+    lo, hi = shard_bounds(total, rank, ws)
+    if grid_fn is None:
+        part = sdf_grid_range(implicit_surface, volume_size, N, lo, hi - lo)
+    else:
+        part = grid_fn(lo, hi - lo)
+    if not gather:
+        return part, (lo, hi)
+    return gather_rays(part, total, dim=0).reshape(N, N, N)

@@ -22,26 +22,35 @@ from .base import _no_training
 _GRID_CHUNK = 1 << 22  # points per native launch (48 MB of coordinates in the workspace)
 
 
-def sdf_grid(implicit_surface, volume_size=2.0, N=512, chunk=None, device=None):
-    """SDF of extract_mesh's N^3 grid (mesh_util.py:82-108) as a device tensor [N, N, N]."""
+def sdf_grid_range(implicit_surface, volume_size, N, start, count, chunk=None, device=None):
+    """SDF at flat voxel indices [start, start+count) of extract_mesh's N^3 grid -> device tensor [count]."""
     _no_training(implicit_surface)
     dev = torch.device(device) if device is not None else next(implicit_surface.parameters()).device
     if dev.type != 'cuda':
         raise RuntimeError('neurecon_amd: sdf_grid needs the model on a GPU (ROCm) device; the path is HIP-only')
-    N = int(N)
-    total = N ** 3
-    chunk = min(int(chunk or _GRID_CHUNK), total)
+    N, start, count = int(N), int(start), int(count)
+    if start < 0 or count < 0 or start + count > N ** 3:
+        raise ValueError(f'voxel range [{start}, {start + count}) outside the {N}^3 grid')
+    out = torch.empty(count, device=dev)
+    if count == 0:
+        return out
+    chunk = min(int(chunk or _GRID_CHUNK), count)
     desc, packed = implicit_surface.nr_packed(dev)
     lib = L.lib()
-    out = torch.empty(total, device=dev)
     ws_bytes = lib.nr_sdf_grid_workspace_bytes(chunk)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     st = L.stream_of(dev)
-    for i0 in range(0, total, chunk):
-        n = min(chunk, total - i0)
-        L.check(lib.nr_sdf_grid(ctypes.byref(desc), L.ptr(packed), ctypes.c_double(float(volume_size)), N, i0, n,
-                                ctypes.c_void_p(out.data_ptr() + 4 * i0), L.ptr(ws), ws_bytes, st))
-    return out.reshape(N, N, N)
+    for j in range(0, count, chunk):
+        n = min(chunk, count - j)
+        L.check(lib.nr_sdf_grid(ctypes.byref(desc), L.ptr(packed), ctypes.c_double(float(volume_size)), N,
+                                start + j, n, ctypes.c_void_p(out.data_ptr() + 4 * j), L.ptr(ws), ws_bytes, st))
+    return out
+
+
+def sdf_grid(implicit_surface, volume_size=2.0, N=512, chunk=None, device=None):
+    """SDF of extract_mesh's N^3 grid (mesh_util.py:82-108) as a device tensor [N, N, N]."""
+    N = int(N)
+    return sdf_grid_range(implicit_surface, volume_size, N, 0, N ** 3, chunk, device).reshape(N, N, N)
 
 
 def convert_sigma_samples_to_ply(input_3d_sigma_array, voxel_grid_origin, volume_size, ply_filename_out, level=5.0,

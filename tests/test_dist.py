@@ -72,3 +72,54 @@ def test_shard_bounds_cover_and_align():
                 assert b[0][0] == 0 and b[-1][1] == n
                 assert all(b[i][1] == b[i + 1][0] for i in range(ws - 1))
                 assert all(lo % align == 0 for lo, _ in b if lo < n)
+
+
+def _fake_surface_render(ro, rd, model, batched=True, **kw):
+    # surface_render's return convention: (colors, depths, extras without rgb/depth keys)
+    c = torch.stack([ro.sum(-1), rd.sum(-1), (ro * rd).sum(-1)], -1)
+    d = ro.norm(dim=-1)
+    return c, d, {'implicit_nablas': rd * 2, 'mask_surface': d > 1.0}
+
+
+def _fake_grid(N, s):
+    from oracle.surface import grid_points
+    pts = torch.from_numpy(grid_points(N, s))
+    return lambda i0, n: pts[i0:i0 + n].norm(dim=-1)
+
+
+def _worker_surface(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=ws)
+    try:
+        g = torch.Generator().manual_seed(1)
+        ro = torch.randn(1, 41, 3, generator=g)
+        rd = torch.randn(1, 41, 3, generator=g)
+        c, d, ex = nd.render_sharded(_fake_surface_render, ro, rd, None, batched=True)
+        ref = _fake_surface_render(ro, rd, None)
+        ok = (torch.equal(c, ref[0]) and torch.equal(d, ref[1]) and
+              torch.equal(ex['implicit_nablas'], ref[2]['implicit_nablas']) and
+              torch.equal(ex['mask_surface'], ref[2]['mask_surface']))
+        N, s = 9, 2.0
+        grid = nd.sdf_grid_sharded(None, s, N, grid_fn=_fake_grid(N, s))
+        ok = ok and torch.equal(grid, _fake_grid(N, s)(0, N ** 3).reshape(N, N, N))
+        part, (lo, hi) = nd.sdf_grid_sharded(None, s, N, gather=False, grid_fn=_fake_grid(N, s))
+        ok = ok and part.numel() == hi - lo
+        q.put((rank, ok, lo, hi))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_surface_render_and_grid_world2():
+    """surface_render's (colors, depths, extras) convention and the voxel-range split of the mesh grid
+    reassemble exactly into the single-process result."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_surface, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _, _ in res), res
+    assert res[0][2] == 0 and res[0][3] == res[1][2] and res[1][3] == 9 ** 3

@@ -198,3 +198,17 @@ def test_root_finding_cfgs_vs_golden(golden):
     assert report('d', d, g['rf2_d'], RT, AT)[0].all()
     err = np.abs(p.cpu().numpy() - g['rf2_pts']).max(-1)
     assert (err <= RT * np.abs(g['rf2_d']) + AT).all(), err.max()
+
+
+def test_sdf_grid_range_matches_full_grid():
+    """A voxel sub-range (what one rank of dist.sdf_grid_sharded evaluates) is bit-identical to the
+    same slice of the whole grid; out-of-range requests raise."""
+    from neurecon_amd.mesh_util import sdf_grid, sdf_grid_range
+    m = neus_model(wg.neus_state(seed=1), precision='f16x3')
+    N = 24
+    with torch.no_grad():
+        full = sdf_grid(m.implicit_surface, 1.5, N).reshape(-1)
+        part = sdf_grid_range(m.implicit_surface, 1.5, N, 1000, 5001, chunk=777)
+    assert torch.equal(part, full[1000:6001])
+    with pytest.raises(ValueError):
+        sdf_grid_range(m.implicit_surface, 1.5, N, N ** 3 - 3, 4)
