@@ -29,7 +29,11 @@ F16X3_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / 3
 MAC_SDF_FWD = 524_544             # SURVEY §8(a) A5 (incl. the 257-row last layer)
 MAC_SDF_BWD = 459_008             # SURVEY §8(a) A6 (reverse pass for the nablas)
 MAC_RAD = 271_360                 # SURVEY §8(a) A7, NeuS radiance input 289
-RAY_FLOP = 704.8e6                # 128 no-grad SDF + 255 SDF-with-nabla + 127 radiance
+# reference algorithm per ray: 128 no-grad SDF + 255 SDF-with-nabla + 127 radiance.
+# This path evaluates each of the 128 samples once (SDF + nabla when it is drawn):
+# 128 + 127 SDF-with-nabla + 127 radiance; step_tflops counts that executed work.
+RAY_FLOP_REF = 704.8e6
+RAY_FLOP = 2.0 * (255 * (MAC_SDF_FWD + MAC_SDF_BWD) + 127 * MAC_RAD)
 # HBM-side bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc passes of this bench,
 # tools/gpu_pmc.sh); counters cannot be read live, so the latest committed summary is reported.
 PMC_SUMMARY = {'f16x3': 'profiles/r01/f16x3_pmc_summary.json'}  # refreshed with tools/gpu_pmc.sh

@@ -165,6 +165,15 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   c.t_out = a.t_outside;
   c.d_out = F(pl.o_dout); c.x4 = F(pl.o_x4); c.sig_o = F(pl.o_sigo); c.rad_o = F(pl.o_rado);
   c.pts_nog = F(pl.o_ptsn); c.s_nog = F(pl.o_sn);
+  // official_solution evaluates every final sample exactly once, when it is drawn: the coarse and
+  // upsampled points are bit-identical to the final `pts` (neus.py:284 recomputes o + d*dir from
+  // the same depths), so one SDF+nabla launch per round replaces the forward-only round launches
+  // plus the reference's second pass over all samples (neus.py:294); sdf and nablas ride along the
+  // sorted merges.
+  const bool fused = !direct;
+  c.nv = fused ? c.nab_f : nullptr;
+  c.nnew = fused ? F(pl.o_nnew) : nullptr;
+  if (fused) c.sdf_f = c.sv;
   void* mlp_ws = ws + pl.o_mlp;
   const size_t mlp_bytes = a.workspace_bytes - pl.o_mlp;
   const SdfLayout SL = sdf_layout(*a.sdf);
@@ -180,8 +189,8 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   NR_HIP_CHECK(hipGetLastError());
   // coarse SDF (no grad, neus.py:220 / :251); direct_more uses its own uniform depths instead
   if (a.upsample_algo != NR_UPSAMPLE_DIRECT_MORE &&
-      (rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)a.N_samples * R, c.sv, nullptr, nullptr, a.sdf->multires,
-                       nullptr, 0, st)))
+      (rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)a.N_samples * R, c.sv, c.nv, nullptr, a.sdf->multires,
+                       fused ? mlp_ws : nullptr, fused ? mlp_bytes : 0, st)))
     return rc;
   if (a.upsample_algo == NR_UPSAMPLE_DIRECT_MORE) {  // SDF at N_nograd_samples uniform depths
     hipLaunchKernelGGL(neus_nograd_points, grd, blk, 0, st, c);
@@ -202,8 +211,8 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
       hipLaunchKernelGGL(neus_upsample, grd, blk, 0, st, c, it, a.u_fine);
     }
     NR_HIP_CHECK(hipGetLastError());
-    if ((rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)n_up * R, c.snew, nullptr, nullptr, a.sdf->multires,
-                         nullptr, 0, st)))
+    if ((rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)n_up * R, c.snew, c.nnew, nullptr, a.sdf->multires,
+                         fused ? mlp_ws : nullptr, fused ? mlp_bytes : 0, st)))
       return rc;
   }
   {
@@ -211,9 +220,9 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
     hipLaunchKernelGGL(neus_points, grd, blk, 0, st, c);
   }
   NR_HIP_CHECK(hipGetLastError());
-  // SDF + nablas at the samples (neus.py:294)
-  if ((rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)c.S * R, c.sdf_f, c.nab_f, nullptr, a.sdf->multires, mlp_ws,
-                       mlp_bytes, st)))
+  // SDF + nablas at the samples (neus.py:294); already in sv / nv on the fused path
+  if (!fused && (rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)c.S * R, c.sdf_f, c.nab_f, nullptr,
+                                 a.sdf->multires, mlp_ws, mlp_bytes, st)))
     return rc;
   // SDF + nablas + geometry feature at the mid-points, then the radiance net (neus.py:103-106, :298)
   if ((rc = launch_sdf(SL, a.sdf_packed, c.mids, (int64_t)(c.S - 1) * R, c.sdf_m, c.nab_m, c.feat_m,

@@ -53,32 +53,46 @@ __global__ void neus_prologue(NeusChunk c, const float* __restrict__ rays_o, con
   }
 }
 
-// merge the sorted list (dv,sv)[0..L) with the n_up new samples (dnew,snew), in place
+// merge the sorted list (dv,sv[,nv])[0..L) with the n_up new samples (dnew,snew[,nnew]), in place
 __device__ void merge_new(const NeusChunk& c, int r, int L) {
   float dn[kMaxUp], sn[kMaxUp];
+  int8_t pk[kMaxUp];  // original slot of each sorted new sample (to fetch its nabla)
   const int n = c.n_up;
   for (int k = 0; k < n; ++k) {
     dn[k] = c.dnew[(int64_t)k * c.R + r];
     sn[k] = c.snew[(int64_t)k * c.R + r];
+    pk[k] = (int8_t)k;
   }
   for (int k = 1; k < n; ++k) {  // insertion sort (new samples are sorted up to rounding)
     const float d = dn[k], s = sn[k];
+    const int8_t p = pk[k];
     int m = k - 1;
-    while (m >= 0 && dn[m] > d) { dn[m + 1] = dn[m]; sn[m + 1] = sn[m]; --m; }
+    while (m >= 0 && dn[m] > d) { dn[m + 1] = dn[m]; sn[m + 1] = sn[m]; pk[m + 1] = pk[m]; --m; }
     dn[m + 1] = d;
     sn[m + 1] = s;
+    pk[m + 1] = p;
   }
   int i = L - 1, j = n - 1;
   for (int k = L + n - 1; k >= 0 && j >= 0; --k) {
     const int64_t qk = (int64_t)k * c.R + r;
     const float di = i >= 0 ? c.dv[(int64_t)i * c.R + r] : 0.f;
     if (i >= 0 && di > dn[j]) {
+      const int64_t qi = (int64_t)i * c.R + r;
       c.dv[qk] = di;
-      c.sv[qk] = c.sv[(int64_t)i * c.R + r];
+      c.sv[qk] = c.sv[qi];
+      if (c.nv) {
+#pragma unroll
+        for (int e = 0; e < 3; ++e) c.nv[qk * 3 + e] = c.nv[qi * 3 + e];
+      }
       --i;
     } else {
       c.dv[qk] = dn[j];
       c.sv[qk] = sn[j];
+      if (c.nv) {
+        const int64_t qn = (int64_t)pk[j] * c.R + r;
+#pragma unroll
+        for (int e = 0; e < 3; ++e) c.nv[qk * 3 + e] = c.nnew[qn * 3 + e];
+      }
       --j;
     }
   }
@@ -514,6 +528,7 @@ NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc) {
   p.o_rado = take((size_t)(a.N_outside > 0 ? M : 1) * Rc * 3);
   p.o_ptsn = take((size_t)(n_nog > 0 ? n_nog : 1) * Rc * 3);
   p.o_sn = take((size_t)(n_nog > 0 ? n_nog : 1) * Rc);
+  p.o_nnew = take((size_t)(n_up > 0 ? n_up : 1) * Rc * 3);
   p.o_mlp = off;
   p.total = off + nr_mlp_workspace_bytes(1);
   return p;

@@ -17,20 +17,24 @@ import numpy as np
 import torch
 
 from . import _lib as L
-from .base import _no_training
 
 _GRID_CHUNK = 1 << 22  # points per native launch (48 MB of coordinates in the workspace)
 
 
 def sdf_grid_range(implicit_surface, volume_size, N, start, count, chunk=None, device=None):
-    """SDF at flat voxel indices [start, start+count) of extract_mesh's N^3 grid -> device tensor [count]."""
-    _no_training(implicit_surface)
-    dev = torch.device(device) if device is not None else next(implicit_surface.parameters()).device
-    if dev.type != 'cuda':
-        raise RuntimeError('neurecon_amd: sdf_grid needs the model on a GPU (ROCm) device; the path is HIP-only')
+    """SDF at flat voxel indices [start, start+count) of extract_mesh's N^3 grid -> device tensor [count].
+    Inference only, like the reference (`.data`, mesh_util.py:104): no graph, also under grad mode."""
     N, start, count = int(N), int(start), int(count)
     if start < 0 or count < 0 or start + count > N ** 3:
         raise ValueError(f'voxel range [{start}, {start + count}) outside the {N}^3 grid')
+    dev = torch.device(device) if device is not None else next(implicit_surface.parameters()).device
+    if dev.type != 'cuda':
+        raise RuntimeError('neurecon_amd: sdf_grid needs the model on a GPU (ROCm) device; the path is HIP-only')
+    with torch.no_grad():
+        return _grid_range(implicit_surface, volume_size, N, start, count, chunk, dev)
+
+
+def _grid_range(implicit_surface, volume_size, N, start, count, chunk, dev):
     out = torch.empty(count, device=dev)
     if count == 0:
         return out
