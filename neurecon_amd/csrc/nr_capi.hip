@@ -168,12 +168,15 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   // official_solution evaluates every final sample exactly once, when it is drawn: the coarse and
   // upsampled points are bit-identical to the final `pts` (neus.py:284 recomputes o + d*dir from
   // the same depths), so one SDF+nabla launch per round replaces the forward-only round launches
-  // plus the reference's second pass over all samples (neus.py:294); sdf and nablas ride along the
-  // sorted merges.
+  // plus the reference's second pass over all samples (neus.py:294).  sdf rides along the sorted
+  // merges (sv); nablas stay in evaluation order (nraw) and are gathered once by neus_points.
   const bool fused = !direct;
-  c.nv = fused ? c.nab_f : nullptr;
-  c.nnew = fused ? F(pl.o_nnew) : nullptr;
-  if (fused) c.sdf_f = c.sv;
+  c.nraw = fused ? c.nab_f : nullptr;
+  c.idv = fused ? (int*)(ws + pl.o_idv) : nullptr;
+  if (fused) {
+    c.sdf_f = c.sv;
+    c.nab_f = F(pl.o_nsort);
+  }
   void* mlp_ws = ws + pl.o_mlp;
   const size_t mlp_bytes = a.workspace_bytes - pl.o_mlp;
   const SdfLayout SL = sdf_layout(*a.sdf);
@@ -189,7 +192,7 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   NR_HIP_CHECK(hipGetLastError());
   // coarse SDF (no grad, neus.py:220 / :251); direct_more uses its own uniform depths instead
   if (a.upsample_algo != NR_UPSAMPLE_DIRECT_MORE &&
-      (rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)a.N_samples * R, c.sv, c.nv, nullptr, a.sdf->multires,
+      (rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)a.N_samples * R, c.sv, c.nraw, nullptr, a.sdf->multires,
                        fused ? mlp_ws : nullptr, fused ? mlp_bytes : 0, st)))
     return rc;
   if (a.upsample_algo == NR_UPSAMPLE_DIRECT_MORE) {  // SDF at N_nograd_samples uniform depths
@@ -211,7 +214,8 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
       hipLaunchKernelGGL(neus_upsample, grd, blk, 0, st, c, it, a.u_fine);
     }
     NR_HIP_CHECK(hipGetLastError());
-    if ((rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)n_up * R, c.snew, c.nnew, nullptr, a.sdf->multires,
+    float* nslot = fused ? c.nraw + (size_t)(a.N_samples + it * n_up) * R * 3 : nullptr;
+    if ((rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)n_up * R, c.snew, nslot, nullptr, a.sdf->multires,
                          fused ? mlp_ws : nullptr, fused ? mlp_bytes : 0, st)))
       return rc;
   }

@@ -17,9 +17,11 @@ struct NeusChunk {
   float* dv; float* sv; float* wtmp; float* dnew; float* snew;
   float* pts; float* mids; float* dmid;
   float* sdf_f; float* nab_f;
-  // official_solution: nablas computed when a sample is first evaluated and carried through the
-  // merges (nv [S][R][3] parallel to sv, nnew [n_up][R][3] parallel to snew); NULL otherwise
-  float* nv; float* nnew;
+  // official_solution: SDF + nablas computed when a sample is first evaluated.  nraw [S][R][3]
+  // holds the nablas in evaluation order (coarse samples, then each round's new ones); the merges
+  // carry each sample's evaluation slot in idv [S][R] (parallel to dv / sv), and neus_points
+  // gathers the sorted nablas once.  idv == NULL: not fused.
+  float* nraw; int* idv;
   float* sdf_m; float* nab_m; float* feat_m; float* rad_m;
   // NeRF++ background (N_out = 0: none); M = S-1+N_out samples, sample-major
   int N_out;
@@ -46,7 +48,7 @@ struct NeusPlan {
   int64_t Rc;
   size_t o_ro, o_rd, o_near, o_far, o_dv, o_sv, o_wtmp, o_dnew, o_snew, o_pts, o_mids, o_dmid;
   size_t o_sdf_f, o_nab_f, o_sdf_m, o_nab_m, o_feat_m, o_rad_m, o_dout, o_x4, o_sigo, o_rado, o_ptsn, o_sn, o_mlp;
-  size_t o_nnew;
+  size_t o_idv, o_nsort;
   size_t total;
 };
 

@@ -47,13 +47,14 @@ __global__ void neus_prologue(NeusChunk c, const float* __restrict__ rays_o, con
     const float d = fadd(fmul(nr, fsub(1.0f, t)), fmul(fr, t));
     const int64_t q = (int64_t)s * c.R + r;
     c.dv[q] = d;
+    if (c.idv) c.idv[q] = s;
     c.pts[q * 3 + 0] = fadd(ox, fmul(dx, d));
     c.pts[q * 3 + 1] = fadd(oy, fmul(dy, d));
     c.pts[q * 3 + 2] = fadd(oz, fmul(dz, d));
   }
 }
 
-// merge the sorted list (dv,sv[,nv])[0..L) with the n_up new samples (dnew,snew[,nnew]), in place
+// merge the sorted list (dv,sv[,idv])[0..L) with the n_up new samples (dnew,snew), in place
 __device__ void merge_new(const NeusChunk& c, int r, int L) {
   float dn[kMaxUp], sn[kMaxUp];
   int8_t pk[kMaxUp];  // original slot of each sorted new sample (to fetch its nabla)
@@ -80,19 +81,12 @@ __device__ void merge_new(const NeusChunk& c, int r, int L) {
       const int64_t qi = (int64_t)i * c.R + r;
       c.dv[qk] = di;
       c.sv[qk] = c.sv[qi];
-      if (c.nv) {
-#pragma unroll
-        for (int e = 0; e < 3; ++e) c.nv[qk * 3 + e] = c.nv[qi * 3 + e];
-      }
+      if (c.idv) c.idv[qk] = c.idv[qi];
       --i;
     } else {
       c.dv[qk] = dn[j];
       c.sv[qk] = sn[j];
-      if (c.nv) {
-        const int64_t qn = (int64_t)pk[j] * c.R + r;
-#pragma unroll
-        for (int e = 0; e < 3; ++e) c.nv[qk * 3 + e] = c.nnew[qn * 3 + e];
-      }
+      if (c.idv) c.idv[qk] = L + pk[j];  // new samples were evaluated in slots L .. L+n-1
       --j;
     }
   }
@@ -184,9 +178,15 @@ __global__ void neus_points(NeusChunk c) {
   for (int s = 0; s < S; ++s) {
     const int64_t q = s * R + r;
     const float d = c.dv[q];
-    c.pts[q * 3 + 0] = fadd(ox, fmul(dx, d));
-    c.pts[q * 3 + 1] = fadd(oy, fmul(dy, d));
-    c.pts[q * 3 + 2] = fadd(oz, fmul(dz, d));
+    if (c.idv) {  // fused: nablas of the sorted samples from their evaluation slots
+      const int64_t qs = (int64_t)c.idv[q] * R + r;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) c.nab_f[q * 3 + e] = c.nraw[qs * 3 + e];
+    } else {
+      c.pts[q * 3 + 0] = fadd(ox, fmul(dx, d));
+      c.pts[q * 3 + 1] = fadd(oy, fmul(dy, d));
+      c.pts[q * 3 + 2] = fadd(oz, fmul(dz, d));
+    }
     if (s > 0) {
       const float dm = fmul(0.5f, fadd(d, dprev));
       const int64_t qm = (s - 1) * R + r;
@@ -528,7 +528,8 @@ NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc) {
   p.o_rado = take((size_t)(a.N_outside > 0 ? M : 1) * Rc * 3);
   p.o_ptsn = take((size_t)(n_nog > 0 ? n_nog : 1) * Rc * 3);
   p.o_sn = take((size_t)(n_nog > 0 ? n_nog : 1) * Rc);
-  p.o_nnew = take((size_t)(n_up > 0 ? n_up : 1) * Rc * 3);
+  p.o_idv = take((size_t)S * Rc);
+  p.o_nsort = take((size_t)S * Rc * 3);
   p.o_mlp = off;
   p.total = off + nr_mlp_workspace_bytes(1);
   return p;
