@@ -37,8 +37,10 @@ RAY_FLOP = 2.0 * (255 * (MAC_SDF_FWD + MAC_SDF_BWD) + 127 * MAC_RAD)
 # HBM-side bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc passes of this bench,
 # tools/gpu_pmc.sh); counters cannot be read live, so the latest committed summary is reported.
 PMC_SUMMARY = {'f16x3': 'profiles/r01/f16x3_pmc_summary.json'}  # refreshed with tools/gpu_pmc.sh
-PMC_KERNEL = {('sdf_nabla', 'f16x3'): 'void nr::sdf4_kernel<true, false>(nr::SdfKArgs)',
-              ('sdf_nabla', 'fp32'): 'void nr::sdf_kernel<0, true>(nr::SdfKArgs)'}
+# device kernels behind each merged library kernel name (sdf_nabla = samples + mid-points launches)
+PMC_KERNEL = {('sdf_nabla', 'f16x3'): ('void nr::sdf4_kernel<true, false>(nr::SdfKArgs)',
+                                       'void nr::sdf4_kernel<true, true>(nr::SdfKArgs)'),
+              ('sdf_nabla', 'fp32'): ('void nr::sdf_kernel<0, true>(nr::SdfKArgs)',)}
 
 
 def parse():
@@ -148,13 +150,19 @@ KERNEL_MAC = {'sdf_fwd': MAC_SDF_FWD, 'sdf_feat': MAC_SDF_FWD, 'sdf_nabla': MAC_
 
 
 def pmc_traffic(kernel, precision):
+    """HBM bytes per launch of `kernel`, averaged over the launches of every device kernel behind it
+    (the same launch mix the live HIP-event average covers)."""
     path = os.path.join(ROOT, PMC_SUMMARY.get(precision, '-'))
-    name = PMC_KERNEL.get((kernel, precision))
-    if not name or not os.path.exists(path):
+    names = PMC_KERNEL.get((kernel, precision))
+    if not names or not os.path.exists(path):
         return None, None
     with open(path) as f:
-        rec = json.load(f).get(name)
-    return (rec['hbm_bytes_per_launch'], PMC_SUMMARY[precision]) if rec else (None, None)
+        summary = json.load(f)
+    recs = [summary[n] for n in names if n in summary]
+    n = sum(r['launches'] for r in recs)
+    if not n:
+        return None, None
+    return sum(r['hbm_bytes_per_launch'] * r['launches'] for r in recs) / n, PMC_SUMMARY[precision]
 
 
 def roofline(kstats, precision):
