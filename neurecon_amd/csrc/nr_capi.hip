@@ -181,7 +181,7 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   const size_t mlp_bytes = a.workspace_bytes - pl.o_mlp;
   const SdfLayout SL = sdf_layout(*a.sdf);
   const RadLayout RL = rad_layout(*a.rad);
-  const dim3 blk(256), grd((R + 255) / 256);
+  const dim3 blk(64), grd((R + 63) / 64);  // one wave per block: a 4096-ray chunk spreads over 64 CUs
   int rc;
 
   {

@@ -26,7 +26,7 @@ __device__ __forceinline__ void normalize3(float& x, float& y, float& z) {
 // prologue: normalize rays_d (neus.py:169-172), near/far (rend_util.py:167-185), coarse depths
 // (neus.py:209-210) and their points (neus.py:251)
 // ---------------------------------------------------------------------------------------------
-__global__ void neus_prologue(NeusChunk c, const float* __restrict__ rays_o, const float* __restrict__ rays_d,
+__global__ __launch_bounds__(64) void neus_prologue(NeusChunk c, const float* __restrict__ rays_o, const float* __restrict__ rays_d,
                               const float* __restrict__ t_coarse, float r_obj, float near_bypass, float far_bypass) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= c.R) return;
@@ -123,7 +123,7 @@ __device__ void sample_pdf_ray(const float* __restrict__ bins, const float* __re
 
 // one "official_solution" upsampling round (neus.py:252-276) for rays of this chunk:
 // merge last round's samples, then draw n_up new depths and write their points.
-__global__ void neus_upsample(NeusChunk c, int it, const float* __restrict__ u) {
+__global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const float* __restrict__ u) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= c.R) return;
   int L = c.N_samples + it * c.n_up;
@@ -166,7 +166,7 @@ __global__ void neus_upsample(NeusChunk c, int it, const float* __restrict__ u) 
 }
 
 // final merge; points at the S sorted depths (neus.py:284) and at the S-1 mid-points (:287-288)
-__global__ void neus_points(NeusChunk c) {
+__global__ __launch_bounds__(64) void neus_points(NeusChunk c) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= c.R) return;
   const int S = c.S;
@@ -200,7 +200,7 @@ __global__ void neus_points(NeusChunk c) {
 }
 
 // compositing (neus.py:296, :346-380)
-__global__ void neus_composite(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd) {
+__global__ __launch_bounds__(64) void neus_composite(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= c.R) return;
   const int S = c.S;
@@ -278,7 +278,7 @@ __global__ void neus_composite(NeusChunk c, NeusOut o, float s_inv, int calc_nor
 // 'direct_use' / 'direct_more' upsampling (neus.py:215-243): one sample_pdf of N_importance over
 // the visibility weights of the coarse (or N_nograd_samples uniform) depths, s = 1/fixed_s_recp
 // ---------------------------------------------------------------------------------------------
-__global__ void neus_nograd_points(NeusChunk c) {
+__global__ __launch_bounds__(64) void neus_nograd_points(NeusChunk c) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= c.R) return;
   const int64_t R = c.R;
@@ -295,7 +295,7 @@ __global__ void neus_nograd_points(NeusChunk c) {
   }
 }
 
-__global__ void neus_direct_upsample(NeusChunk c, int more, const float* __restrict__ u) {
+__global__ __launch_bounds__(64) void neus_direct_upsample(NeusChunk c, int more, const float* __restrict__ u) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= c.R) return;
   const int64_t R = c.R;
@@ -354,7 +354,7 @@ __global__ void neus_direct_upsample(NeusChunk c, int more, const float* __restr
 // NeRF++ background (neus.py:303-343)
 // ---------------------------------------------------------------------------------------------
 // d_vals_out = cat([d_mid, far / flip(linspace(0,1,N_out+2)[1:-1])]); x_out = [p / |p|, 1 / |p|]
-__global__ void neus_outside_points(NeusChunk c) {
+__global__ __launch_bounds__(64) void neus_outside_points(NeusChunk c) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= c.R) return;
   const int64_t R = c.R;
@@ -376,7 +376,7 @@ __global__ void neus_outside_points(NeusChunk c) {
 __device__ __forceinline__ float softplus1(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
 
 // compositing with the background merged in (neus.py:325-343, :346-380)
-__global__ void neus_composite_outside(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd) {
+__global__ __launch_bounds__(64) void neus_composite_outside(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= c.R) return;
   const int S = c.S, S1 = S - 1, M = S1 + c.N_out;
