@@ -222,6 +222,8 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   {
     ProfScope prof("neus_points", (double)R, st);
     hipLaunchKernelGGL(neus_points, grd, blk, 0, st, c);
+    NR_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(neus_expand, dim3((unsigned)(((int64_t)c.S * R + 255) / 256)), dim3(256), 0, st, c);
   }
   NR_HIP_CHECK(hipGetLastError());
   // SDF + nablas at the samples (neus.py:294); already in sv / nv on the fused path

@@ -58,6 +58,7 @@ __global__ void neus_prologue(NeusChunk c, const float* rays_o, const float* ray
                               float r_obj, float near_bypass, float far_bypass);
 __global__ void neus_upsample(NeusChunk c, int it, const float* u);
 __global__ void neus_points(NeusChunk c);
+__global__ void neus_expand(NeusChunk c);
 __global__ void neus_composite(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd);
 __global__ void neus_outside_points(NeusChunk c);
 __global__ void neus_nograd_points(NeusChunk c);

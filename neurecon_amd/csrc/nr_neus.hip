@@ -165,37 +165,39 @@ __global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const f
   }
 }
 
-// final merge; points at the S sorted depths (neus.py:284) and at the S-1 mid-points (:287-288)
+// final merge of the last round (neus.py:276); points / mid-points follow in neus_expand
 __global__ __launch_bounds__(64) void neus_points(NeusChunk c) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= c.R) return;
-  const int S = c.S;
-  if (c.n_iters > 0) merge_new(c, r, S - c.n_up);
+  if (c.n_iters > 0) merge_new(c, r, c.S - c.n_up);
+}
+
+// per (sample, ray) after the final merge: sample points (or, fused, the sorted nablas) and the
+// S-1 mid-points d_mid = (d_s + d_{s-1}) / 2 (neus.py:284-288); sample-major, fully parallel
+__global__ void neus_expand(NeusChunk c) {
   const int64_t R = c.R;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (int64_t)c.S * R) return;
+  const int64_t s = q / R, r = q - s * R;
   const float ox = c.ro[r * 3], oy = c.ro[r * 3 + 1], oz = c.ro[r * 3 + 2];
   const float dx = c.rd[r * 3], dy = c.rd[r * 3 + 1], dz = c.rd[r * 3 + 2];
-  float dprev = 0.f;
-  for (int s = 0; s < S; ++s) {
-    const int64_t q = s * R + r;
-    const float d = c.dv[q];
-    if (c.idv) {  // fused: nablas of the sorted samples from their evaluation slots
-      const int64_t qs = (int64_t)c.idv[q] * R + r;
+  const float d = c.dv[q];
+  if (c.idv) {  // fused: nablas of the sorted samples from their evaluation slots
+    const int64_t qs = (int64_t)c.idv[q] * R + r;
 #pragma unroll
-      for (int e = 0; e < 3; ++e) c.nab_f[q * 3 + e] = c.nraw[qs * 3 + e];
-    } else {
-      c.pts[q * 3 + 0] = fadd(ox, fmul(dx, d));
-      c.pts[q * 3 + 1] = fadd(oy, fmul(dy, d));
-      c.pts[q * 3 + 2] = fadd(oz, fmul(dz, d));
-    }
-    if (s > 0) {
-      const float dm = fmul(0.5f, fadd(d, dprev));
-      const int64_t qm = (s - 1) * R + r;
-      c.dmid[qm] = dm;
-      c.mids[qm * 3 + 0] = fadd(ox, fmul(dx, dm));
-      c.mids[qm * 3 + 1] = fadd(oy, fmul(dy, dm));
-      c.mids[qm * 3 + 2] = fadd(oz, fmul(dz, dm));
-    }
-    dprev = d;
+    for (int e = 0; e < 3; ++e) c.nab_f[q * 3 + e] = c.nraw[qs * 3 + e];
+  } else {
+    c.pts[q * 3 + 0] = fadd(ox, fmul(dx, d));
+    c.pts[q * 3 + 1] = fadd(oy, fmul(dy, d));
+    c.pts[q * 3 + 2] = fadd(oz, fmul(dz, d));
+  }
+  if (s > 0) {
+    const float dm = fmul(0.5f, fadd(d, c.dv[q - R]));
+    const int64_t qm = q - R;
+    c.dmid[qm] = dm;
+    c.mids[qm * 3 + 0] = fadd(ox, fmul(dx, dm));
+    c.mids[qm * 3 + 1] = fadd(oy, fmul(dy, dm));
+    c.mids[qm * 3 + 2] = fadd(oz, fmul(dz, dm));
   }
 }
 
