@@ -208,7 +208,26 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
                        a.u_fine);
   }
   NR_HIP_CHECK(hipGetLastError());
+  // sorted sample lists ping-pong between two buffers; each merge writes the other one
+  float* dvb[2] = {c.dv, F(pl.o_dv2)};
+  float* svb[2] = {c.sv, F(pl.o_sv2)};
+  int* idb[2] = {c.idv, fused ? (int*)(ws + pl.o_idv2) : nullptr};
+  int cur = 0;
+  auto merge = [&](int L) -> int {
+    ProfScope prof("neus_merge", (double)R, st);
+    const int64_t nt = (int64_t)(L + n_up) * R;
+    hipLaunchKernelGGL(neus_merge, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, c, L, dvb[cur ^ 1],
+                       svb[cur ^ 1], idb[cur ^ 1]);
+    cur ^= 1;
+    c.dv = dvb[cur];
+    c.sv = svb[cur];
+    c.idv = idb[cur];
+    if (fused) c.sdf_f = c.sv;
+    NR_HIP_CHECK(hipGetLastError());
+    return NR_OK;
+  };
   for (int it = 0; it < c.n_iters; ++it) {
+    if (it > 0 && (rc = merge(a.N_samples + (it - 1) * n_up))) return rc;
     {
       ProfScope prof("neus_upsample", (double)R, st);
       hipLaunchKernelGGL(neus_upsample, grd, blk, 0, st, c, it, a.u_fine);
@@ -219,10 +238,9 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
                          fused ? mlp_ws : nullptr, fused ? mlp_bytes : 0, st)))
       return rc;
   }
+  if (c.n_iters > 0 && (rc = merge(c.S - n_up))) return rc;
   {
     ProfScope prof("neus_points", (double)R, st);
-    hipLaunchKernelGGL(neus_points, grd, blk, 0, st, c);
-    NR_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(neus_expand, dim3((unsigned)(((int64_t)c.S * R + 255) / 256)), dim3(256), 0, st, c);
   }
   NR_HIP_CHECK(hipGetLastError());

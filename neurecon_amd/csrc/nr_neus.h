@@ -48,7 +48,7 @@ struct NeusPlan {
   int64_t Rc;
   size_t o_ro, o_rd, o_near, o_far, o_dv, o_sv, o_wtmp, o_dnew, o_snew, o_pts, o_mids, o_dmid;
   size_t o_sdf_f, o_nab_f, o_sdf_m, o_nab_m, o_feat_m, o_rad_m, o_dout, o_x4, o_sigo, o_rado, o_ptsn, o_sn, o_mlp;
-  size_t o_idv, o_nsort;
+  size_t o_idv, o_nsort, o_dv2, o_sv2, o_idv2;
   size_t total;
 };
 
@@ -57,7 +57,7 @@ NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc);
 __global__ void neus_prologue(NeusChunk c, const float* rays_o, const float* rays_d, const float* t_coarse,
                               float r_obj, float near_bypass, float far_bypass);
 __global__ void neus_upsample(NeusChunk c, int it, const float* u);
-__global__ void neus_points(NeusChunk c);
+__global__ void neus_merge(NeusChunk c, int L, float* dv2, float* sv2, int* idv2);
 __global__ void neus_expand(NeusChunk c);
 __global__ void neus_composite(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd);
 __global__ void neus_outside_points(NeusChunk c);

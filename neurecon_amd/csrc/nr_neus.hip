@@ -54,44 +54,6 @@ __global__ __launch_bounds__(64) void neus_prologue(NeusChunk c, const float* __
   }
 }
 
-// merge the sorted list (dv,sv[,idv])[0..L) with the n_up new samples (dnew,snew), in place
-__device__ void merge_new(const NeusChunk& c, int r, int L) {
-  float dn[kMaxUp], sn[kMaxUp];
-  int8_t pk[kMaxUp];  // original slot of each sorted new sample (to fetch its nabla)
-  const int n = c.n_up;
-  for (int k = 0; k < n; ++k) {
-    dn[k] = c.dnew[(int64_t)k * c.R + r];
-    sn[k] = c.snew[(int64_t)k * c.R + r];
-    pk[k] = (int8_t)k;
-  }
-  for (int k = 1; k < n; ++k) {  // insertion sort (new samples are sorted up to rounding)
-    const float d = dn[k], s = sn[k];
-    const int8_t p = pk[k];
-    int m = k - 1;
-    while (m >= 0 && dn[m] > d) { dn[m + 1] = dn[m]; sn[m + 1] = sn[m]; pk[m + 1] = pk[m]; --m; }
-    dn[m + 1] = d;
-    sn[m + 1] = s;
-    pk[m + 1] = p;
-  }
-  int i = L - 1, j = n - 1;
-  for (int k = L + n - 1; k >= 0 && j >= 0; --k) {
-    const int64_t qk = (int64_t)k * c.R + r;
-    const float di = i >= 0 ? c.dv[(int64_t)i * c.R + r] : 0.f;
-    if (i >= 0 && di > dn[j]) {
-      const int64_t qi = (int64_t)i * c.R + r;
-      c.dv[qk] = di;
-      c.sv[qk] = c.sv[qi];
-      if (c.idv) c.idv[qk] = c.idv[qi];
-      --i;
-    } else {
-      c.dv[qk] = dn[j];
-      c.sv[qk] = sn[j];
-      if (c.idv) c.idv[qk] = L + pk[j];  // new samples were evaluated in slots L .. L+n-1
-      --j;
-    }
-  }
-}
-
 // sample_pdf(bins=dv[0..L), weights=wtmp[0..L-1) (already +1e-5), N=n, u) -> out[k*R + r]
 // total = sum of the (+1e-5) weights.  rend_util.py:255-292.
 __device__ void sample_pdf_ray(const float* __restrict__ bins, const float* __restrict__ w, int64_t stride, int L,
@@ -126,8 +88,7 @@ __device__ void sample_pdf_ray(const float* __restrict__ bins, const float* __re
 __global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const float* __restrict__ u) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= c.R) return;
-  int L = c.N_samples + it * c.n_up;
-  if (it > 0) merge_new(c, r, L - c.n_up);
+  const int L = c.N_samples + it * c.n_up;  // last round's samples were merged by neus_merge
   const int64_t R = c.R;
   const float S = (float)(64 << it);  // 64 * 2**i
   float prev_slope = 0.0f;
@@ -165,11 +126,44 @@ __global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const f
   }
 }
 
-// final merge of the last round (neus.py:276); points / mid-points follow in neus_expand
-__global__ __launch_bounds__(64) void neus_points(NeusChunk c) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= c.R) return;
-  if (c.n_iters > 0) merge_new(c, r, c.S - c.n_up);
+// merge (neus.py:276: cat + sort + gather) of the sorted list (dv, sv, idv)[0..L) with the n_up new
+// samples (dnew, snew) into (dv2, sv2, idv2)[0..L+n_up), one thread per (output element, ray):
+// old element i lands at i + #(new < d_i), new element j at rank_j + #(old <= d_j) (stable; ties put
+// new after old) — the order of a stable sort of the concatenation.
+__global__ void neus_merge(NeusChunk c, int L, float* __restrict__ dv2, float* __restrict__ sv2,
+                           int* __restrict__ idv2) {
+  const int64_t R = c.R;
+  const int n = c.n_up;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)(L + n) * R) return;
+  const int64_t e = t / R, r = t - e * R;
+  if (e < L) {
+    const int64_t q = e * R + r;
+    const float d = c.dv[q];
+    int cnt = 0;
+    for (int k = 0; k < n; ++k) cnt += c.dnew[k * R + r] < d ? 1 : 0;
+    const int64_t qo = (e + cnt) * R + r;
+    dv2[qo] = d;
+    sv2[qo] = c.sv[q];
+    if (idv2) idv2[qo] = c.idv[q];
+  } else {
+    const int j = (int)(e - L);
+    const float d = c.dnew[j * R + r];
+    int rank = 0;
+    for (int k = 0; k < n; ++k) {
+      const float v = c.dnew[k * R + r];
+      rank += (v < d || (v == d && k < j)) ? 1 : 0;
+    }
+    int lo = 0, hi = L;  // upper bound of d in the sorted old list
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if (c.dv[m * R + r] <= d) lo = m + 1; else hi = m;
+    }
+    const int64_t qo = (int64_t)(rank + lo) * R + r;
+    dv2[qo] = d;
+    sv2[qo] = c.snew[j * R + r];
+    if (idv2) idv2[qo] = L + j;  // new samples were evaluated in slots L .. L+n-1
+  }
 }
 
 // per (sample, ray) after the final merge: sample points (or, fused, the sorted nablas) and the
@@ -532,6 +526,9 @@ NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc) {
   p.o_sn = take((size_t)(n_nog > 0 ? n_nog : 1) * Rc);
   p.o_idv = take((size_t)S * Rc);
   p.o_nsort = take((size_t)S * Rc * 3);
+  p.o_dv2 = take((size_t)S * Rc);  // merge ping-pong buffers
+  p.o_sv2 = take((size_t)S * Rc);
+  p.o_idv2 = take((size_t)S * Rc);
   p.o_mlp = off;
   p.total = off + nr_mlp_workspace_bytes(1);
   return p;
