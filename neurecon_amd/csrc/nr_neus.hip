@@ -130,6 +130,9 @@ __global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const f
 // samples (dnew, snew) into (dv2, sv2, idv2)[0..L+n_up), one thread per (output element, ray):
 // old element i lands at i + #(new < d_i), new element j at rank_j + #(old <= d_j) (stable; ties put
 // new after old) — the order of a stable sort of the concatenation.
+// sort key: NaN after everything (torch.sort order), so positions stay a permutation for any input
+__device__ __forceinline__ float merge_key(float v) { return v != v ? __builtin_inff() : v; }
+
 __global__ void neus_merge(NeusChunk c, int L, float* __restrict__ dv2, float* __restrict__ sv2,
                            int* __restrict__ idv2) {
   const int64_t R = c.R;
@@ -139,25 +142,25 @@ __global__ void neus_merge(NeusChunk c, int L, float* __restrict__ dv2, float* _
   const int64_t e = t / R, r = t - e * R;
   if (e < L) {
     const int64_t q = e * R + r;
-    const float d = c.dv[q];
+    const float d = c.dv[q], kd = merge_key(d);
     int cnt = 0;
-    for (int k = 0; k < n; ++k) cnt += c.dnew[k * R + r] < d ? 1 : 0;
+    for (int k = 0; k < n; ++k) cnt += merge_key(c.dnew[k * R + r]) < kd ? 1 : 0;
     const int64_t qo = (e + cnt) * R + r;
     dv2[qo] = d;
     sv2[qo] = c.sv[q];
     if (idv2) idv2[qo] = c.idv[q];
   } else {
     const int j = (int)(e - L);
-    const float d = c.dnew[j * R + r];
+    const float d = c.dnew[j * R + r], kd = merge_key(d);
     int rank = 0;
     for (int k = 0; k < n; ++k) {
-      const float v = c.dnew[k * R + r];
-      rank += (v < d || (v == d && k < j)) ? 1 : 0;
+      const float v = merge_key(c.dnew[k * R + r]);
+      rank += (v < kd || (v == kd && k < j)) ? 1 : 0;
     }
     int lo = 0, hi = L;  // upper bound of d in the sorted old list
     while (lo < hi) {
       const int m = (lo + hi) >> 1;
-      if (c.dv[m * R + r] <= d) lo = m + 1; else hi = m;
+      if (merge_key(c.dv[m * R + r]) <= kd) lo = m + 1; else hi = m;
     }
     const int64_t qo = (int64_t)(rank + lo) * R + r;
     dv2[qo] = d;
