@@ -94,6 +94,7 @@ __global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const f
   float prev_slope = 0.0f;
   double T = 1.0;
   float s0 = c.sv[r], z0 = c.dv[r];
+#pragma unroll 8  // independent loads of the next intervals issue ahead of the serial scan
   for (int i = 0; i < L - 1; ++i) {
     const float s1 = c.sv[(i + 1) * R + r], z1 = c.dv[(i + 1) * R + r];
     const float mid = fmul(fadd(s0, s1), 0.5f);
@@ -208,6 +209,7 @@ __global__ __launch_bounds__(64) void neus_composite(NeusChunk c, NeusOut o, flo
   double T = 1.0, acc = 0.0, rgb0 = 0.0, rgb1 = 0.0, rgb2 = 0.0, n0 = 0.0, n1 = 0.0, n2 = 0.0;
   float cprev = sigmoidf_ref(fmul(c.sdf_f[r], s_inv));
   if (o.cdf) o.cdf[ro * S] = cprev;
+#pragma unroll 4  // the per-sample loads (sdf, radiance, nablas) issue ahead of the serial scan
   for (int i = 0; i < S - 1; ++i) {
     const float cn = sigmoidf_ref(fmul(c.sdf_f[(i + 1) * R + r], s_inv));
     const float alpha = fmaxf(fdiv(fsub(cprev, cn), fadd(cprev, 1e-10f)), 0.0f);
@@ -234,6 +236,7 @@ __global__ __launch_bounds__(64) void neus_composite(NeusChunk c, NeusOut o, flo
   const float accf = (float)acc;
   const float denom = fadd(accf, 1e-10f);
   double depth = 0.0;
+#pragma unroll 8
   for (int i = 0; i < S - 1; ++i) {
     const int64_t q = i * R + r;
     depth += (double)fmul(fdiv(c.wtmp[q], denom), c.dmid[q]);
