@@ -14,10 +14,10 @@ sys.path.insert(0, os.path.join(ROOT, 'tests'))
 sys.path.insert(0, os.path.join(ROOT, 'tests', 'golden'))
 
 
-def rays(dev):
+def rays(dev, key='b'):
     import weightgen as wg
     from neurecon_amd import rend_util
-    H, W, f, dist = wg.CAMERAS['b']
+    H, W, f, dist = wg.CAMERAS[key]
     c2w = wg.look_at_c2w(dist)[None].to(dev)
     K = wg.intrinsics(f, H, W)[None].to(dev)
     ro, rd, _ = rend_util.get_rays(c2w, K, H, W)
@@ -45,6 +45,7 @@ def main():
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--precision', default='f16x3')
+    ap.add_argument('--configs', action='store_true', help='also time BASELINE configs (c), (d), (e)')
     args = ap.parse_args()
     import weightgen as wg
     from helpers import unisurf_model, volsdf_model
@@ -66,7 +67,41 @@ def main():
         dt, ks = timeit(lambda: unisurf.volume_render(ro, rd, mu, batched=True, calc_normal=True,
                                                       detailed_output=False, logit_tau=0.0), args.steps, args.warmup)
     out['unisurf'] = {'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3, 'kernels': ks}
-    print(json.dumps(out, default=str))
+    print(json.dumps(out, default=str), flush=True)
+    if args.configs:
+        print(json.dumps(configs(args), default=str), flush=True)
+
+
+def configs(args):
+    """BASELINE.json configs (c), (d), (e) on one GPU: VolSDF 2048 rays x (128 + 128) error-bounded
+    samples (32x64 camera); NeuS + NeRF++ full 800x600 frame (480,000 rays, 64 + 64 + 32 outside);
+    UNISURF 4096 rays (64x64 camera, secant root finding)."""
+    import weightgen as wg
+    from helpers import neus_model, unisurf_model, volsdf_model
+    from neurecon_amd.frameworks import neus, unisurf, volsdf
+    dev = torch.device('cuda')
+    res = {}
+    ro, rd = rays(dev, 'c')
+    mv = volsdf_model(wg.volsdf_state(seed=5, beta_init=1e-3), 1e-3, precision=args.precision)
+    kw = dict(near=0.0, far=6.0, batched=True, calc_normal=True, detailed_output=False, N_samples=128,
+              N_importance=128, max_upsample_steps=6)
+    with torch.no_grad():
+        dt, ks = timeit(lambda: volsdf.volume_render(ro, rd, mv, **kw), args.steps, args.warmup)
+    res['c_volsdf_2048x256'] = {'rays': ro.shape[1], 'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3}
+    ro, rd = rays(dev, 'd')
+    mn = neus_model(wg.neus_state(seed=4, use_outside_nerf=True), use_outside_nerf=True, precision=args.precision)
+    kw = dict(obj_bounding_radius=1.0, batched=True, calc_normal=True, detailed_output=False, N_samples=64,
+              N_importance=64, N_outside=32)
+    with torch.no_grad():
+        dt, ks = timeit(lambda: neus.volume_render(ro, rd, mn, **kw), max(1, args.steps // 2), 1)
+    res['d_neus_nerfpp_800x600'] = {'rays': ro.shape[1], 'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3}
+    ro, rd = rays(dev, 'e')
+    mu = unisurf_model(wg.unisurf_state(seed=3), precision=args.precision)
+    with torch.no_grad():
+        dt, ks = timeit(lambda: unisurf.volume_render(ro, rd, mu, batched=True, calc_normal=True,
+                                                      detailed_output=False, logit_tau=0.0), args.steps, args.warmup)
+    res['e_unisurf_4096'] = {'rays': ro.shape[1], 'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3}
+    return res
 
 
 if __name__ == '__main__':
