@@ -240,3 +240,31 @@ def test_f16x3_sdf_net_ragged_and_scaled(gain):
         assert report(f'f16x3 sdf(no grad) P={P}', s0, ref_s, 1e-4, 1e-6 * scale)[0].all()
         assert report(f'f16x3 nabla P={P}', n, ref_n, 1e-3, 1e-3 * float(ref_n.abs().max()))[0].all()
         assert report(f'f16x3 h P={P}', h, ref_h, 1e-4, 1e-5 * float(ref_h.abs().max()))[0].all()
+
+
+@pytest.mark.parametrize('framework', ['neus', 'volsdf'])
+def test_multi_chunk_render_is_chunk_invariant(framework):
+    """n_rays above the library's internal chunk (16384 rays) runs several chunks through the same
+    workspace (NeuS: ping-pong merge buffers, evaluation slots; VolSDF: sampler lists): the result
+    must be bit-identical to rendering the same rays in separate calls."""
+    from helpers import volsdf_model
+    from neurecon_amd.frameworks import neus, volsdf
+    H, W, f, dist = wg.CAMERAS['d']
+    from neurecon_amd import rend_util
+    ro, rd, _ = rend_util.get_rays(wg.look_at_c2w(dist)[None].cuda(), wg.intrinsics(f, H, W)[None].cuda(), H, W)
+    n = 16384 + 3000
+    ro, rd = ro[:, 200000:200000 + n].contiguous(), rd[:, 200000:200000 + n].contiguous()
+    if framework == 'neus':
+        m = neus_model(wg.neus_state(seed=1), precision='f16x3')
+        fn = lambda o, d: neus.volume_render(o, d, m, batched=True, calc_normal=True, detailed_output=False,
+                                             N_samples=64, N_importance=64)
+    else:
+        m = volsdf_model(wg.volsdf_state(seed=2, beta_init=0.1), 0.1, precision='f16x3')
+        fn = lambda o, d: volsdf.volume_render(o, d, m, batched=True, calc_normal=True, detailed_output=False,
+                                               N_samples=64, N_importance=64, max_upsample_steps=6)
+    with torch.no_grad():
+        rgb, depth, ex = fn(ro, rd)
+        parts = [fn(ro[:, a:b].contiguous(), rd[:, a:b].contiguous()) for a, b in [(0, 5000), (5000, n)]]
+    assert torch.equal(rgb, torch.cat([p[0] for p in parts], 1))
+    assert torch.equal(depth, torch.cat([p[1] for p in parts], 1))
+    assert torch.equal(ex['normals_volume'], torch.cat([p[2]['normals_volume'] for p in parts], 1))
