@@ -230,7 +230,8 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
     if (it > 0 && (rc = merge(a.N_samples + (it - 1) * n_up))) return rc;
     {
       ProfScope prof("neus_upsample", (double)R, st);
-      hipLaunchKernelGGL(neus_upsample, grd, blk, 0, st, c, it, a.u_fine);
+      hipLaunchKernelGGL(neus_upsample, dim3((unsigned)R), dim3(64), (4 * c.S + 1) * sizeof(float), st, c, it,
+                         a.u_fine);
     }
     NR_HIP_CHECK(hipGetLastError());
     float* nslot = fused ? c.nraw + (size_t)(a.N_samples + it * n_up) * R * 3 : nullptr;

@@ -83,44 +83,76 @@ __device__ void sample_pdf_ray(const float* __restrict__ bins, const float* __re
   for (; k < n; ++k) out[k * out_stride] = invert_one(u[k], c_prev, c_prev, b_prev, b_prev);
 }
 
-// one "official_solution" upsampling round (neus.py:252-276) for rays of this chunk:
-// merge last round's samples, then draw n_up new depths and write their points.
+// one "official_solution" upsampling round (neus.py:252-276): one wave per ray.  The per-interval
+// work (slopes, logistic CDFs, alpha) runs across the lanes; the three order-sensitive scans
+// (transmittance cumprod, the ATen-order weight sum, the CDF cumsum) run on lane 0 over LDS with
+// exactly the arithmetic of the per-ray version; the n_up inverse-CDF draws run across lanes.
 __global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const float* __restrict__ u) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= c.R) return;
+  extern __shared__ float lds[];
+  const int r = blockIdx.x, l = threadIdx.x;
   const int L = c.N_samples + it * c.n_up;  // last round's samples were merged by neus_merge
   const int64_t R = c.R;
+  float* sz = lds;           // depths [L]
+  float* ss = sz + c.S;      // sdf [L]
+  float* sa = ss + c.S;      // alpha, then weights [L-1]
+  float* scdf = sa + c.S;    // cdf [L]
+  float* stot = scdf + c.S;  // [1] weight total
+  for (int i = l; i < L; i += 64) {
+    sz[i] = c.dv[i * R + r];
+    ss[i] = c.sv[i * R + r];
+  }
+  __syncthreads();
   const float S = (float)(64 << it);  // 64 * 2**i
-  float prev_slope = 0.0f;
-  double T = 1.0;
-  float s0 = c.sv[r], z0 = c.dv[r];
-#pragma unroll 8  // independent loads of the next intervals issue ahead of the serial scan
-  for (int i = 0; i < L - 1; ++i) {
-    const float s1 = c.sv[(i + 1) * R + r], z1 = c.dv[(i + 1) * R + r];
+  for (int i = l; i < L - 1; i += 64) {
+    const float s0 = ss[i], s1 = ss[i + 1], z0 = sz[i], z1 = sz[i + 1];
     const float mid = fmul(fadd(s0, s1), 0.5f);
     const float slope = fdiv(fsub(s1, s0), fadd(fsub(z1, z0), 1e-5f));
+    const float prev_slope = i > 0 ? fdiv(fsub(s0, ss[i - 1]), fadd(fsub(z0, sz[i - 1]), 1e-5f)) : 0.0f;
     float m = fminf(prev_slope, slope);
-    prev_slope = slope;
     m = fminf(fmaxf(m, -10.0f), 0.0f);
     const float dist = fsub(z1, z0);
     const float md = fmul(fmul(m, dist), 0.5f);
     const float c0 = sigmoidf_ref(fmul(fsub(mid, md), S));
     const float c1 = sigmoidf_ref(fmul(fadd(mid, md), S));
-    const float alpha = fdiv(fadd(fsub(c0, c1), 1e-5f), fadd(c0, 1e-5f));
-    const float w = fmul(alpha, (float)T);
-    T *= (double)fadd(fsub(1.0f, alpha), 1e-10f);
-    c.wtmp[i * R + r] = w;
-    s0 = s1;
-    z0 = z1;
+    sa[i] = fdiv(fadd(fsub(c0, c1), 1e-5f), fadd(c0, 1e-5f));
   }
-  const float* wr = c.wtmp + r;
-  const float total = aten_row_sum(L - 1, [&](int i) { return fadd(wr[i * R], 1e-5f); });
-  sample_pdf_ray(c.dv + r, wr, R, L, total, u, c.n_up, c.dnew + r, R);
+  __syncthreads();
+  if (l == 0) {
+    double T = 1.0;
+    for (int i = 0; i < L - 1; ++i) {
+      const float alpha = sa[i];
+      sa[i] = fmul(alpha, (float)T);
+      T *= (double)fadd(fsub(1.0f, alpha), 1e-10f);
+    }
+    const float total = aten_row_sum(L - 1, [&](int i) { return fadd(sa[i], 1e-5f); });
+    // sample_pdf's cdf (rend_util.py:259-264): fp64 running sum of the normalised weights
+    double acc = 0.0;
+    scdf[0] = 0.0f;
+    for (int i = 0; i < L - 1; ++i) {
+      acc += (double)fdiv(fadd(sa[i], 1e-5f), total);
+      scdf[i + 1] = (float)acc;
+    }
+    stot[0] = total;
+  }
+  __syncthreads();
   const float ox = c.ro[r * 3], oy = c.ro[r * 3 + 1], oz = c.ro[r * 3 + 2];
   const float dx = c.rd[r * 3], dy = c.rd[r * 3 + 1], dz = c.rd[r * 3 + 2];
-  for (int k = 0; k < c.n_up; ++k) {
+  for (int k = l; k < c.n_up; k += 64) {
+    const float uk = u[k];
+    float d;
+    if (uk <= 0.0f) {  // searchsorted -> 0: below = above = 0
+      d = invert_one(uk, 0.0f, 0.0f, sz[0], sz[0]);
+    } else {
+      int lo = 0, hi = L - 1;  // first interval i with uk <= cdf[i+1]
+      while (lo < hi) {
+        const int mm = (lo + hi) >> 1;
+        if (uk <= scdf[mm + 1]) hi = mm; else lo = mm + 1;
+      }
+      d = lo < L - 1 ? invert_one(uk, scdf[lo], scdf[lo + 1], sz[lo], sz[lo + 1])
+                     : invert_one(uk, scdf[L - 1], scdf[L - 1], sz[L - 1], sz[L - 1]);  // above every cdf
+    }
     const int64_t q = k * R + r;
-    const float d = c.dnew[q];
+    c.dnew[q] = d;
     c.pts[q * 3 + 0] = fadd(ox, fmul(dx, d));
     c.pts[q * 3 + 1] = fadd(oy, fmul(dy, d));
     c.pts[q * 3 + 2] = fadd(oz, fmul(dz, d));
