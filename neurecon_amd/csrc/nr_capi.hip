@@ -268,7 +268,8 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
     hipLaunchKernelGGL(neus_composite_outside, grd, blk, 0, st, c, o, a.s, a.calc_normal, a.white_bkgd);
   } else {
     ProfScope prof("neus_composite", (double)R, st);
-    hipLaunchKernelGGL(neus_composite, grd, blk, 0, st, c, o, a.s, a.calc_normal, a.white_bkgd);
+    hipLaunchKernelGGL(neus_composite, dim3((unsigned)R), dim3(64), 8 * c.S * sizeof(float), st, c, o, a.s,
+                       a.calc_normal, a.white_bkgd);
   }
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;

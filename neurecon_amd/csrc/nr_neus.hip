@@ -231,65 +231,82 @@ __global__ void neus_expand(NeusChunk c) {
   }
 }
 
-// compositing (neus.py:296, :346-380)
+// compositing (neus.py:296, :346-380), one wave per ray: logistic CDFs, alpha, radiance and unit
+// normals per sample across the lanes (LDS); the transmittance product and the fp64 rgb / acc /
+// normal / depth accumulations on lane 0 in sample order, exactly as the per-ray version did.
 __global__ __launch_bounds__(64) void neus_composite(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= c.R) return;
+  extern __shared__ float lds[];
+  const int r = blockIdx.x, l = threadIdx.x;
   const int S = c.S;
   const int64_t R = c.R;
   const int64_t ro = o.ray0 + r;  // global ray index for outputs
-  double T = 1.0, acc = 0.0, rgb0 = 0.0, rgb1 = 0.0, rgb2 = 0.0, n0 = 0.0, n1 = 0.0, n2 = 0.0;
-  float cprev = sigmoidf_ref(fmul(c.sdf_f[r], s_inv));
-  if (o.cdf) o.cdf[ro * S] = cprev;
-#pragma unroll 4  // the per-sample loads (sdf, radiance, nablas) issue ahead of the serial scan
-  for (int i = 0; i < S - 1; ++i) {
-    const float cn = sigmoidf_ref(fmul(c.sdf_f[(i + 1) * R + r], s_inv));
-    const float alpha = fmaxf(fdiv(fsub(cprev, cn), fadd(cprev, 1e-10f)), 0.0f);
-    const float w = fmul(alpha, (float)T);
-    T *= (double)fadd(fsub(1.0f, alpha), 1e-10f);
+  float* scdf = lds;          // [S]
+  float* sal = scdf + S;      // [S-1] alpha, then weights
+  float* srad = sal + S;      // [S-1][3]
+  float* snrm = srad + 3 * S; // [S-1][3] unit nablas
+  for (int i = l; i < S; i += 64) {
+    const float cdf = sigmoidf_ref(fmul(c.sdf_f[i * R + r], s_inv));
+    scdf[i] = cdf;
+    if (o.cdf) o.cdf[ro * S + i] = cdf;
+  }
+  __syncthreads();
+  for (int i = l; i < S - 1; i += 64) {
+    const float cp = scdf[i], cn = scdf[i + 1];
+    const float alpha = fmaxf(fdiv(fsub(cp, cn), fadd(cp, 1e-10f)), 0.0f);
+    sal[i] = alpha;
+    if (o.alpha) o.alpha[ro * (S - 1) + i] = alpha;
     const int64_t q = i * R + r;
-    rgb0 += (double)fmul(w, c.rad_m[q * 3 + 0]);
-    rgb1 += (double)fmul(w, c.rad_m[q * 3 + 1]);
-    rgb2 += (double)fmul(w, c.rad_m[q * 3 + 2]);
-    acc += (double)w;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) srad[i * 3 + e] = c.rad_m[q * 3 + e];
     if (calc_normal) {
       float x = c.nab_f[q * 3 + 0], y = c.nab_f[q * 3 + 1], z = c.nab_f[q * 3 + 2];
       normalize3(x, y, z);
-      n0 += (double)fmul(x, w);
-      n1 += (double)fmul(y, w);
-      n2 += (double)fmul(z, w);
+      snrm[i * 3 + 0] = x;
+      snrm[i * 3 + 1] = y;
+      snrm[i * 3 + 2] = z;
     }
-    c.wtmp[q] = w;
-    if (o.cdf) o.cdf[ro * S + i + 1] = cn;
-    if (o.alpha) o.alpha[ro * (S - 1) + i] = alpha;
-    if (o.weights) o.weights[ro * (S - 1) + i] = w;
-    cprev = cn;
   }
-  const float accf = (float)acc;
-  const float denom = fadd(accf, 1e-10f);
-  double depth = 0.0;
-#pragma unroll 8
-  for (int i = 0; i < S - 1; ++i) {
-    const int64_t q = i * R + r;
-    depth += (double)fmul(fdiv(c.wtmp[q], denom), c.dmid[q]);
+  __syncthreads();
+  if (l == 0) {
+    double T = 1.0, acc = 0.0, rgb0 = 0.0, rgb1 = 0.0, rgb2 = 0.0, n0 = 0.0, n1 = 0.0, n2 = 0.0;
+    for (int i = 0; i < S - 1; ++i) {
+      const float alpha = sal[i];
+      const float w = fmul(alpha, (float)T);
+      T *= (double)fadd(fsub(1.0f, alpha), 1e-10f);
+      rgb0 += (double)fmul(w, srad[i * 3 + 0]);
+      rgb1 += (double)fmul(w, srad[i * 3 + 1]);
+      rgb2 += (double)fmul(w, srad[i * 3 + 2]);
+      acc += (double)w;
+      if (calc_normal) {
+        n0 += (double)fmul(snrm[i * 3 + 0], w);
+        n1 += (double)fmul(snrm[i * 3 + 1], w);
+        n2 += (double)fmul(snrm[i * 3 + 2], w);
+      }
+      sal[i] = w;
+    }
+    const float accf = (float)acc;
+    const float denom = fadd(accf, 1e-10f);
+    double depth = 0.0;
+    for (int i = 0; i < S - 1; ++i) depth += (double)fmul(fdiv(sal[i], denom), c.dmid[i * R + r]);
+    float r0 = (float)rgb0, r1 = (float)rgb1, r2 = (float)rgb2;
+    if (white_bkgd) {
+      const float bg = fsub(1.0f, accf);
+      r0 = fadd(r0, bg); r1 = fadd(r1, bg); r2 = fadd(r2, bg);
+    }
+    o.rgb[ro * 3 + 0] = r0;
+    o.rgb[ro * 3 + 1] = r1;
+    o.rgb[ro * 3 + 2] = r2;
+    o.depth[ro] = (float)depth;
+    o.acc[ro] = accf;
+    if (calc_normal && o.normals) {
+      o.normals[ro * 3 + 0] = (float)n0;
+      o.normals[ro * 3 + 1] = (float)n1;
+      o.normals[ro * 3 + 2] = (float)n2;
+    }
   }
-  float r0 = (float)rgb0, r1 = (float)rgb1, r2 = (float)rgb2;
-  if (white_bkgd) {
-    const float bg = fsub(1.0f, accf);
-    r0 = fadd(r0, bg); r1 = fadd(r1, bg); r2 = fadd(r2, bg);
-  }
-  o.rgb[ro * 3 + 0] = r0;
-  o.rgb[ro * 3 + 1] = r1;
-  o.rgb[ro * 3 + 2] = r2;
-  o.depth[ro] = (float)depth;
-  o.acc[ro] = accf;
-  if (calc_normal && o.normals) {
-    o.normals[ro * 3 + 0] = (float)n0;
-    o.normals[ro * 3 + 1] = (float)n1;
-    o.normals[ro * 3 + 2] = (float)n2;
-  }
+  __syncthreads();
   // detailed per-sample outputs, ray-major
-  for (int i = 0; i < S; ++i) {
+  for (int i = l; i < S; i += 64) {
     const int64_t q = i * R + r;
     if (o.sdf) o.sdf[ro * S + i] = c.sdf_f[q];
     if (o.nablas) {
@@ -298,11 +315,12 @@ __global__ __launch_bounds__(64) void neus_composite(NeusChunk c, NeusOut o, flo
       o.nablas[(ro * S + i) * 3 + 2] = c.nab_f[q * 3 + 2];
     }
     if (i < S - 1) {
+      if (o.weights) o.weights[ro * (S - 1) + i] = sal[i];
       if (o.d_final) o.d_final[ro * (S - 1) + i] = c.dmid[q];
       if (o.radiance) {
-        o.radiance[(ro * (S - 1) + i) * 3 + 0] = c.rad_m[q * 3 + 0];
-        o.radiance[(ro * (S - 1) + i) * 3 + 1] = c.rad_m[q * 3 + 1];
-        o.radiance[(ro * (S - 1) + i) * 3 + 2] = c.rad_m[q * 3 + 2];
+        o.radiance[(ro * (S - 1) + i) * 3 + 0] = srad[i * 3 + 0];
+        o.radiance[(ro * (S - 1) + i) * 3 + 1] = srad[i * 3 + 1];
+        o.radiance[(ro * (S - 1) + i) * 3 + 2] = srad[i * 3 + 2];
       }
     }
   }
