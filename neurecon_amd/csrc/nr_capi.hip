@@ -441,7 +441,7 @@ static int unisurf_chunk(const NrUnisurfArgs& a, const UniPlan& pl, int64_t ray0
   const size_t mlp_bytes = a.workspace_bytes - pl.o_mlp;
   const SdfLayout SL = sdf_layout(*a.sdf);
   const RadLayout RL = rad_layout(*a.rad);
-  const dim3 blk(256), grd((R + 255) / 256);
+  const dim3 blk(64), grd((R + 63) / 64);  // one wave per block: a 4096-ray chunk spreads over 64 CUs
   const int64_t P = (int64_t)c.P * R;
   int rc;
   {

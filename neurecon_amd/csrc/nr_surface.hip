@@ -278,7 +278,7 @@ int nr_root_find(const NrSdfDesc* d, const void* packed, const float* rays_o, co
     c.ro = F(pl.o_ro); c.rd = F(pl.o_rd); c.near = F(pl.o_near); c.far = F(pl.o_far);
     c.pts_m = F(pl.o_ptsm); c.sm = F(pl.o_sm); c.sec = F(pl.o_sec); c.pts_s = F(pl.o_ptss); c.ss = F(pl.o_ss);
     c.t_march = t_march;
-    const dim3 blk(256), grd((R + 255) / 256);
+    const dim3 blk(64), grd((R + 63) / 64);
     {
       ProfScope prof("root_prologue", (double)R, st);
       hipLaunchKernelGGL(rf_prologue, grd, blk, 0, st, c, rays_o + r0 * 3, rays_d + r0 * 3, near, far);
