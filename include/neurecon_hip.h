@@ -176,6 +176,14 @@ typedef struct {
   const float* t_nograd;  /* torch.linspace(0, 1, N_nograd_samples)  */
   void* workspace;
   size_t workspace_bytes;
+  /* perturb=True (training) uniforms, drawn by the caller exactly as the reference draws them
+   * (rend_util.py:271 in sample_pdf, neus.py:306-311 for NeRF++); NULL = deterministic:
+   * u_rand: official_solution [N_upsample_iters][n_rays][N_importance/N_upsample_iters],
+   *         direct_use / direct_more [n_rays][N_importance] (replace u_fine's linspace);
+   * t_out_rand: [n_rays][N_outside] stratification of the inverted-sphere depths. */
+  const float* u_rand;
+  const float* t_out_rand;
+  const float* s_dev; /* optional device scalar s (overrides `s`): no host round trip per call */
 } NrNeusArgs;
 
 size_t nr_neus_workspace_bytes(const NrNeusArgs* a);
@@ -286,17 +294,37 @@ typedef struct {
   float* weights_out;    /* [n_rays, P] visibility_weights */
   void* workspace;
   size_t workspace_bytes;
+  /* perturb=True (unisurf.py:158-165, :187-194): the caller's stratification uniforms (torch.rand
+   * in the reference's order), u_query [n_rays, N_query], u_free [n_rays, N_freespace]; t_query /
+   * t_free then hold the N+1 bin edges linspace(0, 1, N+1).  NULL = deterministic. */
+  const float* u_query;
+  const float* u_free;
+  /* Multi-GPU ray shard with normal_mode 1: the reference's F.normalize windows span
+   * the whole batch (unisurf.py:36, train_util.py:23-71), so every rank computes its partial sums of
+   * nabla^2 per window into window_ss ([B][nr_unisurf_window_count][3] fp64, zeroed by the caller),
+   * then the library calls window_reduce(window_user) exactly once per nr_unisurf_render call (an
+   * all-reduce over the ranks, enqueued on `stream`) and normalises with the totals.  rays are this
+   * rank's [B, n_rays / B] slice starting at row-relative ray shard_ray0 of rows of shard_row_rays
+   * rays; the shard must be <= 65536 rays.  shard_row_rays = 0: not sharded. */
+  int64_t shard_ray0;
+  int64_t shard_row_rays;
+  double* window_ss;
+  int (*window_reduce)(void* user);
+  void* window_user;
 } NrUnisurfArgs;
 
 size_t nr_unisurf_workspace_bytes(const NrUnisurfArgs* a);
 int nr_unisurf_render(const NrUnisurfArgs* a, void* stream);
+/* F.normalize windows per batch row of the whole batch (normal_mode 1), for sizing window_ss */
+int64_t nr_unisurf_window_count(const NrUnisurfArgs* a);
 
 /* ------------------------------------------------------------------------------------------
- * Inverse-CDF sampling (rend_util.sample_pdf, det=True or caller-provided u):
- * bins [R, L], weights [R, L-1], u [N] (shared) -> samples [R, N].
+ * Inverse-CDF sampling (rend_util.sample_pdf, utils/rend_util.py:255-292): bins [R, L],
+ * weights [R, L-1] -> samples [R, N].  det=True: u [N] shared and ascending (u_stride = 0);
+ * det=False: the caller's uniforms u[r * u_stride + k] (any order), e.g. torch.rand([R, N]).
  * ------------------------------------------------------------------------------------------ */
-int nr_sample_pdf(const float* bins, const float* weights, int64_t R, int L, const float* u, int N, float* out,
-                  void* stream);
+int nr_sample_pdf(const float* bins, const float* weights, int64_t R, int L, const float* u, int64_t u_stride, int N,
+                  float* out, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Pixel -> ray (rend_util.get_rays, pose-matrix form): c2w [B,4,4], K [B,4,4] (row-major),

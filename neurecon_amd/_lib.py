@@ -54,6 +54,7 @@ class NrNeusArgs(ctypes.Structure):
         ('sigma_out', _c_p), ('radiance_bg_out', _c_p),
         ('upsample_algo', _c_i), ('fixed_s', _c_f), ('N_nograd_samples', _c_i), ('t_nograd', _c_p),
         ('workspace', _c_p), ('workspace_bytes', _c_sz),
+        ('u_rand', _c_p), ('t_out_rand', _c_p), ('s_dev', _c_p),
     ]
 
 
@@ -92,7 +93,13 @@ class NrUnisurfArgs(ctypes.Structure):
         ('surface_points', _c_p), ('mask_surface', _c_p), ('depth_surface', _c_p),
         ('radiance_out', _c_p), ('sdf_out', _c_p), ('nablas_out', _c_p), ('alpha_out', _c_p), ('weights_out', _c_p),
         ('workspace', _c_p), ('workspace_bytes', _c_sz),
+        ('u_query', _c_p), ('u_free', _c_p),
+        ('shard_ray0', _c_i64), ('shard_row_rays', _c_i64), ('window_ss', _c_p), ('window_reduce', _c_p),
+        ('window_user', _c_p),
     ]
+
+
+WINDOW_REDUCE = ctypes.CFUNCTYPE(_c_i, _c_p)
 
 
 class NrKernelStat(ctypes.Structure):
@@ -120,7 +127,8 @@ _SIGS = {
     'nr_volsdf_render': (_c_i, [ctypes.POINTER(NrVolsdfArgs), _c_p]),
     'nr_unisurf_workspace_bytes': (_c_sz, [ctypes.POINTER(NrUnisurfArgs)]),
     'nr_unisurf_render': (_c_i, [ctypes.POINTER(NrUnisurfArgs), _c_p]),
-    'nr_sample_pdf': (_c_i, [_c_p, _c_p, _c_i64, _c_i, _c_p, _c_i, _c_p, _c_p]),
+    'nr_unisurf_window_count': (_c_i64, [ctypes.POINTER(NrUnisurfArgs)]),
+    'nr_sample_pdf': (_c_i, [_c_p, _c_p, _c_i64, _c_i, _c_p, _c_i64, _c_i, _c_p, _c_p]),
     'nr_get_rays': (_c_i, [_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p]),
     'nr_sphere_trace_workspace_bytes': (_c_sz, [_c_i64]),
     'nr_sphere_trace': (_c_i, [ctypes.POINTER(NrSdfDesc), _c_p, _c_p, _c_p, _c_i64, ctypes.c_float, ctypes.c_float,
@@ -188,6 +196,21 @@ def profile_read():
     n = ctypes.c_int(0)
     check(lib().nr_profile_read(buf, 64, ctypes.byref(n)))
     return {buf[i].name.decode(): (buf[i].launches, buf[i].ms, buf[i].units) for i in range(n.value)}
+
+
+_WS = {}
+
+
+def workspace(device, nbytes):
+    """Scratch for one library call, reused across calls on the device (grow-only): calls are
+    ordered on the caller's stream, so one buffer per device serves them all."""
+    key = str(device)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        _WS.pop(key, None)
+        buf = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
 
 
 def require_gpu(t, what='input'):

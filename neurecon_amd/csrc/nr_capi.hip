@@ -204,8 +204,10 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   }
   if (direct) {
     ProfScope prof("neus_upsample", (double)R, st);
-    hipLaunchKernelGGL(neus_direct_upsample, grd, blk, 0, st, c, (int)(a.upsample_algo == NR_UPSAMPLE_DIRECT_MORE),
-                       a.u_fine);
+    // perturb: this chunk's rows of the caller's [n_rays][N_importance] uniforms
+    const float* u = a.u_rand ? a.u_rand + ray0 * a.N_importance : a.u_fine;
+    hipLaunchKernelGGL(neus_direct_upsample, grd, blk, 0, st, c, (int)(a.upsample_algo == NR_UPSAMPLE_DIRECT_MORE), u,
+                       (int64_t)(a.u_rand ? a.N_importance : 0));
   }
   NR_HIP_CHECK(hipGetLastError());
   // sorted sample lists ping-pong between two buffers; each merge writes the other one
@@ -230,8 +232,10 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
     if (it > 0 && (rc = merge(a.N_samples + (it - 1) * n_up))) return rc;
     {
       ProfScope prof("neus_upsample", (double)R, st);
-      hipLaunchKernelGGL(neus_upsample, dim3((unsigned)R), dim3(64), (4 * c.S + 1) * sizeof(float), st, c, it,
-                         a.u_fine);
+      // perturb: round it's [n_rays][n_up] block of the caller's uniforms
+      const float* u = a.u_rand ? a.u_rand + ((int64_t)it * a.n_rays + ray0) * n_up : a.u_fine;
+      hipLaunchKernelGGL(neus_upsample, dim3((unsigned)R), dim3(64), (4 * c.S + 1) * sizeof(float), st, c, it, u,
+                         (int64_t)(a.u_rand ? n_up : 0));
     }
     NR_HIP_CHECK(hipGetLastError());
     float* nslot = fused ? c.nraw + (size_t)(a.N_samples + it * n_up) * R * 3 : nullptr;
@@ -259,16 +263,17 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   NeusOut o{ray0, a.rgb, a.depth, a.acc, a.normals, a.d_final, a.sdf_out, a.nablas_out,
             a.radiance_out, a.alpha_out, a.cdf_out, a.weights_out, a.sigma_out, a.radiance_bg_out};
   if (a.N_outside > 0) {  // NeRF++ background on [mid-points ; inverted-sphere samples]
-    hipLaunchKernelGGL(neus_outside_points, grd, blk, 0, st, c);
+    hipLaunchKernelGGL(neus_outside_points, grd, blk, 0, st, c,
+                       a.t_out_rand ? a.t_out_rand + ray0 * a.N_outside : (const float*)nullptr);
     NR_HIP_CHECK(hipGetLastError());
     const int64_t Po = (int64_t)(c.S - 1 + a.N_outside) * R;
     if ((rc = launch_nerf(nerf_layout(*a.nerf), a.nerf_packed, c.x4, c.rd, 1, R, Po, c.sig_o, c.rad_o, st)))
       return rc;
     ProfScope prof("neus_composite", (double)R, st);
-    hipLaunchKernelGGL(neus_composite_outside, grd, blk, 0, st, c, o, a.s, a.calc_normal, a.white_bkgd);
+    hipLaunchKernelGGL(neus_composite_outside, grd, blk, 0, st, c, o, a.s_dev, a.s, a.calc_normal, a.white_bkgd);
   } else {
     ProfScope prof("neus_composite", (double)R, st);
-    hipLaunchKernelGGL(neus_composite, dim3((unsigned)R), dim3(64), 8 * c.S * sizeof(float), st, c, o, a.s,
+    hipLaunchKernelGGL(neus_composite, dim3((unsigned)R), dim3(64), 8 * c.S * sizeof(float), st, c, o, a.s_dev, a.s,
                        a.calc_normal, a.white_bkgd);
   }
   NR_HIP_CHECK(hipGetLastError());
@@ -392,10 +397,13 @@ static int check_volsdf(const NrVolsdfArgs* a) {
   int rc = check_sdf_desc(a->sdf);
   if (rc) return rc;
   if ((rc = check_rad_desc(a->rad))) return rc;
-  NR_REQUIRE(a->rays_o && a->rays_d && a->sdf_packed && a->rad_packed && a->t_coarse && a->t_init && a->u_up &&
-                 a->u_fine && a->rgb && a->depth && a->acc,
-             NR_ERR_ARG, "nr_volsdf_render: null argument");
-  NR_REQUIRE(!a->calc_normal || a->normals, NR_ERR_ARG, "nr_volsdf_render: calc_normal needs normals output");
+  // an empty shard (multi-GPU ray sharding) may pass null ray / output pointers
+  NR_REQUIRE(a->n_rays <= 0 || (a->rays_o && a->rays_d && a->rgb && a->depth && a->acc), NR_ERR_ARG,
+             "nr_volsdf_render: null ray or output pointer");
+  NR_REQUIRE(a->sdf_packed && a->rad_packed && a->t_coarse && a->t_init && a->u_up && a->u_fine, NR_ERR_ARG,
+             "nr_volsdf_render: null argument");
+  NR_REQUIRE(a->n_rays <= 0 || !a->calc_normal || a->normals, NR_ERR_ARG,
+             "nr_volsdf_render: calc_normal needs normals output");
   NR_REQUIRE(a->N_samples >= 1 && a->N_importance >= 1 && a->max_upsample_steps >= 0 && a->max_bisection_steps >= 0,
              NR_ERR_ARG, "nr_volsdf_render: bad sample counts");
   NR_REQUIRE(4 * a->N_samples <= 1024 && a->N_importance <= 1024, NR_ERR_UNSUPPORTED,
@@ -416,7 +424,10 @@ static int check_volsdf(const NrVolsdfArgs* a) {
 // point) -> secant] x N_secant_steps -> samples -> SDF+nablas+feature -> F.normalize -> radiance
 // -> composite.
 // ---------------------------------------------------------------------------------------------
-static int unisurf_chunk(const NrUnisurfArgs& a, const UniPlan& pl, int64_t ray0, int R, hipStream_t st) {
+// rays [ray0, ray0 + R) of the call = `R / nloc` batch rows of nloc rays, starting at row-relative
+// ray row_ray0 (internal chunks: one row; a multi-GPU shard: all of its rows in one chunk)
+static int unisurf_chunk(const NrUnisurfArgs& a, const UniPlan& pl, int64_t ray0, int R, int64_t row_ray0, int nloc,
+                         hipStream_t st) {
   char* ws = (char*)a.workspace;
   auto F = [&](size_t o) { return (float*)(ws + o); };
   UniChunk c{};
@@ -436,7 +447,17 @@ static int unisurf_chunk(const NrUnisurfArgs& a, const UniPlan& pl, int64_t ray0
   c.d_all = F(pl.o_dall); c.pts_f = F(pl.o_ptsf); c.sdf_f = F(pl.o_sdff); c.nab_f = F(pl.o_nabf);
   c.feat_f = F(pl.o_featf); c.nrm_f = F(pl.o_nrmf); c.rad_f = F(pl.o_radf); c.wss = (double*)(ws + pl.o_wss);
   c.netchunk = a.netchunk;
+  const bool sharded = a.normal_mode == 1 && a.shard_row_rays > 0;
+  if (a.normal_mode == 1) {
+    unisurf_windows(a, c.rc_rays, c.nw_full, c.nw_row);
+    c.row_rays = sharded ? a.shard_row_rays : (a.rays_per_batch > 0 ? a.rays_per_batch : a.n_rays);
+    c.row_ray0 = row_ray0;
+    c.nloc = nloc;
+    if (sharded) c.wss = a.window_ss;  // the caller's [B][nw_row][3], all-reduced by window_reduce
+  }
   c.t_march = a.t_march; c.t_query = a.t_query; c.t_free = a.t_free;
+  c.u_q = a.u_query ? a.u_query + ray0 * a.N_query : nullptr;
+  c.u_f = a.u_free ? a.u_free + ray0 * a.N_freespace : nullptr;
   void* mlp_ws = ws + pl.o_mlp;
   const size_t mlp_bytes = a.workspace_bytes - pl.o_mlp;
   const SdfLayout SL = sdf_layout(*a.sdf);
@@ -468,9 +489,12 @@ static int unisurf_chunk(const NrUnisurfArgs& a, const UniPlan& pl, int64_t ray0
                        st)))
     return rc;
   if (a.normal_mode == 1) {
-    const int64_t nw = (P + a.netchunk - 1) / a.netchunk;
-    hipLaunchKernelGGL(uni_window_ss, dim3((unsigned)nw), dim3(256), 0, st, c);
+    hipLaunchKernelGGL(uni_window_ss, dim3((unsigned)c.nw_row, (unsigned)(R / nloc)), dim3(256), 0, st, c);
     NR_HIP_CHECK(hipGetLastError());
+    if (sharded) {  // every rank's partial sums -> the sums of the whole batch (collective, stream-ordered)
+      const int rr = a.window_reduce(a.window_user);
+      NR_REQUIRE(rr == 0, NR_ERR_ARG, "nr_unisurf_render: window_reduce callback failed");
+    }
   }
   hipLaunchKernelGGL(uni_normalize, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, c, a.normal_mode);
   NR_HIP_CHECK(hipGetLastError());
@@ -490,19 +514,29 @@ static int check_unisurf(const NrUnisurfArgs* a) {
   int rc = check_sdf_desc(a->sdf);
   if (rc) return rc;
   if ((rc = check_rad_desc(a->rad))) return rc;
-  NR_REQUIRE(a->rays_o && a->rays_d && a->sdf_packed && a->rad_packed && a->t_march && a->t_query && a->t_free &&
-                 a->rgb && a->depth && a->acc,
-             NR_ERR_ARG, "nr_unisurf_render: null argument");
-  NR_REQUIRE(!a->calc_normal || a->normals, NR_ERR_ARG, "nr_unisurf_render: calc_normal needs normals output");
+  NR_REQUIRE(a->n_rays <= 0 || (a->rays_o && a->rays_d && a->rgb && a->depth && a->acc), NR_ERR_ARG,
+             "nr_unisurf_render: null ray or output pointer");
+  NR_REQUIRE(a->sdf_packed && a->rad_packed && a->t_march && a->t_query && a->t_free, NR_ERR_ARG,
+             "nr_unisurf_render: null argument");
+  NR_REQUIRE(a->n_rays <= 0 || !a->calc_normal || a->normals, NR_ERR_ARG,
+             "nr_unisurf_render: calc_normal needs normals output");
   NR_REQUIRE(a->N_steps >= 2 && a->N_secant_steps >= 0 && a->N_query >= 1 && a->N_freespace >= 1, NR_ERR_ARG,
              "nr_unisurf_render: bad sample counts");
   NR_REQUIRE(a->normal_mode == 0 || a->normal_mode == 1, NR_ERR_ARG, "nr_unisurf_render: normal_mode must be 0|1");
+  NR_REQUIRE(!a->u_query == !a->u_free, NR_ERR_ARG, "nr_unisurf_render: u_query and u_free go together");
   NR_REQUIRE(a->normal_mode == 0 || (a->rayschunk > 0 && a->netchunk > 0), NR_ERR_ARG,
              "nr_unisurf_render: rayschunk/netchunk must be positive");
   if (a->rays_per_batch > 0)
     NR_REQUIRE(a->n_rays % a->rays_per_batch == 0, NR_ERR_ARG, "nr_unisurf_render: n_rays % rays_per_batch != 0");
   NR_REQUIRE(unisurf_chunk_rays(*a) > 0, NR_ERR_UNSUPPORTED,
              "nr_unisurf_render: rayschunk too large for windowed normalisation unless netchunk % P == 0");
+  if (a->shard_row_rays > 0) {
+    NR_REQUIRE(a->normal_mode == 1 && a->window_ss && a->window_reduce, NR_ERR_ARG,
+               "nr_unisurf_render: a sharded render needs normal_mode 1, window_ss and window_reduce");
+    const int64_t nloc = a->rays_per_batch > 0 ? a->rays_per_batch : a->n_rays;
+    NR_REQUIRE(a->shard_ray0 >= 0 && a->shard_ray0 + nloc <= a->shard_row_rays, NR_ERR_ARG,
+               "nr_unisurf_render: shard outside its batch row");
+  }
   return NR_OK;
 }
 
@@ -668,10 +702,13 @@ int nr_neus_render(const NrNeusArgs* a, void* stream) {
   int rc = check_sdf_desc(a->sdf);
   if (rc) return rc;
   if ((rc = check_rad_desc(a->rad))) return rc;
-  NR_REQUIRE(a->rays_o && a->rays_d && a->sdf_packed && a->rad_packed && a->t_coarse && a->rgb && a->depth && a->acc,
-             NR_ERR_ARG, "nr_neus_render: null argument");
+  // an empty shard (multi-GPU ray sharding) may pass null ray / output pointers
+  NR_REQUIRE(a->n_rays <= 0 || (a->rays_o && a->rays_d && a->rgb && a->depth && a->acc), NR_ERR_ARG,
+             "nr_neus_render: null ray or output pointer");
+  NR_REQUIRE(a->sdf_packed && a->rad_packed && a->t_coarse, NR_ERR_ARG, "nr_neus_render: null argument");
   NR_REQUIRE(a->N_samples >= 2, NR_ERR_ARG, "nr_neus_render: N_samples must be >= 2");
-  NR_REQUIRE(!a->calc_normal || a->normals, NR_ERR_ARG, "nr_neus_render: calc_normal needs normals output");
+  NR_REQUIRE(a->n_rays <= 0 || !a->calc_normal || a->normals, NR_ERR_ARG,
+             "nr_neus_render: calc_normal needs normals output");
   NR_REQUIRE(a->N_outside >= 0, NR_ERR_ARG, "nr_neus_render: N_outside must be >= 0");
   if (a->N_outside > 0) {
     if ((rc = check_nerf_desc(a->nerf))) return rc;
@@ -693,6 +730,16 @@ int nr_neus_render(const NrNeusArgs* a, void* stream) {
   const int64_t Rc = neus_chunk_rays(a);
   const NeusPlan pl = neus_plan(*a, Rc);
   NR_REQUIRE(a->workspace && a->workspace_bytes >= pl.total, NR_ERR_WORKSPACE, "nr_neus_render: workspace too small");
+  {  // the wave-per-ray upsampling / compositing kernels stage S samples per ray in LDS
+    const bool direct = a->upsample_algo != NR_UPSAMPLE_OFFICIAL;
+    const int S = direct ? a->N_samples + a->N_importance
+                         : a->N_samples + a->N_upsample_iters * (a->N_upsample_iters > 0 ? a->N_importance / a->N_upsample_iters : 0);
+    int dev = 0, lds_max = 65536;
+    NR_HIP_CHECK(hipGetDevice(&dev));
+    NR_HIP_CHECK(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
+    NR_REQUIRE((size_t)8 * S * sizeof(float) <= (size_t)lds_max, NR_ERR_UNSUPPORTED,
+               "nr_neus_render: N_samples + N_importance too large for the per-ray LDS staging of the compositing");
+  }
   for (int64_t r0 = 0; r0 < a->n_rays; r0 += Rc) {
     const int R = (int)((a->n_rays - r0) < Rc ? (a->n_rays - r0) : Rc);
     if ((rc = neus_chunk(*a, pl, r0, R, (hipStream_t)stream))) return rc;
@@ -730,14 +777,28 @@ size_t nr_unisurf_workspace_bytes(const NrUnisurfArgs* a) {
   return unisurf_plan(*a, unisurf_chunk_rays(*a)).total;
 }
 
+int64_t nr_unisurf_window_count(const NrUnisurfArgs* a) {
+  if (!a || a->normal_mode != 1) return 0;
+  int64_t rc_rays, nw_full, nw_row;
+  unisurf_windows(*a, rc_rays, nw_full, nw_row);
+  return nw_row;
+}
+
 int nr_unisurf_render(const NrUnisurfArgs* a, void* stream) {
   int rc = check_unisurf(a);
   if (rc) return rc;
-  if (a->n_rays <= 0) return NR_OK;
+  const bool sharded = a->shard_row_rays > 0;
+  if (a->n_rays <= 0) {  // an empty shard still joins the collective
+    if (sharded) NR_REQUIRE(a->window_reduce(a->window_user) == 0, NR_ERR_ARG, "nr_unisurf_render: window_reduce failed");
+    return NR_OK;
+  }
   const int64_t Rc = unisurf_chunk_rays(*a);
   const UniPlan pl = unisurf_plan(*a, Rc);
   NR_REQUIRE(a->workspace && a->workspace_bytes >= pl.total, NR_ERR_WORKSPACE,
              "nr_unisurf_render: workspace too small");
+  if (sharded)  // the whole shard (every batch row) is one chunk: one window reduction per call
+    return unisurf_chunk(*a, pl, 0, (int)a->n_rays, a->shard_ray0,
+                         (int)(a->rays_per_batch > 0 ? a->rays_per_batch : a->n_rays), (hipStream_t)stream);
   const int64_t per_b = (a->normal_mode == 1 && a->rays_per_batch > 0) ? a->rays_per_batch : a->n_rays;
   // window mode: chunks restart at every batch row and at every reference ray chunk
   const int64_t span = a->normal_mode == 1 ? (a->rayschunk < per_b ? a->rayschunk : per_b) : per_b;
@@ -747,19 +808,20 @@ int nr_unisurf_render(const NrUnisurfArgs* a, void* stream) {
       const int64_t c1 = c0 + span < b1 ? c0 + span : b1;
       for (int64_t r0 = c0; r0 < c1; r0 += Rc) {
         const int R = (int)((c1 - r0) < Rc ? (c1 - r0) : Rc);
-        if ((rc = unisurf_chunk(*a, pl, r0, R, (hipStream_t)stream))) return rc;
+        if ((rc = unisurf_chunk(*a, pl, r0, R, r0 - b0, R, (hipStream_t)stream))) return rc;
       }
     }
   }
   return NR_OK;
 }
 
-int nr_sample_pdf(const float* bins, const float* weights, int64_t R, int L, const float* u, int N, float* out,
-                  void* stream) {
-  NR_REQUIRE(bins && weights && u && out && L >= 2 && N >= 1, NR_ERR_ARG, "nr_sample_pdf: bad argument");
+int nr_sample_pdf(const float* bins, const float* weights, int64_t R, int L, const float* u, int64_t u_stride, int N,
+                  float* out, void* stream) {
+  NR_REQUIRE(bins && weights && u && out && L >= 2 && N >= 1 && u_stride >= 0, NR_ERR_ARG,
+             "nr_sample_pdf: bad argument");
   if (R <= 0) return NR_OK;
   hipLaunchKernelGGL(sample_pdf_kernel, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, (hipStream_t)stream, bins,
-                     weights, R, L, u, N, out);
+                     weights, R, L, u, u_stride, N, out);
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;
 }

@@ -6,6 +6,16 @@
 
 #include "../../include/neurecon_hip.h"
 
+// NR_EXP_* switches skip work inside the kernels (timing experiments, results are garbage): only
+// tools/build_variants.py may set them, and it also defines NR_VARIANT_BUILD
+#if !defined(NR_VARIANT_BUILD) &&                                                                  \
+    (defined(NR_EXP_NO_DMA) || defined(NR_EXP_NO_ESTORE) || defined(NR_EXP_NO_ELOAD) ||             \
+     defined(NR_EXP_NO_SOFTPLUS) || defined(NR_EXP_NO_SPLIT) || defined(NR_EXP_NO_BARRIER) ||       \
+     defined(NR_EXP_UNROLL) || defined(NR_EXP_NO_PINGPONG) || defined(NR_EXP_NO_EPI) ||             \
+     defined(NR_EXP_NO_MFMA))
+#error "NR_EXP_* experiment switches are for tools/build_variants.py builds only"
+#endif
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 

@@ -56,15 +56,16 @@ NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc);
 
 __global__ void neus_prologue(NeusChunk c, const float* rays_o, const float* rays_d, const float* t_coarse,
                               float r_obj, float near_bypass, float far_bypass);
-__global__ void neus_upsample(NeusChunk c, int it, const float* u);
+__global__ void neus_upsample(NeusChunk c, int it, const float* u, int64_t u_stride);
 __global__ void neus_merge(NeusChunk c, int L, float* dv2, float* sv2, int* idv2);
 __global__ void neus_expand(NeusChunk c);
-__global__ void neus_composite(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd);
-__global__ void neus_outside_points(NeusChunk c);
+__global__ void neus_composite(NeusChunk c, NeusOut o, const float* s_dev, float s_val, int calc_normal, int white_bkgd);
+__global__ void neus_outside_points(NeusChunk c, const float* t_rand);
 __global__ void neus_nograd_points(NeusChunk c);
-__global__ void neus_direct_upsample(NeusChunk c, int more, const float* u);
-__global__ void neus_composite_outside(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd);
-__global__ void sample_pdf_kernel(const float* bins, const float* weights, int64_t R, int L, const float* u, int N,
-                                  float* out);
+__global__ void neus_direct_upsample(NeusChunk c, int more, const float* u, int64_t u_stride);
+__global__ void neus_composite_outside(NeusChunk c, NeusOut o, const float* s_dev, float s_val, int calc_normal,
+                                       int white_bkgd);
+__global__ void sample_pdf_kernel(const float* bins, const float* weights, int64_t R, int L, const float* u,
+                                  int64_t u_stride, int N, float* out);
 
 }  // namespace nr

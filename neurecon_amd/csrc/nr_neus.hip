@@ -83,11 +83,36 @@ __device__ void sample_pdf_ray(const float* __restrict__ bins, const float* __re
   for (; k < n; ++k) out[k * out_stride] = invert_one(u[k], c_prev, c_prev, b_prev, b_prev);
 }
 
+// sample_pdf with det=False (rend_util.py:268-290): the caller's uniforms u[0..n) are in any order,
+// so each draw does its own searchsorted(cdf, u, right=False).  The cdf overwrites the weights in
+// place (w[i] <- cdf[i+1], same fp64 running sum as above) and is binary-searched per draw.
+__device__ void sample_pdf_ray_rand(const float* __restrict__ bins, float* __restrict__ w, int64_t stride, int L,
+                                    float total, const float* __restrict__ u, int n, float* __restrict__ out,
+                                    int64_t out_stride) {
+  double acc = 0.0;
+  for (int i = 0; i < L - 1; ++i) {
+    acc += (double)fdiv(fadd(w[i * stride], 1e-5f), total);
+    w[i * stride] = (float)acc;
+  }
+  auto cdf = [&](int j) { return j == 0 ? 0.0f : w[(int64_t)(j - 1) * stride]; };
+  for (int k = 0; k < n; ++k) {
+    const float uk = u[k];
+    int lo = 0, hi = L;  // first j in [0, L) with cdf[j] >= uk, L if none
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if (cdf(m) >= uk) hi = m; else lo = m + 1;
+    }
+    const int below = lo > 0 ? lo - 1 : 0, above = lo < L - 1 ? lo : L - 1;
+    out[k * out_stride] = invert_one(uk, cdf(below), cdf(above), bins[below * stride], bins[above * stride]);
+  }
+}
+
 // one "official_solution" upsampling round (neus.py:252-276): one wave per ray.  The per-interval
 // work (slopes, logistic CDFs, alpha) runs across the lanes; the three order-sensitive scans
 // (transmittance cumprod, the ATen-order weight sum, the CDF cumsum) run on lane 0 over LDS with
 // exactly the arithmetic of the per-ray version; the n_up inverse-CDF draws run across lanes.
-__global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const float* __restrict__ u) {
+// u: the round's uniforms, u[r * u_stride + k] (u_stride 0: the shared deterministic linspace)
+__global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const float* __restrict__ u, int64_t u_stride) {
   extern __shared__ float lds[];
   const int r = blockIdx.x, l = threadIdx.x;
   const int L = c.N_samples + it * c.n_up;  // last round's samples were merged by neus_merge
@@ -138,7 +163,7 @@ __global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const f
   const float ox = c.ro[r * 3], oy = c.ro[r * 3 + 1], oz = c.ro[r * 3 + 2];
   const float dx = c.rd[r * 3], dy = c.rd[r * 3 + 1], dz = c.rd[r * 3 + 2];
   for (int k = l; k < c.n_up; k += 64) {
-    const float uk = u[k];
+    const float uk = u[r * u_stride + k];
     float d;
     if (uk <= 0.0f) {  // searchsorted -> 0: below = above = 0
       d = invert_one(uk, 0.0f, 0.0f, sz[0], sz[0]);
@@ -234,8 +259,11 @@ __global__ void neus_expand(NeusChunk c) {
 // compositing (neus.py:296, :346-380), one wave per ray: logistic CDFs, alpha, radiance and unit
 // normals per sample across the lanes (LDS); the transmittance product and the fp64 rgb / acc /
 // normal / depth accumulations on lane 0 in sample order, exactly as the per-ray version did.
-__global__ __launch_bounds__(64) void neus_composite(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd) {
+// s = exp(ln_s * speed_factor) (neus.py:108-109): *s_dev when given (device scalar, no host sync), else s_val
+__global__ __launch_bounds__(64) void neus_composite(NeusChunk c, NeusOut o, const float* __restrict__ s_dev,
+                                                     float s_val, int calc_normal, int white_bkgd) {
   extern __shared__ float lds[];
+  const float s_inv = s_dev ? *s_dev : s_val;
   const int r = blockIdx.x, l = threadIdx.x;
   const int S = c.S;
   const int64_t R = c.R;
@@ -347,7 +375,8 @@ __global__ __launch_bounds__(64) void neus_nograd_points(NeusChunk c) {
   }
 }
 
-__global__ __launch_bounds__(64) void neus_direct_upsample(NeusChunk c, int more, const float* __restrict__ u) {
+__global__ __launch_bounds__(64) void neus_direct_upsample(NeusChunk c, int more, const float* __restrict__ u,
+                                                         int64_t u_stride) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= c.R) return;
   const int64_t R = c.R;
@@ -373,10 +402,11 @@ __global__ __launch_bounds__(64) void neus_direct_upsample(NeusChunk c, int more
     T *= (double)fadd(fsub(1.0f, alpha), 1e-10f);
     cprev = cn;
   }
-  const float* wr = c.wtmp + r;
+  float* wr = c.wtmp + r;
   const float total = aten_row_sum(L - 1, [&](int i) { return fadd(wr[(int64_t)i * R], 1e-5f); });
   float* dn = c.dnew + r;
-  sample_pdf_ray(bins, wr, R, L, total, u, c.n_imp, dn, R);
+  if (u_stride) sample_pdf_ray_rand(bins, wr, R, L, total, u + r * u_stride, c.n_imp, dn, R);
+  else sample_pdf_ray(bins, wr, R, L, total, u, c.n_imp, dn, R);
   // sort(cat([d_coarse, d_fine])) (neus.py:227-228): insertion-sort the new column, merge in place
   const int n = c.n_imp;
   for (int k = 1; k < n; ++k) {
@@ -406,7 +436,9 @@ __global__ __launch_bounds__(64) void neus_direct_upsample(NeusChunk c, int more
 // NeRF++ background (neus.py:303-343)
 // ---------------------------------------------------------------------------------------------
 // d_vals_out = cat([d_mid, far / flip(linspace(0,1,N_out+2)[1:-1])]); x_out = [p / |p|, 1 / |p|]
-__global__ __launch_bounds__(64) void neus_outside_points(NeusChunk c) {
+// perturb (neus.py:306-311): d_k = lower_k + (upper_k - lower_k) * t_rand[r][k] with the mid-point
+// brackets of the deterministic inverted-sphere depths (t_rand: the caller's uniforms, or null)
+__global__ __launch_bounds__(64) void neus_outside_points(NeusChunk c, const float* __restrict__ t_rand) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= c.R) return;
   const int64_t R = c.R;
@@ -414,8 +446,21 @@ __global__ __launch_bounds__(64) void neus_outside_points(NeusChunk c) {
   const float ox = c.ro[r * 3], oy = c.ro[r * 3 + 1], oz = c.ro[r * 3 + 2];
   const float dx = c.rd[r * 3], dy = c.rd[r * 3 + 1], dz = c.rd[r * 3 + 2];
   const float fr = c.far[r];
+  const int No = c.N_out;
+  auto dvo = [&](int j) { return fdiv(fr, c.t_out[No - j]); };  // far / flip(linspace(0,1,No+2)[1:-1])[j]
   for (int k = 0; k < M; ++k) {
-    const float d = k < S1 ? c.dmid[(int64_t)k * R + r] : fdiv(fr, c.t_out[c.N_out - (k - S1)]);
+    float d;
+    if (k < S1) {
+      d = c.dmid[(int64_t)k * R + r];
+    } else {
+      const int j = k - S1;
+      d = dvo(j);
+      if (t_rand) {
+        const float lower = j > 0 ? fmul(0.5f, fadd(dvo(j), dvo(j - 1))) : dvo(0);
+        const float upper = j + 1 < No ? fmul(0.5f, fadd(dvo(j + 1), dvo(j))) : dvo(No - 1);
+        d = fadd(lower, fmul(fsub(upper, lower), t_rand[(int64_t)r * No + j]));
+      }
+    }
     const int64_t q = (int64_t)k * R + r;
     c.d_out[q] = d;
     const float px = fadd(ox, fmul(dx, d)), py = fadd(oy, fmul(dy, d)), pz = fadd(oz, fmul(dz, d));
@@ -428,7 +473,9 @@ __global__ __launch_bounds__(64) void neus_outside_points(NeusChunk c) {
 __device__ __forceinline__ float softplus1(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
 
 // compositing with the background merged in (neus.py:325-343, :346-380)
-__global__ __launch_bounds__(64) void neus_composite_outside(NeusChunk c, NeusOut o, float s_inv, int calc_normal, int white_bkgd) {
+__global__ __launch_bounds__(64) void neus_composite_outside(NeusChunk c, NeusOut o, const float* __restrict__ s_dev,
+                                                             float s_val, int calc_normal, int white_bkgd) {
+  const float s_inv = s_dev ? *s_dev : s_val;
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= c.R) return;
   const int S = c.S, S1 = S - 1, M = S1 + c.N_out;
@@ -530,13 +577,23 @@ __global__ __launch_bounds__(64) void neus_composite_outside(NeusChunk c, NeusOu
 // ---------------------------------------------------------------------------------------------
 // generic sample_pdf entry (rend_util.py:255-292), bins/weights ray-major [R][L], u [N]
 // ---------------------------------------------------------------------------------------------
+// u: shared sorted uniforms (u_stride 0, det=True) or per-row uniforms u[r * u_stride + k] in any
+// order (det=False): each of those is inverted by its own cumsum walk (weights stay read-only)
 __global__ void sample_pdf_kernel(const float* __restrict__ bins, const float* __restrict__ weights, int64_t R, int L,
-                                  const float* __restrict__ u, int N, float* __restrict__ out) {
+                                  const float* __restrict__ u, int64_t u_stride, int N, float* __restrict__ out) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
   const float* wr = weights + r * (L - 1);
   const float total = aten_row_sum(L - 1, [&](int i) { return fadd(wr[i], 1e-5f); });
-  sample_pdf_ray(bins + r * L, wr, 1, L, total, u, N, out + r * N, 1);
+  if (!u_stride) {
+    sample_pdf_ray(bins + r * L, wr, 1, L, total, u, N, out + r * N, 1);
+    return;
+  }
+  const float* br = bins + r * L;
+  for (int k = 0; k < N; ++k) {
+    const float uk = u[r * u_stride + k];
+    sample_pdf_ray(br, wr, 1, L, total, &uk, 1, out + r * N + k, 1);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -573,7 +630,8 @@ NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc) {
   p.o_feat_m = take((size_t)(S - 1) * Rc * 256);
   p.o_rad_m = take((size_t)(S - 1) * Rc * 3);
   const int M = S - 1 + a.N_outside;
-  p.o_wtmp = a.N_outside > 0 ? take((size_t)M * Rc) : p.o_wtmp;  // weights of all M samples
+  // weights of all M samples; direct_more also writes its n_nog-1 no-grad weights here first
+  p.o_wtmp = a.N_outside > 0 ? take((size_t)(M > n_nog ? M : n_nog) * Rc) : p.o_wtmp;
   p.o_dout = take((size_t)(a.N_outside > 0 ? (M > n_nog ? M : n_nog) : (n_nog > 0 ? n_nog : 1)) * Rc);
   p.o_x4 = take((size_t)(a.N_outside > 0 ? M : 1) * Rc * 4);
   p.o_sigo = take((size_t)(a.N_outside > 0 ? M : 1) * Rc);

@@ -22,9 +22,22 @@ struct UniChunk {
   float* d_all;      // [P][R]
   float* pts_f;      // [P][R][3]
   float* sdf_f; float* nab_f; float* feat_f; float* nrm_f; float* rad_f;
-  double* wss;       // [windows][3] sum of squares of the nablas per normalisation window
-  int64_t netchunk;  // points per F.normalize window (normal_mode 1)
+  // F.normalize windows (normal_mode 1): window w of a batch row covers points q in
+  // [j*netchunk, (j+1)*netchunk) of reference ray chunk k = w / nw_full (j = w % nw_full), q = ray-major
+  // index (ray - k*rc_rays) * P + s inside that chunk.  The chunk's R rays are `rows` batch rows of
+  // nloc rays each, starting at row-relative ray row_ray0 (a multi-GPU shard, or an internal chunk).
+  double* wss;       // [rows][nw_row][3] sum of squares of the nablas per window
+  int64_t netchunk;  // points per F.normalize window
+  int64_t rc_rays;   // the reference's rayschunk (clipped to the row)
+  int64_t row_rays;  // rays per batch row of the whole (unsharded) batch
+  int64_t row_ray0;  // row-relative index of this chunk's first ray
+  int64_t nw_full;   // windows per full reference ray chunk
+  int64_t nw_row;    // windows per batch row (row stride of wss)
+  int nloc;          // rays per batch row in this chunk (R = rows * nloc)
   const float* t_march; const float* t_query; const float* t_free;
+  // perturb (unisurf.py:158-165, :187-194): per-ray stratification uniforms of this chunk, rows of
+  // N_query / N_free (null: deterministic linspace; else t_query / t_free hold N+1 bin edges)
+  const float* u_q; const float* u_f;
 };
 
 struct UniOut {
@@ -44,6 +57,9 @@ struct UniPlan {
 
 UniPlan unisurf_plan(const NrUnisurfArgs& a, int64_t Rc);
 int64_t unisurf_chunk_rays(const NrUnisurfArgs& a);
+// window geometry of one batch row of the whole batch: (rayschunk clipped, windows per full chunk,
+// windows per row)
+void unisurf_windows(const NrUnisurfArgs& a, int64_t& rc_rays, int64_t& nw_full, int64_t& nw_row);
 
 __global__ void uni_prologue(UniChunk c, const float* rays_o, const float* rays_d);
 __global__ void uni_root(UniChunk c);
@@ -52,7 +68,7 @@ __global__ void rf_finish(UniChunk c, int64_t ray0, float* d_out, float* pts, ui
                           int fill_inf);
 __global__ void uni_secant(UniChunk c, int last);
 __global__ void uni_samples(UniChunk c, UniOut o);
-__global__ void uni_window_ss(UniChunk c);
+__global__ void uni_window_ss(UniChunk c);  // grid (nw_row, rows)
 __global__ void uni_normalize(UniChunk c, int mode);
 __global__ void uni_composite(UniChunk c, UniOut o, int calc_normal, int white_bkgd);
 

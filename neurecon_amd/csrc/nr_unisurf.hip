@@ -195,18 +195,28 @@ __global__ void uni_samples(UniChunk c, UniOut o) {
   const int64_t R = c.R;
   float* da = c.d_all + r;
   int jf = 0, jq = 0;
-  float vf = nf > 0 ? lerp_ref(nr, d_lo2, c.t_free[0]) : 0.0f;
-  float vq = nq > 0 ? lerp_ref(d_lo, d_up, c.t_query[0]) : 0.0f;
+  // sample j of a run on [a, b]: the linspace point, or (perturb) lower + (upper - lower) * u with the
+  // bin edges of linspace(0, 1, n+1); both runs stay ascending
+  auto run = [&](float a, float b, const float* t, const float* u, int j) {
+    const float lo = lerp_ref(a, b, t[j]);
+    if (!u) return lo;
+    const float hi = lerp_ref(a, b, t[j + 1]);
+    return fadd(lo, fmul(fsub(hi, lo), u[j]));
+  };
+  const float* uq = c.u_q ? c.u_q + (int64_t)r * nq : nullptr;
+  const float* uf = c.u_f ? c.u_f + (int64_t)r * nf : nullptr;
+  float vf = nf > 0 ? run(nr, d_lo2, c.t_free, uf, 0) : 0.0f;
+  float vq = nq > 0 ? run(d_lo, d_up, c.t_query, uq, 0) : 0.0f;
   for (int k = 0; k < P; ++k) {
     const bool take_f = jq >= nq || (jf < nf && vf <= vq);
     if (take_f) {
       da[k * R] = vf;
       ++jf;
-      if (jf < nf) vf = lerp_ref(nr, d_lo2, c.t_free[jf]);
+      if (jf < nf) vf = run(nr, d_lo2, c.t_free, uf, jf);
     } else {
       da[k * R] = vq;
       ++jq;
-      if (jq < nq) vq = lerp_ref(d_lo, d_up, c.t_query[jq]);
+      if (jq < nq) vq = run(d_lo, d_up, c.t_query, uq, jq);
     }
   }
   for (int k = 1; k < P; ++k) {
@@ -227,17 +237,27 @@ __global__ void uni_samples(UniChunk c, UniOut o) {
   }
 }
 
-// sum of squares of every nabla component over each F.normalize window (one block per window):
-// window w = points q in [w*netchunk, (w+1)*netchunk) of the chunk's ray-major flat order q = r*P+s
+// window of the point (row-relative ray rg, sample s)
+__device__ __forceinline__ int64_t uni_window(const UniChunk& c, int64_t rg, int64_t s) {
+  const int64_t k = rg / c.rc_rays;
+  return k * c.nw_full + ((rg - k * c.rc_rays) * c.P + s) / c.netchunk;
+}
+
+// sum of squares of every nabla component over the part of each F.normalize window that lies in
+// this chunk (one block per (window, batch row); windows the chunk does not touch get zeros)
 __global__ void uni_window_ss(UniChunk c) {
   __shared__ double red[3][256];
-  const int64_t w = blockIdx.x, t = threadIdx.x;
-  const int64_t n = (int64_t)c.R * c.P;
-  const int64_t q0 = w * c.netchunk, q1 = min(n, q0 + c.netchunk);
+  const int64_t w = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int64_t P = c.P, k = w / c.nw_full, j = w % c.nw_full;
+  const int64_t k0 = k * c.rc_rays;  // first ray of reference chunk k
+  const int64_t rays_k = min(c.rc_rays, c.row_rays - k0);
+  int64_t q0 = j * c.netchunk, q1 = min((j + 1) * c.netchunk, rays_k * P);
+  q0 = max(q0, (c.row_ray0 - k0) * P);           // points of this chunk's rays only
+  q1 = min(q1, (c.row_ray0 + c.nloc - k0) * P);
   double a0 = 0.0, a1 = 0.0, a2 = 0.0;
   for (int64_t q = q0 + t; q < q1; q += blockDim.x) {
-    const int64_t r = q / c.P, s = q % c.P;
-    const int64_t p = s * c.R + r;
+    const int64_t rl = k0 + q / P - c.row_ray0, s = q % P;  // ray within this chunk's row
+    const int64_t p = s * c.R + b * c.nloc + rl;            // sample-major point index
     const double x = c.nab_f[p * 3 + 0], y = c.nab_f[p * 3 + 1], z = c.nab_f[p * 3 + 2];
     a0 += x * x;
     a1 += y * y;
@@ -256,9 +276,10 @@ __global__ void uni_window_ss(UniChunk c) {
     __syncthreads();
   }
   if (t == 0) {
-    c.wss[w * 3 + 0] = red[0][0];
-    c.wss[w * 3 + 1] = red[1][0];
-    c.wss[w * 3 + 2] = red[2][0];
+    double* o = c.wss + (b * c.nw_row + w) * 3;
+    o[0] = red[0][0];
+    o[1] = red[1][0];
+    o[2] = red[2][0];
   }
 }
 
@@ -275,11 +296,12 @@ __global__ void uni_normalize(UniChunk c, int mode) {
     c.nrm_f[p * 3 + 1] = fdiv(y, d);
     c.nrm_f[p * 3 + 2] = fdiv(z, d);
   } else {
-    const int64_t r = p % c.R, s = p / c.R;
-    const int64_t w = (r * c.P + s) / c.netchunk;
-    c.nrm_f[p * 3 + 0] = fdiv(x, fmaxf((float)sqrt(c.wss[w * 3 + 0]), 1e-12f));
-    c.nrm_f[p * 3 + 1] = fdiv(y, fmaxf((float)sqrt(c.wss[w * 3 + 1]), 1e-12f));
-    c.nrm_f[p * 3 + 2] = fdiv(z, fmaxf((float)sqrt(c.wss[w * 3 + 2]), 1e-12f));
+    const int64_t rf = p % c.R, s = p / c.R;
+    const int64_t b = rf / c.nloc, rg = c.row_ray0 + rf % c.nloc;
+    const double* ws = c.wss + (b * c.nw_row + uni_window(c, rg, s)) * 3;
+    c.nrm_f[p * 3 + 0] = fdiv(x, fmaxf((float)sqrt(ws[0]), 1e-12f));
+    c.nrm_f[p * 3 + 1] = fdiv(y, fmaxf((float)sqrt(ws[1]), 1e-12f));
+    c.nrm_f[p * 3 + 2] = fdiv(z, fmaxf((float)sqrt(ws[2]), 1e-12f));
   }
 }
 
@@ -363,6 +385,8 @@ static constexpr int64_t kUniMaxChunk = 65536;
 // window, i.e. it is the reference's ray chunk (rayschunk) or a whole number of windows of it
 int64_t unisurf_chunk_rays(const NrUnisurfArgs& a) {
   const int64_t P = a.N_query + a.N_freespace;
+  if (a.normal_mode == 1 && a.shard_row_rays > 0)  // a multi-GPU shard is one chunk
+    return a.n_rays <= kUniMaxChunk ? (a.n_rays > 0 ? a.n_rays : 1) : -1;
   const int64_t per_b = a.rays_per_batch > 0 ? a.rays_per_batch : a.n_rays;
   if (a.normal_mode == 1) {
     const int64_t rc = a.rayschunk < per_b ? a.rayschunk : per_b;
@@ -375,11 +399,24 @@ int64_t unisurf_chunk_rays(const NrUnisurfArgs& a) {
   return a.n_rays < kUniMaxChunk ? (a.n_rays > 0 ? a.n_rays : 1) : kUniMaxChunk;
 }
 
+void unisurf_windows(const NrUnisurfArgs& a, int64_t& rc_rays, int64_t& nw_full, int64_t& nw_row) {
+  const int64_t P = a.N_query + a.N_freespace;
+  const int64_t row = a.shard_row_rays > 0 ? a.shard_row_rays : (a.rays_per_batch > 0 ? a.rays_per_batch : a.n_rays);
+  const int64_t nc = a.netchunk > 0 ? a.netchunk : 1;
+  rc_rays = a.rayschunk > 0 ? (a.rayschunk < row ? a.rayschunk : row) : (row > 0 ? row : 1);
+  if (rc_rays < 1) rc_rays = 1;
+  nw_full = (rc_rays * P + nc - 1) / nc;
+  nw_row = ((row + rc_rays - 1) / rc_rays) * nw_full;
+  if (nw_row < 1) nw_row = 1;
+}
+
 UniPlan unisurf_plan(const NrUnisurfArgs& a, int64_t Rc) {
   UniPlan p{};
   const int P = a.N_query + a.N_freespace;
   p.Rc = Rc;
-  p.max_windows = a.normal_mode == 1 ? (Rc * P + a.netchunk - 1) / a.netchunk : 1;
+  int64_t rc_rays = 1, nw_full = 1, nw_row = 1;
+  if (a.normal_mode == 1) unisurf_windows(a, rc_rays, nw_full, nw_row);
+  p.max_windows = nw_row;  // one batch row's windows (internal chunks never span rows)
   size_t off = 0;
   auto take = [&](size_t words) { size_t o = off; off = align_up(off + words * 4); return o; };
   p.o_ro = take(Rc * 3);

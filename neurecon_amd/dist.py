@@ -6,8 +6,8 @@ the per-ray maps are all-gathered once (RCCL over xGMI with backend 'nccl', gloo
 The same driver shards surface_render (sphere tracing / root finding are per ray) and
 `sdf_grid_sharded` splits extract_mesh's voxel grid by contiguous index ranges.
 UNISURF's F.normalize(nablas) couples the points of one `rayschunk` (unisurf.py:36,
-train_util.py:23-71); `align` keeps shard boundaries on those chunk boundaries so the result is
-identical to a single-process render.
+train_util.py:23-71): its shards exchange the per-window sums of nabla^2 (3 doubles per window, one
+all-reduce per render call) so the result equals a single-process render at any shard split.
 """
 import torch
 import torch.distributed as dist
@@ -41,6 +41,8 @@ def gather_rays(t, n_total, dim=0, align=1):
     rank, ws = world()
     if ws == 1:
         return t
+    if t.is_cuda and dist.get_backend() == 'gloo':  # gloo gathers host tensors only
+        return gather_rays(t.cpu(), n_total, dim, align).to(t.device)
     t = t.contiguous()
     sizes = [shard_bounds(n_total, r, ws, align) for r in range(ws)]
     cap = max(hi - lo for lo, hi in sizes)
@@ -53,14 +55,18 @@ def gather_rays(t, n_total, dim=0, align=1):
     return torch.cat([p.narrow(dim, 0, hi - lo) for p, (lo, hi) in zip(parts, sizes)], dim)
 
 
-def render_sharded(render_fn, rays_o, rays_d, model, gather=True, align=1, **kw):
+def render_sharded(render_fn, rays_o, rays_d, model, gather=True, align=1, group=None, **kw):
     """Render this rank's slice of the rays with `render_fn(rays_o, rays_d, model, **kw)` (any of the
     frameworks' volume_render); with gather=True the per-ray maps (rgb, depth, every extras entry
-    with a ray dimension) are all-gathered so every rank holds the full result."""
+    with a ray dimension) are all-gathered so every rank holds the full result.  A render whose
+    batched normalisation couples rays across shards (UNISURF, `render_fn.window_sharded`) is told
+    its slice and reduces those sums over the ranks itself (one small all-reduce per call)."""
     batched = kw.get('batched', False)
     dim = 1 if batched else 0
     n = rays_o.shape[dim]
-    ro, rd, _ = shard_rays(rays_o, rays_d, align=align, dim=dim)
+    ro, rd, (lo, hi) = shard_rays(rays_o, rays_d, align=align, dim=dim)
+    if getattr(render_fn, 'window_sharded', False) and batched and world()[1] > 1:
+        kw = dict(kw, shard=(lo, n, group))
     rgb, depth, extras = render_fn(ro, rd, model, **kw)
     if not gather:
         return rgb, depth, extras

@@ -62,16 +62,40 @@ def _linspace_table(n, device):
     return t
 
 
+def _neus_uniforms(B, N, batched, rayschunk, direct, n_iters, n_up, N_importance, N_outside, dev):
+    """perturb=True uniforms in the reference's draw order (neus.py:385-397 ray-chunk loop; per chunk
+    sample_pdf's torch.rand(..., device) per upsampling round (rend_util.py:271) and the NeRF++
+    stratification's CPU torch.rand (neus.py:310)), laid out for the library: u_rand
+    [n_iters][B*N][n_up] (direct: [B*N][N_importance]), t_out [B*N][N_outside]."""
+    pre = [B] if batched else []
+    rd = 1 + len(pre) if not direct else len(pre)  # ray dim of the drawn blocks
+    ups, outs = [], []
+    for r0 in range(0, N, rayschunk):
+        nc = min(rayschunk, N - r0)
+        if direct:
+            ups.append(rend_util.uniform([*pre, nc, N_importance], dev))
+        elif n_iters > 0:
+            ups.append(torch.stack([rend_util.uniform([*pre, nc, n_up], dev) for _ in range(n_iters)], 0))
+        if N_outside > 0:
+            outs.append(rend_util.uniform([*pre, nc, N_outside]).float().to(dev))
+    u = None
+    if ups:
+        u = torch.cat(ups, rd)
+        u = (u.reshape(B * N, N_importance) if direct else u.reshape(n_iters, B * N, n_up)).contiguous()
+    t_out = torch.cat(outs, len(pre)).reshape(B * N, N_outside).contiguous() if outs else None
+    return u, t_out
+
+
 def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False, batched_info={},
                   calc_normal=False, use_view_dirs=True, rayschunk=65536, netchunk=1048576, white_bkgd=False,
                   near_bypass=None, far_bypass=None, detailed_output=True, show_progress=False, perturb=False,
                   fixed_s_recp=1 / 64., N_samples=64, N_importance=64, N_outside=0,
                   upsample_algo='official_solution', N_nograd_samples=2048, N_upsample_iters=4, **dummy_kwargs):
-    """neus.py:118-397, render mode.  rays_o/rays_d: [(B,) N_rays, 3]; rays_d need not be normalized."""
+    """neus.py:118-397, render mode.  rays_o/rays_d: [(B,) N_rays, 3]; rays_d need not be normalized.
+    perturb=True draws the reference's uniforms (same generators, shapes and order) and hands them
+    to the kernels."""
     L.require_gpu(rays_o, 'rays_o')
     _no_training(model)
-    if perturb:
-        raise NotImplementedError('neurecon_amd: stratified (perturb=True) sampling is a training feature')
     if upsample_algo not in L.UPSAMPLE:
         raise NotImplementedError(upsample_algo)
     direct = upsample_algo != 'official_solution'
@@ -96,7 +120,7 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
 
     sdf_desc, sdf_packed = model.implicit_surface.nr_packed(dev)
     rad_desc, rad_packed = model.radiance_net.nr_packed(dev)
-    s = float(model.forward_s().detach().float().reshape(-1)[0].item())
+    s_dev = model.forward_s().detach().float().reshape(-1)[:1].contiguous()  # stays on the device
     t_coarse = _linspace_table(N_samples, dev)
     u_fine = _linspace_table(max(n_up, 1), dev)
 
@@ -117,7 +141,7 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     a.rays_o, a.rays_d, a.n_rays = L.ptr(ro), L.ptr(rd), n
     a.sdf, a.sdf_packed = ctypes.pointer(sdf_desc), L.ptr(sdf_packed)
     a.rad, a.rad_packed = ctypes.pointer(rad_desc), L.ptr(rad_packed)
-    a.s = s
+    a.s, a.s_dev = 0.0, L.ptr(s_dev)
     a.obj_bounding_radius = float(obj_bounding_radius)
     a.near_bypass = float('nan') if near_bypass is None else float(near_bypass)
     a.far_bypass = float('nan') if far_bypass is None else float(far_bypass)
@@ -145,9 +169,14 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
         a.nerf, a.nerf_packed = ctypes.pointer(nerf_desc), L.ptr(nerf_packed)
         a.N_outside, a.t_outside = N_outside, L.ptr(t_out)
         a.sigma_out, a.radiance_bg_out = L.ptr(det.get('sigma_out')), L.ptr(det.get('radiance_out'))
+    if perturb:
+        B = rays_d.shape[0] if batched else 1
+        u_rand, t_out_rand = _neus_uniforms(B, n // B, batched, int(rayschunk), direct, N_upsample_iters, n_up,
+                                            N_importance, N_outside, dev)
+        a.u_rand, a.t_out_rand = L.ptr(u_rand), L.ptr(t_out_rand)
     lib = L.lib()
     ws_bytes = lib.nr_neus_workspace_bytes(ctypes.byref(a))
-    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    ws = L.workspace(dev, ws_bytes)
     a.workspace, a.workspace_bytes = L.ptr(ws), ws_bytes
     L.check(lib.nr_neus_render(ctypes.byref(a), L.stream_of(dev)))
 

@@ -59,16 +59,45 @@ class UNISURF(nn.Module):
         return odds / (1 + odds)
 
 
+def _unisurf_uniforms(B, N, batched, rayschunk, N_query, N_freespace, dev):
+    """perturb=True stratification uniforms in the reference's draw order: per ray chunk the interval
+    samples' torch.rand then the free-space samples' (unisurf.py:164, :193)."""
+    pre = [B] if batched else []
+    uq, uf = [], []
+    for r0 in range(0, N, rayschunk):
+        nc = min(rayschunk, N - r0)
+        uq.append(rend_util.uniform([*pre, nc, N_query], dev))
+        uf.append(rend_util.uniform([*pre, nc, N_freespace], dev))
+    cat = lambda xs, k: torch.cat(xs, len(pre)).reshape(B * N, k).float().contiguous()
+    return cat(uq, N_query), cat(uf, N_freespace)
+
+
+def _window_reducer(window_ss, group=None):
+    """window_reduce callback of a sharded render: all-reduce (sum) the per-window partial sums."""
+    import torch.distributed as dist
+
+    def cb(_user):
+        try:
+            dist.all_reduce(window_ss, op=dist.ReduceOp.SUM, group=group)
+            return 0
+        except Exception as e:  # reported through the library's error path
+            print(f'neurecon_amd: window_reduce failed: {e!r}')
+            return 1
+    return L.WINDOW_REDUCE(cb)
+
+
 def volume_render(rays_o, rays_d, model, batched=False, batched_info={}, calc_normal=False, logit_tau=0.0,
                   use_view_dirs=True, method='secant', rayschunk=65536, netchunk=1048576, white_bkgd=False,
                   near_bypass=None, far_bypass=None, detailed_output=True, show_progress=False,
                   radius_of_interest=4.0, perturb=False, interval=1.0, too_close_threshold=0.1, N_query=64,
-                  N_freespace=32, **dummy_kwargs):
-    """unisurf.py:62-283, render mode.  rays_o/rays_d: [(B,) N_rays, 3]."""
+                  N_freespace=32, shard=None, **dummy_kwargs):
+    """unisurf.py:62-283, render mode.  rays_o/rays_d: [(B,) N_rays, 3].
+    shard = (ray0, row_rays, group): these rays are ranks' slice [ray0, ray0 + N) of batch rows of
+    row_rays rays (neurecon_amd.dist.render_sharded); the windowed F.normalize then sums its nabla^2
+    windows over all ranks (one all-reduce of B x windows x 3 doubles), so the result equals the
+    single-process render of the whole batch."""
     L.require_gpu(rays_o, 'rays_o')
     _no_training(model)
-    if perturb:
-        raise NotImplementedError('neurecon_amd: stratified (perturb=True) sampling is a training feature')
     if method != 'secant':
         raise NotImplementedError(f'neurecon_amd: root finding method={method!r} not native')
     if not use_view_dirs:
@@ -88,8 +117,9 @@ def volume_render(rays_o, rays_d, model, batched=False, batched_info={}, calc_no
     sdf_desc, sdf_packed = model.implicit_surface.nr_packed(dev)
     rad_desc, rad_packed = model.radiance_net.nr_packed(dev)
     t_march = _linspace_table(N_STEPS, dev)
-    t_query = _linspace_table(N_query, dev)
-    t_free = _linspace_table(N_freespace, dev)
+    # perturb: bin edges linspace(0, 1, N+1) (unisurf.py:159, :188)
+    t_query = _linspace_table(N_query + (1 if perturb else 0), dev)
+    t_free = _linspace_table(N_freespace + (1 if perturb else 0), dev)
 
     rgb = torch.empty(n, 3, device=dev)
     depth = torch.empty(n, device=dev)
@@ -126,13 +156,27 @@ def volume_render(rays_o, rays_d, model, batched=False, batched_info={}, calc_no
     a.nablas_out = L.ptr(det.get('implicit_nablas'))
     a.alpha_out = L.ptr(det.get('alpha'))
     a.weights_out = L.ptr(det.get('visibility_weights'))
+    if perturb:
+        B = rays_d.shape[0] if batched else 1
+        u_q, u_f = _unisurf_uniforms(B, n // B, batched, int(rayschunk), N_query, N_freespace, dev)
+        a.u_query, a.u_free = L.ptr(u_q), L.ptr(u_f)
     lib = L.lib()
+    keep = None
+    if shard is not None and batched:
+        ray0, row_rays, group = shard
+        a.shard_ray0, a.shard_row_rays = int(ray0), int(row_rays)
+        B = rays_d.shape[0]
+        window_ss = torch.zeros(B, max(int(lib.nr_unisurf_window_count(ctypes.byref(a))), 1), 3,
+                                dtype=torch.float64, device=dev)
+        keep = _window_reducer(window_ss, group)
+        a.window_ss, a.window_reduce = L.ptr(window_ss), ctypes.cast(keep, ctypes.c_void_p)
     ws_bytes = lib.nr_unisurf_workspace_bytes(ctypes.byref(a))
     if ws_bytes == 0:
         raise NotImplementedError('neurecon_amd: ' + lib.nr_last_error().decode())
-    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    ws = L.workspace(dev, ws_bytes)
     a.workspace, a.workspace_bytes = L.ptr(ws), ws_bytes
     L.check(lib.nr_unisurf_render(ctypes.byref(a), L.stream_of(dev)))
+    del keep
 
     ret = OrderedDict([('rgb', rgb.reshape(*prefix, 3)), ('depth_volume', depth.reshape(prefix)),
                        ('mask_volume', acc.reshape(prefix))])
@@ -159,6 +203,9 @@ class SingleRenderer(nn.Module):
 
     def forward(self, rays_o, rays_d, **kwargs):
         return volume_render(rays_o, rays_d, self.model, **kwargs)
+
+
+volume_render.window_sharded = True  # render_sharded passes `shard=` (cross-rank F.normalize windows)
 
 
 class Trainer(nn.Module):

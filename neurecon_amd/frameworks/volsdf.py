@@ -144,7 +144,9 @@ def volume_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=
         a.beta_plus_k = float(np.float32(4 * (N0 - 1) * np.log(1 + epsilon)))
     a.eps = float(epsilon)
     a.near, a.far = float(near), float(far)
-    a.obj_bounding_radius = float(model.obj_bounding_radius)
+    # builtin background: the model's radius (volsdf.py:310-325); NeRF++: the sphere-exit far comes
+    # from volume_render's own argument (volsdf.py:404), like the background radii rs_out above
+    a.obj_bounding_radius = float(obj_bounding_radius) if No > 0 else float(model.obj_bounding_radius)
     a.use_sphere_bg = int(bool(model.use_sphere_bg))
     a.N_samples, a.N_importance = N_samples, N_importance
     a.max_upsample_steps, a.max_bisection_steps = max_upsample_steps, max_bisection_steps

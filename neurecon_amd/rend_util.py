@@ -37,6 +37,12 @@ def get_rays(c2w, intrinsics, H, W, N_rays=-1):
     return ro.reshape(*prefix, N, 3), rd.reshape(*prefix, N, 3), select_inds
 
 
+def uniform(shape, device=None):
+    """torch.rand(shape, device=device): every perturb=True draw of the render path goes through here,
+    in the reference's order, generators and shapes (tests replay recorded draws by patching it)."""
+    return torch.rand(list(shape), device=device)
+
+
 def near_far_from_sphere(ray_origins, ray_directions, r=1.0, keepdim=True):
     """rend_util.py:167-185 (the render kernels compute this in-kernel; kept for API users)."""
     mid = -torch.sum(ray_origins * ray_directions, dim=-1, keepdim=keepdim)
@@ -44,17 +50,20 @@ def near_far_from_sphere(ray_origins, ray_directions, r=1.0, keepdim=True):
 
 
 def sample_pdf(bins, weights, N_importance, det=False, eps=1e-5):
-    """rend_util.py:255-292 on the HIP kernel (det=True)."""
-    if not det:
-        raise NotImplementedError('neurecon_amd.sample_pdf: stochastic sampling is a training feature')
+    """rend_util.py:255-292 on the HIP kernel.  det=False draws u = torch.rand([..., N_importance],
+    device=weights.device) exactly as the reference (rend_util.py:271)."""
     L.require_gpu(bins, 'bins')
     shape = bins.shape[:-1]
     Lb = bins.shape[-1]
     b = bins.reshape(-1, Lb).float().contiguous()
     w = weights.reshape(-1, Lb - 1).float().contiguous()
-    u = torch.linspace(0.0, 1.0, steps=N_importance).float().to(bins.device)
+    if det:
+        u, stride = torch.linspace(0.0, 1.0, steps=N_importance).float().to(bins.device), 0
+    else:
+        u = uniform(list(weights.shape[:-1]) + [N_importance], weights.device).float().reshape(-1, N_importance)
+        u, stride = u.to(bins.device).contiguous(), N_importance
     out = torch.empty(b.shape[0], N_importance, device=bins.device)
-    L.check(L.lib().nr_sample_pdf(L.ptr(b), L.ptr(w), b.shape[0], Lb, L.ptr(u), N_importance, L.ptr(out),
+    L.check(L.lib().nr_sample_pdf(L.ptr(b), L.ptr(w), b.shape[0], Lb, L.ptr(u), stride, N_importance, L.ptr(out),
                                   L.stream_of(bins.device)))
     return out.reshape(*shape, N_importance)
 

@@ -384,13 +384,76 @@ def gen_surface(R):
          rf_normals=ex_rf['normals_surface'], rf2_d=rf[0], rf2_pts=rf[1], rf2_mask=rf[2], rf2_msc=rf[3])
 
 
+class _RecordRand:
+    """torch.rand wrapper recording every draw (in call order) of a perturb=True reference render, so
+    the GPU test can replay exactly these uniforms through neurecon_amd.rend_util.uniform."""
+
+    def __init__(self):
+        self.draws = []
+
+    def __enter__(self):
+        self.orig = torch.rand
+
+        def rand(*a, **k):
+            t = self.orig(*a, **k)
+            self.draws.append(t.detach().clone())
+            return t
+        torch.rand = rand
+        return self
+
+    def __exit__(self, *exc):
+        torch.rand = self.orig
+
+
+def gen_perturb(R):
+    """perturb=True renders (stratified / stochastic sampling, the training-time path) of configs (b),
+    (d) and (e) on 64-ray sub-grids, with the uniforms the reference drew."""
+    out = {}
+    for key, seed, nerfpp in [('b', 1, False), ('d', 4, True)]:
+        sd = wg.neus_state(seed=seed, use_outside_nerf=nerfpp)
+        model = _neus_model(R, sd, nerfpp)
+        H, W, _, _ = wg.CAMERAS[key]
+        idx = grid_idx(H, W) if key == 'b' else grid_idx(H, W, n=8, lo=0.02, hi=0.98)
+        ro, rd = camera_rays(R, key, idx)
+        torch.manual_seed(100 + seed)
+        with torch.no_grad(), _RecordRand() as rec:
+            rgb, depth, ex = R.neus.volume_render(
+                ro, rd, model, obj_bounding_radius=1.0, batched=True, calc_normal=True, detailed_output=True,
+                perturb=True, N_samples=64, N_importance=64, N_outside=32 if nerfpp else 0,
+                upsample_algo='official_solution', N_upsample_iters=4)
+        out.update({f'{key}_rays_o': ro, f'{key}_rays_d': rd, f'{key}_rgb': rgb, f'{key}_depth': depth,
+                    f'{key}_mask': ex['mask_volume'], f'{key}_normals': ex['normals_volume'],
+                    f'{key}_d_final': ex['d_final'], f'{key}_n_draws': len(rec.draws)})
+        out.update({f'{key}_u{i}': u for i, u in enumerate(rec.draws)})
+    save('neus_perturb.npz', **out)
+
+    sd = wg.unisurf_state(seed=3)
+    m = R.unisurf.UNISURF(W_geo_feat=256, surface_cfg=dict(radius_init=1.0, **SURF),
+                          radiance_cfg=dict(use_siren=False, embed_multires=-1, embed_multires_view=-1,
+                                            use_view_dirs=True, D=4, W=256, skips=[]))
+    m.load_state_dict(sd)
+    m.eval()
+    H, W, _, _ = wg.CAMERAS['e']
+    ro, rd = camera_rays(R, 'e', grid_idx(H, W, n=8, lo=0.1, hi=0.9))
+    logit_tau = R.unisurf.UNISURF.get_surface_from_opacity(0.5)
+    torch.manual_seed(103)
+    with torch.no_grad(), _RecordRand() as rec:
+        rgb, depth, ex = R.unisurf.volume_render(
+            ro, rd, m, batched=True, calc_normal=True, detailed_output=True, perturb=True, logit_tau=logit_tau,
+            radius_of_interest=4.0, interval=1.0, N_query=64, N_freespace=32)
+    save('unisurf_perturb.npz', seed=3, logit_tau=float(logit_tau), rays_o=ro, rays_d=rd, rgb=rgb, depth=depth,
+         mask=ex['mask_volume'], normals=ex['normals_volume'], d_vals=ex.get('d_vals', depth),
+         sdf=ex['implicit_surface'], weights=ex['visibility_weights'], n_draws=len(rec.draws),
+         **{f'u{i}': u for i, u in enumerate(rec.draws)})
+
+
 def main():
     torch.set_num_threads(8)
     R = _import_reference()
     only = sys.argv[1:]
     gens = dict(components=gen_components, sampling=gen_sampling, neus=gen_neus, volsdf=gen_volsdf,
                 unisurf=gen_unisurf, surface=gen_surface,
-                volsdf_nerfpp=gen_volsdf_nerfpp)
+                volsdf_nerfpp=gen_volsdf_nerfpp, perturb=gen_perturb)
     for name, fn in gens.items():
         if not only or name in only:
             fn(R)

@@ -1,0 +1,106 @@
+"""GPU parity of perturb=True (training-time stochastic sampling) vs the reference.
+
+The reference draws its uniforms with torch.rand inside the render (rend_util.py:271 for every
+upsampling round's sample_pdf, neus.py:306-311 for the NeRF++ depths, unisurf.py:164/193 for the
+interval / free-space strata).  tests/golden/gen_golden.py recorded those draws; here they are
+replayed through neurecon_amd.rend_util.uniform -- same shapes, same order -- so the HIP kernels
+invert exactly the uniforms the reference inverted.  Bar: 1e-4 relative + 1e-6 on rgb / depth /
+mask; rays whose sample depths moved (discrete sampling decisions, see test_gpu_parity.py) are
+reported, and no ray with identical samples may miss the bar.
+"""
+import numpy as np
+import pytest
+import torch
+
+import weightgen as wg
+from helpers import neus_model, report, to_gpu, unisurf_model
+
+pytestmark = pytest.mark.gpu
+
+RT, AT = 1e-4, 1e-6
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from neurecon_amd import _lib
+    _lib.lib()
+
+
+class Replay:
+    """stand-in for rend_util.uniform returning the recorded draws in order (shape-checked)"""
+
+    def __init__(self, draws):
+        self.draws = list(draws)
+
+    def __call__(self, shape, device=None):
+        assert self.draws, 'more draws than the reference made'
+        u = self.draws.pop(0)
+        assert tuple(u.shape) == tuple(shape), (u.shape, shape)
+        return torch.from_numpy(u).to(device if device is not None else 'cpu')
+
+
+def _replay(monkeypatch, g, prefix):
+    from neurecon_amd import rend_util
+    n = int(g[prefix + 'n_draws'])
+    r = Replay([g[f'{prefix}u{i}'] for i in range(n)])
+    monkeypatch.setattr(rend_util, 'uniform', r)
+    return r
+
+
+@pytest.mark.parametrize('key', ['b', 'd'])
+@pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
+def test_neus_perturb_vs_golden(golden, monkeypatch, key, precision):
+    g = golden('neus_perturb')
+    nerfpp = key == 'd'
+    m = neus_model(wg.neus_state(seed=1 if key == 'b' else 4, use_outside_nerf=nerfpp), use_outside_nerf=nerfpp,
+                   precision=precision)
+    r = _replay(monkeypatch, g, key + '_')
+    from neurecon_amd.frameworks.neus import volume_render
+    with torch.no_grad():
+        rgb, depth, ex = volume_render(to_gpu(g[key + '_rays_o']), to_gpu(g[key + '_rays_d']), m,
+                                       obj_bounding_radius=1.0, batched=True, calc_normal=True, detailed_output=True,
+                                       perturb=True, N_samples=64, N_importance=64, N_outside=32 if nerfpp else 0,
+                                       upsample_algo='official_solution', N_upsample_iters=4)
+    assert not r.draws, 'fewer draws than the reference made'
+    ok_d, _ = report(f'{key} d_final', ex['d_final'], g[key + '_d_final'], 1e-5, 1e-6)
+    same = ok_d.reshape(-1, ok_d.shape[-1]).all(-1)
+    ok_rgb, _ = report(f'{key} rgb', rgb, g[key + '_rgb'], RT, AT)
+    ok_dep, _ = report(f'{key} depth', depth, g[key + '_depth'], RT, AT)
+    ok_m, _ = report(f'{key} mask', ex['mask_volume'], g[key + '_mask'], RT, AT)
+    ok_n, _ = report(f'{key} normals', ex['normals_volume'], g[key + '_normals'], RT, 1e-4)
+    ray_ok = (ok_rgb.all(-1) & ok_dep & ok_m).reshape(-1)
+    print(f'{key}/{precision}: identical samples on {same.mean() * 100:.1f}% of rays, per-ray pass '
+          f'{ray_ok.mean() * 100:.1f}%, failing rays with identical samples {(~ray_ok & same).sum()}')
+    assert (~ray_ok & same).sum() == 0
+    assert ok_n.all(-1).reshape(-1)[same].all()
+    assert same.mean() >= 0.6 and ray_ok.mean() >= 0.9
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
+def test_unisurf_perturb_vs_golden(golden, monkeypatch, precision):
+    g = golden('unisurf_perturb')
+    m = unisurf_model(wg.unisurf_state(seed=int(g['seed'])), precision=precision)
+    r = _replay(monkeypatch, g, '')
+    from neurecon_amd.frameworks.unisurf import volume_render
+    with torch.no_grad():
+        rgb, depth, ex = volume_render(to_gpu(g['rays_o']), to_gpu(g['rays_d']), m, batched=True, calc_normal=True,
+                                       detailed_output=True, perturb=True, logit_tau=float(g['logit_tau']),
+                                       radius_of_interest=4.0, interval=1.0, N_query=64, N_freespace=32)
+    assert not r.draws
+    assert report('unisurf perturb sdf', ex['implicit_surface'], g['sdf'], RT, AT)[0].all()
+    assert report('unisurf perturb weights', ex['visibility_weights'], g['weights'], RT, AT)[0].all()
+    assert report('unisurf perturb rgb', rgb, g['rgb'], RT, AT)[0].all()
+    assert report('unisurf perturb depth', depth, g['depth'], RT, AT)[0].all()
+    assert report('unisurf perturb mask', ex['mask_volume'], g['mask'], RT, AT)[0].all()
+    assert report('unisurf perturb normals', ex['normals_volume'], g['normals'], RT, 1e-4)[0].all()
+
+
+def test_sample_pdf_random_u_vs_golden(golden, monkeypatch):
+    """rend_util.sample_pdf(det=False): the reference's draw u (recorded) inverted on the GPU."""
+    from neurecon_amd import rend_util
+    g = golden('sampling')
+    monkeypatch.setattr(rend_util, 'uniform', Replay([g['u_rand']]))
+    s = rend_util.sample_pdf(to_gpu(g['bins']), to_gpu(g['weights']), 16, det=False)
+    assert report('sample_pdf det=False', s, g['s_rand'], 1e-6, 1e-6)[0].all()

@@ -83,3 +83,35 @@ def test_unisurf_rayschunk_invariance():
         b = volume_render(ro[0].cuda(), rd[0].cuda(), m, batched=False, calc_normal=True, logit_tau=0.0)
     assert a[0].shape == (1, H * W, 3) and b[0].shape == (H * W, 3)
     assert torch.isfinite(a[0]).all() and torch.isfinite(b[0]).all()
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
+def test_unisurf_full_config_e_vs_oracle(precision):
+    """config (e) at full size: all 4096 rays of the 64x64 camera in ONE F.normalize window (4096 x 96
+    points < netchunk), vs the oracle on the host.  The hit mask decides the interval samples: rays
+    whose hit flag agrees must meet the bar on every output."""
+    from oracle.unisurf import UNISURFOracle
+    from oracle import rays as orays
+    from neurecon_amd.frameworks.unisurf import volume_render
+    H, W, f, dist = wg.CAMERAS['e']
+    ro, rd, _ = orays.get_rays(wg.look_at_c2w(dist)[None], wg.intrinsics(f, H, W)[None], H, W)
+    sd = wg.unisurf_state(seed=3)
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    with torch.no_grad():
+        ref = UNISURFOracle(sd).render(ro, rd, logit_tau=0.0)
+        m = unisurf_model(sd, precision=precision)
+        rgb, depth, ex = volume_render(ro.cuda(), rd.cuda(), m, batched=True, calc_normal=True, detailed_output=True,
+                                       logit_tau=0.0, N_query=64, N_freespace=32)
+    hit_same = (ex['mask_surface'].cpu().numpy() == ref['mask_surface'].numpy()).reshape(-1)
+    ok_rgb, _ = report(f'[e full {precision}] rgb', rgb, ref['rgb'], RT, AT)
+    ok_dep, _ = report(f'[e full {precision}] depth', depth, ref['depth_volume'], RT, AT)
+    ok_m, _ = report(f'[e full {precision}] mask', ex['mask_volume'], ref['mask_volume'], RT, AT)
+    ok_n, _ = report(f'[e full {precision}] normals', ex['normals_volume'], ref['normals_volume'], RT, 1e-4)
+    ok_ds, _ = report(f'[e full {precision}] depth_surface', ex['depth_surface'], ref['depth_surface'], RT, AT)
+    ray_ok = (ok_rgb.all(-1) & ok_dep & ok_m & ok_n.all(-1)).reshape(-1)
+    print(f'[e full {precision}] hit rays {int(ref["mask_surface"].sum())}/4096, hit flags identical '
+          f'{hit_same.mean() * 100:.3f}%, per-ray pass {ray_ok.mean() * 100:.3f}%, failing rays with identical hit '
+          f'flag {(~ray_ok & hit_same).sum()}')
+    assert hit_same.mean() >= 0.999
+    assert (~ray_ok & hit_same).sum() == 0
+    assert ok_ds.reshape(-1)[hit_same].all()

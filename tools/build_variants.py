@@ -35,7 +35,7 @@ def one(name):
     objs = []
     for src in B._sources():
         obj = os.path.join(out_dir, f'{name}_{os.path.basename(src)}.o')
-        subprocess.check_call([B.HIPCC] + B.FLAGS + VARIANTS[name] + ['-c', src, '-o', obj])
+        subprocess.check_call([B.HIPCC] + B.FLAGS + ['-DNR_VARIANT_BUILD'] + VARIANTS[name] + ['-c', src, '-o', obj])
         objs.append(obj)
     lib = os.path.join(out_dir, f'libnrhip_{name}.so')
     subprocess.check_call([B.HIPCC, '-shared', '-fPIC', f'--offload-arch={B.ARCH}', '-o', lib] + objs)
