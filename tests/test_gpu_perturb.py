@@ -89,7 +89,10 @@ def test_unisurf_perturb_vs_golden(golden, monkeypatch, precision):
                                        detailed_output=True, perturb=True, logit_tau=float(g['logit_tau']),
                                        radius_of_interest=4.0, interval=1.0, N_query=64, N_freespace=32)
     assert not r.draws
-    assert report('unisurf perturb sdf', ex['implicit_surface'], g['sdf'], RT, AT)[0].all()
+    # per-sample logits: the f16x3 GEMMs keep 22 significant bits, ~1e-6 of the activations' O(1..10)
+    # magnitude -> 1e-5 absolute near the surface (|logit| < 0.1); fp32 holds 1e-6
+    assert report('unisurf perturb sdf', ex['implicit_surface'], g['sdf'], RT,
+                  AT if precision == 'fp32' else 1e-5)[0].all()
     assert report('unisurf perturb weights', ex['visibility_weights'], g['weights'], RT, AT)[0].all()
     assert report('unisurf perturb rgb', rgb, g['rgb'], RT, AT)[0].all()
     assert report('unisurf perturb depth', depth, g['depth'], RT, AT)[0].all()
