@@ -184,6 +184,12 @@ typedef struct {
   const float* u_rand;
   const float* t_out_rand;
   const float* s_dev; /* optional device scalar s (overrides `s`): no host round trip per call */
+  /* sample_only = 1 (training, neus.py:206-279 under torch.no_grad): stop after the upsampling and
+   * write the sorted sample depths d_all_out [n_rays, S]; rgb / depth / acc may then be NULL.  The
+   * differentiable part of the step (SDF + nablas, radiance, compositing) runs through the
+   * nr_train entry points below. */
+  int sample_only;
+  float* d_all_out;
 } NrNeusArgs;
 
 size_t nr_neus_workspace_bytes(const NrNeusArgs* a);
@@ -333,6 +339,10 @@ int nr_sample_pdf(const float* bins, const float* weights, int64_t R, int L, con
  * ------------------------------------------------------------------------------------------ */
 int nr_get_rays(const float* c2w, const float* K, int B, int H, int W, const int64_t* select_inds, int64_t N,
                 float* rays_o, float* rays_d, void* stream);
+/* training targets of a random ray batch (neus.py:432 torch.gather of ground_truth['rgb'], :449 of
+ * the object mask): out[b, n] = src[b, idx[b, n]] for rows of row_bytes bytes, src [B, HW, ...] */
+int nr_gather_rows(const void* src, int64_t B, int64_t HW, int64_t row_bytes, const int64_t* idx, int64_t N, void* out,
+                   void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Surface rendering (models/ray_casting.py:163-263).
@@ -372,6 +382,49 @@ int nr_surface_finish(float* rgb, const float* nablas, const uint8_t* mask, int6
 size_t nr_sdf_grid_workspace_bytes(int64_t n_points);
 int nr_sdf_grid(const NrSdfDesc* d, const void* packed, double volume_size, int64_t N, int64_t i0, int64_t n,
                 float* sdf, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Training path (models/frameworks/neus.py:417-485, models/base.py:265-282 with
+ * create_graph=True).  The host runs the step layer by layer: the dense [P, K] x [K, N] layer
+ * products go to hipBLASLt, every per-point / per-ray step between them is one of these kernels.
+ * The double backward through the nablas is reverse mode over the (primal, tangent) network (see
+ * nr_train.hip): tangent seed J_emb(x) grad_nabla, adjoint zbar = hbar s + g zdot s'.
+ *   nr_embed          Embedder.forward (base.py:46-64): [P,3] -> [P, 3+6F]
+ *   nr_embed_jvp      J_emb(x) v                      (tangent seed)
+ *   nr_embed_vjp      J_emb(x)^T (e0 + s1 e1) -> [P,3] (nablas; autograd.grad through the encoding)
+ *   nr_softplus100    Softplus(beta=100, threshold=20) (base.py:202) and softplus_backward's factor
+ *   nr_scale_cols     out = a[:, col0:col0+n] * scale (* s)  (skip-connection split, delta = s * g)
+ *   nr_softplus_adjoint  zbar = hbar * s + g * zdot * 100 s (1 - s)  (softplus_double_backward)
+ *   nr_mul / nr_activation  elementwise product; ReLU / sigmoid forward (in place) and backward
+ *   nr_radiance_input cat([x, embed_view(v), normals, feature]) (base.py:379-384)
+ *   nr_neus_points    pts / d_mid / pts_mid of the sorted sample depths (neus.py:284-288)
+ *   nr_neus_composite_fwd/bwd  sdf_to_alpha, alpha_to_w, rgb / depth / acc (neus.py:28-70, 346-355)
+ *                      and their gradient w.r.t. sdf, radiance and s (per-ray partials of d s)
+ * ------------------------------------------------------------------------------------------ */
+int nr_embed(const float* x, int64_t P, int nfreq, float* out, void* stream);
+int nr_embed_jvp(const float* x, const float* v, int64_t P, int nfreq, float* out, void* stream);
+int nr_embed_vjp(const float* x, const float* e0, int ld0, const float* e1, int ld1, float s1, int64_t P, int nfreq,
+                 float* out, void* stream);
+int nr_softplus100(const float* z, int64_t n, float* h, float* s, void* stream);
+int nr_scale_cols(const float* a, int64_t P, int lda, int col0, int ncols, const float* s, float scale, float* out,
+                  void* stream);
+int nr_softplus_adjoint(const float* hbar, int ldh, const float* s, const float* g, const float* zdot, int64_t P,
+                        int n, float* zbar, void* stream);
+int nr_mul(const float* a, const float* b, int64_t n, float* out, void* stream);
+/* mode 0: y = relu(y); 1: g *= (y > 0); 2: y = sigmoid(y); 3: g *= y (1 - y) */
+int nr_activation(float* y, float* g, int64_t n, int mode, void* stream);
+int nr_radiance_input(const float* x, const float* v, const float* nrm, const float* feat, int64_t P, int nfreq_view,
+                      int wfeat, float* out, void* stream);
+int nr_neus_points(const float* rays_o, const float* rays_d, const float* d_all, int64_t R, int S, float* pts,
+                   float* mids, float* dmid, void* stream);
+int nr_neus_composite_fwd(const float* sdf, const float* s_dev, const float* rad, const float* dmid, int64_t R, int S,
+                          int white_bkgd, float* rgb, float* depth, float* acc, float* weights, float* alpha,
+                          float* cdf, void* stream);
+size_t nr_neus_composite_bwd_workspace_bytes(int64_t R, int S);
+int nr_neus_composite_bwd(const float* sdf, const float* s_dev, const float* rad, const float* dmid, int64_t R, int S,
+                          int white_bkgd, const float* g_rgb, const float* g_depth, const float* g_acc,
+                          const float* g_weights, float* d_sdf, float* d_rad, float* d_s, void* workspace,
+                          size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Opt-in kernel timing (diagnostics / bench roofline).  While enabled, every kernel launch of

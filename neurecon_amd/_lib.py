@@ -54,7 +54,7 @@ class NrNeusArgs(ctypes.Structure):
         ('sigma_out', _c_p), ('radiance_bg_out', _c_p),
         ('upsample_algo', _c_i), ('fixed_s', _c_f), ('N_nograd_samples', _c_i), ('t_nograd', _c_p),
         ('workspace', _c_p), ('workspace_bytes', _c_sz),
-        ('u_rand', _c_p), ('t_out_rand', _c_p), ('s_dev', _c_p),
+        ('u_rand', _c_p), ('t_out_rand', _c_p), ('s_dev', _c_p), ('sample_only', _c_i), ('d_all_out', _c_p),
     ]
 
 
@@ -130,6 +130,7 @@ _SIGS = {
     'nr_unisurf_window_count': (_c_i64, [ctypes.POINTER(NrUnisurfArgs)]),
     'nr_sample_pdf': (_c_i, [_c_p, _c_p, _c_i64, _c_i, _c_p, _c_i64, _c_i, _c_p, _c_p]),
     'nr_get_rays': (_c_i, [_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p]),
+    'nr_gather_rows': (_c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_p, _c_p]),
     'nr_sphere_trace_workspace_bytes': (_c_sz, [_c_i64]),
     'nr_sphere_trace': (_c_i, [ctypes.POINTER(NrSdfDesc), _c_p, _c_p, _c_p, _c_i64, ctypes.c_float, ctypes.c_float,
                                _c_i, _c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
@@ -141,6 +142,22 @@ _SIGS = {
     'nr_sdf_grid_workspace_bytes': (_c_sz, [_c_i64]),
     'nr_sdf_grid': (_c_i, [ctypes.POINTER(NrSdfDesc), _c_p, ctypes.c_double, _c_i64, _c_i64, _c_i64, _c_p, _c_p,
                            _c_sz, _c_p]),
+    # training path (nr_train.hip)
+    'nr_embed': (_c_i, [_c_p, _c_i64, _c_i, _c_p, _c_p]),
+    'nr_embed_jvp': (_c_i, [_c_p, _c_p, _c_i64, _c_i, _c_p, _c_p]),
+    'nr_embed_vjp': (_c_i, [_c_p, _c_p, _c_i, _c_p, _c_i, _c_f, _c_i64, _c_i, _c_p, _c_p]),
+    'nr_softplus100': (_c_i, [_c_p, _c_i64, _c_p, _c_p, _c_p]),
+    'nr_scale_cols': (_c_i, [_c_p, _c_i64, _c_i, _c_i, _c_i, _c_p, _c_f, _c_p, _c_p]),
+    'nr_softplus_adjoint': (_c_i, [_c_p, _c_i, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_p, _c_p]),
+    'nr_mul': (_c_i, [_c_p, _c_p, _c_i64, _c_p, _c_p]),
+    'nr_activation': (_c_i, [_c_p, _c_p, _c_i64, _c_i, _c_p]),
+    'nr_radiance_input': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_p, _c_p]),
+    'nr_neus_points': (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_i, _c_p, _c_p, _c_p, _c_p]),
+    'nr_neus_composite_fwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                     _c_p]),
+    'nr_neus_composite_bwd_workspace_bytes': (_c_sz, [_c_i64, _c_i]),
+    'nr_neus_composite_bwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                     _c_p, _c_p, _c_sz, _c_p]),
     'nr_profile_enable': (_c_i, [_c_i]),
     'nr_profile_read': (_c_i, [ctypes.POINTER(NrKernelStat), _c_i, ctypes.POINTER(_c_i)]),
 }

@@ -103,14 +103,22 @@ import ctypes  # noqa: E402
 ctypes_void_p = ctypes.c_void_p
 
 
-def _no_training(*tensors_or_modules):
-    if torch.is_grad_enabled():
-        for m in tensors_or_modules:
-            ps = m.parameters() if isinstance(m, nn.Module) else [m]
-            if any(getattr(p, 'requires_grad', False) for p in ps):
-                raise NotImplementedError(
-                    'neurecon_amd: the native HIP path implements render mode (no autograd graph); wrap the call '
-                    'in torch.no_grad() -- the training backward is the next milestone (SURVEY.md §8f)')
+def wants_graph(*tensors_or_modules):
+    """True when the call must build an autograd graph (grad mode and a parameter that needs grad)."""
+    if not torch.is_grad_enabled():
+        return False
+    for m in tensors_or_modules:
+        ps = m.parameters() if isinstance(m, nn.Module) else [m]
+        if any(getattr(p, 'requires_grad', False) for p in ps):
+            return True
+    return False
+
+
+def _no_training(*tensors_or_modules, what='this call'):
+    if wants_graph(*tensors_or_modules):
+        raise NotImplementedError(
+            f'neurecon_amd: {what} has no native training (autograd) path; wrap it in torch.no_grad() '
+            '(training runs through the NeuS / SDF / radiance autograd functions of neurecon_amd.training)')
 
 
 # ---------------------------------------------------------------------------------------------
@@ -193,8 +201,11 @@ class ImplicitSurface(nn.Module):
 
     def _run(self, x, nabla, feature):
         L.require_gpu(x, 'points')
-        _no_training(self)
         shape = x.shape[:-1]
+        if wants_graph(self):  # training: differentiable sdf / nablas / feature (double backward)
+            from .training import sdf_nablas
+            sdf, nab, feat = sdf_nablas(self, x, True)
+            return [sdf.reshape(shape), nab.reshape(*shape, 3), feat.reshape(*shape, self.W_geo_feat)]
         pts = x.reshape(-1, 3).float().contiguous()
         P = pts.shape[0]
         dev = pts.device
@@ -231,6 +242,8 @@ class ImplicitSurface(nn.Module):
 # RadianceNet (models/base.py:312-391)
 # ---------------------------------------------------------------------------------------------
 class RadianceNet(nn.Module):
+    """RadianceNet (base.py:312-391)."""
+
     def __init__(self, D=4, W=256, skips=[], W_geo_feat=256, embed_multires=6, embed_multires_view=4,
                  use_view_dirs=True, weight_norm=True, use_siren=False, precision=None):
         super().__init__()
@@ -269,10 +282,18 @@ class RadianceNet(nn.Module):
         return desc, packed
 
     def forward(self, x, view_dirs, normals, geometry_feature):
-        """base.py:372-391 (render mode)."""
+        """base.py:372-391 (render mode; with a graph when training)."""
         L.require_gpu(x, 'points')
-        _no_training(self)
         shape = x.shape[:-1]
+        if wants_graph(self, normals, geometry_feature):
+            from .training import radiance
+            v = view_dirs.reshape(-1, 3).float()
+            P = x.reshape(-1, 3).shape[0]
+            if v.shape[0] != P:
+                raise ValueError('view_dirs must have one direction per point')
+            rgb = radiance(self, x.reshape(-1, 3).float(), v, normals.reshape(-1, 3).float(),
+                           geometry_feature.reshape(-1, self.W_geo_feat).float())
+            return rgb.reshape(*shape, 3)
         dev = x.device
         xs = x.reshape(-1, 3).float().contiguous()
         P = xs.shape[0]
@@ -340,7 +361,7 @@ class NeRF(nn.Module):
     def forward(self, input_pts, input_views):
         """base.py:426-453 (render mode): returns (sigma [...], rgb [..., 3])."""
         L.require_gpu(input_pts, 'points')
-        _no_training(self)
+        _no_training(self, what='the NeRF++ background net')
         shape = input_pts.shape[:-1]
         dev = input_pts.device
         x = input_pts.reshape(-1, 4).float().contiguous()

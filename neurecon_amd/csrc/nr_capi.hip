@@ -170,7 +170,7 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   // the same depths), so one SDF+nabla launch per round replaces the forward-only round launches
   // plus the reference's second pass over all samples (neus.py:294).  sdf rides along the sorted
   // merges (sv); nablas stay in evaluation order (nraw) and are gathered once by neus_points.
-  const bool fused = !direct;
+  const bool fused = !direct && !a.sample_only;  // the sample pass needs no nablas
   c.nraw = fused ? c.nab_f : nullptr;
   c.idv = fused ? (int*)(ws + pl.o_idv) : nullptr;
   if (fused) {
@@ -244,6 +244,12 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
       return rc;
   }
   if (c.n_iters > 0 && (rc = merge(c.S - n_up))) return rc;
+  if (a.sample_only) {  // training: the sorted depths are the whole output (neus.py:279)
+    hipLaunchKernelGGL(neus_write_dall, dim3((unsigned)(((int64_t)c.S * R + 255) / 256)), dim3(256), 0, st, c.dv,
+                       (int64_t)R, c.S, ray0, a.d_all_out);
+    NR_HIP_CHECK(hipGetLastError());
+    return NR_OK;
+  }
   {
     ProfScope prof("neus_points", (double)R, st);
     hipLaunchKernelGGL(neus_expand, dim3((unsigned)(((int64_t)c.S * R + 255) / 256)), dim3(256), 0, st, c);
@@ -703,11 +709,12 @@ int nr_neus_render(const NrNeusArgs* a, void* stream) {
   if (rc) return rc;
   if ((rc = check_rad_desc(a->rad))) return rc;
   // an empty shard (multi-GPU ray sharding) may pass null ray / output pointers
-  NR_REQUIRE(a->n_rays <= 0 || (a->rays_o && a->rays_d && a->rgb && a->depth && a->acc), NR_ERR_ARG,
-             "nr_neus_render: null ray or output pointer");
+  NR_REQUIRE(a->n_rays <= 0 || (a->rays_o && a->rays_d && (a->sample_only ? a->d_all_out != nullptr
+                                                                            : (a->rgb && a->depth && a->acc))),
+             NR_ERR_ARG, "nr_neus_render: null ray or output pointer");
   NR_REQUIRE(a->sdf_packed && a->rad_packed && a->t_coarse, NR_ERR_ARG, "nr_neus_render: null argument");
   NR_REQUIRE(a->N_samples >= 2, NR_ERR_ARG, "nr_neus_render: N_samples must be >= 2");
-  NR_REQUIRE(a->n_rays <= 0 || !a->calc_normal || a->normals, NR_ERR_ARG,
+  NR_REQUIRE(a->n_rays <= 0 || a->sample_only || !a->calc_normal || a->normals, NR_ERR_ARG,
              "nr_neus_render: calc_normal needs normals output");
   NR_REQUIRE(a->N_outside >= 0, NR_ERR_ARG, "nr_neus_render: N_outside must be >= 0");
   if (a->N_outside > 0) {

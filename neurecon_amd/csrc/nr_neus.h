@@ -65,6 +65,7 @@ __global__ void neus_nograd_points(NeusChunk c);
 __global__ void neus_direct_upsample(NeusChunk c, int more, const float* u, int64_t u_stride);
 __global__ void neus_composite_outside(NeusChunk c, NeusOut o, const float* s_dev, float s_val, int calc_normal,
                                        int white_bkgd);
+__global__ void neus_write_dall(const float* dv, int64_t R, int S, int64_t ray0, float* out);
 __global__ void sample_pdf_kernel(const float* bins, const float* weights, int64_t R, int L, const float* u,
                                   int64_t u_stride, int N, float* out);
 

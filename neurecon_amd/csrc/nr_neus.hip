@@ -574,6 +574,14 @@ __global__ __launch_bounds__(64) void neus_composite_outside(NeusChunk c, NeusOu
   }
 }
 
+// sorted sample depths, sample-major [S][R] -> ray-major rows of the output (training sample pass)
+__global__ void neus_write_dall(const float* __restrict__ dv, int64_t R, int S, int64_t ray0, float* __restrict__ out) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (int64_t)S * R) return;
+  const int64_t s = q / R, r = q - s * R;
+  out[(ray0 + r) * S + s] = dv[q];
+}
+
 // ---------------------------------------------------------------------------------------------
 // generic sample_pdf entry (rend_util.py:255-292), bins/weights ray-major [R][L], u [N]
 // ---------------------------------------------------------------------------------------------

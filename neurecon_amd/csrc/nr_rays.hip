@@ -40,3 +40,28 @@ extern "C" int nr_get_rays(const float* c2w, const float* K, int B, int H, int W
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;
 }
+
+namespace nr {
+// training ray batch targets (neus.py:432, :449): out[b, n, :] = src[b, idx[b, n], :] for rows of
+// row_bytes bytes (rgb: 12, mask: 1 or 4), one thread per output byte-word
+__global__ void gather_rows_kernel(const uint8_t* __restrict__ src, int64_t HW, int64_t row_bytes,
+                                   const int64_t* __restrict__ idx, int64_t N, int64_t total, uint8_t* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int64_t row = t / row_bytes, k = t - row * row_bytes;
+  const int64_t b = row / N;
+  out[t] = src[(b * HW + idx[row]) * row_bytes + k];
+}
+}  // namespace nr
+
+extern "C" int nr_gather_rows(const void* src, int64_t B, int64_t HW, int64_t row_bytes, const int64_t* idx,
+                              int64_t N, void* out, void* stream) {
+  NR_REQUIRE(src && idx && out && B >= 0 && HW > 0 && row_bytes > 0 && N >= 0, NR_ERR_ARG,
+             "nr_gather_rows: bad argument");
+  const int64_t total = B * N * row_bytes;
+  if (total <= 0) return NR_OK;
+  hipLaunchKernelGGL(nr::gather_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t*)src, HW, row_bytes, idx, N, total, (uint8_t*)out);
+  NR_HIP_CHECK(hipGetLastError());
+  return NR_OK;
+}

@@ -1,0 +1,468 @@
+// neurecon_amd — training path kernels: the per-point / per-ray arithmetic of
+// the NeuS training step's forward and backward, between the layer GEMMs (plain [P, K] x [K, N]
+// products issued to hipBLASLt by the host).
+//
+// What the reference computes (models/frameworks/neus.py:417-485, models/base.py:265-282): the SDF
+// net's nablas with create_graph=True, so the eikonal loss and the radiance net (which eats the
+// nablas) differentiate THROUGH the input gradient -- a double backward.  The host formulates it as
+// reverse mode over the (primal, tangent) network:
+//   primal   z_l = W_l hin_l + b_l,  h_l = softplus100(z_l),  s_l = softplus100'(z_l)
+//   nabla    g_l = W_{l+1}^T delta_{l+1} (skip-split at layer 4),  delta_l = s_l * g_l,
+//            nabla = J_emb(x)^T (W_0^T delta_0 + skip part)
+//   tangent  hdot_0 = J_emb(x) grad_nabla,  zdot_l = W_l hdot_in_l,  hdot_l = s_l * zdot_l
+//   adjoint  zbar_l = hbar_l * s_l + g_l * zdot_l * s'_l   (s'_l = 100 s_l (1 - s_l), 0 on torch's
+//            linear branch: softplus_double_backward), dW_l = zbar_l^T hin_l + delta_l^T hdot_in_l
+// This file holds every elementwise step of that recipe plus the NeuS compositing forward/backward.
+#include "nr_common.h"
+
+namespace nr {
+namespace {
+
+constexpr int kBlk = 256;
+
+inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + kBlk - 1) / kBlk)); }
+
+// positional encoding feature f of [x, sin(2^0 x), cos(2^0 x), ..., sin(2^{F-1} x), cos(2^{F-1} x)]
+// (models/base.py:14-64; F < 0: identity, 3 features)
+__device__ float emb_f(int f, const float (&x)[3], int nfreq) {
+  if (f < 3) return x[f];
+  const int fp = f - 3, band = fp / 6, m = fp - band * 6, c = m % 3;
+  const float v = fmul(x[c], (float)(1 << band));
+  return m < 3 ? sinf(v) : cosf(v);
+}
+
+__global__ void embed_kernel(const float* __restrict__ x, int64_t P, int nfreq, float* __restrict__ out) {
+  const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P * nf) return;
+  const int64_t p = i / nf;
+  const int f = (int)(i - p * nf);
+  const float xs[3] = {x[p * 3], x[p * 3 + 1], x[p * 3 + 2]};
+  out[i] = emb_f(f, xs, nfreq);
+}
+
+// J_emb(x) v: d/dt embed(x + t v) (the tangent seed of the double backward)
+__global__ void embed_jvp_kernel(const float* __restrict__ x, const float* __restrict__ v, int64_t P, int nfreq,
+                                 float* __restrict__ out) {
+  const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P * nf) return;
+  const int64_t p = i / nf;
+  const int f = (int)(i - p * nf);
+  if (f < 3) {
+    out[i] = v[p * 3 + f];
+    return;
+  }
+  const int fp = f - 3, band = fp / 6, m = fp - band * 6, c = m % 3;
+  const float freq = (float)(1 << band);
+  const float a = fmul(x[p * 3 + c], freq);
+  const float d = m < 3 ? cosf(a) : -sinf(a);
+  out[i] = fmul(fmul(v[p * 3 + c], d), freq);
+}
+
+// J_emb(x)^T (e0 + s1 e1) -> [P, 3] (autograd's Sin/Cos backward then the Mul by the frequency,
+// contributions summed in feature order)
+__global__ void embed_vjp_kernel(const float* __restrict__ x, const float* __restrict__ e0, int ld0,
+                                 const float* __restrict__ e1, int ld1, float s1, int64_t P, int nfreq,
+                                 float* __restrict__ out) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
+  float n[3] = {0.f, 0.f, 0.f};
+  for (int f = 0; f < nf; ++f) {
+    float gf = e0[p * ld0 + f];
+    if (e1) gf = fadd(gf, fmul(e1[p * ld1 + f], s1));
+    if (f < 3) {
+      n[f] = fadd(n[f], gf);
+      continue;
+    }
+    const int fp = f - 3, band = fp / 6, m = fp - band * 6, c = m % 3;
+    const float freq = (float)(1 << band);
+    const float a = fmul(x[p * 3 + c], freq);
+    const float contrib = m < 3 ? fmul(fmul(gf, cosf(a)), freq) : fmul(fmul(gf, -sinf(a)), freq);
+    n[c] = fadd(n[c], contrib);
+  }
+  out[p * 3 + 0] = n[0];
+  out[p * 3 + 1] = n[1];
+  out[p * 3 + 2] = n[2];
+}
+
+// Softplus(beta=100, threshold=20) (base.py:202) and torch's softplus_backward factor
+// e / (e + 1), e = exp(100 z) (1 on the linear branch)
+__global__ void softplus100_kernel(const float* __restrict__ z, int64_t n, float* __restrict__ h,
+                                   float* __restrict__ s) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float zi = z[i];
+  const float t = fmul(zi, 100.0f);
+  if (t > 20.0f) {
+    h[i] = zi;
+    s[i] = 1.0f;
+  } else {
+    const float e = expf(t);
+    h[i] = fdiv(log1pf(e), 100.0f);
+    s[i] = fdiv(e, fadd(e, 1.0f));
+  }
+}
+
+// out[p, j] = a[p, col0 + j] * scale (* s[p, j])
+__global__ void scale_cols_kernel(const float* __restrict__ a, int64_t P, int lda, int col0, int ncols,
+                                  const float* __restrict__ s, float scale, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P * ncols) return;
+  const int64_t p = i / ncols;
+  const int j = (int)(i - p * ncols);
+  float v = a[p * lda + col0 + j];
+  if (scale != 1.0f) v = fmul(v, scale);
+  if (s) v = fmul(v, s[i]);
+  out[i] = v;
+}
+
+// zbar = hbar * s + g * zdot * 100 s (1 - s)   (hbar rows of stride ldh; the rest [P, n] dense)
+__global__ void softplus_adjoint_kernel(const float* __restrict__ hbar, int ldh, const float* __restrict__ s,
+                                        const float* __restrict__ g, const float* __restrict__ zdot, int64_t P, int n,
+                                        float* __restrict__ zbar) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P * n) return;
+  const int64_t p = i / n;
+  const int j = (int)(i - p * n);
+  const float si = s[i];
+  const float d2 = fmul(fmul(si, fsub(1.0f, si)), 100.0f);  // sigmoid_backward * beta; 0 where s == 1
+  float v = fmul(hbar[p * ldh + j], si);
+  if (g) v = fadd(v, fmul(fmul(g[i], zdot[i]), d2));
+  zbar[i] = v;
+}
+
+__global__ void mul_kernel(const float* __restrict__ a, const float* __restrict__ b, int64_t n, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = fmul(a[i], b[i]);
+}
+
+// y = relu(y) in place (mode 0), g *= (y > 0) (mode 1), y = sigmoid(y) in place (mode 2),
+// g *= y (1 - y) (mode 3)
+__global__ void act_kernel(float* __restrict__ y, float* __restrict__ g, int64_t n, int mode) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  switch (mode) {
+    case 0: y[i] = fmaxf(y[i], 0.0f); break;
+    case 1: if (!(y[i] > 0.0f)) g[i] = 0.0f; break;
+    case 2: y[i] = sigmoidf_ref(y[i]); break;
+    default: g[i] = fmul(g[i], fmul(y[i], fsub(1.0f, y[i]))); break;
+  }
+}
+
+// RadianceNet input cat([x, embed_view(v), normals, feature]) (base.py:379-384), one row per point;
+// v is indexed per point
+__global__ void radiance_input_kernel(const float* __restrict__ x, const float* __restrict__ v,
+                                      const float* __restrict__ nrm, const float* __restrict__ feat, int64_t P,
+                                      int nfreq_view, int wfeat, float* __restrict__ out) {
+  const int nv = nfreq_view < 0 ? 3 : 3 + 6 * nfreq_view;
+  const int ld = 3 + nv + 3 + wfeat;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P * ld) return;
+  const int64_t p = i / ld;
+  int f = (int)(i - p * ld);
+  float val;
+  if (f < 3) {
+    val = x[p * 3 + f];
+  } else if ((f -= 3) < nv) {
+    const float vs[3] = {v[p * 3], v[p * 3 + 1], v[p * 3 + 2]};
+    val = emb_f(f, vs, nfreq_view);
+  } else if ((f -= nv) < 3) {
+    val = nrm[p * 3 + f];
+  } else {
+    val = feat[p * wfeat + f - 3];
+  }
+  out[i] = val;
+}
+
+// training sample points (neus.py:284-288): pts = o + d t_s, d_mid = (t_s + t_{s-1}) / 2, pts_mid
+__global__ void neus_points_kernel(const float* __restrict__ ro, const float* __restrict__ rd,
+                                   const float* __restrict__ d_all, int64_t R, int S, float* __restrict__ pts,
+                                   float* __restrict__ mids, float* __restrict__ dmid) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * S) return;
+  const int64_t r = i / S;
+  const int s = (int)(i - r * S);
+  const float t = d_all[i];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) pts[i * 3 + k] = fadd(ro[r * 3 + k], fmul(rd[r * 3 + k], t));
+  if (s + 1 < S) {
+    const int64_t m = r * (S - 1) + s;
+    const float tm = fmul(0.5f, fadd(d_all[i + 1], t));
+    dmid[m] = tm;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) mids[m * 3 + k] = fadd(ro[r * 3 + k], fmul(rd[r * 3 + k], tm));
+  }
+}
+
+// NeuS compositing with a differentiable graph (neus.py:28-70, :346-355), one thread per ray.
+// sdf [R,S], radiance [R,S-1,3], dmid [R,S-1]; s from the device.  fp64 prefix products / sums
+// rounded per element, as in the render kernels.
+__global__ void neus_composite_fwd_kernel(const float* __restrict__ sdf, const float* __restrict__ s_dev,
+                                          const float* __restrict__ rad, const float* __restrict__ dmid, int64_t R,
+                                          int S, int white_bkgd, float* __restrict__ rgb, float* __restrict__ depth,
+                                          float* __restrict__ acc, float* __restrict__ w_out,
+                                          float* __restrict__ alpha_out, float* __restrict__ cdf_out) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const float s = *s_dev;
+  const float* sd = sdf + r * S;
+  double T = 1.0, a_acc = 0.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
+  float cp = sigmoidf_ref(fmul(sd[0], s));
+  if (cdf_out) cdf_out[r * S] = cp;
+  for (int i = 0; i < S - 1; ++i) {
+    const float cn = sigmoidf_ref(fmul(sd[i + 1], s));
+    if (cdf_out) cdf_out[r * S + i + 1] = cn;
+    const float al = fmaxf(fdiv(fsub(cp, cn), fadd(cp, 1e-10f)), 0.0f);
+    const float w = fmul(al, (float)T);
+    T *= (double)fadd(fsub(1.0f, al), 1e-10f);
+    const int64_t q = r * (S - 1) + i;
+    c0 += (double)fmul(w, rad[q * 3 + 0]);
+    c1 += (double)fmul(w, rad[q * 3 + 1]);
+    c2 += (double)fmul(w, rad[q * 3 + 2]);
+    a_acc += (double)w;
+    w_out[q] = w;
+    if (alpha_out) alpha_out[q] = al;
+    cp = cn;
+  }
+  const float accf = (float)a_acc;
+  const float den = fadd(accf, 1e-10f);
+  double dep = 0.0;
+  for (int i = 0; i < S - 1; ++i) dep += (double)fmul(fdiv(w_out[r * (S - 1) + i], den), dmid[r * (S - 1) + i]);
+  float o0 = (float)c0, o1 = (float)c1, o2 = (float)c2;
+  if (white_bkgd) {
+    const float bg = fsub(1.0f, accf);
+    o0 = fadd(o0, bg); o1 = fadd(o1, bg); o2 = fadd(o2, bg);
+  }
+  rgb[r * 3 + 0] = o0;
+  rgb[r * 3 + 1] = o1;
+  rgb[r * 3 + 2] = o2;
+  depth[r] = (float)dep;
+  acc[r] = accf;
+}
+
+// backward of the above: grads of rgb [R,3], depth [R], acc [R] and (optional) the visibility
+// weights [R,S-1] -> d sdf [R,S], d radiance [R,S-1,3], d s per ray [R] (summed by the host).
+// alpha_i = max((c_i - c_{i+1}) / (c_i + 1e-10), 0) (clamp_min passes the gradient where >= 0);
+// T = exclusive cumprod of (1 - alpha + 1e-10) (cumprod_backward: suffix sums / input).
+__global__ void neus_composite_bwd_kernel(const float* __restrict__ sdf, const float* __restrict__ s_dev,
+                                          const float* __restrict__ rad, const float* __restrict__ dmid, int64_t R,
+                                          int S, int white_bkgd, const float* __restrict__ g_rgb,
+                                          const float* __restrict__ g_depth, const float* __restrict__ g_acc,
+                                          const float* __restrict__ g_w, float* __restrict__ work,
+                                          float* __restrict__ d_sdf, float* __restrict__ d_rad,
+                                          float* __restrict__ d_s) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const int S1 = S - 1;
+  const float s = *s_dev;
+  const float* sd = sdf + r * S;
+  // work rows: c [S], alpha [S-1], T [S-1], w [S-1], wbar [S-1]
+  float* c = work + r * (5 * S);
+  float* al = c + S;
+  float* Tt = al + S;
+  float* w = Tt + S;
+  float* wb = w + S;
+  for (int i = 0; i < S; ++i) c[i] = sigmoidf_ref(fmul(sd[i], s));
+  double T = 1.0, a_acc = 0.0, wd = 0.0;
+  for (int i = 0; i < S1; ++i) {
+    const float a = fmaxf(fdiv(fsub(c[i], c[i + 1]), fadd(c[i], 1e-10f)), 0.0f);
+    al[i] = a;
+    Tt[i] = (float)T;
+    w[i] = fmul(a, (float)T);
+    T *= (double)fadd(fsub(1.0f, a), 1e-10f);
+    a_acc += (double)w[i];
+  }
+  const float accf = (float)a_acc;
+  const double A = (double)fadd(accf, 1e-10f);
+  for (int i = 0; i < S1; ++i) wd += (double)w[i] * (double)dmid[r * S1 + i];
+  const float gr0 = g_rgb ? g_rgb[r * 3 + 0] : 0.f, gr1 = g_rgb ? g_rgb[r * 3 + 1] : 0.f,
+              gr2 = g_rgb ? g_rgb[r * 3 + 2] : 0.f;
+  const double gd = g_depth ? (double)g_depth[r] : 0.0;
+  // white_bkgd: rgb += 1 - acc -> acc receives -sum(g_rgb)
+  const double ga = (g_acc ? (double)g_acc[r] : 0.0) - (white_bkgd ? (double)gr0 + gr1 + gr2 : 0.0);
+  for (int i = 0; i < S1; ++i) {
+    const int64_t q = r * S1 + i;
+    double v = (double)gr0 * rad[q * 3 + 0] + (double)gr1 * rad[q * 3 + 1] + (double)gr2 * rad[q * 3 + 2] + ga;
+    v += gd * ((double)dmid[q] / A - wd / (A * A));
+    if (g_w) v += (double)g_w[q];
+    wb[i] = (float)v;
+    d_rad[q * 3 + 0] = fmul(w[i], gr0);
+    d_rad[q * 3 + 1] = fmul(w[i], gr1);
+    d_rad[q * 3 + 2] = fmul(w[i], gr2);
+  }
+  // alpha-bar: w = alpha * T -> alpha gets wbar * T; T_i = prod_{j<i} u_j (u_j = 1 - alpha_j + 1e-10)
+  // -> u_j gets (sum_{k > j} wbar_k alpha_k T_k) / u_j, alpha_j gets minus that
+  double suffix = 0.0;  // sum_{k > i} wbar_k * alpha_k * T_k
+  double sbar = 0.0;
+  for (int i = S - 1; i >= 0; --i) d_sdf[r * S + i] = 0.0f;
+  float cbar_next = 0.0f;  // contribution to c_{i+1} accumulated from alpha_i
+  // walk backwards: alpha_i depends on c_i, c_{i+1}
+  for (int i = S1 - 1; i >= 0; --i) {
+    const double u = (double)fadd(fsub(1.0f, al[i]), 1e-10f);
+    const double abar = (double)wb[i] * Tt[i] - suffix / u;
+    suffix += (double)wb[i] * al[i] * Tt[i];
+    const float num = fsub(c[i], c[i + 1]), den = fadd(c[i], 1e-10f);
+    const bool pass = fdiv(num, den) >= 0.0f;
+    double ci_bar = 0.0, cn_bar = 0.0;
+    if (pass) {
+      ci_bar = abar / den - abar * num / ((double)den * den);
+      cn_bar = -abar / den;
+    }
+    // c_{i+1} collects cn_bar here plus ci_bar from alpha_{i+1} (already in cbar_next)
+    const double cb_next = cn_bar + (double)cbar_next;
+    {
+      const float cc = c[i + 1];
+      const double sg = cb_next * cc * (1.0 - cc);
+      d_sdf[r * S + i + 1] = (float)(sg * s);
+      sbar += sg * sd[i + 1];
+    }
+    cbar_next = (float)ci_bar;
+  }
+  {
+    const float cc = c[0];
+    const double sg = (double)cbar_next * cc * (1.0 - cc);
+    d_sdf[r * S] = (float)(sg * s);
+    sbar += sg * sd[0];
+  }
+  d_s[r] = (float)sbar;
+}
+
+}  // namespace
+}  // namespace nr
+
+using namespace nr;
+
+#define NR_LAUNCH_CHECK() NR_HIP_CHECK(hipGetLastError())
+
+extern "C" {
+
+int nr_embed(const float* x, int64_t P, int nfreq, float* out, void* stream) {
+  NR_REQUIRE(x && out && P >= 0 && nfreq <= 10, NR_ERR_ARG, "nr_embed: bad argument");
+  const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
+  if (P == 0) return NR_OK;
+  hipLaunchKernelGGL(embed_kernel, grid1(P * nf), dim3(kBlk), 0, (hipStream_t)stream, x, P, nfreq, out);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_embed_jvp(const float* x, const float* v, int64_t P, int nfreq, float* out, void* stream) {
+  NR_REQUIRE(x && v && out && P >= 0 && nfreq <= 10, NR_ERR_ARG, "nr_embed_jvp: bad argument");
+  const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
+  if (P == 0) return NR_OK;
+  hipLaunchKernelGGL(embed_jvp_kernel, grid1(P * nf), dim3(kBlk), 0, (hipStream_t)stream, x, v, P, nfreq, out);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_embed_vjp(const float* x, const float* e0, int ld0, const float* e1, int ld1, float s1, int64_t P, int nfreq,
+                 float* out, void* stream) {
+  NR_REQUIRE(x && e0 && out && P >= 0 && nfreq <= 10, NR_ERR_ARG, "nr_embed_vjp: bad argument");
+  if (P == 0) return NR_OK;
+  hipLaunchKernelGGL(embed_vjp_kernel, grid1(P), dim3(kBlk), 0, (hipStream_t)stream, x, e0, ld0, e1, ld1, s1, P,
+                     nfreq, out);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_softplus100(const float* z, int64_t n, float* h, float* s, void* stream) {
+  NR_REQUIRE(z && h && s && n >= 0, NR_ERR_ARG, "nr_softplus100: bad argument");
+  if (n == 0) return NR_OK;
+  hipLaunchKernelGGL(softplus100_kernel, grid1(n), dim3(kBlk), 0, (hipStream_t)stream, z, n, h, s);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_scale_cols(const float* a, int64_t P, int lda, int col0, int ncols, const float* s, float scale, float* out,
+                  void* stream) {
+  NR_REQUIRE(a && out && P >= 0 && col0 >= 0 && ncols >= 0 && col0 + ncols <= lda, NR_ERR_ARG,
+             "nr_scale_cols: bad argument");
+  if (P == 0 || ncols == 0) return NR_OK;
+  hipLaunchKernelGGL(scale_cols_kernel, grid1(P * ncols), dim3(kBlk), 0, (hipStream_t)stream, a, P, lda, col0, ncols,
+                     s, scale, out);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_softplus_adjoint(const float* hbar, int ldh, const float* s, const float* g, const float* zdot, int64_t P,
+                        int n, float* zbar, void* stream) {
+  NR_REQUIRE(hbar && s && zbar && (!g == !zdot) && P >= 0 && n >= 0 && ldh >= n, NR_ERR_ARG,
+             "nr_softplus_adjoint: bad argument");
+  if (P == 0 || n == 0) return NR_OK;
+  hipLaunchKernelGGL(softplus_adjoint_kernel, grid1(P * n), dim3(kBlk), 0, (hipStream_t)stream, hbar, ldh, s, g, zdot,
+                     P, n, zbar);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_mul(const float* a, const float* b, int64_t n, float* out, void* stream) {
+  NR_REQUIRE(a && b && out && n >= 0, NR_ERR_ARG, "nr_mul: bad argument");
+  if (n == 0) return NR_OK;
+  hipLaunchKernelGGL(mul_kernel, grid1(n), dim3(kBlk), 0, (hipStream_t)stream, a, b, n, out);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_activation(float* y, float* g, int64_t n, int mode, void* stream) {
+  NR_REQUIRE(y && n >= 0 && mode >= 0 && mode <= 3 && (mode % 2 == 0 || g), NR_ERR_ARG, "nr_activation: bad argument");
+  if (n == 0) return NR_OK;
+  hipLaunchKernelGGL(act_kernel, grid1(n), dim3(kBlk), 0, (hipStream_t)stream, y, g, n, mode);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_radiance_input(const float* x, const float* v, const float* nrm, const float* feat, int64_t P, int nfreq_view,
+                      int wfeat, float* out, void* stream) {
+  NR_REQUIRE(x && v && nrm && feat && out && P >= 0 && nfreq_view <= 10 && wfeat > 0, NR_ERR_ARG,
+             "nr_radiance_input: bad argument");
+  const int nv = nfreq_view < 0 ? 3 : 3 + 6 * nfreq_view;
+  if (P == 0) return NR_OK;
+  hipLaunchKernelGGL(radiance_input_kernel, grid1(P * (6 + nv + wfeat)), dim3(kBlk), 0, (hipStream_t)stream, x, v,
+                     nrm, feat, P, nfreq_view, wfeat, out);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_neus_points(const float* rays_o, const float* rays_d, const float* d_all, int64_t R, int S, float* pts,
+                   float* mids, float* dmid, void* stream) {
+  NR_REQUIRE(rays_o && rays_d && d_all && pts && mids && dmid && R >= 0 && S >= 2, NR_ERR_ARG,
+             "nr_neus_points: bad argument");
+  if (R == 0) return NR_OK;
+  hipLaunchKernelGGL(neus_points_kernel, grid1(R * S), dim3(kBlk), 0, (hipStream_t)stream, rays_o, rays_d, d_all, R, S,
+                     pts, mids, dmid);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_neus_composite_fwd(const float* sdf, const float* s_dev, const float* rad, const float* dmid, int64_t R, int S,
+                          int white_bkgd, float* rgb, float* depth, float* acc, float* weights, float* alpha,
+                          float* cdf, void* stream) {
+  NR_REQUIRE(sdf && s_dev && rad && dmid && rgb && depth && acc && weights && R >= 0 && S >= 2, NR_ERR_ARG,
+             "nr_neus_composite_fwd: bad argument");
+  if (R == 0) return NR_OK;
+  hipLaunchKernelGGL(neus_composite_fwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream, sdf,
+                     s_dev, rad, dmid, R, S, white_bkgd, rgb, depth, acc, weights, alpha, cdf);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+size_t nr_neus_composite_bwd_workspace_bytes(int64_t R, int S) { return (size_t)R * 5 * S * sizeof(float); }
+
+int nr_neus_composite_bwd(const float* sdf, const float* s_dev, const float* rad, const float* dmid, int64_t R, int S,
+                          int white_bkgd, const float* g_rgb, const float* g_depth, const float* g_acc,
+                          const float* g_weights, float* d_sdf, float* d_rad, float* d_s, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+  NR_REQUIRE(sdf && s_dev && rad && dmid && d_sdf && d_rad && d_s && R >= 0 && S >= 2, NR_ERR_ARG,
+             "nr_neus_composite_bwd: bad argument");
+  if (R == 0) return NR_OK;
+  NR_REQUIRE(workspace && workspace_bytes >= nr_neus_composite_bwd_workspace_bytes(R, S), NR_ERR_WORKSPACE,
+             "nr_neus_composite_bwd: workspace too small");
+  hipLaunchKernelGGL(neus_composite_bwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream, sdf,
+                     s_dev, rad, dmid, R, S, white_bkgd, g_rgb, g_depth, g_acc, g_weights, (float*)workspace, d_sdf,
+                     d_rad, d_s);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+}  // extern "C"

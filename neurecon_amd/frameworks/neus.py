@@ -13,9 +13,10 @@ from collections import OrderedDict
 import numpy as np
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .. import _lib as L
-from ..base import ImplicitSurface, NeRF, RadianceNet, _no_training
+from ..base import ImplicitSurface, NeRF, RadianceNet, _no_training, wants_graph
 from .. import rend_util
 
 
@@ -95,7 +96,14 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     perturb=True draws the reference's uniforms (same generators, shapes and order) and hands them
     to the kernels."""
     L.require_gpu(rays_o, 'rays_o')
-    _no_training(model)
+    if wants_graph(model):
+        return _train_render(rays_o, rays_d, model, obj_bounding_radius=obj_bounding_radius, batched=batched,
+                             calc_normal=calc_normal, use_view_dirs=use_view_dirs, rayschunk=rayschunk,
+                             white_bkgd=white_bkgd, near_bypass=near_bypass, far_bypass=far_bypass,
+                             detailed_output=detailed_output, perturb=perturb, fixed_s_recp=fixed_s_recp,
+                             N_samples=N_samples, N_importance=N_importance, N_outside=N_outside,
+                             upsample_algo=upsample_algo, N_nograd_samples=N_nograd_samples,
+                             N_upsample_iters=N_upsample_iters)
     if upsample_algo not in L.UPSAMPLE:
         raise NotImplementedError(upsample_algo)
     direct = upsample_algo != 'official_solution'
@@ -198,6 +206,106 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     return ret['rgb'], ret['depth_volume'], ret
 
 
+def _sample_depths(ro, rd, model, dev, obj_bounding_radius, batched, B, rayschunk, near_bypass, far_bypass, perturb,
+                   fixed_s_recp, N_samples, N_importance, upsample_algo, N_nograd_samples, N_upsample_iters):
+    """The no-grad upsampling of a training step (neus.py:206-279): sorted sample depths [n, S] from
+    the render kernels' sample pass (forward-only SDF launches, no compositing)."""
+    direct = upsample_algo != 'official_solution'
+    n = ro.shape[0]
+    n_up = N_importance if direct else (N_importance // N_upsample_iters if N_upsample_iters > 0 else 0)
+    S = N_samples + (N_importance if direct else N_upsample_iters * n_up)
+    sdf_desc, sdf_packed = model.implicit_surface.nr_packed(dev)
+    rad_desc, rad_packed = model.radiance_net.nr_packed(dev)
+    d_all = torch.empty(n, S, device=dev)
+    a = L.NrNeusArgs()
+    a.rays_o, a.rays_d, a.n_rays = L.ptr(ro), L.ptr(rd), n
+    a.sdf, a.sdf_packed = ctypes.pointer(sdf_desc), L.ptr(sdf_packed)
+    a.rad, a.rad_packed = ctypes.pointer(rad_desc), L.ptr(rad_packed)
+    a.obj_bounding_radius = float(obj_bounding_radius)
+    a.near_bypass = float('nan') if near_bypass is None else float(near_bypass)
+    a.far_bypass = float('nan') if far_bypass is None else float(far_bypass)
+    a.N_samples, a.N_importance, a.N_upsample_iters = N_samples, N_importance, N_upsample_iters
+    t_coarse = _linspace_table(N_samples, dev)
+    u_fine = _linspace_table(max(n_up, 1), dev)
+    a.t_coarse, a.u_fine = L.ptr(t_coarse), L.ptr(u_fine)
+    a.upsample_algo = L.UPSAMPLE[upsample_algo]
+    a.fixed_s = 1. / fixed_s_recp
+    if upsample_algo == 'direct_more':
+        t_nograd = _linspace_table(N_nograd_samples, dev)
+        a.N_nograd_samples, a.t_nograd = N_nograd_samples, L.ptr(t_nograd)
+    if perturb:
+        u_rand, _ = _neus_uniforms(B, n // B, batched, int(rayschunk), direct, N_upsample_iters, n_up, N_importance,
+                                   0, dev)
+        a.u_rand = L.ptr(u_rand)
+    a.sample_only, a.d_all_out = 1, L.ptr(d_all)
+    lib = L.lib()
+    ws_bytes = lib.nr_neus_workspace_bytes(ctypes.byref(a))
+    ws = L.workspace(dev, ws_bytes)
+    a.workspace, a.workspace_bytes = L.ptr(ws), ws_bytes
+    L.check(lib.nr_neus_render(ctypes.byref(a), L.stream_of(dev)))
+    return d_all
+
+
+def _train_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False, calc_normal=False,
+                  use_view_dirs=True, rayschunk=65536, white_bkgd=False, near_bypass=None, far_bypass=None,
+                  detailed_output=True, perturb=False, fixed_s_recp=1 / 64., N_samples=64, N_importance=64,
+                  N_outside=0, upsample_algo='official_solution', N_nograd_samples=2048, N_upsample_iters=4):
+    """neus.py:118-397 with an autograd graph (training): sample depths from the no-grad sample pass,
+    then SDF + nablas at the samples and mid-points (double-backward capable), the radiance net and
+    the compositing as neurecon_amd.training autograd functions.  Returns the reference's
+    (rgb, depth, extras) with graph-carrying rgb, depth_volume, mask_volume, implicit_nablas,
+    implicit_surface, radiance, visibility_weights."""
+    from .. import training as T
+    if N_outside > 0:
+        raise NotImplementedError('neurecon_amd: training with the NeRF++ background (N_outside > 0) is not native')
+    if not use_view_dirs:
+        raise NotImplementedError('neurecon_amd: use_view_dirs=False not supported')
+    if upsample_algo not in L.UPSAMPLE:
+        raise NotImplementedError(upsample_algo)
+    dev = rays_o.device
+    B = rays_d.shape[0] if batched else 1
+    prefix = [B, -1] if batched else [-1]
+    ro = rays_o.reshape(-1, 3).float().contiguous()
+    rd_raw = rays_d.reshape(-1, 3).float().contiguous()
+    n = ro.shape[0]
+    rd = torch.empty_like(rd_raw)  # F.normalize(rays_d, dim=-1) (neus.py:172)
+    L.check(L.lib().nr_normalize3(L.ptr(rd_raw), n, L.ptr(rd), L.stream_of(dev)))
+    with torch.no_grad():
+        d_all = _sample_depths(ro, rd_raw, model, dev, obj_bounding_radius, batched, B, rayschunk, near_bypass,
+                               far_bypass, perturb, fixed_s_recp, N_samples, N_importance, upsample_algo,
+                               N_nograd_samples, N_upsample_iters)
+    S = d_all.shape[1]
+    pts = torch.empty(n, S, 3, device=dev)
+    mids = torch.empty(n, S - 1, 3, device=dev)
+    dmid = torch.empty(n, S - 1, device=dev)
+    L.check(L.lib().nr_neus_points(L.ptr(ro), L.ptr(rd), L.ptr(d_all), n, S, L.ptr(pts), L.ptr(mids), L.ptr(dmid),
+                                   L.stream_of(dev)))
+    surf = model.implicit_surface
+    sdf, nablas, _ = T.sdf_nablas(surf, pts.reshape(-1, 3), False)            # neus.py:294
+    _, nab_m, feat_m = T.sdf_nablas(surf, mids.reshape(-1, 3), True)           # neus.py:103-106, :298
+    view = rd[:, None, :].expand(n, S - 1, 3).reshape(-1, 3).contiguous()
+    rad = T.radiance(model.radiance_net, mids.reshape(-1, 3), view, nab_m, feat_m)
+    s = model.forward_s().float().reshape(-1)[:1]
+    rgb, depth, acc, w, alpha, cdf = T.NeuSComposite.apply(sdf.reshape(n, S), s, rad.reshape(n, S - 1, 3), dmid,
+                                                          bool(white_bkgd))
+    nablas = nablas.reshape(n, S, 3)
+    ret = OrderedDict([('rgb', rgb.reshape(*prefix, 3)), ('depth_volume', depth.reshape(prefix)),
+                       ('mask_volume', acc.reshape(prefix))])
+    if calc_normal:  # neus.py:364-368
+        nrm = F.normalize(nablas, dim=-1)
+        k = min(w.shape[-1], nrm.shape[-2])
+        ret['normals_volume'] = (nrm[:, :k, :] * w[:, :k, None]).sum(dim=-2).reshape(*prefix, 3)
+    if detailed_output:
+        ret['implicit_nablas'] = nablas.reshape(*prefix, S, 3)
+        ret['implicit_surface'] = sdf.reshape(*prefix, S)
+        ret['radiance'] = rad.reshape(*prefix, S - 1, 3)
+        ret['alpha'] = alpha.reshape(*prefix, S - 1)
+        ret['cdf'] = cdf.reshape(*prefix, S)
+        ret['visibility_weights'] = w.reshape(*prefix, S - 1)
+        ret['d_final'] = dmid.reshape(*prefix, S - 1)
+    return ret['rgb'], ret['depth_volume'], ret
+
+
 class SingleRenderer(nn.Module):
     """neus.py:399-405 -- an nn.Module so nn.DataParallel can scatter rays over dim 1."""
 
@@ -210,8 +318,10 @@ class SingleRenderer(nn.Module):
 
 
 class Trainer(nn.Module):
-    """neus.py:408-485.  The training step needs the backward of the render kernels (next milestone,
-    SURVEY.md §8f); forward() therefore raises from the render call while grad is enabled."""
+    """neus.py:408-485: one training step's forward -- random rays of the image, the render with a
+    graph (training autograd functions on libnrhip.so), L1 rgb + eikonal + BCE mask losses.  Returns
+    OrderedDict(losses=..., extras=...) exactly like the reference; train.py calls backward() on
+    losses['total'] (under DDP the gradient all-reduce runs over RCCL)."""
 
     def __init__(self, model, device_ids=[0], batched=True):
         super().__init__()
@@ -222,11 +332,45 @@ class Trainer(nn.Module):
         self.device = device_ids[0]
 
     def forward(self, args, indices, model_input, ground_truth, render_kwargs_train, it, device='cuda'):
+        from ..config import as_cfg
+        args = as_cfg(args)
         intrinsics = model_input['intrinsics'].to(device)
         c2w = model_input['c2w'].to(device)
-        rays_o, rays_d, select_inds = rend_util.get_rays(c2w, intrinsics, render_kwargs_train['H'],
-                                                         render_kwargs_train['W'], N_rays=args.data.N_rays)
-        return self.renderer(rays_o, rays_d, detailed_output=True, **render_kwargs_train)
+        H, W = render_kwargs_train['H'], render_kwargs_train['W']
+        rays_o, rays_d, select_inds = rend_util.get_rays(c2w, intrinsics, H, W, N_rays=args.data.N_rays)
+        # [B, N_rays, 3] (neus.py:432)
+        target_rgb = rend_util.gather_rays(ground_truth['rgb'].to(device), select_inds)
+        mask_ignore = rend_util.gather_rays(model_input['mask_ignore'].to(device), select_inds) \
+            if 'mask_ignore' in model_input else None
+        rgb, depth_v, extras = self.renderer(rays_o, rays_d, detailed_output=True, **render_kwargs_train)
+        nablas = extras['implicit_nablas']
+        nablas_norm = torch.norm(nablas, dim=-1)
+        mask_volume = torch.clamp(extras['mask_volume'], 1e-3, 1 - 1e-3)
+        extras['mask_volume_clipped'] = mask_volume
+        losses = OrderedDict()
+        losses['loss_img'] = F.l1_loss(rgb, target_rgb, reduction='none')
+        losses['loss_eikonal'] = args.training.w_eikonal * F.mse_loss(
+            nablas_norm, nablas_norm.new_ones(nablas_norm.shape), reduction='mean')
+        if args.training.with_mask:
+            target_mask = rend_util.gather_rays(model_input['object_mask'].to(device), select_inds)
+            losses['loss_mask'] = args.training.w_mask * F.binary_cross_entropy(mask_volume, target_mask.float(),
+                                                                                reduction='mean')
+            if mask_ignore is not None:
+                target_mask = torch.logical_and(target_mask, mask_ignore)
+            losses['loss_img'] = (losses['loss_img'] * target_mask[..., None].float()).sum() / \
+                (target_mask.sum() + 1e-10)
+        elif mask_ignore is not None:
+            losses['loss_img'] = (losses['loss_img'] * mask_ignore[..., None].float()).sum() / (mask_ignore.sum() + 1e-10)
+        else:
+            losses['loss_img'] = losses['loss_img'].mean()
+        loss = 0
+        for k, v in losses.items():
+            loss += losses[k]
+        losses['total'] = loss
+        extras['implicit_nablas_norm'] = nablas_norm
+        extras['scalars'] = {'1/s': 1. / self.model.forward_s().data}
+        extras['select_inds'] = select_inds
+        return OrderedDict([('losses', losses), ('extras', extras)])
 
 
 def get_model(args):

@@ -8,9 +8,10 @@ import torch.nn.functional as F
 from . import _lib as L
 
 
-def get_rays(c2w, intrinsics, H, W, N_rays=-1):
+def get_rays(c2w, intrinsics, H, W, N_rays=-1, device_rng=False):
     """rend_util.py:112-164 (pose-matrix form).  Random pixel selection draws
-    randint(H)*W + randint(W) with torch's generator exactly like the reference."""
+    randint(H)*W + randint(W) with torch's CPU generator exactly like the reference (rend_util.py:137-138);
+    device_rng=True draws them on the GPU instead (no host work per step, a different random stream)."""
     L.require_gpu(c2w, 'c2w')
     if c2w.shape[-1] == 7:
         raise NotImplementedError('quaternion camera poses (rend_util.py:114-119) are not supported')
@@ -21,8 +22,9 @@ def get_rays(c2w, intrinsics, H, W, N_rays=-1):
     K = intrinsics.to(dev).reshape(-1, 4, 4).float().expand(B, 4, 4).contiguous()
     if N_rays > 0:
         N_rays = min(N_rays, H * W)
-        hs = torch.randint(0, H, size=[N_rays]).to(dev)
-        ws = torch.randint(0, W, size=[N_rays]).to(dev)
+        gen_dev = dev if device_rng else None
+        hs = torch.randint(0, H, size=[N_rays], device=gen_dev).to(dev)
+        ws = torch.randint(0, W, size=[N_rays], device=gen_dev).to(dev)
         select_inds = (hs * W + ws).expand([*prefix, N_rays])
         sel = select_inds.reshape(B, N_rays).contiguous()
         N = N_rays
@@ -35,6 +37,20 @@ def get_rays(c2w, intrinsics, H, W, N_rays=-1):
     L.check(L.lib().nr_get_rays(L.ptr(m), L.ptr(K), B, H, W, L.ptr(sel), N, L.ptr(ro), L.ptr(rd),
                                 L.stream_of(dev)))
     return ro.reshape(*prefix, N, 3), rd.reshape(*prefix, N, 3), select_inds
+
+
+def gather_rays(src, select_inds):
+    """Targets of a random ray batch: torch.gather(src, 1, select_inds[..., None].expand(...)) on the
+    device (neus.py:432, :449): src [B, H*W, ...] (rgb, masks), select_inds [B, N] -> [B, N, ...]."""
+    L.require_gpu(src, 'src')
+    B, HW = src.shape[0], src.shape[1]
+    idx = select_inds.to(src.device).reshape(B, -1).long().contiguous()
+    N = idx.shape[1]
+    s = src.contiguous()
+    row_bytes = s.element_size() * int(np.prod(s.shape[2:], dtype=np.int64))
+    out = torch.empty(B, N, *s.shape[2:], dtype=s.dtype, device=s.device)
+    L.check(L.lib().nr_gather_rows(L.ptr(s), B, HW, row_bytes, L.ptr(idx), N, L.ptr(out), L.stream_of(s.device)))
+    return out
 
 
 def uniform(shape, device=None):

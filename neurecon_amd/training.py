@@ -1,0 +1,264 @@
+"""Training path of the render hot loop: autograd Functions whose forward and
+backward run on libnrhip.so's training kernels (nr_train.hip) with the dense layer products on
+hipBLASLt (torch.addmm / mm on the ROCm device -- plain library GEMMs, fp32).
+
+What the reference differentiates (models/frameworks/neus.py:284-485, models/base.py:265-282):
+  * ImplicitSurface.forward_with_nablas with create_graph=True: sdf, nablas = d sdf / d x and the
+    geometry feature, where the eikonal loss and the radiance net both consume the nablas -> the
+    parameter gradient needs the DOUBLE backward through the SDF MLP;
+  * RadianceNet on [x, embed_view(v), nablas, feature];
+  * sdf_to_alpha / alpha_to_w / the rgb, depth and mask sums, and s = exp(ln_s * speed_factor).
+`SdfNabla` computes the double backward as reverse mode over the (primal, tangent) network
+(nr_train.hip header): the tangent seed is J_emb(x) * grad_nablas, and since the tangent's adjoint
+equals the nabla chain's own gradients, one tangent sweep and one adjoint sweep give every weight
+gradient: dW_l = zbar_l^T hin_l + delta_l^T hdot_in_l.
+"""
+import ctypes
+import math
+
+import torch
+
+from . import _lib as L
+
+_ISQ2 = 1.0 / math.sqrt(2.0)
+
+
+def _st(t):
+    return L.stream_of(t.device)
+
+
+def _embed(x, nfreq):
+    out = torch.empty(x.shape[0], 3 + 6 * nfreq if nfreq >= 0 else 3, device=x.device)
+    L.check(L.lib().nr_embed(L.ptr(x), x.shape[0], nfreq, L.ptr(out), _st(x)))
+    return out
+
+
+def _softplus(z):
+    h = torch.empty_like(z)
+    s = torch.empty_like(z)
+    L.check(L.lib().nr_softplus100(L.ptr(z), z.numel(), L.ptr(h), L.ptr(s), _st(z)))
+    return h, s
+
+
+def _cols(a, col0, ncols, s=None, scale=1.0):
+    """a[:, col0:col0+ncols] * scale (* s), contiguous"""
+    out = torch.empty(a.shape[0], ncols, device=a.device)
+    L.check(L.lib().nr_scale_cols(L.ptr(a), a.shape[0], a.shape[1], col0, ncols, L.ptr(s), float(scale), L.ptr(out),
+                                  _st(a)))
+    return out
+
+
+def _mul(a, b):
+    out = torch.empty_like(a)
+    L.check(L.lib().nr_mul(L.ptr(a), L.ptr(b), a.numel(), L.ptr(out), _st(a)))
+    return out
+
+
+class SdfNabla(torch.autograd.Function):
+    """ImplicitSurface.forward_with_nablas with a differentiable graph (base.py:265-282,
+    create_graph=True): x [P,3] (no grad) -> sdf [P], nablas [P,3], feature [P,W_geo] (or None).
+    params = W_0..W_D, b_0..b_D (effective weight-normed weights, [out, in])."""
+
+    @staticmethod
+    def forward(ctx, x, cfg, *params):
+        D, skips, nfreq, want_feat = cfg
+        Ws, bs = params[:D + 1], params[D + 1:]
+        x = x.contiguous()
+        h0 = _embed(x, nfreq)
+        hin, ss = [], []
+        h = h0
+        for l in range(D):
+            hi = torch.cat([h, h0], -1).div_(math.sqrt(2)) if l in skips else h  # base.py:250
+            z = torch.addmm(bs[l], hi, Ws[l].t())
+            h, s = _softplus(z)
+            hin.append(hi)
+            ss.append(s)
+        hin.append(h)
+        out = torch.addmm(bs[D], h, Ws[D].t())
+        sdf = out[:, 0].contiguous()
+        feat = out[:, 1:].contiguous() if want_feat else None
+        # nabla chain: g_l = d sdf / d h_l, delta_l = s_l * g_l
+        gs = [None] * D
+        g = Ws[D][0:1, :].expand(h.shape[0], -1)
+        e_skip = None
+        e_first = None
+        for l in range(D - 1, -1, -1):
+            gs[l] = g.contiguous()
+            delta = _mul(ss[l], gs[l])
+            gin = delta @ Ws[l]
+            if l in skips:
+                n_prev = Ws[l - 1].shape[0]
+                e_skip = _cols(gin, n_prev, gin.shape[1] - n_prev, scale=_ISQ2)
+                g = _cols(gin, 0, n_prev, scale=_ISQ2)
+            elif l > 0:
+                g = gin
+            else:
+                e_first = gin.contiguous()
+        nab = torch.empty(x.shape[0], 3, device=x.device)
+        L.check(L.lib().nr_embed_vjp(L.ptr(x), L.ptr(e_first), e_first.shape[1], L.ptr(e_skip),
+                                     0 if e_skip is None else e_skip.shape[1], 1.0, x.shape[0], nfreq, L.ptr(nab),
+                                     _st(x)))
+        ctx.cfg = cfg
+        ctx.save_for_backward(x, *Ws, *hin, *ss, *gs)
+        outs = (sdf, nab, feat) if want_feat else (sdf, nab)
+        return outs
+
+    @staticmethod
+    def backward(ctx, g_sdf, g_nab, *rest):
+        D, skips, nfreq, want_feat = ctx.cfg
+        saved = ctx.saved_tensors
+        x = saved[0]
+        Ws = saved[1:D + 2]
+        hin = saved[D + 2:2 * D + 3]
+        ss = saved[2 * D + 3:3 * D + 3]
+        gs = saved[3 * D + 3:4 * D + 3]
+        g_feat = rest[0] if want_feat else None
+        P = x.shape[0]
+        dev = x.device
+        lib = L.lib()
+        # output-layer adjoint [d sdf, d feature]
+        ob = torch.zeros(P, Ws[D].shape[0], device=dev)
+        if g_sdf is not None:
+            ob[:, 0] = g_sdf
+        if g_feat is not None:
+            ob[:, 1:] = g_feat
+        # tangent sweep (forward mode along grad_nablas): hdot_0 = J_emb(x) g_nab
+        tangent = g_nab is not None
+        zdots, hdins = [None] * D, [None] * (D + 1)
+        if tangent:
+            g_nab = g_nab.contiguous()
+            hd0 = torch.empty(P, 3 + 6 * nfreq if nfreq >= 0 else 3, device=dev)
+            L.check(lib.nr_embed_jvp(L.ptr(x), L.ptr(g_nab), P, nfreq, L.ptr(hd0), _st(x)))
+            hd = hd0
+            for l in range(D):
+                hdi = torch.cat([hd, hd0], -1).div_(math.sqrt(2)) if l in skips else hd
+                zd = hdi @ Ws[l].t()
+                hdins[l], zdots[l] = hdi, zd
+                hd = _mul(ss[l], zd)
+            hdins[D] = hd
+        dW = [None] * (D + 1)
+        db = [None] * (D + 1)
+        dW[D] = ob.t() @ hin[D]
+        db[D] = ob.sum(0)
+        if tangent:  # d(g_nab . nabla) / d W_D[0, :] = sum_p hdot_{D-1}
+            dW[D][0] += hdins[D].sum(0)
+        hbar = ob @ Ws[D]
+        for l in range(D - 1, -1, -1):
+            n = ss[l].shape[1]
+            zbar = torch.empty(P, n, device=dev)
+            L.check(lib.nr_softplus_adjoint(L.ptr(hbar), hbar.shape[1], L.ptr(ss[l]), L.ptr(gs[l] if tangent else None),
+                                            L.ptr(zdots[l]), P, n, L.ptr(zbar), _st(x)))
+            dW[l] = zbar.t() @ hin[l]
+            if tangent:
+                delta = _mul(ss[l], gs[l])  # the tangent's adjoint (= the nabla chain's delta_l)
+                dW[l].addmm_(delta.t(), hdins[l])
+            db[l] = zbar.sum(0)
+            if l > 0:
+                hb = zbar @ Ws[l]
+                hbar = _cols(hb, 0, Ws[l - 1].shape[0], scale=_ISQ2) if l in skips else hb
+        return (None, None, *dW, *db)
+
+
+class RadianceFn(torch.autograd.Function):
+    """RadianceNet.forward with a graph (base.py:372-391): [x, embed_view(v), normals, feature] ->
+    D x (Linear + ReLU) -> Linear(3) + sigmoid.  Gradients flow to normals, feature and the params."""
+
+    @staticmethod
+    def forward(ctx, x, v, nrm, feat, cfg, *params):
+        D, nfreq_view = cfg
+        Ws, bs = params[:D + 1], params[D + 1:]
+        P = x.shape[0]
+        wf = feat.shape[1]
+        nv = 3 if nfreq_view < 0 else 3 + 6 * nfreq_view
+        inp = torch.empty(P, 6 + nv + wf, device=x.device)
+        L.check(L.lib().nr_radiance_input(L.ptr(x), L.ptr(v), L.ptr(nrm), L.ptr(feat), P, nfreq_view, wf, L.ptr(inp),
+                                          _st(x)))
+        hs = [inp]
+        h = inp
+        for l in range(D):
+            h = torch.addmm(bs[l], h, Ws[l].t())
+            L.check(L.lib().nr_activation(L.ptr(h), None, h.numel(), 0, _st(x)))
+            hs.append(h)
+        y = torch.addmm(bs[D], h, Ws[D].t())
+        L.check(L.lib().nr_activation(L.ptr(y), None, y.numel(), 2, _st(x)))
+        ctx.cfg = (D, nv, wf)
+        ctx.save_for_backward(y, *Ws, *hs)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        D, nv, wf = ctx.cfg
+        saved = ctx.saved_tensors
+        y = saved[0]
+        Ws = saved[1:D + 2]
+        hs = saved[D + 2:]
+        g = gy.contiguous().clone()
+        L.check(L.lib().nr_activation(L.ptr(y), L.ptr(g), g.numel(), 3, _st(g)))
+        dW, db = [None] * (D + 1), [None] * (D + 1)
+        for l in range(D, -1, -1):
+            dW[l] = g.t() @ hs[l]
+            db[l] = g.sum(0)
+            g = g @ Ws[l]
+            if l > 0:
+                L.check(L.lib().nr_activation(L.ptr(hs[l]), L.ptr(g), g.numel(), 1, _st(g)))
+        d_nrm = _cols(g, 3 + nv, 3)
+        d_feat = _cols(g, 6 + nv, wf)
+        return (None, None, d_nrm, d_feat, None, *dW, *db)
+
+
+class NeuSComposite(torch.autograd.Function):
+    """sdf_to_alpha / alpha_to_w / rgb, depth, acc sums (neus.py:28-70, :346-355) with a graph:
+    sdf [R,S], s [1], radiance [R,S-1,3], d_mid [R,S-1] (no grad) -> rgb [R,3], depth [R], acc [R],
+    visibility weights [R,S-1] (+ alpha, cdf, not differentiable)."""
+
+    @staticmethod
+    def forward(ctx, sdf, s, rad, dmid, white_bkgd):
+        R, S = sdf.shape
+        dev = sdf.device
+        sdf, rad, dmid, s = sdf.contiguous(), rad.contiguous(), dmid.contiguous(), s.reshape(-1)[:1].contiguous()
+        rgb = torch.empty(R, 3, device=dev)
+        depth = torch.empty(R, device=dev)
+        acc = torch.empty(R, device=dev)
+        w = torch.empty(R, S - 1, device=dev)
+        alpha = torch.empty(R, S - 1, device=dev)
+        cdf = torch.empty(R, S, device=dev)
+        L.check(L.lib().nr_neus_composite_fwd(L.ptr(sdf), L.ptr(s), L.ptr(rad), L.ptr(dmid), R, S, int(white_bkgd),
+                                              L.ptr(rgb), L.ptr(depth), L.ptr(acc), L.ptr(w), L.ptr(alpha), L.ptr(cdf),
+                                              _st(sdf)))
+        ctx.white = int(white_bkgd)
+        ctx.save_for_backward(sdf, s, rad, dmid)
+        ctx.mark_non_differentiable(alpha, cdf)
+        return rgb, depth, acc, w, alpha, cdf
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_depth, g_acc, g_w, _ga, _gc):
+        sdf, s, rad, dmid = ctx.saved_tensors
+        R, S = sdf.shape
+        c = lambda t: None if t is None else t.contiguous()
+        d_sdf = torch.empty_like(sdf)
+        d_rad = torch.empty_like(rad)
+        d_s = torch.empty(R, device=sdf.device)
+        lib = L.lib()
+        wb = lib.nr_neus_composite_bwd_workspace_bytes(R, S)
+        ws = torch.empty(max(wb, 1), dtype=torch.uint8, device=sdf.device)
+        g_rgb, g_depth, g_acc, g_w = c(g_rgb), c(g_depth), c(g_acc), c(g_w)
+        L.check(lib.nr_neus_composite_bwd(L.ptr(sdf), L.ptr(s), L.ptr(rad), L.ptr(dmid), R, S, ctx.white, L.ptr(g_rgb),
+                                          L.ptr(g_depth), L.ptr(g_acc), L.ptr(g_w), L.ptr(d_sdf), L.ptr(d_rad),
+                                          L.ptr(d_s), L.ptr(ws), wb, _st(sdf)))
+        return d_sdf, d_s.sum().reshape(1), d_rad, None, None
+
+
+def sdf_nablas(surface, x, want_feat):
+    """Differentiable (sdf, nablas, feature) of a neurecon_amd ImplicitSurface at points x [P,3]."""
+    Ws = [l.effective_weight() for l in surface.surface_fc_layers]
+    bs = [l.bias for l in surface.surface_fc_layers]
+    cfg = (surface.D, tuple(surface.skips), surface.embed_multires, bool(want_feat))
+    out = SdfNabla.apply(x.reshape(-1, 3).float().contiguous(), cfg, *Ws, *bs)
+    return out if want_feat else (out[0], out[1], None)
+
+
+def radiance(net, x, v, nrm, feat):
+    Ws = [l.effective_weight() for l in net.layers]
+    bs = [l.bias for l in net.layers]
+    return RadianceFn.apply(x.contiguous(), v.contiguous(), nrm.contiguous(), feat.contiguous(),
+                            (net.D, net.embed_multires_view), *Ws, *bs)

@@ -51,6 +51,13 @@ class NeuSOracle:
         d = F.normalize(rays_d.reshape(rays_d.shape[0], -1, 3).float(), dim=-1)
         near, far = R.near_far_from_sphere(o, d, r=obj_bounding_radius)
         view = d
+        d_all = self.sample_depths(o, d, near, far, N_samples, N_importance, upsample_algo, N_upsample_iters,
+                                   N_nograd_samples, fixed_s_recp)
+        return self.integrate(o, d, near, far, d_all, view, obj_bounding_radius, calc_normal, N_outside, white_bkgd)
+
+    def sample_depths(self, o, d, near, far, N_samples=64, N_importance=64, upsample_algo='official_solution',
+                      N_upsample_iters=4, N_nograd_samples=2048, fixed_s_recp=1 / 64.):
+        """the no-grad upsampling (neus.py:206-279) -> sorted sample depths [B, N, S]"""
         pts_of = lambda dv: o.unsqueeze(-2) + dv.unsqueeze(-1) * d.unsqueeze(-2)
         t = torch.linspace(0, 1, N_samples).float()
         d_coarse = near * (1 - t) + far * t                                   # neus.py:209-210
@@ -90,7 +97,11 @@ class NeuSOracle:
                 d_all = dv
             else:
                 raise NotImplementedError(upsample_algo)
+        return d_all
 
+    def integrate(self, o, d, near, far, d_all, view, obj_bounding_radius=1.0, calc_normal=True, N_outside=0,
+                  white_bkgd=False):
+        """neus.py:284-382 from given sample depths"""
         pts = o[..., None, :] + d[..., None, :] * d_all[..., :, None]          # neus.py:284
         d_mid = 0.5 * (d_all[..., 1:] + d_all[..., :-1])                       # neus.py:287
         pts_mid = o[..., None, :] + d[..., None, :] * d_mid[..., :, None]

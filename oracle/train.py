@@ -1,0 +1,57 @@
+"""ORACLE (test infrastructure only): the NeuS training step's forward -- the render with an
+autograd graph and the reference Trainer's losses -- restated from models/frameworks/neus.py:417-485
+(render: :284-355; nablas with create_graph=True: models/base.py:265-282).  Parameters are the leaf
+tensors of a reference-format state_dict; .backward() on the returned total gives the reference's
+parameter gradients (weight_g / weight_v through weight_norm, ln_s through s = exp(ln_s * speed))."""
+import torch
+import torch.nn.functional as F
+
+from . import rays as R
+from .nets import SDFNet, RadianceNet
+from .neus import NeuSOracle, alpha_to_w, sdf_to_alpha
+
+
+def nablas_graph(net, x):
+    """ImplicitSurface.forward_with_nablas with create_graph=True (base.py:265-282)"""
+    x = x.detach().requires_grad_(True)
+    s, h = net.forward(x)
+    g = torch.autograd.grad(s, x, torch.ones_like(s), create_graph=True, retain_graph=True, only_inputs=True)[0]
+    return s, g, h
+
+
+def neus_train_losses(sd, rays_o, rays_d, target_rgb, target_mask, w_eikonal=0.1, w_mask=1.0, with_mask=True,
+                      d_all=None, speed_factor=10.0, obj_bounding_radius=1.0, N_samples=64, N_importance=64,
+                      N_upsample_iters=4):
+    """losses (neus.py:453-478) of one training render of rays [B, N, 3]; d_all [B, N, S] optional
+    (the sorted sample depths; computed with the no-grad upsampling when None)."""
+    o = rays_o.reshape(rays_o.shape[0], -1, 3).float()
+    d = F.normalize(rays_d.reshape(rays_d.shape[0], -1, 3).float(), dim=-1)
+    near, far = R.near_far_from_sphere(o, d, r=obj_bounding_radius)
+    orc = NeuSOracle({k: v.detach() for k, v in sd.items()}, speed_factor=speed_factor)
+    if d_all is None:
+        d_all = orc.sample_depths(o, d, near, far, N_samples, N_importance, 'official_solution', N_upsample_iters)
+    sdf_net = SDFNet(sd)
+    rad_net = RadianceNet(sd, multires_view=4)
+    pts = o[..., None, :] + d[..., None, :] * d_all[..., :, None]          # neus.py:284
+    d_mid = 0.5 * (d_all[..., 1:] + d_all[..., :-1])
+    pts_mid = o[..., None, :] + d[..., None, :] * d_mid[..., :, None]
+    sdf, nablas, _ = nablas_graph(sdf_net, pts)                             # neus.py:294
+    s = torch.exp(sd['ln_s'] * speed_factor)
+    cdf, alpha = sdf_to_alpha(sdf, s)
+    _, n_m, h_m = nablas_graph(sdf_net, pts_mid)                            # neus.py:103-106, :298
+    rad = rad_net.forward(pts_mid, d.unsqueeze(-2).expand_as(pts_mid), n_m, h_m)
+    w = alpha_to_w(alpha)
+    rgb = torch.sum(w[..., None] * rad, -2)
+    acc = torch.sum(w, -1)
+    nablas_norm = torch.norm(nablas, dim=-1)                                # neus.py:453-478
+    mask_volume = torch.clamp(acc, 1e-3, 1 - 1e-3)
+    losses = {'loss_img': F.l1_loss(rgb, target_rgb, reduction='none'),
+              'loss_eikonal': w_eikonal * F.mse_loss(nablas_norm, nablas_norm.new_ones(nablas_norm.shape),
+                                                     reduction='mean')}
+    if with_mask:
+        losses['loss_mask'] = w_mask * F.binary_cross_entropy(mask_volume, target_mask.float(), reduction='mean')
+        losses['loss_img'] = (losses['loss_img'] * target_mask[..., None].float()).sum() / (target_mask.sum() + 1e-10)
+    else:
+        losses['loss_img'] = losses['loss_img'].mean()
+    losses['total'] = sum(losses.values())
+    return losses, d_all

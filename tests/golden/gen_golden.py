@@ -447,13 +447,62 @@ def gen_perturb(R):
          **{f'u{i}': u for i, u in enumerate(rec.draws)})
 
 
+# parameters whose full gradient is stored; the large weight_v tensors keep norm, sum and a fixed
+# sample of 4096 elements (tests/test_oracle_golden.py compares those)
+def _grad_summary(named):
+    out = {}
+    g = torch.Generator().manual_seed(7)
+    for k, p in named:
+        gr = p.grad.detach().reshape(-1).clone()
+        out[f'g_norm/{k}'] = gr.norm()
+        out[f'g_sum/{k}'] = gr.double().sum()
+        if gr.numel() <= 4096:
+            out[f'g_full/{k}'] = gr
+        else:
+            idx = torch.randperm(gr.numel(), generator=g)[:4096]
+            out[f'g_idx/{k}'] = idx
+            out[f'g_val/{k}'] = gr[idx]
+    return out
+
+
+def gen_train(R):
+    """One NeuS training step's losses and parameter gradients (models/frameworks/neus.py:417-485 ->
+    train.py:205 backward) on an 8x8 camera (64 rays, N_rays=-1 so no random pixels), perturb=False,
+    with_mask=True, seeded random targets."""
+    import types as _t
+    sd = wg.neus_state(seed=1)
+    model = _neus_model(R, sd, False)
+    model.train()
+    H = W = 8
+    c2w = wg.look_at_c2w(3.0)[None]
+    K = wg.intrinsics(20.0, H, W)[None]
+    g = torch.Generator().manual_seed(5)
+    target_rgb = torch.rand(1, H * W, 3, generator=g)
+    target_mask = (torch.rand(1, H * W, generator=g) > 0.4)
+    args = _t.SimpleNamespace(data=_t.SimpleNamespace(N_rays=-1),
+                              training=_t.SimpleNamespace(w_eikonal=0.1, w_mask=1.0, with_mask=True))
+    kw = dict(H=H, W=W, upsample_algo='official_solution', N_nograd_samples=2048, N_upsample_iters=4, N_outside=0,
+              obj_bounding_radius=1.0, batched=True, perturb=False, white_bkgd=False)
+    trainer = R.neus.Trainer(model, device_ids=[0], batched=True)
+    ret = trainer.forward(args, None, {'intrinsics': K, 'c2w': c2w, 'object_mask': target_mask},
+                          {'rgb': target_rgb}, kw, 0, device='cpu')
+    losses = {k: torch.mean(v) for k, v in ret['losses'].items()}
+    model.zero_grad()
+    losses['total'].backward()
+    ex = ret['extras']
+    save('neus_train.npz', seed=1, H=H, W=W, f=20.0, dist=3.0, target_rgb=target_rgb, target_mask=target_mask,
+         c2w=c2w, K=K, **{f'loss/{k}': v.detach() for k, v in losses.items()},
+         rgb=ex['rgb'].detach(), mask_volume=ex['mask_volume'].detach(), d_final=ex['d_final'].detach(),
+         **_grad_summary(model.named_parameters()))
+
+
 def main():
     torch.set_num_threads(8)
     R = _import_reference()
     only = sys.argv[1:]
     gens = dict(components=gen_components, sampling=gen_sampling, neus=gen_neus, volsdf=gen_volsdf,
                 unisurf=gen_unisurf, surface=gen_surface,
-                volsdf_nerfpp=gen_volsdf_nerfpp, perturb=gen_perturb)
+                volsdf_nerfpp=gen_volsdf_nerfpp, perturb=gen_perturb, train=gen_train)
     for name, fn in gens.items():
         if not only or name in only:
             fn(R)

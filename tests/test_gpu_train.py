@@ -1,0 +1,290 @@
+"""GPU parity of the training path: the NeuS training step's losses and EVERY
+parameter gradient -- through the double backward of the SDF MLP's nablas -- vs the oracle's
+autograd (oracle/train.py, pinned to the reference's own Trainer.forward + backward by
+tests/test_oracle_golden.py::test_oracle_train_step_vs_golden) and vs that reference golden.
+
+Bar: |grad - ref| <= 1e-4 |ref| + 1e-5 max|ref| per parameter tensor (components near zero of a
+large gradient), losses 1e-5 relative.  The gradient GEMMs run in fp32 (hipBLASLt); the no-grad
+sample pass runs in the model's precision -- the oracle gets the GPU's sample depths so a flipped
+sampling decision cannot masquerade as a gradient error.
+"""
+import os
+import socket
+import types
+
+import numpy as np
+import pytest
+import torch
+
+import weightgen as wg
+from helpers import neus_model, report
+from test_oracle_golden import check_grads, train_grads_oracle
+
+pytestmark = pytest.mark.gpu
+
+RTOL, ATOL_FRAC = 1e-4, 1e-5
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from neurecon_amd import _lib
+    _lib.lib()
+
+
+def _args():
+    return types.SimpleNamespace(data=types.SimpleNamespace(N_rays=-1),
+                                 training=types.SimpleNamespace(w_eikonal=0.1, w_mask=1.0, with_mask=True))
+
+
+def _kw(H, W):
+    return dict(H=H, W=W, upsample_algo='official_solution', N_nograd_samples=2048, N_upsample_iters=4, N_outside=0,
+                obj_bounding_radius=1.0, batched=True, perturb=False, white_bkgd=False)
+
+
+def _gpu_step(g, precision):
+    from neurecon_amd.frameworks.neus import Trainer
+    m = neus_model(wg.neus_state(seed=int(g['seed'])), precision=precision)
+    m.train()
+    H, W = int(g['H']), int(g['W'])
+    T = lambda a: torch.from_numpy(np.asarray(a)).cuda()
+    trainer = Trainer(m, device_ids=[0])
+    ret = trainer.forward(_args(), None, {'intrinsics': T(g['K']), 'c2w': T(g['c2w']),
+                                          'object_mask': T(g['target_mask'])},
+                          {'rgb': T(g['target_rgb'])}, _kw(H, W), 0, device='cuda')
+    losses = {k: torch.mean(v) for k, v in ret['losses'].items()}
+    m.zero_grad()
+    losses['total'].backward()
+    torch.cuda.synchronize()
+    grads = {k: p.grad.detach().cpu() for k, p in m.named_parameters()}
+    return m, losses, grads, ret['extras']
+
+
+def _gpu_sample_depths(m, g):
+    from neurecon_amd import rend_util
+    from neurecon_amd.frameworks.neus import _sample_depths
+    H, W = int(g['H']), int(g['W'])
+    ro, rd, _ = rend_util.get_rays(torch.from_numpy(g['c2w']).cuda(), torch.from_numpy(g['K']).cuda(), H, W)
+    with torch.no_grad():
+        d = _sample_depths(ro.reshape(-1, 3).contiguous(), rd.reshape(-1, 3).contiguous(), m, ro.device, 1.0, True, 1,
+                           65536, None, None, False, 1 / 64., 64, 64, 'official_solution', 2048, 4)
+    return d.reshape(1, H * W, -1).cpu()
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
+def test_neus_train_step_vs_oracle_and_golden(golden, precision):
+    g = golden('neus_train')
+    m, losses, grads, ex = _gpu_step(g, precision)
+    d_all = _gpu_sample_depths(m, g)
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    ref_losses, ref_grads, d_ref = train_grads_oracle(g, d_all=d_all)
+    for k in ('loss_img', 'loss_eikonal', 'loss_mask', 'total'):
+        a, b = float(losses[k]), float(ref_losses[k])
+        print(f'{precision} {k}: gpu {a:.8f} oracle {b:.8f} golden {float(g["loss/" + k]):.8f}')
+        assert abs(a - b) <= 1e-5 * abs(b) + 1e-7
+    worst = check_grads(grads, _as_golden(ref_grads, g), RTOL, ATOL_FRAC)
+    print(f'{precision}: worst gradient error / tensor scale {worst:.3e}')
+    # and straight against the reference's golden when the sample depths agree with its own
+    _, _, d_own = train_grads_oracle(g)
+    if torch.equal(d_own, d_all):
+        check_grads(grads, g, RTOL, ATOL_FRAC)
+        print(f'{precision}: sample depths identical to the reference -> gradients checked against the golden too')
+
+
+def _as_golden(ref_grads, g):
+    """the oracle's full gradients in the golden's summary layout (same sampled indices)"""
+    out = {}
+    for k in g.keys():
+        if not k.startswith('g_norm/'):
+            continue
+        name = k.split('/', 1)[1]
+        gr = ref_grads[name].detach().reshape(-1)
+        out[f'g_norm/{name}'] = np.asarray(float(gr.norm()))
+        if f'g_full/{name}' in g.keys():
+            out[f'g_full/{name}'] = gr.numpy()
+        else:
+            idx = g[f'g_idx/{name}']
+            out[f'g_idx/{name}'] = idx
+            out[f'g_val/{name}'] = gr.numpy()[idx]
+    return out
+
+
+def test_sdf_double_backward_vs_autograd():
+    """SdfNabla on its own: random points (ragged P), random upstream gradients for sdf, nablas and
+    the geometry feature -> every SDF-net parameter gradient vs torch autograd (create_graph) on CPU."""
+    from oracle.nets import SDFNet
+    from oracle.train import nablas_graph
+    from neurecon_amd import training as T
+    sd = wg.neus_state(seed=11)
+    m = neus_model(sd)
+    m.train()
+    torch.manual_seed(3)
+    for P in (1, 130, 2000):
+        x = torch.randn(P, 3) * 0.7
+        gs, gn, gf = torch.randn(P), torch.randn(P, 3), torch.randn(P, 256) * 0.01
+        sdp = {k: v.clone().requires_grad_(True) for k, v in sd.items() if k.startswith('implicit_surface.')
+               and not k.endswith('obj_bounding_size')}
+        s, n, h = nablas_graph(SDFNet(sdp), x)
+        ((s * gs).sum() + (n * gn).sum() + (h * gf).sum()).backward()
+        m.zero_grad()
+        s2, n2, h2 = T.sdf_nablas(m.implicit_surface, x.cuda(), True)
+        assert report(f'train sdf P={P}', s2, s.detach(), 1e-5, 1e-6)[0].all()
+        assert report(f'train nablas P={P}', n2, n.detach(), 1e-4, 1e-5)[0].all()
+        ((s2 * gs.cuda()).sum() + (n2 * gn.cuda()).sum() + (h2 * gf.cuda()).sum()).backward()
+        for k, p in m.implicit_surface.named_parameters():
+            ref = sdp['implicit_surface.' + k].grad
+            got = p.grad.detach().cpu()
+            scale = float(ref.abs().max())
+            ok, _ = report(f'  d {k} P={P}', got, ref, RTOL, ATOL_FRAC * scale)
+            assert ok.all(), k
+
+
+def test_radiance_backward_vs_autograd():
+    from oracle.nets import RadianceNet
+    from neurecon_amd import training as T
+    sd = wg.neus_state(seed=11)
+    m = neus_model(sd)
+    m.train()
+    torch.manual_seed(4)
+    P = 777
+    x, v = torch.randn(P, 3), torch.nn.functional.normalize(torch.randn(P, 3), dim=-1)
+    nrm, feat = torch.randn(P, 3).requires_grad_(True), torch.randn(P, 256).requires_grad_(True)
+    gy = torch.randn(P, 3)
+    rp = {k: t.clone().requires_grad_(True) for k, t in sd.items() if k.startswith('radiance_net.')}
+    net = RadianceNet(rp, multires_view=4)
+    # ReLU's derivative jumps at 0: a pre-activation within rounding of the kink may take either
+    # side on the GPU and the CPU.  Points with such a unit get no upstream gradient (on both sides).
+    from oracle.nets import embed
+    with torch.no_grad():
+        h = torch.cat([x, embed(v, 4), nrm, feat], -1)
+        kink = torch.zeros(P, dtype=torch.bool)
+        for W, b in net.layers[:-1]:
+            z = torch.nn.functional.linear(h, W, b)
+            kink |= (z.abs() < 1e-4).any(-1)
+            h = torch.relu(z)
+    print(f'points next to a ReLU kink (masked): {int(kink.sum())} / {P}')
+    assert kink.float().mean() < 0.05
+    gy[kink] = 0.0
+    y = net.forward(x, v, nrm, feat)
+    (y * gy).sum().backward()
+    nrm2 = nrm.detach().cuda().requires_grad_(True)
+    feat2 = feat.detach().cuda().requires_grad_(True)
+    y2 = T.radiance(m.radiance_net, x.cuda(), v.cuda(), nrm2, feat2)
+    assert report('train radiance', y2, y.detach(), 1e-5, 1e-6)[0].all()
+    (y2 * gy.cuda()).sum().backward()
+    assert report('d normals', nrm2.grad, nrm.grad, RTOL, ATOL_FRAC * float(nrm.grad.abs().max()))[0].all()
+    assert report('d feature', feat2.grad, feat.grad, RTOL, ATOL_FRAC * float(feat.grad.abs().max()))[0].all()
+    for k, p in m.radiance_net.named_parameters():
+        ref = rp['radiance_net.' + k].grad
+        assert report(f'  d {k}', p.grad, ref, RTOL, ATOL_FRAC * float(ref.abs().max()))[0].all(), k
+
+
+@pytest.mark.parametrize('white_bkgd', [False, True])
+def test_neus_composite_backward_vs_autograd(white_bkgd):
+    """NeuSComposite vs autograd through the oracle's sdf_to_alpha / alpha_to_w / sums, with
+    gradients on rgb, depth and acc and on the visibility weights."""
+    from oracle.neus import alpha_to_w, sdf_to_alpha
+    from neurecon_amd import training as T
+    torch.manual_seed(5)
+    R, S = 300, 128
+    sdf = (torch.randn(R, S).cumsum(-1) * 0.05 + 0.3).requires_grad_(True)
+    s = torch.tensor([20.0], requires_grad=True)
+    rad = torch.rand(R, S - 1, 3).requires_grad_(True)
+    dmid = torch.linspace(0.5, 3.0, S - 1).expand(R, S - 1).contiguous()
+    g_rgb, g_d, g_a, g_w = torch.randn(R, 3), torch.randn(R), torch.randn(R), torch.randn(R, S - 1) * 0.1
+    _, alpha = sdf_to_alpha(sdf, s)
+    w = alpha_to_w(alpha)
+    rgb = (w[..., None] * rad).sum(-2)
+    acc = w.sum(-1)
+    depth = (w / (w.sum(-1, keepdim=True) + 1e-10) * dmid).sum(-1)
+    if white_bkgd:
+        rgb = rgb + (1.0 - acc[..., None])
+    ((rgb * g_rgb).sum() + (depth * g_d).sum() + (acc * g_a).sum() + (w * g_w).sum()).backward()
+    sdf2 = sdf.detach().cuda().requires_grad_(True)
+    s2 = s.detach().cuda().requires_grad_(True)
+    rad2 = rad.detach().cuda().requires_grad_(True)
+    rgb2, depth2, acc2, w2, _, _ = T.NeuSComposite.apply(sdf2, s2, rad2, dmid.cuda(), white_bkgd)
+    assert report('composite rgb', rgb2, rgb.detach(), 1e-5, 1e-6)[0].all()
+    assert report('composite depth', depth2, depth.detach(), 1e-5, 1e-6)[0].all()
+    ((rgb2 * g_rgb.cuda()).sum() + (depth2 * g_d.cuda()).sum() + (acc2 * g_a.cuda()).sum() +
+     (w2 * g_w.cuda()).sum()).backward()
+    assert report('d sdf', sdf2.grad, sdf.grad, RTOL, ATOL_FRAC * float(sdf.grad.abs().max()))[0].all()
+    assert report('d radiance', rad2.grad, rad.grad, RTOL, ATOL_FRAC * float(rad.grad.abs().max()))[0].all()
+    assert report('d s', s2.grad, s.grad, RTOL, 0.0)[0].all()
+
+
+# ---------------------------------------------------------------------------------------------
+# DDP: the gradient all-reduce of train.py:124 over two ranks (gloo: both ranks on the one GPU)
+# ---------------------------------------------------------------------------------------------
+def _free_port():
+    so = socket.socket()
+    so.bind(('127.0.0.1', 0))
+    p = so.getsockname()[1]
+    so.close()
+    return p
+
+
+def _ddp_worker(rank, ws, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.join(here, 'golden'), os.path.dirname(here)]
+    import torch.distributed as dist
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=ws)
+    try:
+        from neurecon_amd.frameworks.neus import Trainer
+        g = dict(np.load(os.path.join(here, 'golden', 'neus_train.npz')))
+        T = lambda a: torch.from_numpy(np.asarray(a)).cuda()
+        m = neus_model(wg.neus_state(seed=1))
+        m.train()
+        trainer = DDP(Trainer(m, device_ids=[0]), device_ids=None, find_unused_parameters=False)
+
+        def batch(r):  # per-rank image: the fixture's targets, rolled by rank
+            return ({'intrinsics': T(g['K']), 'c2w': T(g['c2w']), 'object_mask': T(np.roll(g['target_mask'], 7 * r))},
+                    {'rgb': T(np.roll(g['target_rgb'], 11 * r, axis=1))})
+        mi, gt = batch(rank)
+        ret = trainer(_args(), None, mi, gt, _kw(8, 8), 0, device='cuda')
+        ret['losses']['total'].mean().backward()
+        ddp_grads = {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters()}
+        if rank == 0:  # single-process reference: mean of both ranks' gradients
+            ref = {}
+            for r in range(ws):
+                m.zero_grad()
+                mi, gt = batch(r)
+                trainer.module(_args(), None, mi, gt, _kw(8, 8), 0, device='cuda')['losses']['total'].mean().backward()
+                for k, p in m.named_parameters():
+                    ref[k] = ref.get(k, 0) + p.grad.detach().cpu() / ws
+            worst = max(float((ddp_grads[k] - ref[k]).abs().max() / (ref[k].abs().max() + 1e-30)) for k in ref)
+            q.put(('diff', worst))
+        q.put(('done', rank))
+    except Exception:
+        import traceback
+        q.put(('error', traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_gradient_allreduce_world2():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    msgs = []
+    try:
+        while sum(1 for m in msgs if m[0] in ('done', 'error')) < 2:
+            msgs.append(q.get(timeout=240))
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    errs = [m for m in msgs if m[0] == 'error']
+    assert not errs, errs[0][1]
+    worst = [m[1] for m in msgs if m[0] == 'diff'][0]
+    print(f'DDP-averaged vs single-process mean gradient: worst error / scale {worst:.3e}')
+    assert worst <= 1e-5

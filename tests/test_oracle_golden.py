@@ -221,3 +221,49 @@ def test_surface_render_root_finding(golden):
         np.testing.assert_array_equal(msc.numpy(), g['rf2_msc'].astype(bool))
         close(dp, g['rf2_d'], 1e-6, 1e-6)
         close(p, g['rf2_pts'], 1e-6, 1e-6)
+
+
+def train_grads_oracle(g, d_all=None):
+    """oracle/train.py on the neus_train fixture: (losses, {param: grad}, d_all)"""
+    from oracle.train import neus_train_losses
+    sd = {k: v.clone().requires_grad_(v.is_floating_point() and k != 'implicit_surface.obj_bounding_size')
+          for k, v in wg.neus_state(seed=int(g['seed'])).items()}
+    H, W = int(g['H']), int(g['W'])
+    ro, rd, _ = rays.get_rays(T(g['c2w']), T(g['K']), H, W)
+    losses, d_all = neus_train_losses(sd, ro, rd, T(g['target_rgb']), T(g['target_mask']), d_all=d_all)
+    losses['total'].backward()
+    return losses, {k: v.grad for k, v in sd.items() if v.grad is not None}, d_all
+
+
+def check_grads(grads, g, rtol, atol_frac, report=print):
+    """per parameter: full gradient, or (norm, sum, 4096 sampled entries) for the big weight_v tensors;
+    atol = atol_frac * max |grad| of the tensor (components near zero of a large gradient)"""
+    keys = list(g.keys())
+    names = sorted({k.split('/', 1)[1] for k in keys if k.startswith('g_norm/')})
+    worst = 0.0
+    for k in names:
+        gr = grads[k].detach().reshape(-1).double().cpu().numpy()
+        scale = float(np.abs(gr).max()) + 1e-30
+        if f'g_full/{k}' in keys:
+            ref, mine = g[f'g_full/{k}'].astype(np.float64), gr
+        else:
+            ref, mine = g[f'g_val/{k}'].astype(np.float64), gr[g[f'g_idx/{k}']]
+        err = np.abs(mine - ref)
+        ok = err <= rtol * np.abs(ref) + atol_frac * scale
+        rel_norm = abs(np.linalg.norm(gr) - float(g[f'g_norm/{k}'])) / (float(g[f'g_norm/{k}']) + 1e-30)
+        worst = max(worst, float((err / scale).max()))
+        report(f'{k}: max err {err.max():.3e} (scale {scale:.3e}), norm rel {rel_norm:.2e}, pass {ok.mean() * 100:.2f}%')
+        assert ok.all(), k
+        assert rel_norm <= rtol, k
+    return worst
+
+
+def test_oracle_train_step_vs_golden(golden):
+    """the oracle's NeuS training losses and every parameter gradient vs the reference's own
+    Trainer.forward + backward (double backward through the nablas)"""
+    g = golden('neus_train')
+    torch.set_num_threads(8)
+    losses, grads, _ = train_grads_oracle(g)
+    for k in ('loss_img', 'loss_eikonal', 'loss_mask', 'total'):
+        close(losses[k], g[f'loss/{k}'], 1e-5, 1e-7)
+    check_grads(grads, g, 1e-4, 1e-6)
