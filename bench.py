@@ -27,6 +27,7 @@ F16_MFMA_PEAK_TFLOPS = 2500.0     # MI355X dense fp16/bf16 matrix (MI355X_MICROA
 # f16x3 spends 3 fp16 MFMA products (hi*hi + hi*lo + lo*hi) per algorithmic fp32 MAC
 F16X3_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / 3
 MAC_SDF_FWD = 524_544             # SURVEY §8(a) A5 (incl. the 257-row last layer)
+MAC_SDF_FWD_NOFEAT = 459_008      # the same without the 256 geometry-feature rows (sdf row only)
 MAC_SDF_BWD = 459_008             # SURVEY §8(a) A6 (reverse pass for the nablas)
 MAC_RAD = 271_360                 # SURVEY §8(a) A7, NeuS radiance input 289
 # reference algorithm per ray: 128 no-grad SDF + 255 SDF-with-nabla + 127 radiance.
@@ -51,7 +52,11 @@ def parse():
     ap.add_argument('--rays', type=int, default=4096)
     ap.add_argument('--precision', default=os.environ.get('NR_PRECISION', 'f16x3'), choices=['f16x3', 'fp32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-rays', type=int, default=4096)
+    ap.add_argument('--workload', default='b', choices=['b', 'frame_d', 'train'],
+                    help="b: the BASELINE metric (default); frame_d: config (d) full frame sharded over the GPUs; "
+                         "train: NeuS training step")
+    ap.add_argument('--train-rays', type=int, default=512)
+    ap.add_argument('--cpu-rays', type=int, default=1024)
     return ap.parse_args()
 
 
@@ -85,8 +90,24 @@ def render_kwargs():
                 N_samples=64, N_importance=64, N_outside=0, upsample_algo='official_solution', N_upsample_iters=4)
 
 
-def cpu_baseline(n_rays):
-    """Oracle (clean-room CPU restatement, parity-pinned to the reference) timed on the host cores."""
+def host_cpu():
+    """model name and logical CPU count from lscpu (the box's CPU, of which we use `threads`)"""
+    import subprocess
+    info = {}
+    try:
+        for line in subprocess.run(['lscpu'], capture_output=True, text=True, timeout=10).stdout.splitlines():
+            k, _, v = line.partition(':')
+            if k.strip() in ('Model name', 'CPU(s)', 'Socket(s)', 'Core(s) per socket'):
+                info[k.strip()] = v.strip()
+    except Exception:
+        pass
+    return info
+
+
+def cpu_baseline(n_rays, reps=3):
+    """Oracle (clean-room CPU restatement, parity-pinned to the reference) timed on the host cores:
+    warm-up, then the median of `reps` runs over a bounded sample of the config-(b) rays
+    (BASELINE.md §3)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, 'tests', 'golden'))
     from oracle.neus import NeuSOracle
@@ -102,14 +123,20 @@ def cpu_baseline(n_rays):
     if n_rays < 4096:
         idx = torch.linspace(0, 4095, n_rays).round().long()
         ro, rd = ro[:, idx], rd[:, idx]
+    times = []
     with torch.no_grad():
-        orc.render(ro[:, :32], rd[:, :32])  # warm-up
-        t = time.perf_counter()
-        orc.render(ro, rd)
-        dt = time.perf_counter() - t
+        orc.render(ro[:, :64], rd[:, :64])  # warm-up
+        for _ in range(reps):
+            t = time.perf_counter()
+            orc.render(ro, rd)
+            times.append(time.perf_counter() - t)
+    dt = sorted(times)[len(times) // 2]
+    cpu = host_cpu()
     return {'value': round(n_rays / dt, 2), 'unit': 'rays/s', 'cores': threads, 'kind': 'port',
-            'sample': f'{n_rays} of the 4096 config-(b) rays, oracle/neus.py, '
-                      f'torch {torch.__version__} CPU fp32, {threads} threads, {dt:.1f} s'}
+            'host_cpu': cpu,
+            'sample': f'{n_rays} of the 4096 config-(b) rays (evenly spaced), oracle/neus.py, torch {torch.__version__} '
+                      f'CPU fp32, {threads} threads of {cpu.get("CPU(s)", "?")} logical CPUs '
+                      f'({cpu.get("Model name", "?")}), warm-up + median of {reps}: {dt:.2f} s per run'}
 
 
 def eager_gpu_baseline(dev, n_rays, reps=3):
@@ -144,8 +171,9 @@ def eager_gpu_baseline(dev, n_rays, reps=3):
                       f'{dt * 1e3:.1f} ms'}
 
 
-# algorithmic MACs per unit (point) of each library kernel, SURVEY.md §8(a)
-KERNEL_MAC = {'sdf_fwd': MAC_SDF_FWD, 'sdf_feat': MAC_SDF_FWD, 'sdf_nabla': MAC_SDF_FWD + MAC_SDF_BWD,
+# MACs per unit (point) that each library kernel executes (SURVEY.md §8(a) layer shapes): launches
+# without the geometry feature skip its 256 rows of the last layer
+KERNEL_MAC = {'sdf_fwd': MAC_SDF_FWD_NOFEAT, 'sdf_feat': MAC_SDF_FWD, 'sdf_nabla': MAC_SDF_FWD_NOFEAT + MAC_SDF_BWD,
               'sdf_nabla_feat': MAC_SDF_FWD + MAC_SDF_BWD, 'radiance': MAC_RAD}
 
 
@@ -166,7 +194,17 @@ def pmc_traffic(kernel, precision):
 
 
 def roofline(kstats, precision):
-    """Dominant kernel (largest device time): algorithmic FLOPs per launch / mean launch duration."""
+    """Dominant kernel (largest device time): executed FLOPs per launch / mean launch duration, both
+    launch types of the nabla kernel merged (sample launches without the feature rows, the
+    mid-point launch with them), plus each launch type on its own."""
+    peak = FP32_MFMA_PEAK_TFLOPS if precision == 'fp32' else F16X3_PEAK_TFLOPS
+    per_type = {}
+    for name, (n, ms, units) in kstats.items():
+        if name.startswith('sdf_nabla') and n:
+            fl = units * 2.0 * KERNEL_MAC[name]
+            per_type[name] = {'launches': n, 'avg_launch_ms': round(ms / n, 4),
+                              'achieved': round(fl / (ms * 1e-3) / 1e12, 2),
+                              'frac': round(fl / (ms * 1e-3) / 1e12 / peak, 4)}
     # the two sdf_kernel<nabla> launches (samples, mid-points) are one kernel
     merged = {}
     for name, (n, ms, units) in kstats.items():
@@ -180,13 +218,76 @@ def roofline(kstats, precision):
     dom, (n, ms, fl) = max(merged.items(), key=lambda kv: kv[1][1])
     per_launch_ms = ms / n
     achieved = fl / n / (per_launch_ms * 1e-3) / 1e12
-    peak = FP32_MFMA_PEAK_TFLOPS if precision == 'fp32' else F16X3_PEAK_TFLOPS
     traffic, src = pmc_traffic(dom, precision)
     return {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': peak, 'unit': 'TFLOP/s',
             'frac': round(achieved / peak, 4), 'traffic': traffic, 'traffic_unit': 'bytes/launch',
             'traffic_source': src, 'kernel': dom,
             'avg_launch_ms': round(per_launch_ms, 4), 'launches': n,
-            'flop_per_launch': fl / n, 'share_of_device_time': round(ms / total_ms, 4)}
+            'flop_per_launch': fl / n, 'share_of_device_time': round(ms / total_ms, 4),
+            'per_launch_type': per_type}
+
+
+def frame_d_setup(dev, precision):
+    """config (d): NeuS + NeRF++ (N_outside=32), full 800x600 frame of the config-(d) camera (H=600,
+    W=800, f=800, camera at distance 2), rays sharded over the ranks; the frame's maps are
+    all-gathered (RCCL) inside the timed step."""
+    import numpy as np
+    from neurecon_amd import dist as nd, rend_util
+    from neurecon_amd.frameworks.neus import NeuS, volume_render
+    torch.manual_seed(0)
+    surf = dict(use_siren=False, embed_multires=6, radius_init=0.5, geometric_init=True, D=8, W=256, skips=[4],
+                precision=precision)
+    rad = dict(use_siren=False, embed_multires=-1, embed_multires_view=4, use_view_dirs=True, D=4, W=256, skips=[],
+               precision=precision)
+    model = NeuS(variance_init=0.05, speed_factor=10.0, W_geo_feat=256, use_outside_nerf=True, obj_bounding_radius=1.0,
+                 surface_cfg=surf, radiance_cfg=rad).to(dev).eval()
+    H, W, f, dist = 600, 800, 800.0, 2.0
+    cam = np.array([0.0, 0.0, -dist])
+    fwd = -cam / np.linalg.norm(cam)
+    x = np.cross([0.0, -1.0, 0.0], fwd); x /= np.linalg.norm(x)
+    y = np.cross(fwd, x)
+    c2w = np.eye(4); c2w[:3, 0], c2w[:3, 1], c2w[:3, 2], c2w[:3, 3] = x, y, fwd, cam
+    K = np.eye(4); K[0, 0] = K[1, 1] = f; K[0, 2] = W / 2; K[1, 2] = H / 2
+    ro, rd, _ = rend_util.get_rays(torch.tensor(c2w, dtype=torch.float32, device=dev)[None],
+                                   torch.tensor(K, dtype=torch.float32, device=dev)[None], H, W)
+    kw = dict(obj_bounding_radius=1.0, batched=True, calc_normal=True, detailed_output=False, perturb=False,
+              N_samples=64, N_importance=64, N_outside=32, upsample_algo='official_solution', N_upsample_iters=4,
+              rayschunk=4096)
+
+    def step():
+        with torch.no_grad():
+            return nd.render_sharded(volume_render, ro, rd, model, gather=True, **kw)
+    return step, H * W
+
+
+def train_setup(dev, precision, n_rays, world):
+    """NeuS training step (configs/neus.yaml: N_rays=512 per rank, perturb=True, with_mask): random
+    rays of a synthetic 64x64 image, render with the autograd graph (neurecon_amd.training), the
+    reference's losses, backward (DDP gradient all-reduce over RCCL when world > 1), Adam."""
+    import types
+    from neurecon_amd.frameworks.neus import Trainer
+    model = make_model(dev, precision)
+    model.train()
+    trainer = Trainer(model, device_ids=[dev.index or 0])
+    if world > 1:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        trainer = DDP(trainer, device_ids=[dev.index or 0])
+    opt = torch.optim.Adam(model.parameters(), lr=5e-4)
+    c2w, K = camera(dev)
+    g = torch.Generator().manual_seed(1)
+    mi = {'intrinsics': K, 'c2w': c2w, 'object_mask': (torch.rand(1, 4096, generator=g) > 0.5).to(dev)}
+    gt = {'rgb': torch.rand(1, 4096, 3, generator=g).to(dev)}
+    a = types.SimpleNamespace(data=types.SimpleNamespace(N_rays=n_rays),
+                              training=types.SimpleNamespace(w_eikonal=0.1, w_mask=1.0, with_mask=True))
+    kw = dict(H=64, W=64, upsample_algo='official_solution', N_nograd_samples=2048, N_upsample_iters=4, N_outside=0,
+              obj_bounding_radius=1.0, batched=True, perturb=True, white_bkgd=False)
+
+    def step():
+        ret = trainer(a, None, mi, gt, kw, 0, device=dev)
+        opt.zero_grad()
+        ret['losses']['total'].backward()
+        opt.step()
+    return step
 
 
 def main():
@@ -202,18 +303,26 @@ def main():
     dev = torch.device('cuda', local)
     from neurecon_amd import rend_util
     from neurecon_amd.frameworks.neus import volume_render
-    model = make_model(dev, args.precision)
-    c2w, K = camera(dev)
-    ro, rd, _ = rend_util.get_rays(c2w, K, 64, 64)
-    if args.rays != 4096:
-        reps = math.ceil(args.rays / 4096)
-        ro = ro.repeat(1, reps, 1)[:, :args.rays].contiguous()
-        rd = rd.repeat(1, reps, 1)[:, :args.rays].contiguous()
-    kw = render_kwargs()
+    if args.workload == 'frame_d':
+        step, rays_per_step = frame_d_setup(dev, args.precision)   # all ranks together render one frame
+        n_rays = rays_per_step
+    elif args.workload == 'train':
+        step = train_setup(dev, args.precision, args.train_rays, world)
+        n_rays = args.train_rays * world
+    else:
+        model = make_model(dev, args.precision)
+        c2w, K = camera(dev)
+        ro, rd, _ = rend_util.get_rays(c2w, K, 64, 64)
+        if args.rays != 4096:
+            reps = math.ceil(args.rays / 4096)
+            ro = ro.repeat(1, reps, 1)[:, :args.rays].contiguous()
+            rd = rd.repeat(1, reps, 1)[:, :args.rays].contiguous()
+        kw = render_kwargs()
 
-    def step():
-        with torch.no_grad():
-            return volume_render(ro, rd, model, **kw)
+        def step():
+            with torch.no_grad():
+                return volume_render(ro, rd, model, **kw)
+        n_rays = ro.shape[1] * world
 
     for _ in range(args.warmup):
         step()
@@ -237,30 +346,52 @@ def main():
         t = torch.tensor([dt], device=dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         dt = float(t.item())
-    n_rays = ro.shape[1]
-    total_rays = n_rays * args.steps * world
+    total_rays = n_rays * args.steps
     value = total_rays / dt
     if rank == 0:
         ms = dt / args.steps * 1e3
         roof = roofline(kstats, args.precision)
-        out = {
-            'metric': 'rays/sec (4096 rays x 128 samples, 8-layer x256 SDF MLP)',
-            'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None, 'dtype': 'f32' if args.precision == 'fp32' else args.precision,
-            'data': 'synthetic (config-(b) camera rays, seeded geometric-init weights)',
-            'config': {'workload': 'NeuS render, configs/neus.yaml architecture, 64x64 camera = 4096 rays x '
-                                   '(64 coarse + 4x16 upsampled) samples, render mode',
-                       'rays_per_gpu': n_rays, 'samples_per_ray': 128, 'precision': args.precision,
-                       'parallelism': f'ray-sharded x{world}'},
-            'roofline': roof,
-            'step_tflops': round(RAY_FLOP * n_rays / (dt / args.steps) / 1e12, 2),
-        }
-        if not args.no_cpu_baseline and world == 1:
-            out['cpu_baseline'] = cpu_baseline(args.cpu_rays)
-            eg = eager_gpu_baseline(dev, n_rays)
-            eg['speedup'] = round(value / eg['value'], 2)
-            out['cpu_baseline']['eager_gpu_reference'] = eg
+        dtype = 'f32' if args.precision == 'fp32' else args.precision
+        if args.workload == 'frame_d':
+            out = {'metric': 'rays/sec, config (d): NeuS+NeRF++ full 800x600 frame, rays sharded over the GPUs',
+                   'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
+                   'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
+                   'scaling': 'strong', 'vs_baseline': None, 'dtype': dtype,
+                   'data': 'synthetic (config-(d) camera rays, seeded init weights)',
+                   'config': {'workload': 'NeuS + NeRF++ (N_outside 32) render of one 800x600 frame per step, '
+                                          '64 + 4x16 + 32 samples, maps all-gathered in the step',
+                              'rays_per_step': n_rays, 'precision': args.precision,
+                              'parallelism': f'ray-sharded x{world} + all_gather'},
+                   'roofline': roof}
+        elif args.workload == 'train':
+            out = {'metric': 'training rays/sec, NeuS (configs/neus.yaml: 512 rays per GPU, fwd+bwd+Adam)',
+                   'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
+                   'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
+                   'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32 (gradient GEMMs); sampling ' + dtype,
+                   'data': 'synthetic (random 64x64 targets, config-(b) camera, seeded geometric-init weights)',
+                   'config': {'workload': 'NeuS Trainer.forward + backward (double backward through the nablas) + '
+                                          'Adam step', 'rays_per_gpu': args.train_rays, 'samples_per_ray': 128,
+                              'parallelism': f'DDP x{world}' if world > 1 else 'single GPU'},
+                   'roofline': roof}
+        else:
+            out = {
+                'metric': 'rays/sec (4096 rays x 128 samples, 8-layer x256 SDF MLP)',
+                'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
+                'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
+                'vs_baseline': None, 'dtype': dtype,
+                'data': 'synthetic (config-(b) camera rays, seeded geometric-init weights)',
+                'config': {'workload': 'NeuS render, configs/neus.yaml architecture, 64x64 camera = 4096 rays x '
+                                       '(64 coarse + 4x16 upsampled) samples, render mode',
+                           'rays_per_gpu': n_rays // world, 'samples_per_ray': 128, 'precision': args.precision,
+                           'parallelism': f'ray-sharded x{world}'},
+                'roofline': roof,
+                'step_tflops': round(RAY_FLOP * (n_rays // world) / (dt / args.steps) / 1e12, 2),
+            }
+            if not args.no_cpu_baseline and world == 1:
+                out['cpu_baseline'] = cpu_baseline(args.cpu_rays)
+                eg = eager_gpu_baseline(dev, n_rays)
+                eg['speedup'] = round(value / eg['value'], 2)
+                out['cpu_baseline']['eager_gpu_reference'] = eg
         print(json.dumps(out), flush=True)
     if dist:
         tdist.destroy_process_group()

@@ -103,7 +103,14 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
     case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
     case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;  // callers stay <= 15
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
+    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 21: asm volatile("s_waitcnt vmcnt(21)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;  // callers stay <= 22
   }
 }
 
@@ -873,13 +880,17 @@ struct Pend4 {
   }
 };
 
+constexpr int kSlabRing = 3;  // softplus' slabs in LDS: one being read, one landing, one being staged
+
 template <int CBMAX>
 struct WStream4 {
   char* lds;
-  char* slab;  // 2 x kSlab4
+  char* slab;  // kSlabRing x kSlab4
   int cur;     // ring slot of the chunk being computed
-  int es;      // slab slot staged in this chunk's iteration (read in the next one)
+  int es;      // slab slot the next stage_slab() writes
+  int er;      // slab slot the next consumed chunk's epilogue reads
   __device__ __forceinline__ static int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+  __device__ __forceinline__ static int next3(int i) { return i == 2 ? 0 : i + 1; }
   // BYTES/1 KB pieces; every wave issues ceil(pieces/kW4) (a wave past the end repeats the last
   // piece: identical bytes to the same LDS address) so the count is one constant in every wave
   template <int BYTES>
@@ -938,45 +949,57 @@ struct WStream4 {
   __device__ __forceinline__ void start(const char* g0, const char* g1) {
     cur = 0;
     es = 0;
+    er = 0;
     dma<B0>(g0, 0);
     dma<B1>(g1, 1);
     wait_vmcnt(pieces<B1>());
     __syncthreads();
   }
   template <int BYTES>
-  __device__ __forceinline__ void issue(const char* gsrc) { dma<BYTES>(gsrc, (cur + 2) % kRing); }
-  // this wave's softplus' of chunk c (blocks 2c, 2c+1, both columns: 4 KB contiguous) -> slab slot es
-  __device__ __forceinline__ void stage_slab(const float4* e, int c) {
+  __device__ __forceinline__ void issue(const char* gsrc) { dma<BYTES>(gsrc, cur == 0 ? 2 : cur - 1); }
+  // this wave's softplus' slab of chunk c (blocks 2c, 2c+1, both columns: 4 KB contiguous) -> the next
+  // slab slot; one M0 setting, the instruction offset steps global and LDS address together.  Staged
+  // two chunk-iterations before the epilogue that reads it.  Returns the DMA instructions issued.
+  __device__ __forceinline__ int stage_slab(const float4* e, int c) {
+#ifdef NR_EXP_NO_ELOAD  // timing experiment: softplus' slab not read back
+    return 0;
+#endif
     const uint32_t voff = (threadIdx.x & 63) * 16;
     const char* g = (const char*)uniform_ptr(e + 4 * c * 64);
     const uint32_t base =
         __builtin_amdgcn_readfirstlane(lds_u32(slab) + (uint32_t)(es * kSlab4 + wave_id() * 4096));
-#pragma unroll
-    for (int i = 0; i < 4; ++i) glds16m(g + i * 1024, voff, base + i * 1024);
+    asm volatile(
+        "s_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %0, %1\n\t"
+        "global_load_lds_dwordx4 %0, %1 offset:1024\n\t"
+        "global_load_lds_dwordx4 %0, %1 offset:2048\n\t"
+        "global_load_lds_dwordx4 %0, %1 offset:3072"
+        :
+        : "v"(voff), "s"(g), "s"(base)
+        : "memory", "m0");
+    es = next3(es);
+    return 4;
   }
-  // the slab staged in the previous iteration (the chunk whose epilogue runs now)
-  __device__ __forceinline__ const float4* slab_prev() const {
-    uint32_t off = (es ^ 1) * kSlab4 + wave_id() * 4096;
+  // the slab of the chunk whose epilogue runs now (staged two iterations ago)
+  __device__ __forceinline__ const float4* slab_read() const {
+    uint32_t off = er * kSlab4 + wave_id() * 4096;
     asm volatile("" : "+s"(off));
     return (const float4*)(slab + off);
   }
+  __device__ __forceinline__ void slab_consumed() { er = next3(er); }
   __device__ __forceinline__ const float4* buf() const {
     uint32_t off = cur * CBMAX;
     asm volatile("" : "+s"(off));
     return (const float4*)(lds + off);
   }
-  // PEND: the newest chunk's DMA pieces; extra: stores issued after them in this iteration
-  // (vmcnt retires in issue order, so they are simply not waited for)
-  template <int PEND>
-  __device__ __forceinline__ void flip(int extra = 0) {
-    static_assert(PEND + 4 <= 15, "vmcnt switch covers 0..15");
-    if (extra == 4) wait_vmcnt(PEND + 4);
-    else wait_vmcnt(PEND);
+  // n: DMA / store instructions this wave issued in the current iteration (vmcnt retires in issue
+  // order: everything older -- the current-plus-one chunk's weights and slab -- has landed after it)
+  __device__ __forceinline__ void flip(int n) {
+    wait_vmcnt(n);
 #ifndef NR_EXP_NO_BARRIER
     __syncthreads();
 #endif
-    cur = (cur + 1) % kRing;
-    es ^= 1;
+    cur = next3(cur);
   }
 };
 
@@ -1029,8 +1052,13 @@ struct Z4 {
 
 // One GEMM op: out = W · B (+ bias), NBO/2 chunks, fully unrolled; chunk c's epilogue runs in chunk
 // c+1's iteration (after its DMA issue, beside its MFMAs).
-//  pre(c): first thing in chunk c's iteration (slab staging of chunk c for its epilogue)
-template <int KB, int NBO, int NXT_CB, bool AUX, class WS, class Pre, class Epi>
+//  pre(c): issued right after chunk c's weight DMA (slab staging for a later chunk's epilogue);
+//          returns the DMA instructions it issued
+//  TS:     the epilogue wants t = 100 log2(e) z instead of z (forward softplus ops: the bias slot's
+//          floats 96..127 hold bias * 100 log2(e), packed by pack_op_kernel)
+constexpr float kT = 144.269504088896341f;  // 100 log2(e)
+
+template <int KB, int NBO, int NXT_CB, bool AUX, bool TS, class WS, class Pre, class Epi>
 __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const char* nxt, const f16x8 (&bh)[2][12],
                                     const f16x8 (&bl)[2][12], const float (&xinv)[2], Pend4& pd, Pre&& pre,
                                     Epi&& epi, int lane) {
@@ -1041,16 +1069,22 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
   Z4 zq{};
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    pre(c);
     // opaque per chunk: keeps the scheduler from computing every chunk's address up front
     const char* opc = op;
     const char* nxc = nxt;
     asm volatile("" : "+s"(opc), "+s"(nxc));
-    if (c + 2 < NCH) ws.template issue<CB>(opc + (c + 2) * CB);
-    else if (nxc) ws.template issue<NXT_CB>(nxc + (c + 2 - NCH) * NXT_CB);
-    // the previous chunk's stores go out after this chunk's weight DMA: this chunk's flip does not
-    // wait for them (the next one does, two chunk-times after issue)
-    const int nst = pd.flush();
+    int npend = 0;
+    if (c + 2 < NCH) {
+      ws.template issue<CB>(opc + (c + 2) * CB);
+      npend = WS::template pieces<CB>();
+    } else if (nxc) {
+      ws.template issue<NXT_CB>(nxc + (c + 2 - NCH) * NXT_CB);
+      npend = WS::template pieces<NXT_CB>();
+    }
+    npend += pre(c);
+    // the previous chunk's stores go out after this chunk's DMA: this chunk's flip does not wait for
+    // them (the next one does, two chunk-times after issue)
+    npend += pd.flush();
     const float4* A = ws.buf();
     f32x4 acc[2][2] = {};
     // the previous chunk's epilogue, 8 stages spread over this chunk's KB/2 k-steps
@@ -1065,8 +1099,9 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
           if (e * (KB / 2) / 8 == st) epi(c - 1, zq, e);
       }
     });
-    const float wi = A[2 * KB * 64 + 8].x;
-    const float4 b0 = A[2 * KB * 64 + g], b1 = A[2 * KB * 64 + 4 + g];
+    float wi = A[2 * KB * 64 + 8].x;
+    if constexpr (TS) wi *= kT;
+    const float4 b0 = A[2 * KB * 64 + (TS ? 24 : 0) + g], b1 = A[2 * KB * 64 + (TS ? 28 : 4) + g];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const float inv = xinv[q] * wi;
@@ -1077,9 +1112,7 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
       zq.aux[0] = A[2 * KB * 64 + 16 + g];
       zq.aux[1] = A[2 * KB * 64 + 20 + g];
     }
-    if (c + 2 < NCH) ws.template flip<WS::template pieces<CB>()>(nst);
-    else if (nxt) ws.template flip<WS::template pieces<NXT_CB>()>(nst);
-    else ws.template flip<0>(0);
+    ws.flip(npend);
   }
   pd.flush();  // chunk NCH-2's stores, put by its epilogue in the last iteration
 #pragma unroll
@@ -1112,89 +1145,81 @@ __device__ __forceinline__ void pend_chunk(Pend4& pd, float4* base, int first_bl
   pd.put(base, 4, nt);
 }
 
-// forward softplus op: out -> next operand (k-step c of oh/ol), slab <- softplus'.
-// Staged by operation, not by value: each stage applies one step of the softplus to all 16 values
-// of the chunk (2 columns x 2 blocks x 4), so the ~24 VALU a k-step region receives are
-// independent of each other and issue back to back between its MFMAs (a value-by-value chain
-// would stall the single wave on every transcendental's latency).
-//   y = max(log2(1 + 2^t) ln2/100, z), t = min(100 log2(e) z, 126); s = 2^t / (1 + 2^t)
-// equals torch's softplus(beta=100, threshold=20) / softplus_backward up to ~1e-10 relative: on
-// the linear branch (100 z > 20) the log path exceeds z by log1p(e^-100z)/100 < 2e-11, and where
-// the clamp bites (z > 0.873) the max returns z itself; s there is 1 - 2^-126.
+// forward softplus op: out -> next operand (k-step c of oh/ol), slab <- L = log2(1 + 2^t).
+// Staged by operation, not by value: each stage applies one step to all 16 values of the chunk
+// (2 columns x 2 blocks x 4), so the VALU a k-step region receives is independent work that issues
+// between its MFMAs.  Input t = 100 log2(e) z (op4's TS mode), then
+//   L = log2(1 + 2^min(t, 126)),  y = max(L, t) * ln2/100
+// equals torch's softplus(beta=100, threshold=20) up to ~1e-10 relative (on the linear branch,
+// 100 z > 20, L exceeds t by log2(1 + 2^-t) < 3e-9; where the clamp bites (z > 0.873) the max returns
+// t itself).  The backward needs softplus' = sigmoid(100 z) = 1 - 2^-L: the slab stores L and the
+// backward epilogue forms g - g 2^-L with one exp2 + one fma (no reciprocal here: the forward
+// epilogue, which carries the heavier VALU load, issues 2 transcendentals per value instead of 3).
+// The running max tracks max(L, t) >= 0; finish() scales it by ln2/100.
+constexpr float kC = 0.693147180559945309f * 0.01f;  // ln2 / 100
+
 template <bool NABLA>
 struct FwdEpi4 {
   f16x8 (&oh)[2][12];
   f16x8 (&ol)[2][12];
-  const float (&sc)[2];
+  const float (&sc)[2];  // operand scale of y (the split multiplies max(L, t) by sc * ln2/100)
   float4* sl;
   float (&mrun)[2];
   Pend4& pd;
   int lane;
-  float e[16], w[16], y[16];  // value i = (2q + o) * 4 + r: column q, block o, register r
+  float e[16], L[16], m[16];  // value i = (2q + o) * 4 + r: column q, block o, register r
   __device__ __forceinline__ static float zval(const Z4& zz, int i) {
     const float4 v = zz.z[i >> 3][(i >> 2) & 1];
     const int r = i & 3;
     return r == 0 ? v.x : (r == 1 ? v.y : (r == 2 ? v.z : v.w));
   }
   __device__ __forceinline__ void operator()(int c, const Z4& zz, int st) {
-    constexpr float K = 144.269504088896341f, C = 0.693147180559945309f * 0.01f;
     if (st == 0) {
 #pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        const f2v t = f2v{zval(zz, i), zval(zz, i + 1)} * f2v{K, K};
-        e[i] = fminf(t.x, 126.0f);
-        e[i + 1] = fminf(t.y, 126.0f);
-      }
+      for (int i = 0; i < 16; ++i) e[i] = fminf(zval(zz, i), 126.0f);
     } else if (st == 1) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) e[i] = __builtin_amdgcn_exp2f(e[i]);
     } else if (st == 2) {
 #pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        const f2v u = f2v{e[i], e[i + 1]} + f2v{1.0f, 1.0f};
-        w[i] = u.x;
-        w[i + 1] = u.y;
-      }
+      for (int i = 0; i < 16; ++i) e[i] = e[i] + 1.0f;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) y[i] = __builtin_amdgcn_logf(w[i]);
+      for (int i = 0; i < 8; ++i) L[i] = __builtin_amdgcn_logf(e[i]);
     } else if (st == 3) {
-      if constexpr (NABLA) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_rcpf(w[i]);
-      }
+      for (int i = 8; i < 16; ++i) L[i] = __builtin_amdgcn_logf(e[i]);
     } else if (st == 4) {
 #pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        const f2v v = f2v{y[i], y[i + 1]} * f2v{C, C};
-        y[i] = fmaxf(v.x, zval(zz, i));
-        y[i + 1] = fmaxf(v.y, zval(zz, i + 1));
-      }
+      for (int i = 0; i < 16; ++i) m[i] = fmaxf(L[i], zval(zz, i));
     } else if (st == 5) {
-      if constexpr (NABLA) {  // softplus' straight into the pending-store slots ([block][column])
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int i = 8 * q;
+        float r = mrun[q];
+        r = __builtin_fmaxf(r, __builtin_fmaxf(m[i + 0], m[i + 1]));
+        r = __builtin_fmaxf(r, __builtin_fmaxf(m[i + 2], m[i + 3]));
+        r = __builtin_fmaxf(r, __builtin_fmaxf(m[i + 4], m[i + 5]));
+        r = __builtin_fmaxf(r, __builtin_fmaxf(m[i + 6], m[i + 7]));
+        mrun[q] = r;
+      }
+      if constexpr (NABLA) {  // L straight into the pending-store slots ([block][column])
 #pragma unroll
         for (int q = 0; q < 2; ++q)
 #pragma unroll
           for (int o = 0; o < 2; ++o) {
             const int i = (2 * q + o) * 4;
-            const f2v s01 = f2v{e[i], e[i + 1]} * f2v{w[i], w[i + 1]};
-            const f2v s23 = f2v{e[i + 2], e[i + 3]} * f2v{w[i + 2], w[i + 3]};
-            pd.v[2 * o + q] = make_float4(s01.x, s01.y, s23.x, s23.y);
+            pd.v[2 * o + q] = make_float4(L[i], L[i + 1], L[i + 2], L[i + 3]);
           }
       }
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int i = 8 * q;
-        mrun[q] = amax8(mrun[q], make_float4(y[i], y[i + 1], y[i + 2], y[i + 3]),
-                        make_float4(y[i + 4], y[i + 5], y[i + 6], y[i + 7]));
-      }
     } else if (st == 6) {
-      const int q = 0;
-      split8a(make_float4(y[0], y[1], y[2], y[3]), make_float4(y[4], y[5], y[6], y[7]), sc[q], oh[q][c], ol[q][c]);
+      split8a(make_float4(m[0], m[1], m[2], m[3]), make_float4(m[4], m[5], m[6], m[7]), sc[0] * kC, oh[0][c],
+              ol[0][c]);
     } else {
-      const int q = 1;
-      split8a(make_float4(y[8], y[9], y[10], y[11]), make_float4(y[12], y[13], y[14], y[15]), sc[q], oh[q][c],
-              ol[q][c]);
+      split8a(make_float4(m[8], m[9], m[10], m[11]), make_float4(m[12], m[13], m[14], m[15]), sc[1] * kC, oh[1][c],
+              ol[1][c]);
+#ifndef NR_EXP_NO_ESTORE  // timing experiment: softplus' slab not written
       if constexpr (NABLA) pend_chunk(pd, sl, 2 * c, pd.v[0], pd.v[1], pd.v[2], pd.v[3], lane, true);
+#endif
     }
   }
 };
@@ -1255,13 +1280,18 @@ struct BwdEpi4 {
   __device__ __forceinline__ void operator()(int c, const Z4& zz, int st) {
     if (2 * c < NMAIN) {
       const int q = st >> 2, k = st & 3;
-      if (k < 2) {
-        const float4 sv = ws.slab_prev()[(2 * k + q) * 64 + lane];
-        y[q][k] = mul4(zz.z[q][k], sv);
+      if (k < 2) {  // g * softplus'(z) = g - g 2^-L  (FwdEpi4's slab)
+        const float4 Lv = ws.slab_read()[(2 * k + q) * 64 + lane];
+        const float4 gv = zz.z[q][k];
+        y[q][k] = make_float4(__builtin_fmaf(-gv.x, __builtin_amdgcn_exp2f(-Lv.x), gv.x),
+                              __builtin_fmaf(-gv.y, __builtin_amdgcn_exp2f(-Lv.y), gv.y),
+                              __builtin_fmaf(-gv.z, __builtin_amdgcn_exp2f(-Lv.z), gv.z),
+                              __builtin_fmaf(-gv.w, __builtin_amdgcn_exp2f(-Lv.w), gv.w));
       } else if (k == 2) {
         mrun[q] = amax8(mrun[q], y[q][0], y[q][1]);
       } else {
         split8a(y[q][0], y[q][1], sc[q], oh[q][c], ol[q][c]);
+        if (q == 1) ws.slab_consumed();
       }
     } else if (st == 7) {
       pend_chunk(pd, park, park_blk + 2 * c - NMAIN, zz.z[0][0], zz.z[1][0], zz.z[0][1], zz.z[1][1], lane, false);
@@ -1270,7 +1300,7 @@ struct BwdEpi4 {
 };
 
 struct NoPre4 {
-  __device__ __forceinline__ void operator()(int) const {}
+  __device__ __forceinline__ int operator()(int) const { return 0; }
 };
 
 template <bool NABLA, bool FEAT>
@@ -1278,8 +1308,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(kT4, kT4), amdgpu_waves_pe
 void sdf4_kernel(SdfKArgs a) {
   constexpr int CB = chunk_bytes(18);  // largest SDF op chunk (F4: 14 + 4 input blocks)
   constexpr int C16 = chunk_bytes(16), C4 = chunk_bytes(4), C14 = chunk_bytes(14), C18 = chunk_bytes(18);
-  __shared__ __attribute__((aligned(16))) char smem[kRing * CB + (NABLA ? 2 * kSlab4 : 0)];
-  WStream4<CB> ws{smem, NABLA ? smem + kRing * CB : nullptr, 0, 0};
+  __shared__ __attribute__((aligned(16))) char smem[kRing * CB + (NABLA ? kSlabRing * kSlab4 : 0)];
+  static_assert(kRing * CB + kSlabRing * kSlab4 <= 160 * 1024, "LDS budget");
+  WStream4<CB> ws{smem, NABLA ? smem + kRing * CB : nullptr, 0, 0, 0};
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int j = lane & 15, g = lane >> 4;
   const char* W = a.packed;
@@ -1362,10 +1393,12 @@ void sdf4_kernel(SdfKArgs a) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) sc[q] = bound_scale(fmaxf(fmaf(v.y, m_in[q], v.z) + extra, floor_max[q]));
     };
-    auto finish = [&](const float (&sc)[2]) {  // end of an op: its output becomes the next operand
+    // end of an op: its output becomes the next operand; mscale converts the running max to output
+    // units (forward softplus epilogues track max(L, t), i.e. y / (ln2/100))
+    auto finish = [&](const float (&sc)[2], float mscale = 1.0f) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        m_in[q] = max4_groups(mrun[q]);
+        m_in[q] = max4_groups(mrun[q]) * mscale;
         mrun[q] = 0.0f;
         xinv[q] = 1.0f / sc[q];
       }
@@ -1379,26 +1412,26 @@ void sdf4_kernel(SdfKArgs a) {
     {
       float sc[2];
       next_scales(4, kSpSlack, zero2, sc);
-      op4<4, 16, C16, false>(ws, OP(F0), OP(F1), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(0)), lane);
-      finish(sc);
+      op4<4, 16, C16, false, true>(ws, OP(F0), OP(F1), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(0)), lane);
+      finish(sc, kC);
     }
     {
       float sc[2];
       next_scales(16, kSpSlack, zero2, sc);
-      op4<16, 16, C16, false>(ws, OP(F1), OP(F2), Vh, Vl, xinv, pd, nopre, fwd_epi(Uh, Ul, sc, slab(1)), lane);
-      finish(sc);
+      op4<16, 16, C16, false, true>(ws, OP(F1), OP(F2), Vh, Vl, xinv, pd, nopre, fwd_epi(Uh, Ul, sc, slab(1)), lane);
+      finish(sc, kC);
     }
     {
       float sc[2];
       next_scales(16, kSpSlack, zero2, sc);
-      op4<16, 16, C16, false>(ws, OP(F2), OP(F3), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(2)), lane);
-      finish(sc);
+      op4<16, 16, C16, false, true>(ws, OP(F2), OP(F3), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(2)), lane);
+      finish(sc, kC);
     }
     {
       // F3's outputs (h3: 217 rows in 14 blocks) and the embedding form F4's operand: one scale
       float sc[2];
       next_scales(16, kSpSlack, mE, sc);
-      op4<16, 14, C18, false>(ws, OP(F3), OP(F4), Vh, Vl, xinv, pd, nopre, fwd_epi(Uh, Ul, sc, slab(3)), lane);
+      op4<16, 14, C18, false, true>(ws, OP(F3), OP(F4), Vh, Vl, xinv, pd, nopre, fwd_epi(Uh, Ul, sc, slab(3)), lane);
       if constexpr (NABLA) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
@@ -1410,27 +1443,27 @@ void sdf4_kernel(SdfKArgs a) {
       for (int q = 0; q < 2; ++q) {
         split8a(E[q][0], E[q][1], sc[q], Uh[q][7], Ul[q][7]);
         split8a(E[q][2], E[q][3], sc[q], Uh[q][8], Ul[q][8]);
-        mrun[q] = fmaxf(mrun[q], mE[q]);
+        mrun[q] = fmaxf(mrun[q], mE[q] * (1.0f / kC));  // mrun is in max(L, t) units here
       }
-      finish(sc);
+      finish(sc, kC);
     }
     {
       float sc[2];
       next_scales(18, kSpSlack, zero2, sc);
-      op4<18, 16, C16, false>(ws, OP(F4), OP(F5), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(4)), lane);
-      finish(sc);
+      op4<18, 16, C16, false, true>(ws, OP(F4), OP(F5), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(4)), lane);
+      finish(sc, kC);
     }
     {
       float sc[2];
       next_scales(16, kSpSlack, zero2, sc);
-      op4<16, 16, C16, false>(ws, OP(F5), OP(F6), Vh, Vl, xinv, pd, nopre, fwd_epi(Uh, Ul, sc, slab(5)), lane);
-      finish(sc);
+      op4<16, 16, C16, false, true>(ws, OP(F5), OP(F6), Vh, Vl, xinv, pd, nopre, fwd_epi(Uh, Ul, sc, slab(5)), lane);
+      finish(sc, kC);
     }
     {
       float sc[2];
       next_scales(16, kSpSlack, zero2, sc);
-      op4<16, 16, C16, false>(ws, OP(F6), OP(F7), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(6)), lane);
-      finish(sc);
+      op4<16, 16, C16, false, true>(ws, OP(F6), OP(F7), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(6)), lane);
+      finish(sc, kC);
     }
     // F7: softplus, sdf row (aux = W8[0, :]) as a running dot product, d sdf / d z7 parked in slab 7,
     // h7 split for F8 when the geometry feature is wanted
@@ -1441,7 +1474,7 @@ void sdf4_kernel(SdfKArgs a) {
       F7Epi4<NABLA, FEAT> epi{Uh, Ul, sc, slab(7), mrun, sdf_part, pd, lane};
       constexpr int NXT = (NABLA || FEAT) ? C16 : C4;
       const char* n = FEAT ? OP(F8) : (NABLA ? OP(B7) : (has_next ? OP(F0) : nullptr));
-      op4<16, 16, NXT, true>(ws, OP(F7), n, Vh, Vl, xinv, pd, nopre, epi, lane);
+      op4<16, 16, NXT, true, false>(ws, OP(F7), n, Vh, Vl, xinv, pd, nopre, epi, lane);
       finish(sc);
     }
 #pragma unroll
@@ -1471,7 +1504,7 @@ void sdf4_kernel(SdfKArgs a) {
       };
       constexpr int NXT = NABLA ? C16 : C4;
       const char* n = NABLA ? OP(B7) : (has_next ? OP(F0) : nullptr);
-      op4<16, 16, NXT, false>(ws, OP(F8), n, Uh, Ul, xinv, pd, nopre, epi, lane);
+      op4<16, 16, NXT, false, false>(ws, OP(F8), n, Uh, Ul, xinv, pd, nopre, epi, lane);
     }
     if constexpr (NABLA) {
       // ---- reverse pass (autograd.grad of sdf w.r.t. x, base.py:265-282) ------------------------
@@ -1493,21 +1526,25 @@ void sdf4_kernel(SdfKArgs a) {
         xinv[q] = 1.0f / sc;
       }
       float4* park = slab(7);  // embedding gradients [block 8][column 2][lane]: skip layer 0-3, first layer 4-7
-      // backward op: out = Wᵀ G, scaled by softplus'(z) of the layer below (its slab, staged into
-      // LDS in the chunk's own iteration, read by its epilogue in the next); output chunks >=
+      // backward op: out = Wᵀ G, scaled by softplus'(z) of the layer below (its slab, staged into LDS
+      // two chunk-iterations ahead of the epilogue that reads it: chunk c+1's slab goes out right after
+      // chunk c's weight DMA, the next op's chunk 0 during this op's last chunk); output chunks >=
       // NMAIN/2 are embedding gradients, parked in fp32
+      ws.stage_slab(slab(6), 0);  // B7's chunk 0 (consumed in B7's second iteration)
       auto bwd = [&](auto kb_tag, auto nbo_tag, auto nmain_tag, auto nxt_tag, int opi, const char* nxt,
                      f16x8(&ih)[2][12], f16x8(&il)[2][12], f16x8(&oh)[2][12], f16x8(&ol)[2][12], int lcur,
-                     int park_blk) {
+                     int park_blk, int lnext) {
         constexpr int KBo = decltype(kb_tag)::value, NBOo = decltype(nbo_tag)::value;
         constexpr int NMAIN = decltype(nmain_tag)::value, NXC = decltype(nxt_tag)::value;
         float sc[2];
         next_scales(KBo, 0.0f, zero2, sc);
-        auto pre = [&](int c) {
-          if (2 * c < NMAIN) ws.stage_slab(slab(lcur), c);
+        auto pre = [&](int c) -> int {
+          if (2 * (c + 1) < NMAIN) return ws.stage_slab(slab(lcur), c + 1);
+          if (c + 1 == NBOo / 2 && lnext >= 0) return ws.stage_slab(slab(lnext), 0);
+          return 0;
         };
         BwdEpi4<NMAIN, WStream4<CB>> epi{oh, ol, sc, ws, park, park_blk, mrun, pd, lane};
-        op4<KBo, NBOo, NXC, false>(ws, OP(opi), nxt, ih, il, xinv, pd, pre, epi, lane);
+        op4<KBo, NBOo, NXC, false, false>(ws, OP(opi), nxt, ih, il, xinv, pd, pre, epi, lane);
         finish(sc);
       };
       using I0 = std::integral_constant<int, 0>;
@@ -1518,15 +1555,15 @@ void sdf4_kernel(SdfKArgs a) {
       using IC16 = std::integral_constant<int, C16>;
       using IC14 = std::integral_constant<int, C14>;
       using IC4 = std::integral_constant<int, C4>;
-      bwd(I16{}, I16{}, I16{}, IC16{}, B7, OP(B6), Uh, Ul, Vh, Vl, 6, 0);
-      bwd(I16{}, I16{}, I16{}, IC16{}, B6, OP(B5), Vh, Vl, Uh, Ul, 5, 0);
-      bwd(I16{}, I16{}, I16{}, IC16{}, B5, OP(B4), Uh, Ul, Vh, Vl, 4, 0);
+      bwd(I16{}, I16{}, I16{}, IC16{}, B7, OP(B6), Uh, Ul, Vh, Vl, 6, 0, 5);
+      bwd(I16{}, I16{}, I16{}, IC16{}, B6, OP(B5), Vh, Vl, Uh, Ul, 5, 0, 4);
+      bwd(I16{}, I16{}, I16{}, IC16{}, B5, OP(B4), Uh, Ul, Vh, Vl, 4, 0, 3);
       // skip layer: rows 0..216 -> h3 (scaled by softplus'(z3)), rows 217..255 -> embedding
-      bwd(I16{}, I18{}, I14{}, IC14{}, B4, OP(B3), Vh, Vl, Uh, Ul, 3, 0);
-      bwd(I14{}, I16{}, I16{}, IC16{}, B3, OP(B2), Uh, Ul, Vh, Vl, 2, 0);
-      bwd(I16{}, I16{}, I16{}, IC16{}, B2, OP(B1), Vh, Vl, Uh, Ul, 1, 0);
-      bwd(I16{}, I16{}, I16{}, IC16{}, B1, OP(B0), Uh, Ul, Vh, Vl, 0, 0);
-      bwd(I16{}, I4{}, I0{}, IC4{}, B0, has_next ? OP(F0) : nullptr, Vh, Vl, Uh, Ul, 0, 4);
+      bwd(I16{}, I18{}, I14{}, IC14{}, B4, OP(B3), Vh, Vl, Uh, Ul, 3, 0, 2);
+      bwd(I14{}, I16{}, I16{}, IC16{}, B3, OP(B2), Uh, Ul, Vh, Vl, 2, 0, 1);
+      bwd(I16{}, I16{}, I16{}, IC16{}, B2, OP(B1), Vh, Vl, Uh, Ul, 1, 0, 0);
+      bwd(I16{}, I16{}, I16{}, IC16{}, B1, OP(B0), Uh, Ul, Vh, Vl, 0, 0, -1);
+      bwd(I16{}, I4{}, I0{}, IC4{}, B0, has_next ? OP(F0) : nullptr, Vh, Vl, Uh, Ul, 0, 4, -1);
       pd.flush();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // chain rule through the positional encoding (autograd sums both uses of embed(x))
@@ -1833,6 +1870,16 @@ __global__ void pack_op_kernel(PackOp op, uint32_t* __restrict__ dst, int64_t n)
       v = 1.0f / wscale(op);
     } else if ((idx == 33 || idx == 34) && op.bound) {
       v = op.bound[idx - 33];
+    } else if (idx >= 96 && idx < 128 && op.bias) {  // bias * 100 log2(e): op4's TS mode (softplus ops)
+      int ob_loc = 2 * c + (idx - 96) / 16;
+      for (int s = 0; s < 2; ++s) {
+        if (ob_loc < op.out[s].nblk) {
+          const int rl = 16 * ob_loc + (idx & 15);
+          if (rl < op.out[s].nvalid) v = op.bias[op.out[s].off + rl] * 144.269504088896341f;
+          break;
+        }
+        ob_loc -= op.out[s].nblk;
+      }
     } else if (idx >= 64 && idx < 96 && op.aux) {
       int ob_loc = 2 * c + (idx - 64) / 16;
       for (int s = 0; s < 2; ++s) {

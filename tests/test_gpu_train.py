@@ -87,9 +87,9 @@ def test_neus_train_step_vs_oracle_and_golden(golden, precision):
     print(f'{precision}: worst gradient error / tensor scale {worst:.3e}')
     # and straight against the reference's golden when the sample depths agree with its own
     _, _, d_own = train_grads_oracle(g)
-    if torch.equal(d_own, d_all):
+    if torch.allclose(d_own, d_all, rtol=1e-6, atol=1e-6):
         check_grads(grads, g, RTOL, ATOL_FRAC)
-        print(f'{precision}: sample depths identical to the reference -> gradients checked against the golden too')
+        print(f'{precision}: sample depths match the reference (1e-6) -> gradients checked against the golden too')
 
 
 def _as_golden(ref_grads, g):
@@ -161,10 +161,10 @@ def test_radiance_backward_vs_autograd():
         kink = torch.zeros(P, dtype=torch.bool)
         for W, b in net.layers[:-1]:
             z = torch.nn.functional.linear(h, W, b)
-            kink |= (z.abs() < 1e-4).any(-1)
+            kink |= (z.abs() < 2e-5).any(-1)
             h = torch.relu(z)
     print(f'points next to a ReLU kink (masked): {int(kink.sum())} / {P}')
-    assert kink.float().mean() < 0.05
+    assert kink.float().mean() < 0.1
     gy[kink] = 0.0
     y = net.forward(x, v, nrm, feat)
     (y * gy).sum().backward()
