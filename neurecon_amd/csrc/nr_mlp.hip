@@ -1056,7 +1056,13 @@ struct Z4 {
 //          returns the DMA instructions it issued
 //  TS:     the epilogue wants t = 100 log2(e) z instead of z (forward softplus ops: the bias slot's
 //          floats 96..127 hold bias * 100 log2(e), packed by pack_op_kernel)
-constexpr float kT = 144.269504088896341f;  // 100 log2(e)
+// kT ~ 100 log2(e) and kC ~ ln2 / 100 as a float pair whose product is 1 within 2e-10: on softplus'
+// linear branch the value path is t * kC = z * kT * kC, so the correctly rounded constants
+// (product 1 - 4.7e-8) would shrink every positive activation by that factor per layer, a bias that
+// compounds over the network's 8 layers.  kT sits 4.5e-7 relative below 100 log2(e) (softplus' beta
+// moves by that much: <= 3e-9 absolute on its output).  pack_op_kernel packs bias * kT.
+constexpr float kT = 144.26944f;
+constexpr float kC = 0.0069314749f;
 
 template <int KB, int NBO, int NXT_CB, bool AUX, bool TS, class WS, class Pre, class Epi>
 __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const char* nxt, const f16x8 (&bh)[2][12],
@@ -1156,7 +1162,6 @@ __device__ __forceinline__ void pend_chunk(Pend4& pd, float4* base, int first_bl
 // backward epilogue forms g - g 2^-L with one exp2 + one fma (no reciprocal here: the forward
 // epilogue, which carries the heavier VALU load, issues 2 transcendentals per value instead of 3).
 // The running max tracks max(L, t) >= 0; finish() scales it by ln2/100.
-constexpr float kC = 0.693147180559945309f * 0.01f;  // ln2 / 100
 
 template <bool NABLA>
 struct FwdEpi4 {
@@ -1870,12 +1875,12 @@ __global__ void pack_op_kernel(PackOp op, uint32_t* __restrict__ dst, int64_t n)
       v = 1.0f / wscale(op);
     } else if ((idx == 33 || idx == 34) && op.bound) {
       v = op.bound[idx - 33];
-    } else if (idx >= 96 && idx < 128 && op.bias) {  // bias * 100 log2(e): op4's TS mode (softplus ops)
+    } else if (idx >= 96 && idx < 128 && op.bias) {  // bias * kT: op4's TS mode (softplus ops)
       int ob_loc = 2 * c + (idx - 96) / 16;
       for (int s = 0; s < 2; ++s) {
         if (ob_loc < op.out[s].nblk) {
           const int rl = 16 * ob_loc + (idx & 15);
-          if (rl < op.out[s].nvalid) v = op.bias[op.out[s].off + rl] * 144.269504088896341f;
+          if (rl < op.out[s].nvalid) v = op.bias[op.out[s].off + rl] * kT;
           break;
         }
         ob_loc -= op.out[s].nblk;
