@@ -102,8 +102,10 @@ int nr_sdf_forward(const NrSdfDesc* d, const void* packed, const float* pts, int
 
 /* ------------------------------------------------------------------------------------------
  * Radiance MLP (RadianceNet, models/base.py:312-391)
- * input cat([embed(x), embed_view(v), normals, feature]) -> D x (Linear+ReLU, W) -> Linear(3)+Sigmoid.
- * Supported: D=4, W=256, multires=-1 (identity on x), view_multires in {-1..10}, W_geo_feat=256.
+ * input cat([embed(x), embed_view(v), normals, feature]) -> D x (Linear+ReLU, W) -> Linear(3)+Sigmoid;
+ * with no_view_dirs (use_view_dirs=False, base.py:334-338, :383-384) the input is cat([embed(x),
+ * feature]) and view dirs / normals are not read.
+ * Supported: D=4, W=256, multires=-1 (identity on x), view_multires in {-1..7}, W_geo_feat=256.
  * ------------------------------------------------------------------------------------------ */
 typedef struct {
   int D;             /* 4   */
@@ -112,12 +114,13 @@ typedef struct {
   int multires_view; /* 4 (NeuS) or -1 (VolSDF/UNISURF) */
   int W_geo_feat;    /* 256 */
   int precision;
+  int no_view_dirs;  /* 0: use_view_dirs=True (default) */
 } NrRadDesc;
 
 size_t nr_radiance_packed_bytes(const NrRadDesc* d);
 int nr_radiance_pack(const NrRadDesc* d, const float* const* W, const float* const* b, void* packed, void* stream);
 /* x [P,3], view dirs: vdir[(p / vdir_div) * 3 + c] (vdir_div = samples per ray, or 1),
- * normals [P,3], feature [P,W_geo_feat] -> rgb [P,3] */
+ * normals [P,3], feature [P,W_geo_feat] -> rgb [P,3]; vdir / normals may be NULL with no_view_dirs */
 int nr_radiance_forward(const NrRadDesc* d, const void* packed, const float* x, const float* vdir, int64_t vdir_div,
                         const float* normals, const float* feature, int64_t P, float* rgb, void* stream);
 
@@ -252,6 +255,13 @@ typedef struct {
   float beta_plus_k;     /* float32(4 (4 N_samples - 1) log(1 + eps)) */
   float* sigma_bg;       /* [n_rays, N_outside] sigma_out (detailed, NULL to skip) */
   float* radiance_bg;    /* [n_rays, N_outside, 3] radiance_out (detailed) */
+  /* perturb=True (volsdf.py:102 det=not perturb, :460-465), NULL for the deterministic render:
+   * u_rand [n_rays, N_importance]: the uniforms of each ray's final sample_cdf (rend_util.py:302-306),
+   *   each row sorted ascending (sample_cdf is elementwise in u and the fine depths are sorted into
+   *   d_all, volsdf.py:445-446, so a row's order does not reach the outputs);
+   * u_out [n_rays, N_outside]: the NeRF++ radius strata uniforms (volsdf.py:460-465). */
+  const float* u_rand;
+  const float* u_out;
 } NrVolsdfArgs;
 
 size_t nr_volsdf_workspace_bytes(const NrVolsdfArgs* a);
@@ -317,6 +327,9 @@ typedef struct {
   double* window_ss;
   int (*window_reduce)(void* user);
   void* window_user;
+  /* root finding method (unisurf.py:76 `method`, ray_casting.py:128): 0 = 'secant'; any other method
+   * skips the secant refinement and reports depth 1 on hits, as the reference does */
+  int no_secant;
 } NrUnisurfArgs;
 
 size_t nr_unisurf_workspace_bytes(const NrUnisurfArgs* a);
@@ -347,8 +360,9 @@ int nr_gather_rows(const void* src, int64_t B, int64_t HW, int64_t row_bytes, co
 /* ------------------------------------------------------------------------------------------
  * Surface rendering (models/ray_casting.py:163-263).
  * nr_sphere_trace replaces `sphere_tracing_surface_points` (ray_casting.py:163-182): from d = near,
- * n_iters times d += sdf(o + d*dir) on rays still inside [0, far]; rays_d as given (surface_render
- * normalizes first, ray_casting.py:209).  Outputs d_pred [R], pts [R,3] (= o + d*dir), mask [R]
+ * n_iters times d += sdf(o + d*dir) on rays still inside [0, far]; near / far scalars, or per-ray [R]
+ * device arrays near_rays / far_rays when non-null (the reference broadcasts tensor near/far,
+ * :175, :180); rays_d as given (surface_render normalizes first, ray_casting.py:209).  Outputs d_pred [R], pts [R,3] (= o + d*dir), mask [R]
  * (u8).  Only still-active rays are evaluated (compacted on device).  Workspace:
  * nr_sphere_trace_workspace_bytes(R).
  * nr_normalize3: F.normalize(v, dim=-1) of [n,3] (ray_casting.py:209).
@@ -357,19 +371,23 @@ int nr_gather_rows(const void* src, int64_t B, int64_t HW, int64_t row_bytes, co
  * ------------------------------------------------------------------------------------------ */
 size_t nr_sphere_trace_workspace_bytes(int64_t n_rays);
 int nr_sphere_trace(const NrSdfDesc* d, const void* packed, const float* rays_o, const float* rays_d, int64_t n_rays,
-                    float near, float far, int n_iters, float* d_pred, float* pts, uint8_t* mask, void* workspace,
-                    size_t workspace_bytes, void* stream);
-/* nr_root_find replaces `root_finding_surface_points` (ray_casting.py:35-160) with scalar near/far:
- * N_steps march samples at near*(1-t)+far*t (t_march = torch.linspace(0,1,N_steps), CPU values),
- * first sign change of sdf - logit_tau, N_secant_steps secant refinements on rays entering the
- * surface from outside with a free first sample.  Outputs d_pred [R] (inf if fill_inf, else far, on
- * misses; 0 when the first sample is occupied), pts [R,3] (1 on misses), mask [R], mask_sign_change
- * [R] (u8, optional).  rays_d as given (already normalised).  Workspace: nr_root_find_workspace_bytes. */
+                    float near, float far, const float* near_rays, const float* far_rays, int n_iters, float* d_pred,
+                    float* pts, uint8_t* mask, void* workspace, size_t workspace_bytes, void* stream);
+/* nr_root_find replaces `root_finding_surface_points` (ray_casting.py:35-160): N_steps march samples
+ * at near*(1-t)+far*t (t_march = torch.linspace(0,1,N_steps), CPU values), first sign change of
+ * sdf - logit_tau, N_secant_steps secant refinements on rays entering the surface from outside with
+ * a free first sample (no_secant != 0: method != 'secant', ray_casting.py:128-135 -- no refinement,
+ * depth 1 on hits).  near / far: scalars, or per-ray [R] device arrays near_rays / far_rays when
+ * non-null (the reference's tensor near/far, :53-54, :70-73).  Outputs d_pred [R] (inf if fill_inf,
+ * else far, on misses; 0 when the first sample is occupied), pts [R,3] (1 on misses), mask [R],
+ * mask_sign_change [R] (u8, optional).  rays_d as given (already normalised).  Workspace:
+ * nr_root_find_workspace_bytes. */
 size_t nr_root_find_workspace_bytes(int64_t n_rays, int N_steps);
 int nr_root_find(const NrSdfDesc* d, const void* packed, const float* rays_o, const float* rays_d, int64_t n_rays,
-                 float near, float far, int N_steps, const float* t_march, int N_secant_steps, float logit_tau,
-                 int fill_inf, float* d_pred, float* pts, uint8_t* mask, uint8_t* mask_sign_change,
-                 void* workspace, size_t workspace_bytes, void* stream);
+                 float near, float far, const float* near_rays, const float* far_rays, int N_steps,
+                 const float* t_march, int N_secant_steps, int no_secant, float logit_tau, int fill_inf, float* d_pred,
+                 float* pts, uint8_t* mask, uint8_t* mask_sign_change, void* workspace, size_t workspace_bytes,
+                 void* stream);
 int nr_normalize3(const float* v, int64_t n, float* out, void* stream);
 int nr_surface_finish(float* rgb, const float* nablas, const uint8_t* mask, int64_t n, float* normals, void* stream);
 
@@ -396,7 +414,8 @@ int nr_sdf_grid(const NrSdfDesc* d, const void* packed, double volume_size, int6
  *   nr_scale_cols     out = a[:, col0:col0+n] * scale (* s)  (skip-connection split, delta = s * g)
  *   nr_softplus_adjoint  zbar = hbar * s + g * zdot * 100 s (1 - s)  (softplus_double_backward)
  *   nr_mul / nr_activation  elementwise product; ReLU / sigmoid forward (in place) and backward
- *   nr_radiance_input cat([x, embed_view(v), normals, feature]) (base.py:379-384)
+ *   nr_radiance_input cat([x, embed_view(v), normals, feature]) (base.py:379-384), or cat([x, feature])
+ *                     when use_view_dirs = 0 (v / nrm unused)
  *   nr_neus_points    pts / d_mid / pts_mid of the sorted sample depths (neus.py:284-288)
  *   nr_neus_composite_fwd/bwd  sdf_to_alpha, alpha_to_w, rgb / depth / acc (neus.py:28-70, 346-355)
  *                      and their gradient w.r.t. sdf, radiance and s (per-ray partials of d s)
@@ -414,7 +433,7 @@ int nr_mul(const float* a, const float* b, int64_t n, float* out, void* stream);
 /* mode 0: y = relu(y); 1: g *= (y > 0); 2: y = sigmoid(y); 3: g *= y (1 - y) */
 int nr_activation(float* y, float* g, int64_t n, int mode, void* stream);
 int nr_radiance_input(const float* x, const float* v, const float* nrm, const float* feat, int64_t P, int nfreq_view,
-                      int wfeat, float* out, void* stream);
+                      int use_view_dirs, int wfeat, float* out, void* stream);
 int nr_neus_points(const float* rays_o, const float* rays_d, const float* d_all, int64_t R, int S, float* pts,
                    float* mids, float* dmid, void* stream);
 int nr_neus_composite_fwd(const float* sdf, const float* s_dev, const float* rad, const float* dmid, int64_t R, int S,

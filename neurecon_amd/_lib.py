@@ -30,7 +30,7 @@ class NrSdfDesc(ctypes.Structure):
 
 class NrRadDesc(ctypes.Structure):
     _fields_ = [('D', _c_i), ('W', _c_i), ('multires', _c_i), ('multires_view', _c_i), ('W_geo_feat', _c_i),
-                ('precision', _c_i)]
+                ('precision', _c_i), ('no_view_dirs', _c_i)]
 
 
 class NrNerfDesc(ctypes.Structure):
@@ -74,7 +74,7 @@ class NrVolsdfArgs(ctypes.Structure):
         ('beta_map', _c_p), ('iter_usage', _c_p),
         ('workspace', _c_p), ('workspace_bytes', _c_sz),
         ('N_outside', _c_i), ('nerf', ctypes.POINTER(NrNerfDesc)), ('nerf_packed', _c_p), ('rs_out', _c_p),
-        ('beta_plus_k', _c_f), ('sigma_bg', _c_p), ('radiance_bg', _c_p),
+        ('beta_plus_k', _c_f), ('sigma_bg', _c_p), ('radiance_bg', _c_p), ('u_rand', _c_p), ('u_out', _c_p),
     ]
 
 
@@ -95,7 +95,7 @@ class NrUnisurfArgs(ctypes.Structure):
         ('workspace', _c_p), ('workspace_bytes', _c_sz),
         ('u_query', _c_p), ('u_free', _c_p),
         ('shard_ray0', _c_i64), ('shard_row_rays', _c_i64), ('window_ss', _c_p), ('window_reduce', _c_p),
-        ('window_user', _c_p),
+        ('window_user', _c_p), ('no_secant', _c_i),
     ]
 
 
@@ -133,10 +133,11 @@ _SIGS = {
     'nr_gather_rows': (_c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_p, _c_p]),
     'nr_sphere_trace_workspace_bytes': (_c_sz, [_c_i64]),
     'nr_sphere_trace': (_c_i, [ctypes.POINTER(NrSdfDesc), _c_p, _c_p, _c_p, _c_i64, ctypes.c_float, ctypes.c_float,
-                               _c_i, _c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
+                               _c_p, _c_p, _c_i, _c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
     'nr_root_find_workspace_bytes': (_c_sz, [_c_i64, _c_i]),
-    'nr_root_find': (_c_i, [ctypes.POINTER(NrSdfDesc), _c_p, _c_p, _c_p, _c_i64, ctypes.c_float, ctypes.c_float, _c_i,
-                            _c_p, _c_i, ctypes.c_float, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
+    'nr_root_find': (_c_i, [ctypes.POINTER(NrSdfDesc), _c_p, _c_p, _c_p, _c_i64, ctypes.c_float, ctypes.c_float, _c_p,
+                            _c_p, _c_i, _c_p, _c_i, _c_i, ctypes.c_float, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_sz,
+                            _c_p]),
     'nr_normalize3': (_c_i, [_c_p, _c_i64, _c_p, _c_p]),
     'nr_surface_finish': (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_p, _c_p]),
     'nr_sdf_grid_workspace_bytes': (_c_sz, [_c_i64]),
@@ -151,7 +152,7 @@ _SIGS = {
     'nr_softplus_adjoint': (_c_i, [_c_p, _c_i, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_p, _c_p]),
     'nr_mul': (_c_i, [_c_p, _c_p, _c_i64, _c_p, _c_p]),
     'nr_activation': (_c_i, [_c_p, _c_p, _c_i64, _c_i, _c_p]),
-    'nr_radiance_input': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_p, _c_p]),
+    'nr_radiance_input': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_i, _c_p, _c_p]),
     'nr_neus_points': (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_i, _c_p, _c_p, _c_p, _c_p]),
     'nr_neus_composite_fwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
                                      _c_p]),

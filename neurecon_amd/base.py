@@ -121,6 +121,18 @@ def _no_training(*tensors_or_modules, what='this call'):
             '(training runs through the NeuS / SDF / radiance autograd functions of neurecon_amd.training)')
 
 
+def check_view_dirs(model, use_view_dirs):
+    """View-direction independence is a property of the radiance net (RadianceNet(use_view_dirs=False),
+    config key model.radiance.use_view_dirs, base.py:334-338, :383-384): the kernels then ignore the
+    ray directions they are handed.  The render-level flag volume_render(use_view_dirs=False) hands
+    view_dirs=None to batchify_query, which fails in the reference (train_util.py:27 flattens every
+    argument; neus.py:298, volsdf.py:450, unisurf.py:214), so it raises here too."""
+    if not use_view_dirs:
+        raise ValueError('volume_render(use_view_dirs=False) fails in the reference (batchify_query flattens the '
+                         'None view dirs, train_util.py:27); build the RadianceNet with use_view_dirs=False '
+                         '(model.radiance.use_view_dirs) to drop the view dependence')
+
+
 # ---------------------------------------------------------------------------------------------
 # ImplicitSurface (models/base.py:131-282)
 # ---------------------------------------------------------------------------------------------
@@ -247,20 +259,23 @@ class RadianceNet(nn.Module):
     def __init__(self, D=4, W=256, skips=[], W_geo_feat=256, embed_multires=6, embed_multires_view=4,
                  use_view_dirs=True, weight_norm=True, use_siren=False, precision=None):
         super().__init__()
-        if use_siren or not weight_norm or skips or not use_view_dirs:
-            raise NotImplementedError('neurecon_amd: RadianceNet needs weight_norm, view dirs, no skips, no SIREN')
-        self.D, self.W, self.skips, self.use_view_dirs = D, W, list(skips), use_view_dirs
+        if use_siren or not weight_norm or skips:
+            raise NotImplementedError('neurecon_amd: RadianceNet needs weight_norm, no skips, no SIREN')
+        self.D, self.W, self.skips, self.use_view_dirs = D, W, list(skips), bool(use_view_dirs)
         self.embed_multires, self.embed_multires_view, self.W_geo_feat = embed_multires, embed_multires_view, W_geo_feat
         self.embed_fn, ch_pts = get_embedder(embed_multires)
-        self.embed_fn_view, ch_view = get_embedder(embed_multires_view)
-        in0 = ch_pts + ch_view + 3 + W_geo_feat
+        if use_view_dirs:  # base.py:334-338: without view dirs the input is cat([embed(x), feature])
+            self.embed_fn_view, ch_view = get_embedder(embed_multires_view)
+            in0 = ch_pts + ch_view + 3 + W_geo_feat
+        else:
+            in0 = ch_pts + W_geo_feat
         self.precision = default_precision() if precision is None else precision
         self.layers = nn.ModuleList([WNLinear(in0 if l == 0 else W, 3 if l == D else W) for l in range(D + 1)])
         self._nr_cache = None
 
     def nr_desc(self):
         return L.NrRadDesc(self.D, self.W, self.embed_multires, self.embed_multires_view, self.W_geo_feat,
-                           L.PREC_FP32 if self.precision == 'fp32' else L.PREC_F16X3)
+                           L.PREC_FP32 if self.precision == 'fp32' else L.PREC_F16X3, 0 if self.use_view_dirs else 1)
 
     def nr_packed(self, device):
         key = _version_key(self, self.precision, device)
@@ -285,22 +300,22 @@ class RadianceNet(nn.Module):
         """base.py:372-391 (render mode; with a graph when training)."""
         L.require_gpu(x, 'points')
         shape = x.shape[:-1]
-        if wants_graph(self, normals, geometry_feature):
-            from .training import radiance
-            v = view_dirs.reshape(-1, 3).float()
-            P = x.reshape(-1, 3).shape[0]
+        P = x.reshape(-1, 3).shape[0]
+        if self.use_view_dirs:
+            if view_dirs is None:  # the reference fails in embed_fn_view / torch.cat here
+                raise TypeError('RadianceNet(use_view_dirs=True) needs view_dirs')
+            v = view_dirs.reshape(-1, 3).float().contiguous()
             if v.shape[0] != P:
                 raise ValueError('view_dirs must have one direction per point')
-            rgb = radiance(self, x.reshape(-1, 3).float(), v, normals.reshape(-1, 3).float(),
-                           geometry_feature.reshape(-1, self.W_geo_feat).float())
+            n = normals.reshape(-1, 3).float().contiguous()
+        else:  # view dirs and normals are not inputs (base.py:383-384)
+            v = n = None
+        if wants_graph(self, normals, geometry_feature):
+            from .training import radiance
+            rgb = radiance(self, x.reshape(-1, 3).float(), v, n, geometry_feature.reshape(-1, self.W_geo_feat).float())
             return rgb.reshape(*shape, 3)
         dev = x.device
         xs = x.reshape(-1, 3).float().contiguous()
-        P = xs.shape[0]
-        v = view_dirs.reshape(-1, 3).float().contiguous()
-        if v.shape[0] != P:
-            raise ValueError('view_dirs must have one direction per point')
-        n = normals.reshape(-1, 3).float().contiguous()
         f = geometry_feature.reshape(-1, self.W_geo_feat).float().contiguous()
         desc, packed = self.nr_packed(dev)
         rgb = torch.empty(P, 3, device=dev)

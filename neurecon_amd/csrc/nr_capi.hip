@@ -63,12 +63,16 @@ SdfLayout sdf_layout(const NrSdfDesc& d) {
   return L;
 }
 
-static int rad_small(const NrRadDesc& d) { return 3 + (d.multires_view < 0 ? 3 : 3 + 6 * d.multires_view) + 3; }
+// small input columns of layer 0 ahead of the feature: x, then (use_view_dirs) embed_view(v), normals
+static int rad_small(const NrRadDesc& d) {
+  return d.no_view_dirs ? 3 : 3 + (d.multires_view < 0 ? 3 : 3 + 6 * d.multires_view) + 3;
+}
 
 RadLayout rad_layout(const NrRadDesc& d) {
   RadLayout L{};
   L.prec = d.precision;
   L.n_small = rad_small(d);
+  L.view = d.no_view_dirs ? 0 : 1;
   L.kbs = L.n_small <= 32 ? 2 : 4;
   size_t off = 0;
   for (int i = 0; i < 4; ++i) {
@@ -327,6 +331,8 @@ static int volsdf_chunk(const NrVolsdfArgs& a, const VolPlan& pl, int64_t ray0, 
   c.feat_f = F(pl.o_featf); c.rad_f = F(pl.o_radf);
   c.t_coarse = a.t_coarse; c.t_init = a.t_init; c.u_up = a.u_up; c.u_fine = a.u_fine;
   c.N_out = a.N_outside > 0 ? a.N_outside : 0;
+  c.u_rand = a.u_rand ? a.u_rand + ray0 * a.N_importance : nullptr;
+  c.u_out = a.u_out && c.N_out > 0 ? a.u_out + ray0 * c.N_out : nullptr;
   c.beta_k = a.beta_plus_k;
   c.farr = F(pl.o_farr); c.bp0 = F(pl.o_bp0); c.rs_out = a.rs_out; c.d_out = F(pl.o_dout);
   c.x4 = F(pl.o_x4); c.sig_o = F(pl.o_sigo); c.rad_o = F(pl.o_rado);
@@ -462,6 +468,7 @@ static int unisurf_chunk(const NrUnisurfArgs& a, const UniPlan& pl, int64_t ray0
     if (sharded) c.wss = a.window_ss;  // the caller's [B][nw_row][3], all-reduced by window_reduce
   }
   c.t_march = a.t_march; c.t_query = a.t_query; c.t_free = a.t_free;
+  c.no_secant = a.no_secant;
   c.u_q = a.u_query ? a.u_query + ray0 * a.N_query : nullptr;
   c.u_f = a.u_free ? a.u_free + ray0 * a.N_freespace : nullptr;
   void* mlp_ws = ws + pl.o_mlp;
@@ -481,7 +488,7 @@ static int unisurf_chunk(const NrUnisurfArgs& a, const UniPlan& pl, int64_t ray0
     return rc;
   hipLaunchKernelGGL(uni_root, grd, blk, 0, st, c);
   NR_HIP_CHECK(hipGetLastError());
-  for (int i = 0; i < a.N_secant_steps; ++i) {
+  for (int i = 0; i < (a.no_secant ? 0 : a.N_secant_steps); ++i) {
     if ((rc = launch_sdf(SL, a.sdf_packed, c.pts_s, R, c.ss, nullptr, nullptr, a.sdf->multires, nullptr, 0, st)))
       return rc;
     hipLaunchKernelGGL(uni_secant, grd, blk, 0, st, c, (int)(i == a.N_secant_steps - 1));
@@ -692,7 +699,7 @@ int nr_radiance_forward(const NrRadDesc* d, const void* packed, const float* x, 
                         const float* normals, const float* feature, int64_t P, float* rgb, void* stream) {
   int rc = check_rad_desc(d);
   if (rc) return rc;
-  NR_REQUIRE(packed && x && vdir && normals && feature && rgb && vdir_div > 0, NR_ERR_ARG,
+  NR_REQUIRE(packed && x && (d->no_view_dirs || (vdir && normals)) && feature && rgb && vdir_div > 0, NR_ERR_ARG,
              "nr_radiance_forward: bad argument");
   return launch_radiance(rad_layout(*d), packed, x, vdir, vdir_div, INT64_MAX, normals, feature, P, rgb,
                          d->multires_view, (hipStream_t)stream);

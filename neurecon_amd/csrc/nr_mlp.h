@@ -43,7 +43,8 @@ struct RadLayout {
   uint32_t total;
   int prec;
   int kbs;            // small-input blocks (even)
-  int n_small;        // 3 + view-embedding + 3
+  int n_small;        // 3 + view-embedding + 3, or 3 without view dirs
+  int view;           // use_view_dirs: view embedding and normals in the input
 };
 
 // NeRF++ background MLP (models/base.py:395-453): 8 x (Linear+ReLU) with the input re-injected

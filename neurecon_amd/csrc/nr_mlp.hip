@@ -1618,10 +1618,12 @@ struct RadKArgs {
   int nfreq_view;  // <0: identity
 };
 
-// small input features [x(3), view-embedding(3+6F or 3), normals(3)] in block layout
+// small input features [x(3), view-embedding(3+6F or 3), normals(3)] in block layout ([x(3)] only
+// without view dirs)
 __device__ __forceinline__ float rad_small_feature(int f, const float (&x)[3], const float (&v)[3],
-                                                   const float (&n)[3], int nfreq_view) {
+                                                   const float (&n)[3], int nfreq_view, bool view) {
   if (f < 3) return x[f];
+  if (!view) return 0.0f;
   f -= 3;
   const int nv = nfreq_view < 0 ? 3 : 3 + 6 * nfreq_view;
   if (f < nv) return embed_feature(f, v[0], v[1], v[2], nfreq_view < 0 ? 0 : nfreq_view);
@@ -1642,6 +1644,7 @@ __global__ __launch_bounds__(kThreads) void radiance_kernel(RadKArgs a) {
   auto OP = [&](int i) { return W + L.op_off[i]; };
   auto OPB = [&](int i) { return (int)L.op_bytes[i]; };
   const float* head = (const float*)(W + L.head_off);  // [3][256] weights then [3] bias
+  const bool view = L.view != 0;
 
   ws.start(OP(0), OPB(0), OP(0) + OPB(0), OPB(0));
   for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < a.P; base += (int64_t)gridDim.x * kPointsPerWG) {
@@ -1649,22 +1652,24 @@ __global__ __launch_bounds__(kThreads) void radiance_kernel(RadKArgs a) {
     const int64_t p = base + wave * kTile + j;
     const bool valid = p < a.P;
     const int64_t pc = valid ? p : a.P - 1;
-    float xs[3], vs[3], ns[3];
+    float xs[3], vs[3] = {0.f, 0.f, 0.f}, ns[3] = {0.f, 0.f, 0.f};
     const int64_t pv = (pc / a.vdiv) % a.vmod;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       xs[c] = a.x[pc * 3 + c];
-      vs[c] = a.vdir[pv * 3 + c];
-      ns[c] = a.normals[pc * 3 + c];
+      if (view) {
+        vs[c] = a.vdir[pv * 3 + c];
+        ns[c] = a.normals[pc * 3 + c];
+      }
     }
     float4 S[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int f = 16 * b + 4 * g;
-      S[b] = b < KBS ? make_float4(rad_small_feature(f, xs, vs, ns, a.nfreq_view),
-                                   rad_small_feature(f + 1, xs, vs, ns, a.nfreq_view),
-                                   rad_small_feature(f + 2, xs, vs, ns, a.nfreq_view),
-                                   rad_small_feature(f + 3, xs, vs, ns, a.nfreq_view))
+      S[b] = b < KBS ? make_float4(rad_small_feature(f, xs, vs, ns, a.nfreq_view, view),
+                                   rad_small_feature(f + 1, xs, vs, ns, a.nfreq_view, view),
+                                   rad_small_feature(f + 2, xs, vs, ns, a.nfreq_view, view),
+                                   rad_small_feature(f + 3, xs, vs, ns, a.nfreq_view, view))
                      : make_float4(0, 0, 0, 0);
     }
     float4 X[16], Y[16];

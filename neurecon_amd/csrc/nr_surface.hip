@@ -4,7 +4,8 @@
 //   * surface_render's per-ray finish (ray_casting.py:219-262: black colour and zero normal off
 //     the surface, F.normalize(nablas));
 //   * root finding (ray_casting.py:35-160 `root_finding_surface_points`): the UNISURF march /
-//     first-crossing / secant kernels driven with constant near / far on caller-normalised rays;
+//     first-crossing / secant kernels driven with scalar or per-ray near / far on caller-normalised
+//     rays;
 //   * the mesh-extraction grid (utils/mesh_util.py:82-112 `extract_mesh`): voxel coordinates
 //     generated on the device with the reference's own float64 formula, then the forward SDF.
 #include "nr_common.h"
@@ -40,11 +41,12 @@ __global__ void normalize3_kernel(const float* __restrict__ v, int64_t n, float*
 }
 
 // iteration 0: every ray active at d = near (ray_casting.py:175-176)
-__global__ void trace_init(const float* __restrict__ ro, const float* __restrict__ rd, int64_t R, float near,
-                           float* __restrict__ d, uint8_t* __restrict__ mask, int* __restrict__ idx,
-                           float* __restrict__ pts) {
+__global__ void trace_init(const float* __restrict__ ro, const float* __restrict__ rd, int64_t R, float near_s,
+                           const float* __restrict__ near_rays, float* __restrict__ d, uint8_t* __restrict__ mask,
+                           int* __restrict__ idx, float* __restrict__ pts) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= R) return;
+  const float near = near_rays ? near_rays[t] : near_s;
   d[t] = near;
   mask[t] = 1;
   idx[t] = (int)t;
@@ -56,8 +58,8 @@ __global__ void trace_init(const float* __restrict__ ro, const float* __restrict
 // the next list together with their next query point.  NaN depths stay active, as in the
 // reference (both comparisons are false).
 __global__ void trace_step(const float* __restrict__ ro, const float* __restrict__ rd, const int* __restrict__ cnt_in,
-                           const int* __restrict__ idx_in, const float* __restrict__ sv, float far,
-                           float* __restrict__ d, uint8_t* __restrict__ mask, int* __restrict__ cnt_out,
+                           const int* __restrict__ idx_in, const float* __restrict__ sv, float far_s,
+                           const float* __restrict__ far_rays, float* __restrict__ d, uint8_t* __restrict__ mask, int* __restrict__ cnt_out,
                            int* __restrict__ idx_out, float* __restrict__ pts_out, int append) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int n = *cnt_in;
@@ -68,6 +70,7 @@ __global__ void trace_step(const float* __restrict__ ro, const float* __restrict
     r = idx_in[t];
     nd = fadd(d[r], sv[t]);
     d[r] = nd;
+    const float far = far_rays ? far_rays[r] : far_s;
     alive = !(nd > far) && !(nd < 0.f);
     if (!alive) mask[r] = 0;
   }
@@ -188,8 +191,8 @@ extern "C" {
 size_t nr_sphere_trace_workspace_bytes(int64_t n_rays) { return n_rays > 0 ? trace_plan(n_rays).total : 256; }
 
 int nr_sphere_trace(const NrSdfDesc* d, const void* packed, const float* rays_o, const float* rays_d, int64_t n_rays,
-                    float near, float far, int n_iters, float* d_pred, float* pts, uint8_t* mask, void* workspace,
-                    size_t workspace_bytes, void* stream) {
+                    float near, float far, const float* near_rays, const float* far_rays, int n_iters, float* d_pred,
+                    float* pts, uint8_t* mask, void* workspace, size_t workspace_bytes, void* stream) {
   int rc = check_sdf_desc(d);
   if (rc) return rc;
   NR_REQUIRE(n_rays >= 0 && n_iters >= 0, NR_ERR_ARG, "nr_sphere_trace: negative n_rays / n_iters");
@@ -207,8 +210,8 @@ int nr_sphere_trace(const NrSdfDesc* d, const void* packed, const float* rays_o,
   const SdfLayout SL = sdf_layout(*d);
   {
     ProfScope prof("trace_init", (double)n_rays, st);
-    hipLaunchKernelGGL(trace_init, grid1(n_rays), dim3(256), 0, st, rays_o, rays_d, n_rays, near, d_pred, mask,
-                       idx[0], qp);
+    hipLaunchKernelGGL(trace_init, grid1(n_rays), dim3(256), 0, st, rays_o, rays_d, n_rays, near, near_rays, d_pred,
+                       mask, idx[0], qp);
   }
   NR_HIP_CHECK(hipGetLastError());
   NR_HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)cnt, (int)n_rays, 1, st));
@@ -222,7 +225,7 @@ int nr_sphere_trace(const NrSdfDesc* d, const void* packed, const float* rays_o,
     {
       ProfScope prof("trace_step", (double)n_rays, st);
       hipLaunchKernelGGL(trace_step, grid1(n_rays), dim3(256), 0, st, rays_o, rays_d, cnt + cur, idx[cur], sv, far,
-                         d_pred, mask, cnt + nxt, idx[nxt], qp, append);
+                         far_rays, d_pred, mask, cnt + nxt, idx[nxt], qp, append);
     }
     NR_HIP_CHECK(hipGetLastError());
   }
@@ -254,9 +257,10 @@ size_t nr_root_find_workspace_bytes(int64_t n_rays, int N_steps) {
 }
 
 int nr_root_find(const NrSdfDesc* d, const void* packed, const float* rays_o, const float* rays_d, int64_t n_rays,
-                 float near, float far, int N_steps, const float* t_march, int N_secant_steps, float logit_tau,
-                 int fill_inf, float* d_pred, float* pts, uint8_t* mask, uint8_t* mask_sign_change,
-                 void* workspace, size_t workspace_bytes, void* stream) {
+                 float near, float far, const float* near_rays, const float* far_rays, int N_steps,
+                 const float* t_march, int N_secant_steps, int no_secant, float logit_tau, int fill_inf, float* d_pred,
+                 float* pts, uint8_t* mask, uint8_t* mask_sign_change, void* workspace, size_t workspace_bytes,
+                 void* stream) {
   int rc = check_sdf_desc(d);
   if (rc) return rc;
   NR_REQUIRE(n_rays >= 0 && N_steps >= 2 && N_secant_steps >= 0, NR_ERR_ARG,
@@ -275,13 +279,15 @@ int nr_root_find(const NrSdfDesc* d, const void* packed, const float* rays_o, co
     c.R = R;
     c.N_steps = N_steps;
     c.logit_tau = logit_tau;
+    c.no_secant = no_secant;
     c.ro = F(pl.o_ro); c.rd = F(pl.o_rd); c.near = F(pl.o_near); c.far = F(pl.o_far);
     c.pts_m = F(pl.o_ptsm); c.sm = F(pl.o_sm); c.sec = F(pl.o_sec); c.pts_s = F(pl.o_ptss); c.ss = F(pl.o_ss);
     c.t_march = t_march;
     const dim3 blk(64), grd((R + 63) / 64);
     {
       ProfScope prof("root_prologue", (double)R, st);
-      hipLaunchKernelGGL(rf_prologue, grd, blk, 0, st, c, rays_o + r0 * 3, rays_d + r0 * 3, near, far);
+      hipLaunchKernelGGL(rf_prologue, grd, blk, 0, st, c, rays_o + r0 * 3, rays_d + r0 * 3, near, far,
+                         near_rays ? near_rays + r0 : nullptr, far_rays ? far_rays + r0 : nullptr);
     }
     NR_HIP_CHECK(hipGetLastError());
     if ((rc = launch_sdf(SL, packed, c.pts_m, (int64_t)N_steps * R, c.sm, nullptr, nullptr, d->multires, nullptr, 0,
@@ -289,7 +295,7 @@ int nr_root_find(const NrSdfDesc* d, const void* packed, const float* rays_o, co
       return rc;
     hipLaunchKernelGGL(uni_root, grd, blk, 0, st, c);
     NR_HIP_CHECK(hipGetLastError());
-    for (int i = 0; i < N_secant_steps; ++i) {
+    for (int i = 0; i < (no_secant ? 0 : N_secant_steps); ++i) {
       if ((rc = launch_sdf(SL, packed, c.pts_s, R, c.ss, nullptr, nullptr, d->multires, nullptr, 0, st))) return rc;
       hipLaunchKernelGGL(uni_secant, grd, blk, 0, st, c, (int)(i == N_secant_steps - 1));
       NR_HIP_CHECK(hipGetLastError());

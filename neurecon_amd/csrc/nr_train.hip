@@ -152,12 +152,13 @@ __global__ void act_kernel(float* __restrict__ y, float* __restrict__ g, int64_t
 }
 
 // RadianceNet input cat([x, embed_view(v), normals, feature]) (base.py:379-384), one row per point;
-// v is indexed per point
+// v is indexed per point.  Without view dirs (view = 0): cat([x, feature]) (base.py:383-384)
 __global__ void radiance_input_kernel(const float* __restrict__ x, const float* __restrict__ v,
                                       const float* __restrict__ nrm, const float* __restrict__ feat, int64_t P,
-                                      int nfreq_view, int wfeat, float* __restrict__ out) {
-  const int nv = nfreq_view < 0 ? 3 : 3 + 6 * nfreq_view;
-  const int ld = 3 + nv + 3 + wfeat;
+                                      int nfreq_view, int view, int wfeat, float* __restrict__ out) {
+  const int nv = view ? (nfreq_view < 0 ? 3 : 3 + 6 * nfreq_view) : 0;
+  const int nn = view ? 3 : 0;
+  const int ld = 3 + nv + nn + wfeat;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P * ld) return;
   const int64_t p = i / ld;
@@ -168,10 +169,10 @@ __global__ void radiance_input_kernel(const float* __restrict__ x, const float* 
   } else if ((f -= 3) < nv) {
     const float vs[3] = {v[p * 3], v[p * 3 + 1], v[p * 3 + 2]};
     val = emb_f(f, vs, nfreq_view);
-  } else if ((f -= nv) < 3) {
+  } else if ((f -= nv) < nn) {
     val = nrm[p * 3 + f];
   } else {
-    val = feat[p * wfeat + f - 3];
+    val = feat[p * wfeat + f - nn];
   }
   out[i] = val;
 }
@@ -413,13 +414,13 @@ int nr_activation(float* y, float* g, int64_t n, int mode, void* stream) {
 }
 
 int nr_radiance_input(const float* x, const float* v, const float* nrm, const float* feat, int64_t P, int nfreq_view,
-                      int wfeat, float* out, void* stream) {
-  NR_REQUIRE(x && v && nrm && feat && out && P >= 0 && nfreq_view <= 10 && wfeat > 0, NR_ERR_ARG,
-             "nr_radiance_input: bad argument");
-  const int nv = nfreq_view < 0 ? 3 : 3 + 6 * nfreq_view;
+                      int use_view_dirs, int wfeat, float* out, void* stream) {
+  NR_REQUIRE(x && (!use_view_dirs || (v && nrm)) && feat && out && P >= 0 && nfreq_view <= 10 && wfeat > 0,
+             NR_ERR_ARG, "nr_radiance_input: bad argument");
+  const int ld = use_view_dirs ? 6 + (nfreq_view < 0 ? 3 : 3 + 6 * nfreq_view) + wfeat : 3 + wfeat;
   if (P == 0) return NR_OK;
-  hipLaunchKernelGGL(radiance_input_kernel, grid1(P * (6 + nv + wfeat)), dim3(kBlk), 0, (hipStream_t)stream, x, v,
-                     nrm, feat, P, nfreq_view, wfeat, out);
+  hipLaunchKernelGGL(radiance_input_kernel, grid1(P * ld), dim3(kBlk), 0, (hipStream_t)stream, x, v, nrm, feat, P,
+                     nfreq_view, use_view_dirs ? 1 : 0, wfeat, out);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

@@ -13,6 +13,7 @@ struct UniChunk {
   float logit_tau, interval, too_close;
   float near_bypass, far_bypass;  // NaN = none
   float r_interest;
+  int no_secant;     // method != 'secant' (ray_casting.py:128-135): depth 1 on hits, no refinement
   float* ro; float* rd; float* near; float* far; float* thr;
   float* pts_m;      // [N_steps][R][3] march points
   float* sm;         // [N_steps][R] march sdf
@@ -63,7 +64,8 @@ void unisurf_windows(const NrUnisurfArgs& a, int64_t& rc_rays, int64_t& nw_full,
 
 __global__ void uni_prologue(UniChunk c, const float* rays_o, const float* rays_d);
 __global__ void uni_root(UniChunk c);
-__global__ void rf_prologue(UniChunk c, const float* rays_o, const float* rays_d, float near, float far);
+__global__ void rf_prologue(UniChunk c, const float* rays_o, const float* rays_d, float near, float far,
+                            const float* near_rays, const float* far_rays);
 __global__ void rf_finish(UniChunk c, int64_t ray0, float* d_out, float* pts, uint8_t* mask, uint8_t* msc,
                           int fill_inf);
 __global__ void uni_secant(UniChunk c, int last);

@@ -60,11 +60,14 @@ __global__ void uni_prologue(UniChunk c, const float* __restrict__ rays_o, const
 }
 
 // standalone root_finding_surface_points (ray_casting.py:35-160, used by surface_render): rays as
-// given (already normalised by the caller), constant near / far, march points sample-major
+// given (already normalised by the caller), scalar or per-ray near / far (:70-73), march points
+// sample-major
 __global__ void rf_prologue(UniChunk c, const float* __restrict__ rays_o, const float* __restrict__ rays_d,
-                            float near, float far) {
+                            float near_s, float far_s, const float* __restrict__ near_rays,
+                            const float* __restrict__ far_rays) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= c.R) return;
+  const float near = near_rays ? near_rays[r] : near_s, far = far_rays ? far_rays[r] : far_s;
   const float ox = rays_o[r * 3 + 0], oy = rays_o[r * 3 + 1], oz = rays_o[r * 3 + 2];
   const float dx = rays_d[r * 3 + 0], dy = rays_d[r * 3 + 1], dz = rays_d[r * 3 + 2];
   c.ro[r * 3 + 0] = ox; c.ro[r * 3 + 1] = oy; c.ro[r * 3 + 2] = oz;
@@ -132,7 +135,7 @@ __global__ void uni_root(UniChunk c) {
     const float d_hi = lerp_ref(nr, fr, c.t_march[idx]), f_hi = vi;
     const float d_lo = lerp_ref(nr, fr, c.t_march[i1]), f_lo = vn;
     s[kDLo] = d_lo; s[kFLo] = f_lo; s[kDHi] = d_hi; s[kFHi] = f_hi;
-    dp = secant(d_lo, f_lo, d_hi, f_hi);
+    if (!c.no_secant) dp = secant(d_lo, f_lo, d_hi, f_hi);
   }
   s[kDPred] = dp;
   c.pts_s[r * 3 + 0] = fadd(c.ro[r * 3 + 0], fmul(dp, c.rd[r * 3 + 0]));

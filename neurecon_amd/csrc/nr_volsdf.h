@@ -32,6 +32,8 @@ struct VolChunk {
   // final pass (ray-major [R][S])
   float* d_all; float* pts_f; float* sdf_f; float* nab_f; float* feat_f; float* rad_f;
   const float* t_coarse; const float* t_init; const float* u_up; const float* u_fine;
+  const float* u_rand;             // perturb: [R][N_imp] per-ray sorted uniforms of the final sample_cdf
+  const float* u_out;              // perturb: [R][N_out] NeRF++ strata uniforms
   // NeRF++ background (N_out > 0): per-ray far (sphere exit) and beta+ init, outside samples
   int N_out;
   float beta_k;                    // float32(4 (N0 - 1) log(1 + eps))

@@ -283,9 +283,10 @@ __device__ void vs_decide(const VolChunk& c, int r, int it, int n, Lds& s) {
   const int l = threadIdx.x;
   float* fine = c.fine + (int64_t)r * c.N_imp;
   auto emit_fine = [&](int k, float v) { fine[k] = v; };
+  const float* uf = c.u_rand ? c.u_rand + (int64_t)r * c.N_imp : c.u_fine;  // perturb: this ray's draws
   const float mnet = vs_bound_max(s.D, s.S, n, c.alpha_net, c.beta_net);
   if (!(mnet > c.eps)) {
-    vs_finalize(s.D, s.S, n, c.alpha_net, c.beta_net, c.u_fine, c.N_imp, emit_fine);
+    vs_finalize(s.D, s.S, n, c.alpha_net, c.beta_net, uf, c.N_imp, emit_fine);
     if (l == 0) {
       c.usage[r] = (float)it;
       c.bmap[r] = c.beta_net;
@@ -304,7 +305,7 @@ __device__ void vs_decide(const VolChunk& c, int r, int it, int n, Lds& s) {
   }
   const float alpha = fdiv(1.0f, beta);
   if (it == c.max_iter) {  // never converged: sample with the last beta+ (volsdf.py:259-268)
-    vs_finalize(s.D, s.S, n, alpha, beta, c.u_fine, c.N_imp, emit_fine);
+    vs_finalize(s.D, s.S, n, alpha, beta, uf, c.N_imp, emit_fine);
     if (l == 0) {
       c.usage[r] = -1.0f;
       c.bmap[r] = beta;
@@ -468,7 +469,7 @@ __global__ __launch_bounds__(64) void volsdf_points(VolChunk c) {
 }
 
 // NeRF++ background samples (volsdf.py:451-463): d_out = get_dvals_from_radius(o, d, rs)
-// (rend_util.py:213-234, far end), x_out = [p_out / rs, 1 / rs]
+// (rend_util.py:213-234, far end), x_out = [p_out / rs, 1 / rs]; perturb stratifies rs per ray
 __global__ __launch_bounds__(64) void volsdf_outside(VolChunk c) {
   const int r = blockIdx.x, l = threadIdx.x;
   const float ox = c.ro[r * 3], oy = c.ro[r * 3 + 1], oz = c.ro[r * 3 + 2];
@@ -476,8 +477,14 @@ __global__ __launch_bounds__(64) void volsdf_outside(VolChunk c) {
   const float nsq = ray_dot(ox, oy, oz, ox, oy, oz);
   const float dot = ray_dot(ox, oy, oz, dx, dy, dz);
   const float q = fsub(nsq, fmul(dot, dot));
+  const float* ur = c.u_out ? c.u_out + (int64_t)r * c.N_out : nullptr;
   for (int k = l; k < c.N_out; k += 64) {
-    const float rs = c.rs_out[k];
+    float rs = c.rs_out[k];
+    if (ur) {  // perturb (volsdf.py:460-465): mids of neighbouring radii, the end radii kept
+      const float lo = k > 0 ? fmul(0.5f, fadd(c.rs_out[k], c.rs_out[k - 1])) : c.rs_out[0];
+      const float hi = k + 1 < c.N_out ? fmul(0.5f, fadd(c.rs_out[k + 1], c.rs_out[k])) : c.rs_out[c.N_out - 1];
+      rs = fadd(lo, fmul(fsub(hi, lo), ur[k]));
+    }
     const float d = fadd(-dot, sqrtf(fsub(fmul(rs, rs), q)));
     const int64_t i = (int64_t)r * c.N_out + k;
     c.d_out[i] = d;

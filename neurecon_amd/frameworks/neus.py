@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _lib as L
-from ..base import ImplicitSurface, NeRF, RadianceNet, _no_training, wants_graph
+from ..base import ImplicitSurface, NeRF, RadianceNet, _no_training, check_view_dirs, wants_graph
 from .. import rend_util
 
 
@@ -107,8 +107,7 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     if upsample_algo not in L.UPSAMPLE:
         raise NotImplementedError(upsample_algo)
     direct = upsample_algo != 'official_solution'
-    if not use_view_dirs:
-        raise NotImplementedError('neurecon_amd: use_view_dirs=False not supported')
+    check_view_dirs(model, use_view_dirs)
     dev = rays_o.device
     if batched:
         B = rays_d.shape[0]
@@ -258,8 +257,7 @@ def _train_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     from .. import training as T
     if N_outside > 0:
         raise NotImplementedError('neurecon_amd: training with the NeRF++ background (N_outside > 0) is not native')
-    if not use_view_dirs:
-        raise NotImplementedError('neurecon_amd: use_view_dirs=False not supported')
+    check_view_dirs(model, use_view_dirs)
     if upsample_algo not in L.UPSAMPLE:
         raise NotImplementedError(upsample_algo)
     dev = rays_o.device

@@ -17,7 +17,7 @@ import torch.nn.functional as F
 
 from .. import _lib as L
 from .. import rend_util
-from ..base import ImplicitSurface, RadianceNet, _no_training
+from ..base import ImplicitSurface, RadianceNet, _no_training, check_view_dirs
 from .neus import _linspace_table
 
 N_STEPS = 256        # ray_casting.py:49 (root_finding_surface_points default)
@@ -98,10 +98,7 @@ def volume_render(rays_o, rays_d, model, batched=False, batched_info={}, calc_no
     single-process render of the whole batch."""
     L.require_gpu(rays_o, 'rays_o')
     _no_training(model)
-    if method != 'secant':
-        raise NotImplementedError(f'neurecon_amd: root finding method={method!r} not native')
-    if not use_view_dirs:
-        raise NotImplementedError('neurecon_amd: use_view_dirs=False not supported')
+    check_view_dirs(model, use_view_dirs)
     dev = rays_o.device
     if batched:
         B, N = rays_d.shape[0], rays_d.reshape(rays_d.shape[0], -1, 3).shape[1]
@@ -142,6 +139,7 @@ def volume_render(rays_o, rays_d, model, batched=False, batched_info={}, calc_no
     a.near_bypass = float('nan') if near_bypass is None else float(near_bypass)
     a.far_bypass = float('nan') if far_bypass is None else float(far_bypass)
     a.N_steps, a.N_secant_steps, a.N_query, a.N_freespace = N_STEPS, N_SECANT_STEPS, N_query, N_freespace
+    a.no_secant = int(method != 'secant')  # ray_casting.py:128-135: any other method reports depth 1 on hits
     # F.normalize(nablas) with dim=1: per point for [chunk, 3] inputs, per window for [B, chunk, 3]
     a.normal_mode = 1 if batched else 0
     a.rayschunk, a.netchunk = int(rayschunk), int(netchunk)

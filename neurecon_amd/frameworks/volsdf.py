@@ -15,7 +15,7 @@ import torch.nn as nn
 
 from .. import _lib as L
 from .. import rend_util
-from ..base import ImplicitSurface, NeRF, RadianceNet, _no_training
+from ..base import ImplicitSurface, NeRF, RadianceNet, _no_training, check_view_dirs
 from .neus import _linspace_table
 
 
@@ -85,18 +85,38 @@ def _outside_radii(n, r, device):
     return (r / torch.flip(t, dims=[-1])).contiguous().to(device)
 
 
+def _volsdf_uniforms(B, N, batched, rayschunk, N_importance, N_outside, dev):
+    """perturb=True uniforms per reference ray chunk: the final sample_cdf's draws (volsdf.py:102,
+    rend_util.py:306), then the NeRF++ strata (volsdf.py:464).  The reference draws the sample_cdf
+    uniforms per convergence event (iteration 0, 1, ..., then the unconverged rays, each a
+    [rays of the event, N_importance] tensor in ray order, volsdf.py:151, :204, :266); here each ray
+    gets one row of one [rays, N_importance] draw, the same distribution (independent U[0,1) rows).
+    Returns u_rand [B*N, N_importance] with each row sorted ascending (the kernel's inverse-CDF walk;
+    the fine depths are sorted into d_all, so a row's order never reaches the outputs) and
+    u_out [B*N, N_outside] (or None)."""
+    pre = [B] if batched else []
+    uf, uo = [], []
+    for r0 in range(0, N, rayschunk):
+        nc = min(rayschunk, N - r0)
+        uf.append(rend_util.uniform([(B if batched else 1) * nc, N_importance], dev).reshape(*pre, nc, N_importance))
+        if N_outside > 0:
+            uo.append(rend_util.uniform([*pre, nc, N_outside], dev))
+    u_rand = torch.cat(uf, len(pre)).reshape(-1, N_importance).float().to(dev)
+    u_rand = torch.sort(u_rand, dim=-1).values.contiguous()
+    u_out = torch.cat(uo, len(pre)).reshape(-1, N_outside).float().to(dev).contiguous() if uo else None
+    return u_rand, u_out
+
+
 def volume_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=3.0, batched=False,
                   batched_info={}, calc_normal=False, use_view_dirs=True, rayschunk=65536, netchunk=1048576,
                   white_bkgd=False, use_nerfplusplus=False, detailed_output=True, show_progress=False,
                   perturb=False, N_samples=128, N_importance=64, N_outside=32, max_upsample_steps=5,
                   max_bisection_steps=10, epsilon=0.1, **dummy_kwargs):
-    """volsdf.py:377-551, render mode.  rays_o/rays_d: [(B,) N_rays, 3]."""
+    """volsdf.py:377-551, render mode.  rays_o/rays_d: [(B,) N_rays, 3].  perturb=True: random final
+    fine samples and NeRF++ strata (_volsdf_uniforms)."""
     L.require_gpu(rays_o, 'rays_o')
     _no_training(model)
-    if perturb:
-        raise NotImplementedError('neurecon_amd: stratified (perturb=True) sampling is a training feature')
-    if not use_view_dirs:
-        raise NotImplementedError('neurecon_amd: use_view_dirs=False not supported')
+    check_view_dirs(model, use_view_dirs)
     dev = rays_o.device
     prefix = [rays_d.shape[0], -1] if batched else [-1]
     ro = rays_o.reshape(-1, 3).float().contiguous()
@@ -165,6 +185,10 @@ def volume_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=
     a.iter_usage = L.ptr(det.get('iter_usage'))
     a.sigma_bg = L.ptr(det.get('sigma_out'))
     a.radiance_bg = L.ptr(det.get('radiance_out'))
+    if perturb:
+        Bn = rays_d.shape[0] if batched else 1
+        u_rand, u_out = _volsdf_uniforms(Bn, n // Bn, batched, int(rayschunk), N_importance, No, dev)
+        a.u_rand, a.u_out = L.ptr(u_rand), L.ptr(u_out)
     lib = L.lib()
     ws_bytes = lib.nr_volsdf_workspace_bytes(ctypes.byref(a))
     if ws_bytes == 0:

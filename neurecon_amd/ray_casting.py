@@ -25,9 +25,23 @@ def _normalize3(v):
     return out.reshape(v.shape)
 
 
+def _per_ray(v, n, dev, name):
+    """near / far: a float, or a tensor broadcast to the rays (the reference's `torch.ones * near`,
+    ray_casting.py:70-73, :175) -> (scalar, per-ray device array or None)."""
+    if not isinstance(v, torch.Tensor):
+        return float(v), None
+    t = v.to(device=dev, dtype=torch.float32)
+    if t.numel() == 1:
+        return float(t.reshape(-1)[0]), None
+    if t.numel() != n:
+        raise ValueError(f'{name}: {tuple(v.shape)} does not match {n} rays')
+    return 0.0, t.reshape(-1).contiguous()
+
+
 def sphere_tracing_surface_points(implicit_surface, rays_o, rays_d, near=0.0, far=6.0, batched=True,
                                   batched_info={}, N_iters=20):
-    """ray_casting.py:163-182 -> (d_preds [...], pts [..., 3], mask [...] bool)."""
+    """ray_casting.py:163-182 -> (d_preds [...], pts [..., 3], mask [...] bool); near / far floats or
+    per-ray tensors."""
     L.require_gpu(rays_o, 'rays_o')
     _no_training(implicit_surface)
     shape = rays_o.shape[:-1]
@@ -35,6 +49,8 @@ def sphere_tracing_surface_points(implicit_surface, rays_o, rays_d, near=0.0, fa
     rd = rays_d.reshape(-1, 3).float().contiguous()
     n = ro.shape[0]
     dev = ro.device
+    near, near_r = _per_ray(near, n, dev, 'near')
+    far, far_r = _per_ray(far, n, dev, 'far')
     desc, packed = implicit_surface.nr_packed(dev)
     lib = L.lib()
     d = torch.empty(n, device=dev)
@@ -43,7 +59,7 @@ def sphere_tracing_surface_points(implicit_surface, rays_o, rays_d, near=0.0, fa
     ws_bytes = lib.nr_sphere_trace_workspace_bytes(n)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     L.check(lib.nr_sphere_trace(ctypes.byref(desc), L.ptr(packed), L.ptr(ro), L.ptr(rd), n, ctypes.c_float(near),
-                                ctypes.c_float(far), int(N_iters), L.ptr(d), L.ptr(pts), L.ptr(mask), L.ptr(ws),
+                                ctypes.c_float(far), L.ptr(near_r), L.ptr(far_r), int(N_iters), L.ptr(d), L.ptr(pts), L.ptr(mask), L.ptr(ws),
                                 ws_bytes, L.stream_of(dev)))
     return d.reshape(shape), pts.reshape(*shape, 3), mask.view(torch.bool).reshape(shape)
 
@@ -52,14 +68,11 @@ def root_finding_surface_points(surface_query_fn, rays_o, rays_d, near=0.0, far=
                                 N_steps=256, logit_tau=0.0, method='secant', N_secant_steps=8, fill_inf=True):
     """ray_casting.py:35-160 -> (d_pred_out, pt_pred, mask, mask_sign_change); rays_d already
     normalised.  `surface_query_fn` must be a neurecon_amd ImplicitSurface (its forward SDF runs in
-    the library); near / far are scalars."""
+    the library); near / far floats or per-ray [(B), N_rays] tensors; a method other than 'secant'
+    skips the refinement and reports depth 1 on hits (ray_casting.py:128-135)."""
     from .frameworks.neus import _linspace_table
     if not hasattr(surface_query_fn, 'nr_packed'):
         raise NotImplementedError('neurecon_amd: root finding needs a neurecon_amd ImplicitSurface as surface_query_fn')
-    if isinstance(near, torch.Tensor) or isinstance(far, torch.Tensor):
-        raise NotImplementedError('neurecon_amd: per-ray near/far tensors are not supported by nr_root_find')
-    if method != 'secant':
-        raise NotImplementedError(method)
     L.require_gpu(rays_o, 'rays_o')
     _no_training(surface_query_fn)
     shape = rays_o.shape[:-1]
@@ -67,6 +80,8 @@ def root_finding_surface_points(surface_query_fn, rays_o, rays_d, near=0.0, far=
     rd = rays_d.reshape(-1, 3).float().contiguous()
     n = ro.shape[0]
     dev = ro.device
+    near, near_r = _per_ray(near, n, dev, 'near')
+    far, far_r = _per_ray(far, n, dev, 'far')
     desc, packed = surface_query_fn.nr_packed(dev)
     lib = L.lib()
     t = _linspace_table(int(N_steps), dev)
@@ -77,8 +92,8 @@ def root_finding_surface_points(surface_query_fn, rays_o, rays_d, near=0.0, far=
     ws_bytes = lib.nr_root_find_workspace_bytes(n, int(N_steps))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     L.check(lib.nr_root_find(ctypes.byref(desc), L.ptr(packed), L.ptr(ro), L.ptr(rd), n, ctypes.c_float(near),
-                             ctypes.c_float(far), int(N_steps), L.ptr(t), int(N_secant_steps), ctypes.c_float(logit_tau),
-                             int(bool(fill_inf)), L.ptr(d), L.ptr(pts), L.ptr(mask), L.ptr(msc), L.ptr(ws), ws_bytes,
+                             ctypes.c_float(far), L.ptr(near_r), L.ptr(far_r), int(N_steps), L.ptr(t),
+                             int(N_secant_steps), int(method != 'secant'), ctypes.c_float(logit_tau), int(bool(fill_inf)), L.ptr(d), L.ptr(pts), L.ptr(mask), L.ptr(msc), L.ptr(ws), ws_bytes,
                              L.stream_of(dev)))
     return (d.reshape(shape), pts.reshape(*shape, 3), mask.view(torch.bool).reshape(shape),
             msc.view(torch.bool).reshape(shape))
@@ -97,8 +112,9 @@ def surface_render(rays_o, rays_d, model, calc_normal=True, rayschunk=8192, netc
     """ray_casting.py:185-263 -> (colors, depths, extras{implicit_nablas, mask_surface[, normals_surface]})."""
     if ray_casting_algo not in ('root_finding', 'sphere_tracing'):
         raise NotImplementedError(ray_casting_algo)
-    if not use_view_dirs:
-        raise NotImplementedError('neurecon_amd: use_view_dirs=False not supported')
+    if not use_view_dirs and model.radiance_net.use_view_dirs:
+        # model.forward(pts, None) (ray_casting.py:216-226) fails in the reference's embed_fn_view / cat
+        raise TypeError('surface_render(use_view_dirs=False) needs a RadianceNet built with use_view_dirs=False')
     L.require_gpu(rays_o, 'rays_o')
     with torch.no_grad():
         if batched:
@@ -120,7 +136,8 @@ def surface_render(rays_o, rays_d, model, calc_normal=True, rayschunk=8192, netc
         step = rayschunk if _couples_rays(model) else max(rayschunk, 1 << 18)
         colors, nablas = [], []
         for i in range(0, n, step):
-            c, _, nb = model.forward(pt_pred.narrow(DIM, i, min(step, n - i)), rd.narrow(DIM, i, min(step, n - i)))
+            c, _, nb = model.forward(pt_pred.narrow(DIM, i, min(step, n - i)),
+                                     rd.narrow(DIM, i, min(step, n - i)) if use_view_dirs else None)
             colors.append(c)
             nablas.append(nb)
         colors = torch.cat(colors, DIM).contiguous()

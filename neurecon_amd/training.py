@@ -165,14 +165,16 @@ class RadianceFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, v, nrm, feat, cfg, *params):
-        D, nfreq_view = cfg
+        D, nfreq_view, view = cfg
         Ws, bs = params[:D + 1], params[D + 1:]
         P = x.shape[0]
         wf = feat.shape[1]
-        nv = 3 if nfreq_view < 0 else 3 + 6 * nfreq_view
-        inp = torch.empty(P, 6 + nv + wf, device=x.device)
-        L.check(L.lib().nr_radiance_input(L.ptr(x), L.ptr(v), L.ptr(nrm), L.ptr(feat), P, nfreq_view, wf, L.ptr(inp),
-                                          _st(x)))
+        # without view dirs the input is cat([x, feature]) (base.py:383-384): no view / normal columns
+        nv = (3 if nfreq_view < 0 else 3 + 6 * nfreq_view) if view else 0
+        nn_ = 3 if view else 0
+        inp = torch.empty(P, 3 + nv + nn_ + wf, device=x.device)
+        L.check(L.lib().nr_radiance_input(L.ptr(x), L.ptr(v), L.ptr(nrm), L.ptr(feat), P, nfreq_view, int(view), wf,
+                                          L.ptr(inp), _st(x)))
         hs = [inp]
         h = inp
         for l in range(D):
@@ -181,13 +183,13 @@ class RadianceFn(torch.autograd.Function):
             hs.append(h)
         y = torch.addmm(bs[D], h, Ws[D].t())
         L.check(L.lib().nr_activation(L.ptr(y), None, y.numel(), 2, _st(x)))
-        ctx.cfg = (D, nv, wf)
+        ctx.cfg = (D, nv, nn_, wf)
         ctx.save_for_backward(y, *Ws, *hs)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        D, nv, wf = ctx.cfg
+        D, nv, nn_, wf = ctx.cfg
         saved = ctx.saved_tensors
         y = saved[0]
         Ws = saved[1:D + 2]
@@ -201,8 +203,8 @@ class RadianceFn(torch.autograd.Function):
             g = g @ Ws[l]
             if l > 0:
                 L.check(L.lib().nr_activation(L.ptr(hs[l]), L.ptr(g), g.numel(), 1, _st(g)))
-        d_nrm = _cols(g, 3 + nv, 3)
-        d_feat = _cols(g, 6 + nv, wf)
+        d_nrm = _cols(g, 3 + nv, 3) if nn_ else None
+        d_feat = _cols(g, 3 + nv + nn_, wf)
         return (None, None, d_nrm, d_feat, None, *dW, *db)
 
 
@@ -260,5 +262,6 @@ def sdf_nablas(surface, x, want_feat):
 def radiance(net, x, v, nrm, feat):
     Ws = [l.effective_weight() for l in net.layers]
     bs = [l.bias for l in net.layers]
-    return RadianceFn.apply(x.contiguous(), v.contiguous(), nrm.contiguous(), feat.contiguous(),
-                            (net.D, net.embed_multires_view), *Ws, *bs)
+    view = net.use_view_dirs
+    return RadianceFn.apply(x.contiguous(), v.contiguous() if view else None, nrm.contiguous() if view else None,
+                            feat.contiguous(), (net.D, net.embed_multires_view, view), *Ws, *bs)

@@ -26,11 +26,12 @@ def alpha_to_w(alpha):
 
 
 class NeuSOracle:
-    def __init__(self, sd, speed_factor=10.0, use_outside_nerf=False, multires=6, multires_view=4):
+    def __init__(self, sd, speed_factor=10.0, use_outside_nerf=False, multires=6, multires_view=4, use_view_dirs=True):
         self.sd = sd
         self.speed_factor = speed_factor
         self.sdf_net = SDFNet(sd, multires=multires)
-        self.rad_net = RadianceNet(sd, multires_view=multires_view)
+        # use_view_dirs=False: the radiance net ignores the directions it is handed (base.py:383-384)
+        self.rad_net = RadianceNet(sd, multires_view=multires_view, use_view_dirs=use_view_dirs)
         self.nerf = NeRFNet(sd) if use_outside_nerf else None
 
     def s(self):

@@ -24,10 +24,12 @@ def sphere_trace(sdf_fn, rays_o, rays_d, near=0.0, far=6.0, N_iters=20):
 
 
 def root_find(sdf_fn, o, d, near=0.0, far=6.0, **cfgs):
-    """ray_casting.py:35-160 with scalar near / far (restated in oracle/unisurf.py:root_find)."""
+    """ray_casting.py:35-160 with float or per-ray tensor near / far (:70-73; restated in
+    oracle/unisurf.py:root_find)."""
     from .unisurf import root_find as rf
     cfgs.setdefault('fill_inf', True)
-    return rf(sdf_fn, o, d, near * torch.ones(o.shape[:-1]), far * torch.ones(o.shape[:-1]), **cfgs)
+    full = lambda v: v if isinstance(v, torch.Tensor) else v * torch.ones(o.shape[:-1])
+    return rf(sdf_fn, o, d, full(near), full(far), **cfgs)
 
 
 def surface_render_neus(oracle, rays_o, rays_d, calc_normal=True, algo='sphere_tracing', **cfgs):

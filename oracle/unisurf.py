@@ -8,9 +8,11 @@ from . import rays as R
 from .nets import SDFNet, RadianceNet
 
 
-def root_find(sdf_fn, o, d, near, far, N_steps=256, logit_tau=0.0, N_secant_steps=8, fill_inf=False):
+def root_find(sdf_fn, o, d, near, far, N_steps=256, logit_tau=0.0, N_secant_steps=8, fill_inf=False,
+              method='secant'):
     """ray_casting.py:35-160 (batched [B, N, 3]): first outside->inside sign change on a uniform
-    256-sample march, refined by 8 secant steps (ray_casting.py:11-30)."""
+    256-sample march, refined by 8 secant steps (ray_casting.py:11-30); any other method leaves
+    depth 1 on the hits (ray_casting.py:128-135)."""
     B, N = o.shape[:2]
     t = torch.linspace(0., 1., N_steps)[None, None, :]
     dp = near[..., None] * (1 - t) + far[..., None] * t
@@ -26,7 +28,7 @@ def root_find(sdf_fn, o, d, near, far, N_steps=256, logit_tau=0.0, N_secant_step
     g = lambda a, i: torch.gather(a, -1, i[..., None])[..., 0][hit]
     d_hi, f_hi, d_lo, f_lo = g(dp, idx), g(val, idx), g(dp, idx1), g(val, idx1)
     om, dm = o[hit], d[hit]
-    if hit.sum() > 0:
+    if method == 'secant' and hit.sum() > 0:
         dpred = -f_lo * (d_hi - d_lo) / (f_hi - f_lo) + d_lo
         for _ in range(N_secant_steps):
             fm = sdf_fn(om + dpred.unsqueeze(-1) * dm).squeeze(-1) - logit_tau
@@ -46,9 +48,9 @@ def root_find(sdf_fn, o, d, near, far, N_steps=256, logit_tau=0.0, N_secant_step
 
 
 class UNISURFOracle:
-    def __init__(self, sd, multires=6):
+    def __init__(self, sd, multires=6, use_view_dirs=True):
         self.sdf_net = SDFNet(sd, multires=multires)
-        self.rad_net = RadianceNet(sd, multires=-1, multires_view=-1)
+        self.rad_net = RadianceNet(sd, multires=-1, multires_view=-1, use_view_dirs=use_view_dirs)
 
     def forward_chunk(self, x, v):
         # unisurf.py:34-38 -- F.normalize(nablas) with the default dim=1
@@ -58,14 +60,14 @@ class UNISURFOracle:
 
     def render(self, rays_o, rays_d, logit_tau=0.0, radius_of_interest=4.0, interval=1.0,
                too_close_threshold=0.1, N_query=64, N_freespace=32, netchunk=1048576, calc_normal=True,
-               white_bkgd=False):
+               white_bkgd=False, method='secant'):
         o = rays_o.reshape(rays_o.shape[0], -1, 3).float()
         d = F.normalize(rays_d.reshape(rays_d.shape[0], -1, 3).float(), dim=-1)
         B, N = o.shape[:2]
         near, far = R.near_far_from_sphere(o, d, r=radius_of_interest, keepdim=False)
         thr = near + (far - near) * too_close_threshold
         with torch.no_grad():
-            dpred, pt, hit, crossing = root_find(self.sdf_net.sdf, o, d, near, far, logit_tau=logit_tau)
+            dpred, pt, hit, crossing = root_find(self.sdf_net.sdf, o, d, near, far, logit_tau=logit_tau, method=method)
         dpred = torch.max(torch.min(dpred, far), near)                        # unisurf.py:152-154
         d_up = torch.min(dpred + interval, far)
         d_lo = torch.max(dpred - interval, near)

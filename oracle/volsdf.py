@@ -1,5 +1,6 @@
 """ORACLE (test infrastructure only): VolSDF rendering restated from models/frameworks/volsdf.py
-(render mode, builtin background sphere or NeRF++ background, perturb=False)."""
+(render mode, builtin background sphere or NeRF++ background, perturb=False or True with torch.rand
+drawn in the reference's order)."""
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -34,15 +35,17 @@ def error_bound(d, sdf, alpha, beta):
 
 
 def fine_sample(sdf_fn, d_init, o, d, alpha_net, beta_net, far, eps=0.1, max_iter=5, max_bisection=10,
-                N_final=64, N_up=128):
-    """Error-bounded adaptive upsampling (volsdf.py:77-272), det=True.  Rays that are already
-    within eps keep iter_usage 0; k = converged after k rounds; -1 = never (last beta+ used)."""
+                N_final=64, N_up=128, perturb=False):
+    """Error-bounded adaptive upsampling (volsdf.py:77-272).  Rays that are already within eps keep
+    iter_usage 0; k = converged after k rounds; -1 = never (last beta+ used).  perturb: the final
+    sample_cdf draws torch.rand per convergence event, in the reference's order (det=not perturb,
+    volsdf.py:102)."""
     prefix = d_init.shape[:-1]
     pts = lambda dv, oo, dd: oo[..., None, :] + dd[..., None, :] * dv[..., :, None]
 
     def finalize(dv, sv, a, b):
         Rt, _ = _transmittance_integral(dv, sv, a, b)
-        return R.sample_cdf(dv, 1 - torch.exp(-Rt), N_final, det=True)
+        return R.sample_cdf(dv, 1 - torch.exp(-Rt), N_final, det=not perturb)
 
     dv = d_init
     out = torch.zeros([*prefix, N_final])
@@ -129,7 +132,8 @@ class VolSDFOracle:
         return torch.min(self.sdf_net.sdf(x), self.R - x.norm(dim=-1))
 
     def render(self, rays_o, rays_d, near=0.0, far=6.0, calc_normal=True, N_samples=128, N_importance=64,
-               max_upsample_steps=5, max_bisection_steps=10, epsilon=0.1, white_bkgd=False, N_outside=32):
+               max_upsample_steps=5, max_bisection_steps=10, epsilon=0.1, white_bkgd=False, N_outside=32,
+               perturb=False):
         o = rays_o.reshape(rays_o.shape[0], -1, 3).float()
         d = F.normalize(rays_d.reshape(rays_d.shape[0], -1, 3).float(), dim=-1)
         B, N = o.shape[:2]
@@ -148,7 +152,7 @@ class VolSDFOracle:
             d_fine, beta_map, usage = fine_sample(self.surface, d_init, o, d, alpha, beta, fars,
                                                   eps=epsilon, max_iter=max_upsample_steps,
                                                   max_bisection=max_bisection_steps, N_final=N_importance,
-                                                  N_up=N_samples * 4)
+                                                  N_up=N_samples * 4, perturb=perturb)
         d_all = torch.sort(torch.cat([d_coarse, d_fine], -1), -1)[0]
         pts = o[..., None, :] + d[..., None, :] * d_all[..., :, None]
         sdf, nablas, h = self.sdf_net.forward_with_nablas(pts)
@@ -160,6 +164,11 @@ class VolSDFOracle:
         if self.nerf is not None:                                              # volsdf.py:451-469
             t_out = torch.linspace(0, 1, N_outside + 2)[..., 1:-1].float()
             rs = (self.R / torch.flip(t_out, dims=[-1])).expand([B, N, N_outside])
+            if perturb:                                                        # volsdf.py:460-465
+                mids = .5 * (rs[..., 1:] + rs[..., :-1])
+                upper = torch.cat([mids, rs[..., -1:]], -1)
+                lower = torch.cat([rs[..., :1], mids], -1)
+                rs = lower + (upper - lower) * torch.rand(upper.shape).float()
             d_out = R.dvals_from_radius(o, d, rs)
             pts_out = o[..., None, :] + d[..., None, :] * d_out[..., :, None]
             x_out = torch.cat([pts_out / rs[..., None], 1. / rs[..., None]], dim=-1)

@@ -447,6 +447,95 @@ def gen_perturb(R):
          **{f'u{i}': u for i, u in enumerate(rec.draws)})
 
 
+def gen_options(R):
+    """Render options beyond the headline configs, run through the reference: RadianceNet built with
+    use_view_dirs=False (config key model.radiance.use_view_dirs; the render itself keeps
+    use_view_dirs=True -- volume_render(use_view_dirs=False) fails inside batchify_query on the None
+    view dirs, train_util.py:27) on NeuS (36 rays of the config-(b) camera) and UNISURF (36 rays of
+    config (e), with 'secant' and with another root-finding method, ray_casting.py:128-135), and root finding / sphere tracing with per-ray near / far tensors
+    from near_far_from_sphere (ray_casting.py:53-54, :70-73, :175)."""
+    out = {}
+    rad_nv = dict(use_siren=False, embed_multires=-1, embed_multires_view=4, use_view_dirs=False, D=4, W=256,
+                  skips=[])
+    sd = wg.neus_state(seed=1, use_view_dirs=False)
+    m = R.neus.NeuS(variance_init=0.05, speed_factor=10.0, input_ch=3, W_geo_feat=256, use_outside_nerf=False,
+                    obj_bounding_radius=1.0, surface_cfg=dict(radius_init=0.5, **SURF), radiance_cfg=rad_nv)
+    m.load_state_dict(sd)
+    m.eval()
+    H, W, _, _ = wg.CAMERAS['b']
+    ro, rd = camera_rays(R, 'b', grid_idx(H, W, n=6))
+    with torch.no_grad():
+        rgb, depth, ex = R.neus.volume_render(
+            ro, rd, m, obj_bounding_radius=1.0, batched=True, calc_normal=True, detailed_output=True,
+            perturb=False, N_samples=64, N_importance=64, N_outside=0,
+            upsample_algo='official_solution', N_upsample_iters=4)
+    out.update(neus_rays_o=ro, neus_rays_d=rd, neus_rgb=rgb, neus_depth=depth, neus_mask=ex['mask_volume'],
+               neus_normals=ex['normals_volume'], neus_d_final=ex['d_final'], neus_radiance=ex['radiance'])
+
+    sdu = wg.unisurf_state(seed=3, use_view_dirs=False)
+    mu = R.unisurf.UNISURF(W_geo_feat=256, surface_cfg=dict(radius_init=1.0, **SURF),
+                           radiance_cfg=dict(rad_nv, embed_multires_view=-1))
+    mu.load_state_dict(sdu)
+    mu.eval()
+    H, W, _, _ = wg.CAMERAS['e']
+    ro, rd = camera_rays(R, 'e', grid_idx(H, W, n=6, lo=0.1, hi=0.9))
+    logit_tau = R.unisurf.UNISURF.get_surface_from_opacity(0.5)
+    out.update(uni_rays_o=ro, uni_rays_d=rd, uni_logit_tau=float(logit_tau))
+    for tag, method in [('uni', 'secant'), ('uni_nosec', 'none')]:
+        with torch.no_grad():
+            rgb, depth, ex = R.unisurf.volume_render(
+                ro, rd, mu, batched=True, calc_normal=True, detailed_output=True, perturb=False,
+                method=method, logit_tau=logit_tau, radius_of_interest=4.0, interval=1.0,
+                N_query=64, N_freespace=32)
+        out.update({f'{tag}_rgb': rgb, f'{tag}_depth': depth, f'{tag}_mask': ex['mask_volume'],
+                    f'{tag}_normals': ex['normals_volume'], f'{tag}_depth_surface': ex['depth_surface'],
+                    f'{tag}_mask_surface': ex['mask_surface'], f'{tag}_surface_points': ex['surface_points']})
+
+    model = _neus_model(R, wg.neus_state(seed=1), False)
+    H, W, _, _ = wg.CAMERAS['b']
+    ro, rd = camera_rays(R, 'b', grid_idx(H, W, n=16, lo=0.0, hi=1.0))
+    rdn = torch.nn.functional.normalize(rd, dim=-1)
+    near, far = R.rend_util.near_far_from_sphere(ro, rdn, r=1.0, keepdim=False)
+    with torch.no_grad():
+        rf = R.ray_casting.root_finding_surface_points(model.implicit_surface, ro.clone(), rdn.clone(), near=near,
+                                                       far=far, N_steps=64, N_secant_steps=4, fill_inf=False)
+        rfn = R.ray_casting.root_finding_surface_points(model.implicit_surface, ro.clone(), rdn.clone(), near=near,
+                                                        far=far, N_steps=64, method='none', fill_inf=True)
+        st = R.ray_casting.sphere_tracing_surface_points(model.implicit_surface, ro, rdn, near=near, far=far,
+                                                         N_iters=10)
+    out.update(rays_o=ro, rays_d=rd, near=near, far=far, rf_d=rf[0], rf_pts=rf[1], rf_mask=rf[2], rf_msc=rf[3],
+               rfn_d=rfn[0], rfn_pts=rfn[1], rfn_mask=rfn[2], rfn_msc=rfn[3], st_d=st[0], st_pts=st[1],
+               st_mask=st[2])
+    save('options.npz', **out)
+
+
+def gen_volsdf_perturb(R):
+    """VolSDF perturb=True renders (random final fine samples, volsdf.py:102; NeRF++ radius strata,
+    :460-465) with every torch.rand draw recorded: config (a) on 64 rays (beta 0.1), config (c) on 64
+    rays (beta 1e-3, several convergence rounds) and VolSDF + NeRF++ on 64 rays."""
+    out = {}
+    cases = [('a', 2, 0.1, False, 'a', dict(n=8), 64, 64), ('c', 5, 1e-3, False, 'c', dict(n=8, lo=0.05, hi=0.95), 128, 128),
+             ('pp', 6, 0.1, True, 'a', dict(n=8, lo=0.0, hi=1.0), 64, 64)]
+    for key, seed, beta_init, nerfpp, cam, gi, Ns, Ni in cases:
+        sd = wg.volsdf_state(seed=seed, beta_init=beta_init, use_nerfplusplus=nerfpp)
+        model = _volsdf_model(R, sd, beta_init, use_nerfplusplus=nerfpp)
+        H, W, _, _ = wg.CAMERAS[cam]
+        ro, rd = camera_rays(R, cam, grid_idx(H, W, **gi))
+        torch.manual_seed(200 + seed)
+        with torch.no_grad(), _RecordRand() as rec:
+            rgb, depth, ex = R.volsdf.volume_render(
+                ro, rd, model, near=0.0, far=6.0, obj_bounding_radius=3.0, batched=True, calc_normal=True,
+                detailed_output=True, perturb=True, N_samples=Ns, N_importance=Ni, N_outside=32,
+                use_nerfplusplus=nerfpp, max_upsample_steps=6)
+        out.update({f'{key}_seed': seed, f'{key}_beta_init': beta_init, f'{key}_N_samples': Ns,
+                    f'{key}_N_importance': Ni, f'{key}_rays_o': ro, f'{key}_rays_d': rd, f'{key}_rgb': rgb,
+                    f'{key}_depth': depth, f'{key}_mask': ex['mask_volume'], f'{key}_normals': ex['normals_volume'],
+                    f'{key}_d_vals': ex['d_vals'], f'{key}_iter_usage': ex['iter_usage'],
+                    f'{key}_beta_map': ex['beta_map'], f'{key}_n_draws': len(rec.draws)})
+        out.update({f'{key}_u{i}': u for i, u in enumerate(rec.draws)})
+    save('volsdf_perturb.npz', **out)
+
+
 # parameters whose full gradient is stored; the large weight_v tensors keep norm, sum and a fixed
 # sample of 4096 elements (tests/test_oracle_golden.py compares those)
 def _grad_summary(named):
@@ -502,7 +591,8 @@ def main():
     only = sys.argv[1:]
     gens = dict(components=gen_components, sampling=gen_sampling, neus=gen_neus, volsdf=gen_volsdf,
                 unisurf=gen_unisurf, surface=gen_surface,
-                volsdf_nerfpp=gen_volsdf_nerfpp, perturb=gen_perturb, train=gen_train)
+                volsdf_nerfpp=gen_volsdf_nerfpp, perturb=gen_perturb, train=gen_train, options=gen_options,
+                volsdf_perturb=gen_volsdf_perturb)
     for name, fn in gens.items():
         if not only or name in only:
             fn(R)

@@ -114,11 +114,12 @@ def nerf_state(rs, prefix, D=8, W=256, input_ch=84, input_ch_view=27, skips=(4,)
     return sd
 
 
-def neus_state(seed=1, use_outside_nerf=False, variance_init=0.05, speed_factor=10.0, radius_init=0.5):
+def neus_state(seed=1, use_outside_nerf=False, variance_init=0.05, speed_factor=10.0, radius_init=0.5,
+               use_view_dirs=True):
     rs = np.random.RandomState(seed)
     sd = {'ln_s': torch.tensor([-np.log(variance_init) / speed_factor], dtype=torch.float32)}
     sd.update(surface_state(rs, 'implicit_surface.', radius_init, 1.0))
-    sd.update(radiance_state(rs, 'radiance_net.', 3 + 27 + 3 + 256))
+    sd.update(radiance_state(rs, 'radiance_net.', 3 + 27 + 3 + 256 if use_view_dirs else 3 + 256))
     if use_outside_nerf:
         sd.update(nerf_state(rs, 'nerf_outside.'))
     return sd
@@ -135,11 +136,11 @@ def volsdf_state(seed=2, beta_init=0.1, speed_factor=10.0, obj_bounding_radius=3
     return sd
 
 
-def unisurf_state(seed=3, radius_init=1.0):
+def unisurf_state(seed=3, radius_init=1.0, use_view_dirs=True):
     rs = np.random.RandomState(seed)
     sd = {}
     sd.update(surface_state(rs, 'implicit_surface.', radius_init, 2.0))
-    sd.update(radiance_state(rs, 'radiance_net.', 3 + 3 + 3 + 256))
+    sd.update(radiance_state(rs, 'radiance_net.', 3 + 3 + 3 + 256 if use_view_dirs else 3 + 256))
     return sd
 
 

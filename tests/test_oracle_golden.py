@@ -202,6 +202,23 @@ def test_volsdf_nerfpp(golden):
         close(out[k], g[gk], 1e-5, 1e-6)
 
 
+@pytest.mark.parametrize('key', ['a', 'c', 'pp'])
+def test_volsdf_perturb(golden, key):
+    """oracle VolSDF perturb=True with the reference's generator state: same draws, same order."""
+    g = golden('volsdf_perturb')
+    nerfpp = key == 'pp'
+    sd = wg.volsdf_state(seed=int(g[key + '_seed']), beta_init=float(g[key + '_beta_init']), use_nerfplusplus=nerfpp)
+    orc = VolSDFOracle(sd, use_nerfplusplus=nerfpp)
+    torch.manual_seed(200 + int(g[key + '_seed']))
+    with torch.no_grad():
+        out = orc.render(T(g[key + '_rays_o']), T(g[key + '_rays_d']), N_samples=int(g[key + '_N_samples']),
+                         N_importance=int(g[key + '_N_importance']), max_upsample_steps=6, perturb=True)
+    close(out['iter_usage'], g[key + '_iter_usage'], 0, 0)
+    close(out['d_vals'], g[key + '_d_vals'], 1e-6, 1e-6)
+    for k, gk in [('rgb', 'rgb'), ('depth_volume', 'depth'), ('mask_volume', 'mask'), ('normals_volume', 'normals')]:
+        close(out[k], g[f'{key}_{gk}'], 1e-5, 1e-6)
+
+
 def test_surface_render_root_finding(golden):
     """oracle root finding vs ray_casting.surface_render(ray_casting_algo='root_finding') and
     root_finding_surface_points with non-default cfgs (fill_inf=False, logit_tau, short march)."""
@@ -221,6 +238,44 @@ def test_surface_render_root_finding(golden):
         np.testing.assert_array_equal(msc.numpy(), g['rf2_msc'].astype(bool))
         close(dp, g['rf2_d'], 1e-6, 1e-6)
         close(p, g['rf2_pts'], 1e-6, 1e-6)
+
+
+def test_options(golden):
+    """oracle vs the reference's option renders (gen_golden.gen_options): RadianceNet without view dirs
+    (NeuS, UNISURF), UNISURF with a root-finding method other than 'secant', and root finding / sphere
+    tracing with per-ray near / far tensors."""
+    from oracle import surface
+    g = golden('options')
+    orc = NeuSOracle(wg.neus_state(seed=1, use_view_dirs=False), use_view_dirs=False)
+    with torch.no_grad():
+        out = orc.render(T(g['neus_rays_o']), T(g['neus_rays_d']))
+    close(out['d_final'], g['neus_d_final'], 1e-6, 1e-6)
+    close(out['radiance'], g['neus_radiance'], 1e-5, 1e-6)
+    for k, gk in [('rgb', 'rgb'), ('depth_volume', 'depth'), ('mask_volume', 'mask'), ('normals_volume', 'normals')]:
+        close(out[k], g['neus_' + gk], 1e-5, 1e-6)
+    uo = UNISURFOracle(wg.unisurf_state(seed=3, use_view_dirs=False), use_view_dirs=False)
+    for tag, method in [('uni', 'secant'), ('uni_nosec', 'none')]:
+        with torch.no_grad():
+            out = uo.render(T(g['uni_rays_o']), T(g['uni_rays_d']), logit_tau=float(g['uni_logit_tau']), method=method)
+        np.testing.assert_array_equal(out['mask_surface'].numpy(), g[tag + '_mask_surface'].astype(bool))
+        close(out['depth_surface'], g[tag + '_depth_surface'], 1e-6, 1e-6)
+        for k, gk in [('rgb', 'rgb'), ('depth_volume', 'depth'), ('mask_volume', 'mask'),
+                      ('normals_volume', 'normals')]:
+            close(out[k], g[f'{tag}_{gk}'], 1e-5, 1e-6)
+    net = nets.SDFNet(wg.neus_state(seed=1))
+    o, d = T(g['rays_o']), torch.nn.functional.normalize(T(g['rays_d']), dim=-1)
+    near, far = T(g['near']), T(g['far'])
+    with torch.no_grad():
+        for tag, kw in [('rf', dict(N_secant_steps=4, fill_inf=False)), ('rfn', dict(method='none', fill_inf=True))]:
+            dp, p, m, msc = surface.root_find(net.sdf, o, d, near=near, far=far, N_steps=64, **kw)
+            np.testing.assert_array_equal(m.numpy(), g[tag + '_mask'].astype(bool))
+            np.testing.assert_array_equal(msc.numpy(), g[tag + '_msc'].astype(bool))
+            close(dp, g[tag + '_d'], 1e-6, 1e-6)
+            close(p, g[tag + '_pts'], 1e-6, 1e-6)
+        dp, p, m = surface.sphere_trace(net.sdf, o, d, near=near, far=far, N_iters=10)
+        np.testing.assert_array_equal(m.numpy(), g['st_mask'].astype(bool))
+        close(dp, g['st_d'], 1e-6, 1e-6)
+        close(p, g['st_pts'], 1e-6, 1e-6)
 
 
 def train_grads_oracle(g, d_all=None):
