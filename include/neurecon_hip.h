@@ -81,14 +81,18 @@ int nr_nerf_forward(const NrNerfDesc* d, const void* packed, const float* x4, co
  * D+1 weight-normed linear layers, Softplus(beta=100) hidden activation, skip connection
  * cat([h, embed(x)]) / sqrt(2) before layer `skip`; output row 0 = sdf, rows 1..W_geo_feat =
  * geometry feature.  Supported: D=8, W=256, skip=4, multires in [1,10], W_geo_feat=256.
+ * siren != 0: SirenLayer hidden layers h = sin(30 (W h + b)) (base.py:84-115, use_siren, as in
+ * configs/volsdf_siren.yaml): D=5, W=256, no skip (skip = -1), identity embedding (multires = -1),
+ * W_geo_feat=256.
  * ------------------------------------------------------------------------------------------ */
 typedef struct {
-  int D;          /* 8   */
+  int D;          /* 8   (5 with siren) */
   int W;          /* 256 */
-  int skip;       /* 4   */
-  int multires;   /* 6   */
+  int skip;       /* 4   (-1 with siren) */
+  int multires;   /* 6   (-1 with siren) */
   int W_geo_feat; /* 256 */
   int precision;  /* NR_PREC_* */
+  int siren;      /* 0: Softplus(beta=100) layers */
 } NrSdfDesc;
 
 size_t nr_sdf_packed_bytes(const NrSdfDesc* d);
@@ -105,7 +109,8 @@ int nr_sdf_forward(const NrSdfDesc* d, const void* packed, const float* pts, int
  * input cat([embed(x), embed_view(v), normals, feature]) -> D x (Linear+ReLU, W) -> Linear(3)+Sigmoid;
  * with no_view_dirs (use_view_dirs=False, base.py:334-338, :383-384) the input is cat([embed(x),
  * feature]) and view dirs / normals are not read.
- * Supported: D=4, W=256, multires=-1 (identity on x), view_multires in {-1..7}, W_geo_feat=256.
+ * Supported: D=4 or 5, W=256, multires=-1 (identity on x), view_multires in {-1..7}, W_geo_feat=256,
+ * ReLU or (siren) sine hidden layers.
  * ------------------------------------------------------------------------------------------ */
 typedef struct {
   int D;             /* 4   */
@@ -115,6 +120,7 @@ typedef struct {
   int W_geo_feat;    /* 256 */
   int precision;
   int no_view_dirs;  /* 0: use_view_dirs=True (default) */
+  int siren;         /* hidden layers sin(30 (W h + b)) instead of ReLU (base.py:357-361); D = 4 or 5 */
 } NrRadDesc;
 
 size_t nr_radiance_packed_bytes(const NrRadDesc* d);

@@ -25,12 +25,12 @@ _c_sz = ctypes.c_size_t
 
 class NrSdfDesc(ctypes.Structure):
     _fields_ = [('D', _c_i), ('W', _c_i), ('skip', _c_i), ('multires', _c_i), ('W_geo_feat', _c_i),
-                ('precision', _c_i)]
+                ('precision', _c_i), ('siren', _c_i)]
 
 
 class NrRadDesc(ctypes.Structure):
     _fields_ = [('D', _c_i), ('W', _c_i), ('multires', _c_i), ('multires_view', _c_i), ('W_geo_feat', _c_i),
-                ('precision', _c_i), ('no_view_dirs', _c_i)]
+                ('precision', _c_i), ('no_view_dirs', _c_i), ('siren', _c_i)]
 
 
 class NrNerfDesc(ctypes.Structure):

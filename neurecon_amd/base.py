@@ -68,6 +68,18 @@ class WNLinear(nn.Module):
         return torch._weight_norm(self.weight_v, self.weight_g, 0)
 
 
+def _siren_init(in_dim, out_dim, is_first, w0=30.0, c=6.0):
+    """SirenLayer.reset_parameters (base.py:98-106): nn.Linear's init, then
+    weight ~ U(-w_std, w_std), w_std = 1/in (first layer) or sqrt(c/in)/w0; bias keeps Linear's init."""
+    w = torch.empty(out_dim, in_dim)
+    nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+    k = 1.0 / math.sqrt(in_dim)
+    b = torch.empty(out_dim).uniform_(-k, k)
+    w_std = (1 / in_dim) if is_first else (math.sqrt(c / in_dim) / w0)
+    w.uniform_(-w_std, w_std)
+    return w, b
+
+
 PRECISIONS = ('f16x3', 'fp32')
 
 
@@ -140,13 +152,16 @@ class ImplicitSurface(nn.Module):
     def __init__(self, W=256, D=8, skips=[4], W_geo_feat=256, input_ch=3, radius_init=1.0, obj_bounding_size=2.0,
                  geometric_init=True, embed_multires=6, weight_norm=True, use_siren=False, precision=None):
         super().__init__()
-        if use_siren or not weight_norm:
-            raise NotImplementedError('neurecon_amd: SIREN / non-weight-normed surface nets are out of scope')
+        if not weight_norm:
+            raise NotImplementedError('neurecon_amd: non-weight-normed surface nets are out of scope')
         self.radius_init = radius_init
         self.register_buffer('obj_bounding_size', torch.tensor([obj_bounding_size]).float())
         self.geometric_init = geometric_init
         self.D, self.W, self.W_geo_feat, self.skips = D, W, W_geo_feat, list(skips)
-        self.use_siren = False
+        self.use_siren = bool(use_siren)
+        if use_siren:  # base.py:170-172
+            assert len(skips) == 0, 'do not use skips for siren'
+            self.register_buffer('is_pretrained', torch.tensor([False], dtype=torch.bool))
         self.embed_multires = embed_multires
         self.embed_fn, in_ch = get_embedder(embed_multires)
         self.input_ch = in_ch
@@ -162,7 +177,9 @@ class ImplicitSurface(nn.Module):
             in_dim = in_ch if l == 0 else W
             w = torch.empty(out_dim, in_dim)
             b = torch.empty(out_dim)
-            if geometric_init:  # SAL / IDR sphere init (base.py:207-224)
+            if use_siren and l != D:  # SirenLayer (base.py:194-196)
+                layers.append(WNLinear(in_dim, out_dim, *_siren_init(in_dim, out_dim, l == 0)))
+            elif geometric_init and not use_siren:  # SAL / IDR sphere init (base.py:207-224)
                 if l == D:
                     nn.init.normal_(w, mean=np.sqrt(np.pi) / np.sqrt(in_dim), std=0.0001)
                     nn.init.constant_(b, -radius_init)
@@ -185,10 +202,12 @@ class ImplicitSurface(nn.Module):
 
     # -- native plumbing ----------------------------------------------------------------------
     def nr_desc(self):
+        prec = L.PREC_FP32 if self.precision == 'fp32' else L.PREC_F16X3
+        if self.use_siren:
+            return L.NrSdfDesc(self.D, self.W, -1, self.embed_multires, self.W_geo_feat, prec, 1)
         if len(self.skips) != 1:
             raise NotImplementedError('neurecon_amd: SDF nets with exactly one skip layer are supported')
-        return L.NrSdfDesc(self.D, self.W, self.skips[0], self.embed_multires, self.W_geo_feat,
-                           L.PREC_FP32 if self.precision == 'fp32' else L.PREC_F16X3)
+        return L.NrSdfDesc(self.D, self.W, self.skips[0], self.embed_multires, self.W_geo_feat, prec, 0)
 
     def nr_packed(self, device):
         """Effective weights folded (weight_norm) and packed into the kernel layout; cached until a
@@ -215,6 +234,9 @@ class ImplicitSurface(nn.Module):
         L.require_gpu(x, 'points')
         shape = x.shape[:-1]
         if wants_graph(self):  # training: differentiable sdf / nablas / feature (double backward)
+            if self.use_siren:
+                raise NotImplementedError('neurecon_amd: the training (autograd) path covers the softplus SDF net; '
+                                          'SIREN nets render (no_grad) only')
             from .training import sdf_nablas
             sdf, nab, feat = sdf_nablas(self, x, True)
             return [sdf.reshape(shape), nab.reshape(*shape, 3), feat.reshape(*shape, self.W_geo_feat)]
@@ -259,9 +281,10 @@ class RadianceNet(nn.Module):
     def __init__(self, D=4, W=256, skips=[], W_geo_feat=256, embed_multires=6, embed_multires_view=4,
                  use_view_dirs=True, weight_norm=True, use_siren=False, precision=None):
         super().__init__()
-        if use_siren or not weight_norm or skips:
-            raise NotImplementedError('neurecon_amd: RadianceNet needs weight_norm, no skips, no SIREN')
+        if not weight_norm or skips:
+            raise NotImplementedError('neurecon_amd: RadianceNet needs weight_norm and no skips')
         self.D, self.W, self.skips, self.use_view_dirs = D, W, list(skips), bool(use_view_dirs)
+        self.use_siren = bool(use_siren)
         self.embed_multires, self.embed_multires_view, self.W_geo_feat = embed_multires, embed_multires_view, W_geo_feat
         self.embed_fn, ch_pts = get_embedder(embed_multires)
         if use_view_dirs:  # base.py:334-338: without view dirs the input is cat([embed(x), feature])
@@ -270,12 +293,16 @@ class RadianceNet(nn.Module):
         else:
             in0 = ch_pts + W_geo_feat
         self.precision = default_precision() if precision is None else precision
-        self.layers = nn.ModuleList([WNLinear(in0 if l == 0 else W, 3 if l == D else W) for l in range(D + 1)])
+        # hidden layers: DenseLayer(ReLU) or SirenLayer (base.py:357-361); head: DenseLayer(Sigmoid)
+        self.layers = nn.ModuleList([
+            WNLinear(in0 if l == 0 else W, W, *_siren_init(in0 if l == 0 else W, W, l == 0))
+            if use_siren and l != D else WNLinear(in0 if l == 0 else W, 3 if l == D else W) for l in range(D + 1)])
         self._nr_cache = None
 
     def nr_desc(self):
         return L.NrRadDesc(self.D, self.W, self.embed_multires, self.embed_multires_view, self.W_geo_feat,
-                           L.PREC_FP32 if self.precision == 'fp32' else L.PREC_F16X3, 0 if self.use_view_dirs else 1)
+                           L.PREC_FP32 if self.precision == 'fp32' else L.PREC_F16X3, 0 if self.use_view_dirs else 1,
+                           1 if self.use_siren else 0)
 
     def nr_packed(self, device):
         key = _version_key(self, self.precision, device)
@@ -311,6 +338,8 @@ class RadianceNet(nn.Module):
         else:  # view dirs and normals are not inputs (base.py:383-384)
             v = n = None
         if wants_graph(self, normals, geometry_feature):
+            if self.use_siren or self.D != 4:
+                raise NotImplementedError('neurecon_amd: the training (autograd) path covers the D=4 ReLU radiance net')
             from .training import radiance
             rgb = radiance(self, x.reshape(-1, 3).float(), v, n, geometry_feature.reshape(-1, self.W_geo_feat).float())
             return rgb.reshape(*shape, 3)

@@ -22,6 +22,14 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // ---------------------------------------------------------------------------------------------
 int check_sdf_desc(const NrSdfDesc* d) {
   NR_REQUIRE(d, NR_ERR_ARG, "null NrSdfDesc");
+  if (d->siren) {
+    NR_REQUIRE(d->D == 5 && d->W == 256 && d->skip < 0 && d->multires < 0 && d->W_geo_feat == 256,
+               NR_ERR_UNSUPPORTED,
+               "SIREN SDF net: only D=5, W=256, skips=[], embed_multires=-1, W_geo_feat=256 (configs/volsdf_siren.yaml)");
+    NR_REQUIRE(d->precision == NR_PREC_FP32 || d->precision == NR_PREC_F16X3, NR_ERR_UNSUPPORTED,
+               "SDF net: unknown precision mode");
+    return NR_OK;
+  }
   NR_REQUIRE(d->D == 8 && d->W == 256 && d->skip == 4 && d->multires == 6 && d->W_geo_feat == 256,
              NR_ERR_UNSUPPORTED,
              "SDF net: only D=8, W=256, skips=[4], embed_multires=6, W_geo_feat=256 are implemented");
@@ -32,9 +40,10 @@ int check_sdf_desc(const NrSdfDesc* d) {
 
 int check_rad_desc(const NrRadDesc* d) {
   NR_REQUIRE(d, NR_ERR_ARG, "null NrRadDesc");
-  NR_REQUIRE(d->D == 4 && d->W == 256 && d->multires < 0 && d->W_geo_feat == 256 && d->multires_view <= 7,
+  NR_REQUIRE((d->D == 4 || d->D == 5) && d->W == 256 && d->multires < 0 && d->W_geo_feat == 256 &&
+                 d->multires_view <= 7,
              NR_ERR_UNSUPPORTED,
-             "radiance net: only D=4, W=256, embed_multires=-1, embed_multires_view<=7, W_geo_feat=256");
+             "radiance net: only D=4 or 5, W=256, embed_multires=-1, embed_multires_view<=7, W_geo_feat=256");
   NR_REQUIRE(d->precision == NR_PREC_FP32 || d->precision == NR_PREC_F16X3, NR_ERR_UNSUPPORTED,
              "radiance net: unknown precision mode");
   return NR_OK;
@@ -44,11 +53,15 @@ int check_rad_desc(const NrRadDesc* d) {
 SdfLayout sdf_layout(const NrSdfDesc& d) {
   SdfLayout L{};
   L.prec = d.precision;
+  L.siren = d.siren ? 1 : 0;
+  const int nops = L.siren ? kSirenOps : kSdfOps;
+  const int* KB = L.siren ? kSirenKB : kSdfKB;
+  const int* NBO = L.siren ? kSirenNBO : kSdfNBO;
   size_t off = 0;
-  for (int i = 0; i < kSdfOps; ++i) {
-    L.op_bytes[i] = (2 * kSdfKB[i] + 1) * 1024;
+  for (int i = 0; i < nops; ++i) {
+    L.op_bytes[i] = (2 * KB[i] + 1) * 1024;
     L.op_off[i] = (uint32_t)off;
-    off += (size_t)(kSdfNBO[i] / 2) * L.op_bytes[i];
+    off += (size_t)(NBO[i] / 2) * L.op_bytes[i];
   }
   static_assert(sdf_op_off(kSdfOps - 1) + (kSdfNBO[kSdfOps - 1] / 2) * (2 * kSdfKB[kSdfOps - 1] + 1) * 1024 > 0, "");
   L.scale_off = (uint32_t)off;
@@ -73,16 +86,18 @@ RadLayout rad_layout(const NrRadDesc& d) {
   L.prec = d.precision;
   L.n_small = rad_small(d);
   L.view = d.no_view_dirs ? 0 : 1;
+  L.D = d.D;
+  L.siren = d.siren ? 1 : 0;
   L.kbs = L.n_small <= 32 ? 2 : 4;
   size_t off = 0;
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < L.D; ++i) {
     const int kb = i == 0 ? 16 + L.kbs : 16;
     L.op_bytes[i] = (2 * kb + 1) * 1024;
     L.op_off[i] = (uint32_t)off;
     off += 8 * (size_t)L.op_bytes[i];
   }
   L.scale_off = (uint32_t)off;
-  off = align256(off + 4 * 4);
+  off = align256(off + 5 * 4);
   L.head_off = (uint32_t)off;
   off = align256(off + (3 * 256 + 4) * 4);
   L.total = (uint32_t)off;
@@ -571,10 +586,31 @@ int nr_sdf_pack(const NrSdfDesc* d, const float* const* W, const float* const* b
   int rc = check_sdf_desc(d);
   if (rc) return rc;
   NR_REQUIRE(W && b && packed, NR_ERR_ARG, "nr_sdf_pack: null argument");
-  for (int l = 0; l <= 8; ++l) NR_REQUIRE(W[l] && b[l], NR_ERR_ARG, "nr_sdf_pack: null layer pointer");
+  for (int l = 0; l <= d->D; ++l) NR_REQUIRE(W[l] && b[l], NR_ERR_ARG, "nr_sdf_pack: null layer pointer");
   hipStream_t st = (hipStream_t)stream;
   const SdfLayout L = sdf_layout(*d);
   char* P = (char*)packed;
+  if (L.siren) {  // S0..S4, SF, SB4..SB0 (nr_mlp.h SirenOp); layer 5 = Linear(256 -> 257)
+    const int prec = d->precision;
+    float* wmax = (float*)(P + L.scale_off);
+    float* bound = (float*)(P + L.bound_off);
+    PackOp ops[kSirenOps];
+    ops[S0] = mkop(W[0], b[0], 256, 3, 0, seg(16, 0, 256), none(), seg(4, 0, 3), none(), 1.0f, prec, wmax + S0);
+    for (int l = 1; l < 5; ++l)
+      ops[S0 + l] = mkop(W[l], b[l], 256, 256, 0, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec,
+                         wmax + S0 + l);
+    ops[SF] = mkop(W[5], b[5], 257, 256, 0, seg(16, 1, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + SF);
+    for (int l = 4; l >= 1; --l)
+      ops[SB4 + (4 - l)] = mkop(W[l], nullptr, 256, 256, 1, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f,
+                                prec, wmax + SB4 + (4 - l));
+    ops[SB0] = mkop(W[0], nullptr, 256, 3, 1, seg(4, 0, 3), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + SB0);
+    for (int i = 0; i < kSirenOps; ++i) {
+      ops[i].bound = bound + 2 * i;
+      if ((rc = launch_pack_op(ops[i], P + L.op_off[i], st))) return rc;
+    }
+    if ((rc = launch_pack_vec(W[5], 0, 256, 256, P + L.w8row0_off, st))) return rc;
+    return launch_pack_vec(b[5], 0, 1, 4, P + L.misc_off, st);
+  }
   const int in0 = 39, n3 = 217;
   const float isq2 = 1.0f / 1.41421356237309504880f;
   const int prec = d->precision;
@@ -676,22 +712,22 @@ int nr_radiance_pack(const NrRadDesc* d, const float* const* W, const float* con
   int rc = check_rad_desc(d);
   if (rc) return rc;
   NR_REQUIRE(W && b && packed, NR_ERR_ARG, "nr_radiance_pack: null argument");
-  for (int l = 0; l <= 4; ++l) NR_REQUIRE(W[l] && b[l], NR_ERR_ARG, "nr_radiance_pack: null layer pointer");
+  for (int l = 0; l <= d->D; ++l) NR_REQUIRE(W[l] && b[l], NR_ERR_ARG, "nr_radiance_pack: null layer pointer");
   hipStream_t st = (hipStream_t)stream;
   const RadLayout L = rad_layout(*d);
   char* P = (char*)packed;
   const int ns = L.n_small, ld0 = ns + 256;
-  PackOp ops[4];
+  PackOp ops[5];
   const int prec = d->precision;
   float* wmax = (float*)(P + L.scale_off);
   ops[0] = mkop(W[0], b[0], 256, ld0, 0, seg(16, 0, 256), none(), seg(16, ns, 256), seg(L.kbs, 0, ns), 1.0f, prec, wmax);
-  for (int i = 1; i < 4; ++i)
+  for (int i = 1; i < L.D; ++i)
     ops[i] = mkop(W[i], b[i], 256, 256, 0, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + i);
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < L.D; ++i) {
     if ((rc = launch_pack_op(ops[i], P + L.op_off[i], st))) return rc;
   }
-  if ((rc = launch_pack_vec(W[4], 0, 768, 768, P + L.head_off, st))) return rc;
-  if ((rc = launch_pack_vec(b[4], 0, 3, 4, P + L.head_off + 768 * 4, st))) return rc;
+  if ((rc = launch_pack_vec(W[L.D], 0, 768, 768, P + L.head_off, st))) return rc;
+  if ((rc = launch_pack_vec(b[L.D], 0, 3, 4, P + L.head_off + 768 * 4, st))) return rc;
   return NR_OK;
 }
 

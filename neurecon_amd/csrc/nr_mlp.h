@@ -24,6 +24,14 @@ __host__ __device__ constexpr uint32_t sdf_op_off(int i) {
   return off;
 }
 
+// SIREN SDF net (base.py:84-115, D=5, no skip, identity embedding): forward S0..S4, feature SF,
+// backward SB4..SB0; S0 reads the 3 coordinates from a 4-block (64-feature, zero-padded) input and
+// SB0 writes their gradient into 4 blocks, as the softplus net's F0 / B0 do
+enum SirenOp { S0, S1, S2, S3, S4, SF, SB4, SB3, SB2, SB1, SB0, kSirenOps };
+constexpr int kSirenKB[kSirenOps] = {4, 16, 16, 16, 16, 16, 16, 16, 16, 16, 16};
+constexpr int kSirenNBO[kSirenOps] = {16, 16, 16, 16, 16, 16, 16, 16, 16, 16, 4};
+static_assert(kSirenOps <= kSdfOps, "SIREN ops share SdfLayout's offset table");
+
 struct SdfLayout {
   uint32_t op_off[kSdfOps];
   uint32_t op_bytes[kSdfOps];  // bytes of one chunk of the op
@@ -33,11 +41,12 @@ struct SdfLayout {
   uint32_t misc_off;           // [0] = sdf bias
   uint32_t total;
   int prec;
+  int siren;                   // op_off / op_bytes indexed by SirenOp
 };
 
 struct RadLayout {
-  uint32_t op_off[4];
-  uint32_t op_bytes[4];
+  uint32_t op_off[5];
+  uint32_t op_bytes[5];
   uint32_t head_off;  // [3][256] weights, then [3] bias
   uint32_t scale_off; // [4] max |W| per op
   uint32_t total;
@@ -45,6 +54,8 @@ struct RadLayout {
   int kbs;            // small-input blocks (even)
   int n_small;        // 3 + view-embedding + 3, or 3 without view dirs
   int view;           // use_view_dirs: view embedding and normals in the input
+  int D;              // hidden layers (4 or 5)
+  int siren;          // sine hidden layers
 };
 
 // NeRF++ background MLP (models/base.py:395-453): 8 x (Linear+ReLU) with the input re-injected

@@ -281,7 +281,22 @@ __device__ __forceinline__ float softplus_bwd(float g, float e) {
   else return __builtin_isinf(e) ? g : g * e * __builtin_amdgcn_rcpf(e + 1.0f);
 }
 
-enum { ACT_NONE = 0, ACT_SOFTPLUS = 1, ACT_RELU = 2 };
+enum { ACT_NONE = 0, ACT_SOFTPLUS = 1, ACT_RELU = 2, ACT_SINE = 3 };
+
+// SirenLayer (base.py:84-115): h = sin(w0 z), w0 = 30, the argument rounded as torch's w0 * x.
+// The slab keeps cos(w0 z); autograd's backward is (g * cos(w0 z)) * w0 (SinBackward, then MulBackward)
+constexpr float kSirenW0 = 30.0f;
+__device__ __forceinline__ void sine_fwd(float z, float& y, float& e) {
+  const float t = fmul(kSirenW0, z);
+  y = sinf(t);
+  e = cosf(t);
+}
+__device__ __forceinline__ float sine_bwd(float g, float e) { return fmul(fmul(g, e), kSirenW0); }
+template <int P, int ACT>
+__device__ __forceinline__ float act_bwd(float g, float e) {
+  if constexpr (ACT == ACT_SINE) return sine_bwd(g, e);
+  else return softplus_bwd<P>(g, e);
+}
 
 // chunk = [A: 2*KB KB][bias slot: 32 floats (2 output blocks), [32] = 1/weight-scale; 1 KB]
 __host__ __device__ constexpr int chunk_bytes(int KB) { return (2 * KB + 1) * 1024; }
@@ -406,7 +421,7 @@ __device__ __forceinline__ void gemm_fwd(WS& ws, const char* __restrict__ op, co
   int pc = -1;
   auto drain = [&]() {
     if (pc >= 0) {
-      if constexpr (ACT == ACT_SOFTPLUS) {
+      if constexpr (ACT == ACT_SOFTPLUS || ACT == ACT_SINE) {
 #ifndef NR_EXP_NO_ESTORE  // timing experiment: skip the e-slab stores
         if (e_out) {  // streamed: non-temporal so the slab does not evict the weights from L2
           using gf4 = __attribute__((address_space(1))) f32x4;
@@ -452,6 +467,12 @@ NR_CHUNK_UNROLL
       softplus_fwd<P>(acc1[0], y1.x, p1.x); softplus_fwd<P>(acc1[1], y1.y, p1.y);
       softplus_fwd<P>(acc1[2], y1.z, p1.z); softplus_fwd<P>(acc1[3], y1.w, p1.w);
       pc = c;
+    } else if constexpr (ACT == ACT_SINE) {
+      sine_fwd(acc0[0], y0.x, p0.x); sine_fwd(acc0[1], y0.y, p0.y);
+      sine_fwd(acc0[2], y0.z, p0.z); sine_fwd(acc0[3], y0.w, p0.w);
+      sine_fwd(acc1[0], y1.x, p1.x); sine_fwd(acc1[1], y1.y, p1.y);
+      sine_fwd(acc1[2], y1.z, p1.z); sine_fwd(acc1[3], y1.w, p1.w);
+      pc = c;
     } else if constexpr (ACT == ACT_RELU) {
       y0 = make_float4(fmaxf(acc0[0], 0.f), fmaxf(acc0[1], 0.f), fmaxf(acc0[2], 0.f), fmaxf(acc0[3], 0.f));
       y1 = make_float4(fmaxf(acc1[0], 0.f), fmaxf(acc1[1], 0.f), fmaxf(acc1[2], 0.f), fmaxf(acc1[3], 0.f));
@@ -469,10 +490,10 @@ NR_CHUNK_UNROLL
 }
 
 // Backward GEMM layer: out = Wᵀ · G (no bias).  The first NBO1 output blocks are scaled by
-// softplus'(z) of the previous layer (slab e_cur, staged into LDS one chunk ahead) and rotated
+// act'(z) of the previous layer (slab e_cur, staged into LDS one chunk ahead) and rotated
 // into Y; the remaining NBO2 blocks are gradients w.r.t. the positional encoding and are handed to
 // `emb(block, value)` as produced.  The last chunk stages e_next blocks 0,1 for the next op.
-template <int P, int KBG, int NBO1, int NBO2, class WS, class EmbFn>
+template <int P, int KBG, int NBO1, int NBO2, int ACTB = ACT_SOFTPLUS, class WS, class EmbFn>
 __device__ __forceinline__ void gemm_bwd(WS& ws, const char* __restrict__ op, const char* nxt, int nxt_bytes,
                                          const float4 (&G)[16], float4 (&Y)[16], const float4* __restrict__ e_cur,
                                          const float4* __restrict__ e_next, int lane, EmbFn&& emb) {
@@ -515,10 +536,10 @@ NR_CHUNK_UNROLL
 #else
         const float4 e0 = eb[lane], e1 = eb[64 + lane];
 #endif
-        y0 = make_float4(softplus_bwd<P>(y0.x, e0.x), softplus_bwd<P>(y0.y, e0.y), softplus_bwd<P>(y0.z, e0.z),
-                         softplus_bwd<P>(y0.w, e0.w));
-        y1 = make_float4(softplus_bwd<P>(y1.x, e1.x), softplus_bwd<P>(y1.y, e1.y), softplus_bwd<P>(y1.z, e1.z),
-                         softplus_bwd<P>(y1.w, e1.w));
+        y0 = make_float4(act_bwd<P, ACTB>(y0.x, e0.x), act_bwd<P, ACTB>(y0.y, e0.y), act_bwd<P, ACTB>(y0.z, e0.z),
+                         act_bwd<P, ACTB>(y0.w, e0.w));
+        y1 = make_float4(act_bwd<P, ACTB>(y1.x, e1.x), act_bwd<P, ACTB>(y1.y, e1.y), act_bwd<P, ACTB>(y1.z, e1.z),
+                         act_bwd<P, ACTB>(y1.w, e1.w));
       }
       if constexpr (NBO1 > 0) push2<NBO1>(Y, y0, y1);
     } else {
@@ -1602,7 +1623,107 @@ void sdf4_kernel(SdfKArgs a) {
 }
 
 // =============================================================================================
-// Radiance kernel (RadianceNet): cat([x, embed_view(v), normals, feature]) -> 4x ReLU(256) -> 3
+// SIREN SDF kernel (base.py:84-115 SirenLayer, ImplicitSurface(use_siren=True) with
+// configs/volsdf_siren.yaml's D=5, skips=[], embed_multires=-1): h_{l+1} = sin(30 (W_l h_l + b_l)),
+// l = 0..4, then Linear(256 -> 257): row 0 = sdf, rows 1..256 = geometry feature.  The reverse pass
+// (autograd.grad of sdf w.r.t. x, base.py:265-282) runs back through the transposed layers with
+// the cos(30 z) slabs; the gradient w.r.t. the 3 raw coordinates is the nabla (identity embedding).
+// Same streamed-weight GEMM building blocks as sdf_kernel.
+// =============================================================================================
+template <int P, bool NABLA>
+__global__ __launch_bounds__(kThreads) void siren_sdf_kernel(SdfKArgs a) {
+  constexpr int CB = chunk_bytes(16);
+  __shared__ __attribute__((aligned(16))) char smem[kRing * CB + (NABLA ? 2 * kSlabChunk : 0)];
+  WStream<CB> ws{smem, NABLA ? smem + kRing * CB : nullptr, 0, 0, 0};
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  const SdfLayout& L = a.L;
+  const char* W = a.packed;
+  auto OP = [&](int i) { return W + L.op_off[i]; };
+  auto OPB = [&](int i) { return (int)L.op_bytes[i]; };
+  const float* wl = (const float*)(W + L.w8row0_off);  // row 0 of the last layer
+  const float bl = *(const float*)(W + L.misc_off);
+  float4* escr = uniform_ptr(a.scratch + (size_t)(blockIdx.x * kWaves + wave) * (8 * 16 * 64));
+  const bool want_feat = a.feature != nullptr;
+
+  ws.start(OP(S0), OPB(S0), OP(S0) + OPB(S0), OPB(S0));
+
+  const int64_t Pn = a.P_dev ? min(a.P, (int64_t)(*a.P_dev) * a.P_mult) : a.P;
+  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < Pn; base += (int64_t)gridDim.x * kPointsPerWG) {
+    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < Pn;
+    const int64_t p = base + wave * kTile + j;
+    const bool valid = p < Pn;
+    const int64_t pc = valid ? p : Pn - 1;
+    const float x0 = a.pts[pc * 3 + 0], x1 = a.pts[pc * 3 + 1], x2 = a.pts[pc * 3 + 2];
+    // identity embedding: features 0..2 of block 0 (lane group 0), zero padding elsewhere
+    float4 E[4];
+    E[0] = g == 0 ? make_float4(x0, x1, x2, 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int b = 1; b < 4; ++b) E[b] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 X[16], Y[16];
+    float4* e_l[5];
+#pragma unroll
+    for (int l = 0; l < 5; ++l) e_l[l] = NABLA ? escr + l * 16 * 64 : nullptr;
+
+    // ---- forward: 5 sine layers --------------------------------------------------------------
+    gemm_fwd<P, 0, 4, 16, ACT_SINE>(ws, OP(S0), OP(S1), OPB(S1), X, E, Y, e_l[0], nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_SINE>(ws, OP(S1), OP(S2), OPB(S2), Y, E, X, e_l[1], nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_SINE>(ws, OP(S2), OP(S3), OPB(S3), X, E, Y, e_l[2], nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT_SINE>(ws, OP(S3), OP(S4), OPB(S4), Y, E, X, e_l[3], nullptr, false, lane);
+    {
+      const char* n = want_feat ? OP(SF) : (NABLA ? OP(SB4) : (has_next ? OP(S0) : nullptr));
+      const int nb = want_feat ? OPB(SF) : (NABLA ? OPB(SB4) : OPB(S0));
+      gemm_fwd<P, 16, 0, 16, ACT_SINE>(ws, OP(S4), n, nb, X, E, Y, e_l[4], nullptr, false, lane);
+    }
+    // ---- last layer row 0 = sdf (VALU dot product over h5 = Y) ----------------------------------
+    float part = 0.0f;
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const float4 w = *(const float4*)(wl + 16 * b + 4 * g);
+      part = fmaf(Y[b].x, w.x, part);
+      part = fmaf(Y[b].y, w.y, part);
+      part = fmaf(Y[b].z, w.z, part);
+      part = fmaf(Y[b].w, w.w, part);
+    }
+    const float sdf = wave_sum4(part) + bl;
+    if (valid && g == 0) a.sdf[p] = sdf;
+    if (want_feat) {  // rows 1..256 (X is free: only the feature stores are kept)
+      const char* n = NABLA ? OP(SB4) : (has_next ? OP(S0) : nullptr);
+      const int nb = NABLA ? OPB(SB4) : OPB(S0);
+      gemm_fwd<P, 16, 0, 16, ACT_NONE>(ws, OP(SF), n, nb, Y, E, X, nullptr, a.feature + pc * 256, valid, lane);
+    }
+    if constexpr (NABLA) {
+      // d sdf / d z4 = W5[0, :] * 30 cos(30 z4)
+#pragma unroll
+      for (int b = 0; b < 16; ++b) {
+        const float4 w = *(const float4*)(wl + 16 * b + 4 * g);
+        const float4 e = e_l[4][b * 64 + lane];
+        X[b] = make_float4(sine_bwd(w.x, e.x), sine_bwd(w.y, e.y), sine_bwd(w.z, e.z), sine_bwd(w.w, e.w));
+      }
+      auto noemb = [](int, float4) {};
+      // d sdf / d x: features 0..2 of block 0 (lane group 0) of W0^T g
+      auto coords = [&](int eb, float4 gv) {
+        if (eb == 0 && g == 0 && valid) {
+          a.nabla[p * 3 + 0] = gv.x;
+          a.nabla[p * 3 + 1] = gv.y;
+          a.nabla[p * 3 + 2] = gv.z;
+        }
+      };
+      ws.slab_now(e_l[3], 0);
+      gemm_bwd<P, 16, 16, 0, ACT_SINE>(ws, OP(SB4), OP(SB3), OPB(SB3), X, Y, e_l[3], e_l[2], lane, noemb);
+      gemm_bwd<P, 16, 16, 0, ACT_SINE>(ws, OP(SB3), OP(SB2), OPB(SB2), Y, X, e_l[2], e_l[1], lane, noemb);
+      gemm_bwd<P, 16, 16, 0, ACT_SINE>(ws, OP(SB2), OP(SB1), OPB(SB1), X, Y, e_l[1], e_l[0], lane, noemb);
+      gemm_bwd<P, 16, 16, 0, ACT_SINE>(ws, OP(SB1), OP(SB0), OPB(SB0), Y, X, e_l[0], nullptr, lane, noemb);
+      gemm_bwd<P, 16, 0, 4, ACT_SINE>(ws, OP(SB0), has_next ? OP(S0) : nullptr, OPB(S0), X, Y, nullptr, nullptr,
+                                      lane, coords);
+    }
+  }
+  wait_vmcnt(0);  // a block without tiles still has the prologue's second chunk in flight
+}
+
+// =============================================================================================
+// Radiance kernel (RadianceNet): cat([x, embed_view(v), normals, feature]) -> D x ReLU(256) -> 3
+// (D = 4), or D = 5 SirenLayers sin(30 z) (base.py:357-361, configs/volsdf_siren.yaml)
 // =============================================================================================
 struct RadKArgs {
   const char* packed;
@@ -1632,8 +1753,9 @@ __device__ __forceinline__ float rad_small_feature(int f, const float (&x)[3], c
   return 0.0f;
 }
 
-template <int P, int KBS>
+template <int P, int KBS, int ACT, int D>
 __global__ __launch_bounds__(kThreads) void radiance_kernel(RadKArgs a) {
+  static_assert(D == 4 || D == 5, "radiance net depth");
   constexpr int CB = chunk_bytes(16 + KBS);
   __shared__ __attribute__((aligned(16))) char smem[kRing * CB];
   WStream<CB> ws{smem, nullptr, 0, 0, 0};
@@ -1676,11 +1798,18 @@ __global__ __launch_bounds__(kThreads) void radiance_kernel(RadKArgs a) {
 #pragma unroll
     for (int b = 0; b < 16; ++b) X[b] = *(const float4*)(a.feature + pc * 256 + 16 * b + 4 * g);
 
-    gemm_fwd<P, 16, KBS, 16, ACT_RELU>(ws, OP(0), OP(1), OPB(1), X, S, Y, nullptr, nullptr, false, lane);
-    gemm_fwd<P, 16, 0, 16, ACT_RELU>(ws, OP(1), OP(2), OPB(2), Y, S, X, nullptr, nullptr, false, lane);
-    gemm_fwd<P, 16, 0, 16, ACT_RELU>(ws, OP(2), OP(3), OPB(3), X, S, Y, nullptr, nullptr, false, lane);
-    gemm_fwd<P, 16, 0, 16, ACT_RELU>(ws, OP(3), has_next ? OP(0) : nullptr, OPB(0), Y, S, X, nullptr,
-                                  nullptr, false, lane);
+    gemm_fwd<P, 16, KBS, 16, ACT>(ws, OP(0), OP(1), OPB(1), X, S, Y, nullptr, nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT>(ws, OP(1), OP(2), OPB(2), Y, S, X, nullptr, nullptr, false, lane);
+    gemm_fwd<P, 16, 0, 16, ACT>(ws, OP(2), OP(3), OPB(3), X, S, Y, nullptr, nullptr, false, lane);
+    if constexpr (D == 4) {
+      gemm_fwd<P, 16, 0, 16, ACT>(ws, OP(3), has_next ? OP(0) : nullptr, OPB(0), Y, S, X, nullptr, nullptr, false,
+                                  lane);
+    } else {
+      gemm_fwd<P, 16, 0, 16, ACT>(ws, OP(3), OP(4), OPB(4), Y, S, X, nullptr, nullptr, false, lane);
+      gemm_fwd<P, 16, 0, 16, ACT>(ws, OP(4), has_next ? OP(0) : nullptr, OPB(0), X, S, Y, nullptr, nullptr, false,
+                                  lane);
+    }
+    const float4(&H)[16] = D == 4 ? X : Y;  // last hidden layer
     // head: Linear(256 -> 3) + sigmoid  (VALU dot products)
     float r[3];
 #pragma unroll
@@ -1689,10 +1818,10 @@ __global__ __launch_bounds__(kThreads) void radiance_kernel(RadKArgs a) {
 #pragma unroll
       for (int b = 0; b < 16; ++b) {
         const float4 w = *(const float4*)(head + o * 256 + 16 * b + 4 * g);
-        part = fmaf(X[b].x, w.x, part);
-        part = fmaf(X[b].y, w.y, part);
-        part = fmaf(X[b].z, w.z, part);
-        part = fmaf(X[b].w, w.w, part);
+        part = fmaf(H[b].x, w.x, part);
+        part = fmaf(H[b].y, w.y, part);
+        part = fmaf(H[b].z, w.z, part);
+        part = fmaf(H[b].w, w.w, part);
       }
       r[o] = sigmoidf_ref(wave_sum4(part) + head[3 * 256 + o]);
     }
@@ -2013,6 +2142,21 @@ int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t
   SdfKArgs a{(const char*)packed, L, pts, P, sdf, nabla, feature, (float4*)ws, nfreq, P_dev, P_mult};
   ProfScope prof(nabla ? (feature ? "sdf_nabla_feat" : "sdf_nabla") : (feature ? "sdf_feat" : "sdf_fwd"), (double)P,
                  stream);
+  if (L.siren) {
+    if (nabla) {
+      const size_t need = (size_t)grid * kScratchPerWG;
+      NR_REQUIRE(ws && ws_bytes >= need, NR_ERR_WORKSPACE, "sdf nabla workspace too small");
+      if (L.prec == NR_PREC_F16X3)
+        hipLaunchKernelGGL((siren_sdf_kernel<NR_PREC_F16X3, true>), dim3(grid), dim3(kThreads), 0, stream, a);
+      else hipLaunchKernelGGL((siren_sdf_kernel<NR_PREC_FP32, true>), dim3(grid), dim3(kThreads), 0, stream, a);
+    } else {
+      if (L.prec == NR_PREC_F16X3)
+        hipLaunchKernelGGL((siren_sdf_kernel<NR_PREC_F16X3, false>), dim3(grid), dim3(kThreads), 0, stream, a);
+      else hipLaunchKernelGGL((siren_sdf_kernel<NR_PREC_FP32, false>), dim3(grid), dim3(kThreads), 0, stream, a);
+    }
+    NR_HIP_CHECK(hipGetLastError());
+    return NR_OK;
+  }
   if (nabla) {
     const size_t need = (size_t)grid * kScratchPerWG;
     NR_REQUIRE(ws && ws_bytes >= need, NR_ERR_WORKSPACE, "sdf nabla workspace too small");
@@ -2052,17 +2196,28 @@ int launch_radiance(const RadLayout& L, const void* packed, const float* x, cons
   RadKArgs a{(const char*)packed, L, x, vdir, vdiv, vmod, normals, feature, P, rgb, nfreq_view};
   ProfScope prof("radiance", (double)P, stream);
   const bool h3 = L.prec == NR_PREC_F16X3;
-  switch (L.kbs) {
-    case 2:
-      if (h3) hipLaunchKernelGGL((radiance_kernel<NR_PREC_F16X3, 2>), dim3(grid), dim3(kThreads), 0, stream, a);
-      else hipLaunchKernelGGL((radiance_kernel<NR_PREC_FP32, 2>), dim3(grid), dim3(kThreads), 0, stream, a);
-      break;
-    case 4:
-      if (h3) hipLaunchKernelGGL((radiance_kernel<NR_PREC_F16X3, 4>), dim3(grid), dim3(kThreads), 0, stream, a);
-      else hipLaunchKernelGGL((radiance_kernel<NR_PREC_FP32, 4>), dim3(grid), dim3(kThreads), 0, stream, a);
-      break;
-    default: set_error("radiance: unsupported small-input block count"); return NR_ERR_UNSUPPORTED;
+  // (small-input blocks, activation, depth) variants
+#define NR_RAD_LAUNCH(KBS, ACT, D)                                                                            \
+  do {                                                                                                        \
+    if (h3) hipLaunchKernelGGL((radiance_kernel<NR_PREC_F16X3, KBS, ACT, D>), dim3(grid), dim3(kThreads), 0, \
+                               stream, a);                                                                    \
+    else hipLaunchKernelGGL((radiance_kernel<NR_PREC_FP32, KBS, ACT, D>), dim3(grid), dim3(kThreads), 0,     \
+                            stream, a);                                                                       \
+  } while (0)
+  if (L.kbs != 2 && L.kbs != 4) {
+    set_error("radiance: unsupported small-input block count");
+    return NR_ERR_UNSUPPORTED;
   }
+  if (!L.siren && L.D == 4) {
+    if (L.kbs == 2) NR_RAD_LAUNCH(2, ACT_RELU, 4); else NR_RAD_LAUNCH(4, ACT_RELU, 4);
+  } else if (!L.siren && L.D == 5) {
+    if (L.kbs == 2) NR_RAD_LAUNCH(2, ACT_RELU, 5); else NR_RAD_LAUNCH(4, ACT_RELU, 5);
+  } else if (L.D == 4) {
+    if (L.kbs == 2) NR_RAD_LAUNCH(2, ACT_SINE, 4); else NR_RAD_LAUNCH(4, ACT_SINE, 4);
+  } else {
+    if (L.kbs == 2) NR_RAD_LAUNCH(2, ACT_SINE, 5); else NR_RAD_LAUNCH(4, ACT_SINE, 5);
+  }
+#undef NR_RAD_LAUNCH
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;
 }

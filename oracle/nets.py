@@ -32,11 +32,18 @@ def softplus100(z):
     return F.softplus(z, beta=100, threshold=20)
 
 
-class SDFNet:
-    """ImplicitSurface (models/base.py:131-282) over a state_dict slice."""
+def sine30(z):
+    # base.py:84-91 Sine(w0=30): torch.sin(w0 * x)
+    return torch.sin(30 * z)
 
-    def __init__(self, sd, prefix='implicit_surface.', D=8, skips=(4,), multires=6, W_geo_feat=256):
+
+class SDFNet:
+    """ImplicitSurface (models/base.py:131-282) over a state_dict slice; siren=True: SirenLayer
+    hidden layers (base.py:93-115, use_siren)."""
+
+    def __init__(self, sd, prefix='implicit_surface.', D=8, skips=(4,), multires=6, W_geo_feat=256, siren=False):
         self.D, self.skips, self.multires, self.W_geo_feat = D, tuple(skips), multires, W_geo_feat
+        self.act = sine30 if siren else softplus100
         self.layers = [(wn_weight(sd, f'{prefix}surface_fc_layers.{l}'), sd[f'{prefix}surface_fc_layers.{l}.bias'])
                        for l in range(D + 1)]
 
@@ -48,7 +55,7 @@ class SDFNet:
             if i in self.skips:
                 h = torch.cat([h, xe], dim=-1) / math.sqrt(2)
             W, b = self.layers[i]
-            h = softplus100(F.linear(h, W, b))
+            h = self.act(F.linear(h, W, b))
         W, b = self.layers[self.D]
         out = F.linear(h, W, b)
         if self.W_geo_feat > 0:
@@ -70,8 +77,9 @@ class SDFNet:
 class RadianceNet:
     """RadianceNet (models/base.py:312-391)."""
 
-    def __init__(self, sd, prefix='radiance_net.', D=4, multires=-1, multires_view=4, use_view_dirs=True):
+    def __init__(self, sd, prefix='radiance_net.', D=4, multires=-1, multires_view=4, use_view_dirs=True, siren=False):
         self.D, self.multires, self.multires_view, self.use_view_dirs = D, multires, multires_view, use_view_dirs
+        self.act = sine30 if siren else torch.relu
         self.layers = [(wn_weight(sd, f'{prefix}layers.{l}'), sd[f'{prefix}layers.{l}.bias']) for l in range(D + 1)]
 
     def forward(self, x, v, normals, feature):
@@ -82,7 +90,7 @@ class RadianceNet:
             h = torch.cat([xe, feature], dim=-1)
         for i, (W, b) in enumerate(self.layers):
             z = F.linear(h, W, b)
-            h = torch.sigmoid(z) if i == self.D else torch.relu(z)
+            h = torch.sigmoid(z) if i == self.D else self.act(z)
         return h
 
 

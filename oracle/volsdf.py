@@ -112,12 +112,17 @@ def fine_sample(sdf_fn, d_init, o, d, alpha_net, beta_net, far, eps=0.1, max_ite
 
 
 class VolSDFOracle:
-    def __init__(self, sd, speed_factor=10.0, obj_bounding_radius=3.0, multires=6, use_nerfplusplus=False):
+    def __init__(self, sd, speed_factor=10.0, obj_bounding_radius=3.0, multires=6, use_nerfplusplus=False,
+                 siren=False):
         self.sd = sd
         self.speed_factor = speed_factor
         self.R = obj_bounding_radius
-        self.sdf_net = SDFNet(sd, multires=multires)
-        self.rad_net = RadianceNet(sd, multires=-1, multires_view=-1)
+        if siren:  # configs/volsdf_siren.yaml: D=5 SIREN nets, identity embedding, view embedding 4
+            self.sdf_net = SDFNet(sd, D=5, skips=(), multires=-1, siren=True)
+            self.rad_net = RadianceNet(sd, D=5, multires=-1, multires_view=4, siren=True)
+        else:
+            self.sdf_net = SDFNet(sd, multires=multires)
+            self.rad_net = RadianceNet(sd, multires=-1, multires_view=-1)
         self.nerf = NeRFNet(sd) if use_nerfplusplus else None  # use_sphere_bg = not use_nerfplusplus
 
     def forward_ab(self):

@@ -536,6 +536,41 @@ def gen_volsdf_perturb(R):
     save('volsdf_perturb.npz', **out)
 
 
+def gen_siren(R):
+    """SIREN nets of configs/volsdf_siren.yaml (base.py:84-115): ImplicitSurface(use_siren, D=5,
+    skips=[], embed_multires=-1) forward + nablas + feature on 512 points, RadianceNet(use_siren, D=5,
+    embed_multires_view=4) on 256 points, and a VolSDF render with both on 64 rays of the config-(a)
+    camera (64 + 64 samples; weights from weightgen.volsdf_siren_state, loaded as if pretrained)."""
+    sd = wg.volsdf_siren_state(seed=7)
+    surf_cfg = dict(use_siren=True, D=5, W=256, skips=[], embed_multires=-1, radius_init=1.0, geometric_init=True)
+    rad_cfg = dict(use_siren=True, D=5, W=256, skips=[], embed_multires=-1, embed_multires_view=4,
+                   use_view_dirs=True)
+    m = R.volsdf.VolSDF(beta_init=0.1, speed_factor=10.0, input_ch=3, W_geo_feat=256, obj_bounding_radius=3.0,
+                        use_nerfplusplus=False, surface_cfg=surf_cfg, radiance_cfg=rad_cfg)
+    m.load_state_dict(sd)
+    m.eval()
+    torch.manual_seed(321)
+    pts = torch.randn(512, 3) * 0.8
+    sdf, nab, h = m.implicit_surface.forward_with_nablas(pts)
+    P = 256
+    rx = torch.randn(P, 3) * 0.5
+    rv = torch.nn.functional.normalize(torch.randn(P, 3), dim=-1)
+    rn = torch.randn(P, 3)
+    rf = torch.randn(P, 256) * 0.3
+    with torch.no_grad():
+        rgb_r = m.radiance_net(rx, rv, rn, rf)
+    H, W, _, _ = wg.CAMERAS['a']
+    ro, rd = camera_rays(R, 'a', grid_idx(H, W, n=8, lo=0.0, hi=1.0))
+    with torch.no_grad():
+        rgb, depth, ex = R.volsdf.volume_render(
+            ro, rd, m, near=0.0, far=6.0, obj_bounding_radius=3.0, batched=True, calc_normal=True,
+            detailed_output=True, perturb=False, N_samples=64, N_importance=64, max_upsample_steps=6)
+    save('siren.npz', seed=7, pts=pts, sdf=sdf.detach(), nablas=nab.detach(), h=h.detach()[:64], x=rx, v=rv, n=rn,
+         f=rf, rgb_radiance=rgb_r, rays_o=ro, rays_d=rd, rgb=rgb, depth=depth, mask=ex['mask_volume'],
+         normals=ex['normals_volume'], beta_map=ex['beta_map'], iter_usage=ex['iter_usage'], d_vals=ex['d_vals'],
+         vol_sdf=ex['implicit_surface'], vol_nablas=ex['implicit_nablas'], weights=ex['visibility_weights'])
+
+
 # parameters whose full gradient is stored; the large weight_v tensors keep norm, sum and a fixed
 # sample of 4096 elements (tests/test_oracle_golden.py compares those)
 def _grad_summary(named):
@@ -592,7 +627,7 @@ def main():
     gens = dict(components=gen_components, sampling=gen_sampling, neus=gen_neus, volsdf=gen_volsdf,
                 unisurf=gen_unisurf, surface=gen_surface,
                 volsdf_nerfpp=gen_volsdf_nerfpp, perturb=gen_perturb, train=gen_train, options=gen_options,
-                volsdf_perturb=gen_volsdf_perturb)
+                volsdf_perturb=gen_volsdf_perturb, siren=gen_siren)
     for name, fn in gens.items():
         if not only or name in only:
             fn(R)

@@ -136,6 +136,42 @@ def volsdf_state(seed=2, beta_init=0.1, speed_factor=10.0, obj_bounding_radius=3
     return sd
 
 
+def siren_layers(rs, prefix, dims, w0=30.0, c=6.0, last=None):
+    """weight-normed SirenLayers (base.py:93-106 init ranges): layer l maps dims[l] -> dims[l+1];
+    first layer U(+-1/in), others U(+-sqrt(c/in)/w0), bias U(+-1/sqrt(in)); `last` = (out, in) of a
+    plain weight-normed Linear head with nn.Linear's ranges."""
+    sd = {}
+    n = len(dims) - 1
+    for l in range(n):
+        i, o = dims[l], dims[l + 1]
+        s = (1.0 / i) if l == 0 else math.sqrt(c / i) / w0
+        v = torch.tensor(rs.uniform(-s, s, size=(o, i)), dtype=torch.float32)
+        b = torch.tensor(rs.uniform(-1 / math.sqrt(i), 1 / math.sqrt(i), size=(o,)), dtype=torch.float32)
+        sd[f'{prefix}{l}.weight_g'] = torch.norm_except_dim(v, 2, 0)
+        sd[f'{prefix}{l}.weight_v'] = v
+        sd[f'{prefix}{l}.bias'] = b
+    if last is not None:
+        o, i = last
+        k = 1 / math.sqrt(i)
+        v = torch.tensor(rs.uniform(-k, k, size=(o, i)), dtype=torch.float32)
+        sd[f'{prefix}{n}.weight_g'] = torch.norm_except_dim(v, 2, 0)
+        sd[f'{prefix}{n}.weight_v'] = v
+        sd[f'{prefix}{n}.bias'] = torch.tensor(rs.uniform(-k, k, size=(o,)), dtype=torch.float32)
+    return sd
+
+
+def volsdf_siren_state(seed=7, beta_init=0.1, speed_factor=10.0):
+    """VolSDF with configs/volsdf_siren.yaml's nets: SIREN surface D=5 (3 -> 256 x5 -> 257) and SIREN
+    radiance D=5 (3 + 27 + 3 + 256 -> 256 x5 -> 3); no pretraining (the weights are loaded as-is)."""
+    rs = np.random.RandomState(seed)
+    sd = {'ln_beta': torch.tensor([np.log(beta_init) / speed_factor], dtype=torch.float32),
+          'implicit_surface.obj_bounding_size': torch.tensor([3.0]),
+          'implicit_surface.is_pretrained': torch.tensor([True])}
+    sd.update(siren_layers(rs, 'implicit_surface.surface_fc_layers.', [3] + [256] * 5, last=(257, 256)))
+    sd.update(siren_layers(rs, 'radiance_net.layers.', [3 + 27 + 3 + 256] + [256] * 5, last=(3, 256)))
+    return sd
+
+
 def unisurf_state(seed=3, radius_init=1.0, use_view_dirs=True):
     rs = np.random.RandomState(seed)
     sd = {}

@@ -53,8 +53,8 @@ def test_descriptor_validation_without_gpu(lib):
 
 def test_struct_sizes(lib):
     from neurecon_amd import _lib
-    assert ctypes.sizeof(_lib.NrSdfDesc) == 24
-    assert ctypes.sizeof(_lib.NrRadDesc) == 28
+    assert ctypes.sizeof(_lib.NrSdfDesc) == 28
+    assert ctypes.sizeof(_lib.NrRadDesc) == 32
     assert ctypes.sizeof(_lib.NrNerfDesc) == 28
 
 

@@ -219,6 +219,24 @@ def test_volsdf_perturb(golden, key):
         close(out[k], g[f'{key}_{gk}'], 1e-5, 1e-6)
 
 
+def test_siren(golden):
+    """SIREN nets (base.py:84-115) and a VolSDF render with them (configs/volsdf_siren.yaml)."""
+    g = golden('siren')
+    sd = wg.volsdf_siren_state(seed=int(g['seed']))
+    orc = VolSDFOracle(sd, siren=True)
+    s, n, h = orc.sdf_net.forward_with_nablas(T(g['pts']))
+    close(s, g['sdf'], 1e-5, 1e-6)
+    close(n, g['nablas'], 1e-5, 1e-5)
+    close(h[:64], g['h'], 1e-5, 1e-6)
+    close(orc.rad_net.forward(*[T(g[k]) for k in ('x', 'v', 'n', 'f')]), g['rgb_radiance'], 1e-5, 1e-6)
+    with torch.no_grad():
+        out = orc.render(T(g['rays_o']), T(g['rays_d']), N_samples=64, N_importance=64, max_upsample_steps=6)
+    close(out['iter_usage'], g['iter_usage'], 0, 0)
+    close(out['d_vals'], g['d_vals'], 1e-6, 1e-6)
+    for k, gk in [('rgb', 'rgb'), ('depth_volume', 'depth'), ('mask_volume', 'mask'), ('normals_volume', 'normals')]:
+        close(out[k], g[gk], 1e-5, 1e-6)
+
+
 def test_surface_render_root_finding(golden):
     """oracle root finding vs ray_casting.surface_render(ray_casting_algo='root_finding') and
     root_finding_surface_points with non-default cfgs (fill_inf=False, logit_tau, short march)."""
