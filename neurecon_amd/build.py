@@ -24,6 +24,15 @@ FLAGS = ['-O3', '-std=c++17', '-fPIC', f'--offload-arch={ARCH}', '-I', CSRC, '-I
          '-munsafe-fp-atomics', '-Wno-unused-result']
 
 
+# per-file extra flags: the MLP kernels keep scalar fp32 VALU beside their MFMAs (the SLP vectoriser
+# would pack adjacent f32 ops into v_pk_*, which cost ~22 extra cycles there, MI355X_MICROARCH.md)
+FILE_FLAGS = {'nr_mlp.hip': ['-fno-slp-vectorize']}
+
+
+def flags_for(src):
+    return FLAGS + FILE_FLAGS.get(os.path.basename(src), [])
+
+
 def _sources():
     return sorted(glob.glob(os.path.join(CSRC, '*.hip')))
 
@@ -41,7 +50,7 @@ def up_to_date():
 
 def _compile(src):
     obj = os.path.join(OUT, os.path.basename(src) + '.o')
-    cmd = [HIPCC] + FLAGS + ['-c', src, '-o', obj]
+    cmd = [HIPCC] + flags_for(src) + ['-c', src, '-o', obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f'hipcc failed for {src}:\n{r.stderr}')

@@ -12,7 +12,8 @@
     (defined(NR_EXP_NO_DMA) || defined(NR_EXP_NO_ESTORE) || defined(NR_EXP_NO_ELOAD) ||             \
      defined(NR_EXP_NO_SOFTPLUS) || defined(NR_EXP_NO_SPLIT) || defined(NR_EXP_NO_BARRIER) ||       \
      defined(NR_EXP_UNROLL) || defined(NR_EXP_NO_PINGPONG) || defined(NR_EXP_NO_EPI) ||             \
-     defined(NR_EXP_NO_MFMA))
+     defined(NR_EXP_NO_MFMA) || defined(NR_EXP_NO_TRANS) || defined(NR_EXP_NO_EPISPLIT) ||   \
+     defined(NR_EXP_SHARED_W))
 #error "NR_EXP_* experiment switches are for tools/build_variants.py builds only"
 #endif
 

@@ -774,15 +774,18 @@ __device__ __forceinline__ void split8s(float4 a, float4 b, float sc, f16x8& h, 
   h = __builtin_bit_cast(f16x8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
   l = __builtin_bit_cast(f16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
 }
-// ... with the lo halves from v_fma_mix (f16(v*sc - hi) fused, written straight into the packed
-// halves), parked in AGPRs: B operands are read only by MFMAs, which take AGPR sources directly
+// ... with both halves from v_fma_mix, written straight into the packed f16 pairs: hi = f16(v*sc)
+// (one rounding of the exact product), lo = f16(v*sc - hi); no packed-fp32 multiply (v_pk_mul_f32
+// issued beside MFMAs costs ~22 cycles more than scalar VALU, MI355X_MICROARCH.md).  The pairs are
+// parked in AGPRs: B operands are read only by MFMAs, which take AGPR sources directly
 __device__ __forceinline__ void split8a(float4 a, float4 b, float sc, f16x8& h, f16x8& l) {
   const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
   uint32_t hw[4], lw[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const f2v p = f2v{v[2 * i], v[2 * i + 1]} * f2v{sc, sc};
-    const uint32_t hh = cvt_pk_h(p.x, p.y);
+    uint32_t hh;
+    asm volatile("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(hh) : "v"(v[2 * i]), "v"(sc));
+    asm volatile("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(hh) : "v"(v[2 * i + 1]), "v"(sc));
     uint32_t lo;
     asm volatile("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(lo) : "v"(v[2 * i]), "v"(sc), "v"(hh));
     asm volatile("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
@@ -821,31 +824,32 @@ __device__ __forceinline__ void softplus3(float z, float& y, float& s) {
   y = lin ? z : yy;
   if constexpr (DERIV) s = lin ? 1.0f : ex * __builtin_amdgcn_rcpf(u);
 }
-// the same on a pair, with packed fp32 arithmetic and 100 log2(e) folded into one multiply
-// (the linear-branch test t > 20 becomes t log2(e) > 20 log2(e); differs from softplus3 by
-// rounding only)
+// the same on a pair with 100 log2(e) folded into one multiply (the linear-branch test t > 20
+// becomes t log2(e) > 20 log2(e); differs from softplus3 by rounding only).  Scalar fp32 on purpose:
+// this runs beside MFMAs, where packed fp32 VALU costs ~22 extra cycles (MI355X_MICROARCH.md)
+__device__ __forceinline__ void softplus1(float z, float& y, float& s) {
+  const float t = z * 144.269504088896341f;
+  const float ex = __builtin_amdgcn_exp2f(t);
+  const float u = ex + 1.0f;
+  const bool lin = t > 28.8539008f;
+  y = lin ? z : __builtin_amdgcn_logf(u) * (0.693147180559945309f * 0.01f);
+  s = lin ? 1.0f : ex * __builtin_amdgcn_rcpf(u);
+}
 template <bool DERIV>
 __device__ __forceinline__ void softplus_pk(float z0, float z1, float& y0, float& y1, float& s0, float& s1) {
-  const f2v z = {z0, z1};
-  const f2v t = z * f2v{144.269504088896341f, 144.269504088896341f};
-  const f2v ex = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
-  const f2v u = ex + f2v{1.0f, 1.0f};
-  const f2v yy = f2v{__builtin_amdgcn_logf(u.x), __builtin_amdgcn_logf(u.y)} *
-                 f2v{0.693147180559945309f * 0.01f, 0.693147180559945309f * 0.01f};
-  const bool l0 = t.x > 28.8539008f, l1 = t.y > 28.8539008f;
-  y0 = l0 ? z0 : yy.x;
-  y1 = l1 ? z1 : yy.y;
+  float d0, d1;
+  softplus1(z0, y0, d0);
+  softplus1(z1, y1, d1);
   if constexpr (DERIV) {
-    const f2v sv = ex * f2v{__builtin_amdgcn_rcpf(u.x), __builtin_amdgcn_rcpf(u.y)};
-    s0 = l0 ? 1.0f : sv.x;
-    s1 = l1 ? 1.0f : sv.y;
+    s0 = d0;
+    s1 = d1;
   }
 }
+// a * m + b per component as scalar FMAs (nr_mlp.hip is built without SLP vectorisation, so these
+// stay v_fma_f32: packed fp32 beside MFMAs is an anti-lever, MI355X_MICROARCH.md)
 __device__ __forceinline__ float4 fma4s(f32x4 a, float m, float4 b) {
-  const f2v m2 = {m, m};
-  const f2v lo = __builtin_elementwise_fma(f2v{a[0], a[1]}, m2, f2v{b.x, b.y});
-  const f2v hi = __builtin_elementwise_fma(f2v{a[2], a[3]}, m2, f2v{b.z, b.w});
-  return make_float4(lo.x, lo.y, hi.x, hi.y);
+  return make_float4(__builtin_fmaf(a[0], m, b.x), __builtin_fmaf(a[1], m, b.y), __builtin_fmaf(a[2], m, b.z),
+                     __builtin_fmaf(a[3], m, b.w));
 }
 
 using gf4 = __attribute__((address_space(1))) f32x4;
@@ -1185,6 +1189,13 @@ __device__ __forceinline__ void pend_chunk(Pend4& pd, float4* base, int first_bl
 // The running max tracks max(L, t) >= 0; finish() scales it by ln2/100.
 
 template <bool NABLA>
+#ifdef NR_EXP_NO_TRANS  // timing experiment: epilogue transcendentals replaced by moves (results are garbage)
+#define NR_EXP2(x) (x)
+#define NR_LOG2(x) (x)
+#else
+#define NR_EXP2(x) __builtin_amdgcn_exp2f(x)
+#define NR_LOG2(x) __builtin_amdgcn_logf(x)
+#endif
 struct FwdEpi4 {
   f16x8 (&oh)[2][12];
   f16x8 (&ol)[2][12];
@@ -1205,15 +1216,15 @@ struct FwdEpi4 {
       for (int i = 0; i < 16; ++i) e[i] = fminf(zval(zz, i), 126.0f);
     } else if (st == 1) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) e[i] = __builtin_amdgcn_exp2f(e[i]);
+      for (int i = 0; i < 16; ++i) e[i] = NR_EXP2(e[i]);
     } else if (st == 2) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) e[i] = e[i] + 1.0f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) L[i] = __builtin_amdgcn_logf(e[i]);
+      for (int i = 0; i < 8; ++i) L[i] = NR_LOG2(e[i]);
     } else if (st == 3) {
 #pragma unroll
-      for (int i = 8; i < 16; ++i) L[i] = __builtin_amdgcn_logf(e[i]);
+      for (int i = 8; i < 16; ++i) L[i] = NR_LOG2(e[i]);
     } else if (st == 4) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) m[i] = fmaxf(L[i], zval(zz, i));
@@ -1238,11 +1249,15 @@ struct FwdEpi4 {
           }
       }
     } else if (st == 6) {
+#ifndef NR_EXP_NO_EPISPLIT  // timing experiment: next operand not written (results are garbage)
       split8a(make_float4(m[0], m[1], m[2], m[3]), make_float4(m[4], m[5], m[6], m[7]), sc[0] * kC, oh[0][c],
               ol[0][c]);
+#endif
     } else {
+#ifndef NR_EXP_NO_EPISPLIT
       split8a(make_float4(m[8], m[9], m[10], m[11]), make_float4(m[12], m[13], m[14], m[15]), sc[1] * kC, oh[1][c],
               ol[1][c]);
+#endif
 #ifndef NR_EXP_NO_ESTORE  // timing experiment: softplus' slab not written
       if constexpr (NABLA) pend_chunk(pd, sl, 2 * c, pd.v[0], pd.v[1], pd.v[2], pd.v[3], lane, true);
 #endif
@@ -1309,14 +1324,14 @@ struct BwdEpi4 {
       if (k < 2) {  // g * softplus'(z) = g - g 2^-L  (FwdEpi4's slab)
         const float4 Lv = ws.slab_read()[(2 * k + q) * 64 + lane];
         const float4 gv = zz.z[q][k];
-        y[q][k] = make_float4(__builtin_fmaf(-gv.x, __builtin_amdgcn_exp2f(-Lv.x), gv.x),
-                              __builtin_fmaf(-gv.y, __builtin_amdgcn_exp2f(-Lv.y), gv.y),
-                              __builtin_fmaf(-gv.z, __builtin_amdgcn_exp2f(-Lv.z), gv.z),
-                              __builtin_fmaf(-gv.w, __builtin_amdgcn_exp2f(-Lv.w), gv.w));
+        y[q][k] = make_float4(__builtin_fmaf(-gv.x, NR_EXP2(-Lv.x), gv.x), __builtin_fmaf(-gv.y, NR_EXP2(-Lv.y), gv.y),
+                              __builtin_fmaf(-gv.z, NR_EXP2(-Lv.z), gv.z), __builtin_fmaf(-gv.w, NR_EXP2(-Lv.w), gv.w));
       } else if (k == 2) {
         mrun[q] = amax8(mrun[q], y[q][0], y[q][1]);
       } else {
+#ifndef NR_EXP_NO_EPISPLIT
         split8a(y[q][0], y[q][1], sc[q], oh[q][c], ol[q][c]);
+#endif
         if (q == 1) ws.slab_consumed();
       }
     } else if (st == 7) {
@@ -1345,6 +1360,12 @@ void sdf4_kernel(SdfKArgs a) {
   auto OP = [&](int i) {  // ops packed back to back (nr_mlp.h)
     const char* w = W;
     asm volatile("" : "+s"(w));
+#ifdef NR_EXP_SHARED_W  // timing experiment: backward ops stream the forward ops' bytes (half the footprint)
+    if (i >= B7) {
+      constexpr int map[8] = {F1, F2, F3, F4, F5, F6, F7, F1};  // B7..B0
+      return w + sdf_op_off(map[i - B7]);
+    }
+#endif
     return w + sdf_op_off(i);
   };
   const float b8 = *(const float*)(W + a.L.misc_off);

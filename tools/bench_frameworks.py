@@ -24,6 +24,22 @@ def rays(dev, key='b'):
     return ro, rd
 
 
+def mlp_roofline(ks, precision, rad_in):
+    """per MLP kernel type: launches, ms, executed TFLOP/s and fraction of the matrix peak (bench.py's
+    MAC counts; the radiance net's first layer has rad_in inputs)"""
+    import bench as B
+    peak = B.FP32_MFMA_PEAK_TFLOPS if precision == 'fp32' else B.F16X3_PEAK_TFLOPS
+    mac = dict(B.KERNEL_MAC, radiance=rad_in * 256 + 3 * 256 * 256 + 3 * 256)
+    out = {}
+    for name, (n, ms, units) in ks.items():
+        # sdf_fwd runs inside VolSDF's sampler on device-side counts: its recorded units are the
+        # launch capacity, not the points evaluated, so no rate is derived for it
+        if name in mac and name != 'sdf_fwd' and n and ms > 0:
+            tf = units * 2.0 * mac[name] / (ms * 1e-3) / 1e12
+            out[name] = {'launches': n, 'ms': round(ms, 3), 'tflops': round(tf, 1), 'frac': round(tf / peak, 4)}
+    return out
+
+
 def timeit(fn, steps, warmup):
     from neurecon_amd import _lib as L
     for _ in range(warmup):
@@ -61,12 +77,14 @@ def main():
         _, _, ex = volsdf.volume_render(ro, rd, mv, **dict(kw, detailed_output=True))
     it = ex['iter_usage'].flatten()
     out['volsdf'] = {'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3, 'kernels': ks,
+                     'roofline': mlp_roofline(ks, args.precision, 265),
                      'iter_usage': {str(k): int((it == k).sum()) for k in it.unique().tolist()}}
     mu = unisurf_model(wg.unisurf_state(seed=3), precision=args.precision)
     with torch.no_grad():
         dt, ks = timeit(lambda: unisurf.volume_render(ro, rd, mu, batched=True, calc_normal=True,
                                                       detailed_output=False, logit_tau=0.0), args.steps, args.warmup)
-    out['unisurf'] = {'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3, 'kernels': ks}
+    out['unisurf'] = {'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3, 'kernels': ks,
+                      'roofline': mlp_roofline(ks, args.precision, 265)}
     print(json.dumps(out, default=str), flush=True)
     if args.configs:
         print(json.dumps(configs(args), default=str), flush=True)
@@ -87,20 +105,23 @@ def configs(args):
               N_importance=128, max_upsample_steps=6)
     with torch.no_grad():
         dt, ks = timeit(lambda: volsdf.volume_render(ro, rd, mv, **kw), args.steps, args.warmup)
-    res['c_volsdf_2048x256'] = {'rays': ro.shape[1], 'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3}
+    res['c_volsdf_2048x256'] = {'rays': ro.shape[1], 'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3,
+                                'roofline': mlp_roofline(ks, args.precision, 265)}
     ro, rd = rays(dev, 'd')
     mn = neus_model(wg.neus_state(seed=4, use_outside_nerf=True), use_outside_nerf=True, precision=args.precision)
     kw = dict(obj_bounding_radius=1.0, batched=True, calc_normal=True, detailed_output=False, N_samples=64,
               N_importance=64, N_outside=32)
     with torch.no_grad():
         dt, ks = timeit(lambda: neus.volume_render(ro, rd, mn, **kw), max(1, args.steps // 2), 1)
-    res['d_neus_nerfpp_800x600'] = {'rays': ro.shape[1], 'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3}
+    res['d_neus_nerfpp_800x600'] = {'rays': ro.shape[1], 'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3,
+                                    'roofline': mlp_roofline(ks, args.precision, 289)}
     ro, rd = rays(dev, 'e')
     mu = unisurf_model(wg.unisurf_state(seed=3), precision=args.precision)
     with torch.no_grad():
         dt, ks = timeit(lambda: unisurf.volume_render(ro, rd, mu, batched=True, calc_normal=True,
                                                       detailed_output=False, logit_tau=0.0), args.steps, args.warmup)
-    res['e_unisurf_4096'] = {'rays': ro.shape[1], 'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3}
+    res['e_unisurf_4096'] = {'rays': ro.shape[1], 'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3,
+                             'roofline': mlp_roofline(ks, args.precision, 265)}
     return res
 
 

@@ -1,6 +1,8 @@
 """Build timing-experiment variants of libnrhip.so into neurecon_amd/_exp/ (select one at run time
 with NR_LIB=...).  Variants switch off parts of the MLP kernels (results are NOT valid) to measure
-what each part costs: NR_EXP_NO_DMA, NR_EXP_NO_ESTORE, NR_EXP_NO_ELOAD."""
+what each part costs: NR_EXP_NO_DMA, NR_EXP_NO_ESTORE, NR_EXP_NO_ELOAD, NR_EXP_NO_EPI, NR_EXP_NO_MFMA,
+NR_EXP_NO_TRANS (epilogue transcendentals), NR_EXP_NO_EPISPLIT (next-operand split),
+NR_EXP_SHARED_W (backward ops re-stream the forward weights: half the weight footprint)."""
 import os
 import subprocess
 import sys
@@ -27,6 +29,10 @@ VARIANTS = {
     'v3nomfma': ['-DNR_EXP_NO_MFMA'],
     'v3noslab': ['-DNR_EXP_NO_ESTORE', '-DNR_EXP_NO_ELOAD'],
     'unroll_nosplit': ['-DNR_EXP_UNROLL', '-DNR_EXP_NO_SPLIT'],
+    'v3notrans': ['-DNR_EXP_NO_TRANS'],
+    'sharedw': ['-DNR_EXP_SHARED_W'],
+    'v3noepisplit': ['-DNR_EXP_NO_EPISPLIT'],
+    'v3nomfma_noepi': ['-DNR_EXP_NO_MFMA', '-DNR_EXP_NO_EPI'],
 }
 
 
@@ -35,7 +41,7 @@ def one(name):
     objs = []
     for src in B._sources():
         obj = os.path.join(out_dir, f'{name}_{os.path.basename(src)}.o')
-        subprocess.check_call([B.HIPCC] + B.FLAGS + ['-DNR_VARIANT_BUILD'] + VARIANTS[name] + ['-c', src, '-o', obj])
+        subprocess.check_call([B.HIPCC] + B.flags_for(src) + ['-DNR_VARIANT_BUILD'] + VARIANTS[name] + ['-c', src, '-o', obj])
         objs.append(obj)
     lib = os.path.join(out_dir, f'libnrhip_{name}.so')
     subprocess.check_call([B.HIPCC, '-shared', '-fPIC', f'--offload-arch={B.ARCH}', '-o', lib] + objs)

@@ -15,7 +15,7 @@ def main():
     ap.add_argument('--points', type=int, default=524288)
     ap.add_argument('--iters', type=int, default=5)
     ap.add_argument('--precision', default='f16x3')
-    ap.add_argument('--mode', default='nabla', choices=['nabla', 'fwd', 'radiance'])
+    ap.add_argument('--mode', default='nabla', choices=['nabla', 'nabla0', 'fwd', 'radiance'])
     a = ap.parse_args()
     from neurecon_amd.base import ImplicitSurface, RadianceNet
     torch.manual_seed(0)
@@ -28,6 +28,8 @@ def main():
                             precision=a.precision).cuda().eval()
             _, n, h = s.forward_with_nablas(x)
             fn = lambda: r.forward(x, x, n, h)
+        elif a.mode == 'nabla0':  # sdf + nablas without the geometry feature (the sample launches)
+            fn = lambda: s._run(x, nabla=True, feature=False)
         elif a.mode == 'fwd':
             fn = lambda: s.forward(x)
         else:
