@@ -450,6 +450,26 @@ int nr_neus_composite_bwd(const float* sdf, const float* s_dev, const float* rad
                           int white_bkgd, const float* g_rgb, const float* g_depth, const float* g_acc,
                           const float* g_weights, float* d_sdf, float* d_rad, float* d_s, void* workspace,
                           size_t workspace_bytes, void* stream);
+/* NeRF++ background in the training step (neus.py:303-343):
+ *   nr_nerf_train_input  x_emb [R*M, 84] = Embedder(4, 10)([p/|p|, 1/|p|]), p = o + d_out*dir;
+ *                        v_emb [R*M, 27] = Embedder(3, 4)(dir); inside [R, n_mid] = |p_k| <= r_obj
+ *                        for the first n_mid (= S-1 mid-point) depths
+ *   nr_neus_composite_bg_fwd / _bwd  the compositing with the background merged (neus.py:325-352):
+ *                        sdf [R,S], radiance [R,S-1,3] of the surface net, sigma_out [R,M] and
+ *                        radiance_out [R,M,3] of the background net at d_out [R,M] (M = S-1+N_outside);
+ *                        weights / alpha [R,M]; backward also -> d sigma_out, d radiance_out */
+int nr_nerf_train_input(const float* rays_o, const float* rays_d, const float* d_out, int64_t R, int M, int n_mid,
+                        float r_obj, float* x_emb, float* v_emb, uint8_t* inside, void* stream);
+int nr_neus_composite_bg_fwd(const float* sdf, const float* s_dev, const float* rad, const float* sigma_out,
+                             const float* rad_out, const float* d_out, const uint8_t* inside, int64_t R, int S, int M,
+                             int white_bkgd, float* rgb, float* depth, float* acc, float* weights, float* alpha,
+                             float* cdf, void* stream);
+size_t nr_neus_composite_bg_bwd_workspace_bytes(int64_t R, int S, int M);
+int nr_neus_composite_bg_bwd(const float* sdf, const float* s_dev, const float* rad, const float* sigma_out,
+                             const float* rad_out, const float* d_out, const uint8_t* inside, int64_t R, int S, int M,
+                             int white_bkgd, const float* g_rgb, const float* g_depth, const float* g_acc,
+                             const float* g_weights, float* d_sdf, float* d_rad, float* d_sigma_out,
+                             float* d_rad_out, float* d_s, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Opt-in kernel timing (diagnostics / bench roofline).  While enabled, every kernel launch of

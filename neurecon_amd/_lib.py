@@ -159,6 +159,12 @@ _SIGS = {
     'nr_neus_composite_bwd_workspace_bytes': (_c_sz, [_c_i64, _c_i]),
     'nr_neus_composite_bwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
                                      _c_p, _c_p, _c_sz, _c_p]),
+    'nr_nerf_train_input': (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, ctypes.c_float, _c_p, _c_p, _c_p, _c_p]),
+    'nr_neus_composite_bg_fwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_i, _c_p, _c_p,
+                                        _c_p, _c_p, _c_p, _c_p, _c_p]),
+    'nr_neus_composite_bg_bwd_workspace_bytes': (_c_sz, [_c_i64, _c_i, _c_i]),
+    'nr_neus_composite_bg_bwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_i, _c_p, _c_p,
+                                        _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
     'nr_profile_enable': (_c_i, [_c_i]),
     'nr_profile_read': (_c_i, [ctypes.POINTER(NrKernelStat), _c_i, ctypes.POINTER(_c_i)]),
 }

@@ -330,6 +330,206 @@ __global__ void neus_composite_bwd_kernel(const float* __restrict__ sdf, const f
   d_s[r] = (float)sbar;
 }
 
+// ---- NeRF++ background in the training step (neus.py:303-343) ------------------------------------
+// inputs of the background MLP at the R x M depths d_out (= cat([d_mid, d_vals_out])): p = o + d dir,
+// x4 = [p / |p|, 1 / |p|] embedded with 10 log-sampled frequencies (Embedder(input_dim=4)), the view
+// direction embedded with 4; inside[k] = |p_k| <= r_obj for the S-1 mid-points (k < n_mid)
+__device__ __forceinline__ float emb4_f(int f, const float (&x)[4]) {
+  if (f < 4) return x[f];
+  const int fp = f - 4, band = fp >> 3, m = fp & 7;
+  const float v = fmul(x[m & 3], (float)(1 << band));
+  return m < 4 ? sinf(v) : cosf(v);
+}
+__global__ void nerf_train_input_kernel(const float* __restrict__ ro, const float* __restrict__ rd,
+                                        const float* __restrict__ d_out, int64_t R, int M, int n_mid, float r_obj,
+                                        float* __restrict__ x_emb, float* __restrict__ v_emb,
+                                        uint8_t* __restrict__ inside) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * M) return;
+  const int64_t r = i / M;
+  const int k = (int)(i - r * M);
+  const float d = d_out[i];
+  const float px = fadd(ro[r * 3 + 0], fmul(rd[r * 3 + 0], d)), py = fadd(ro[r * 3 + 1], fmul(rd[r * 3 + 1], d)),
+              pz = fadd(ro[r * 3 + 2], fmul(rd[r * 3 + 2], d));
+  const float rr = norm3_ref(px, py, pz);
+  const float x4[4] = {fdiv(px, rr), fdiv(py, rr), fdiv(pz, rr), fdiv(1.0f, rr)};
+  for (int f = 0; f < 84; ++f) x_emb[i * 84 + f] = emb4_f(f, x4);
+  const float vs[3] = {rd[r * 3], rd[r * 3 + 1], rd[r * 3 + 2]};
+  for (int f = 0; f < 27; ++f) v_emb[i * 27 + f] = emb_f(f, vs, 4);
+  if (k < n_mid) inside[r * n_mid + k] = rr <= r_obj ? 1 : 0;
+}
+
+// F.softplus (beta 1, threshold 20) and its derivative (softplus_backward)
+__device__ __forceinline__ float sp1(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
+__device__ __forceinline__ double sp1_grad(float x) { return x > 20.0f ? 1.0 : 1.0 / (1.0 + exp(-(double)x)); }
+
+// composite with the background merged (neus.py:325-352): sample k < S-1 takes the SDF alpha and the
+// radiance net's colour where inside[k], else the background's; k >= S-1 are background samples.
+// alpha_out = 1 - exp(-softplus(sigma) dist), dist = d_{k+1} - d_k (1e10 for the last).
+__global__ void neus_composite_bg_fwd_kernel(const float* __restrict__ sdf, const float* __restrict__ s_dev,
+                                             const float* __restrict__ rad, const float* __restrict__ sig_o,
+                                             const float* __restrict__ rad_o, const float* __restrict__ d_out,
+                                             const uint8_t* __restrict__ inside, int64_t R, int S, int M,
+                                             int white_bkgd, float* __restrict__ rgb, float* __restrict__ depth,
+                                             float* __restrict__ acc, float* __restrict__ w_out,
+                                             float* __restrict__ alpha_out, float* __restrict__ cdf_out) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const float s = *s_dev;
+  const int S1 = S - 1;
+  const float* sd = sdf + r * S;
+  const float* dk = d_out + r * M;
+  double T = 1.0, a_acc = 0.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
+  float cp = sigmoidf_ref(fmul(sd[0], s));
+  if (cdf_out) cdf_out[r * S] = cp;
+  for (int k = 0; k < M; ++k) {
+    const float dist = k + 1 < M ? fsub(dk[k + 1], dk[k]) : 1e10f;
+    const float a_o = fsub(1.0f, expf(fmul(-sp1(sig_o[r * M + k]), dist)));
+    float al = a_o;
+    const float* col = rad_o + (r * M + k) * 3;
+    if (k < S1) {
+      const float cn = sigmoidf_ref(fmul(sd[k + 1], s));
+      if (cdf_out) cdf_out[r * S + k + 1] = cn;
+      const float a_in = fmaxf(fdiv(fsub(cp, cn), fadd(cp, 1e-10f)), 0.0f);
+      cp = cn;
+      if (inside[r * S1 + k]) {
+        al = a_in;
+        col = rad + (r * S1 + k) * 3;
+      }
+    }
+    const float w = fmul(al, (float)T);
+    T *= (double)fadd(fsub(1.0f, al), 1e-10f);
+    c0 += (double)fmul(w, col[0]);
+    c1 += (double)fmul(w, col[1]);
+    c2 += (double)fmul(w, col[2]);
+    a_acc += (double)w;
+    w_out[r * M + k] = w;
+    if (alpha_out) alpha_out[r * M + k] = al;
+  }
+  const float accf = (float)a_acc;
+  const float den = fadd(accf, 1e-10f);
+  double dep = 0.0;
+  for (int k = 0; k < M; ++k) dep += (double)fmul(fdiv(w_out[r * M + k], den), dk[k]);
+  float o0 = (float)c0, o1 = (float)c1, o2 = (float)c2;
+  if (white_bkgd) {
+    const float bg = fsub(1.0f, accf);
+    o0 = fadd(o0, bg); o1 = fadd(o1, bg); o2 = fadd(o2, bg);
+  }
+  rgb[r * 3 + 0] = o0;
+  rgb[r * 3 + 1] = o1;
+  rgb[r * 3 + 2] = o2;
+  depth[r] = (float)dep;
+  acc[r] = accf;
+}
+
+// backward of the above -> d sdf [R,S], d radiance [R,S-1,3], d sigma_out [R,M], d radiance_out
+// [R,M,3], d s per ray [R].  Work rows (floats): c [S], alpha [M], T [M], w [M], wbar [M], a_in [S-1]
+__global__ void neus_composite_bg_bwd_kernel(const float* __restrict__ sdf, const float* __restrict__ s_dev,
+                                             const float* __restrict__ rad, const float* __restrict__ sig_o,
+                                             const float* __restrict__ rad_o, const float* __restrict__ d_out,
+                                             const uint8_t* __restrict__ inside, int64_t R, int S, int M,
+                                             int white_bkgd, const float* __restrict__ g_rgb,
+                                             const float* __restrict__ g_depth, const float* __restrict__ g_acc,
+                                             const float* __restrict__ g_w, float* __restrict__ work,
+                                             float* __restrict__ d_sdf, float* __restrict__ d_rad,
+                                             float* __restrict__ d_sig, float* __restrict__ d_rad_o,
+                                             float* __restrict__ d_s) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const int S1 = S - 1;
+  const float s = *s_dev;
+  const float* sd = sdf + r * S;
+  const float* dk = d_out + r * M;
+  float* c = work + r * (size_t)(2 * S + 4 * M);
+  float* al = c + S;
+  float* Tt = al + M;
+  float* w = Tt + M;
+  float* wb = w + M;
+  float* ain = wb + M;
+  for (int i = 0; i < S; ++i) c[i] = sigmoidf_ref(fmul(sd[i], s));
+  auto is_in = [&](int k) { return k < S1 && inside[r * S1 + k] != 0; };
+  double T = 1.0, a_acc = 0.0, wd = 0.0;
+  for (int k = 0; k < M; ++k) {
+    float a;
+    if (k < S1) ain[k] = fmaxf(fdiv(fsub(c[k], c[k + 1]), fadd(c[k], 1e-10f)), 0.0f);
+    if (is_in(k)) {
+      a = ain[k];
+    } else {
+      const float dist = k + 1 < M ? fsub(dk[k + 1], dk[k]) : 1e10f;
+      a = fsub(1.0f, expf(fmul(-sp1(sig_o[r * M + k]), dist)));
+    }
+    al[k] = a;
+    Tt[k] = (float)T;
+    w[k] = fmul(a, (float)T);
+    T *= (double)fadd(fsub(1.0f, a), 1e-10f);
+    a_acc += (double)w[k];
+  }
+  const float accf = (float)a_acc;
+  const double A = (double)fadd(accf, 1e-10f);
+  for (int k = 0; k < M; ++k) wd += (double)w[k] * (double)dk[k];
+  const float gr0 = g_rgb ? g_rgb[r * 3 + 0] : 0.f, gr1 = g_rgb ? g_rgb[r * 3 + 1] : 0.f,
+              gr2 = g_rgb ? g_rgb[r * 3 + 2] : 0.f;
+  const double gd = g_depth ? (double)g_depth[r] : 0.0;
+  const double ga = (g_acc ? (double)g_acc[r] : 0.0) - (white_bkgd ? (double)gr0 + gr1 + gr2 : 0.0);
+  for (int k = 0; k < M; ++k) {
+    const bool in = is_in(k);
+    const float* col = in ? rad + (r * S1 + k) * 3 : rad_o + (r * M + k) * 3;
+    double v = (double)gr0 * col[0] + (double)gr1 * col[1] + (double)gr2 * col[2] + ga;
+    v += gd * ((double)dk[k] / A - wd / (A * A));
+    if (g_w) v += (double)g_w[r * M + k];
+    wb[k] = (float)v;
+    float* dro = d_rad_o + (r * M + k) * 3;
+    dro[0] = in ? 0.f : fmul(w[k], gr0);
+    dro[1] = in ? 0.f : fmul(w[k], gr1);
+    dro[2] = in ? 0.f : fmul(w[k], gr2);
+    if (k < S1) {
+      float* dri = d_rad + (r * S1 + k) * 3;
+      dri[0] = in ? fmul(w[k], gr0) : 0.f;
+      dri[1] = in ? fmul(w[k], gr1) : 0.f;
+      dri[2] = in ? fmul(w[k], gr2) : 0.f;
+    }
+  }
+  double suffix = 0.0, sbar = 0.0;
+  float cbar_next = 0.0f;  // gradient reaching c_{k+1} from alpha_{k+1}'s c_i term
+  for (int k = M - 1; k >= 0; --k) {
+    const double u = (double)fadd(fsub(1.0f, al[k]), 1e-10f);
+    const double abar = (double)wb[k] * Tt[k] - suffix / u;
+    suffix += (double)wb[k] * al[k] * Tt[k];
+    if (is_in(k)) {
+      d_sig[r * M + k] = 0.f;
+    } else {
+      const float dist = k + 1 < M ? fsub(dk[k + 1], dk[k]) : 1e10f;
+      const float x = sig_o[r * M + k];
+      // d alpha_out / d sigma = exp(-softplus(sigma) dist) dist softplus'(sigma)
+      const double e = exp(-(double)sp1(x) * (double)dist);
+      d_sig[r * M + k] = (float)(abar * e * (double)dist * sp1_grad(x));
+    }
+    if (k < S1) {
+      double ci_bar = 0.0, cn_bar = 0.0;
+      if (is_in(k)) {
+        const float num = fsub(c[k], c[k + 1]), den = fadd(c[k], 1e-10f);
+        if (fdiv(num, den) >= 0.0f) {
+          ci_bar = abar / den - abar * num / ((double)den * den);
+          cn_bar = -abar / den;
+        }
+      }
+      const double cb_next = cn_bar + (double)cbar_next;
+      const float cc = c[k + 1];
+      const double sg = cb_next * cc * (1.0 - cc);
+      d_sdf[r * S + k + 1] = (float)(sg * s);
+      sbar += sg * sd[k + 1];
+      cbar_next = (float)ci_bar;
+    }
+  }
+  {
+    const float cc = c[0];
+    const double sg = (double)cbar_next * cc * (1.0 - cc);
+    d_sdf[r * S] = (float)(sg * s);
+    sbar += sg * sd[0];
+  }
+  d_s[r] = (float)sbar;
+}
+
 }  // namespace
 }  // namespace nr
 
@@ -462,6 +662,54 @@ int nr_neus_composite_bwd(const float* sdf, const float* s_dev, const float* rad
   hipLaunchKernelGGL(neus_composite_bwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream, sdf,
                      s_dev, rad, dmid, R, S, white_bkgd, g_rgb, g_depth, g_acc, g_weights, (float*)workspace, d_sdf,
                      d_rad, d_s);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_nerf_train_input(const float* rays_o, const float* rays_d, const float* d_out, int64_t R, int M, int n_mid,
+                        float r_obj, float* x_emb, float* v_emb, uint8_t* inside, void* stream) {
+  NR_REQUIRE(rays_o && rays_d && d_out && x_emb && v_emb && inside && R >= 0 && M >= 1 && n_mid >= 0 && n_mid <= M,
+             NR_ERR_ARG, "nr_nerf_train_input: bad argument");
+  if (R == 0) return NR_OK;
+  hipLaunchKernelGGL(nerf_train_input_kernel, grid1(R * M), dim3(kBlk), 0, (hipStream_t)stream, rays_o, rays_d, d_out,
+                     R, M, n_mid, r_obj, x_emb, v_emb, inside);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_neus_composite_bg_fwd(const float* sdf, const float* s_dev, const float* rad, const float* sigma_out,
+                             const float* rad_out, const float* d_out, const uint8_t* inside, int64_t R, int S, int M,
+                             int white_bkgd, float* rgb, float* depth, float* acc, float* weights, float* alpha,
+                             float* cdf, void* stream) {
+  NR_REQUIRE(sdf && s_dev && rad && sigma_out && rad_out && d_out && inside && rgb && depth && acc && weights &&
+                 R >= 0 && S >= 2 && M >= S - 1,
+             NR_ERR_ARG, "nr_neus_composite_bg_fwd: bad argument");
+  if (R == 0) return NR_OK;
+  hipLaunchKernelGGL(neus_composite_bg_fwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
+                     sdf, s_dev, rad, sigma_out, rad_out, d_out, inside, R, S, M, white_bkgd, rgb, depth, acc, weights,
+                     alpha, cdf);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+size_t nr_neus_composite_bg_bwd_workspace_bytes(int64_t R, int S, int M) {
+  return (size_t)(R > 0 ? R : 1) * (size_t)(2 * S + 4 * M) * sizeof(float);
+}
+
+int nr_neus_composite_bg_bwd(const float* sdf, const float* s_dev, const float* rad, const float* sigma_out,
+                             const float* rad_out, const float* d_out, const uint8_t* inside, int64_t R, int S, int M,
+                             int white_bkgd, const float* g_rgb, const float* g_depth, const float* g_acc,
+                             const float* g_weights, float* d_sdf, float* d_rad, float* d_sigma_out,
+                             float* d_rad_out, float* d_s, void* workspace, size_t workspace_bytes, void* stream) {
+  NR_REQUIRE(sdf && s_dev && rad && sigma_out && rad_out && d_out && inside && d_sdf && d_rad && d_sigma_out &&
+                 d_rad_out && d_s && R >= 0 && S >= 2 && M >= S - 1,
+             NR_ERR_ARG, "nr_neus_composite_bg_bwd: bad argument");
+  if (R == 0) return NR_OK;
+  NR_REQUIRE(workspace && workspace_bytes >= nr_neus_composite_bg_bwd_workspace_bytes(R, S, M), NR_ERR_WORKSPACE,
+             "nr_neus_composite_bg_bwd: workspace too small");
+  hipLaunchKernelGGL(neus_composite_bg_bwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
+                     sdf, s_dev, rad, sigma_out, rad_out, d_out, inside, R, S, M, white_bkgd, g_rgb, g_depth, g_acc,
+                     g_weights, (float*)workspace, d_sdf, d_rad, d_sigma_out, d_rad_out, d_s);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

@@ -206,9 +206,11 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
 
 
 def _sample_depths(ro, rd, model, dev, obj_bounding_radius, batched, B, rayschunk, near_bypass, far_bypass, perturb,
-                   fixed_s_recp, N_samples, N_importance, upsample_algo, N_nograd_samples, N_upsample_iters):
+                   fixed_s_recp, N_samples, N_importance, upsample_algo, N_nograd_samples, N_upsample_iters,
+                   N_outside=0):
     """The no-grad upsampling of a training step (neus.py:206-279): sorted sample depths [n, S] from
-    the render kernels' sample pass (forward-only SDF launches, no compositing)."""
+    the render kernels' sample pass (forward-only SDF launches, no compositing), and with perturb the
+    NeRF++ strata uniforms [n, N_outside] (or None)."""
     direct = upsample_algo != 'official_solution'
     n = ro.shape[0]
     n_up = N_importance if direct else (N_importance // N_upsample_iters if N_upsample_iters > 0 else 0)
@@ -232,9 +234,10 @@ def _sample_depths(ro, rd, model, dev, obj_bounding_radius, batched, B, rayschun
     if upsample_algo == 'direct_more':
         t_nograd = _linspace_table(N_nograd_samples, dev)
         a.N_nograd_samples, a.t_nograd = N_nograd_samples, L.ptr(t_nograd)
-    if perturb:
-        u_rand, _ = _neus_uniforms(B, n // B, batched, int(rayschunk), direct, N_upsample_iters, n_up, N_importance,
-                                   0, dev)
+    t_out = None
+    if perturb:  # the NeRF++ strata uniforms are drawn in the same per-chunk order as the render's
+        u_rand, t_out = _neus_uniforms(B, n // B, batched, int(rayschunk), direct, N_upsample_iters, n_up,
+                                       N_importance, N_outside, dev)
         a.u_rand = L.ptr(u_rand)
     a.sample_only, a.d_all_out = 1, L.ptr(d_all)
     lib = L.lib()
@@ -242,7 +245,23 @@ def _sample_depths(ro, rd, model, dev, obj_bounding_radius, batched, B, rayschun
     ws = L.workspace(dev, ws_bytes)
     a.workspace, a.workspace_bytes = L.ptr(ws), ws_bytes
     L.check(lib.nr_neus_render(ctypes.byref(a), L.stream_of(dev)))
-    return d_all
+    return d_all, t_out
+
+
+def _outside_depths(ro, rd, obj_bounding_radius, far_bypass, N_outside, t_out):
+    """NeRF++ background depths (neus.py:303-311): far / flip(linspace(0,1,N+2)[1:-1]), stratified
+    with t_out when perturbing; far from near_far_from_sphere on the normalised rays (neus.py:176-178)."""
+    _, far = rend_util.near_far_from_sphere(ro, rd, r=obj_bounding_radius)
+    if far_bypass is not None:
+        far = far_bypass * torch.ones_like(far)
+    t = torch.linspace(0, 1, N_outside + 2)[..., 1:-1].float().to(ro.device)
+    d = far / torch.flip(t, dims=[-1])
+    if t_out is not None:
+        mids = .5 * (d[..., 1:] + d[..., :-1])
+        upper = torch.cat([mids, d[..., -1:]], -1)
+        lower = torch.cat([d[..., :1], mids], -1)
+        d = lower + (upper - lower) * t_out
+    return d.contiguous()
 
 
 def _train_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False, calc_normal=False,
@@ -255,8 +274,6 @@ def _train_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     (rgb, depth, extras) with graph-carrying rgb, depth_volume, mask_volume, implicit_nablas,
     implicit_surface, radiance, visibility_weights."""
     from .. import training as T
-    if N_outside > 0:
-        raise NotImplementedError('neurecon_amd: training with the NeRF++ background (N_outside > 0) is not native')
     check_view_dirs(model, use_view_dirs)
     if upsample_algo not in L.UPSAMPLE:
         raise NotImplementedError(upsample_algo)
@@ -269,9 +286,9 @@ def _train_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     rd = torch.empty_like(rd_raw)  # F.normalize(rays_d, dim=-1) (neus.py:172)
     L.check(L.lib().nr_normalize3(L.ptr(rd_raw), n, L.ptr(rd), L.stream_of(dev)))
     with torch.no_grad():
-        d_all = _sample_depths(ro, rd_raw, model, dev, obj_bounding_radius, batched, B, rayschunk, near_bypass,
-                               far_bypass, perturb, fixed_s_recp, N_samples, N_importance, upsample_algo,
-                               N_nograd_samples, N_upsample_iters)
+        d_all, t_out = _sample_depths(ro, rd_raw, model, dev, obj_bounding_radius, batched, B, rayschunk, near_bypass,
+                                      far_bypass, perturb, fixed_s_recp, N_samples, N_importance, upsample_algo,
+                                      N_nograd_samples, N_upsample_iters, N_outside)
     S = d_all.shape[1]
     pts = torch.empty(n, S, 3, device=dev)
     mids = torch.empty(n, S - 1, 3, device=dev)
@@ -284,8 +301,27 @@ def _train_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     view = rd[:, None, :].expand(n, S - 1, 3).reshape(-1, 3).contiguous()
     rad = T.radiance(model.radiance_net, mids.reshape(-1, 3), view, nab_m, feat_m)
     s = model.forward_s().float().reshape(-1)[:1]
-    rgb, depth, acc, w, alpha, cdf = T.NeuSComposite.apply(sdf.reshape(n, S), s, rad.reshape(n, S - 1, 3), dmid,
-                                                          bool(white_bkgd))
+    if N_outside > 0:  # neus.py:303-343: the background net at cat([d_mid, outside depths])
+        with torch.no_grad():
+            d_out = torch.cat([dmid, _outside_depths(ro, rd, obj_bounding_radius, far_bypass, N_outside, t_out)], -1)
+            d_out = d_out.contiguous()
+            M = d_out.shape[1]
+            x_emb = torch.empty(n * M, 84, device=dev)
+            v_emb = torch.empty(n * M, 27, device=dev)
+            inside = torch.empty(n, S - 1, dtype=torch.uint8, device=dev)
+            L.check(L.lib().nr_nerf_train_input(L.ptr(ro), L.ptr(rd), L.ptr(d_out), n, M, S - 1,
+                                                float(obj_bounding_radius), L.ptr(x_emb), L.ptr(v_emb), L.ptr(inside),
+                                                L.stream_of(dev)))
+        sig_o, rad_o = T.nerf(model.nerf_outside, x_emb, v_emb)
+        rgb, depth, acc, w, alpha, cdf = T.NeuSCompositeBG.apply(sdf.reshape(n, S), s, rad.reshape(n, S - 1, 3),
+                                                                 sig_o.reshape(n, M), rad_o.reshape(n, M, 3), d_out,
+                                                                 inside, bool(white_bkgd))
+        d_final = d_out
+    else:
+        rgb, depth, acc, w, alpha, cdf = T.NeuSComposite.apply(sdf.reshape(n, S), s, rad.reshape(n, S - 1, 3), dmid,
+                                                              bool(white_bkgd))
+        d_final = dmid
+    Mw = w.shape[1]
     nablas = nablas.reshape(n, S, 3)
     ret = OrderedDict([('rgb', rgb.reshape(*prefix, 3)), ('depth_volume', depth.reshape(prefix)),
                        ('mask_volume', acc.reshape(prefix))])
@@ -296,11 +332,14 @@ def _train_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     if detailed_output:
         ret['implicit_nablas'] = nablas.reshape(*prefix, S, 3)
         ret['implicit_surface'] = sdf.reshape(*prefix, S)
-        ret['radiance'] = rad.reshape(*prefix, S - 1, 3)
-        ret['alpha'] = alpha.reshape(*prefix, S - 1)
+        ret['radiance'] = rad.reshape(*prefix, S - 1, 3)  # the surface net's colours at the mid-points
+        ret['alpha'] = alpha.reshape(*prefix, Mw)
         ret['cdf'] = cdf.reshape(*prefix, S)
-        ret['visibility_weights'] = w.reshape(*prefix, S - 1)
-        ret['d_final'] = dmid.reshape(*prefix, S - 1)
+        ret['visibility_weights'] = w.reshape(*prefix, Mw)
+        ret['d_final'] = d_final.reshape(*prefix, Mw)
+        if N_outside > 0:
+            ret['sigma_out'] = sig_o.reshape(*prefix, Mw)
+            ret['radiance_out'] = rad_o.reshape(*prefix, Mw, 3)
     return ret['rgb'], ret['depth_volume'], ret
 
 

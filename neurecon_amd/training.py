@@ -250,6 +250,129 @@ class NeuSComposite(torch.autograd.Function):
         return d_sdf, d_s.sum().reshape(1), d_rad, None, None
 
 
+class NeRFFn(torch.autograd.Function):
+    """NeRF.forward (base.py:426-453, NeRF++ background: 8 x ReLU(256) with cat([input, h]) after the
+    skip layer, alpha / feature heads, views Linear(256+27 -> 128) + ReLU, rgb Linear + sigmoid) with a
+    graph: GEMMs on hipBLASLt (torch.addmm), activations in libnrhip.  Inputs are the embedded points
+    x_emb [P,84] and views v_emb [P,27] (no gradient: they depend on the rays and the no-grad depths).
+    Returns sigma [P], rgb [P,3]; gradients reach every parameter."""
+
+    @staticmethod
+    def forward(ctx, xe, ve, cfg, *params):
+        D, skips = cfg
+        Ws, bs = params[:D], params[D:2 * D]
+        Wa, ba, Wf, bf, Wv, bv, Wr, br = params[2 * D:]
+        st = _st(xe)
+        lib = L.lib()
+        ins, outs = [], []
+        h = xe
+        for i in range(D):
+            ins.append(h)
+            z = torch.addmm(bs[i], h, Ws[i].t())
+            L.check(lib.nr_activation(L.ptr(z), None, z.numel(), 0, st))
+            outs.append(z)
+            h = torch.cat([xe, z], -1) if i in skips else z
+        sigma = torch.addmm(ba, h, Wa.t())
+        feat = torch.addmm(bf, h, Wf.t())
+        hv_in = torch.cat([feat, ve], -1)
+        hv = torch.addmm(bv, hv_in, Wv.t())
+        L.check(lib.nr_activation(L.ptr(hv), None, hv.numel(), 0, st))
+        rgb = torch.addmm(br, hv, Wr.t())
+        L.check(lib.nr_activation(L.ptr(rgb), None, rgb.numel(), 2, st))
+        ctx.cfg = (D, tuple(skips), xe.shape[1])
+        ctx.save_for_backward(rgb, hv, hv_in, h, *ins, *outs, *params)
+        return sigma[:, 0], rgb
+
+    @staticmethod
+    def backward(ctx, g_sigma, g_rgb):
+        D, skips, nx = ctx.cfg
+        saved = ctx.saved_tensors
+        rgb, hv, hv_in, h = saved[:4]
+        ins, outs = saved[4:4 + D], saved[4 + D:4 + 2 * D]
+        params = saved[4 + 2 * D:]
+        Ws = params[:D]
+        Wa, ba, Wf, bf, Wv, bv, Wr, br = params[2 * D:]
+        st = _st(rgb)
+        lib = L.lib()
+        P = rgb.shape[0]
+        g = torch.zeros_like(rgb) if g_rgb is None else g_rgb.contiguous().clone()
+        L.check(lib.nr_activation(L.ptr(rgb), L.ptr(g), g.numel(), 3, st))          # sigmoid'
+        dWr, dbr = g.t() @ hv, g.sum(0)
+        ghv = g @ Wr
+        L.check(lib.nr_activation(L.ptr(hv), L.ptr(ghv), ghv.numel(), 1, st))      # ReLU'
+        dWv, dbv = ghv.t() @ hv_in, ghv.sum(0)
+        g_feat = (ghv @ Wv)[:, :Wf.shape[0]].contiguous()                           # views: no gradient
+        dWf, dbf = g_feat.t() @ h, g_feat.sum(0)
+        gh = g_feat @ Wf
+        gs = (torch.zeros(P, 1, device=rgb.device) if g_sigma is None else g_sigma.reshape(P, 1).contiguous())
+        dWa, dba = gs.t() @ h, gs.sum(0)
+        gh = torch.addmm(gh, gs, Wa)
+        dW, db = [None] * D, [None] * D
+        for i in range(D - 1, -1, -1):
+            gz = gh.contiguous()
+            L.check(lib.nr_activation(L.ptr(outs[i]), L.ptr(gz), gz.numel(), 1, st))  # ReLU'
+            dW[i], db[i] = gz.t() @ ins[i], gz.sum(0)
+            if i > 0:
+                gin = gz @ Ws[i]
+                gh = gin[:, nx:] if (i - 1) in skips else gin                          # drop the re-injected input
+        return (None, None, None, *dW, *db, dWa, dba, dWf, dbf, dWv, dbv, dWr, dbr)
+
+
+class NeuSCompositeBG(torch.autograd.Function):
+    """NeuSComposite with the NeRF++ background merged (neus.py:325-352): sdf [R,S], s [1], radiance
+    [R,S-1,3], sigma_out [R,M], radiance_out [R,M,3]; d_out [R,M] and inside [R,S-1] (no grad) ->
+    rgb, depth, acc, visibility weights [R,M] (+ alpha [R,M], cdf [R,S], not differentiable)."""
+
+    @staticmethod
+    def forward(ctx, sdf, s, rad, sig_o, rad_o, d_out, inside, white_bkgd):
+        R, S = sdf.shape
+        M = d_out.shape[1]
+        dev = sdf.device
+        sdf, rad, s = sdf.contiguous(), rad.contiguous(), s.reshape(-1)[:1].contiguous()
+        sig_o, rad_o = sig_o.contiguous(), rad_o.contiguous()
+        rgb = torch.empty(R, 3, device=dev)
+        depth = torch.empty(R, device=dev)
+        acc = torch.empty(R, device=dev)
+        w = torch.empty(R, M, device=dev)
+        alpha = torch.empty(R, M, device=dev)
+        cdf = torch.empty(R, S, device=dev)
+        L.check(L.lib().nr_neus_composite_bg_fwd(L.ptr(sdf), L.ptr(s), L.ptr(rad), L.ptr(sig_o), L.ptr(rad_o),
+                                                 L.ptr(d_out), L.ptr(inside), R, S, M, int(white_bkgd), L.ptr(rgb),
+                                                 L.ptr(depth), L.ptr(acc), L.ptr(w), L.ptr(alpha), L.ptr(cdf), _st(sdf)))
+        ctx.white = int(white_bkgd)
+        ctx.save_for_backward(sdf, s, rad, sig_o, rad_o, d_out, inside)
+        ctx.mark_non_differentiable(alpha, cdf)
+        return rgb, depth, acc, w, alpha, cdf
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_depth, g_acc, g_w, _ga, _gc):
+        sdf, s, rad, sig_o, rad_o, d_out, inside = ctx.saved_tensors
+        R, S = sdf.shape
+        M = d_out.shape[1]
+        c = lambda t: None if t is None else t.contiguous()
+        d_sdf, d_rad = torch.empty_like(sdf), torch.empty_like(rad)
+        d_sig, d_rad_o = torch.empty_like(sig_o), torch.empty_like(rad_o)
+        d_s = torch.empty(R, device=sdf.device)
+        lib = L.lib()
+        wb = lib.nr_neus_composite_bg_bwd_workspace_bytes(R, S, M)
+        ws = torch.empty(max(wb, 1), dtype=torch.uint8, device=sdf.device)
+        g_rgb, g_depth, g_acc, g_w = c(g_rgb), c(g_depth), c(g_acc), c(g_w)
+        L.check(lib.nr_neus_composite_bg_bwd(L.ptr(sdf), L.ptr(s), L.ptr(rad), L.ptr(sig_o), L.ptr(rad_o),
+                                             L.ptr(d_out), L.ptr(inside), R, S, M, ctx.white, L.ptr(g_rgb),
+                                             L.ptr(g_depth), L.ptr(g_acc), L.ptr(g_w), L.ptr(d_sdf), L.ptr(d_rad),
+                                             L.ptr(d_sig), L.ptr(d_rad_o), L.ptr(d_s), L.ptr(ws), wb, _st(sdf)))
+        return d_sdf, d_s.sum().reshape(1), d_rad, d_sig, d_rad_o, None, None, None
+
+
+def nerf(net, x_emb, v_emb):
+    """Differentiable (sigma [P], rgb [P,3]) of a neurecon_amd NeRF background net."""
+    Ws = [l.weight for l in net.pts_linears]
+    bs = [l.bias for l in net.pts_linears]
+    heads = [net.alpha_linear.weight, net.alpha_linear.bias, net.feature_linear.weight, net.feature_linear.bias,
+             net.views_linears[0].weight, net.views_linears[0].bias, net.rgb_linear.weight, net.rgb_linear.bias]
+    return NeRFFn.apply(x_emb, v_emb, (len(Ws), tuple(net.skips)), *Ws, *bs, *heads)
+
+
 def sdf_nablas(surface, x, want_feat):
     """Differentiable (sdf, nablas, feature) of a neurecon_amd ImplicitSurface at points x [P,3]."""
     Ws = [l.effective_weight() for l in surface.surface_fc_layers]

@@ -7,7 +7,7 @@ import torch
 import torch.nn.functional as F
 
 from . import rays as R
-from .nets import SDFNet, RadianceNet
+from .nets import NeRFNet, SDFNet, RadianceNet
 from .neus import NeuSOracle, alpha_to_w, sdf_to_alpha
 
 
@@ -21,9 +21,10 @@ def nablas_graph(net, x):
 
 def neus_train_losses(sd, rays_o, rays_d, target_rgb, target_mask, w_eikonal=0.1, w_mask=1.0, with_mask=True,
                       d_all=None, speed_factor=10.0, obj_bounding_radius=1.0, N_samples=64, N_importance=64,
-                      N_upsample_iters=4):
+                      N_upsample_iters=4, N_outside=0):
     """losses (neus.py:453-478) of one training render of rays [B, N, 3]; d_all [B, N, S] optional
-    (the sorted sample depths; computed with the no-grad upsampling when None)."""
+    (the sorted sample depths; computed with the no-grad upsampling when None); N_outside > 0 adds the
+    NeRF++ background (neus.py:303-343, perturb=False) with its parameters in the graph."""
     o = rays_o.reshape(rays_o.shape[0], -1, 3).float()
     d = F.normalize(rays_d.reshape(rays_d.shape[0], -1, 3).float(), dim=-1)
     near, far = R.near_far_from_sphere(o, d, r=obj_bounding_radius)
@@ -40,6 +41,21 @@ def neus_train_losses(sd, rays_o, rays_d, target_rgb, target_mask, w_eikonal=0.1
     cdf, alpha = sdf_to_alpha(sdf, s)
     _, n_m, h_m = nablas_graph(sdf_net, pts_mid)                            # neus.py:103-106, :298
     rad = rad_net.forward(pts_mid, d.unsqueeze(-2).expand_as(pts_mid), n_m, h_m)
+    if N_outside > 0:                                                       # neus.py:303-343
+        tt = torch.linspace(0, 1, N_outside + 2)[..., 1:-1].float()
+        d_out = torch.cat([d_mid, far / torch.flip(tt, dims=[-1])], -1)
+        p_out = o[..., None, :] + d[..., None, :] * d_out[..., :, None]
+        r = p_out.norm(dim=-1, keepdim=True)
+        x_out = torch.cat([p_out / r, 1. / r], -1)
+        sigma_out, rad_out = NeRFNet(sd).forward(x_out, d.unsqueeze(-2).expand_as(x_out[..., :3]))
+        dists = d_out[..., 1:] - d_out[..., :-1]
+        dists = torch.cat([dists, 1e10 * torch.ones(dists[..., :1].shape)], -1)
+        alpha_out = 1 - torch.exp(-F.softplus(sigma_out) * dists)
+        n1 = d_mid.shape[-1]
+        inside = (pts_mid.norm(dim=-1) <= obj_bounding_radius)
+        alpha = torch.cat([alpha * inside.float() + alpha_out[..., :n1] * (~inside).float(), alpha_out[..., n1:]], -1)
+        rad = torch.cat([rad * inside.float()[..., None] + rad_out[..., :n1, :] * (~inside).float()[..., None],
+                         rad_out[..., n1:, :]], -2)
     w = alpha_to_w(alpha)
     rgb = torch.sum(w[..., None] * rad, -2)
     acc = torch.sum(w, -1)

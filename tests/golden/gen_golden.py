@@ -592,21 +592,28 @@ def _grad_summary(named):
 def gen_train(R):
     """One NeuS training step's losses and parameter gradients (models/frameworks/neus.py:417-485 ->
     train.py:205 backward) on an 8x8 camera (64 rays, N_rays=-1 so no random pixels), perturb=False,
-    with_mask=True, seeded random targets."""
+    with_mask=True, seeded random targets; and the same with the NeRF++ background (N_outside=32)."""
+    _gen_train(R, 'neus_train.npz', 1, 0)
+    _gen_train(R, 'neus_train_nerfpp.npz', 4, 32)
+
+
+def _gen_train(R, name, seed, N_outside):
     import types as _t
-    sd = wg.neus_state(seed=1)
-    model = _neus_model(R, sd, False)
+    sd = wg.neus_state(seed=seed, use_outside_nerf=N_outside > 0)
+    model = _neus_model(R, sd, N_outside > 0)
     model.train()
     H = W = 8
     c2w = wg.look_at_c2w(3.0)[None]
+    if N_outside > 0:  # off-centre: the centre ray's mid-point samples must not hit the origin (x_out = p/|p|)
+        c2w[0, 0, 3] += 0.0137
     K = wg.intrinsics(20.0, H, W)[None]
     g = torch.Generator().manual_seed(5)
     target_rgb = torch.rand(1, H * W, 3, generator=g)
     target_mask = (torch.rand(1, H * W, generator=g) > 0.4)
     args = _t.SimpleNamespace(data=_t.SimpleNamespace(N_rays=-1),
                               training=_t.SimpleNamespace(w_eikonal=0.1, w_mask=1.0, with_mask=True))
-    kw = dict(H=H, W=W, upsample_algo='official_solution', N_nograd_samples=2048, N_upsample_iters=4, N_outside=0,
-              obj_bounding_radius=1.0, batched=True, perturb=False, white_bkgd=False)
+    kw = dict(H=H, W=W, upsample_algo='official_solution', N_nograd_samples=2048, N_upsample_iters=4,
+              N_outside=N_outside, obj_bounding_radius=1.0, batched=True, perturb=False, white_bkgd=False)
     trainer = R.neus.Trainer(model, device_ids=[0], batched=True)
     ret = trainer.forward(args, None, {'intrinsics': K, 'c2w': c2w, 'object_mask': target_mask},
                           {'rgb': target_rgb}, kw, 0, device='cpu')
@@ -614,7 +621,8 @@ def gen_train(R):
     model.zero_grad()
     losses['total'].backward()
     ex = ret['extras']
-    save('neus_train.npz', seed=1, H=H, W=W, f=20.0, dist=3.0, target_rgb=target_rgb, target_mask=target_mask,
+    save(name, seed=seed, N_outside=N_outside, H=H, W=W, f=20.0, dist=3.0, target_rgb=target_rgb,
+         target_mask=target_mask,
          c2w=c2w, K=K, **{f'loss/{k}': v.detach() for k, v in losses.items()},
          rgb=ex['rgb'].detach(), mask_volume=ex['mask_volume'].detach(), d_final=ex['d_final'].detach(),
          **_grad_summary(model.named_parameters()))

@@ -299,11 +299,13 @@ def test_options(golden):
 def train_grads_oracle(g, d_all=None):
     """oracle/train.py on the neus_train fixture: (losses, {param: grad}, d_all)"""
     from oracle.train import neus_train_losses
+    No = int(g['N_outside']) if 'N_outside' in g else 0
     sd = {k: v.clone().requires_grad_(v.is_floating_point() and k != 'implicit_surface.obj_bounding_size')
-          for k, v in wg.neus_state(seed=int(g['seed'])).items()}
+          for k, v in wg.neus_state(seed=int(g['seed']), use_outside_nerf=No > 0).items()}
     H, W = int(g['H']), int(g['W'])
     ro, rd, _ = rays.get_rays(T(g['c2w']), T(g['K']), H, W)
-    losses, d_all = neus_train_losses(sd, ro, rd, T(g['target_rgb']), T(g['target_mask']), d_all=d_all)
+    losses, d_all = neus_train_losses(sd, ro, rd, T(g['target_rgb']), T(g['target_mask']), d_all=d_all,
+                                      N_outside=No)
     losses['total'].backward()
     return losses, {k: v.grad for k, v in sd.items() if v.grad is not None}, d_all
 
@@ -331,10 +333,12 @@ def check_grads(grads, g, rtol, atol_frac, report=print):
     return worst
 
 
-def test_oracle_train_step_vs_golden(golden):
+@pytest.mark.parametrize('name', ['neus_train', 'neus_train_nerfpp'])
+def test_oracle_train_step_vs_golden(golden, name):
     """the oracle's NeuS training losses and every parameter gradient vs the reference's own
-    Trainer.forward + backward (double backward through the nablas)"""
-    g = golden('neus_train')
+    Trainer.forward + backward (double backward through the nablas; with the NeRF++ background's
+    parameters for neus_train_nerfpp)"""
+    g = golden(name)
     torch.set_num_threads(8)
     losses, grads, _ = train_grads_oracle(g)
     for k in ('loss_img', 'loss_eikonal', 'loss_mask', 'total'):
