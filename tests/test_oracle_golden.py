@@ -310,15 +310,21 @@ def train_grads_oracle(g, d_all=None):
     return losses, {k: v.grad for k, v in sd.items() if v.grad is not None}, d_all
 
 
-def check_grads(grads, g, rtol, atol_frac, report=print):
+def check_grads(grads, g, rtol, atol_frac, report=print, net_scale=False):
     """per parameter: full gradient, or (norm, sum, 4096 sampled entries) for the big weight_v tensors;
-    atol = atol_frac * max |grad| of the tensor (components near zero of a large gradient)"""
+    atol = atol_frac * max |grad| of the tensor (components near zero of a large gradient), or with
+    net_scale of the tensor's whole network (first name component: implicit_surface / radiance_net /
+    nerf_outside)"""
     keys = list(g.keys())
     names = sorted({k.split('/', 1)[1] for k in keys if k.startswith('g_norm/')})
+    net_max = {}
+    for k in names:
+        net = k.split('.')[0]
+        net_max[net] = max(net_max.get(net, 0.0), float(grads[k].detach().abs().max()))
     worst = 0.0
     for k in names:
         gr = grads[k].detach().reshape(-1).double().cpu().numpy()
-        scale = float(np.abs(gr).max()) + 1e-30
+        scale = (net_max[k.split('.')[0]] if net_scale else float(np.abs(gr).max())) + 1e-30
         if f'g_full/{k}' in keys:
             ref, mine = g[f'g_full/{k}'].astype(np.float64), gr
         else:
