@@ -193,6 +193,29 @@ def pmc_traffic(kernel, precision):
     return sum(r['hbm_bytes_per_launch'] * r['launches'] for r in recs) / n, PMC_SUMMARY[precision]
 
 
+# L2 -> LDS weight stream of sdf4_kernel: every 128-point tile streams the whole packed network
+# (nr_mlp.h kSdfKB / kSdfNBO: 3.93 MB without the feature op, 4.20 MB with it), by LDS-DMA, whose
+# chip-wide fill rate is ~6.4 TB/s (MI355X_MICROARCH.md, 'ldsdma-fill'); f16x3 only
+SDF_TILE_POINTS = 128
+SDF_PACKED_BYTES = {'sdf_nabla': 3_926_016, 'sdf_nabla_feat': 4_196_352}
+LDSDMA_FILL_TBPS = 6.4
+
+
+def weight_stream(kstats):
+    """bytes the nabla launches streamed into LDS / their device time"""
+    nb, ms = 0.0, 0.0
+    for name, (n, t, units) in kstats.items():
+        if name in SDF_PACKED_BYTES and n:
+            nb += math.ceil(units / n / SDF_TILE_POINTS) * n * SDF_PACKED_BYTES[name]
+            ms += t
+    if not ms:
+        return None
+    tbps = nb / (ms * 1e-3) / 1e12
+    return {'bytes_per_launch_avg': nb / sum(kstats[k][0] for k in SDF_PACKED_BYTES if k in kstats),
+            'achieved_TBps': round(tbps, 2), 'ldsdma_fill_TBps': LDSDMA_FILL_TBPS,
+            'frac': round(tbps / LDSDMA_FILL_TBPS, 3)}
+
+
 def roofline(kstats, precision):
     """Dominant kernel (largest device time): executed FLOPs per launch / mean launch duration, both
     launch types of the nabla kernel merged (sample launches without the feature rows, the
@@ -224,7 +247,8 @@ def roofline(kstats, precision):
             'traffic_source': src, 'kernel': dom,
             'avg_launch_ms': round(per_launch_ms, 4), 'launches': n,
             'flop_per_launch': fl / n, 'share_of_device_time': round(ms / total_ms, 4),
-            'per_launch_type': per_type}
+            'per_launch_type': per_type,
+            'weight_stream': weight_stream(kstats) if precision == 'f16x3' else None}
 
 
 def frame_d_setup(dev, precision):
