@@ -734,6 +734,14 @@ __global__ __launch_bounds__(kThreads) void sdf_kernel(SdfKArgs a) {
 
 // =============================================================================================
 // f16x3 operand helpers of the v3 SDF pipeline (sdf4_kernel, below)
+// NR_SDF4_NC: 16-point MFMA columns per wave of sdf4_kernel.  1 (default): 8 waves of 16 points, two
+// waves per SIMD with up to 256 registers each, every operand in VGPRs (no AGPR moves); the two
+// waves of a SIMD hide each other's DMA / LDS / barrier stalls.  2: 4 waves of 32 points, one per
+// SIMD with 512 registers, B operands parked in AGPRs; each weight fragment read from LDS feeds
+// both columns (half the LDS read traffic).  Measured on config (b): 1 is ~5 % faster.
+#ifndef NR_SDF4_NC
+#define NR_SDF4_NC 1
+#endif
 // =============================================================================================
 // What changes against sdf_kernel<F16X3> (which stays the reference design for the radiance and
 // NeRF++ kernels):
@@ -776,8 +784,9 @@ __device__ __forceinline__ void split8s(float4 a, float4 b, float sc, f16x8& h, 
 }
 // ... with both halves from v_fma_mix, written straight into the packed f16 pairs: hi = f16(v*sc)
 // (one rounding of the exact product), lo = f16(v*sc - hi); no packed-fp32 multiply (v_pk_mul_f32
-// issued beside MFMAs costs ~22 cycles more than scalar VALU, MI355X_MICROARCH.md).  The pairs are
-// parked in AGPRs: B operands are read only by MFMAs, which take AGPR sources directly
+// issued beside MFMAs costs ~22 cycles more than scalar VALU, MI355X_MICROARCH.md).  With 32-point
+// waves (NR_SDF4_NC 2) the pairs are parked in AGPRs: B operands are read only by MFMAs, which take
+// AGPR sources directly
 __device__ __forceinline__ void split8a(float4 a, float4 b, float sc, f16x8& h, f16x8& l) {
   const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
   uint32_t hw[4], lw[4];
@@ -796,7 +805,9 @@ __device__ __forceinline__ void split8a(float4 a, float4 b, float sc, f16x8& h, 
   }
   h = __builtin_bit_cast(f16x8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
   l = __builtin_bit_cast(f16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
+#if NR_SDF4_NC == 2 && !defined(NR_SPLIT_VGPR)
   asm volatile("" : "+a"(h), "+a"(l));
+#endif
 }
 __device__ __forceinline__ float max3abs(float m, float a, float b) {
   return __builtin_fmaxf(m, __builtin_fmaxf(fabsf(a), fabsf(b)));  // -> v_max3_f32 with |.| modifiers
@@ -855,18 +866,22 @@ __device__ __forceinline__ float4 fma4s(f32x4 a, float m, float4 b) {
 using gf4 = __attribute__((address_space(1))) f32x4;
 
 // =============================================================================================
-// f16x3 SDF pipeline v3 (sdf4_kernel): one wave per SIMD, 32 points per wave
+// f16x3 SDF pipeline v3 (sdf4_kernel): kNC 16-point columns per wave, 128-point tile
 // =============================================================================================
-// * 4 waves x 32 points (two 16-point MFMA column tiles per wave) = the same 128-point tile; each
-//   A (weight) fragment read from LDS feeds both columns, and a wave may hold 512 registers, so
-//   the B operands of the op being computed AND of the op being produced stay in registers.
+// * 8 waves x 16 points (two per SIMD, 256 registers each) or 4 waves x 32 points (one per SIMD,
+//   512 registers, each A fragment read from LDS feeds both columns): either way the B operands of
+//   the op being computed AND of the op being produced stay in registers.
 // * Chunk c's epilogue (bias, activation, slab I/O, per-chunk operand split) is issued in the same
 //   basic block as chunk c+1's MFMAs, so the wave's VALU work fills the matrix core's issue gaps.
 // * The operand split uses per-point power-of-two scales fixed before the op runs, from a bound on
 //   its outputs (see the v2 notes above: split8s / bound_scale / softplus3).
-constexpr int kW4 = 4;          // waves per workgroup (one per SIMD)
-constexpr int kT4 = 64 * kW4;   // 256 threads
-constexpr int kSlab4 = kW4 * 4096;  // one chunk's softplus' values (2 blocks x 2 columns) per wave: 16 KB
+constexpr int kNC = NR_SDF4_NC;   // 16-point MFMA columns per wave (1: two waves per SIMD; 2: one)
+static_assert(kNC == 1 || kNC == 2, "columns per wave");
+constexpr int kW4 = 8 / kNC;      // waves per workgroup: the tile stays 128 points
+constexpr int kT4 = 64 * kW4;
+constexpr int kWPE = kW4 / 4;     // waves per SIMD
+constexpr int kSlabW = 2 * kNC * 1024;  // one chunk's slab values of one wave (2 blocks x kNC columns)
+constexpr int kSlab4 = kW4 * kSlabW;    // ... of the workgroup: 16 KB
 
 // Deferred stores of one chunk (up to 4 x 16 B per lane), issued at the start of the next chunk
 // before its weight DMA, so flip()'s counted wait never stands behind a store younger than the
@@ -970,6 +985,18 @@ struct WStream4 {
         glds16m(gj, voff, mj);
     }
   }
+  // piece j (0 <= j < pieces<BYTES>()) of this wave's run of a chunk, into the slot issue() fills
+  template <int BYTES>
+  __device__ __forceinline__ void dma_piece(const char* gsrc, int j) {
+#ifdef NR_EXP_NO_DMA
+    return;
+#endif
+    constexpr int NB = BYTES / 1024, NPW = pieces<BYTES>();
+    const int first = __builtin_amdgcn_readfirstlane(min(wave_id() * NPW, NB - NPW)) + j;
+    const int slot = cur == 0 ? 2 : cur - 1;
+    glds16m(uniform_ptr(gsrc) + first * 1024, (threadIdx.x & 63) * 16,
+            __builtin_amdgcn_readfirstlane(lds_u32(lds) + (uint32_t)(slot * CBMAX) + (uint32_t)(first * 1024)));
+  }
   template <int B0, int B1>
   __device__ __forceinline__ void start(const char* g0, const char* g1) {
     cur = 0;
@@ -982,32 +1009,41 @@ struct WStream4 {
   }
   template <int BYTES>
   __device__ __forceinline__ void issue(const char* gsrc) { dma<BYTES>(gsrc, cur == 0 ? 2 : cur - 1); }
-  // this wave's softplus' slab of chunk c (blocks 2c, 2c+1, both columns: 4 KB contiguous) -> the next
-  // slab slot; one M0 setting, the instruction offset steps global and LDS address together.  Staged
-  // two chunk-iterations before the epilogue that reads it.  Returns the DMA instructions issued.
+  // this wave's softplus' slab of chunk c (blocks 2c, 2c+1, all kNC columns: 2 or 4 KB contiguous) ->
+  // the next slab slot; one M0 setting, the instruction offset steps global and LDS address together.
+  // Staged two chunk-iterations before the epilogue that reads it.  Returns the DMA instructions issued.
   __device__ __forceinline__ int stage_slab(const float4* e, int c) {
 #ifdef NR_EXP_NO_ELOAD  // timing experiment: softplus' slab not read back
     return 0;
 #endif
     const uint32_t voff = (threadIdx.x & 63) * 16;
-    const char* g = (const char*)uniform_ptr(e + 4 * c * 64);
+    const char* g = (const char*)uniform_ptr(e + 2 * kNC * c * 64);
     const uint32_t base =
-        __builtin_amdgcn_readfirstlane(lds_u32(slab) + (uint32_t)(es * kSlab4 + wave_id() * 4096));
-    asm volatile(
-        "s_mov_b32 m0, %2\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %0, %1\n\t"
-        "global_load_lds_dwordx4 %0, %1 offset:1024\n\t"
-        "global_load_lds_dwordx4 %0, %1 offset:2048\n\t"
-        "global_load_lds_dwordx4 %0, %1 offset:3072"
-        :
-        : "v"(voff), "s"(g), "s"(base)
-        : "memory", "m0");
+        __builtin_amdgcn_readfirstlane(lds_u32(slab) + (uint32_t)(es * kSlab4 + wave_id() * kSlabW));
+    if constexpr (kNC == 2)
+      asm volatile(
+          "s_mov_b32 m0, %2\n\ts_nop 0\n\t"
+          "global_load_lds_dwordx4 %0, %1\n\t"
+          "global_load_lds_dwordx4 %0, %1 offset:1024\n\t"
+          "global_load_lds_dwordx4 %0, %1 offset:2048\n\t"
+          "global_load_lds_dwordx4 %0, %1 offset:3072"
+          :
+          : "v"(voff), "s"(g), "s"(base)
+          : "memory", "m0");
+    else
+      asm volatile(
+          "s_mov_b32 m0, %2\n\ts_nop 0\n\t"
+          "global_load_lds_dwordx4 %0, %1\n\t"
+          "global_load_lds_dwordx4 %0, %1 offset:1024"
+          :
+          : "v"(voff), "s"(g), "s"(base)
+          : "memory", "m0");
     es = next3(es);
-    return 4;
+    return 2 * kNC;
   }
   // the slab of the chunk whose epilogue runs now (staged two iterations ago)
   __device__ __forceinline__ const float4* slab_read() const {
-    uint32_t off = er * kSlab4 + wave_id() * 4096;
+    uint32_t off = er * kSlab4 + wave_id() * kSlabW;
     asm volatile("" : "+s"(off));
     return (const float4*)(slab + off);
   }
@@ -1028,23 +1064,32 @@ struct WStream4 {
   }
 };
 
-// one k-step pair of output blocks x two point columns: 12 MFMAs per k-step
-// Software-pipelined one k-step deep (step s+1's 4 fragments are read while step s's 12 MFMAs
+// one k-step pair of output blocks x kNC point columns: 6 kNC MFMAs per k-step
+// Software-pipelined one k-step deep (step s+1's 4 fragments are read while step s's MFMAs
 // issue).  stage(s) is VALU work of the previous chunk's epilogue placed in k-step s's scheduling
 // region, so it fills the matrix core's issue gaps instead of running before or after the MFMAs.
+__device__ __forceinline__ f16x8 rd_frag(const float4* __restrict__ A, int i, int lane) {
+#ifdef NR_EXP_NO_AREAD  // timing experiment: weight fragments not read from LDS (results are garbage)
+  uint4 v = make_uint4(i, i, i, i);
+  asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+  return __builtin_bit_cast(f16x8, v);
+#else
+  return as_h8(A[i * 64 + lane]);
+#endif
+}
 template <int NS, class Stage>
-__device__ __forceinline__ void mma4(const float4* __restrict__ A, const f16x8 (&bh)[2][12], const f16x8 (&bl)[2][12],
-                                     f32x4 (&acc)[2][2], int lane, Stage&& stage) {
-  f16x8 nh0 = as_h8(A[0 * 64 + lane]), nl0 = as_h8(A[1 * 64 + lane]);
-  f16x8 nh1 = as_h8(A[(NS * 2) * 64 + lane]), nl1 = as_h8(A[(NS * 2 + 1) * 64 + lane]);
+__device__ __forceinline__ void mma4(const float4* __restrict__ A, const f16x8 (&bh)[kNC][12],
+                                     const f16x8 (&bl)[kNC][12], f32x4 (&acc)[kNC][2], int lane, Stage&& stage) {
+  f16x8 nh0 = rd_frag(A, 0, lane), nl0 = rd_frag(A, 1, lane);
+  f16x8 nh1 = rd_frag(A, NS * 2, lane), nl1 = rd_frag(A, NS * 2 + 1, lane);
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const f16x8 h0 = nh0, l0 = nl0, h1 = nh1, l1 = nl1;
     if (s + 1 < NS) {
-      nh0 = as_h8(A[((s + 1) * 2) * 64 + lane]);
-      nl0 = as_h8(A[((s + 1) * 2 + 1) * 64 + lane]);
-      nh1 = as_h8(A[((NS + s + 1) * 2) * 64 + lane]);
-      nl1 = as_h8(A[((NS + s + 1) * 2 + 1) * 64 + lane]);
+      nh0 = rd_frag(A, (s + 1) * 2, lane);
+      nl0 = rd_frag(A, (s + 1) * 2 + 1, lane);
+      nh1 = rd_frag(A, (NS + s + 1) * 2, lane);
+      nl1 = rd_frag(A, (NS + s + 1) * 2 + 1, lane);
     }
     stage(s);
 #ifdef NR_EXP_NO_MFMA  // timing experiment: fragments read, no matrix work (results are garbage)
@@ -1052,7 +1097,7 @@ __device__ __forceinline__ void mma4(const float4* __restrict__ A, const f16x8 (
     continue;
 #endif
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < kNC; ++q) {
       acc[q][0] = mfma16h(l0, bh[q][s], acc[q][0]);
       acc[q][1] = mfma16h(l1, bh[q][s], acc[q][1]);
       acc[q][0] = mfma16h(h0, bl[q][s], acc[q][0]);
@@ -1063,7 +1108,7 @@ __device__ __forceinline__ void mma4(const float4* __restrict__ A, const f16x8 (
     // the next step's 4 fragment reads ahead of this step's MFMAs (a whole region of prefetch
     // distance); the epilogue VALU is left to the scheduler
     if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 6 * kNC, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -1071,7 +1116,7 @@ __device__ __forceinline__ void mma4(const float4* __restrict__ A, const f16x8 (
 // Pre-activations of one chunk: z[q][o] = column q, output block 2c+o; aux[o] = the op's per-row
 // vector (bias-slot floats 64..95) for block o
 struct Z4 {
-  float4 z[2][2];
+  float4 z[kNC][2];
   float4 aux[2];
 };
 
@@ -1090,8 +1135,8 @@ constexpr float kT = 144.26944f;
 constexpr float kC = 0.0069314749f;
 
 template <int KB, int NBO, int NXT_CB, bool AUX, bool TS, class WS, class Pre, class Epi>
-__device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const char* nxt, const f16x8 (&bh)[2][12],
-                                    const f16x8 (&bl)[2][12], const float (&xinv)[2], Pend4& pd, Pre&& pre,
+__device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const char* nxt, const f16x8 (&bh)[kNC][12],
+                                    const f16x8 (&bl)[kNC][12], const float (&xinv)[kNC], Pend4& pd, Pre&& pre,
                                     Epi&& epi, int lane) {
   constexpr int CB = chunk_bytes(KB);
   constexpr int NCH = NBO / 2;
@@ -1105,6 +1150,19 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
     const char* nxc = nxt;
     asm volatile("" : "+s"(opc), "+s"(nxc));
     int npend = 0;
+#ifdef NR_DMA_SPREAD  // the chunk-two-ahead's pieces go out one per k-step region, beside the MFMAs
+    const char* dsrc = nullptr;
+    int dkind = 0;
+    if (c + 2 < NCH) {
+      dsrc = opc + (c + 2) * CB;
+      dkind = 1;
+      npend = WS::template pieces<CB>();
+    } else if (nxc) {
+      dsrc = nxc + (c + 2 - NCH) * NXT_CB;
+      dkind = 2;
+      npend = WS::template pieces<NXT_CB>();
+    }
+#else
     if (c + 2 < NCH) {
       ws.template issue<CB>(opc + (c + 2) * CB);
       npend = WS::template pieces<CB>();
@@ -1112,14 +1170,29 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
       ws.template issue<NXT_CB>(nxc + (c + 2 - NCH) * NXT_CB);
       npend = WS::template pieces<NXT_CB>();
     }
+#endif
     npend += pre(c);
     // the previous chunk's stores go out after this chunk's DMA: this chunk's flip does not wait for
     // them (the next one does, two chunk-times after issue)
     npend += pd.flush();
     const float4* A = ws.buf();
-    f32x4 acc[2][2] = {};
+    f32x4 acc[kNC][2] = {};
     // the previous chunk's epilogue, 8 stages spread over this chunk's KB/2 k-steps
     mma4<KB / 2>(A, bh, bl, acc, lane, [&](int st) {
+#ifdef NR_DMA_SPREAD
+      {
+        constexpr int NS = KB / 2, N1 = WS::template pieces<CB>(), N2 = WS::template pieces<NXT_CB>();
+        if (dkind == 1) {
+#pragma unroll
+          for (int j = 0; j < N1; ++j)
+            if (j * NS / N1 == st) ws.template dma_piece<CB>(dsrc, j);
+        } else if (dkind == 2) {
+#pragma unroll
+          for (int j = 0; j < N2; ++j)
+            if (j * NS / N2 == st) ws.template dma_piece<NXT_CB>(dsrc, j);
+        }
+      }
+#endif
 #ifdef NR_EXP_NO_EPI
       if (c > 0 && st == 7) epi(c - 1, zq, 7);
       return;
@@ -1134,7 +1207,7 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
     if constexpr (TS) wi *= kT;
     const float4 b0 = A[2 * KB * 64 + (TS ? 24 : 0) + g], b1 = A[2 * KB * 64 + (TS ? 28 : 4) + g];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < kNC; ++q) {
       const float inv = xinv[q] * wi;
       zq.z[q][0] = fma4s(acc[q][0], inv, b0);
       zq.z[q][1] = fma4s(acc[q][1], inv, b1);
@@ -1143,6 +1216,10 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
       zq.aux[0] = A[2 * KB * 64 + 16 + g];
       zq.aux[1] = A[2 * KB * 64 + 20 + g];
     }
+#ifdef NR_EXP_NO_EPI  // keep the MFMAs alive (their results would otherwise be dead code)
+#pragma unroll
+    for (int q = 0; q < kNC; ++q) asm volatile("" : : "v"(tof(zq.z[q][0])), "v"(tof(zq.z[q][1])));
+#endif
     ws.flip(npend);
   }
   pd.flush();  // chunk NCH-2's stores, put by its epilogue in the last iteration
@@ -1161,19 +1238,18 @@ __device__ __forceinline__ void sp_pair(const Z4& zz, int q, int k, float4 (&y)[
   else softplus_pk<NABLA>(z.z, z.w, y[o].z, y[o].w, s.z, s.w);
 }
 __device__ __forceinline__ float4 mul4(float4 a, float4 b) { return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w); }
-// slab layout [block][column][lane]: the chunk's blocks 2c, 2c+1 of both columns = 4 KB
+// slab layout [block][column][lane]: the chunk's blocks 2c, 2c+1 of all kNC columns = 2 kNC KB
 __device__ __forceinline__ uint32_t opaque_lane(int lane) {  // not hoistable: offsets built at use
   uint32_t l = (uint32_t)lane;
   asm volatile("" : "+v"(l));
   return l;
 }
-__device__ __forceinline__ void pend_chunk(Pend4& pd, float4* base, int first_blk, float4 c0b0, float4 c1b0,
-                                           float4 c0b1, float4 c1b1, int lane, bool nt) {
-  pd.v[0] = c0b0; pd.v[1] = c1b0; pd.v[2] = c0b1; pd.v[3] = c1b1;
+// pd.v[o * kNC + q] (block first_blk + o, column q) -> its slab slot
+__device__ __forceinline__ void pend_chunk(Pend4& pd, float4* base, int first_blk, int lane, bool nt) {
   const uint32_t l = opaque_lane(lane);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) pd.o[i] = (2 * first_blk + i) * 64 + l;
-  pd.put(base, 4, nt);
+  for (int i = 0; i < 2 * kNC; ++i) pd.o[i] = (kNC * first_blk + i) * 64 + l;
+  pd.put(base, 2 * kNC, nt);
 }
 
 // forward softplus op: out -> next operand (k-step c of oh/ol), slab <- L = log2(1 + 2^t).
@@ -1197,14 +1273,15 @@ template <bool NABLA>
 #define NR_LOG2(x) __builtin_amdgcn_logf(x)
 #endif
 struct FwdEpi4 {
-  f16x8 (&oh)[2][12];
-  f16x8 (&ol)[2][12];
-  const float (&sc)[2];  // operand scale of y (the split multiplies max(L, t) by sc * ln2/100)
+  static constexpr int NV = 8 * kNC;  // values per lane and chunk
+  f16x8 (&oh)[kNC][12];
+  f16x8 (&ol)[kNC][12];
+  const float (&sc)[kNC];  // operand scale of y (the split multiplies max(L, t) by sc * ln2/100)
   float4* sl;
-  float (&mrun)[2];
+  float (&mrun)[kNC];
   Pend4& pd;
   int lane;
-  float e[16], L[16], m[16];  // value i = (2q + o) * 4 + r: column q, block o, register r
+  float e[NV], L[NV], m[NV];  // value i = (2q + o) * 4 + r: column q, block o, register r
   __device__ __forceinline__ static float zval(const Z4& zz, int i) {
     const float4 v = zz.z[i >> 3][(i >> 2) & 1];
     const int r = i & 3;
@@ -1213,24 +1290,24 @@ struct FwdEpi4 {
   __device__ __forceinline__ void operator()(int c, const Z4& zz, int st) {
     if (st == 0) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) e[i] = fminf(zval(zz, i), 126.0f);
+      for (int i = 0; i < NV; ++i) e[i] = fminf(zval(zz, i), 126.0f);
     } else if (st == 1) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) e[i] = NR_EXP2(e[i]);
+      for (int i = 0; i < NV; ++i) e[i] = NR_EXP2(e[i]);
     } else if (st == 2) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) e[i] = e[i] + 1.0f;
+      for (int i = 0; i < NV; ++i) e[i] = e[i] + 1.0f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) L[i] = NR_LOG2(e[i]);
+      for (int i = 0; i < NV / 2; ++i) L[i] = NR_LOG2(e[i]);
     } else if (st == 3) {
 #pragma unroll
-      for (int i = 8; i < 16; ++i) L[i] = NR_LOG2(e[i]);
+      for (int i = NV / 2; i < NV; ++i) L[i] = NR_LOG2(e[i]);
     } else if (st == 4) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) m[i] = fmaxf(L[i], zval(zz, i));
+      for (int i = 0; i < NV; ++i) m[i] = fmaxf(L[i], zval(zz, i));
     } else if (st == 5) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
+      for (int q = 0; q < kNC; ++q) {
         const int i = 8 * q;
         float r = mrun[q];
         r = __builtin_fmaxf(r, __builtin_fmaxf(m[i + 0], m[i + 1]));
@@ -1241,11 +1318,11 @@ struct FwdEpi4 {
       }
       if constexpr (NABLA) {  // L straight into the pending-store slots ([block][column])
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
+        for (int q = 0; q < kNC; ++q)
 #pragma unroll
           for (int o = 0; o < 2; ++o) {
             const int i = (2 * q + o) * 4;
-            pd.v[2 * o + q] = make_float4(L[i], L[i + 1], L[i + 2], L[i + 3]);
+            pd.v[kNC * o + q] = make_float4(L[i], L[i + 1], L[i + 2], L[i + 3]);
           }
       }
     } else if (st == 6) {
@@ -1255,11 +1332,12 @@ struct FwdEpi4 {
 #endif
     } else {
 #ifndef NR_EXP_NO_EPISPLIT
-      split8a(make_float4(m[8], m[9], m[10], m[11]), make_float4(m[12], m[13], m[14], m[15]), sc[1] * kC, oh[1][c],
-              ol[1][c]);
+      if constexpr (kNC == 2)
+        split8a(make_float4(m[8], m[9], m[10], m[11]), make_float4(m[12], m[13], m[14], m[15]), sc[1] * kC,
+                oh[kNC - 1][c], ol[kNC - 1][c]);
 #endif
 #ifndef NR_EXP_NO_ESTORE  // timing experiment: softplus' slab not written
-      if constexpr (NABLA) pend_chunk(pd, sl, 2 * c, pd.v[0], pd.v[1], pd.v[2], pd.v[3], lane, true);
+      if constexpr (NABLA) pend_chunk(pd, sl, 2 * c, lane, true);
 #endif
     }
   }
@@ -1269,19 +1347,20 @@ struct FwdEpi4 {
 // h7 split for F8 when the geometry feature is wanted
 template <bool NABLA, bool FEAT>
 struct F7Epi4 {
-  f16x8 (&oh)[2][12];
-  f16x8 (&ol)[2][12];
-  const float (&sc)[2];
+  f16x8 (&oh)[kNC][12];
+  f16x8 (&ol)[kNC][12];
+  const float (&sc)[kNC];
   float4* g7;
-  float (&mrun)[2];
-  float (&sdf_part)[2];
+  float (&mrun)[kNC];
+  float (&sdf_part)[kNC];
   Pend4& pd;
   int lane;
-  float4 y[2][2], s[2][2];
+  float4 y[kNC][2], s[kNC][2];
   __device__ __forceinline__ void operator()(int c, const Z4& zz, int st) {
+    // stages 4q..4q+3: column q (one column per wave: stages 4..7 only finish the chunk)
     const int q = st >> 2, k = st & 3;
-    sp_pair<NABLA>(zz, q, k, y[q], s[q][0], s[q][1]);
-    if (k == 3) {
+    if (q < kNC) sp_pair<NABLA>(zz, q, k, y[q], s[q][0], s[q][1]);
+    if (q < kNC && k == 3) {
       const float4 w0 = zz.aux[0], w1 = zz.aux[1];
       float sp = sdf_part[q];
       sp = fmaf(y[q][0].x, w0.x, sp); sp = fmaf(y[q][0].y, w0.y, sp);
@@ -1291,7 +1370,7 @@ struct F7Epi4 {
       sdf_part[q] = sp;
       if constexpr (NABLA) {
         pd.v[q] = mul4(w0, s[q][0]);
-        pd.v[2 + q] = mul4(w1, s[q][1]);
+        pd.v[kNC + q] = mul4(w1, s[q][1]);
       }
       if constexpr (FEAT) {
         mrun[q] = amax8(mrun[q], y[q][0], y[q][1]);
@@ -1299,7 +1378,7 @@ struct F7Epi4 {
       }
     }
     if constexpr (NABLA)
-      if (st == 7) pend_chunk(pd, g7, 2 * c, pd.v[0], pd.v[1], pd.v[2], pd.v[3], lane, false);
+      if (st == 7) pend_chunk(pd, g7, 2 * c, lane, false);
   }
 };
 
@@ -1308,21 +1387,22 @@ struct F7Epi4 {
 // gradients, parked in fp32 from block park_blk on
 template <int NMAIN, class WS>
 struct BwdEpi4 {
-  f16x8 (&oh)[2][12];
-  f16x8 (&ol)[2][12];
-  const float (&sc)[2];
+  f16x8 (&oh)[kNC][12];
+  f16x8 (&ol)[kNC][12];
+  const float (&sc)[kNC];
   WS& ws;
   float4* park;
   int park_blk;
-  float (&mrun)[2];
+  float (&mrun)[kNC];
   Pend4& pd;
   int lane;
-  float4 y[2][2];
+  float4 y[kNC][2];
   __device__ __forceinline__ void operator()(int c, const Z4& zz, int st) {
     if (2 * c < NMAIN) {
       const int q = st >> 2, k = st & 3;
+      if (q >= kNC) return;
       if (k < 2) {  // g * softplus'(z) = g - g 2^-L  (FwdEpi4's slab)
-        const float4 Lv = ws.slab_read()[(2 * k + q) * 64 + lane];
+        const float4 Lv = ws.slab_read()[(kNC * k + q) * 64 + lane];
         const float4 gv = zz.z[q][k];
         y[q][k] = make_float4(__builtin_fmaf(-gv.x, NR_EXP2(-Lv.x), gv.x), __builtin_fmaf(-gv.y, NR_EXP2(-Lv.y), gv.y),
                               __builtin_fmaf(-gv.z, NR_EXP2(-Lv.z), gv.z), __builtin_fmaf(-gv.w, NR_EXP2(-Lv.w), gv.w));
@@ -1332,10 +1412,15 @@ struct BwdEpi4 {
 #ifndef NR_EXP_NO_EPISPLIT
         split8a(y[q][0], y[q][1], sc[q], oh[q][c], ol[q][c]);
 #endif
-        if (q == 1) ws.slab_consumed();
+        if (q == kNC - 1) ws.slab_consumed();
       }
     } else if (st == 7) {
-      pend_chunk(pd, park, park_blk + 2 * c - NMAIN, zz.z[0][0], zz.z[1][0], zz.z[0][1], zz.z[1][1], lane, false);
+#pragma unroll
+      for (int q = 0; q < kNC; ++q) {
+        pd.v[q] = zz.z[q][0];
+        pd.v[kNC + q] = zz.z[q][1];
+      }
+      pend_chunk(pd, park, park_blk + 2 * c - NMAIN, lane, false);
     }
   }
 };
@@ -1345,7 +1430,7 @@ struct NoPre4 {
 };
 
 template <bool NABLA, bool FEAT>
-__global__ __attribute__((amdgpu_flat_work_group_size(kT4, kT4), amdgpu_waves_per_eu(1, 1)))
+__global__ __attribute__((amdgpu_flat_work_group_size(kT4, kT4), amdgpu_waves_per_eu(kWPE, kWPE)))
 void sdf4_kernel(SdfKArgs a) {
   constexpr int CB = chunk_bytes(18);  // largest SDF op chunk (F4: 14 + 4 input blocks)
   constexpr int C16 = chunk_bytes(16), C4 = chunk_bytes(4), C14 = chunk_bytes(14), C18 = chunk_bytes(18);
@@ -1369,12 +1454,12 @@ void sdf4_kernel(SdfKArgs a) {
     return w + sdf_op_off(i);
   };
   const float b8 = *(const float*)(W + a.L.misc_off);
-  // this wave's slabs: [layer 8][block 16][column 2][lane 64] float4 (256 KB)
-  float4* escr = uniform_ptr(a.scratch + (size_t)(blockIdx.x * kW4 + wave) * (8 * 16 * 2 * 64));
+  // this wave's slabs: [layer 8][block 16][column kNC][lane 64] float4 (128 KB per column)
+  float4* escr = uniform_ptr(a.scratch + (size_t)(blockIdx.x * kW4 + wave) * (8 * 16 * kNC * 64));
   auto slab = [&](int l) {
     float4* e = escr;
     asm volatile("" : "+s"(e));
-    return e + l * 16 * 2 * 64;
+    return e + l * 16 * kNC * 64;
   };
 
   ws.template start<C4, C4>(OP(F0), OP(F0) + C4);
@@ -1385,12 +1470,12 @@ void sdf4_kernel(SdfKArgs a) {
   const int64_t Pn = a.P_dev ? min(a.P, (int64_t)(*a.P_dev) * a.P_mult) : a.P;
   for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < Pn; base += (int64_t)gridDim.x * kPointsPerWG) {
     const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < Pn;
-    const int64_t p0 = base + wave * 32;  // this wave's first point
-    int64_t pq[2];
-    bool valid[2];
-    float xs[2][3];
+    const int64_t p0 = base + wave * 16 * kNC;  // this wave's first point
+    int64_t pq[kNC];
+    bool valid[kNC];
+    float xs[kNC][3];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < kNC; ++q) {
       const int64_t p = p0 + 16 * q + j;
       valid[q] = p < Pn;
       pq[q] = valid[q] ? p : Pn - 1;
@@ -1398,11 +1483,11 @@ void sdf4_kernel(SdfKArgs a) {
       xs[q][1] = a.pts[pq[q] * 3 + 1];
       xs[q][2] = a.pts[pq[q] * 3 + 2];
     }
-    float4 E[2][4];
-    float mE[2], xinv[2];
-    f16x8 Uh[2][12], Ul[2][12], Vh[2][12], Vl[2][12];
+    float4 E[kNC][4];
+    float mE[kNC], xinv[kNC];
+    f16x8 Uh[kNC][12], Ul[kNC][12], Vh[kNC][12], Vl[kNC][12];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < kNC; ++q) {
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         const int f = 16 * b + 4 * g;
@@ -1423,71 +1508,77 @@ void sdf4_kernel(SdfKArgs a) {
     if constexpr (NABLA) {
       const uint32_t l = opaque_lane(lane);
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+      for (int q = 0; q < kNC; ++q)
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          const uint32_t off = (((12 + b) * 2 + q) * 64 + l) * 16u;
+          const uint32_t off = (((12 + b) * kNC + q) * 64 + l) * 16u;
           const f32x4 d = tof(E[q][b]);
           asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" : : "v"(off), "v"(d), "s"(epark) : "memory");
         }
     }
-    float mrun[2] = {0.0f, 0.0f};  // running max |output| of the op being computed (lane's values)
-    float m_in[2] = {mE[0], mE[1]};  // max |input| of the op being computed (per point)
+    float mrun[kNC], m_in[kNC];  // running max |output| of the op being computed (lane's values),
+#pragma unroll                   // max |input| of the op being computed (per point)
+    for (int q = 0; q < kNC; ++q) {
+      mrun[q] = 0.0f;
+      m_in[q] = mE[q];
+    }
     // (R, B) of the op about to run ride in its chunks' bias slot (floats 33, 34); its chunk 0 is
     // the current ring slot when it starts
-    auto next_scales = [&](int kb, float extra, const float (&floor_max)[2], float (&sc)[2]) {
+    auto next_scales = [&](int kb, float extra, const float (&floor_max)[kNC], float (&sc)[kNC]) {
       const float4 v = ws.buf()[2 * kb * 64 + 8];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) sc[q] = bound_scale(fmaxf(fmaf(v.y, m_in[q], v.z) + extra, floor_max[q]));
+      for (int q = 0; q < kNC; ++q) sc[q] = bound_scale(fmaxf(fmaf(v.y, m_in[q], v.z) + extra, floor_max[q]));
     };
     // end of an op: its output becomes the next operand; mscale converts the running max to output
     // units (forward softplus epilogues track max(L, t), i.e. y / (ln2/100))
-    auto finish = [&](const float (&sc)[2], float mscale = 1.0f) {
+    auto finish = [&](const float (&sc)[kNC], float mscale = 1.0f) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
+      for (int q = 0; q < kNC; ++q) {
         m_in[q] = max4_groups(mrun[q]) * mscale;
         mrun[q] = 0.0f;
         xinv[q] = 1.0f / sc[q];
       }
     };
-    const float zero2[2] = {0.0f, 0.0f};
-    auto fwd_epi = [&](f16x8(&oh)[2][12], f16x8(&ol)[2][12], const float (&sc)[2], float4* sl) {
+    float zero2[kNC];
+#pragma unroll
+    for (int q = 0; q < kNC; ++q) zero2[q] = 0.0f;
+    auto fwd_epi = [&](f16x8(&oh)[kNC][12], f16x8(&ol)[kNC][12], const float (&sc)[kNC], float4* sl) {
       return FwdEpi4<NABLA>{oh, ol, sc, sl, mrun, pd, lane};
     };
 
     // ---- forward (base.py:243-257) -------------------------------------------------------------
     {
-      float sc[2];
+      float sc[kNC];
       next_scales(4, kSpSlack, zero2, sc);
       op4<4, 16, C16, false, true>(ws, OP(F0), OP(F1), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(0)), lane);
       finish(sc, kC);
     }
     {
-      float sc[2];
+      float sc[kNC];
       next_scales(16, kSpSlack, zero2, sc);
       op4<16, 16, C16, false, true>(ws, OP(F1), OP(F2), Vh, Vl, xinv, pd, nopre, fwd_epi(Uh, Ul, sc, slab(1)), lane);
       finish(sc, kC);
     }
     {
-      float sc[2];
+      float sc[kNC];
       next_scales(16, kSpSlack, zero2, sc);
       op4<16, 16, C16, false, true>(ws, OP(F2), OP(F3), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(2)), lane);
       finish(sc, kC);
     }
     {
       // F3's outputs (h3: 217 rows in 14 blocks) and the embedding form F4's operand: one scale
-      float sc[2];
+      float sc[kNC];
       next_scales(16, kSpSlack, mE, sc);
       op4<16, 14, C18, false, true>(ws, OP(F3), OP(F4), Vh, Vl, xinv, pd, nopre, fwd_epi(Uh, Ul, sc, slab(3)), lane);
       if constexpr (NABLA) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
+        for (int q = 0; q < kNC; ++q)
 #pragma unroll
-          for (int b = 0; b < 4; ++b) E[q][b] = fromf(*((const gf4*)epark + ((12 + b) * 2 + q) * 64 + lane));
+          for (int b = 0; b < 4; ++b) E[q][b] = fromf(*((const gf4*)epark + ((12 + b) * kNC + q) * 64 + lane));
       }
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
+      for (int q = 0; q < kNC; ++q) {
         split8a(E[q][0], E[q][1], sc[q], Uh[q][7], Ul[q][7]);
         split8a(E[q][2], E[q][3], sc[q], Uh[q][8], Ul[q][8]);
         mrun[q] = fmaxf(mrun[q], mE[q] * (1.0f / kC));  // mrun is in max(L, t) units here
@@ -1495,28 +1586,30 @@ void sdf4_kernel(SdfKArgs a) {
       finish(sc, kC);
     }
     {
-      float sc[2];
+      float sc[kNC];
       next_scales(18, kSpSlack, zero2, sc);
       op4<18, 16, C16, false, true>(ws, OP(F4), OP(F5), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(4)), lane);
       finish(sc, kC);
     }
     {
-      float sc[2];
+      float sc[kNC];
       next_scales(16, kSpSlack, zero2, sc);
       op4<16, 16, C16, false, true>(ws, OP(F5), OP(F6), Vh, Vl, xinv, pd, nopre, fwd_epi(Uh, Ul, sc, slab(5)), lane);
       finish(sc, kC);
     }
     {
-      float sc[2];
+      float sc[kNC];
       next_scales(16, kSpSlack, zero2, sc);
       op4<16, 16, C16, false, true>(ws, OP(F6), OP(F7), Uh, Ul, xinv, pd, nopre, fwd_epi(Vh, Vl, sc, slab(6)), lane);
       finish(sc, kC);
     }
     // F7: softplus, sdf row (aux = W8[0, :]) as a running dot product, d sdf / d z7 parked in slab 7,
     // h7 split for F8 when the geometry feature is wanted
-    float sdf_part[2] = {0.0f, 0.0f};
+    float sdf_part[kNC];
+#pragma unroll
+    for (int q = 0; q < kNC; ++q) sdf_part[q] = 0.0f;
     {
-      float sc[2];
+      float sc[kNC];
       next_scales(16, kSpSlack, zero2, sc);
       F7Epi4<NABLA, FEAT> epi{Uh, Ul, sc, slab(7), mrun, sdf_part, pd, lane};
       constexpr int NXT = (NABLA || FEAT) ? C16 : C4;
@@ -1525,7 +1618,7 @@ void sdf4_kernel(SdfKArgs a) {
       finish(sc);
     }
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < kNC; ++q) {
       const float sdf = wave_sum4(sdf_part[q]) + b8;
       if (valid[q] && g == 0) a.sdf[p0 + 16 * q + j] = sdf;
     }
@@ -1534,20 +1627,20 @@ void sdf4_kernel(SdfKArgs a) {
       const int64_t pf = p0 < Pn ? p0 : Pn - 1;
       float4* fb = uniform_ptr((float4*)(a.feature + pf * 256));
       // clamped lanes (past the end) rewrite the last point's row with that point's own values
-      uint32_t frow[2];
+      uint32_t frow[kNC];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) frow[q] = (uint32_t)(pq[q] - pf);
+      for (int q = 0; q < kNC; ++q) frow[q] = (uint32_t)(pq[q] - pf);
       auto epi = [&](int c, const Z4& zz, int st) {
         if (st != 7) return;
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < kNC; ++q) {
           pd.v[2 * q] = zz.z[q][0];
           pd.v[2 * q + 1] = zz.z[q][1];
           const uint32_t r = opaque_lane(frow[q] * 64 + g);
           pd.o[2 * q] = r + (2 * c) * 4;
           pd.o[2 * q + 1] = r + (2 * c + 1) * 4;
         }
-        pd.put(fb, 4, false);
+        pd.put(fb, 2 * kNC, false);
       };
       constexpr int NXT = NABLA ? C16 : C4;
       const char* n = NABLA ? OP(B7) : (has_next ? OP(F0) : nullptr);
@@ -1559,10 +1652,10 @@ void sdf4_kernel(SdfKArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       float4* g7 = slab(7);
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {  // d sdf / d z7 from slab 7, split with the exact max scale
+      for (int q = 0; q < kNC; ++q) {  // d sdf / d z7 from slab 7, split with the exact max scale
         float4 G[16];
 #pragma unroll
-        for (int b = 0; b < 16; ++b) G[b] = fromf(*((const gf4*)g7 + (2 * b + q) * 64 + lane));
+        for (int b = 0; b < 16; ++b) G[b] = fromf(*((const gf4*)g7 + (kNC * b + q) * 64 + lane));
         float m = 0.0f;
 #pragma unroll
         for (int b = 0; b < 16; b += 2) m = amax8(m, G[b], G[b + 1]);
@@ -1579,11 +1672,11 @@ void sdf4_kernel(SdfKArgs a) {
       // NMAIN/2 are embedding gradients, parked in fp32
       ws.stage_slab(slab(6), 0);  // B7's chunk 0 (consumed in B7's second iteration)
       auto bwd = [&](auto kb_tag, auto nbo_tag, auto nmain_tag, auto nxt_tag, int opi, const char* nxt,
-                     f16x8(&ih)[2][12], f16x8(&il)[2][12], f16x8(&oh)[2][12], f16x8(&ol)[2][12], int lcur,
+                     f16x8(&ih)[kNC][12], f16x8(&il)[kNC][12], f16x8(&oh)[kNC][12], f16x8(&ol)[kNC][12], int lcur,
                      int park_blk, int lnext) {
         constexpr int KBo = decltype(kb_tag)::value, NBOo = decltype(nbo_tag)::value;
         constexpr int NMAIN = decltype(nmain_tag)::value, NXC = decltype(nxt_tag)::value;
-        float sc[2];
+        float sc[kNC];
         next_scales(KBo, 0.0f, zero2, sc);
         auto pre = [&](int c) -> int {
           if (2 * (c + 1) < NMAIN) return ws.stage_slab(slab(lcur), c + 1);
@@ -1615,12 +1708,12 @@ void sdf4_kernel(SdfKArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // chain rule through the positional encoding (autograd sums both uses of embed(x))
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
+      for (int q = 0; q < kNC; ++q) {
         float n0 = 0.f, n1 = 0.f, n2 = 0.f;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          const float4 u = fromf(*((const gf4*)park + (2 * b + q) * 64 + lane));
-          const float4 v = fromf(*((const gf4*)park + (2 * (4 + b) + q) * 64 + lane));
+          const float4 u = fromf(*((const gf4*)park + (kNC * b + q) * 64 + lane));
+          const float4 v = fromf(*((const gf4*)park + (kNC * (4 + b) + q) * 64 + lane));
           const int f = 16 * b + 4 * g;
           embed_backward(f + 0, fadd(v.x, u.x), xs[q][0], xs[q][1], xs[q][2], a.nfreq, n0, n1, n2);
           embed_backward(f + 1, fadd(v.y, u.y), xs[q][0], xs[q][1], xs[q][2], a.nfreq, n0, n1, n2);

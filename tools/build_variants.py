@@ -2,7 +2,8 @@
 with NR_LIB=...).  Variants switch off parts of the MLP kernels (results are NOT valid) to measure
 what each part costs: NR_EXP_NO_DMA, NR_EXP_NO_ESTORE, NR_EXP_NO_ELOAD, NR_EXP_NO_EPI, NR_EXP_NO_MFMA,
 NR_EXP_NO_TRANS (epilogue transcendentals), NR_EXP_NO_EPISPLIT (next-operand split),
-NR_EXP_SHARED_W (backward ops re-stream the forward weights: half the weight footprint)."""
+NR_EXP_SHARED_W (backward ops re-stream the forward weights: half the weight footprint).
+NR_SDF4_NC=1 is a layout choice, not an experiment: its results are valid."""
 import os
 import subprocess
 import sys
@@ -33,6 +34,31 @@ VARIANTS = {
     'sharedw': ['-DNR_EXP_SHARED_W'],
     'v3noepisplit': ['-DNR_EXP_NO_EPISPLIT'],
     'v3nomfma_noepi': ['-DNR_EXP_NO_MFMA', '-DNR_EXP_NO_EPI'],
+    # sdf4_kernel layouts (valid results): nc2 = 32-point waves, one per SIMD (the r02 default)
+    'nc2': ['-DNR_SDF4_NC=2'],
+    'nc1': ['-DNR_SDF4_NC=1'],
+    'nc1nodma': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_DMA'],
+    'nc1nobar': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_BARRIER'],
+    'nc1noepi': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_EPI'],
+    'nc1nomfma': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_MFMA'],
+    'nc1nomfma_noepi': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_MFMA', '-DNR_EXP_NO_EPI'],
+    'nc1noslab': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_ESTORE', '-DNR_EXP_NO_ELOAD'],
+    'nc1notrans': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_TRANS'],
+    # skeleton decomposition (no MFMA, no epilogue): DMA only / fragment reads only / no barrier
+    'nc1sk_noaread': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_MFMA', '-DNR_EXP_NO_EPI', '-DNR_EXP_NO_AREAD'],
+    'nc1sk_nodma': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_MFMA', '-DNR_EXP_NO_EPI', '-DNR_EXP_NO_DMA'],
+    'nc1sk_nobar': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_MFMA', '-DNR_EXP_NO_EPI', '-DNR_EXP_NO_BARRIER'],
+    'nc1sk_noslab': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_MFMA', '-DNR_EXP_NO_EPI', '-DNR_EXP_NO_ESTORE', '-DNR_EXP_NO_ELOAD'],
+    'nc1sk_dmaonly': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_MFMA', '-DNR_EXP_NO_EPI', '-DNR_EXP_NO_AREAD',
+                      '-DNR_EXP_NO_ESTORE', '-DNR_EXP_NO_ELOAD'],
+    'nc1noaread': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_AREAD'],
+    # B operands in VGPRs (no AGPR moves; valid results)
+    'nc1v': ['-DNR_SDF4_NC=1', '-DNR_SPLIT_VGPR'],
+    # weight DMA pieces spread over the k-step regions (valid results)
+    'nc1vs': ['-DNR_SDF4_NC=1', '-DNR_SPLIT_VGPR', '-DNR_DMA_SPREAD'],
+    'nc2s': ['-DNR_DMA_SPREAD'],
+    'nc1vnoepi': ['-DNR_SDF4_NC=1', '-DNR_SPLIT_VGPR', '-DNR_EXP_NO_EPI'],
+    'nc2noepi': ['-DNR_EXP_NO_EPI'],
 }
 
 
