@@ -13,7 +13,7 @@
      defined(NR_EXP_NO_SOFTPLUS) || defined(NR_EXP_NO_SPLIT) || defined(NR_EXP_NO_BARRIER) ||       \
      defined(NR_EXP_UNROLL) || defined(NR_EXP_NO_PINGPONG) || defined(NR_EXP_NO_EPI) ||             \
      defined(NR_EXP_NO_MFMA) || defined(NR_EXP_NO_TRANS) || defined(NR_EXP_NO_EPISPLIT) ||   \
-     defined(NR_EXP_SHARED_W) || defined(NR_EXP_NO_AREAD))
+     defined(NR_EXP_SHARED_W) || defined(NR_EXP_NO_AREAD) || defined(NR_EXP_STAMPS))
 #error "NR_EXP_* experiment switches are for tools/build_variants.py builds only"
 #endif
 

@@ -882,6 +882,11 @@ constexpr int kT4 = 64 * kW4;
 constexpr int kWPE = kW4 / 4;     // waves per SIMD
 constexpr int kSlabW = 2 * kNC * 1024;  // one chunk's slab values of one wave (2 blocks x kNC columns)
 constexpr int kSlab4 = kW4 * kSlabW;    // ... of the workgroup: 16 KB
+#ifndef NR_DMA_LOADERS
+#define NR_DMA_LOADERS (8 / NR_SDF4_NC)
+#endif
+constexpr int kLoad = NR_DMA_LOADERS;  // waves that issue the weight stream (the last kLoad)
+static_assert(kLoad >= 1 && kLoad <= kW4, "loader waves");
 
 // Deferred stores of one chunk (up to 4 x 16 B per lane), issued at the start of the next chunk
 // before its weight DMA, so flip()'s counted wait never stands behind a store younger than the
@@ -894,6 +899,7 @@ struct Pend4 {
   bool nt;
   // global_store_dwordx4 with an SGPR base and a 32-bit VGPR byte offset (saddr form), from asm:
   // compiler-built 64-bit per-lane addresses get hoisted out of the tile loop and spilled
+  __device__ __forceinline__ int pending() const { return base ? n : 0; }
   __device__ __forceinline__ int flush() {
     int issued = 0;
     if (base) {
@@ -931,10 +937,14 @@ struct WStream4 {
   int er;      // slab slot the next consumed chunk's epilogue reads
   __device__ __forceinline__ static int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
   __device__ __forceinline__ static int next3(int i) { return i == 2 ? 0 : i + 1; }
-  // BYTES/1 KB pieces; every wave issues ceil(pieces/kW4) (a wave past the end repeats the last
-  // piece: identical bytes to the same LDS address) so the count is one constant in every wave
+  // BYTES/1 KB pieces; every loader wave (the last kLoad of the workgroup) issues ceil(pieces/kLoad)
+  // (a wave past the end repeats the last piece: identical bytes to the same LDS address) so the
+  // count is one constant in every loader wave
   template <int BYTES>
-  __device__ __forceinline__ static constexpr int pieces() { return (BYTES / 1024 + kW4 - 1) / kW4; }
+  __device__ __forceinline__ static constexpr int pieces() { return (BYTES / 1024 + kLoad - 1) / kLoad; }
+  __device__ __forceinline__ static int loader() { return wave_id() - (kW4 - kLoad); }  // < 0: no DMA
+  template <int BYTES>
+  __device__ __forceinline__ static int npieces() { return loader() >= 0 ? pieces<BYTES>() : 0; }
   // Each wave moves a contiguous run of NPW pieces (the last wave's run is shifted back to end at
   // the chunk's end; overlapping pieces are identical bytes to the same LDS address), up to 4 per
   // M0 setting: the instruction offset steps the global and the LDS address together.
@@ -944,7 +954,8 @@ struct WStream4 {
     return;
 #endif
     constexpr int NB = BYTES / 1024, NPW = pieces<BYTES>();
-    const int wave = wave_id();
+    const int wave = loader();
+    if (wave < 0) return;
     const uint32_t voff = (threadIdx.x & 63) * 16;
     const int first = __builtin_amdgcn_readfirstlane(min(wave * NPW, NB - NPW));
     const char* g = uniform_ptr(gsrc) + first * 1024;
@@ -992,7 +1003,8 @@ struct WStream4 {
     return;
 #endif
     constexpr int NB = BYTES / 1024, NPW = pieces<BYTES>();
-    const int first = __builtin_amdgcn_readfirstlane(min(wave_id() * NPW, NB - NPW)) + j;
+    if (loader() < 0) return;
+    const int first = __builtin_amdgcn_readfirstlane(min(loader() * NPW, NB - NPW)) + j;
     const int slot = cur == 0 ? 2 : cur - 1;
     glds16m(uniform_ptr(gsrc) + first * 1024, (threadIdx.x & 63) * 16,
             __builtin_amdgcn_readfirstlane(lds_u32(lds) + (uint32_t)(slot * CBMAX) + (uint32_t)(first * 1024)));
@@ -1004,7 +1016,7 @@ struct WStream4 {
     er = 0;
     dma<B0>(g0, 0);
     dma<B1>(g1, 1);
-    wait_vmcnt(pieces<B1>());
+    wait_vmcnt(npieces<B1>());
     __syncthreads();
   }
   template <int BYTES>
@@ -1134,6 +1146,24 @@ struct Z4 {
 constexpr float kT = 144.26944f;
 constexpr float kC = 0.0069314749f;
 
+#ifdef NR_EXP_STAMPS
+// timing experiment: per-wave shader-clock totals of the four phases of a chunk iteration (VMEM
+// issue, MFMA loop + epilogue stages, bias + vmcnt wait, barrier), copied out at the end of the launch
+constexpr int kStampPh = 5;  // 4 phases + iteration count
+__device__ unsigned long long g_nr_stamps[2048 * 8 * kStampPh];
+__device__ __forceinline__ unsigned long long* stamp_lds() {
+  __shared__ unsigned long long s_stamp[kW4 * kStampPh];
+  return s_stamp;
+}
+__device__ __forceinline__ uint64_t stamp_now() { return __builtin_amdgcn_s_memtime(); }
+__device__ __forceinline__ void stamp_add(int ph, uint64_t dt) {
+  if ((threadIdx.x & 63) == 0) stamp_lds()[(threadIdx.x >> 6) * kStampPh + ph] += dt;
+}
+#define NR_STAMP(var) const uint64_t var = stamp_now()
+#else
+#define NR_STAMP(var)
+#endif
+
 template <int KB, int NBO, int NXT_CB, bool AUX, bool TS, class WS, class Pre, class Epi>
 __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const char* nxt, const f16x8 (&bh)[kNC][12],
                                     const f16x8 (&bl)[kNC][12], const float (&xinv)[kNC], Pend4& pd, Pre&& pre,
@@ -1149,6 +1179,7 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
     const char* opc = op;
     const char* nxc = nxt;
     asm volatile("" : "+s"(opc), "+s"(nxc));
+    NR_STAMP(t0);
     int npend = 0;
 #ifdef NR_DMA_SPREAD  // the chunk-two-ahead's pieces go out one per k-step region, beside the MFMAs
     const char* dsrc = nullptr;
@@ -1156,29 +1187,37 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
     if (c + 2 < NCH) {
       dsrc = opc + (c + 2) * CB;
       dkind = 1;
-      npend = WS::template pieces<CB>();
+      npend = WS::template npieces<CB>();
     } else if (nxc) {
       dsrc = nxc + (c + 2 - NCH) * NXT_CB;
       dkind = 2;
-      npend = WS::template pieces<NXT_CB>();
+      npend = WS::template npieces<NXT_CB>();
     }
 #else
     if (c + 2 < NCH) {
       ws.template issue<CB>(opc + (c + 2) * CB);
-      npend = WS::template pieces<CB>();
+      npend = WS::template npieces<CB>();
     } else if (nxc) {
       ws.template issue<NXT_CB>(nxc + (c + 2 - NCH) * NXT_CB);
-      npend = WS::template pieces<NXT_CB>();
+      npend = WS::template npieces<NXT_CB>();
     }
 #endif
     npend += pre(c);
+#ifdef NR_VMEM_SPREAD  // the previous chunk's stores go out inside the MFMA loop (k-step region 0)
+    npend += pd.pending();
+#else
     // the previous chunk's stores go out after this chunk's DMA: this chunk's flip does not wait for
     // them (the next one does, two chunk-times after issue)
     npend += pd.flush();
+#endif
+    NR_STAMP(t1);
     const float4* A = ws.buf();
     f32x4 acc[kNC][2] = {};
     // the previous chunk's epilogue, 8 stages spread over this chunk's KB/2 k-steps
     mma4<KB / 2>(A, bh, bl, acc, lane, [&](int st) {
+#ifdef NR_VMEM_SPREAD
+      if (st == 0) pd.flush();
+#endif
 #ifdef NR_DMA_SPREAD
       {
         constexpr int NS = KB / 2, N1 = WS::template pieces<CB>(), N2 = WS::template pieces<NXT_CB>();
@@ -1203,6 +1242,7 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
           if (e * (KB / 2) / 8 == st) epi(c - 1, zq, e);
       }
     });
+    NR_STAMP(t2);
     float wi = A[2 * KB * 64 + 8].x;
     if constexpr (TS) wi *= kT;
     const float4 b0 = A[2 * KB * 64 + (TS ? 24 : 0) + g], b1 = A[2 * KB * 64 + (TS ? 28 : 4) + g];
@@ -1220,7 +1260,19 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
 #pragma unroll
     for (int q = 0; q < kNC; ++q) asm volatile("" : : "v"(tof(zq.z[q][0])), "v"(tof(zq.z[q][1])));
 #endif
+#ifdef NR_EXP_STAMPS
+    wait_vmcnt(npend);
+    NR_STAMP(t3);
     ws.flip(npend);
+    NR_STAMP(t4);
+    stamp_add(0, t1 - t0);
+    stamp_add(1, t2 - t1);
+    stamp_add(2, t3 - t2);
+    stamp_add(3, t4 - t3);
+    stamp_add(4, 1);
+#else
+    ws.flip(npend);
+#endif
   }
   pd.flush();  // chunk NCH-2's stores, put by its epilogue in the last iteration
 #pragma unroll
@@ -1462,6 +1514,13 @@ void sdf4_kernel(SdfKArgs a) {
     return e + l * 16 * kNC * 64;
   };
 
+#ifdef NR_EXP_STAMPS
+  if ((threadIdx.x & 63) == 0)
+    for (int i = 0; i < kStampPh; ++i) stamp_lds()[wave * kStampPh + i] = 0;
+#endif
+#ifdef NR_SDF4_PRIO  // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD)
+  if (kWPE == 2 && wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
   ws.template start<C4, C4>(OP(F0), OP(F0) + C4);
   Pend4 pd{};
   NoPre4 nopre;
@@ -1734,6 +1793,11 @@ void sdf4_kernel(SdfKArgs a) {
   }
   pd.flush();
   wait_vmcnt(0);  // a block without tiles still has the prologue's second chunk in flight
+#ifdef NR_EXP_STAMPS
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 2048)
+    for (int i = 0; i < kStampPh; ++i)
+      g_nr_stamps[(blockIdx.x * kW4 + wave) * kStampPh + i] = stamp_lds()[wave * kStampPh + i];
+#endif
 }
 
 // =============================================================================================
@@ -2337,3 +2401,12 @@ int launch_radiance(const RadLayout& L, const void* packed, const float* x, cons
 }
 
 }  // namespace nr
+
+#ifdef NR_EXP_STAMPS
+// per-wave phase totals of the last sdf4_kernel launch (timing experiment builds only)
+extern "C" int nr_exp_stamps(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(nr::g_nr_stamps), sizeof(unsigned long long) * (size_t)n) == hipSuccess
+             ? nr::kW4 * nr::kStampPh
+             : -1;
+}
+#endif

@@ -36,6 +36,16 @@ VARIANTS = {
     'v3nomfma_noepi': ['-DNR_EXP_NO_MFMA', '-DNR_EXP_NO_EPI'],
     # sdf4_kernel layouts (valid results): nc2 = 32-point waves, one per SIMD (the r02 default)
     'nc2': ['-DNR_SDF4_NC=2'],
+    'ld4': ['-DNR_DMA_LOADERS=4'],
+    'ld4s': ['-DNR_DMA_LOADERS=4', '-DNR_DMA_SPREAD'],
+    'ld2': ['-DNR_DMA_LOADERS=2'],
+    # per-phase shader-clock totals (tools/mlp_driver.py --stamps)
+    'stamps': ['-DNR_EXP_STAMPS'],
+    'stamps_nc2': ['-DNR_EXP_STAMPS', '-DNR_SDF4_NC=2'],
+    'stamps_s': ['-DNR_EXP_STAMPS', '-DNR_DMA_SPREAD', '-DNR_VMEM_SPREAD'],
+    'vs': ['-DNR_DMA_SPREAD', '-DNR_VMEM_SPREAD'],
+    'ds': ['-DNR_DMA_SPREAD'],
+    'prio': ['-DNR_SDF4_PRIO'],
     'nc1': ['-DNR_SDF4_NC=1'],
     'nc1nodma': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_DMA'],
     'nc1nobar': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_BARRIER'],

@@ -16,6 +16,7 @@ def main():
     ap.add_argument('--iters', type=int, default=5)
     ap.add_argument('--precision', default='f16x3')
     ap.add_argument('--mode', default='nabla', choices=['nabla', 'nabla0', 'fwd', 'radiance'])
+    ap.add_argument('--stamps', action='store_true', help='print sdf4_kernel phase totals (stamps build)')
     a = ap.parse_args()
     from neurecon_amd.base import ImplicitSurface, RadianceNet
     torch.manual_seed(0)
@@ -42,6 +43,20 @@ def main():
         torch.cuda.synchronize()
     dt = (time.perf_counter() - t) / a.iters
     print(f'{a.mode} {a.precision}: {a.points} points, {dt * 1e3:.3f} ms/launch-set')
+    if a.stamps:
+        import ctypes
+        import numpy as np
+        from neurecon_amd import _lib as L
+        buf = np.zeros(2048 * 8 * 5, dtype=np.uint64)
+        nw = L.lib().nr_exp_stamps(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(buf.size))
+        v = buf.reshape(-1, 5)
+        v = v[v[:, 4] > 0]
+        tot = v[:, :4].sum(1)
+        names = ['vmem issue', 'mfma loop', 'bias+vmcnt', 'barrier']
+        print(f'waves {len(v)} (per WG {nw // 5}), chunk iterations/wave {v[:, 4].mean():.0f}, '
+              f'clocks/iteration {tot.mean() / v[:, 4].mean():.0f}')
+        for i, n in enumerate(names):
+            print(f'  {n:12s} {v[:, i].mean() / v[:, 4].mean():8.0f} clk/iter  {100 * v[:, i].sum() / tot.sum():5.1f} %')
 
 
 if __name__ == '__main__':
