@@ -1021,6 +1021,9 @@ struct WStream4 {
   }
   template <int BYTES>
   __device__ __forceinline__ void issue(const char* gsrc) { dma<BYTES>(gsrc, cur == 0 ? 2 : cur - 1); }
+  // after a mid-chunk flip (cur already names the next chunk's slot): the chunk after that
+  template <int BYTES>
+  __device__ __forceinline__ void issue_next(const char* gsrc) { dma<BYTES>(gsrc, next3(cur)); }
   // this wave's softplus' slab of chunk c (blocks 2c, 2c+1, all kNC columns: 2 or 4 KB contiguous) ->
   // the next slab slot; one M0 setting, the instruction offset steps global and LDS address together.
   // Staged two chunk-iterations before the epilogue that reads it.  Returns the DMA instructions issued.
@@ -1193,7 +1196,7 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
       dkind = 2;
       npend = WS::template npieces<NXT_CB>();
     }
-#else
+#elif !defined(NR_MID_FLIP)
     if (c + 2 < NCH) {
       ws.template issue<CB>(opc + (c + 2) * CB);
       npend = WS::template npieces<CB>();
@@ -1215,6 +1218,17 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
     f32x4 acc[kNC][2] = {};
     // the previous chunk's epilogue, 8 stages spread over this chunk's KB/2 k-steps
     mma4<KB / 2>(A, bh, bl, acc, lane, [&](int st) {
+#ifdef NR_MID_FLIP
+      // the flip sits in the middle of the chunk's MFMA stream: waves reach the barrier with MFMAs
+      // still in the pipe, and the next chunk starts without one.  The wait covers chunk c+1's
+      // weights (issued at the previous chunk's flip); everything issued since is this iteration's.
+      // Then chunk c+2 goes into the slot chunk c-1 left (every wave is past it).
+      if (st == KB / 4) {
+        ws.flip(npend);
+        if (c + 2 < NCH) ws.template issue_next<CB>(opc + (c + 2) * CB);
+        else if (nxc) ws.template issue_next<NXT_CB>(nxc + (c + 2 - NCH) * NXT_CB);
+      }
+#endif
 #ifdef NR_VMEM_SPREAD
       if (st == 0) pd.flush();
 #endif
@@ -1263,14 +1277,16 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
 #ifdef NR_EXP_STAMPS
     wait_vmcnt(npend);
     NR_STAMP(t3);
+#ifndef NR_MID_FLIP
     ws.flip(npend);
+#endif
     NR_STAMP(t4);
     stamp_add(0, t1 - t0);
     stamp_add(1, t2 - t1);
     stamp_add(2, t3 - t2);
     stamp_add(3, t4 - t3);
     stamp_add(4, 1);
-#else
+#elif !defined(NR_MID_FLIP)
     ws.flip(npend);
 #endif
   }

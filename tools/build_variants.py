@@ -46,6 +46,8 @@ VARIANTS = {
     'vs': ['-DNR_DMA_SPREAD', '-DNR_VMEM_SPREAD'],
     'ds': ['-DNR_DMA_SPREAD'],
     'prio': ['-DNR_SDF4_PRIO'],
+    'mid': ['-DNR_MID_FLIP'],
+    'mid_nc2': ['-DNR_MID_FLIP', '-DNR_SDF4_NC=2'],
     'nc1': ['-DNR_SDF4_NC=1'],
     'nc1nodma': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_DMA'],
     'nc1nobar': ['-DNR_SDF4_NC=1', '-DNR_EXP_NO_BARRIER'],
