@@ -471,6 +471,24 @@ int nr_neus_composite_bg_bwd(const float* sdf, const float* s_dev, const float* 
                              const float* g_weights, float* d_sdf, float* d_rad, float* d_sigma_out,
                              float* d_rad_out, float* d_s, void* workspace, size_t workspace_bytes, void* stream);
 
+/* VolSDF training compositing (replaces the autograd graph of volsdf.py:449-506 with the builtin
+ * background of volsdf.py:317-325 and sdf_to_sigma volsdf.py:16-35).  sdf [R,S] network values at
+ * pts [R,S,3], beta_dev [1] = exp(ln_beta * speed_factor), radiance [R,S,3] (the first S-1 rows are
+ * composited), d_all [R,S] sorted depths.  use_bg: min(sdf, r_bg - |x|).  Outputs rgb [R,3], depth [R],
+ * acc [R], tau [R,S-1] (visibility weights), optional p_i [R,S-1], sigma [R,S], sdf_out [R,S]
+ * (background applied).  The backward takes the output gradients (each may be NULL) and returns
+ * d sdf [R,S] (0 where the background value was taken), d radiance [R,S,3] and d beta per ray [R]. */
+int nr_volsdf_composite_fwd(const float* sdf, const float* pts, const float* beta_dev, const float* rad,
+                            const float* d_all, int64_t R, int S, int use_bg, float r_bg, int white_bkgd, float* rgb,
+                            float* depth, float* acc, float* tau, float* p_i, float* sigma, float* sdf_out,
+                            void* stream);
+size_t nr_volsdf_composite_bwd_workspace_bytes(int64_t R, int S);
+int nr_volsdf_composite_bwd(const float* sdf, const float* pts, const float* beta_dev, const float* rad,
+                            const float* d_all, int64_t R, int S, int use_bg, float r_bg, int white_bkgd,
+                            const float* g_rgb, const float* g_depth, const float* g_acc, const float* g_tau,
+                            const float* g_sdf, float* d_sdf, float* d_rad, float* d_beta, void* workspace,
+                            size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Opt-in kernel timing (diagnostics / bench roofline).  While enabled, every kernel launch of
  * the library is bracketed by hipEvents on its stream; nr_profile_read() waits for them and

@@ -165,6 +165,11 @@ _SIGS = {
     'nr_neus_composite_bg_bwd_workspace_bytes': (_c_sz, [_c_i64, _c_i, _c_i]),
     'nr_neus_composite_bg_bwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_i, _c_p, _c_p,
                                         _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
+    'nr_volsdf_composite_fwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_f, _c_i, _c_p, _c_p, _c_p,
+                                       _c_p, _c_p, _c_p, _c_p, _c_p]),
+    'nr_volsdf_composite_bwd_workspace_bytes': (_c_sz, [_c_i64, _c_i]),
+    'nr_volsdf_composite_bwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_f, _c_i, _c_p, _c_p, _c_p,
+                                       _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
     'nr_profile_enable': (_c_i, [_c_i]),
     'nr_profile_read': (_c_i, [ctypes.POINTER(NrKernelStat), _c_i, ctypes.POINTER(_c_i)]),
 }

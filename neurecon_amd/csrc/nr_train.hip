@@ -330,6 +330,167 @@ __global__ void neus_composite_bwd_kernel(const float* __restrict__ sdf, const f
   d_s[r] = (float)sbar;
 }
 
+// ---- VolSDF compositing with a graph (volsdf.py:449-506) ----------------------------------------------
+// One thread per ray.  sdf [R,S] are the network's values at pts [R,S,3]; with the builtin background
+// sphere (volsdf.py:317-325) a sample whose r_bg - |x| is smaller takes that value instead (and then
+// passes no gradient to the network).  sigma = sdf_to_sigma(sdf, 1/beta, beta) (volsdf.py:16-35),
+// p_i = exp(-relu(sigma_i delta_i)), tau_i = (1 - p_i + 1e-10) prod_{j<i} p_j over the first S-1
+// samples; rgb = sum tau radiance[:S-1], depth = sum tau / (sum tau + 1e-10) d, acc = sum tau.  fp64
+// prefix products / sums rounded per element, as in the render kernel (volsdf_composite).
+__device__ __forceinline__ float vs_sigma_t(float v, float alpha, float beta) {
+  const float e = fmul(0.5f, expf(fdiv(-fabsf(v), beta)));
+  return fmul(alpha, v >= 0.0f ? e : fsub(1.0f, e));
+}
+__device__ __forceinline__ float vs_sdf_bg(const float* sdf, const float* pts, int64_t i, int use_bg, float r_bg,
+                                           bool& masked) {
+  float v = sdf[i];
+  masked = false;
+  if (use_bg) {
+    const float x = pts[i * 3], y = pts[i * 3 + 1], z = pts[i * 3 + 2];
+    const float dbg = fsub(r_bg, __fsqrt_rn(fadd(fadd(fmul(x, x), fmul(y, y)), fmul(z, z))));
+    if (dbg < v) {
+      v = dbg;
+      masked = true;
+    }
+  }
+  return v;
+}
+__global__ void volsdf_composite_fwd_kernel(const float* __restrict__ sdf, const float* __restrict__ pts,
+                                            const float* __restrict__ beta_dev, const float* __restrict__ rad,
+                                            const float* __restrict__ d_all, int64_t R, int S, int use_bg, float r_bg,
+                                            int white_bkgd, float* __restrict__ rgb, float* __restrict__ depth,
+                                            float* __restrict__ acc, float* __restrict__ tau_out,
+                                            float* __restrict__ p_out, float* __restrict__ sigma_out,
+                                            float* __restrict__ sdf_out) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const float beta = *beta_dev, alpha = fdiv(1.0f, beta);
+  const int S1 = S - 1;
+  const float* d = d_all + r * S;
+  double T = 1.0, a_acc = 0.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
+  bool m;
+  float sg = vs_sigma_t(vs_sdf_bg(sdf, pts, r * S, use_bg, r_bg, m), alpha, beta);
+  for (int i = 0; i < S; ++i) {
+    const int64_t q = r * S + i;
+    const float v = vs_sdf_bg(sdf, pts, q, use_bg, r_bg, m);
+    const float si = vs_sigma_t(v, alpha, beta);
+    if (sdf_out) sdf_out[q] = v;
+    if (sigma_out) sigma_out[q] = si;
+    if (i == 0) continue;
+    // sample i-1's interval
+    const float p = expf(-fmaxf(fmul(sg, fsub(d[i], d[i - 1])), 0.0f));
+    const float tau = fmul(fadd(fsub(1.0f, p), 1e-10f), (float)T);
+    T *= (double)p;
+    const int64_t k = r * S1 + i - 1;
+    const float* rr = rad + (r * S + i - 1) * 3;
+    c0 += (double)fmul(tau, rr[0]);
+    c1 += (double)fmul(tau, rr[1]);
+    c2 += (double)fmul(tau, rr[2]);
+    a_acc += (double)tau;
+    tau_out[k] = tau;
+    if (p_out) p_out[k] = p;
+    sg = si;
+  }
+  const float accf = (float)a_acc;
+  const float den = fadd(accf, 1e-10f);
+  double dep = 0.0;
+  for (int i = 0; i < S1; ++i) dep += (double)fmul(fdiv(tau_out[r * S1 + i], den), d[i]);
+  float o0 = (float)c0, o1 = (float)c1, o2 = (float)c2;
+  if (white_bkgd) {
+    const float bg = fsub(1.0f, accf);
+    o0 = fadd(o0, bg); o1 = fadd(o1, bg); o2 = fadd(o2, bg);
+  }
+  rgb[r * 3 + 0] = o0;
+  rgb[r * 3 + 1] = o1;
+  rgb[r * 3 + 2] = o2;
+  depth[r] = (float)dep;
+  acc[r] = accf;
+}
+
+// backward of the above: grads of rgb [R,3], depth [R], acc [R], tau [R,S-1] and the background-applied
+// sdf [R,S] (all optional) -> d sdf (network values) [R,S], d radiance [R,S,3] (the last sample's row is
+// 0: volsdf.py:495 uses radiances[..., :-1, :]), d beta per ray [R] (the host sums; both the alpha = 1/beta
+// and the psi(beta) paths).  tau_i = u_i P_i with u_i = 1 - p_i + 1e-10 and P_i = prod_{j<i} p_j, so
+// pbar_i = P_i (G_i - taubar_i) with G_i = sum_{k>i} taubar_k u_k prod_{i<j<k} p_j (no division by p).
+__global__ void volsdf_composite_bwd_kernel(const float* __restrict__ sdf, const float* __restrict__ pts,
+                                            const float* __restrict__ beta_dev, const float* __restrict__ rad,
+                                            const float* __restrict__ d_all, int64_t R, int S, int use_bg, float r_bg,
+                                            int white_bkgd, const float* __restrict__ g_rgb,
+                                            const float* __restrict__ g_depth, const float* __restrict__ g_acc,
+                                            const float* __restrict__ g_tau, const float* __restrict__ g_sdf,
+                                            float* __restrict__ work, float* __restrict__ d_sdf,
+                                            float* __restrict__ d_rad, float* __restrict__ d_beta) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const float beta = *beta_dev, alpha = fdiv(1.0f, beta);
+  const int S1 = S - 1;
+  const float* d = d_all + r * S;
+  // work rows: v (bg-applied sdf) [S], sigma [S], p [S], P [S], tau [S]
+  float* v = work + r * (5 * S);
+  float* sg = v + S;
+  float* p = sg + S;
+  float* P = p + S;
+  float* tau = P + S;
+  double T = 1.0, a_acc = 0.0, wd = 0.0;
+  for (int i = 0; i < S; ++i) {
+    bool m;
+    v[i] = vs_sdf_bg(sdf, pts, r * S + i, use_bg, r_bg, m);
+    sg[i] = vs_sigma_t(v[i], alpha, beta);
+  }
+  for (int i = 0; i < S1; ++i) {
+    p[i] = expf(-fmaxf(fmul(sg[i], fsub(d[i + 1], d[i])), 0.0f));
+    P[i] = (float)T;
+    tau[i] = fmul(fadd(fsub(1.0f, p[i]), 1e-10f), P[i]);
+    T *= (double)p[i];
+    a_acc += (double)tau[i];
+  }
+  const float accf = (float)a_acc;
+  const double A = (double)fadd(accf, 1e-10f);
+  for (int i = 0; i < S1; ++i) wd += (double)tau[i] * (double)d[i];
+  const float gr0 = g_rgb ? g_rgb[r * 3 + 0] : 0.f, gr1 = g_rgb ? g_rgb[r * 3 + 1] : 0.f,
+              gr2 = g_rgb ? g_rgb[r * 3 + 2] : 0.f;
+  const double gd = g_depth ? (double)g_depth[r] : 0.0;
+  const double ga = (g_acc ? (double)g_acc[r] : 0.0) - (white_bkgd ? (double)gr0 + gr1 + gr2 : 0.0);
+  double G = 0.0, bbar = 0.0;
+  const double ib2 = 1.0 / ((double)beta * beta);
+  for (int i = S - 1; i >= 0; --i) {
+    const int64_t q = r * S + i;
+    double vbar = 0.0;
+    if (i < S1) {
+      const float* rr = rad + q * 3;
+      double tb = (double)gr0 * rr[0] + (double)gr1 * rr[1] + (double)gr2 * rr[2] + ga;
+      tb += gd * ((double)d[i] / A - wd / (A * A));
+      if (g_tau) tb += (double)g_tau[r * S1 + i];
+      d_rad[q * 3 + 0] = fmul(tau[i], gr0);
+      d_rad[q * 3 + 1] = fmul(tau[i], gr1);
+      d_rad[q * 3 + 2] = fmul(tau[i], gr2);
+      const double u = (double)fadd(fsub(1.0f, p[i]), 1e-10f);
+      const double pbar = (double)P[i] * (G - tb);
+      G = tb * u + (double)p[i] * G;
+      const float delta = fsub(d[i + 1], d[i]);
+      if (fmul(sg[i], delta) > 0.0f) {
+        const double sbar = -pbar * (double)p[i] * (double)delta;
+        // sigma = alpha psi(v, beta), psi = e or 1 - e, e = 0.5 exp(-|v| / beta)
+        const double e = (double)fmul(0.5f, expf(fdiv(-fabsf(v[i]), beta)));
+        const double sgn = v[i] > 0.0f ? 1.0 : (v[i] < 0.0f ? -1.0 : 0.0);
+        const double psi = v[i] >= 0.0f ? e : 1.0 - e;
+        const double br = v[i] >= 0.0f ? 1.0 : -1.0;  // d psi / d e
+        vbar = sbar * (double)alpha * br * e * (-sgn / (double)beta);
+        bbar += sbar * (psi * (-ib2) + (double)alpha * br * e * fabs((double)v[i]) * ib2);
+      }
+    } else {
+      d_rad[q * 3 + 0] = 0.0f;
+      d_rad[q * 3 + 1] = 0.0f;
+      d_rad[q * 3 + 2] = 0.0f;
+    }
+    if (g_sdf) vbar += (double)g_sdf[q];
+    bool m;
+    (void)vs_sdf_bg(sdf, pts, q, use_bg, r_bg, m);
+    d_sdf[q] = m ? 0.0f : (float)vbar;
+  }
+  d_beta[r] = (float)bbar;
+}
+
 // ---- NeRF++ background in the training step (neus.py:303-343) ------------------------------------
 // inputs of the background MLP at the R x M depths d_out (= cat([d_mid, d_vals_out])): p = o + d dir,
 // x4 = [p / |p|, 1 / |p|] embedded with 10 log-sampled frequencies (Embedder(input_dim=4)), the view
@@ -710,6 +871,41 @@ int nr_neus_composite_bg_bwd(const float* sdf, const float* s_dev, const float* 
   hipLaunchKernelGGL(neus_composite_bg_bwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
                      sdf, s_dev, rad, sigma_out, rad_out, d_out, inside, R, S, M, white_bkgd, g_rgb, g_depth, g_acc,
                      g_weights, (float*)workspace, d_sdf, d_rad, d_sigma_out, d_rad_out, d_s);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_volsdf_composite_fwd(const float* sdf, const float* pts, const float* beta_dev, const float* rad,
+                            const float* d_all, int64_t R, int S, int use_bg, float r_bg, int white_bkgd, float* rgb,
+                            float* depth, float* acc, float* tau, float* p_i, float* sigma, float* sdf_out,
+                            void* stream) {
+  NR_REQUIRE(sdf && pts && beta_dev && rad && d_all && rgb && depth && acc && tau && R >= 0 && S >= 2, NR_ERR_ARG,
+             "nr_volsdf_composite_fwd: bad argument");
+  if (R == 0) return NR_OK;
+  hipLaunchKernelGGL(volsdf_composite_fwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
+                     sdf, pts, beta_dev, rad, d_all, R, S, use_bg, r_bg, white_bkgd, rgb, depth, acc, tau, p_i, sigma,
+                     sdf_out);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+size_t nr_volsdf_composite_bwd_workspace_bytes(int64_t R, int S) {
+  return (size_t)(R > 0 ? R : 1) * 5 * (size_t)S * sizeof(float);
+}
+
+int nr_volsdf_composite_bwd(const float* sdf, const float* pts, const float* beta_dev, const float* rad,
+                            const float* d_all, int64_t R, int S, int use_bg, float r_bg, int white_bkgd,
+                            const float* g_rgb, const float* g_depth, const float* g_acc, const float* g_tau,
+                            const float* g_sdf, float* d_sdf, float* d_rad, float* d_beta, void* workspace,
+                            size_t workspace_bytes, void* stream) {
+  NR_REQUIRE(sdf && pts && beta_dev && rad && d_all && d_sdf && d_rad && d_beta && R >= 0 && S >= 2, NR_ERR_ARG,
+             "nr_volsdf_composite_bwd: bad argument");
+  if (R == 0) return NR_OK;
+  NR_REQUIRE(workspace && workspace_bytes >= nr_volsdf_composite_bwd_workspace_bytes(R, S), NR_ERR_WORKSPACE,
+             "nr_volsdf_composite_bwd: workspace too small");
+  hipLaunchKernelGGL(volsdf_composite_bwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
+                     sdf, pts, beta_dev, rad, d_all, R, S, use_bg, r_bg, white_bkgd, g_rgb, g_depth, g_acc, g_tau,
+                     g_sdf, (float*)workspace, d_sdf, d_rad, d_beta);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

@@ -3,7 +3,9 @@
 `volume_render(rays_o, rays_d, model, **kw) -> (rgb, depth, extras)` keeps the reference's
 signature, argument meaning, output shapes and extras keys (volsdf.py:377-551).  The whole path
 (error-bounded sampling with bisection on beta+, final SDF + nablas + radiance, Laplace-CDF density
-compositing, builtin background sphere) runs in libnrhip.so (`nr_volsdf_render`).
+compositing, builtin background sphere) runs in libnrhip.so (`nr_volsdf_render`).  With grad enabled
+(training) the render builds an autograd graph (`_train_render`) and `Trainer` computes the
+reference's losses (volsdf.py:564-640).
 """
 import copy
 import ctypes
@@ -12,10 +14,11 @@ from collections import OrderedDict
 import numpy as np
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .. import _lib as L
 from .. import rend_util
-from ..base import ImplicitSurface, NeRF, RadianceNet, _no_training, check_view_dirs
+from ..base import ImplicitSurface, NeRF, RadianceNet, check_view_dirs, wants_graph
 from .neus import _linspace_table
 
 
@@ -115,7 +118,13 @@ def volume_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=
     """volsdf.py:377-551, render mode.  rays_o/rays_d: [(B,) N_rays, 3].  perturb=True: random final
     fine samples and NeRF++ strata (_volsdf_uniforms)."""
     L.require_gpu(rays_o, 'rays_o')
-    _no_training(model)
+    if wants_graph(model):
+        return _train_render(rays_o, rays_d, model, near=near, far=far, obj_bounding_radius=obj_bounding_radius,
+                             batched=batched, calc_normal=calc_normal, use_view_dirs=use_view_dirs, rayschunk=rayschunk,
+                             white_bkgd=white_bkgd, use_nerfplusplus=use_nerfplusplus, detailed_output=detailed_output,
+                             perturb=perturb, N_samples=N_samples, N_importance=N_importance, N_outside=N_outside,
+                             max_upsample_steps=max_upsample_steps, max_bisection_steps=max_bisection_steps,
+                             epsilon=epsilon)
     check_view_dirs(model, use_view_dirs)
     dev = rays_o.device
     prefix = [rays_d.shape[0], -1] if batched else [-1]
@@ -218,6 +227,75 @@ def volume_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=
     return ret['rgb'], ret['depth_volume'], ret
 
 
+def _train_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=3.0, batched=False, calc_normal=False,
+                  use_view_dirs=True, rayschunk=65536, white_bkgd=False, use_nerfplusplus=False, detailed_output=True,
+                  perturb=False, N_samples=128, N_importance=64, N_outside=32, max_upsample_steps=5,
+                  max_bisection_steps=10, epsilon=0.1):
+    """volsdf.py:377-551 with an autograd graph (training): the sample depths d_all come from the
+    no-grad render path (error-bounded fine sampling, volsdf.py:420-445, the same call under
+    torch.no_grad), then SDF + nablas + geometry feature at every sample (double-backward capable),
+    the radiance net and the background / sdf_to_sigma / integration as neurecon_amd.training
+    autograd functions.  Gradients reach every surface and radiance parameter and ln_beta.  Returns
+    the reference's (rgb, depth, extras)."""
+    from .. import training as T
+    check_view_dirs(model, use_view_dirs)
+    if use_nerfplusplus:
+        raise NotImplementedError('neurecon_amd: VolSDF training with the NeRF++ background has no native path '
+                                  '(the builtin background sphere trains natively)')
+    dev = rays_o.device
+    prefix = [rays_d.shape[0], -1] if batched else [-1]
+    with torch.no_grad():
+        _, _, ex = volume_render(rays_o, rays_d, model, near=near, far=far, obj_bounding_radius=obj_bounding_radius,
+                                 batched=batched, calc_normal=False, use_view_dirs=use_view_dirs, rayschunk=rayschunk,
+                                 white_bkgd=white_bkgd, use_nerfplusplus=False, detailed_output=True, perturb=perturb,
+                                 N_samples=N_samples, N_importance=N_importance, max_upsample_steps=max_upsample_steps,
+                                 max_bisection_steps=max_bisection_steps, epsilon=epsilon)
+    ro = rays_o.reshape(-1, 3).float().contiguous()
+    rd_raw = rays_d.reshape(-1, 3).float().contiguous()
+    n = ro.shape[0]
+    S = N_samples + N_importance
+    d_all = ex['d_vals'].reshape(n, S).contiguous()
+    rd = torch.empty_like(rd_raw)  # F.normalize(rays_d, dim=-1) (volsdf.py:386)
+    L.check(L.lib().nr_normalize3(L.ptr(rd_raw), n, L.ptr(rd), L.stream_of(dev)))
+    pts = torch.empty(n, S, 3, device=dev)
+    mids = torch.empty(n, S - 1, 3, device=dev)
+    dmid = torch.empty(n, S - 1, device=dev)
+    L.check(L.lib().nr_neus_points(L.ptr(ro), L.ptr(rd), L.ptr(d_all), n, S, L.ptr(pts), L.ptr(mids), L.ptr(dmid),
+                                   L.stream_of(dev)))
+    sdf, nablas, feat = T.sdf_nablas(model.implicit_surface, pts.reshape(-1, 3), True)      # volsdf.py:450
+    view = rd[:, None, :].expand(n, S, 3).reshape(-1, 3).contiguous()
+    rad = T.radiance(model.radiance_net, pts.reshape(-1, 3), view, nablas, feat)
+    _, beta = model.forward_ab()
+    rgb, depth, acc, tau, sdf_bg, p_i, sigma = T.VolSDFComposite.apply(
+        sdf.reshape(n, S), beta, rad.reshape(n, S, 3), pts, d_all, bool(model.use_sphere_bg),
+        float(model.obj_bounding_radius), bool(white_bkgd))
+    nablas = nablas.reshape(n, S, 3)
+    ret = OrderedDict([('rgb', rgb.reshape(*prefix, 3)), ('depth_volume', depth.reshape(prefix)),
+                       ('mask_volume', acc.reshape(prefix))])
+    if calc_normal:  # volsdf.py:508-512
+        nrm = F.normalize(nablas, dim=-1)
+        k = min(tau.shape[-1], nrm.shape[-2])
+        ret['normals_volume'] = (nrm[:, :k, :] * tau[:, :k, None]).sum(dim=-2).reshape(*prefix, 3)
+    if detailed_output:
+        ret['implicit_surface'] = sdf_bg.reshape(*prefix, S)
+        ret['implicit_nablas'] = nablas.reshape(*prefix, S, 3)
+        ret['radiance'] = rad.reshape(*prefix, S, 3)
+        ret['alpha'] = (1.0 - p_i).reshape(*prefix, S - 1)
+        ret['p_i'] = p_i.reshape(*prefix, S - 1)
+        ret['visibility_weights'] = tau.reshape(*prefix, S - 1)
+        ret['d_vals'] = d_all.reshape(*prefix, S)
+        ret['sigma'] = sigma.reshape(*prefix, S)
+        ret['beta_map'] = ex['beta_map'].reshape(*prefix, 1)
+        ret['iter_usage'] = ex['iter_usage'].reshape(prefix)
+    return ret['rgb'], ret['depth_volume'], ret
+
+
+def eikonal_points(like, bound):
+    """volsdf.py:609: torch.empty_like(nablas).uniform_(-bound, bound) (the eikonal samples of the
+    training step; a module function so tests can replay the reference's draws)."""
+    return torch.empty_like(like).uniform_(-bound, bound)
+
+
 class SingleRenderer(nn.Module):
     """volsdf.py:555-561."""
 
@@ -230,8 +308,11 @@ class SingleRenderer(nn.Module):
 
 
 class Trainer(nn.Module):
-    """volsdf.py:564-640.  The training step needs the backward of the render kernels (SURVEY.md §8f);
-    the render call raises while grad is enabled."""
+    """volsdf.py:564-640: one training step's forward -- random rays of the image, the render with a
+    graph (neurecon_amd.training autograd functions on libnrhip.so), L1 rgb + eikonal losses (the
+    nabla of each ray's highest-weight sample and one uniform point per ray).  Returns
+    OrderedDict(losses=..., extras=...) like the reference; train.py calls backward() on
+    losses['total'] (under DDP the gradient all-reduce runs over RCCL)."""
 
     def __init__(self, model, device_ids=[0], batched=True):
         super().__init__()
@@ -241,13 +322,42 @@ class Trainer(nn.Module):
             self.renderer = nn.DataParallel(self.renderer, device_ids=device_ids, dim=1 if batched else 0)
         self.device = device_ids[0]
 
-    def forward(self, args, indices, model_input, ground_truth, render_kwargs_train, it):
-        device = self.device
+    def forward(self, args, indices, model_input, ground_truth, render_kwargs_train, it, device='cuda'):
+        from ..config import as_cfg
+        args = as_cfg(args)
         intrinsics = model_input['intrinsics'].to(device)
         c2w = model_input['c2w'].to(device)
-        rays_o, rays_d, select_inds = rend_util.get_rays(c2w, intrinsics, render_kwargs_train['H'],
-                                                         render_kwargs_train['W'], N_rays=args.data.N_rays)
-        return self.renderer(rays_o, rays_d, detailed_output=True, **render_kwargs_train)
+        H, W = render_kwargs_train['H'], render_kwargs_train['W']
+        rays_o, rays_d, select_inds = rend_util.get_rays(c2w, intrinsics, H, W, N_rays=args.data.N_rays)
+        target_rgb = rend_util.gather_rays(ground_truth['rgb'].to(device), select_inds)      # volsdf.py:588
+        mask_ignore = rend_util.gather_rays(model_input['mask_ignore'].to(device), select_inds) \
+            if 'mask_ignore' in model_input else None
+        rgb, depth_v, extras = self.renderer(rays_o, rays_d, detailed_output=True, **render_kwargs_train)
+        nablas = extras['implicit_nablas']
+        # one point per ray: the sample of highest visibility weight (volsdf.py:604-605)
+        _, ind = extras['visibility_weights'][..., :nablas.shape[-2]].max(dim=-1)
+        nablas = torch.gather(nablas, dim=-2, index=ind[..., None, None].repeat([*(len(nablas.shape) - 1) * [1], 3]))
+        eik = eikonal_points(nablas, args.model.obj_bounding_radius)                      # volsdf.py:607-610
+        _, nablas_eik, _ = self.model.implicit_surface.forward_with_nablas(eik)
+        nablas = torch.cat([nablas, nablas_eik], dim=-2)
+        nablas_norm = torch.norm(nablas, dim=-1)
+        losses = OrderedDict()
+        losses['loss_img'] = F.l1_loss(rgb, target_rgb, reduction='none')
+        losses['loss_eikonal'] = args.training.w_eikonal * F.mse_loss(
+            nablas_norm, nablas_norm.new_ones(nablas_norm.shape), reduction='mean')
+        if mask_ignore is not None:
+            losses['loss_img'] = (losses['loss_img'] * mask_ignore[..., None].float()).sum() / (mask_ignore.sum() + 1e-10)
+        else:
+            losses['loss_img'] = losses['loss_img'].mean()
+        loss = 0
+        for k, v in losses.items():
+            loss += losses[k]
+        losses['total'] = loss
+        extras['implicit_nablas_norm'] = nablas_norm
+        alpha, beta = self.model.forward_ab()
+        extras['scalars'] = {'beta': beta.data, 'alpha': alpha.data}
+        extras['select_inds'] = select_inds
+        return OrderedDict([('losses', losses), ('extras', extras)])
 
 
 def get_model(args):

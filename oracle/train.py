@@ -9,6 +9,7 @@ import torch.nn.functional as F
 from . import rays as R
 from .nets import NeRFNet, SDFNet, RadianceNet
 from .neus import NeuSOracle, alpha_to_w, sdf_to_alpha
+from .volsdf import VolSDFOracle, sdf_to_sigma
 
 
 def nablas_graph(net, x):
@@ -70,4 +71,45 @@ def neus_train_losses(sd, rays_o, rays_d, target_rgb, target_mask, w_eikonal=0.1
     else:
         losses['loss_img'] = losses['loss_img'].mean()
     losses['total'] = sum(losses.values())
+    return losses, d_all
+
+
+def volsdf_train_losses(sd, rays_o, rays_d, target_rgb, eik_points, w_eikonal=0.1, d_all=None, speed_factor=10.0,
+                        obj_bounding_radius=3.0, near=0.0, far=6.0, N_samples=64, N_importance=64,
+                        max_upsample_steps=6):
+    """losses of one VolSDF training step (models/frameworks/volsdf.py:564-640; render :415-506 with
+    a graph, builtin background sphere): L1 rgb + w_eikonal * MSE(|nabla|, 1) over the highest-weight
+    sample of each ray and one eikonal point per ray (eik_points [B, N, 1, 3], the reference's
+    uniform_(-R, R) draws).  d_all [B, N, S] optional (the sorted sample depths; from the oracle's
+    no-grad fine sampling when None)."""
+    o = rays_o.reshape(rays_o.shape[0], -1, 3).float()
+    d = F.normalize(rays_d.reshape(rays_d.shape[0], -1, 3).float(), dim=-1)
+    if d_all is None:
+        orc = VolSDFOracle({k: v.detach() for k, v in sd.items()}, speed_factor=speed_factor,
+                           obj_bounding_radius=obj_bounding_radius)
+        with torch.no_grad():
+            d_all = orc.render(rays_o, rays_d, near=near, far=far, calc_normal=False, N_samples=N_samples,
+                               N_importance=N_importance, max_upsample_steps=max_upsample_steps)['d_vals']
+    sdf_net = SDFNet(sd)
+    rad_net = RadianceNet(sd, multires=-1, multires_view=-1)
+    pts = o[..., None, :] + d[..., None, :] * d_all[..., :, None]            # volsdf.py:446
+    sdf, nablas, h = nablas_graph(sdf_net, pts)                               # volsdf.py:450, :317-325
+    d_bg = obj_bounding_radius - pts.norm(dim=-1)
+    sdf = torch.where(d_bg < sdf, d_bg, sdf)
+    rad = rad_net.forward(pts, d.unsqueeze(-2).expand_as(pts), nablas, h)
+    beta = torch.exp(sd['ln_beta'] * speed_factor)                            # volsdf.py:306-308
+    sigma = sdf_to_sigma(sdf, 1. / beta, beta)
+    delta = d_all[..., 1:] - d_all[..., :-1]                                  # volsdf.py:482-495
+    p = torch.exp(-F.relu(sigma[..., :-1] * delta))
+    tau = (1 - p + 1e-10) * torch.cumprod(torch.cat([torch.ones_like(p[..., :1]), p], -1), -1)[..., :-1]
+    rgb = torch.sum(tau[..., None] * rad[..., :-1, :], -2)
+    _, ind = tau[..., :nablas.shape[-2]].max(dim=-1)                          # volsdf.py:604-610
+    nab = torch.gather(nablas, dim=-2, index=ind[..., None, None].repeat([*(len(nablas.shape) - 1) * [1], 3]))
+    _, nab_eik, _ = nablas_graph(sdf_net, eik_points)
+    nab = torch.cat([nab, nab_eik], dim=-2)
+    nablas_norm = torch.norm(nab, dim=-1)
+    losses = {'loss_img': F.l1_loss(rgb, target_rgb, reduction='none').mean(),
+              'loss_eikonal': w_eikonal * F.mse_loss(nablas_norm, nablas_norm.new_ones(nablas_norm.shape),
+                                                     reduction='mean')}
+    losses['total'] = losses['loss_img'] + losses['loss_eikonal']
     return losses, d_all

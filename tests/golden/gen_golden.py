@@ -628,6 +628,45 @@ def _gen_train(R, name, seed, N_outside):
          **_grad_summary(model.named_parameters()))
 
 
+def gen_train_volsdf(R):
+    """One VolSDF training step (models/frameworks/volsdf.py:564-640 -> train.py:205 backward) on an
+    8x8 camera (64 rays, N_rays=-1), builtin background, 64 + 64 samples, 6 upsampling rounds,
+    perturb=False, seeded random targets; the eikonal points (torch's uniform_(-3, 3), volsdf.py:609)
+    are recorded from the reference's own call so the GPU test can replay them."""
+    import types as _t
+    sd = wg.volsdf_state(seed=3, beta_init=0.1)
+    model = _volsdf_model(R, sd, 0.1)
+    model.train()
+    H = W = 8
+    c2w = wg.look_at_c2w(2.7)[None]
+    K = wg.intrinsics(20.0, H, W)[None]
+    g = torch.Generator().manual_seed(6)
+    target_rgb = torch.rand(1, H * W, 3, generator=g)
+    seen = []
+    fwn = model.implicit_surface.forward_with_nablas
+
+    def rec(x, *a, **k):
+        seen.append(x.detach().clone())
+        return fwn(x, *a, **k)
+    model.implicit_surface.forward_with_nablas = rec
+    args = _t.SimpleNamespace(data=_t.SimpleNamespace(N_rays=-1), model=_t.SimpleNamespace(obj_bounding_radius=3.0),
+                              training=_t.SimpleNamespace(w_eikonal=0.1))
+    kw = dict(H=H, W=W, near=0.0, far=6.0, obj_bounding_radius=3.0, batched=True, perturb=False, white_bkgd=False,
+              max_upsample_steps=6, use_nerfplusplus=False, N_samples=64, N_importance=64)
+    trainer = R.volsdf.Trainer(model, device_ids=[0], batched=True)
+    trainer.device = 'cpu'
+    torch.manual_seed(9)
+    ret = trainer.forward(args, None, {'intrinsics': K, 'c2w': c2w}, {'rgb': target_rgb}, kw, 0)
+    losses = {k: torch.mean(v) for k, v in ret['losses'].items()}
+    model.zero_grad()
+    losses['total'].backward()
+    ex = ret['extras']
+    save('volsdf_train.npz', seed=3, beta_init=0.1, H=H, W=W, f=20.0, dist=2.7, target_rgb=target_rgb, c2w=c2w, K=K,
+         eik_points=seen[-1], **{f'loss/{k}': v.detach() for k, v in losses.items()},
+         rgb=ex['rgb'].detach(), d_vals=ex['d_vals'].detach(), iter_usage=ex['iter_usage'].detach(),
+         **_grad_summary(model.named_parameters()))
+
+
 def main():
     torch.set_num_threads(8)
     R = _import_reference()
@@ -635,7 +674,7 @@ def main():
     gens = dict(components=gen_components, sampling=gen_sampling, neus=gen_neus, volsdf=gen_volsdf,
                 unisurf=gen_unisurf, surface=gen_surface,
                 volsdf_nerfpp=gen_volsdf_nerfpp, perturb=gen_perturb, train=gen_train, options=gen_options,
-                volsdf_perturb=gen_volsdf_perturb, siren=gen_siren)
+                volsdf_perturb=gen_volsdf_perturb, siren=gen_siren, train_volsdf=gen_train_volsdf)
     for name, fn in gens.items():
         if not only or name in only:
             fn(R)

@@ -1,4 +1,4 @@
-"""GPU parity of the training path: the NeuS training step's losses and EVERY
+"""GPU parity of the training path: the NeuS and VolSDF training steps' losses and EVERY
 parameter gradient -- through the double backward of the SDF MLP's nablas -- vs the oracle's
 autograd (oracle/train.py, pinned to the reference's own Trainer.forward + backward by
 tests/test_oracle_golden.py::test_oracle_train_step_vs_golden) and vs that reference golden.
@@ -17,8 +17,8 @@ import pytest
 import torch
 
 import weightgen as wg
-from helpers import neus_model, report
-from test_oracle_golden import check_grads, train_grads_oracle
+from helpers import neus_model, report, volsdf_model
+from test_oracle_golden import check_grads, train_grads_oracle, volsdf_train_grads_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -106,6 +106,52 @@ def test_neus_train_step_vs_oracle_and_golden(golden, precision, name):
     if torch.allclose(d_own, d_all, rtol=1e-6, atol=1e-6):
         check_grads(grads, g, RTOL, atol_frac, net_scale=net_scale)
         print(f'{precision}: sample depths match the reference (1e-6) -> gradients checked against the golden too')
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
+def test_volsdf_train_step_vs_oracle_and_golden(golden, precision, monkeypatch):
+    """VolSDF's training step (volsdf.py:564-640): losses and every parameter gradient -- surface net
+    through the double backward of the nablas, radiance net, ln_beta through sdf_to_sigma -- vs the
+    oracle on the GPU's sample depths, and vs the reference's golden when the depths agree.  The
+    eikonal points replay the reference's draws (volsdf.py:609).  Absolute term: 2e-4 of the largest
+    gradient of the parameter's network, twice the reference's own fp32 sensitivity: its gradients
+    move by up to 1.0e-5 (surface) and 1.0e-4 (radiance) of their network's largest gradient (1e-4 /
+    3.7e-4 of a tensor's) when the positional encodings move by one fp32 ulp
+    (tools/train_sensitivity.py volsdf_train; radiance ReLUs at their kink flip).  Measured here: 1.0e-4
+    (fp32 sample pass) and 1.8e-6 (f16x3 sample pass: other depths, no ReLU near its kink)."""
+    from neurecon_amd.frameworks import volsdf as V
+    g = golden('volsdf_train')
+    T = lambda a: torch.from_numpy(np.asarray(a)).cuda()
+    eik = T(g['eik_points'])
+    monkeypatch.setattr(V, 'eikonal_points', lambda like, bound: eik.reshape(like.shape).to(like.dtype))
+    beta0 = float(g['beta_init'])
+    m = volsdf_model(wg.volsdf_state(seed=int(g['seed']), beta_init=beta0), beta0, precision=precision)
+    m.train()
+    args = types.SimpleNamespace(data=types.SimpleNamespace(N_rays=-1),
+                                 model=types.SimpleNamespace(obj_bounding_radius=3.0),
+                                 training=types.SimpleNamespace(w_eikonal=0.1))
+    kw = dict(H=int(g['H']), W=int(g['W']), near=0.0, far=6.0, obj_bounding_radius=3.0, batched=True, perturb=False,
+              white_bkgd=False, max_upsample_steps=6, use_nerfplusplus=False, N_samples=64, N_importance=64)
+    ret = V.Trainer(m, device_ids=[0]).forward(args, None, {'intrinsics': T(g['K']), 'c2w': T(g['c2w'])},
+                                               {'rgb': T(g['target_rgb'])}, kw, 0, device='cuda')
+    losses = {k: torch.mean(v) for k, v in ret['losses'].items()}
+    m.zero_grad()
+    losses['total'].backward()
+    torch.cuda.synchronize()
+    grads = {k: p.grad.detach().cpu() for k, p in m.named_parameters() if p.grad is not None}
+    d_all = ret['extras']['d_vals'].detach().cpu()
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    ref_losses, ref_grads, _ = volsdf_train_grads_oracle(g, d_all=d_all)
+    for k in ('loss_img', 'loss_eikonal', 'total'):
+        a, b = float(losses[k]), float(ref_losses[k])
+        print(f'{precision} {k}: gpu {a:.8f} oracle {b:.8f} golden {float(g["loss/" + k]):.8f}')
+        assert abs(a - b) <= 1e-5 * abs(b) + 1e-7
+    worst = check_grads(grads, _as_golden(ref_grads, g), RTOL, 2e-4, net_scale=True)
+    print(f'{precision}: worst gradient error / network scale {worst:.3e}')
+    same = torch.allclose(d_all, torch.from_numpy(g['d_vals']), rtol=1e-6, atol=1e-6)
+    print(f'{precision}: sample depths {"match" if same else "differ from"} the reference (1e-6)')
+    if same:
+        check_grads(grads, g, RTOL, 2e-4, net_scale=True)
 
 
 def _as_golden(ref_grads, g):
