@@ -336,6 +336,12 @@ typedef struct {
   /* root finding method (unisurf.py:76 `method`, ray_casting.py:128): 0 = 'secant'; any other method
    * skips the secant refinement and reports depth 1 on hits, as the reference does */
   int no_secant;
+  /* training (unisurf.py:140-211 under torch.no_grad in neurecon_amd's training render): d_all_out
+   * [n_rays, P] receives each ray's sorted sample depths d_all (unisurf.py:201); sample_only != 0 stops
+   * after the sampling (root finding + interval / free-space samples; surface_points / mask_surface /
+   * depth_surface are still written when given) -- rgb / depth / acc may then be NULL */
+  float* d_all_out;
+  int sample_only;
 } NrUnisurfArgs;
 
 size_t nr_unisurf_workspace_bytes(const NrUnisurfArgs* a);
@@ -488,6 +494,20 @@ int nr_volsdf_composite_bwd(const float* sdf, const float* pts, const float* bet
                             const float* g_rgb, const float* g_depth, const float* g_acc, const float* g_tau,
                             const float* g_sdf, float* d_sdf, float* d_rad, float* d_beta, void* workspace,
                             size_t workspace_bytes, void* stream);
+
+/* UNISURF compositing with a graph (unisurf.py:219-236, get_opacity_from_surface :53-62): logits [R,P]
+ * (implicit_surface), radiance [R,P,3], d_all [R,P].  alpha = exp(-l) / (1 + exp(-l)), visibility weights
+ * w = alpha * cumprod(1 - alpha + 1e-10) (exclusive); outputs rgb [R,3], depth [R], acc [R], w [R,P],
+ * optional alpha [R,P].  The backward takes the output gradients (each may be NULL) and returns
+ * d logits [R,P] and d radiance [R,P,3]. */
+int nr_unisurf_composite_fwd(const float* logits, const float* rad, const float* d_all, int64_t R, int P,
+                             int white_bkgd, float* rgb, float* depth, float* acc, float* weights, float* alpha,
+                             void* stream);
+size_t nr_unisurf_composite_bwd_workspace_bytes(int64_t R, int P);
+int nr_unisurf_composite_bwd(const float* logits, const float* rad, const float* d_all, int64_t R, int P,
+                             int white_bkgd, const float* g_rgb, const float* g_depth, const float* g_acc,
+                             const float* g_weights, float* d_logits, float* d_rad, void* workspace,
+                             size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Opt-in kernel timing (diagnostics / bench roofline).  While enabled, every kernel launch of

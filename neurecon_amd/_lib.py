@@ -95,7 +95,7 @@ class NrUnisurfArgs(ctypes.Structure):
         ('workspace', _c_p), ('workspace_bytes', _c_sz),
         ('u_query', _c_p), ('u_free', _c_p),
         ('shard_ray0', _c_i64), ('shard_row_rays', _c_i64), ('window_ss', _c_p), ('window_reduce', _c_p),
-        ('window_user', _c_p), ('no_secant', _c_i),
+        ('window_user', _c_p), ('no_secant', _c_i), ('d_all_out', _c_p), ('sample_only', _c_i),
     ]
 
 
@@ -165,6 +165,10 @@ _SIGS = {
     'nr_neus_composite_bg_bwd_workspace_bytes': (_c_sz, [_c_i64, _c_i, _c_i]),
     'nr_neus_composite_bg_bwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_i, _c_p, _c_p,
                                         _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
+    'nr_unisurf_composite_fwd': (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    'nr_unisurf_composite_bwd_workspace_bytes': (_c_sz, [_c_i64, _c_i]),
+    'nr_unisurf_composite_bwd': (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                        _c_sz, _c_p]),
     'nr_volsdf_composite_fwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_f, _c_i, _c_p, _c_p, _c_p,
                                        _c_p, _c_p, _c_p, _c_p, _c_p]),
     'nr_volsdf_composite_bwd_workspace_bytes': (_c_sz, [_c_i64, _c_i]),

@@ -513,6 +513,12 @@ static int unisurf_chunk(const NrUnisurfArgs& a, const UniPlan& pl, int64_t ray0
            a.radiance_out, a.sdf_out, a.nablas_out, a.alpha_out, a.weights_out};
   hipLaunchKernelGGL(uni_samples, grd, blk, 0, st, c, o);
   NR_HIP_CHECK(hipGetLastError());
+  if (a.d_all_out) {  // training: the sorted sample depths, ray-major (unisurf.py:201)
+    hipLaunchKernelGGL(neus_write_dall, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, c.d_all, (int64_t)R, c.P,
+                       ray0, a.d_all_out);
+    NR_HIP_CHECK(hipGetLastError());
+  }
+  if (a.sample_only) return NR_OK;
   if ((rc = launch_sdf(SL, a.sdf_packed, c.pts_f, P, c.sdf_f, c.nab_f, c.feat_f, a.sdf->multires, mlp_ws, mlp_bytes,
                        st)))
     return rc;
@@ -542,11 +548,14 @@ static int check_unisurf(const NrUnisurfArgs* a) {
   int rc = check_sdf_desc(a->sdf);
   if (rc) return rc;
   if ((rc = check_rad_desc(a->rad))) return rc;
-  NR_REQUIRE(a->n_rays <= 0 || (a->rays_o && a->rays_d && a->rgb && a->depth && a->acc), NR_ERR_ARG,
-             "nr_unisurf_render: null ray or output pointer");
+  NR_REQUIRE(a->n_rays <= 0 || (a->rays_o && a->rays_d && (a->sample_only ? a->d_all_out != nullptr
+                                                                            : (a->rgb && a->depth && a->acc))),
+             NR_ERR_ARG, "nr_unisurf_render: null ray or output pointer");
+  NR_REQUIRE(!a->sample_only || a->shard_row_rays <= 0, NR_ERR_ARG,
+             "nr_unisurf_render: sample_only is not a sharded render");
   NR_REQUIRE(a->sdf_packed && a->rad_packed && a->t_march && a->t_query && a->t_free, NR_ERR_ARG,
              "nr_unisurf_render: null argument");
-  NR_REQUIRE(a->n_rays <= 0 || !a->calc_normal || a->normals, NR_ERR_ARG,
+  NR_REQUIRE(a->n_rays <= 0 || a->sample_only || !a->calc_normal || a->normals, NR_ERR_ARG,
              "nr_unisurf_render: calc_normal needs normals output");
   NR_REQUIRE(a->N_steps >= 2 && a->N_secant_steps >= 0 && a->N_query >= 1 && a->N_freespace >= 1, NR_ERR_ARG,
              "nr_unisurf_render: bad sample counts");

@@ -691,6 +691,99 @@ __global__ void neus_composite_bg_bwd_kernel(const float* __restrict__ sdf, cons
   d_s[r] = (float)sbar;
 }
 
+// ---- UNISURF compositing with a graph (unisurf.py:219-236, get_opacity_from_surface :53-62) ------------
+// One thread per ray, P samples.  alpha_i = odds / (1 + odds), odds = exp(-logit_i); T_i = prod_{j<i}
+// (1 - alpha_j + 1e-10) (the cumprod of the shifted transparency); w_i = alpha_i T_i; rgb = sum w c,
+// acc = sum w, depth = sum w / (acc + 1e-10) d.  Same arithmetic as the render kernel (uni_composite):
+// fp64 prefix product and sums, rounded per element.
+__device__ __forceinline__ float uni_alpha(float lg) {
+  const float odds = expf(-lg);
+  return fdiv(odds, fadd(1.0f, odds));
+}
+__global__ void unisurf_composite_fwd_kernel(const float* __restrict__ logits, const float* __restrict__ rad,
+                                             const float* __restrict__ d_all, int64_t R, int P, int white_bkgd,
+                                             float* __restrict__ rgb, float* __restrict__ depth,
+                                             float* __restrict__ acc, float* __restrict__ w_out,
+                                             float* __restrict__ alpha_out) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  double T = 1.0, a_acc = 0.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
+  for (int i = 0; i < P; ++i) {
+    const int64_t q = r * P + i;
+    const float al = uni_alpha(logits[q]);
+    const float w = fmul(al, (float)T);
+    T *= (double)fadd(fsub(1.0f, al), 1e-10f);
+    c0 += (double)fmul(w, rad[q * 3 + 0]);
+    c1 += (double)fmul(w, rad[q * 3 + 1]);
+    c2 += (double)fmul(w, rad[q * 3 + 2]);
+    a_acc += (double)w;
+    w_out[q] = w;
+    if (alpha_out) alpha_out[q] = al;
+  }
+  const float accf = (float)a_acc;
+  const float den = fadd(accf, 1e-10f);
+  double dep = 0.0;
+  for (int i = 0; i < P; ++i) dep += (double)fmul(fdiv(w_out[r * P + i], den), d_all[r * P + i]);
+  float o0 = (float)c0, o1 = (float)c1, o2 = (float)c2;
+  if (white_bkgd) {
+    const float bg = fsub(1.0f, accf);
+    o0 = fadd(o0, bg); o1 = fadd(o1, bg); o2 = fadd(o2, bg);
+  }
+  rgb[r * 3 + 0] = o0;
+  rgb[r * 3 + 1] = o1;
+  rgb[r * 3 + 2] = o2;
+  depth[r] = (float)dep;
+  acc[r] = accf;
+}
+
+// backward: G_i = dL/dw_i (rgb, acc, depth and direct weight gradients); w_i = alpha_i T_i with
+// T_i = T_k u_k prod_{k<j<i} u_j (u = 1 - alpha + 1e-10), so
+//   dL/dalpha_k = T_k (G_k - S_k),  S_k = sum_{i>k} G_i alpha_i prod_{k<j<i} u_j
+// (suffix recursion S_k = G_{k+1} alpha_{k+1} + u_{k+1} S_{k+1}: no division by u), and
+// dalpha/dlogit = -alpha (1 - alpha).
+__global__ void unisurf_composite_bwd_kernel(const float* __restrict__ logits, const float* __restrict__ rad,
+                                             const float* __restrict__ d_all, int64_t R, int P, int white_bkgd,
+                                             const float* __restrict__ g_rgb, const float* __restrict__ g_depth,
+                                             const float* __restrict__ g_acc, const float* __restrict__ g_w,
+                                             float* __restrict__ work, float* __restrict__ d_logits,
+                                             float* __restrict__ d_rad) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  float* al = work + r * (3 * (int64_t)P);  // alpha, T, w
+  float* Tt = al + P;
+  float* w = Tt + P;
+  double T = 1.0, a_acc = 0.0, wd = 0.0;
+  for (int i = 0; i < P; ++i) {
+    const int64_t q = r * P + i;
+    const float a = uni_alpha(logits[q]);
+    al[i] = a;
+    Tt[i] = (float)T;
+    w[i] = fmul(a, (float)T);
+    T *= (double)fadd(fsub(1.0f, a), 1e-10f);
+    a_acc += (double)w[i];
+    wd += (double)w[i] * (double)d_all[q];
+  }
+  const double A = (double)fadd((float)a_acc, 1e-10f);
+  const float gr0 = g_rgb ? g_rgb[r * 3 + 0] : 0.f, gr1 = g_rgb ? g_rgb[r * 3 + 1] : 0.f,
+              gr2 = g_rgb ? g_rgb[r * 3 + 2] : 0.f;
+  const double gd = g_depth ? (double)g_depth[r] : 0.0;
+  const double ga = (g_acc ? (double)g_acc[r] : 0.0) - (white_bkgd ? (double)gr0 + gr1 + gr2 : 0.0);
+  double S = 0.0;  // S_k for the current k (walking backwards)
+  for (int k = P - 1; k >= 0; --k) {
+    const int64_t q = r * P + k;
+    double G = (double)gr0 * rad[q * 3 + 0] + (double)gr1 * rad[q * 3 + 1] + (double)gr2 * rad[q * 3 + 2] + ga;
+    G += gd * ((double)d_all[q] / A - wd / (A * A));
+    if (g_w) G += (double)g_w[q];
+    const double abar = (double)Tt[k] * (G - S);
+    const double a = al[k];
+    d_logits[q] = (float)(-abar * a * (1.0 - a));
+    d_rad[q * 3 + 0] = fmul(w[k], gr0);
+    d_rad[q * 3 + 1] = fmul(w[k], gr1);
+    d_rad[q * 3 + 2] = fmul(w[k], gr2);
+    S = G * a + (double)fadd(fsub(1.0f, al[k]), 1e-10f) * S;  // S_{k-1}
+  }
+}
+
 }  // namespace
 }  // namespace nr
 
@@ -871,6 +964,38 @@ int nr_neus_composite_bg_bwd(const float* sdf, const float* s_dev, const float* 
   hipLaunchKernelGGL(neus_composite_bg_bwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
                      sdf, s_dev, rad, sigma_out, rad_out, d_out, inside, R, S, M, white_bkgd, g_rgb, g_depth, g_acc,
                      g_weights, (float*)workspace, d_sdf, d_rad, d_sigma_out, d_rad_out, d_s);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_unisurf_composite_fwd(const float* logits, const float* rad, const float* d_all, int64_t R, int P,
+                             int white_bkgd, float* rgb, float* depth, float* acc, float* weights, float* alpha,
+                             void* stream) {
+  NR_REQUIRE(logits && rad && d_all && rgb && depth && acc && weights && R >= 0 && P >= 1, NR_ERR_ARG,
+             "nr_unisurf_composite_fwd: bad argument");
+  if (R == 0) return NR_OK;
+  hipLaunchKernelGGL(unisurf_composite_fwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
+                     logits, rad, d_all, R, P, white_bkgd, rgb, depth, acc, weights, alpha);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+size_t nr_unisurf_composite_bwd_workspace_bytes(int64_t R, int P) {
+  return (size_t)(R > 0 ? R : 1) * 3 * (size_t)P * sizeof(float);
+}
+
+int nr_unisurf_composite_bwd(const float* logits, const float* rad, const float* d_all, int64_t R, int P,
+                             int white_bkgd, const float* g_rgb, const float* g_depth, const float* g_acc,
+                             const float* g_weights, float* d_logits, float* d_rad, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+  NR_REQUIRE(logits && rad && d_all && d_logits && d_rad && R >= 0 && P >= 1, NR_ERR_ARG,
+             "nr_unisurf_composite_bwd: bad argument");
+  if (R == 0) return NR_OK;
+  NR_REQUIRE(workspace && workspace_bytes >= nr_unisurf_composite_bwd_workspace_bytes(R, P), NR_ERR_WORKSPACE,
+             "nr_unisurf_composite_bwd: workspace too small");
+  hipLaunchKernelGGL(unisurf_composite_bwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
+                     logits, rad, d_all, R, P, white_bkgd, g_rgb, g_depth, g_acc, g_weights, (float*)workspace,
+                     d_logits, d_rad);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

@@ -17,7 +17,7 @@ import torch.nn.functional as F
 
 from .. import _lib as L
 from .. import rend_util
-from ..base import ImplicitSurface, RadianceNet, _no_training, check_view_dirs
+from ..base import ImplicitSurface, RadianceNet, check_view_dirs, wants_graph
 from .neus import _linspace_table
 
 N_STEPS = 256        # ray_casting.py:49 (root_finding_surface_points default)
@@ -90,14 +90,23 @@ def volume_render(rays_o, rays_d, model, batched=False, batched_info={}, calc_no
                   use_view_dirs=True, method='secant', rayschunk=65536, netchunk=1048576, white_bkgd=False,
                   near_bypass=None, far_bypass=None, detailed_output=True, show_progress=False,
                   radius_of_interest=4.0, perturb=False, interval=1.0, too_close_threshold=0.1, N_query=64,
-                  N_freespace=32, shard=None, **dummy_kwargs):
+                  N_freespace=32, shard=None, _sample_only=False, **dummy_kwargs):
     """unisurf.py:62-283, render mode.  rays_o/rays_d: [(B,) N_rays, 3].
     shard = (ray0, row_rays, group): these rays are ranks' slice [ray0, ray0 + N) of batch rows of
     row_rays rays (neurecon_amd.dist.render_sharded); the windowed F.normalize then sums its nabla^2
     windows over all ranks (one all-reduce of B x windows x 3 doubles), so the result equals the
     single-process render of the whole batch."""
     L.require_gpu(rays_o, 'rays_o')
-    _no_training(model)
+    if wants_graph(model) and not _sample_only:
+        if shard is not None:
+            raise NotImplementedError('neurecon_amd: a UNISURF training render runs on the whole batch per rank '
+                                      '(DDP); shard= is for render-mode frame sharding')
+        return _train_render(rays_o, rays_d, model, batched=batched, calc_normal=calc_normal, logit_tau=logit_tau,
+                             use_view_dirs=use_view_dirs, method=method, rayschunk=rayschunk, netchunk=netchunk,
+                             white_bkgd=white_bkgd, near_bypass=near_bypass, far_bypass=far_bypass,
+                             detailed_output=detailed_output, radius_of_interest=radius_of_interest, perturb=perturb,
+                             interval=interval, too_close_threshold=too_close_threshold, N_query=N_query,
+                             N_freespace=N_freespace)
     check_view_dirs(model, use_view_dirs)
     dev = rays_o.device
     if batched:
@@ -118,12 +127,16 @@ def volume_render(rays_o, rays_d, model, batched=False, batched_info={}, calc_no
     t_query = _linspace_table(N_query + (1 if perturb else 0), dev)
     t_free = _linspace_table(N_freespace + (1 if perturb else 0), dev)
 
-    rgb = torch.empty(n, 3, device=dev)
-    depth = torch.empty(n, device=dev)
-    acc = torch.empty(n, device=dev)
-    normals = torch.empty(n, 3, device=dev) if calc_normal else None
+    rgb = torch.empty(n, 3, device=dev) if not _sample_only else None
+    depth = torch.empty(n, device=dev) if not _sample_only else None
+    acc = torch.empty(n, device=dev) if not _sample_only else None
+    normals = torch.empty(n, 3, device=dev) if calc_normal and not _sample_only else None
     det = {}
-    if detailed_output:
+    if _sample_only:  # training's no-grad pass: sample depths + surface points only
+        det = dict(surface_points=torch.empty(n, 3, device=dev),
+                   mask_surface=torch.empty(n, dtype=torch.bool, device=dev), depth_surface=torch.empty(n, device=dev),
+                   d_all=torch.empty(n, P, device=dev))
+    elif detailed_output:
         det = dict(surface_points=torch.empty(n, 3, device=dev), mask_surface=torch.empty(n, dtype=torch.bool,
                                                                                            device=dev),
                    depth_surface=torch.empty(n, device=dev), radiance=torch.empty(n, P, 3, device=dev),
@@ -154,6 +167,8 @@ def volume_render(rays_o, rays_d, model, batched=False, batched_info={}, calc_no
     a.nablas_out = L.ptr(det.get('implicit_nablas'))
     a.alpha_out = L.ptr(det.get('alpha'))
     a.weights_out = L.ptr(det.get('visibility_weights'))
+    if _sample_only:
+        a.d_all_out, a.sample_only = L.ptr(det['d_all']), 1
     if perturb:
         B = rays_d.shape[0] if batched else 1
         u_q, u_f = _unisurf_uniforms(B, n // B, batched, int(rayschunk), N_query, N_freespace, dev)
@@ -175,6 +190,8 @@ def volume_render(rays_o, rays_d, model, batched=False, batched_info={}, calc_no
     a.workspace, a.workspace_bytes = L.ptr(ws), ws_bytes
     L.check(lib.nr_unisurf_render(ctypes.byref(a), L.stream_of(dev)))
     del keep
+    if _sample_only:
+        return det
 
     ret = OrderedDict([('rgb', rgb.reshape(*prefix, 3)), ('depth_volume', depth.reshape(prefix)),
                        ('mask_volume', acc.reshape(prefix))])
@@ -192,6 +209,85 @@ def volume_render(rays_o, rays_d, model, batched=False, batched_info={}, calc_no
     return ret['rgb'], ret['depth_volume'], ret
 
 
+def _window_normalize(nab, batched, B, rayschunk, netchunk):
+    """UNISURF.forward's F.normalize(nablas) (default dim=1, unisurf.py:36) over the batchify_query
+    windows it sees (train_util.py:23-71): nab [n, P, 3] ray-major.  Unbatched, the query input is
+    [netchunk, 3] and dim 1 is xyz (per point); batched, it is [B, netchunk, 3] and each xyz column is
+    normalised over the window's points, per batch row and per ray chunk of the render loop."""
+    if not batched:
+        return F.normalize(nab, dim=-1)
+    P = nab.shape[1]
+    x = nab.reshape(B, -1, P, 3)
+    outs = []
+    for r0 in range(0, x.shape[1], rayschunk):
+        seg = x[:, r0:r0 + rayschunk].reshape(B, -1, 3)
+        parts = [F.normalize(seg[:, i:i + netchunk], dim=1) for i in range(0, seg.shape[1], netchunk)]
+        outs.append(torch.cat(parts, 1).reshape(B, -1, P, 3))
+    return torch.cat(outs, 1).reshape(-1, P, 3)
+
+
+def _train_render(rays_o, rays_d, model, batched, calc_normal, logit_tau, use_view_dirs, method, rayschunk, netchunk,
+                  white_bkgd, near_bypass, far_bypass, detailed_output, radius_of_interest, perturb, interval,
+                  too_close_threshold, N_query, N_freespace):
+    """unisurf.py:62-283 with an autograd graph (training): the root finding and the interval /
+    free-space samples come from the no-grad path (the reference's root finding runs under
+    torch.no_grad, ray_casting.py:47; the depths carry no gradient), then occupancy + nablas + geometry
+    feature at every sample (double-backward capable), the windowed F.normalize, the radiance net and
+    the integration as neurecon_amd.training autograd functions.  Returns (rgb, depth, extras)."""
+    from .. import training as T
+    check_view_dirs(model, use_view_dirs)
+    dev = rays_o.device
+    B = rays_d.shape[0] if batched else 1
+    prefix = [B, -1] if batched else [-1]
+    P = N_query + N_freespace
+    with torch.no_grad():
+        ex = volume_render(rays_o, rays_d, model, batched=batched, logit_tau=logit_tau, use_view_dirs=use_view_dirs,
+                           method=method, rayschunk=rayschunk, netchunk=netchunk, near_bypass=near_bypass,
+                           far_bypass=far_bypass, radius_of_interest=radius_of_interest, perturb=perturb,
+                           interval=interval, too_close_threshold=too_close_threshold, N_query=N_query,
+                           N_freespace=N_freespace, _sample_only=True)
+    ro = rays_o.reshape(-1, 3).float().contiguous()
+    rd_raw = rays_d.reshape(-1, 3).float().contiguous()
+    n = ro.shape[0]
+    d_all = ex['d_all']
+    rd = torch.empty_like(rd_raw)  # F.normalize(rays_d, dim=-1) (unisurf.py:118)
+    L.check(L.lib().nr_normalize3(L.ptr(rd_raw), n, L.ptr(rd), L.stream_of(dev)))
+    pts = torch.empty(n, P, 3, device=dev)
+    mids = torch.empty(n, P - 1, 3, device=dev)
+    dmid = torch.empty(n, P - 1, device=dev)
+    L.check(L.lib().nr_neus_points(L.ptr(ro), L.ptr(rd), L.ptr(d_all), n, P, L.ptr(pts), L.ptr(mids), L.ptr(dmid),
+                                   L.stream_of(dev)))
+    logits, nablas, feat = T.sdf_nablas(model.implicit_surface, pts.reshape(-1, 3), True)   # unisurf.py:35
+    nrm = _window_normalize(nablas.reshape(n, P, 3), batched, B, int(rayschunk), int(netchunk))
+    view = rd[:, None, :].expand(n, P, 3).reshape(-1, 3).contiguous()
+    rad = T.radiance(model.radiance_net, pts.reshape(-1, 3), view, nrm.reshape(-1, 3), feat)  # unisurf.py:37
+    rgb, depth, acc, w, alpha = T.UnisurfComposite.apply(logits.reshape(n, P), rad.reshape(n, P, 3), d_all,
+                                                         bool(white_bkgd))
+    nablas = nablas.reshape(n, P, 3)
+    ret = OrderedDict([('rgb', rgb.reshape(*prefix, 3)), ('depth_volume', depth.reshape(prefix)),
+                       ('mask_volume', acc.reshape(prefix))])
+    if calc_normal:  # unisurf.py:249-253
+        nn_ = F.normalize(nablas, dim=-1)
+        ret['normals_volume'] = (nn_ * w[..., None]).sum(dim=-2).reshape(*prefix, 3)
+    if detailed_output:
+        ret['surface_points'] = ex['surface_points'].reshape(*prefix, 3)
+        ret['mask_surface'] = ex['mask_surface'].reshape(prefix)
+        ret['depth_surface'] = ex['depth_surface'].reshape(prefix)
+        ret['radiance'] = rad.reshape(*prefix, P, 3)
+        ret['implicit_surface'] = logits.reshape(*prefix, P)
+        ret['implicit_nablas'] = nablas.reshape(*prefix, P, 3)
+        ret['alpha'] = alpha.reshape(*prefix, P)
+        ret['visibility_weights'] = w.reshape(*prefix, P)
+        ret['d_all'] = d_all.reshape(*prefix, P)
+    return ret['rgb'], ret['depth_volume'], ret
+
+
+def surface_perturbation(like, scale):
+    """unisurf.py:335-336: (torch.rand(shape) - 0.5) * 2 * perturb_surface_pts (a module function so
+    tests can replay the reference's draws)."""
+    return (torch.rand(like.shape, device=like.device) - 0.5) * 2. * scale
+
+
 class SingleRenderer(nn.Module):
     """unisurf.py:286-291."""
 
@@ -207,8 +303,11 @@ volume_render.window_sharded = True  # render_sharded passes `shard=` (cross-ran
 
 
 class Trainer(nn.Module):
-    """unisurf.py:294-351.  Training needs the backward of the render kernels; the
-    render call raises while grad is enabled."""
+    """unisurf.py:294-351: one training step's forward -- random rays of the image, the render with a
+    graph (neurecon_amd.training autograd functions on libnrhip.so), L1 rgb loss and the normal
+    smoothness term on the root-finding surface points.  Returns OrderedDict(losses=..., extras=...)
+    like the reference; train.py calls backward() on losses['total'] (under DDP the gradient
+    all-reduce runs over RCCL)."""
 
     def __init__(self, model, device_ids=[0], batched=True):
         super().__init__()
@@ -219,12 +318,32 @@ class Trainer(nn.Module):
         self.device = device_ids[0]
 
     def forward(self, args, indices, model_input, ground_truth, render_kwargs_train, it, device='cuda'):
+        from ..config import as_cfg
+        args = as_cfg(args)
         intrinsics = model_input['intrinsics'].to(device)
         c2w = model_input['c2w'].to(device)
         rays_o, rays_d, select_inds = rend_util.get_rays(c2w, intrinsics, render_kwargs_train['H'],
                                                          render_kwargs_train['W'], N_rays=args.data.N_rays)
+        target_rgb = rend_util.gather_rays(ground_truth['rgb'].to(device), select_inds)       # unisurf.py:319
         interval = max(args.training.delta_max * np.exp(-it * args.training.delta_beta), args.training.delta_min)
-        return self.renderer(rays_o, rays_d, interval=interval, detailed_output=True, **render_kwargs_train)
+        rgb, depth_v, extras = self.renderer(rays_o, rays_d, interval=interval, detailed_output=True,
+                                             **render_kwargs_train)
+        losses = OrderedDict()
+        losses['loss_img'] = F.l1_loss(rgb, target_rgb)
+        losses['loss_reg'] = torch.tensor(0.).to(device)
+        if args.training.w_reg > 0:                                                           # unisurf.py:331-341
+            pts_surface = extras['surface_points']
+            _, nablas_surface, _ = self.model.implicit_surface.forward_with_nablas(pts_surface)
+            pts_neighbor = pts_surface + surface_perturbation(pts_surface, args.training.perturb_surface_pts)
+            _, nablas_perturb, _ = self.model.implicit_surface.forward_with_nablas(pts_neighbor)
+            losses['loss_reg'] = args.training.w_reg * F.mse_loss(F.normalize(nablas_perturb, dim=-1),
+                                                                  F.normalize(nablas_surface, dim=-1))
+        loss = 0
+        for v in losses.values():
+            loss += v
+        losses['total'] = loss
+        extras['scalars'] = {'interval': torch.tensor([interval]).to(device)}
+        return OrderedDict([('losses', losses), ('extras', extras)])
 
 
 def get_model(args):

@@ -410,6 +410,44 @@ class VolSDFComposite(torch.autograd.Function):
         return d_sdf, d_beta.sum().reshape(1), d_rad, None, None, None, None, None
 
 
+class UnisurfComposite(torch.autograd.Function):
+    """UNISURF's occupancy -> alpha and ray integration (unisurf.py:219-236, :53-62) with a graph:
+    logits [R,P] (implicit_surface), radiance [R,P,3]; d_all [R,P] (no grad) -> rgb [R,3], depth [R],
+    acc [R], visibility weights [R,P] (+ alpha [R,P], not differentiable)."""
+
+    @staticmethod
+    def forward(ctx, logits, rad, d_all, white_bkgd):
+        R, P = logits.shape
+        dev = logits.device
+        logits, rad, d_all = logits.contiguous(), rad.contiguous(), d_all.contiguous()
+        rgb = torch.empty(R, 3, device=dev)
+        depth = torch.empty(R, device=dev)
+        acc = torch.empty(R, device=dev)
+        w = torch.empty(R, P, device=dev)
+        alpha = torch.empty(R, P, device=dev)
+        L.check(L.lib().nr_unisurf_composite_fwd(L.ptr(logits), L.ptr(rad), L.ptr(d_all), R, P, int(white_bkgd),
+                                                 L.ptr(rgb), L.ptr(depth), L.ptr(acc), L.ptr(w), L.ptr(alpha),
+                                                 _st(logits)))
+        ctx.white = int(white_bkgd)
+        ctx.save_for_backward(logits, rad, d_all)
+        ctx.mark_non_differentiable(alpha)
+        return rgb, depth, acc, w, alpha
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_depth, g_acc, g_w, _ga):
+        logits, rad, d_all = ctx.saved_tensors
+        R, P = logits.shape
+        c = lambda t: None if t is None else t.contiguous()
+        d_lg, d_rad = torch.empty_like(logits), torch.empty_like(rad)
+        lib = L.lib()
+        wb = lib.nr_unisurf_composite_bwd_workspace_bytes(R, P)
+        ws = torch.empty(max(wb, 1), dtype=torch.uint8, device=logits.device)
+        L.check(lib.nr_unisurf_composite_bwd(L.ptr(logits), L.ptr(rad), L.ptr(d_all), R, P, ctx.white,
+                                             L.ptr(c(g_rgb)), L.ptr(c(g_depth)), L.ptr(c(g_acc)), L.ptr(c(g_w)),
+                                             L.ptr(d_lg), L.ptr(d_rad), L.ptr(ws), wb, _st(logits)))
+        return d_lg, d_rad, None, None
+
+
 def nerf(net, x_emb, v_emb):
     """Differentiable (sigma [P], rgb [P,3]) of a neurecon_amd NeRF background net."""
     Ws = [l.weight for l in net.pts_linears]

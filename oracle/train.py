@@ -113,3 +113,48 @@ def volsdf_train_losses(sd, rays_o, rays_d, target_rgb, eik_points, w_eikonal=0.
                                                      reduction='mean')}
     losses['total'] = losses['loss_img'] + losses['loss_eikonal']
     return losses, d_all
+
+
+def unisurf_train_losses(sd, rays_o, rays_d, target_rgb, surf_perturb, w_reg=0.01, d_all=None, surface_points=None,
+                         logit_tau=0.0, radius_of_interest=4.0, interval=1.0, N_query=64, N_freespace=32,
+                         netchunk=1048576):
+    """losses of one UNISURF training step (models/frameworks/unisurf.py:303-351; render :140-236 with a
+    graph): L1 rgb + w_reg * MSE(normalize(nablas at surface points + surf_perturb), normalize(nablas at
+    surface points)).  surf_perturb [B, N, 3] = the reference's (torch.rand - 0.5) * 2 * perturb_surface_pts
+    draw.  d_all [B, N, P] / surface_points [B, N, 3] optional (from the oracle's no-grad root finding and
+    sampling when None).  perturb=False, batched rays [B, N, 3] (F.normalize windows of netchunk points)."""
+    from .unisurf import UNISURFOracle
+    o = rays_o.reshape(rays_o.shape[0], -1, 3).float()
+    d = F.normalize(rays_d.reshape(rays_d.shape[0], -1, 3).float(), dim=-1)
+    B, N = o.shape[:2]
+    if d_all is None or surface_points is None:
+        orc = UNISURFOracle({k: v.detach() for k, v in sd.items()})
+        with torch.no_grad():
+            out = orc.render(rays_o, rays_d, logit_tau=logit_tau, radius_of_interest=radius_of_interest,
+                             interval=interval, N_query=N_query, N_freespace=N_freespace, calc_normal=False)
+        d_all = out['d_all'] if d_all is None else d_all
+        surface_points = out['surface_points'] if surface_points is None else surface_points
+    sdf_net = SDFNet(sd)
+    rad_net = RadianceNet(sd, multires=-1, multires_view=-1)
+    pts = o[..., None, :] + d[..., None, :] * d_all[..., :, None]              # unisurf.py:207
+    P = d_all.shape[-1]
+    xf = pts.flatten(1, 2)                                                      # train_util.py:23-71
+    vf = d.unsqueeze(-2).expand_as(pts).flatten(1, 2)
+    rad, logits = [], []
+    for i in range(0, xf.shape[1], netchunk):                                   # unisurf.py:34-38
+        occ, nab, h = nablas_graph(sdf_net, xf[:, i:i + netchunk])
+        rad.append(rad_net.forward(xf[:, i:i + netchunk], vf[:, i:i + netchunk], F.normalize(nab), h))
+        logits.append(occ)
+    rad = torch.cat(rad, 1).reshape(B, N, P, 3)
+    logits = torch.cat(logits, 1).reshape(B, N, P)
+    odds = torch.exp(-1. * logits)                                              # unisurf.py:219-231
+    alpha = odds / (1 + odds)
+    Tr = torch.cumprod(torch.cat([torch.ones_like(alpha[..., :1]), 1.0 - alpha + 1e-10], -1), -1)
+    w = alpha * Tr[..., :-1]
+    rgb = torch.sum(w[..., None] * rad, -2)
+    losses = {'loss_img': F.l1_loss(rgb, target_rgb)}
+    _, nab_s, _ = nablas_graph(sdf_net, surface_points)                         # unisurf.py:331-341
+    _, nab_p, _ = nablas_graph(sdf_net, surface_points + surf_perturb)
+    losses['loss_reg'] = w_reg * F.mse_loss(F.normalize(nab_p, dim=-1), F.normalize(nab_s, dim=-1))
+    losses['total'] = losses['loss_img'] + losses['loss_reg']
+    return losses, d_all, surface_points

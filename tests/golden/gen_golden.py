@@ -667,6 +667,47 @@ def gen_train_volsdf(R):
          **_grad_summary(model.named_parameters()))
 
 
+def gen_train_unisurf(R):
+    """One UNISURF training step (models/frameworks/unisurf.py:303-351 -> train.py:205 backward) on an
+    8x8 camera (64 rays, N_rays=-1), it=0 (interval = delta_max = 1), perturb=False, w_reg=0.01 with
+    perturb_surface_pts=0.01, seeded random targets; the surface-point perturbation (torch.rand,
+    unisurf.py:335) is recorded from the reference's own call so the GPU test can replay it."""
+    import types as _t
+    sd = wg.unisurf_state(seed=3)
+    m = R.unisurf.UNISURF(W_geo_feat=256, surface_cfg=dict(radius_init=1.0, **SURF),
+                          radiance_cfg=dict(use_siren=False, embed_multires=-1, embed_multires_view=-1,
+                                            use_view_dirs=True, D=4, W=256, skips=[]))
+    m.load_state_dict(sd)
+    m.train()
+    H = W = 8
+    c2w = wg.look_at_c2w(2.7)[None]
+    c2w[0, 0, 3] += 0.0137
+    K = wg.intrinsics(20.0, H, W)[None]
+    g = torch.Generator().manual_seed(8)
+    target_rgb = torch.rand(1, H * W, 3, generator=g)
+    args = _t.SimpleNamespace(data=_t.SimpleNamespace(N_rays=-1),
+                              training=_t.SimpleNamespace(w_reg=0.01, perturb_surface_pts=0.01, delta_max=1.0,
+                                                          delta_min=0.05, delta_beta=1.5e-5))
+    logit_tau = float(R.unisurf.UNISURF.get_surface_from_opacity(0.5))
+    kw = dict(H=H, W=W, batched=True, perturb=False, white_bkgd=False, logit_tau=logit_tau, radius_of_interest=4.0,
+              N_query=64, N_freespace=32)
+    trainer = R.unisurf.Trainer(m, device_ids=[0], batched=True)
+    torch.manual_seed(11)
+    with _RecordRand() as rr:
+        ret = trainer.forward(args, None, {'intrinsics': K, 'c2w': c2w}, {'rgb': target_rgb}, kw, 0, device='cpu')
+    assert len(rr.draws) == 1, len(rr.draws)
+    losses = {k: torch.mean(v) for k, v in ret['losses'].items()}
+    m.zero_grad()
+    losses['total'].backward()
+    ex = ret['extras']
+    surf_perturb = (rr.draws[0] - 0.5) * 2. * 0.01
+    save('unisurf_train.npz', seed=3, H=H, W=W, f=20.0, dist=2.7, target_rgb=target_rgb, c2w=c2w, K=K,
+         logit_tau=logit_tau, rand_draw=rr.draws[0], surf_perturb=surf_perturb,
+         **{f'loss/{k}': v.detach() for k, v in losses.items()}, rgb=ex['rgb'].detach(),
+         surface_points=ex['surface_points'].detach(), mask_surface=ex['mask_surface'].detach(),
+         depth_surface=ex['depth_surface'].detach(), **_grad_summary(m.named_parameters()))
+
+
 def main():
     torch.set_num_threads(8)
     R = _import_reference()
@@ -674,7 +715,8 @@ def main():
     gens = dict(components=gen_components, sampling=gen_sampling, neus=gen_neus, volsdf=gen_volsdf,
                 unisurf=gen_unisurf, surface=gen_surface,
                 volsdf_nerfpp=gen_volsdf_nerfpp, perturb=gen_perturb, train=gen_train, options=gen_options,
-                volsdf_perturb=gen_volsdf_perturb, siren=gen_siren, train_volsdf=gen_train_volsdf)
+                volsdf_perturb=gen_volsdf_perturb, siren=gen_siren, train_volsdf=gen_train_volsdf,
+                train_unisurf=gen_train_unisurf)
     for name, fn in gens.items():
         if not only or name in only:
             fn(R)

@@ -17,8 +17,8 @@ import pytest
 import torch
 
 import weightgen as wg
-from helpers import neus_model, report, volsdf_model
-from test_oracle_golden import check_grads, train_grads_oracle, volsdf_train_grads_oracle
+from helpers import neus_model, report, unisurf_model, volsdf_model
+from test_oracle_golden import check_grads, train_grads_oracle, unisurf_train_grads_oracle, volsdf_train_grads_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -150,6 +150,48 @@ def test_volsdf_train_step_vs_oracle_and_golden(golden, precision, monkeypatch):
     print(f'{precision}: worst gradient error / network scale {worst:.3e}')
     same = torch.allclose(d_all, torch.from_numpy(g['d_vals']), rtol=1e-6, atol=1e-6)
     print(f'{precision}: sample depths {"match" if same else "differ from"} the reference (1e-6)')
+    if same:
+        check_grads(grads, g, RTOL, 2e-4, net_scale=True)
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
+def test_unisurf_train_step_vs_oracle_and_golden(golden, precision, monkeypatch):
+    """UNISURF's training step (unisurf.py:303-351): losses and every parameter gradient -- surface net
+    through the double backward of the nablas (windowed F.normalize into the radiance net, and the
+    normal smoothness term on the root-finding surface points), radiance net -- vs the oracle on the
+    GPU's sample depths and surface points, and vs the reference's golden when those agree.  The
+    surface-point perturbation replays the reference's draw (unisurf.py:335)."""
+    from neurecon_amd.frameworks import unisurf as U
+    g = golden('unisurf_train')
+    T = lambda a: torch.from_numpy(np.asarray(a)).cuda()
+    sp_pert = T(g['surf_perturb'])
+    monkeypatch.setattr(U, 'surface_perturbation', lambda like, scale: sp_pert.reshape(like.shape).to(like.dtype))
+    m = unisurf_model(wg.unisurf_state(seed=int(g['seed'])), precision=precision)
+    m.train()
+    args = types.SimpleNamespace(data=types.SimpleNamespace(N_rays=-1),
+                                 training=types.SimpleNamespace(w_reg=0.01, perturb_surface_pts=0.01, delta_max=1.0,
+                                                                delta_min=0.05, delta_beta=1.5e-5))
+    kw = dict(H=int(g['H']), W=int(g['W']), batched=True, perturb=False, white_bkgd=False,
+              logit_tau=float(g['logit_tau']), radius_of_interest=4.0, N_query=64, N_freespace=32)
+    ret = U.Trainer(m, device_ids=[0]).forward(args, None, {'intrinsics': T(g['K']), 'c2w': T(g['c2w'])},
+                                               {'rgb': T(g['target_rgb'])}, kw, 0, device='cuda')
+    losses = {k: torch.mean(v) for k, v in ret['losses'].items()}
+    m.zero_grad()
+    losses['total'].backward()
+    torch.cuda.synchronize()
+    grads = {k: p.grad.detach().cpu() for k, p in m.named_parameters() if p.grad is not None}
+    d_all = ret['extras']['d_all'].detach().cpu()
+    sp = ret['extras']['surface_points'].detach().cpu()
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    ref_losses, ref_grads, _, _ = unisurf_train_grads_oracle(g, d_all=d_all, surface_points=sp)
+    for k in ('loss_img', 'loss_reg', 'total'):
+        a, b = float(losses[k]), float(ref_losses[k])
+        print(f'{precision} {k}: gpu {a:.8f} oracle {b:.8f} golden {float(g["loss/" + k]):.8f}')
+        assert abs(a - b) <= 1e-5 * abs(b) + 1e-9
+    worst = check_grads(grads, _as_golden(ref_grads, g), RTOL, 2e-4, net_scale=True)
+    print(f'{precision}: worst gradient error / network scale {worst:.3e}')
+    same = torch.allclose(sp, torch.from_numpy(g['surface_points']), rtol=1e-6, atol=1e-6)
+    print(f'{precision}: surface points {"match" if same else "differ from"} the reference (1e-6)')
     if same:
         check_grads(grads, g, RTOL, 2e-4, net_scale=True)
 

@@ -375,3 +375,31 @@ def test_oracle_volsdf_train_step_vs_golden(golden):
     for k in ('loss_img', 'loss_eikonal', 'total'):
         close(losses[k], g[f'loss/{k}'], 1e-5, 1e-7)
     check_grads(grads, g, 1e-4, 1e-6)
+
+
+def unisurf_train_grads_oracle(g, d_all=None, surface_points=None):
+    """oracle/train.py on the unisurf_train fixture: (losses, {param: grad}, d_all, surface_points)"""
+    from oracle.train import unisurf_train_losses
+    sd = {k: v.clone().requires_grad_(v.is_floating_point() and k != 'implicit_surface.obj_bounding_size')
+          for k, v in wg.unisurf_state(seed=int(g['seed'])).items()}
+    H, W = int(g['H']), int(g['W'])
+    ro, rd, _ = rays.get_rays(T(g['c2w']), T(g['K']), H, W)
+    losses, d_all, sp = unisurf_train_losses(sd, ro, rd, T(g['target_rgb']), T(g['surf_perturb']),
+                                             logit_tau=float(g['logit_tau']), d_all=d_all,
+                                             surface_points=surface_points)
+    losses['total'].backward()
+    return losses, {k: v.grad for k, v in sd.items() if v.grad is not None}, d_all, sp
+
+
+def test_oracle_unisurf_train_step_vs_golden(golden):
+    """the oracle's UNISURF training losses and every parameter gradient (surface net through the
+    double backward of the nablas: windowed F.normalize into the radiance net and the normal
+    smoothness term; radiance net) vs the reference's own Trainer.forward + backward on the same rays,
+    targets and surface-point perturbation"""
+    g = golden('unisurf_train')
+    torch.set_num_threads(8)
+    losses, grads, d_all, sp = unisurf_train_grads_oracle(g)
+    close(sp, g['surface_points'], 1e-6, 1e-6)
+    for k in ('loss_img', 'loss_reg', 'total'):
+        close(losses[k], g[f'loss/{k}'], 1e-5, 1e-9)
+    check_grads(grads, g, 1e-4, 1e-6)
