@@ -98,6 +98,8 @@ RadLayout rad_layout(const NrRadDesc& d) {
   }
   L.scale_off = (uint32_t)off;
   off = align256(off + 5 * 4);
+  L.bound_off = (uint32_t)off;
+  off = align256(off + 5 * 2 * 4);
   L.head_off = (uint32_t)off;
   off = align256(off + (3 * 256 + 4) * 4);
   L.total = (uint32_t)off;
@@ -732,7 +734,9 @@ int nr_radiance_pack(const NrRadDesc* d, const float* const* W, const float* con
   ops[0] = mkop(W[0], b[0], 256, ld0, 0, seg(16, 0, 256), none(), seg(16, ns, 256), seg(L.kbs, 0, ns), 1.0f, prec, wmax);
   for (int i = 1; i < L.D; ++i)
     ops[i] = mkop(W[i], b[i], 256, 256, 0, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + i);
+  float* bound = (float*)(P + L.bound_off);
   for (int i = 0; i < L.D; ++i) {
+    ops[i].bound = bound + 2 * i;
     if ((rc = launch_pack_op(ops[i], P + L.op_off[i], st))) return rc;
   }
   if ((rc = launch_pack_vec(W[L.D], 0, 768, 768, P + L.head_off, st))) return rc;

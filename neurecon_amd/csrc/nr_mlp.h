@@ -49,6 +49,7 @@ struct RadLayout {
   uint32_t op_bytes[5];
   uint32_t head_off;  // [3][256] weights, then [3] bias
   uint32_t scale_off; // [4] max |W| per op
+  uint32_t bound_off; // [5][2] max row L1 norm, max |bias| per op (rad4_kernel's operand scales)
   uint32_t total;
   int prec;
   int kbs;            // small-input blocks (even)

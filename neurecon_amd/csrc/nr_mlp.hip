@@ -2029,6 +2029,194 @@ __global__ __launch_bounds__(kThreads) void radiance_kernel(RadKArgs a) {
 }
 
 // =============================================================================================
+// Radiance net on the v3 pipeline (rad4_kernel, f16x3, ReLU, D = 4): the sdf4_kernel structure
+// (128-point tile, kNC-column waves, weight ring by LDS-DMA two chunks ahead, per-chunk operand
+// split at a scale fixed from the op's pack-time bound, epilogue staged beside the next chunk's
+// MFMAs) on cat([feature, x, embed_view(v), normals]) -> 3 x ReLU(256) -> ReLU(256) -> 3, with the
+// Linear(256 -> 3) + sigmoid head folded into the last hidden op's epilogue as three running dot
+// products (the lane's 8 outputs of each chunk; summed in the old kernel's order: block by block,
+// then over the 4 lane groups).
+// =============================================================================================
+// ReLU op: out -> next operand (k-step c of oh/ol)
+struct ReluEpi4 {
+  f16x8 (&oh)[kNC][12];
+  f16x8 (&ol)[kNC][12];
+  const float (&sc)[kNC];
+  float (&mrun)[kNC];
+  float4 y[kNC][2];
+  __device__ __forceinline__ void operator()(int c, const Z4& zz, int st) {
+    const int q = st >> 2, k = st & 3;  // stages 4q..4q+3: column q
+    if (q >= kNC) return;
+    if (k < 2) {
+      const float4 z = zz.z[q][k];
+      y[q][k] = make_float4(fmaxf(z.x, 0.0f), fmaxf(z.y, 0.0f), fmaxf(z.z, 0.0f), fmaxf(z.w, 0.0f));
+    } else if (k == 2) {
+      mrun[q] = amax8(mrun[q], y[q][0], y[q][1]);
+    } else {
+      split8a(y[q][0], y[q][1], sc[q], oh[q][c], ol[q][c]);
+    }
+  }
+};
+
+// last hidden op: ReLU, then part[q][o] += sum_r y * head[o][row] over the lane's rows of the chunk
+// (head [3][256] staged in LDS)
+struct HeadEpi4 {
+  const float* head;  // LDS
+  float (&part)[kNC][3];
+  int g;
+  float4 y[kNC][2];
+  __device__ __forceinline__ void operator()(int c, const Z4& zz, int st) {
+    const int q = st >> 2, k = st & 3;
+    if (q >= kNC) return;
+    if (k < 2) {
+      const float4 z = zz.z[q][k];
+      y[q][k] = make_float4(fmaxf(z.x, 0.0f), fmaxf(z.y, 0.0f), fmaxf(z.z, 0.0f), fmaxf(z.w, 0.0f));
+    } else {  // rows 0 (stage 2), 1 and 2 (stage 3)
+#pragma unroll
+      for (int o = 0; o < 3; ++o) {
+        if ((o == 0) != (k == 2)) continue;
+        float p = part[q][o];
+        // opaque lane offset: a hoisted address per (chunk, row, block) would pin 48 registers
+        const uint32_t lo = opaque_lane(4 * g);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {  // block 2c + b, rows 16 (2c + b) + 4 g + r
+          const float4 w = *(const float4*)(head + lo + o * 256 + 16 * (2 * c + b));
+          p = fmaf(y[q][b].x, w.x, p);
+          p = fmaf(y[q][b].y, w.y, p);
+          p = fmaf(y[q][b].z, w.z, p);
+          p = fmaf(y[q][b].w, w.w, p);
+        }
+        asm volatile("" : "+v"(p));  // computed here: sunk to the op's end, every chunk's y would stay live
+        part[q][o] = p;
+      }
+    }
+  }
+};
+
+template <int KBS>
+__global__ __attribute__((amdgpu_flat_work_group_size(kT4, kT4), amdgpu_waves_per_eu(kWPE, kWPE)))
+void rad4_kernel(RadKArgs a) {
+  constexpr int K0 = 16 + KBS;  // op 0's input blocks: feature (16), then the small inputs
+  constexpr int C0 = chunk_bytes(K0), C16 = chunk_bytes(16);
+  __shared__ __attribute__((aligned(16))) char smem[kRing * C0 + (3 * 256 + 4) * 4];
+  static_assert(kRing * C0 + (3 * 256 + 4) * 4 <= 160 * 1024, "LDS budget");
+  WStream4<C0> ws{smem, nullptr, 0, 0, 0};
+  float* head = (float*)(smem + kRing * C0);  // [3][256] weights, then [3] bias
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  const RadLayout& L = a.L;
+  const char* W = a.packed;
+  auto OP = [&](int i) {
+    const char* w = W;
+    asm volatile("" : "+s"(w));
+    return w + L.op_off[i];
+  };
+  const bool view = L.view != 0;
+  {
+    const float* hsrc = (const float*)(W + L.head_off);
+    for (int i = threadIdx.x; i < 3 * 256 + 4; i += kT4) head[i] = hsrc[i];
+  }
+  ws.template start<C0, C0>(OP(0), OP(0) + C0);  // its barrier also publishes the head
+  Pend4 pd{};
+  NoPre4 nopre;
+  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < a.P; base += (int64_t)gridDim.x * kPointsPerWG) {
+    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < a.P;
+    const int64_t p0 = base + wave * 16 * kNC;
+    f16x8 Uh[kNC][12], Ul[kNC][12], Vh[kNC][12], Vl[kNC][12];
+    float m_in[kNC], xinv[kNC], mrun[kNC];
+    bool valid[kNC];
+#pragma unroll
+    for (int q = 0; q < kNC; ++q) {
+      const int64_t p = p0 + 16 * q + j;
+      valid[q] = p < a.P;
+      const int64_t pc = valid[q] ? p : a.P - 1;
+      const int64_t pv = (pc / a.vdiv) % a.vmod;
+      float xs[3], vs[3] = {0.f, 0.f, 0.f}, ns[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        xs[c] = a.x[pc * 3 + c];
+        if (view) {
+          vs[c] = a.vdir[pv * 3 + c];
+          ns[c] = a.normals[pc * 3 + c];
+        }
+      }
+      // the small inputs first: their embedding calls then see few live registers
+      float4 X[16 + KBS];
+      const int gq = (int)opaque_lane(g);  // not hoistable: the 4 KBS feature indices' tests stay in the tile
+#pragma unroll
+      for (int b = 0; b < KBS; ++b) {
+        const int f = 16 * b + 4 * gq;
+        X[16 + b] = make_float4(rad_small_feature(f, xs, vs, ns, a.nfreq_view, view),
+                                rad_small_feature(f + 1, xs, vs, ns, a.nfreq_view, view),
+                                rad_small_feature(f + 2, xs, vs, ns, a.nfreq_view, view),
+                                rad_small_feature(f + 3, xs, vs, ns, a.nfreq_view, view));
+      }
+#pragma unroll
+      for (int b = 0; b < 16; ++b) X[b] = *(const float4*)(a.feature + pc * 256 + 16 * b + 4 * g);
+      float m = 0.0f;
+#pragma unroll
+      for (int b = 0; b < 16 + KBS; b += 2) m = amax8(m, X[b], X[b + 1]);
+      m_in[q] = max4_groups(m);
+      const float s = bound_scale(m_in[q]);  // exact-max scale of op 0's operand
+#pragma unroll
+      for (int k = 0; k < K0 / 2; ++k) split8a(X[2 * k], X[2 * k + 1], s, Uh[q][k], Ul[q][k]);
+      xinv[q] = 1.0f / s;
+      mrun[q] = 0.0f;
+    }
+    auto next_scales = [&](int kb, float (&sc)[kNC]) {
+      const float4 v = ws.buf()[2 * kb * 64 + 8];
+#pragma unroll
+      for (int q = 0; q < kNC; ++q) sc[q] = bound_scale(fmaf(v.y, m_in[q], v.z));
+    };
+    auto finish = [&](const float (&sc)[kNC]) {
+#pragma unroll
+      for (int q = 0; q < kNC; ++q) {
+        m_in[q] = max4_groups(mrun[q]);
+        mrun[q] = 0.0f;
+        xinv[q] = 1.0f / sc[q];
+      }
+    };
+    {
+      float sc[kNC];
+      next_scales(K0, sc);
+      op4<K0, 16, C16, false, false>(ws, OP(0), OP(1), Uh, Ul, xinv, pd, nopre, ReluEpi4{Vh, Vl, sc, mrun}, lane);
+      finish(sc);
+    }
+    {
+      float sc[kNC];
+      next_scales(16, sc);
+      op4<16, 16, C16, false, false>(ws, OP(1), OP(2), Vh, Vl, xinv, pd, nopre, ReluEpi4{Uh, Ul, sc, mrun}, lane);
+      finish(sc);
+    }
+    {
+      float sc[kNC];
+      next_scales(16, sc);
+      op4<16, 16, C16, false, false>(ws, OP(2), OP(3), Uh, Ul, xinv, pd, nopre, ReluEpi4{Vh, Vl, sc, mrun}, lane);
+      finish(sc);
+    }
+    float part[kNC][3];
+#pragma unroll
+    for (int q = 0; q < kNC; ++q) part[q][0] = part[q][1] = part[q][2] = 0.0f;
+    op4<16, 16, C0, false, false>(ws, OP(3), has_next ? OP(0) : nullptr, Vh, Vl, xinv, pd, nopre,
+                                  HeadEpi4{head, part, g}, lane);
+#pragma unroll
+    for (int q = 0; q < kNC; ++q) {
+      float r[3];
+#pragma unroll
+      for (int o = 0; o < 3; ++o) r[o] = sigmoidf_ref(wave_sum4(part[q][o]) + head[3 * 256 + o]);
+      if (valid[q] && g == 0) {
+        const int64_t p = p0 + 16 * q + j;
+        a.rgb[p * 3 + 0] = r[0];
+        a.rgb[p * 3 + 1] = r[1];
+        a.rgb[p * 3 + 2] = r[2];
+      }
+    }
+  }
+  pd.flush();
+  wait_vmcnt(0);  // a block without tiles still has the prologue's second chunk in flight
+}
+
+// =============================================================================================
 // NeRF++ background kernel (models/base.py:395-453, use_view_dirs=True, multires 10 on the 4-D
 // inverted-sphere input [x/r, 1/r], multires_view 4).  Plain nn.Linear layers, ReLU.
 // =============================================================================================
@@ -2402,7 +2590,10 @@ int launch_radiance(const RadLayout& L, const void* packed, const float* x, cons
     set_error("radiance: unsupported small-input block count");
     return NR_ERR_UNSUPPORTED;
   }
-  if (!L.siren && L.D == 4) {
+  if (h3 && !L.siren && L.D == 4) {  // the v3 pipeline (rad4_kernel)
+    if (L.kbs == 2) hipLaunchKernelGGL((rad4_kernel<2>), dim3(grid), dim3(kT4), 0, stream, a);
+    else hipLaunchKernelGGL((rad4_kernel<4>), dim3(grid), dim3(kT4), 0, stream, a);
+  } else if (!L.siren && L.D == 4) {
     if (L.kbs == 2) NR_RAD_LAUNCH(2, ACT_RELU, 4); else NR_RAD_LAUNCH(4, ACT_RELU, 4);
   } else if (!L.siren && L.D == 5) {
     if (L.kbs == 2) NR_RAD_LAUNCH(2, ACT_RELU, 5); else NR_RAD_LAUNCH(4, ACT_RELU, 5);
