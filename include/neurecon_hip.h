@@ -494,6 +494,26 @@ int nr_volsdf_composite_bwd(const float* sdf, const float* pts, const float* bet
                             const float* g_rgb, const float* g_depth, const float* g_acc, const float* g_tau,
                             const float* g_sdf, float* d_sdf, float* d_rad, float* d_beta, void* workspace,
                             size_t workspace_bytes, void* stream);
+/* the same with VolSDF's NeRF++ background (volsdf.py:455-469): N background samples after the S inner
+ * ones, sigma_bg [R,N] (the background net's raw sigma), radiance_bg [R,N,3], d_bg [R,N]; tau / p_i
+ * [R,S+N-1], sigma [R,S+N]; the backward adds d sigma_bg [R,N] and d radiance_bg [R,N,3]. */
+int nr_volsdf_composite_bg_fwd(const float* sdf, const float* pts, const float* beta_dev, const float* rad,
+                               const float* d_all, int64_t R, int S, int use_bg, float r_bg, int white_bkgd,
+                               const float* sigma_bg, const float* rad_bg, const float* d_bg, int N, float* rgb,
+                               float* depth, float* acc, float* tau, float* p_i, float* sigma, float* sdf_out,
+                               void* stream);
+size_t nr_volsdf_composite_bg_bwd_workspace_bytes(int64_t R, int S, int N);
+int nr_volsdf_composite_bg_bwd(const float* sdf, const float* pts, const float* beta_dev, const float* rad,
+                               const float* d_all, int64_t R, int S, int use_bg, float r_bg, int white_bkgd,
+                               const float* sigma_bg, const float* rad_bg, const float* d_bg, int N,
+                               const float* g_rgb, const float* g_depth, const float* g_acc, const float* g_tau,
+                               const float* g_sdf, float* d_sdf, float* d_rad, float* d_beta, float* d_sigma_bg,
+                               float* d_rad_bg, void* workspace, size_t workspace_bytes, void* stream);
+/* inputs of VolSDF's NeRF++ background net in the training step (volsdf.py:456-467): p = o + d_bg*dir,
+ * x_emb [R*N, 84] = Embedder(4, 10)([p / rs, 1 / rs]) at the sample radii rs [R,N], v_emb [R*N, 27] =
+ * Embedder(3, 4)(dir) */
+int nr_volsdf_nerf_input(const float* rays_o, const float* rays_d, const float* d_bg, const float* rs, int64_t R,
+                         int N, float* x_emb, float* v_emb, void* stream);
 
 /* UNISURF compositing with a graph (unisurf.py:219-236, get_opacity_from_surface :53-62): logits [R,P]
  * (implicit_surface), radiance [R,P,3], d_all [R,P].  alpha = exp(-l) / (1 + exp(-l)), visibility weights

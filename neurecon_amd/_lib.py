@@ -169,6 +169,13 @@ _SIGS = {
     'nr_unisurf_composite_bwd_workspace_bytes': (_c_sz, [_c_i64, _c_i]),
     'nr_unisurf_composite_bwd': (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
                                         _c_sz, _c_p]),
+    'nr_volsdf_composite_bg_fwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_f, _c_i, _c_p, _c_p,
+                                          _c_p, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    'nr_volsdf_composite_bg_bwd_workspace_bytes': (_c_sz, [_c_i64, _c_i, _c_i]),
+    'nr_volsdf_composite_bg_bwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_f, _c_i, _c_p, _c_p,
+                                          _c_p, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                          _c_sz, _c_p]),
+    'nr_volsdf_nerf_input': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_p, _c_p, _c_p]),
     'nr_volsdf_composite_fwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_f, _c_i, _c_p, _c_p, _c_p,
                                        _c_p, _c_p, _c_p, _c_p, _c_p]),
     'nr_volsdf_composite_bwd_workspace_bytes': (_c_sz, [_c_i64, _c_i]),

@@ -355,34 +355,49 @@ __device__ __forceinline__ float vs_sdf_bg(const float* sdf, const float* pts, i
   }
   return v;
 }
+// With the NeRF++ background (volsdf.py:455-469) the N background samples follow the S inner ones:
+// sigma_bg [R,N] (the background net's raw sigma), radiance_bg [R,N,3], d_bg [R,N]; M = S + N samples
+// are integrated (p, tau over M-1, sigma over M).  N = 0: the inner samples only.
+struct VsBg {
+  const float* sig;
+  const float* rad;
+  const float* d;
+  int N;
+};
 __global__ void volsdf_composite_fwd_kernel(const float* __restrict__ sdf, const float* __restrict__ pts,
                                             const float* __restrict__ beta_dev, const float* __restrict__ rad,
                                             const float* __restrict__ d_all, int64_t R, int S, int use_bg, float r_bg,
-                                            int white_bkgd, float* __restrict__ rgb, float* __restrict__ depth,
-                                            float* __restrict__ acc, float* __restrict__ tau_out,
-                                            float* __restrict__ p_out, float* __restrict__ sigma_out,
-                                            float* __restrict__ sdf_out) {
+                                            int white_bkgd, VsBg bg, float* __restrict__ rgb,
+                                            float* __restrict__ depth, float* __restrict__ acc,
+                                            float* __restrict__ tau_out, float* __restrict__ p_out,
+                                            float* __restrict__ sigma_out, float* __restrict__ sdf_out) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
   const float beta = *beta_dev, alpha = fdiv(1.0f, beta);
-  const int S1 = S - 1;
-  const float* d = d_all + r * S;
+  const int M = S + bg.N, M1 = M - 1;
+  auto dv = [&](int i) { return i < S ? d_all[r * S + i] : bg.d[r * bg.N + i - S]; };
+  auto rv = [&](int i) { return i < S ? rad + (r * S + i) * 3 : bg.rad + (r * bg.N + i - S) * 3; };
   double T = 1.0, a_acc = 0.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
   bool m;
   float sg = vs_sigma_t(vs_sdf_bg(sdf, pts, r * S, use_bg, r_bg, m), alpha, beta);
-  for (int i = 0; i < S; ++i) {
-    const int64_t q = r * S + i;
-    const float v = vs_sdf_bg(sdf, pts, q, use_bg, r_bg, m);
-    const float si = vs_sigma_t(v, alpha, beta);
-    if (sdf_out) sdf_out[q] = v;
-    if (sigma_out) sigma_out[q] = si;
+  for (int i = 0; i < M; ++i) {
+    float si;
+    if (i < S) {
+      const int64_t q = r * S + i;
+      const float v = vs_sdf_bg(sdf, pts, q, use_bg, r_bg, m);
+      si = vs_sigma_t(v, alpha, beta);
+      if (sdf_out) sdf_out[q] = v;
+    } else {
+      si = bg.sig[r * bg.N + i - S];
+    }
+    if (sigma_out) sigma_out[r * M + i] = si;
     if (i == 0) continue;
     // sample i-1's interval
-    const float p = expf(-fmaxf(fmul(sg, fsub(d[i], d[i - 1])), 0.0f));
+    const float p = expf(-fmaxf(fmul(sg, fsub(dv(i), dv(i - 1))), 0.0f));
     const float tau = fmul(fadd(fsub(1.0f, p), 1e-10f), (float)T);
     T *= (double)p;
-    const int64_t k = r * S1 + i - 1;
-    const float* rr = rad + (r * S + i - 1) * 3;
+    const int64_t k = r * M1 + i - 1;
+    const float* rr = rv(i - 1);
     c0 += (double)fmul(tau, rr[0]);
     c1 += (double)fmul(tau, rr[1]);
     c2 += (double)fmul(tau, rr[2]);
@@ -394,11 +409,11 @@ __global__ void volsdf_composite_fwd_kernel(const float* __restrict__ sdf, const
   const float accf = (float)a_acc;
   const float den = fadd(accf, 1e-10f);
   double dep = 0.0;
-  for (int i = 0; i < S1; ++i) dep += (double)fmul(fdiv(tau_out[r * S1 + i], den), d[i]);
+  for (int i = 0; i < M1; ++i) dep += (double)fmul(fdiv(tau_out[r * M1 + i], den), dv(i));
   float o0 = (float)c0, o1 = (float)c1, o2 = (float)c2;
   if (white_bkgd) {
-    const float bg = fsub(1.0f, accf);
-    o0 = fadd(o0, bg); o1 = fadd(o1, bg); o2 = fadd(o2, bg);
+    const float bg_ = fsub(1.0f, accf);
+    o0 = fadd(o0, bg_); o1 = fadd(o1, bg_); o2 = fadd(o2, bg_);
   }
   rgb[r * 3 + 0] = o0;
   rgb[r * 3 + 1] = o1;
@@ -407,38 +422,47 @@ __global__ void volsdf_composite_fwd_kernel(const float* __restrict__ sdf, const
   acc[r] = accf;
 }
 
-// backward of the above: grads of rgb [R,3], depth [R], acc [R], tau [R,S-1] and the background-applied
-// sdf [R,S] (all optional) -> d sdf (network values) [R,S], d radiance [R,S,3] (the last sample's row is
-// 0: volsdf.py:495 uses radiances[..., :-1, :]), d beta per ray [R] (the host sums; both the alpha = 1/beta
-// and the psi(beta) paths).  tau_i = u_i P_i with u_i = 1 - p_i + 1e-10 and P_i = prod_{j<i} p_j, so
+// backward of the above: grads of rgb [R,3], depth [R], acc [R], tau [R,M-1] and the background-applied
+// sdf [R,S] (all optional) -> d sdf (network values) [R,S], d radiance [R,S,3] (rows past the first M-1
+// samples are 0: volsdf.py:495 uses radiances[..., :-1, :]), d beta per ray [R] (the host sums; both the
+// alpha = 1/beta and the psi(beta) paths), and with the NeRF++ background d sigma_bg [R,N] and
+// d radiance_bg [R,N,3].  tau_i = u_i P_i with u_i = 1 - p_i + 1e-10 and P_i = prod_{j<i} p_j, so
 // pbar_i = P_i (G_i - taubar_i) with G_i = sum_{k>i} taubar_k u_k prod_{i<j<k} p_j (no division by p).
 __global__ void volsdf_composite_bwd_kernel(const float* __restrict__ sdf, const float* __restrict__ pts,
                                             const float* __restrict__ beta_dev, const float* __restrict__ rad,
                                             const float* __restrict__ d_all, int64_t R, int S, int use_bg, float r_bg,
-                                            int white_bkgd, const float* __restrict__ g_rgb,
+                                            int white_bkgd, VsBg bg, const float* __restrict__ g_rgb,
                                             const float* __restrict__ g_depth, const float* __restrict__ g_acc,
                                             const float* __restrict__ g_tau, const float* __restrict__ g_sdf,
                                             float* __restrict__ work, float* __restrict__ d_sdf,
-                                            float* __restrict__ d_rad, float* __restrict__ d_beta) {
+                                            float* __restrict__ d_rad, float* __restrict__ d_beta,
+                                            float* __restrict__ d_sig_bg, float* __restrict__ d_rad_bg) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
   const float beta = *beta_dev, alpha = fdiv(1.0f, beta);
-  const int S1 = S - 1;
-  const float* d = d_all + r * S;
-  // work rows: v (bg-applied sdf) [S], sigma [S], p [S], P [S], tau [S]
-  float* v = work + r * (5 * S);
-  float* sg = v + S;
-  float* p = sg + S;
-  float* P = p + S;
-  float* tau = P + S;
+  const int M = S + bg.N, M1 = M - 1;
+  auto dv = [&](int i) { return i < S ? d_all[r * S + i] : bg.d[r * bg.N + i - S]; };
+  auto rv = [&](int i) { return i < S ? rad + (r * S + i) * 3 : bg.rad + (r * bg.N + i - S) * 3; };
+  auto drv = [&](int i) { return i < S ? d_rad + (r * S + i) * 3 : d_rad_bg + (r * bg.N + i - S) * 3; };
+  // work rows: v (bg-applied sdf) [M], sigma [M], p [M], P [M], tau [M]
+  float* v = work + r * (5 * M);
+  float* sg = v + M;
+  float* p = sg + M;
+  float* P = p + M;
+  float* tau = P + M;
   double T = 1.0, a_acc = 0.0, wd = 0.0;
-  for (int i = 0; i < S; ++i) {
+  for (int i = 0; i < M; ++i) {
     bool m;
-    v[i] = vs_sdf_bg(sdf, pts, r * S + i, use_bg, r_bg, m);
-    sg[i] = vs_sigma_t(v[i], alpha, beta);
+    if (i < S) {
+      v[i] = vs_sdf_bg(sdf, pts, r * S + i, use_bg, r_bg, m);
+      sg[i] = vs_sigma_t(v[i], alpha, beta);
+    } else {
+      v[i] = 0.0f;
+      sg[i] = bg.sig[r * bg.N + i - S];
+    }
   }
-  for (int i = 0; i < S1; ++i) {
-    p[i] = expf(-fmaxf(fmul(sg[i], fsub(d[i + 1], d[i])), 0.0f));
+  for (int i = 0; i < M1; ++i) {
+    p[i] = expf(-fmaxf(fmul(sg[i], fsub(dv(i + 1), dv(i))), 0.0f));
     P[i] = (float)T;
     tau[i] = fmul(fadd(fsub(1.0f, p[i]), 1e-10f), P[i]);
     T *= (double)p[i];
@@ -446,30 +470,30 @@ __global__ void volsdf_composite_bwd_kernel(const float* __restrict__ sdf, const
   }
   const float accf = (float)a_acc;
   const double A = (double)fadd(accf, 1e-10f);
-  for (int i = 0; i < S1; ++i) wd += (double)tau[i] * (double)d[i];
+  for (int i = 0; i < M1; ++i) wd += (double)tau[i] * (double)dv(i);
   const float gr0 = g_rgb ? g_rgb[r * 3 + 0] : 0.f, gr1 = g_rgb ? g_rgb[r * 3 + 1] : 0.f,
               gr2 = g_rgb ? g_rgb[r * 3 + 2] : 0.f;
   const double gd = g_depth ? (double)g_depth[r] : 0.0;
   const double ga = (g_acc ? (double)g_acc[r] : 0.0) - (white_bkgd ? (double)gr0 + gr1 + gr2 : 0.0);
   double G = 0.0, bbar = 0.0;
   const double ib2 = 1.0 / ((double)beta * beta);
-  for (int i = S - 1; i >= 0; --i) {
-    const int64_t q = r * S + i;
-    double vbar = 0.0;
-    if (i < S1) {
-      const float* rr = rad + q * 3;
+  for (int i = M - 1; i >= 0; --i) {
+    double vbar = 0.0, sbar = 0.0;
+    float* dr = drv(i);
+    if (i < M1) {
+      const float* rr = rv(i);
       double tb = (double)gr0 * rr[0] + (double)gr1 * rr[1] + (double)gr2 * rr[2] + ga;
-      tb += gd * ((double)d[i] / A - wd / (A * A));
-      if (g_tau) tb += (double)g_tau[r * S1 + i];
-      d_rad[q * 3 + 0] = fmul(tau[i], gr0);
-      d_rad[q * 3 + 1] = fmul(tau[i], gr1);
-      d_rad[q * 3 + 2] = fmul(tau[i], gr2);
+      tb += gd * ((double)dv(i) / A - wd / (A * A));
+      if (g_tau) tb += (double)g_tau[r * M1 + i];
+      dr[0] = fmul(tau[i], gr0);
+      dr[1] = fmul(tau[i], gr1);
+      dr[2] = fmul(tau[i], gr2);
       const double u = (double)fadd(fsub(1.0f, p[i]), 1e-10f);
       const double pbar = (double)P[i] * (G - tb);
       G = tb * u + (double)p[i] * G;
-      const float delta = fsub(d[i + 1], d[i]);
-      if (fmul(sg[i], delta) > 0.0f) {
-        const double sbar = -pbar * (double)p[i] * (double)delta;
+      const float delta = fsub(dv(i + 1), dv(i));
+      if (fmul(sg[i], delta) > 0.0f) sbar = -pbar * (double)p[i] * (double)delta;
+      if (i < S && sbar != 0.0) {
         // sigma = alpha psi(v, beta), psi = e or 1 - e, e = 0.5 exp(-|v| / beta)
         const double e = (double)fmul(0.5f, expf(fdiv(-fabsf(v[i]), beta)));
         const double sgn = v[i] > 0.0f ? 1.0 : (v[i] < 0.0f ? -1.0 : 0.0);
@@ -479,14 +503,19 @@ __global__ void volsdf_composite_bwd_kernel(const float* __restrict__ sdf, const
         bbar += sbar * (psi * (-ib2) + (double)alpha * br * e * fabs((double)v[i]) * ib2);
       }
     } else {
-      d_rad[q * 3 + 0] = 0.0f;
-      d_rad[q * 3 + 1] = 0.0f;
-      d_rad[q * 3 + 2] = 0.0f;
+      dr[0] = 0.0f;
+      dr[1] = 0.0f;
+      dr[2] = 0.0f;
     }
-    if (g_sdf) vbar += (double)g_sdf[q];
-    bool m;
-    (void)vs_sdf_bg(sdf, pts, q, use_bg, r_bg, m);
-    d_sdf[q] = m ? 0.0f : (float)vbar;
+    if (i < S) {
+      const int64_t q = r * S + i;
+      if (g_sdf) vbar += (double)g_sdf[q];
+      bool m;
+      (void)vs_sdf_bg(sdf, pts, q, use_bg, r_bg, m);
+      d_sdf[q] = m ? 0.0f : (float)vbar;
+    } else {
+      d_sig_bg[r * bg.N + i - S] = (float)sbar;
+    }
   }
   d_beta[r] = (float)bbar;
 }
@@ -518,6 +547,24 @@ __global__ void nerf_train_input_kernel(const float* __restrict__ ro, const floa
   const float vs[3] = {rd[r * 3], rd[r * 3 + 1], rd[r * 3 + 2]};
   for (int f = 0; f < 27; ++f) v_emb[i * 27 + f] = emb_f(f, vs, 4);
   if (k < n_mid) inside[r * n_mid + k] = rr <= r_obj ? 1 : 0;
+}
+
+// inputs of VolSDF's NeRF++ background net (volsdf.py:456-467): p = o + d_bg dir at the radius rs of
+// each sample, x4 = [p / rs, 1 / rs] embedded with 10 frequencies (Embedder(input_dim=4)), the view
+// direction with 4
+__global__ void volsdf_nerf_input_kernel(const float* __restrict__ ro, const float* __restrict__ rd,
+                                         const float* __restrict__ d_bg, const float* __restrict__ rs, int64_t R,
+                                         int N, float* __restrict__ x_emb, float* __restrict__ v_emb) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * N) return;
+  const int64_t r = i / N;
+  const float d = d_bg[i], rr = rs[i];
+  const float px = fadd(ro[r * 3 + 0], fmul(rd[r * 3 + 0], d)), py = fadd(ro[r * 3 + 1], fmul(rd[r * 3 + 1], d)),
+              pz = fadd(ro[r * 3 + 2], fmul(rd[r * 3 + 2], d));
+  const float x4[4] = {fdiv(px, rr), fdiv(py, rr), fdiv(pz, rr), fdiv(1.0f, rr)};
+  for (int f = 0; f < 84; ++f) x_emb[i * 84 + f] = emb4_f(f, x4);
+  const float vs[3] = {rd[r * 3], rd[r * 3 + 1], rd[r * 3 + 2]};
+  for (int f = 0; f < 27; ++f) v_emb[i * 27 + f] = emb_f(f, vs, 4);
 }
 
 // F.softplus (beta 1, threshold 20) and its derivative (softplus_backward)
@@ -1000,22 +1047,56 @@ int nr_unisurf_composite_bwd(const float* logits, const float* rad, const float*
   return NR_OK;
 }
 
-int nr_volsdf_composite_fwd(const float* sdf, const float* pts, const float* beta_dev, const float* rad,
-                            const float* d_all, int64_t R, int S, int use_bg, float r_bg, int white_bkgd, float* rgb,
-                            float* depth, float* acc, float* tau, float* p_i, float* sigma, float* sdf_out,
-                            void* stream) {
-  NR_REQUIRE(sdf && pts && beta_dev && rad && d_all && rgb && depth && acc && tau && R >= 0 && S >= 2, NR_ERR_ARG,
-             "nr_volsdf_composite_fwd: bad argument");
+int nr_volsdf_composite_bg_fwd(const float* sdf, const float* pts, const float* beta_dev, const float* rad,
+                               const float* d_all, int64_t R, int S, int use_bg, float r_bg, int white_bkgd,
+                               const float* sigma_bg, const float* rad_bg, const float* d_bg, int N, float* rgb,
+                               float* depth, float* acc, float* tau, float* p_i, float* sigma, float* sdf_out,
+                               void* stream) {
+  NR_REQUIRE(sdf && pts && beta_dev && rad && d_all && rgb && depth && acc && tau && R >= 0 && S >= 2 && N >= 0 &&
+                 (N == 0 || (sigma_bg && rad_bg && d_bg)),
+             NR_ERR_ARG, "nr_volsdf_composite_fwd: bad argument");
   if (R == 0) return NR_OK;
   hipLaunchKernelGGL(volsdf_composite_fwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
-                     sdf, pts, beta_dev, rad, d_all, R, S, use_bg, r_bg, white_bkgd, rgb, depth, acc, tau, p_i, sigma,
-                     sdf_out);
+                     sdf, pts, beta_dev, rad, d_all, R, S, use_bg, r_bg, white_bkgd, VsBg{sigma_bg, rad_bg, d_bg, N},
+                     rgb, depth, acc, tau, p_i, sigma, sdf_out);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
 
+int nr_volsdf_composite_fwd(const float* sdf, const float* pts, const float* beta_dev, const float* rad,
+                            const float* d_all, int64_t R, int S, int use_bg, float r_bg, int white_bkgd, float* rgb,
+                            float* depth, float* acc, float* tau, float* p_i, float* sigma, float* sdf_out,
+                            void* stream) {
+  return nr_volsdf_composite_bg_fwd(sdf, pts, beta_dev, rad, d_all, R, S, use_bg, r_bg, white_bkgd, nullptr, nullptr,
+                                    nullptr, 0, rgb, depth, acc, tau, p_i, sigma, sdf_out, stream);
+}
+
+size_t nr_volsdf_composite_bg_bwd_workspace_bytes(int64_t R, int S, int N) {
+  return (size_t)(R > 0 ? R : 1) * 5 * (size_t)(S + N) * sizeof(float);
+}
+
 size_t nr_volsdf_composite_bwd_workspace_bytes(int64_t R, int S) {
-  return (size_t)(R > 0 ? R : 1) * 5 * (size_t)S * sizeof(float);
+  return nr_volsdf_composite_bg_bwd_workspace_bytes(R, S, 0);
+}
+
+int nr_volsdf_composite_bg_bwd(const float* sdf, const float* pts, const float* beta_dev, const float* rad,
+                               const float* d_all, int64_t R, int S, int use_bg, float r_bg, int white_bkgd,
+                               const float* sigma_bg, const float* rad_bg, const float* d_bg, int N,
+                               const float* g_rgb, const float* g_depth, const float* g_acc, const float* g_tau,
+                               const float* g_sdf, float* d_sdf, float* d_rad, float* d_beta, float* d_sigma_bg,
+                               float* d_rad_bg, void* workspace, size_t workspace_bytes, void* stream) {
+  NR_REQUIRE(sdf && pts && beta_dev && rad && d_all && d_sdf && d_rad && d_beta && R >= 0 && S >= 2 && N >= 0 &&
+                 (N == 0 || (sigma_bg && rad_bg && d_bg && d_sigma_bg && d_rad_bg)),
+             NR_ERR_ARG, "nr_volsdf_composite_bwd: bad argument");
+  if (R == 0) return NR_OK;
+  NR_REQUIRE(workspace && workspace_bytes >= nr_volsdf_composite_bg_bwd_workspace_bytes(R, S, N), NR_ERR_WORKSPACE,
+             "nr_volsdf_composite_bwd: workspace too small");
+  hipLaunchKernelGGL(volsdf_composite_bwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
+                     sdf, pts, beta_dev, rad, d_all, R, S, use_bg, r_bg, white_bkgd, VsBg{sigma_bg, rad_bg, d_bg, N},
+                     g_rgb, g_depth, g_acc, g_tau, g_sdf, (float*)workspace, d_sdf, d_rad, d_beta, d_sigma_bg,
+                     d_rad_bg);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
 }
 
 int nr_volsdf_composite_bwd(const float* sdf, const float* pts, const float* beta_dev, const float* rad,
@@ -1023,14 +1104,18 @@ int nr_volsdf_composite_bwd(const float* sdf, const float* pts, const float* bet
                             const float* g_rgb, const float* g_depth, const float* g_acc, const float* g_tau,
                             const float* g_sdf, float* d_sdf, float* d_rad, float* d_beta, void* workspace,
                             size_t workspace_bytes, void* stream) {
-  NR_REQUIRE(sdf && pts && beta_dev && rad && d_all && d_sdf && d_rad && d_beta && R >= 0 && S >= 2, NR_ERR_ARG,
-             "nr_volsdf_composite_bwd: bad argument");
+  return nr_volsdf_composite_bg_bwd(sdf, pts, beta_dev, rad, d_all, R, S, use_bg, r_bg, white_bkgd, nullptr, nullptr,
+                                    nullptr, 0, g_rgb, g_depth, g_acc, g_tau, g_sdf, d_sdf, d_rad, d_beta, nullptr,
+                                    nullptr, workspace, workspace_bytes, stream);
+}
+
+int nr_volsdf_nerf_input(const float* rays_o, const float* rays_d, const float* d_bg, const float* rs, int64_t R,
+                         int N, float* x_emb, float* v_emb, void* stream) {
+  NR_REQUIRE(rays_o && rays_d && d_bg && rs && x_emb && v_emb && R >= 0 && N >= 1, NR_ERR_ARG,
+             "nr_volsdf_nerf_input: bad argument");
   if (R == 0) return NR_OK;
-  NR_REQUIRE(workspace && workspace_bytes >= nr_volsdf_composite_bwd_workspace_bytes(R, S), NR_ERR_WORKSPACE,
-             "nr_volsdf_composite_bwd: workspace too small");
-  hipLaunchKernelGGL(volsdf_composite_bwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
-                     sdf, pts, beta_dev, rad, d_all, R, S, use_bg, r_bg, white_bkgd, g_rgb, g_depth, g_acc, g_tau,
-                     g_sdf, (float*)workspace, d_sdf, d_rad, d_beta);
+  hipLaunchKernelGGL(volsdf_nerf_input_kernel, grid1(R * N), dim3(kBlk), 0, (hipStream_t)stream, rays_o, rays_d, d_bg,
+                     rs, R, N, x_emb, v_emb);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

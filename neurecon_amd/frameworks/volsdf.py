@@ -114,7 +114,7 @@ def volume_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=
                   batched_info={}, calc_normal=False, use_view_dirs=True, rayschunk=65536, netchunk=1048576,
                   white_bkgd=False, use_nerfplusplus=False, detailed_output=True, show_progress=False,
                   perturb=False, N_samples=128, N_importance=64, N_outside=32, max_upsample_steps=5,
-                  max_bisection_steps=10, epsilon=0.1, **dummy_kwargs):
+                  max_bisection_steps=10, epsilon=0.1, _uniforms=None, **dummy_kwargs):
     """volsdf.py:377-551, render mode.  rays_o/rays_d: [(B,) N_rays, 3].  perturb=True: random final
     fine samples and NeRF++ strata (_volsdf_uniforms)."""
     L.require_gpu(rays_o, 'rays_o')
@@ -195,8 +195,10 @@ def volume_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=
     a.sigma_bg = L.ptr(det.get('sigma_out'))
     a.radiance_bg = L.ptr(det.get('radiance_out'))
     if perturb:
-        Bn = rays_d.shape[0] if batched else 1
-        u_rand, u_out = _volsdf_uniforms(Bn, n // Bn, batched, int(rayschunk), N_importance, No, dev)
+        if _uniforms is None:
+            Bn = rays_d.shape[0] if batched else 1
+            _uniforms = _volsdf_uniforms(Bn, n // Bn, batched, int(rayschunk), N_importance, No, dev)
+        u_rand, u_out = _uniforms
         a.u_rand, a.u_out = L.ptr(u_rand), L.ptr(u_out)
     lib = L.lib()
     ws_bytes = lib.nr_volsdf_workspace_bytes(ctypes.byref(a))
@@ -233,28 +235,35 @@ def _train_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=
                   max_bisection_steps=10, epsilon=0.1):
     """volsdf.py:377-551 with an autograd graph (training): the sample depths d_all come from the
     no-grad render path (error-bounded fine sampling, volsdf.py:420-445, the same call under
-    torch.no_grad), then SDF + nablas + geometry feature at every sample (double-backward capable),
+    torch.no_grad; with perturb=True both take the same uniforms), then SDF + nablas + geometry feature
+    at every sample (double-backward capable), with use_nerfplusplus the background net at the
+    sampler's outside depths and radii (volsdf.py:455-469),
     the radiance net and the background / sdf_to_sigma / integration as neurecon_amd.training
-    autograd functions.  Gradients reach every surface and radiance parameter and ln_beta.  Returns
+    autograd functions.  Gradients reach every surface, radiance (and background) parameter and
+    ln_beta.  Returns
     the reference's (rgb, depth, extras)."""
     from .. import training as T
     check_view_dirs(model, use_view_dirs)
-    if use_nerfplusplus:
-        raise NotImplementedError('neurecon_amd: VolSDF training with the NeRF++ background has no native path '
-                                  '(the builtin background sphere trains natively)')
     dev = rays_o.device
     prefix = [rays_d.shape[0], -1] if batched else [-1]
-    with torch.no_grad():
-        _, _, ex = volume_render(rays_o, rays_d, model, near=near, far=far, obj_bounding_radius=obj_bounding_radius,
-                                 batched=batched, calc_normal=False, use_view_dirs=use_view_dirs, rayschunk=rayschunk,
-                                 white_bkgd=white_bkgd, use_nerfplusplus=False, detailed_output=True, perturb=perturb,
-                                 N_samples=N_samples, N_importance=N_importance, max_upsample_steps=max_upsample_steps,
-                                 max_bisection_steps=max_bisection_steps, epsilon=epsilon)
+    No = int(N_outside) if use_nerfplusplus else 0
     ro = rays_o.reshape(-1, 3).float().contiguous()
     rd_raw = rays_d.reshape(-1, 3).float().contiguous()
     n = ro.shape[0]
     S = N_samples + N_importance
-    d_all = ex['d_vals'].reshape(n, S).contiguous()
+    uni = None
+    if perturb:  # drawn once: the no-grad sampler and the background radii below use the same draws
+        Bn = rays_d.shape[0] if batched else 1
+        uni = _volsdf_uniforms(Bn, n // Bn, batched, int(rayschunk), N_importance, No, dev)
+    with torch.no_grad():
+        _, _, ex = volume_render(rays_o, rays_d, model, near=near, far=far, obj_bounding_radius=obj_bounding_radius,
+                                 batched=batched, calc_normal=False, use_view_dirs=use_view_dirs, rayschunk=rayschunk,
+                                 white_bkgd=white_bkgd, use_nerfplusplus=use_nerfplusplus, detailed_output=True,
+                                 perturb=perturb, N_samples=N_samples, N_importance=N_importance, N_outside=N_outside,
+                                 max_upsample_steps=max_upsample_steps, max_bisection_steps=max_bisection_steps,
+                                 epsilon=epsilon, _uniforms=uni)
+    d_vals = ex['d_vals'].reshape(n, S + No)
+    d_all = d_vals[:, :S].contiguous()
     rd = torch.empty_like(rd_raw)  # F.normalize(rays_d, dim=-1) (volsdf.py:386)
     L.check(L.lib().nr_normalize3(L.ptr(rd_raw), n, L.ptr(rd), L.stream_of(dev)))
     pts = torch.empty(n, S, 3, device=dev)
@@ -266,9 +275,26 @@ def _train_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=
     view = rd[:, None, :].expand(n, S, 3).reshape(-1, 3).contiguous()
     rad = T.radiance(model.radiance_net, pts.reshape(-1, 3), view, nablas, feat)
     _, beta = model.forward_ab()
+    bg = ()
+    if No > 0:  # NeRF++ background (volsdf.py:455-469) at the sampler's depths d_out and radii rs
+        d_bg = d_vals[:, S:].contiguous()
+        rs = _outside_radii(No, float(obj_bounding_radius), dev).expand(n, No)
+        if perturb:  # volsdf.py:460-465, the draws the sampler used
+            mids = .5 * (rs[..., 1:] + rs[..., :-1])
+            upper = torch.cat([mids, rs[..., -1:]], -1)
+            lower = torch.cat([rs[..., :1], mids], -1)
+            rs = lower + (upper - lower) * uni[1].reshape(n, No)
+        rs = rs.contiguous()
+        x_emb = torch.empty(n * No, 84, device=dev)
+        v_emb = torch.empty(n * No, 27, device=dev)
+        L.check(L.lib().nr_volsdf_nerf_input(L.ptr(ro), L.ptr(rd), L.ptr(d_bg), L.ptr(rs), n, No, L.ptr(x_emb),
+                                             L.ptr(v_emb), L.stream_of(dev)))
+        sig_o, rad_o = T.nerf(model.nerf_outside, x_emb, v_emb)
+        bg = (sig_o.reshape(n, No), rad_o.reshape(n, No, 3), d_bg)
     rgb, depth, acc, tau, sdf_bg, p_i, sigma = T.VolSDFComposite.apply(
         sdf.reshape(n, S), beta, rad.reshape(n, S, 3), pts, d_all, bool(model.use_sphere_bg),
-        float(model.obj_bounding_radius), bool(white_bkgd))
+        float(model.obj_bounding_radius), bool(white_bkgd), *bg)
+    M = S + No
     nablas = nablas.reshape(n, S, 3)
     ret = OrderedDict([('rgb', rgb.reshape(*prefix, 3)), ('depth_volume', depth.reshape(prefix)),
                        ('mask_volume', acc.reshape(prefix))])
@@ -279,14 +305,18 @@ def _train_render(rays_o, rays_d, model, near=0.0, far=6.0, obj_bounding_radius=
     if detailed_output:
         ret['implicit_surface'] = sdf_bg.reshape(*prefix, S)
         ret['implicit_nablas'] = nablas.reshape(*prefix, S, 3)
-        ret['radiance'] = rad.reshape(*prefix, S, 3)
-        ret['alpha'] = (1.0 - p_i).reshape(*prefix, S - 1)
-        ret['p_i'] = p_i.reshape(*prefix, S - 1)
-        ret['visibility_weights'] = tau.reshape(*prefix, S - 1)
-        ret['d_vals'] = d_all.reshape(*prefix, S)
-        ret['sigma'] = sigma.reshape(*prefix, S)
+        radiances = rad.reshape(n, S, 3) if No == 0 else torch.cat([rad.reshape(n, S, 3), bg[1]], 1)
+        ret['radiance'] = radiances.reshape(*prefix, M, 3)
+        ret['alpha'] = (1.0 - p_i).reshape(*prefix, M - 1)
+        ret['p_i'] = p_i.reshape(*prefix, M - 1)
+        ret['visibility_weights'] = tau.reshape(*prefix, M - 1)
+        ret['d_vals'] = d_vals.reshape(*prefix, M)
+        ret['sigma'] = sigma.reshape(*prefix, M)
         ret['beta_map'] = ex['beta_map'].reshape(*prefix, 1)
         ret['iter_usage'] = ex['iter_usage'].reshape(prefix)
+        if No > 0:
+            ret['sigma_out'] = bg[0].reshape(*prefix, No)
+            ret['radiance_out'] = bg[1].reshape(*prefix, No, 3)
     return ret['rgb'], ret['depth_volume'], ret
 
 

@@ -366,48 +366,57 @@ class NeuSCompositeBG(torch.autograd.Function):
 
 class VolSDFComposite(torch.autograd.Function):
     """VolSDF's sdf_to_sigma + ray integration (volsdf.py:16-35, :480-506) with the builtin background
-    (volsdf.py:317-325), with a graph: sdf [R,S] (network values), beta [1], radiance [R,S,3]; pts
-    [R,S,3] and d_all [R,S] (no grad) -> rgb [R,3], depth [R], acc [R], visibility weights [R,S-1],
-    sdf with the background applied [R,S] (+ p_i [R,S-1], sigma [R,S], not differentiable)."""
+    (volsdf.py:317-325) or the NeRF++ background samples (volsdf.py:455-469), with a graph: sdf [R,S]
+    (network values), beta [1], radiance [R,S,3]; pts [R,S,3] and d_all [R,S] (no grad); optional
+    sig_bg [R,N], rad_bg [R,N,3] (the background net's outputs) and d_bg [R,N] -> rgb [R,3], depth [R],
+    acc [R], visibility weights [R,M-1], sdf with the background applied [R,S] (+ p_i [R,M-1],
+    sigma [R,M], not differentiable), M = S + N."""
 
     @staticmethod
-    def forward(ctx, sdf, beta, rad, pts, d_all, use_bg, r_bg, white_bkgd):
+    def forward(ctx, sdf, beta, rad, pts, d_all, use_bg, r_bg, white_bkgd, sig_bg=None, rad_bg=None, d_bg=None):
         R, S = sdf.shape
+        N = 0 if sig_bg is None else sig_bg.shape[1]
+        M = S + N
         dev = sdf.device
+        c = lambda t: None if t is None else t.contiguous()
         sdf, rad, pts, d_all = sdf.contiguous(), rad.contiguous(), pts.contiguous(), d_all.contiguous()
+        sig_bg, rad_bg, d_bg = c(sig_bg), c(rad_bg), c(d_bg)
         beta = beta.reshape(-1)[:1].float().contiguous()
         rgb = torch.empty(R, 3, device=dev)
         depth = torch.empty(R, device=dev)
         acc = torch.empty(R, device=dev)
-        tau = torch.empty(R, S - 1, device=dev)
-        p_i = torch.empty(R, S - 1, device=dev)
-        sigma = torch.empty(R, S, device=dev)
+        tau = torch.empty(R, M - 1, device=dev)
+        p_i = torch.empty(R, M - 1, device=dev)
+        sigma = torch.empty(R, M, device=dev)
         sdf_bg = torch.empty(R, S, device=dev)
-        L.check(L.lib().nr_volsdf_composite_fwd(L.ptr(sdf), L.ptr(pts), L.ptr(beta), L.ptr(rad), L.ptr(d_all), R, S,
-                                                int(use_bg), float(r_bg), int(white_bkgd), L.ptr(rgb), L.ptr(depth),
-                                                L.ptr(acc), L.ptr(tau), L.ptr(p_i), L.ptr(sigma), L.ptr(sdf_bg),
-                                                _st(sdf)))
-        ctx.cfg = (int(use_bg), float(r_bg), int(white_bkgd))
-        ctx.save_for_backward(sdf, beta, rad, pts, d_all)
+        L.check(L.lib().nr_volsdf_composite_bg_fwd(L.ptr(sdf), L.ptr(pts), L.ptr(beta), L.ptr(rad), L.ptr(d_all), R,
+                                                   S, int(use_bg), float(r_bg), int(white_bkgd), L.ptr(sig_bg),
+                                                   L.ptr(rad_bg), L.ptr(d_bg), N, L.ptr(rgb), L.ptr(depth), L.ptr(acc),
+                                                   L.ptr(tau), L.ptr(p_i), L.ptr(sigma), L.ptr(sdf_bg), _st(sdf)))
+        ctx.cfg = (int(use_bg), float(r_bg), int(white_bkgd), N)
+        ctx.save_for_backward(sdf, beta, rad, pts, d_all, sig_bg, rad_bg, d_bg)
         ctx.mark_non_differentiable(p_i, sigma)
         return rgb, depth, acc, tau, sdf_bg, p_i, sigma
 
     @staticmethod
     def backward(ctx, g_rgb, g_depth, g_acc, g_tau, g_sdf, _gp, _gs):
-        sdf, beta, rad, pts, d_all = ctx.saved_tensors
-        use_bg, r_bg, white = ctx.cfg
+        sdf, beta, rad, pts, d_all, sig_bg, rad_bg, d_bg = ctx.saved_tensors
+        use_bg, r_bg, white, N = ctx.cfg
         R, S = sdf.shape
         c = lambda t: None if t is None else t.contiguous()
         d_sdf, d_rad = torch.empty_like(sdf), torch.empty_like(rad)
         d_beta = torch.empty(R, device=sdf.device)
+        d_sig = torch.empty_like(sig_bg) if N else None
+        d_rbg = torch.empty_like(rad_bg) if N else None
         lib = L.lib()
-        wb = lib.nr_volsdf_composite_bwd_workspace_bytes(R, S)
+        wb = lib.nr_volsdf_composite_bg_bwd_workspace_bytes(R, S, N)
         ws = torch.empty(max(wb, 1), dtype=torch.uint8, device=sdf.device)
-        L.check(lib.nr_volsdf_composite_bwd(L.ptr(sdf), L.ptr(pts), L.ptr(beta), L.ptr(rad), L.ptr(d_all), R, S, use_bg,
-                                            r_bg, white, L.ptr(c(g_rgb)), L.ptr(c(g_depth)), L.ptr(c(g_acc)),
-                                            L.ptr(c(g_tau)), L.ptr(c(g_sdf)), L.ptr(d_sdf), L.ptr(d_rad),
-                                            L.ptr(d_beta), L.ptr(ws), wb, _st(sdf)))
-        return d_sdf, d_beta.sum().reshape(1), d_rad, None, None, None, None, None
+        L.check(lib.nr_volsdf_composite_bg_bwd(L.ptr(sdf), L.ptr(pts), L.ptr(beta), L.ptr(rad), L.ptr(d_all), R, S,
+                                               use_bg, r_bg, white, L.ptr(sig_bg), L.ptr(rad_bg), L.ptr(d_bg), N,
+                                               L.ptr(c(g_rgb)), L.ptr(c(g_depth)), L.ptr(c(g_acc)), L.ptr(c(g_tau)),
+                                               L.ptr(c(g_sdf)), L.ptr(d_sdf), L.ptr(d_rad), L.ptr(d_beta),
+                                               L.ptr(d_sig), L.ptr(d_rbg), L.ptr(ws), wb, _st(sdf)))
+        return (d_sdf, d_beta.sum().reshape(1), d_rad, None, None, None, None, None, d_sig, d_rbg, None)
 
 
 class UnisurfComposite(torch.autograd.Function):

@@ -76,29 +76,44 @@ def neus_train_losses(sd, rays_o, rays_d, target_rgb, target_mask, w_eikonal=0.1
 
 def volsdf_train_losses(sd, rays_o, rays_d, target_rgb, eik_points, w_eikonal=0.1, d_all=None, speed_factor=10.0,
                         obj_bounding_radius=3.0, near=0.0, far=6.0, N_samples=64, N_importance=64,
-                        max_upsample_steps=6):
+                        max_upsample_steps=6, N_outside=0):
     """losses of one VolSDF training step (models/frameworks/volsdf.py:564-640; render :415-506 with
-    a graph, builtin background sphere): L1 rgb + w_eikonal * MSE(|nabla|, 1) over the highest-weight
-    sample of each ray and one eikonal point per ray (eik_points [B, N, 1, 3], the reference's
-    uniform_(-R, R) draws).  d_all [B, N, S] optional (the sorted sample depths; from the oracle's
-    no-grad fine sampling when None)."""
+    a graph, builtin background sphere, or with N_outside > 0 the NeRF++ background :451-469 with its
+    parameters in the graph): L1 rgb + w_eikonal * MSE(|nabla|, 1) over the highest-weight sample of
+    each ray and one eikonal point per ray (eik_points [B, N, 1, 3], the reference's uniform_(-R, R)
+    draws).  d_all [B, N, S (+ N_outside)] optional (the sorted sample depths, then the background
+    depths; from the oracle's no-grad fine sampling when None).  perturb=False."""
     o = rays_o.reshape(rays_o.shape[0], -1, 3).float()
     d = F.normalize(rays_d.reshape(rays_d.shape[0], -1, 3).float(), dim=-1)
     if d_all is None:
         orc = VolSDFOracle({k: v.detach() for k, v in sd.items()}, speed_factor=speed_factor,
-                           obj_bounding_radius=obj_bounding_radius)
+                           obj_bounding_radius=obj_bounding_radius, use_nerfplusplus=N_outside > 0)
         with torch.no_grad():
             d_all = orc.render(rays_o, rays_d, near=near, far=far, calc_normal=False, N_samples=N_samples,
-                               N_importance=N_importance, max_upsample_steps=max_upsample_steps)['d_vals']
+                               N_importance=N_importance, max_upsample_steps=max_upsample_steps,
+                               N_outside=max(N_outside, 1))['d_vals']
+    S = N_samples + N_importance
+    d_in = d_all[..., :S]
     sdf_net = SDFNet(sd)
     rad_net = RadianceNet(sd, multires=-1, multires_view=-1)
-    pts = o[..., None, :] + d[..., None, :] * d_all[..., :, None]            # volsdf.py:446
+    pts = o[..., None, :] + d[..., None, :] * d_in[..., :, None]             # volsdf.py:446
     sdf, nablas, h = nablas_graph(sdf_net, pts)                               # volsdf.py:450, :317-325
-    d_bg = obj_bounding_radius - pts.norm(dim=-1)
-    sdf = torch.where(d_bg < sdf, d_bg, sdf)
+    if N_outside == 0:
+        d_bg = obj_bounding_radius - pts.norm(dim=-1)
+        sdf = torch.where(d_bg < sdf, d_bg, sdf)
     rad = rad_net.forward(pts, d.unsqueeze(-2).expand_as(pts), nablas, h)
     beta = torch.exp(sd['ln_beta'] * speed_factor)                            # volsdf.py:306-308
     sigma = sdf_to_sigma(sdf, 1. / beta, beta)
+    if N_outside > 0:                                                         # volsdf.py:455-469
+        B, N = o.shape[:2]
+        t_out = torch.linspace(0, 1, N_outside + 2)[..., 1:-1].float()
+        rs = (obj_bounding_radius / torch.flip(t_out, dims=[-1])).expand([B, N, N_outside])
+        d_out = d_all[..., S:]
+        pts_out = o[..., None, :] + d[..., None, :] * d_out[..., :, None]
+        x_out = torch.cat([pts_out / rs[..., None], 1. / rs[..., None]], dim=-1)
+        sigma_out, rad_out = NeRFNet(sd).forward(x_out, d.unsqueeze(-2).expand_as(pts_out))
+        sigma = torch.cat([sigma, sigma_out], -1)
+        rad = torch.cat([rad, rad_out], -2)
     delta = d_all[..., 1:] - d_all[..., :-1]                                  # volsdf.py:482-495
     p = torch.exp(-F.relu(sigma[..., :-1] * delta))
     tau = (1 - p + 1e-10) * torch.cumprod(torch.cat([torch.ones_like(p[..., :1]), p], -1), -1)[..., :-1]

@@ -630,16 +630,23 @@ def _gen_train(R, name, seed, N_outside):
 
 def gen_train_volsdf(R):
     """One VolSDF training step (models/frameworks/volsdf.py:564-640 -> train.py:205 backward) on an
-    8x8 camera (64 rays, N_rays=-1), builtin background, 64 + 64 samples, 6 upsampling rounds,
+    8x8 camera (64 rays, N_rays=-1), builtin background (volsdf_train.npz) or the NeRF++ background
+    with 32 outside samples (volsdf_train_nerfpp.npz), 64 + 64 samples, 6 upsampling rounds,
     perturb=False, seeded random targets; the eikonal points (torch's uniform_(-3, 3), volsdf.py:609)
     are recorded from the reference's own call so the GPU test can replay them."""
+    _gen_train_volsdf(R, 'volsdf_train.npz', 3, False, 20.0)
+    # wide field of view: a third of the rays miss the surface, so the background net gets gradients
+    _gen_train_volsdf(R, 'volsdf_train_nerfpp.npz', 7, True, 5.0)
+
+
+def _gen_train_volsdf(R, name, seed, nerfpp, f):
     import types as _t
-    sd = wg.volsdf_state(seed=3, beta_init=0.1)
-    model = _volsdf_model(R, sd, 0.1)
+    sd = wg.volsdf_state(seed=seed, beta_init=0.1, use_nerfplusplus=nerfpp)
+    model = _volsdf_model(R, sd, 0.1, use_nerfplusplus=nerfpp)
     model.train()
     H = W = 8
     c2w = wg.look_at_c2w(2.7)[None]
-    K = wg.intrinsics(20.0, H, W)[None]
+    K = wg.intrinsics(f, H, W)[None]
     g = torch.Generator().manual_seed(6)
     target_rgb = torch.rand(1, H * W, 3, generator=g)
     seen = []
@@ -652,7 +659,7 @@ def gen_train_volsdf(R):
     args = _t.SimpleNamespace(data=_t.SimpleNamespace(N_rays=-1), model=_t.SimpleNamespace(obj_bounding_radius=3.0),
                               training=_t.SimpleNamespace(w_eikonal=0.1))
     kw = dict(H=H, W=W, near=0.0, far=6.0, obj_bounding_radius=3.0, batched=True, perturb=False, white_bkgd=False,
-              max_upsample_steps=6, use_nerfplusplus=False, N_samples=64, N_importance=64)
+              max_upsample_steps=6, use_nerfplusplus=nerfpp, N_samples=64, N_importance=64, N_outside=32)
     trainer = R.volsdf.Trainer(model, device_ids=[0], batched=True)
     trainer.device = 'cpu'
     torch.manual_seed(9)
@@ -661,7 +668,7 @@ def gen_train_volsdf(R):
     model.zero_grad()
     losses['total'].backward()
     ex = ret['extras']
-    save('volsdf_train.npz', seed=3, beta_init=0.1, H=H, W=W, f=20.0, dist=2.7, target_rgb=target_rgb, c2w=c2w, K=K,
+    save(name, seed=seed, beta_init=0.1, nerfpp=nerfpp, H=H, W=W, f=f, dist=2.7, target_rgb=target_rgb, c2w=c2w, K=K,
          eik_points=seen[-1], **{f'loss/{k}': v.detach() for k, v in losses.items()},
          rgb=ex['rgb'].detach(), d_vals=ex['d_vals'].detach(), iter_usage=ex['iter_usage'].detach(),
          **_grad_summary(model.named_parameters()))
@@ -682,7 +689,7 @@ def gen_train_unisurf(R):
     H = W = 8
     c2w = wg.look_at_c2w(2.7)[None]
     c2w[0, 0, 3] += 0.0137
-    K = wg.intrinsics(20.0, H, W)[None]
+    K = wg.intrinsics(f, H, W)[None]
     g = torch.Generator().manual_seed(8)
     target_rgb = torch.rand(1, H * W, 3, generator=g)
     args = _t.SimpleNamespace(data=_t.SimpleNamespace(N_rays=-1),
@@ -701,7 +708,7 @@ def gen_train_unisurf(R):
     losses['total'].backward()
     ex = ret['extras']
     surf_perturb = (rr.draws[0] - 0.5) * 2. * 0.01
-    save('unisurf_train.npz', seed=3, H=H, W=W, f=20.0, dist=2.7, target_rgb=target_rgb, c2w=c2w, K=K,
+    save('unisurf_train.npz', seed=3, H=H, W=W, f=f, dist=2.7, target_rgb=target_rgb, c2w=c2w, K=K,
          logit_tau=logit_tau, rand_draw=rr.draws[0], surf_perturb=surf_perturb,
          **{f'loss/{k}': v.detach() for k, v in losses.items()}, rgb=ex['rgb'].detach(),
          surface_points=ex['surface_points'].detach(), mask_surface=ex['mask_surface'].detach(),

@@ -108,8 +108,9 @@ def test_neus_train_step_vs_oracle_and_golden(golden, precision, name):
         print(f'{precision}: sample depths match the reference (1e-6) -> gradients checked against the golden too')
 
 
+@pytest.mark.parametrize('name', ['volsdf_train', 'volsdf_train_nerfpp'])
 @pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
-def test_volsdf_train_step_vs_oracle_and_golden(golden, precision, monkeypatch):
+def test_volsdf_train_step_vs_oracle_and_golden(golden, precision, name, monkeypatch):
     """VolSDF's training step (volsdf.py:564-640): losses and every parameter gradient -- surface net
     through the double backward of the nablas, radiance net, ln_beta through sdf_to_sigma -- vs the
     oracle on the GPU's sample depths, and vs the reference's golden when the depths agree.  The
@@ -120,18 +121,21 @@ def test_volsdf_train_step_vs_oracle_and_golden(golden, precision, monkeypatch):
     (tools/train_sensitivity.py volsdf_train; radiance ReLUs at their kink flip).  Measured here: 1.0e-4
     (fp32 sample pass) and 1.8e-6 (f16x3 sample pass: other depths, no ReLU near its kink)."""
     from neurecon_amd.frameworks import volsdf as V
-    g = golden('volsdf_train')
+    g = golden(name)
+    nerfpp = bool(g['nerfpp']) if 'nerfpp' in g else False
     T = lambda a: torch.from_numpy(np.asarray(a)).cuda()
     eik = T(g['eik_points'])
     monkeypatch.setattr(V, 'eikonal_points', lambda like, bound: eik.reshape(like.shape).to(like.dtype))
     beta0 = float(g['beta_init'])
-    m = volsdf_model(wg.volsdf_state(seed=int(g['seed']), beta_init=beta0), beta0, precision=precision)
+    m = volsdf_model(wg.volsdf_state(seed=int(g['seed']), beta_init=beta0, use_nerfplusplus=nerfpp), beta0,
+                     precision=precision, use_nerfplusplus=nerfpp)
     m.train()
     args = types.SimpleNamespace(data=types.SimpleNamespace(N_rays=-1),
                                  model=types.SimpleNamespace(obj_bounding_radius=3.0),
                                  training=types.SimpleNamespace(w_eikonal=0.1))
     kw = dict(H=int(g['H']), W=int(g['W']), near=0.0, far=6.0, obj_bounding_radius=3.0, batched=True, perturb=False,
-              white_bkgd=False, max_upsample_steps=6, use_nerfplusplus=False, N_samples=64, N_importance=64)
+              white_bkgd=False, max_upsample_steps=6, use_nerfplusplus=nerfpp, N_samples=64, N_importance=64,
+              N_outside=32)
     ret = V.Trainer(m, device_ids=[0]).forward(args, None, {'intrinsics': T(g['K']), 'c2w': T(g['c2w'])},
                                                {'rgb': T(g['target_rgb'])}, kw, 0, device='cuda')
     losses = {k: torch.mean(v) for k, v in ret['losses'].items()}

@@ -355,20 +355,24 @@ def test_oracle_train_step_vs_golden(golden, name):
 def volsdf_train_grads_oracle(g, d_all=None):
     """oracle/train.py on the volsdf_train fixture: (losses, {param: grad}, d_all)"""
     from oracle.train import volsdf_train_losses
+    nerfpp = bool(g['nerfpp']) if 'nerfpp' in g else False
     sd = {k: v.clone().requires_grad_(v.is_floating_point() and k != 'implicit_surface.obj_bounding_size')
-          for k, v in wg.volsdf_state(seed=int(g['seed']), beta_init=float(g['beta_init'])).items()}
+          for k, v in wg.volsdf_state(seed=int(g['seed']), beta_init=float(g['beta_init']),
+                                      use_nerfplusplus=nerfpp).items()}
     H, W = int(g['H']), int(g['W'])
     ro, rd, _ = rays.get_rays(T(g['c2w']), T(g['K']), H, W)
-    losses, d_all = volsdf_train_losses(sd, ro, rd, T(g['target_rgb']), T(g['eik_points']), d_all=d_all)
+    losses, d_all = volsdf_train_losses(sd, ro, rd, T(g['target_rgb']), T(g['eik_points']), d_all=d_all,
+                                        N_outside=32 if nerfpp else 0)
     losses['total'].backward()
     return losses, {k: v.grad for k, v in sd.items() if v.grad is not None}, d_all
 
 
-def test_oracle_volsdf_train_step_vs_golden(golden):
+@pytest.mark.parametrize('name', ['volsdf_train', 'volsdf_train_nerfpp'])
+def test_oracle_volsdf_train_step_vs_golden(golden, name):
     """the oracle's VolSDF training losses and every parameter gradient (surface net through the
-    double backward of the nablas, radiance net, ln_beta) vs the reference's own Trainer.forward +
-    backward on the same rays, targets and eikonal points"""
-    g = golden('volsdf_train')
+    double backward of the nablas, radiance net, ln_beta; with the NeRF++ background its net too) vs
+    the reference's own Trainer.forward + backward on the same rays, targets and eikonal points"""
+    g = golden(name)
     torch.set_num_threads(8)
     losses, grads, d_all = volsdf_train_grads_oracle(g)
     close(d_all, g['d_vals'], 1e-6, 1e-6)
