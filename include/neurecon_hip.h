@@ -441,6 +441,12 @@ int nr_scale_cols(const float* a, int64_t P, int lda, int col0, int ncols, const
                   void* stream);
 int nr_softplus_adjoint(const float* hbar, int ldh, const float* s, const float* g, const float* zdot, int64_t P,
                         int n, float* zbar, void* stream);
+/* SirenLayer activation (base.py:84-115) in the training path: h = sin(30 z), s = 30 cos(30 z); and
+ * the layer's adjoint in the double backward, zbar = hbar * s + g * zdot * (-900 h) (g / zdot optional,
+ * as nr_softplus_adjoint) */
+int nr_sine30(const float* z, int64_t n, float* h, float* s, void* stream);
+int nr_sine_adjoint(const float* hbar, int ldh, const float* s, const float* h, const float* g, const float* zdot,
+                    int64_t P, int n, float* zbar, void* stream);
 int nr_mul(const float* a, const float* b, int64_t n, float* out, void* stream);
 /* mode 0: y = relu(y); 1: g *= (y > 0); 2: y = sigmoid(y); 3: g *= y (1 - y) */
 int nr_activation(float* y, float* g, int64_t n, int mode, void* stream);

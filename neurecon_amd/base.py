@@ -10,6 +10,7 @@ import math
 import numpy as np
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from . import _lib as L
 
@@ -234,9 +235,6 @@ class ImplicitSurface(nn.Module):
         L.require_gpu(x, 'points')
         shape = x.shape[:-1]
         if wants_graph(self):  # training: differentiable sdf / nablas / feature (double backward)
-            if self.use_siren:
-                raise NotImplementedError('neurecon_amd: the training (autograd) path covers the softplus SDF net; '
-                                          'SIREN nets render (no_grad) only')
             from .training import sdf_nablas
             sdf, nab, feat = sdf_nablas(self, x, True)
             return [sdf.reshape(shape), nab.reshape(*shape, 3), feat.reshape(*shape, self.W_geo_feat)]
@@ -269,7 +267,35 @@ class ImplicitSurface(nn.Module):
         return sdf, nab, h
 
     def pretrain_hook(self, configs={}):
+        """base.py:226-233: a geometric-init SIREN net is pretrained to a sphere once (is_pretrained)."""
+        configs['target_radius'] = self.radius_init
+        configs['obj_bounding_size'] = float(self.obj_bounding_size.reshape(-1)[0])
+        if self.geometric_init and self.use_siren and not bool(self.is_pretrained):
+            pretrain_siren_sdf(self, **configs)
+            self.is_pretrained = ~self.is_pretrained
+            return True
         return False
+
+
+def pretrain_siren_sdf(implicit_surface, num_iters=5000, lr=1.0e-4, batch_points=5000, target_radius=0.5,
+                       obj_bounding_size=3.0, logger=None):
+    """base.py:284-310: fit the SIREN SDF to |x| - target_radius (L1, Adam) on uniform points in the
+    bounding cube, drawn on the CPU as the reference does; the forward and its gradient run on the
+    training path's HIP kernels and hipBLASLt GEMMs (neurecon_amd.training)."""
+    from torch import optim
+    device = next(implicit_surface.parameters()).device
+    optimizer = optim.Adam(implicit_surface.parameters(), lr=lr)
+    with torch.enable_grad():
+        for it in range(num_iters):
+            pts = torch.empty([batch_points, 3]).uniform_(-obj_bounding_size, obj_bounding_size).float().to(device)
+            sdf_gt = pts.norm(dim=-1) - target_radius
+            sdf_pred = implicit_surface.forward(pts)
+            loss = F.l1_loss(sdf_pred, sdf_gt, reduction='mean')
+            optimizer.zero_grad()
+            loss.backward()
+            optimizer.step()
+            if logger is not None:
+                logger.add('pretrain_siren', 'loss_l1', loss.item(), it)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -338,8 +364,6 @@ class RadianceNet(nn.Module):
         else:  # view dirs and normals are not inputs (base.py:383-384)
             v = n = None
         if wants_graph(self, normals, geometry_feature):
-            if self.use_siren or self.D != 4:
-                raise NotImplementedError('neurecon_amd: the training (autograd) path covers the D=4 ReLU radiance net')
             from .training import radiance
             rgb = radiance(self, x.reshape(-1, 3).float(), v, n, geometry_feature.reshape(-1, self.W_geo_feat).float())
             return rgb.reshape(*shape, 3)

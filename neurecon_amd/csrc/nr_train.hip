@@ -133,6 +133,28 @@ __global__ void softplus_adjoint_kernel(const float* __restrict__ hbar, int ldh,
   zbar[i] = v;
 }
 
+// SirenLayer activation (base.py:84-115): h = sin(30 z), s = dh/dz = 30 cos(30 z)
+__global__ void sine30_kernel(const float* __restrict__ z, int64_t n, float* __restrict__ h, float* __restrict__ s) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float a = fmul(30.0f, z[i]);
+  h[i] = sinf(a);
+  s[i] = fmul(30.0f, cosf(a));
+}
+
+// the softplus_adjoint_kernel of a sine layer: d2 = ds/dz = -900 sin(30 z) = -900 h
+__global__ void sine_adjoint_kernel(const float* __restrict__ hbar, int ldh, const float* __restrict__ s,
+                                    const float* __restrict__ h, const float* __restrict__ g,
+                                    const float* __restrict__ zdot, int64_t P, int n, float* __restrict__ zbar) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P * n) return;
+  const int64_t p = i / n;
+  const int j = (int)(i - p * n);
+  float v = fmul(hbar[p * ldh + j], s[i]);
+  if (g) v = fadd(v, fmul(fmul(g[i], zdot[i]), fmul(-900.0f, h[i])));
+  zbar[i] = v;
+}
+
 __global__ void mul_kernel(const float* __restrict__ a, const float* __restrict__ b, int64_t n, float* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = fmul(a[i], b[i]);
@@ -893,6 +915,25 @@ int nr_softplus_adjoint(const float* hbar, int ldh, const float* s, const float*
              "nr_softplus_adjoint: bad argument");
   if (P == 0 || n == 0) return NR_OK;
   hipLaunchKernelGGL(softplus_adjoint_kernel, grid1(P * n), dim3(kBlk), 0, (hipStream_t)stream, hbar, ldh, s, g, zdot,
+                     P, n, zbar);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_sine30(const float* z, int64_t n, float* h, float* s, void* stream) {
+  NR_REQUIRE(z && h && s && n >= 0, NR_ERR_ARG, "nr_sine30: bad argument");
+  if (n == 0) return NR_OK;
+  hipLaunchKernelGGL(sine30_kernel, grid1(n), dim3(kBlk), 0, (hipStream_t)stream, z, n, h, s);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int nr_sine_adjoint(const float* hbar, int ldh, const float* s, const float* h, const float* g, const float* zdot,
+                    int64_t P, int n, float* zbar, void* stream) {
+  NR_REQUIRE(hbar && s && h && zbar && P >= 0 && n >= 1 && ldh >= n && (!g || zdot), NR_ERR_ARG,
+             "nr_sine_adjoint: bad argument");
+  if (P == 0) return NR_OK;
+  hipLaunchKernelGGL(sine_adjoint_kernel, grid1(P * n), dim3(kBlk), 0, (hipStream_t)stream, hbar, ldh, s, h, g, zdot,
                      P, n, zbar);
   NR_LAUNCH_CHECK();
   return NR_OK;

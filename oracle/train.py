@@ -76,26 +76,31 @@ def neus_train_losses(sd, rays_o, rays_d, target_rgb, target_mask, w_eikonal=0.1
 
 def volsdf_train_losses(sd, rays_o, rays_d, target_rgb, eik_points, w_eikonal=0.1, d_all=None, speed_factor=10.0,
                         obj_bounding_radius=3.0, near=0.0, far=6.0, N_samples=64, N_importance=64,
-                        max_upsample_steps=6, N_outside=0):
+                        max_upsample_steps=6, N_outside=0, siren=False):
     """losses of one VolSDF training step (models/frameworks/volsdf.py:564-640; render :415-506 with
     a graph, builtin background sphere, or with N_outside > 0 the NeRF++ background :451-469 with its
     parameters in the graph): L1 rgb + w_eikonal * MSE(|nabla|, 1) over the highest-weight sample of
     each ray and one eikonal point per ray (eik_points [B, N, 1, 3], the reference's uniform_(-R, R)
     draws).  d_all [B, N, S (+ N_outside)] optional (the sorted sample depths, then the background
-    depths; from the oracle's no-grad fine sampling when None).  perturb=False."""
+    depths; from the oracle's no-grad fine sampling when None).  perturb=False.  siren: the nets of
+    configs/volsdf_siren.yaml (SirenLayers, D=5, identity embedding, view embedding 4)."""
     o = rays_o.reshape(rays_o.shape[0], -1, 3).float()
     d = F.normalize(rays_d.reshape(rays_d.shape[0], -1, 3).float(), dim=-1)
     if d_all is None:
         orc = VolSDFOracle({k: v.detach() for k, v in sd.items()}, speed_factor=speed_factor,
-                           obj_bounding_radius=obj_bounding_radius, use_nerfplusplus=N_outside > 0)
+                           obj_bounding_radius=obj_bounding_radius, use_nerfplusplus=N_outside > 0, siren=siren)
         with torch.no_grad():
             d_all = orc.render(rays_o, rays_d, near=near, far=far, calc_normal=False, N_samples=N_samples,
                                N_importance=N_importance, max_upsample_steps=max_upsample_steps,
                                N_outside=max(N_outside, 1))['d_vals']
     S = N_samples + N_importance
     d_in = d_all[..., :S]
-    sdf_net = SDFNet(sd)
-    rad_net = RadianceNet(sd, multires=-1, multires_view=-1)
+    if siren:
+        sdf_net = SDFNet(sd, D=5, skips=(), multires=-1, siren=True)
+        rad_net = RadianceNet(sd, D=5, multires=-1, multires_view=4, siren=True)
+    else:
+        sdf_net = SDFNet(sd)
+        rad_net = RadianceNet(sd, multires=-1, multires_view=-1)
     pts = o[..., None, :] + d[..., None, :] * d_in[..., :, None]             # volsdf.py:446
     sdf, nablas, h = nablas_graph(sdf_net, pts)                               # volsdf.py:450, :317-325
     if N_outside == 0:

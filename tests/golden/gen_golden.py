@@ -637,12 +637,23 @@ def gen_train_volsdf(R):
     _gen_train_volsdf(R, 'volsdf_train.npz', 3, False, 20.0)
     # wide field of view: a third of the rays miss the surface, so the background net gets gradients
     _gen_train_volsdf(R, 'volsdf_train_nerfpp.npz', 7, True, 5.0)
+    # configs/volsdf_siren.yaml's nets (SirenLayers, D=5, weights as in gen_siren)
+    _gen_train_volsdf(R, 'volsdf_train_siren.npz', 7, False, 20.0, siren=True)
 
 
-def _gen_train_volsdf(R, name, seed, nerfpp, f):
+def _gen_train_volsdf(R, name, seed, nerfpp, f, siren=False):
     import types as _t
-    sd = wg.volsdf_state(seed=seed, beta_init=0.1, use_nerfplusplus=nerfpp)
-    model = _volsdf_model(R, sd, 0.1, use_nerfplusplus=nerfpp)
+    if siren:
+        sd = wg.volsdf_siren_state(seed=seed)
+        surf_cfg = dict(use_siren=True, D=5, W=256, skips=[], embed_multires=-1, radius_init=1.0, geometric_init=True)
+        rad_cfg = dict(use_siren=True, D=5, W=256, skips=[], embed_multires=-1, embed_multires_view=4,
+                       use_view_dirs=True)
+        model = R.volsdf.VolSDF(beta_init=0.1, speed_factor=10.0, input_ch=3, W_geo_feat=256, obj_bounding_radius=3.0,
+                                use_nerfplusplus=False, surface_cfg=surf_cfg, radiance_cfg=rad_cfg)
+        model.load_state_dict(sd)
+    else:
+        sd = wg.volsdf_state(seed=seed, beta_init=0.1, use_nerfplusplus=nerfpp)
+        model = _volsdf_model(R, sd, 0.1, use_nerfplusplus=nerfpp)
     model.train()
     H = W = 8
     c2w = wg.look_at_c2w(2.7)[None]
@@ -668,7 +679,7 @@ def _gen_train_volsdf(R, name, seed, nerfpp, f):
     model.zero_grad()
     losses['total'].backward()
     ex = ret['extras']
-    save(name, seed=seed, beta_init=0.1, nerfpp=nerfpp, H=H, W=W, f=f, dist=2.7, target_rgb=target_rgb, c2w=c2w, K=K,
+    save(name, seed=seed, beta_init=0.1, nerfpp=nerfpp, siren=siren, H=H, W=W, f=f, dist=2.7, target_rgb=target_rgb, c2w=c2w, K=K,
          eik_points=seen[-1], **{f'loss/{k}': v.detach() for k, v in losses.items()},
          rgb=ex['rgb'].detach(), d_vals=ex['d_vals'].detach(), iter_usage=ex['iter_usage'].detach(),
          **_grad_summary(model.named_parameters()))

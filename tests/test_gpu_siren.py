@@ -72,3 +72,42 @@ def test_siren_volsdf_render_vs_golden(golden, precision):
     print(f'siren/{precision}: identical samples on {same.mean() * 100:.1f}% of rays, per-ray pass {ok.mean() * 100:.1f}%')
     assert ok[same].all() and ok_n[same].all()
     assert ok.mean() >= 0.95
+
+
+def test_siren_pretrain_hook_vs_oracle():
+    """ImplicitSurface.pretrain_hook / pretrain_siren_sdf (base.py:226-233, :284-310): the L1 sphere fit
+    with Adam, its forward and gradient on the training path -- 4 steps of 2048 points vs the same
+    steps on the oracle network (torch CPU autograd + Adam) from the same CPU draws: losses within
+    1e-4 relative, is_pretrained set once."""
+    from oracle.nets import SDFNet
+    from neurecon_amd.base import pretrain_siren_sdf
+    m = siren_model('fp32')
+    surf = m.implicit_surface.train()
+    sd = {k: v.clone().float().requires_grad_(True) for k, v in wg.volsdf_siren_state(seed=7).items()
+          if k.startswith('implicit_surface.surface_fc_layers')}
+
+    class Log:
+        def __init__(self):
+            self.v = []
+
+        def add(self, a, b, val, it):
+            self.v.append(val)
+    log = Log()
+    torch.manual_seed(5)
+    pretrain_siren_sdf(surf, num_iters=4, batch_points=2048, target_radius=1.0, obj_bounding_size=3.0, logger=log)
+    torch.manual_seed(5)
+    opt = torch.optim.Adam(list(sd.values()), lr=1e-4)
+    ref = []
+    for _ in range(4):
+        pts = torch.empty([2048, 3]).uniform_(-3.0, 3.0).float()
+        net = SDFNet(sd, D=5, skips=(), multires=-1, siren=True)
+        loss = torch.nn.functional.l1_loss(net.sdf(pts), pts.norm(dim=-1) - 1.0)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        ref.append(float(loss))
+    print('pretrain losses gpu', log.v, 'oracle', ref)
+    assert np.allclose(log.v, ref, rtol=1e-4, atol=0)
+    surf.is_pretrained.fill_(False)
+    assert surf.pretrain_hook({'num_iters': 1, 'batch_points': 64}) is True
+    assert bool(surf.is_pretrained) and surf.pretrain_hook({'num_iters': 1}) is False

@@ -108,7 +108,7 @@ def test_neus_train_step_vs_oracle_and_golden(golden, precision, name):
         print(f'{precision}: sample depths match the reference (1e-6) -> gradients checked against the golden too')
 
 
-@pytest.mark.parametrize('name', ['volsdf_train', 'volsdf_train_nerfpp'])
+@pytest.mark.parametrize('name', ['volsdf_train', 'volsdf_train_nerfpp', 'volsdf_train_siren'])
 @pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
 def test_volsdf_train_step_vs_oracle_and_golden(golden, precision, name, monkeypatch):
     """VolSDF's training step (volsdf.py:564-640): losses and every parameter gradient -- surface net
@@ -127,8 +127,12 @@ def test_volsdf_train_step_vs_oracle_and_golden(golden, precision, name, monkeyp
     eik = T(g['eik_points'])
     monkeypatch.setattr(V, 'eikonal_points', lambda like, bound: eik.reshape(like.shape).to(like.dtype))
     beta0 = float(g['beta_init'])
-    m = volsdf_model(wg.volsdf_state(seed=int(g['seed']), beta_init=beta0, use_nerfplusplus=nerfpp), beta0,
-                     precision=precision, use_nerfplusplus=nerfpp)
+    if 'siren' in g and bool(g['siren']):  # configs/volsdf_siren.yaml's nets
+        from test_gpu_siren import siren_model
+        m = siren_model(precision)
+    else:
+        m = volsdf_model(wg.volsdf_state(seed=int(g['seed']), beta_init=beta0, use_nerfplusplus=nerfpp), beta0,
+                         precision=precision, use_nerfplusplus=nerfpp)
     m.train()
     args = types.SimpleNamespace(data=types.SimpleNamespace(N_rays=-1),
                                  model=types.SimpleNamespace(obj_bounding_radius=3.0),

@@ -356,18 +356,20 @@ def volsdf_train_grads_oracle(g, d_all=None):
     """oracle/train.py on the volsdf_train fixture: (losses, {param: grad}, d_all)"""
     from oracle.train import volsdf_train_losses
     nerfpp = bool(g['nerfpp']) if 'nerfpp' in g else False
+    siren = bool(g['siren']) if 'siren' in g else False
+    state = wg.volsdf_siren_state(seed=int(g['seed'])) if siren else \
+        wg.volsdf_state(seed=int(g['seed']), beta_init=float(g['beta_init']), use_nerfplusplus=nerfpp)
     sd = {k: v.clone().requires_grad_(v.is_floating_point() and k != 'implicit_surface.obj_bounding_size')
-          for k, v in wg.volsdf_state(seed=int(g['seed']), beta_init=float(g['beta_init']),
-                                      use_nerfplusplus=nerfpp).items()}
+          for k, v in state.items()}
     H, W = int(g['H']), int(g['W'])
     ro, rd, _ = rays.get_rays(T(g['c2w']), T(g['K']), H, W)
     losses, d_all = volsdf_train_losses(sd, ro, rd, T(g['target_rgb']), T(g['eik_points']), d_all=d_all,
-                                        N_outside=32 if nerfpp else 0)
+                                        N_outside=32 if nerfpp else 0, siren=siren)
     losses['total'].backward()
     return losses, {k: v.grad for k, v in sd.items() if v.grad is not None}, d_all
 
 
-@pytest.mark.parametrize('name', ['volsdf_train', 'volsdf_train_nerfpp'])
+@pytest.mark.parametrize('name', ['volsdf_train', 'volsdf_train_nerfpp', 'volsdf_train_siren'])
 def test_oracle_volsdf_train_step_vs_golden(golden, name):
     """the oracle's VolSDF training losses and every parameter gradient (surface net through the
     double backward of the nablas, radiance net, ln_beta; with the NeRF++ background its net too) vs
