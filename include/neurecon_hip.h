@@ -441,6 +441,10 @@ int nr_scale_cols(const float* a, int64_t P, int lda, int col0, int ncols, const
                   void* stream);
 int nr_softplus_adjoint(const float* hbar, int ldh, const float* s, const float* g, const float* zdot, int64_t P,
                         int n, float* zbar, void* stream);
+/* column sums of a row-major [P, n] fp32 matrix (the training path's bias gradients), deterministic
+ * two-pass reduction; workspace nr_colsum_workspace_bytes(n) */
+size_t nr_colsum_workspace_bytes(int n);
+int nr_colsum(const float* a, int64_t P, int n, float* out, void* workspace, size_t workspace_bytes, void* stream);
 /* SirenLayer activation (base.py:84-115) in the training path: h = sin(30 z), s = 30 cos(30 z); and
  * the layer's adjoint in the double backward, zbar = hbar * s + g * zdot * (-900 h) (g / zdot optional,
  * as nr_softplus_adjoint) */

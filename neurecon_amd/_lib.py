@@ -150,6 +150,8 @@ _SIGS = {
     'nr_softplus100': (_c_i, [_c_p, _c_i64, _c_p, _c_p, _c_p]),
     'nr_scale_cols': (_c_i, [_c_p, _c_i64, _c_i, _c_i, _c_i, _c_p, _c_f, _c_p, _c_p]),
     'nr_softplus_adjoint': (_c_i, [_c_p, _c_i, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_p, _c_p]),
+    'nr_colsum_workspace_bytes': (_c_sz, [_c_i]),
+    'nr_colsum': (_c_i, [_c_p, _c_i64, _c_i, _c_p, _c_p, _c_sz, _c_p]),
     'nr_sine30': (_c_i, [_c_p, _c_i64, _c_p, _c_p, _c_p]),
     'nr_sine_adjoint': (_c_i, [_c_p, _c_i, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_p, _c_p]),
     'nr_mul': (_c_i, [_c_p, _c_p, _c_i64, _c_p, _c_p]),

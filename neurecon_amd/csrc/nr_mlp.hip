@@ -2449,15 +2449,18 @@ __global__ void maxabs_kernel(const float* __restrict__ W, int64_t n, float scal
 
 // bound[0] = max over packed output rows of sum_k |W * scale| (row L1 norm of the op's effective
 // matrix), bound[1] = max |bias|; one thread per output row (bound zeroed beforehand)
+// one wave per packed output row (the row's KB x 16 inputs strided over the lanes, then a wave sum):
+// the packing runs every optimizer step in training, where a thread per row took ~85 us per op
 __global__ void bound_kernel(PackOp op, unsigned* __restrict__ bound) {
   const int KB = op.in[0].nblk + op.in[1].nblk;
   const int NBO = op.out[0].nblk + op.out[1].nblk;
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  const int r = blockIdx.x;
   if (r >= NBO * 16) return;
   const int ob = r >> 4, i = r & 15;
   float s = 0.0f;
-  for (int b = 0; b < KB; ++b)
-    for (int fi = 0; fi < 16; ++fi) s += fabsf(pack_src(op, ob, i, b, fi));
+  for (int e = threadIdx.x; e < KB * 16; e += 64) s += fabsf(pack_src(op, ob, i, e >> 4, e & 15));
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (threadIdx.x != 0) return;
   float bb = 0.0f;
   if (op.bias) {
     int ob_loc = ob;
@@ -2494,7 +2497,7 @@ int launch_pack_op(const PackOp& op, char* dst, hipStream_t stream) {
   }
   if (op.bound) {
     NR_HIP_CHECK(hipMemsetAsync(op.bound, 0, 2 * sizeof(float), stream));
-    hipLaunchKernelGGL(bound_kernel, dim3((NBO * 16 + 63) / 64), dim3(64), 0, stream, op, (unsigned*)op.bound);
+    hipLaunchKernelGGL(bound_kernel, dim3(NBO * 16), dim3(64), 0, stream, op, (unsigned*)op.bound);
     NR_HIP_CHECK(hipGetLastError());
   }
   const int64_t n = (int64_t)(NBO / 2) * (2 * KB + 1) * 256;

@@ -133,6 +133,42 @@ __global__ void softplus_adjoint_kernel(const float* __restrict__ hbar, int ldh,
   zbar[i] = v;
 }
 
+// column sums of a row-major [P, n] gradient (bias gradients): block b sums its slab of rows per column
+// (threads across columns: coalesced rows), then one thread per column sums the kColBlocks partials
+constexpr int kColBlocks = 1024;
+__global__ void colsum_partial_kernel(const float* __restrict__ a, int64_t P, int n, float* __restrict__ part) {
+  const int64_t rows = (P + kColBlocks - 1) / kColBlocks;
+  const int64_t r0 = (int64_t)blockIdx.x * rows, r1 = r0 + rows < P ? r0 + rows : P;
+  for (int c = threadIdx.x; c < n; c += blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 loads in flight per thread
+    int64_t r = r0;
+    for (; r + 8 <= r1; r += 8)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += a[(r + k) * n + c];
+    for (; r < r1; ++r) acc[0] += a[r * n + c];
+    part[(int64_t)blockIdx.x * n + c] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  }
+}
+// 1024 threads per 64 columns: 16 partial-row groups per column (64 partials each, 8 loads in
+// flight), combined through LDS in a fixed order
+__global__ void colsum_final_kernel(const float* __restrict__ part, int n, float* __restrict__ out) {
+  __shared__ float red[16][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < n)
+    for (int b = grp * (kColBlocks / 16); b < (grp + 1) * (kColBlocks / 16); b += 8)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += part[(int64_t)(b + k) * n + c];
+  red[grp][cl] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (grp == 0 && c < n) {
+    float t = 0.0f;
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    out[c] = t;
+  }
+}
+
 // SirenLayer activation (base.py:84-115): h = sin(30 z), s = dh/dz = 30 cos(30 z)
 __global__ void sine30_kernel(const float* __restrict__ z, int64_t n, float* __restrict__ h, float* __restrict__ s) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -916,6 +952,20 @@ int nr_softplus_adjoint(const float* hbar, int ldh, const float* s, const float*
   if (P == 0 || n == 0) return NR_OK;
   hipLaunchKernelGGL(softplus_adjoint_kernel, grid1(P * n), dim3(kBlk), 0, (hipStream_t)stream, hbar, ldh, s, g, zdot,
                      P, n, zbar);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+size_t nr_colsum_workspace_bytes(int n) { return (size_t)kColBlocks * (size_t)(n > 0 ? n : 1) * sizeof(float); }
+
+int nr_colsum(const float* a, int64_t P, int n, float* out, void* workspace, size_t workspace_bytes, void* stream) {
+  NR_REQUIRE(a && out && P >= 0 && n >= 1, NR_ERR_ARG, "nr_colsum: bad argument");
+  NR_REQUIRE(workspace && workspace_bytes >= nr_colsum_workspace_bytes(n), NR_ERR_WORKSPACE,
+             "nr_colsum: workspace too small");
+  float* part = (float*)workspace;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(kColBlocks), dim3(256), 0, (hipStream_t)stream, a, P, n, part);
+  NR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((n + 63) / 64), dim3(1024), 0, (hipStream_t)stream, part, n, out);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
