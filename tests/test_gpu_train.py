@@ -337,7 +337,33 @@ def _free_port():
     return p
 
 
-def _ddp_worker(rank, ws, port, q):
+def _ddp_setup(fw):
+    """(model, Trainer class, args, render kwargs, golden) of one framework's 8x8 training fixture"""
+    here = os.path.dirname(os.path.abspath(__file__))
+    if fw == 'neus':
+        from neurecon_amd.frameworks.neus import Trainer
+        g = dict(np.load(os.path.join(here, 'golden', 'neus_train.npz')))
+        return neus_model(wg.neus_state(seed=1)), Trainer, _args(), _kw(8, 8), g
+    if fw == 'volsdf':
+        from neurecon_amd.frameworks.volsdf import Trainer
+        g = dict(np.load(os.path.join(here, 'golden', 'volsdf_train.npz')))
+        args = types.SimpleNamespace(data=types.SimpleNamespace(N_rays=-1),
+                                     model=types.SimpleNamespace(obj_bounding_radius=3.0),
+                                     training=types.SimpleNamespace(w_eikonal=0.1))
+        kw = dict(H=8, W=8, near=0.0, far=6.0, obj_bounding_radius=3.0, batched=True, perturb=False,
+                  white_bkgd=False, max_upsample_steps=6, use_nerfplusplus=False, N_samples=64, N_importance=64)
+        return volsdf_model(wg.volsdf_state(seed=3, beta_init=0.1), 0.1), Trainer, args, kw, g
+    from neurecon_amd.frameworks.unisurf import Trainer
+    g = dict(np.load(os.path.join(here, 'golden', 'unisurf_train.npz')))
+    args = types.SimpleNamespace(data=types.SimpleNamespace(N_rays=-1),
+                                 training=types.SimpleNamespace(w_reg=0.01, perturb_surface_pts=0.01, delta_max=1.0,
+                                                                delta_min=0.05, delta_beta=1.5e-5))
+    kw = dict(H=8, W=8, batched=True, perturb=False, white_bkgd=False, logit_tau=float(g['logit_tau']),
+              radius_of_interest=4.0, N_query=64, N_freespace=32)
+    return unisurf_model(wg.unisurf_state(seed=3)), Trainer, args, kw, g
+
+
+def _ddp_worker(rank, ws, port, q, fw='neus'):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [here, os.path.join(here, 'golden'), os.path.dirname(here)]
@@ -346,28 +372,30 @@ def _ddp_worker(rank, ws, port, q):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=ws)
     try:
-        from neurecon_amd.frameworks.neus import Trainer
-        g = dict(np.load(os.path.join(here, 'golden', 'neus_train.npz')))
+        m, Trainer, args, kw, g = _ddp_setup(fw)
         T = lambda a: torch.from_numpy(np.asarray(a)).cuda()
-        m = neus_model(wg.neus_state(seed=1))
         m.train()
         trainer = DDP(Trainer(m, device_ids=[0]), device_ids=None, find_unused_parameters=False)
 
         def batch(r):  # per-rank image: the fixture's targets, rolled by rank
-            return ({'intrinsics': T(g['K']), 'c2w': T(g['c2w']), 'object_mask': T(np.roll(g['target_mask'], 7 * r))},
-                    {'rgb': T(np.roll(g['target_rgb'], 11 * r, axis=1))})
+            mi = {'intrinsics': T(g['K']), 'c2w': T(g['c2w'])}
+            if 'target_mask' in g:
+                mi['object_mask'] = T(np.roll(g['target_mask'], 7 * r))
+            torch.manual_seed(100 + r)  # the step's random draws (eikonal points, surface perturbation)
+            return mi, {'rgb': T(np.roll(g['target_rgb'], 11 * r, axis=1))}
         mi, gt = batch(rank)
-        ret = trainer(_args(), None, mi, gt, _kw(8, 8), 0, device='cuda')
+        ret = trainer(args, None, mi, gt, kw, 0, device='cuda')
         ret['losses']['total'].mean().backward()
-        ddp_grads = {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters()}
+        ddp_grads = {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters() if p.grad is not None}
         if rank == 0:  # single-process reference: mean of both ranks' gradients
             ref = {}
             for r in range(ws):
                 m.zero_grad()
                 mi, gt = batch(r)
-                trainer.module(_args(), None, mi, gt, _kw(8, 8), 0, device='cuda')['losses']['total'].mean().backward()
+                trainer.module(args, None, mi, gt, kw, 0, device='cuda')['losses']['total'].mean().backward()
                 for k, p in m.named_parameters():
-                    ref[k] = ref.get(k, 0) + p.grad.detach().cpu() / ws
+                    if p.grad is not None:
+                        ref[k] = ref.get(k, 0) + p.grad.detach().cpu() / ws
             worst = max(float((ddp_grads[k] - ref[k]).abs().max() / (ref[k].abs().max() + 1e-30)) for k in ref)
             q.put(('diff', worst))
         q.put(('done', rank))
@@ -378,12 +406,15 @@ def _ddp_worker(rank, ws, port, q):
         dist.destroy_process_group()
 
 
-def test_ddp_gradient_allreduce_world2():
+@pytest.mark.parametrize('fw', ['neus', 'volsdf', 'unisurf'])
+def test_ddp_gradient_allreduce_world2(fw):
+    """train.py:124's DDP over two ranks (gloo, both on the one GPU): every rank's gradient after the
+    all-reduce equals the mean of the two ranks' single-process gradients, for each framework's Trainer"""
     import torch.multiprocessing as mp
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q, fw)) for r in range(2)]
     for p in ps:
         p.start()
     msgs = []
