@@ -294,8 +294,26 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
                        a.t_out_rand ? a.t_out_rand + ray0 * a.N_outside : (const float*)nullptr);
     NR_HIP_CHECK(hipGetLastError());
     const int64_t Po = (int64_t)(c.S - 1 + a.N_outside) * R;
-    if ((rc = launch_nerf(nerf_layout(*a.nerf), a.nerf_packed, c.x4, c.rd, 1, R, Po, c.sig_o, c.rad_o, st)))
-      return rc;
+    if (a.sigma_out || a.radiance_bg_out) {  // detailed outputs: the background at every sample, as the reference
+      if ((rc = launch_nerf(nerf_layout(*a.nerf), a.nerf_packed, c.x4, c.rd, 1, R, Po, c.sig_o, c.rad_o, st)))
+        return rc;
+    } else {  // only the background values the compositing reads (neus_outside_compact)
+      char* wsb = (char*)a.workspace;
+      int* cnt = (int*)(wsb + pl.o_cnt);
+      int* slot = (int*)(wsb + pl.o_slot);
+      float* x4c = (float*)(wsb + pl.o_x4c);
+      float* vdc = (float*)(wsb + pl.o_vdc);
+      float* sigc = (float*)(wsb + pl.o_sigc);
+      float* radc = (float*)(wsb + pl.o_radc);
+      NR_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int), st));
+      const dim3 g1((unsigned)((Po + 255) / 256));
+      hipLaunchKernelGGL(neus_outside_compact, g1, dim3(256), 0, st, c, cnt, slot, x4c, vdc);
+      NR_HIP_CHECK(hipGetLastError());
+      if ((rc = launch_nerf(nerf_layout(*a.nerf), a.nerf_packed, x4c, vdc, 1, INT64_MAX, Po, sigc, radc, st, cnt)))
+        return rc;
+      hipLaunchKernelGGL(neus_outside_scatter, g1, dim3(256), 0, st, slot, sigc, radc, Po, c.sig_o, c.rad_o);
+      NR_HIP_CHECK(hipGetLastError());
+    }
     ProfScope prof("neus_composite", (double)R, st);
     hipLaunchKernelGGL(neus_composite_outside, grd, blk, 0, st, c, o, a.s_dev, a.s, a.calc_normal, a.white_bkgd);
   } else {

@@ -100,7 +100,8 @@ int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t
                float* feature, int nfreq, void* ws, size_t ws_bytes, hipStream_t stream,
                const int* P_dev = nullptr, int P_mult = 0);  // P_dev: device count, P_eff = min(P, *P_dev * P_mult)
 int launch_nerf(const NerfLayout& L, const void* packed, const float* x4, const float* vdir, int64_t vdiv,
-                int64_t vmod, int64_t P, float* sigma, float* rgb, hipStream_t stream);
+                int64_t vmod, int64_t P, float* sigma, float* rgb, hipStream_t stream,
+                const int* P_dev = nullptr);  // P_dev: device count, P_eff = min(P, *P_dev)
 int launch_radiance(const RadLayout& L, const void* packed, const float* x, const float* vdir, int64_t vdiv,
                     int64_t vmod, const float* normals, const float* feature, int64_t P, float* rgb, int nfreq_view,
                     hipStream_t stream);

@@ -2230,6 +2230,7 @@ struct NerfKArgs {
   int64_t P;
   float* sigma;       // [P]
   float* rgb;         // [P][3]
+  const int* P_dev;   // optional device count: the first min(P, *P_dev) points are evaluated
 };
 
 // Embedder(input_dim=4, multires=10): [x, sin(x 2^0), cos(x 2^0), ..., sin(x 2^9), cos(x 2^9)]
@@ -2258,11 +2259,12 @@ __global__ __launch_bounds__(kThreads) void nerf_kernel(NerfKArgs a) {
   const float* wr = (const float*)(W + L.rgb_off);
 
   ws.start(OP(N0), OPB(N0), OP(N0) + OPB(N0), OPB(N0));
-  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < a.P; base += (int64_t)gridDim.x * kPointsPerWG) {
-    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < a.P;
+  const int64_t Pn = a.P_dev ? min(a.P, (int64_t)*a.P_dev) : a.P;
+  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < Pn; base += (int64_t)gridDim.x * kPointsPerWG) {
+    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < Pn;
     const int64_t p = base + wave * kTile + j;
-    const bool valid = p < a.P;
-    const int64_t pc = valid ? p : a.P - 1;
+    const bool valid = p < Pn;
+    const int64_t pc = valid ? p : Pn - 1;
     const float4 xin = *(const float4*)(a.x4 + pc * 4);
     const int64_t pv = (pc / a.vdiv) % a.vmod;
     const float v0 = a.vdir[pv * 3 + 0], v1 = a.vdir[pv * 3 + 1], v2 = a.vdir[pv * 3 + 2];
@@ -2562,10 +2564,10 @@ int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t
 }
 
 int launch_nerf(const NerfLayout& L, const void* packed, const float* x4, const float* vdir, int64_t vdiv,
-                int64_t vmod, int64_t P, float* sigma, float* rgb, hipStream_t stream) {
+                int64_t vmod, int64_t P, float* sigma, float* rgb, hipStream_t stream, const int* P_dev) {
   if (P <= 0) return NR_OK;
   const int grid = grid_for(P);
-  NerfKArgs a{(const char*)packed, L, x4, vdir, vdiv, vmod, P, sigma, rgb};
+  NerfKArgs a{(const char*)packed, L, x4, vdir, vdiv, vmod, P, sigma, rgb, P_dev};
   ProfScope prof("nerf", (double)P, stream);
   if (L.prec == NR_PREC_F16X3) hipLaunchKernelGGL((nerf_kernel<NR_PREC_F16X3>), dim3(grid), dim3(kThreads), 0, stream, a);
   else hipLaunchKernelGGL((nerf_kernel<NR_PREC_FP32>), dim3(grid), dim3(kThreads), 0, stream, a);

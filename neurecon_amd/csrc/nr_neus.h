@@ -49,6 +49,7 @@ struct NeusPlan {
   size_t o_ro, o_rd, o_near, o_far, o_dv, o_sv, o_wtmp, o_dnew, o_snew, o_pts, o_mids, o_dmid;
   size_t o_sdf_f, o_nab_f, o_sdf_m, o_nab_m, o_feat_m, o_rad_m, o_dout, o_x4, o_sigo, o_rado, o_ptsn, o_sn, o_mlp;
   size_t o_idv, o_nsort, o_dv2, o_sv2, o_idv2;
+  size_t o_slot, o_x4c, o_vdc, o_sigc, o_radc, o_cnt;  // NeRF++: compacted background points
   size_t total;
 };
 
@@ -61,6 +62,9 @@ __global__ void neus_merge(NeusChunk c, int L, float* dv2, float* sv2, int* idv2
 __global__ void neus_expand(NeusChunk c);
 __global__ void neus_composite(NeusChunk c, NeusOut o, const float* s_dev, float s_val, int calc_normal, int white_bkgd);
 __global__ void neus_outside_points(NeusChunk c, const float* t_rand);
+__global__ void neus_outside_compact(NeusChunk c, int* count, int* slot, float* x4c, float* vdc);
+__global__ void neus_outside_scatter(const int* slot, const float* sigc, const float* radc, int64_t n, float* sig_o,
+                                     float* rad_o);
 __global__ void neus_nograd_points(NeusChunk c);
 __global__ void neus_direct_upsample(NeusChunk c, int more, const float* u, int64_t u_stride);
 __global__ void neus_composite_outside(NeusChunk c, NeusOut o, const float* s_dev, float s_val, int calc_normal,

@@ -469,6 +469,65 @@ __global__ __launch_bounds__(64) void neus_outside_points(NeusChunk c, const flo
   }
 }
 
+// The background values the compositing reads (neus.py:325-343): every inverted-sphere sample, and the
+// mid-points outside the bounding sphere -- the ones inside take the SDF's alpha and radiance, so the
+// reference's background evaluation there is discarded.  Without detailed outputs only these points
+// go through the NeRF++ net: appended (one atomic per wave) to x4c / vdc, slot[q] = compact index or
+// -1; the inside test is the compositing's own (norm3_ref(o + d dm) <= r_obj).
+__global__ void neus_outside_compact(NeusChunk c, int* __restrict__ count, int* __restrict__ slot,
+                                     float* __restrict__ x4c, float* __restrict__ vdc) {
+  const int64_t R = c.R;
+  const int S1 = c.S - 1, M = S1 + c.N_out;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in_range = q < (int64_t)M * R;
+  int64_t r = 0;
+  bool need = false;
+  if (in_range) {
+    const int k = (int)(q / R);
+    r = q - (int64_t)k * R;
+    if (k >= S1) {
+      need = true;
+    } else {
+      const float dm = c.dmid[q];
+      const float px = fadd(c.ro[r * 3], fmul(c.rd[r * 3], dm)), py = fadd(c.ro[r * 3 + 1], fmul(c.rd[r * 3 + 1], dm)),
+                  pz = fadd(c.ro[r * 3 + 2], fmul(c.rd[r * 3 + 2], dm));
+      need = !(norm3_ref(px, py, pz) <= c.r_obj);
+    }
+  }
+  const uint64_t bal = __ballot(need);
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (bal) {
+    const int leader = __ffsll((unsigned long long)bal) - 1;
+    if (lane == leader) base = atomicAdd(count, __popcll(bal));
+    base = __shfl(base, leader);
+  }
+  if (!in_range) return;
+  if (need) {
+    const int j = base + __popcll(bal & ((1ull << lane) - 1ull));
+    slot[q] = j;
+    *(float4*)(x4c + (int64_t)j * 4) = *(const float4*)(c.x4 + q * 4);
+    vdc[(int64_t)j * 3 + 0] = c.rd[r * 3 + 0];
+    vdc[(int64_t)j * 3 + 1] = c.rd[r * 3 + 1];
+    vdc[(int64_t)j * 3 + 2] = c.rd[r * 3 + 2];
+  } else {
+    slot[q] = -1;
+  }
+}
+
+__global__ void neus_outside_scatter(const int* __restrict__ slot, const float* __restrict__ sigc,
+                                     const float* __restrict__ radc, int64_t n, float* __restrict__ sig_o,
+                                     float* __restrict__ rad_o) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n) return;
+  const int j = slot[q];
+  if (j < 0) return;
+  sig_o[q] = sigc[j];
+  rad_o[q * 3 + 0] = radc[(int64_t)j * 3 + 0];
+  rad_o[q * 3 + 1] = radc[(int64_t)j * 3 + 1];
+  rad_o[q * 3 + 2] = radc[(int64_t)j * 3 + 2];
+}
+
 // F.softplus (beta 1, threshold 20)
 __device__ __forceinline__ float softplus1(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
 
@@ -644,6 +703,13 @@ NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc) {
   p.o_x4 = take((size_t)(a.N_outside > 0 ? M : 1) * Rc * 4);
   p.o_sigo = take((size_t)(a.N_outside > 0 ? M : 1) * Rc);
   p.o_rado = take((size_t)(a.N_outside > 0 ? M : 1) * Rc * 3);
+  const size_t Mo = (size_t)(a.N_outside > 0 ? M : 1) * Rc;
+  p.o_slot = take(Mo);
+  p.o_x4c = take(Mo * 4);
+  p.o_vdc = take(Mo * 3);
+  p.o_sigc = take(Mo);
+  p.o_radc = take(Mo * 3);
+  p.o_cnt = take(1);
   p.o_ptsn = take((size_t)(n_nog > 0 ? n_nog : 1) * Rc * 3);
   p.o_sn = take((size_t)(n_nog > 0 ? n_nog : 1) * Rc);
   p.o_idv = take((size_t)S * Rc);

@@ -105,3 +105,30 @@ def test_neus_direct_more_with_nerfpp_vs_oracle(precision):
     print(f'identical samples {same.mean() * 100:.1f}%, per-ray pass {ray_ok.mean() * 100:.1f}%')
     assert (~ray_ok & same).sum() == 0
     assert same.mean() >= 0.8
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
+def test_neus_nerfpp_compact_background_bit_identical(golden, precision):
+    """Without detailed outputs the NeRF++ net runs only on the samples the compositing reads (every
+    outside sample, mid-points outside the bounding sphere; neus.py:325-343): rgb / depth / mask /
+    normals must be bit-identical to the render that evaluates the background at every sample, on the
+    config-(d) rays plus 192 rays fanned out across the frame so that part of them leave the sphere."""
+    from neurecon_amd.frameworks.neus import volume_render
+    g = golden('neus_d')
+    m = neus_model(wg.neus_state(seed=int(g['seed']), use_outside_nerf=True), use_outside_nerf=True,
+                   precision=precision)
+    ro, rd = to_gpu(g['rays_o']), to_gpu(g['rays_d'])
+    gen = torch.Generator().manual_seed(3)
+    rd2 = rd[:, :1].repeat(1, 192, 1) + (torch.rand(1, 192, 3, generator=gen) - 0.5).cuda() * 0.8
+    ro = torch.cat([ro, ro[:, :1].repeat(1, 192, 1)], 1)
+    rd = torch.cat([rd, rd2], 1)
+    kw = dict(obj_bounding_radius=1.0, batched=True, calc_normal=True, N_samples=64, N_importance=64,
+              N_outside=32, N_upsample_iters=4)
+    with torch.no_grad():
+        rgb_c, dep_c, ex_c = volume_render(ro, rd, m, detailed_output=False, **kw)
+        rgb_f, dep_f, ex_f = volume_render(ro, rd, m, detailed_output=True, **kw)
+    torch.cuda.synchronize()
+    for name, a, b in [('rgb', rgb_c, rgb_f), ('depth', dep_c, dep_f), ('mask', ex_c['mask_volume'], ex_f['mask_volume']),
+                       ('normals', ex_c['normals_volume'], ex_f['normals_volume'])]:
+        assert torch.equal(a, b), (name, float((a - b).abs().max()))
+    print(f'{precision}: compact-background render bit-identical on {rgb_c.shape[1]} rays')
