@@ -314,6 +314,18 @@ def train_setup(dev, precision, n_rays, world):
     return step
 
 
+def executed_flop(kstats):
+    """fp32-equivalent FLOPs the MLP launches executed (units = points actually evaluated)"""
+    return sum(units * 2.0 * KERNEL_MAC.get(name, 0) for name, (n, ms, units) in kstats.items())
+
+
+def mid_frac(kstats, rays, steps):
+    """fraction of the 127 mid-points per ray that went through the SDF + radiance nets"""
+    if 'sdf_nabla_feat' not in kstats:
+        return None
+    return round(kstats['sdf_nabla_feat'][2] / (127.0 * rays * steps), 4)
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -346,6 +358,10 @@ def main():
         def step():
             with torch.no_grad():
                 return volume_render(ro, rd, model, **kw)
+
+        def step_full():  # every mid-point through the nets, as the reference (same outputs bit for bit)
+            with torch.no_grad():
+                return volume_render(ro, rd, model, skip_zero_alpha=False, **kw)
         n_rays = ro.shape[1] * world
 
     for _ in range(args.warmup):
@@ -366,6 +382,29 @@ def main():
     dt = time.perf_counter() - t0
     L.profile_enable(False)
     kstats = L.profile_read()
+    full = None
+    if args.workload not in ('frame_d', 'train'):  # the same steps with every mid-point evaluated
+        for _ in range(args.warmup):
+            step_full()
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+        L.profile_read()
+        L.profile_enable(True)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step_full()
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+        dt_full = time.perf_counter() - t1
+        L.profile_enable(False)
+        kstats_full = L.profile_read()
+        if dist:
+            t = torch.tensor([dt_full], device=dev)
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+            dt_full = float(t.item())
+        full = (dt_full, kstats_full)
     if dist:
         t = torch.tensor([dt], device=dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -409,8 +448,20 @@ def main():
                            'rays_per_gpu': n_rays // world, 'samples_per_ray': 128, 'precision': args.precision,
                            'parallelism': f'ray-sharded x{world}'},
                 'roofline': roof,
-                'step_tflops': round(RAY_FLOP * (n_rays // world) / (dt / args.steps) / 1e12, 2),
+                # executed MLP FLOPs (fp32-equivalent) per second over the whole step
+                'step_tflops': round(executed_flop(kstats) / args.steps / (dt / args.steps) / 1e12, 2),
+                'mid_points_evaluated_frac': mid_frac(kstats, n_rays // world, args.steps),
             }
+            if full is not None:
+                dtf, kf = full
+                out['full_evaluation'] = {
+                    'note': 'same rays, same outputs bit for bit (tests/test_gpu_parity.py); every mid-point through '
+                            'the SDF + radiance nets as the reference does, including the ones whose alpha is exactly 0',
+                    'value': round(total_rays / dtf, 1), 'ms_per_step': round(dtf / args.steps * 1e3, 3),
+                    'step_tflops': round(executed_flop(kf) / dtf / 1e12, 2), 'roofline': roofline(kf, args.precision)}
+            out['config']['zero_alpha_skip'] = ('mid-points whose alpha is exactly 0 (no SDF decrease between the '
+                                                'two samples, neus.py:28-35) get weight 0 and skip the nets; '
+                                                'rgb/depth/mask/normals bit-identical to full evaluation')
             if not args.no_cpu_baseline and world == 1:
                 out['cpu_baseline'] = cpu_baseline(args.cpu_rays)
                 eg = eager_gpu_baseline(dev, n_rays)

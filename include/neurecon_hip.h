@@ -199,6 +199,11 @@ typedef struct {
    * nr_train entry points below. */
   int sample_only;
   float* d_all_out;
+  /* Mid-points whose alpha is exactly 0 (the SDF does not decrease from sample i to i+1, neus.py:28-35)
+   * contribute w = 0 to every map; without NeRF++ and without the radiance output they skip the SDF
+   * and radiance nets (rgb / depth / mask / normals bit-identical).  no_mid_skip != 0: evaluate every
+   * mid-point, as the reference does. */
+  int no_mid_skip;
 } NrNeusArgs;
 
 size_t nr_neus_workspace_bytes(const NrNeusArgs* a);

@@ -55,6 +55,7 @@ class NrNeusArgs(ctypes.Structure):
         ('upsample_algo', _c_i), ('fixed_s', _c_f), ('N_nograd_samples', _c_i), ('t_nograd', _c_p),
         ('workspace', _c_p), ('workspace_bytes', _c_sz),
         ('u_rand', _c_p), ('t_out_rand', _c_p), ('s_dev', _c_p), ('sample_only', _c_i), ('d_all_out', _c_p),
+        ('no_mid_skip', _c_i),
     ]
 
 

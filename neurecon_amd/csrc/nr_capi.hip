@@ -281,12 +281,34 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
                                  a.sdf->multires, mlp_ws, mlp_bytes, st)))
     return rc;
   // SDF + nablas + geometry feature at the mid-points, then the radiance net (neus.py:103-106, :298)
-  if ((rc = launch_sdf(SL, a.sdf_packed, c.mids, (int64_t)(c.S - 1) * R, c.sdf_m, c.nab_m, c.feat_m,
-                       a.sdf->multires, mlp_ws, mlp_bytes, st)))
-    return rc;
-  if ((rc = launch_radiance(RL, a.rad_packed, c.mids, c.rd, 1, R, c.nab_m, c.feat_m, (int64_t)(c.S - 1) * R, c.rad_m,
-                            a.rad->multires_view, st)))
-    return rc;
+  const int64_t Pm = (int64_t)(c.S - 1) * R;
+  if (a.N_outside > 0 || a.radiance_out || a.no_mid_skip) {  // every mid-point, as the reference
+    if ((rc = launch_sdf(SL, a.sdf_packed, c.mids, Pm, c.sdf_m, c.nab_m, c.feat_m, a.sdf->multires, mlp_ws, mlp_bytes,
+                         st)))
+      return rc;
+    if ((rc = launch_radiance(RL, a.rad_packed, c.mids, c.rd, 1, R, c.nab_m, c.feat_m, Pm, c.rad_m,
+                              a.rad->multires_view, st)))
+      return rc;
+  } else {  // only the mid-points whose alpha is not exactly 0 (neus_mid_compact); bit-identical maps
+    char* wsb = (char*)a.workspace;
+    int* cnt = (int*)(wsb + pl.o_mcnt);
+    int* slot = (int*)(wsb + pl.o_mslot);
+    float* midc = (float*)(wsb + pl.o_midc);
+    float* vdc = (float*)(wsb + pl.o_mvd);
+    float* radc = (float*)(wsb + pl.o_mrad);
+    NR_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int), st));
+    const dim3 g1((unsigned)((Pm + 255) / 256));
+    hipLaunchKernelGGL(neus_mid_compact, g1, dim3(256), 0, st, c, a.s_dev, a.s, cnt, slot, midc, vdc);
+    NR_HIP_CHECK(hipGetLastError());
+    if ((rc = launch_sdf(SL, a.sdf_packed, midc, Pm, c.sdf_m, c.nab_m, c.feat_m, a.sdf->multires, mlp_ws, mlp_bytes,
+                         st, cnt, 1)))
+      return rc;
+    if ((rc = launch_radiance(RL, a.rad_packed, midc, vdc, 1, INT64_MAX, c.nab_m, c.feat_m, Pm, radc,
+                              a.rad->multires_view, st, cnt)))
+      return rc;
+    hipLaunchKernelGGL(neus_mid_scatter, g1, dim3(256), 0, st, slot, radc, Pm, c.rad_m);
+    NR_HIP_CHECK(hipGetLastError());
+  }
   NeusOut o{ray0, a.rgb, a.depth, a.acc, a.normals, a.d_final, a.sdf_out, a.nablas_out,
             a.radiance_out, a.alpha_out, a.cdf_out, a.weights_out, a.sigma_out, a.radiance_bg_out};
   if (a.N_outside > 0) {  // NeRF++ background on [mid-points ; inverted-sphere samples]

@@ -48,7 +48,9 @@ void set_error(const std::string& msg);
 bool prof_on();
 class ProfScope {
  public:
-  ProfScope(const char* name, double units, hipStream_t st);
+  // dev_units: optional device-side unit count (a compacted launch); the record's units become
+  // min(units, *dev_units * mult), read when the statistics are
+  ProfScope(const char* name, double units, hipStream_t st, const int* dev_units = nullptr, int mult = 1);
   ~ProfScope();
 
  private:

@@ -104,7 +104,7 @@ int launch_nerf(const NerfLayout& L, const void* packed, const float* x4, const 
                 const int* P_dev = nullptr);  // P_dev: device count, P_eff = min(P, *P_dev)
 int launch_radiance(const RadLayout& L, const void* packed, const float* x, const float* vdir, int64_t vdiv,
                     int64_t vmod, const float* normals, const float* feature, int64_t P, float* rgb, int nfreq_view,
-                    hipStream_t stream);
+                    hipStream_t stream, const int* P_dev = nullptr);  // P_dev: device count, P_eff = min(P, *P_dev)
 
 SdfLayout sdf_layout(const NrSdfDesc& d);
 RadLayout rad_layout(const NrRadDesc& d);

@@ -1931,6 +1931,7 @@ struct RadKArgs {
   int64_t P;
   float* rgb;
   int nfreq_view;  // <0: identity
+  const int* P_dev;  // optional device count: the first min(P, *P_dev) points are evaluated
 };
 
 // small input features [x(3), view-embedding(3+6F or 3), normals(3)] in block layout ([x(3)] only
@@ -1963,11 +1964,12 @@ __global__ __launch_bounds__(kThreads) void radiance_kernel(RadKArgs a) {
   const bool view = L.view != 0;
 
   ws.start(OP(0), OPB(0), OP(0) + OPB(0), OPB(0));
-  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < a.P; base += (int64_t)gridDim.x * kPointsPerWG) {
-    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < a.P;
+  const int64_t Pn = a.P_dev ? min(a.P, (int64_t)*a.P_dev) : a.P;
+  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < Pn; base += (int64_t)gridDim.x * kPointsPerWG) {
+    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < Pn;
     const int64_t p = base + wave * kTile + j;
-    const bool valid = p < a.P;
-    const int64_t pc = valid ? p : a.P - 1;
+    const bool valid = p < Pn;
+    const int64_t pc = valid ? p : Pn - 1;
     float xs[3], vs[3] = {0.f, 0.f, 0.f}, ns[3] = {0.f, 0.f, 0.f};
     const int64_t pv = (pc / a.vdiv) % a.vmod;
 #pragma unroll
@@ -2119,8 +2121,9 @@ void rad4_kernel(RadKArgs a) {
   ws.template start<C0, C0>(OP(0), OP(0) + C0);  // its barrier also publishes the head
   Pend4 pd{};
   NoPre4 nopre;
-  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < a.P; base += (int64_t)gridDim.x * kPointsPerWG) {
-    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < a.P;
+  const int64_t Pn = a.P_dev ? min(a.P, (int64_t)*a.P_dev) : a.P;
+  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < Pn; base += (int64_t)gridDim.x * kPointsPerWG) {
+    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < Pn;
     const int64_t p0 = base + wave * 16 * kNC;
     f16x8 Uh[kNC][12], Ul[kNC][12], Vh[kNC][12], Vl[kNC][12];
     float m_in[kNC], xinv[kNC], mrun[kNC];
@@ -2128,8 +2131,8 @@ void rad4_kernel(RadKArgs a) {
 #pragma unroll
     for (int q = 0; q < kNC; ++q) {
       const int64_t p = p0 + 16 * q + j;
-      valid[q] = p < a.P;
-      const int64_t pc = valid[q] ? p : a.P - 1;
+      valid[q] = p < Pn;
+      const int64_t pc = valid[q] ? p : Pn - 1;
       const int64_t pv = (pc / a.vdiv) % a.vmod;
       float xs[3], vs[3] = {0.f, 0.f, 0.f}, ns[3] = {0.f, 0.f, 0.f};
 #pragma unroll
@@ -2528,7 +2531,7 @@ int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t
   const int grid = grid_for(P);
   SdfKArgs a{(const char*)packed, L, pts, P, sdf, nabla, feature, (float4*)ws, nfreq, P_dev, P_mult};
   ProfScope prof(nabla ? (feature ? "sdf_nabla_feat" : "sdf_nabla") : (feature ? "sdf_feat" : "sdf_fwd"), (double)P,
-                 stream);
+                 stream, P_dev, P_mult);
   if (L.siren) {
     if (nabla) {
       const size_t need = (size_t)grid * kScratchPerWG;
@@ -2568,7 +2571,7 @@ int launch_nerf(const NerfLayout& L, const void* packed, const float* x4, const 
   if (P <= 0) return NR_OK;
   const int grid = grid_for(P);
   NerfKArgs a{(const char*)packed, L, x4, vdir, vdiv, vmod, P, sigma, rgb, P_dev};
-  ProfScope prof("nerf", (double)P, stream);
+  ProfScope prof("nerf", (double)P, stream, P_dev, 1);
   if (L.prec == NR_PREC_F16X3) hipLaunchKernelGGL((nerf_kernel<NR_PREC_F16X3>), dim3(grid), dim3(kThreads), 0, stream, a);
   else hipLaunchKernelGGL((nerf_kernel<NR_PREC_FP32>), dim3(grid), dim3(kThreads), 0, stream, a);
   NR_HIP_CHECK(hipGetLastError());
@@ -2577,11 +2580,11 @@ int launch_nerf(const NerfLayout& L, const void* packed, const float* x4, const 
 
 int launch_radiance(const RadLayout& L, const void* packed, const float* x, const float* vdir, int64_t vdiv,
                     int64_t vmod, const float* normals, const float* feature, int64_t P, float* rgb, int nfreq_view,
-                    hipStream_t stream) {
+                    hipStream_t stream, const int* P_dev) {
   if (P <= 0) return NR_OK;
   const int grid = grid_for(P);
-  RadKArgs a{(const char*)packed, L, x, vdir, vdiv, vmod, normals, feature, P, rgb, nfreq_view};
-  ProfScope prof("radiance", (double)P, stream);
+  RadKArgs a{(const char*)packed, L, x, vdir, vdiv, vmod, normals, feature, P, rgb, nfreq_view, P_dev};
+  ProfScope prof("radiance", (double)P, stream, P_dev, 1);
   const bool h3 = L.prec == NR_PREC_F16X3;
   // (small-input blocks, activation, depth) variants
 #define NR_RAD_LAUNCH(KBS, ACT, D)                                                                            \

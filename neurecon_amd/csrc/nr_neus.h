@@ -50,6 +50,7 @@ struct NeusPlan {
   size_t o_sdf_f, o_nab_f, o_sdf_m, o_nab_m, o_feat_m, o_rad_m, o_dout, o_x4, o_sigo, o_rado, o_ptsn, o_sn, o_mlp;
   size_t o_idv, o_nsort, o_dv2, o_sv2, o_idv2;
   size_t o_slot, o_x4c, o_vdc, o_sigc, o_radc, o_cnt;  // NeRF++: compacted background points
+  size_t o_mslot, o_midc, o_mvd, o_mrad, o_mcnt;        // mid-points of non-zero alpha (compacted)
   size_t total;
 };
 
@@ -63,6 +64,9 @@ __global__ void neus_expand(NeusChunk c);
 __global__ void neus_composite(NeusChunk c, NeusOut o, const float* s_dev, float s_val, int calc_normal, int white_bkgd);
 __global__ void neus_outside_points(NeusChunk c, const float* t_rand);
 __global__ void neus_outside_compact(NeusChunk c, int* count, int* slot, float* x4c, float* vdc);
+__global__ void neus_mid_compact(NeusChunk c, const float* s_dev, float s_val, int* count, int* slot, float* midc,
+                                 float* vdc);
+__global__ void neus_mid_scatter(const int* slot, const float* radc, int64_t n, float* rad_m);
 __global__ void neus_outside_scatter(const int* slot, const float* sigc, const float* radc, int64_t n, float* sig_o,
                                      float* rad_o);
 __global__ void neus_nograd_points(NeusChunk c);

@@ -515,6 +515,59 @@ __global__ void neus_outside_compact(NeusChunk c, int* __restrict__ count, int* 
   }
 }
 
+// Mid-point i of a ray contributes w_i * radiance_i with w_i = alpha_i T_i, and alpha_i = max((c_i -
+// c_{i+1}) / (c_i + 1e-10), 0) is exactly 0 wherever the SDF does not decrease from sample i to i+1
+// (neus.py:28-35): there the radiance (and the mid-point's SDF, nablas and feature that feed it) is
+// multiplied by an exact zero.  Without detailed outputs only the mid-points with alpha != 0 (the
+// compositing's own arithmetic) go through the SDF + radiance nets; the others get radiance 0.
+__global__ void neus_mid_compact(NeusChunk c, const float* __restrict__ s_dev, float s_val, int* __restrict__ count,
+                                 int* __restrict__ slot, float* __restrict__ midc, float* __restrict__ vdc) {
+  const int64_t R = c.R;
+  const int S1 = c.S - 1;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in_range = q < (int64_t)S1 * R;
+  int64_t r = 0;
+  bool need = false;
+  if (in_range) {
+    const float s_inv = s_dev ? *s_dev : s_val;
+    const int i = (int)(q / R);
+    r = q - (int64_t)i * R;
+    const float cp = sigmoidf_ref(fmul(c.sdf_f[(int64_t)i * R + r], s_inv));
+    const float cn = sigmoidf_ref(fmul(c.sdf_f[(int64_t)(i + 1) * R + r], s_inv));
+    const float alpha = fmaxf(fdiv(fsub(cp, cn), fadd(cp, 1e-10f)), 0.0f);
+    need = !(alpha == 0.0f);
+  }
+  const uint64_t bal = __ballot(need);
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (bal) {
+    const int leader = __ffsll((unsigned long long)bal) - 1;
+    if (lane == leader) base = atomicAdd(count, __popcll(bal));
+    base = __shfl(base, leader);
+  }
+  if (!in_range) return;
+  if (need) {
+    const int64_t j = base + __popcll(bal & ((1ull << lane) - 1ull));
+    slot[q] = (int)j;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      midc[j * 3 + e] = c.mids[q * 3 + e];
+      vdc[j * 3 + e] = c.rd[r * 3 + e];
+    }
+  } else {
+    slot[q] = -1;
+  }
+}
+
+__global__ void neus_mid_scatter(const int* __restrict__ slot, const float* __restrict__ radc, int64_t n,
+                                 float* __restrict__ rad_m) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n) return;
+  const int j = slot[q];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) rad_m[q * 3 + e] = j < 0 ? 0.0f : radc[(int64_t)j * 3 + e];
+}
+
 __global__ void neus_outside_scatter(const int* __restrict__ slot, const float* __restrict__ sigc,
                                      const float* __restrict__ radc, int64_t n, float* __restrict__ sig_o,
                                      float* __restrict__ rad_o) {
@@ -710,6 +763,12 @@ NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc) {
   p.o_sigc = take(Mo);
   p.o_radc = take(Mo * 3);
   p.o_cnt = take(1);
+  const size_t Mm = (size_t)(S - 1) * Rc;
+  p.o_mslot = take(Mm);
+  p.o_midc = take(Mm * 3);
+  p.o_mvd = take(Mm * 3);
+  p.o_mrad = take(Mm * 3);
+  p.o_mcnt = take(1);
   p.o_ptsn = take((size_t)(n_nog > 0 ? n_nog : 1) * Rc * 3);
   p.o_sn = take((size_t)(n_nog > 0 ? n_nog : 1) * Rc);
   p.o_idv = take((size_t)S * Rc);

@@ -13,19 +13,32 @@ struct ProfRec {
   const char* name;
   double units;
   hipEvent_t a, b;
+  int slot;  // >= 0: device count copied into g_counts[slot] (units = min(units, count * mult))
+  int mult;
 };
 static std::mutex g_mu;
 static std::vector<ProfRec> g_recs;
 static bool g_on = false;
+constexpr int kCountSlots = 1 << 16;
+static int* g_counts = nullptr;  // device slots for the device-side unit counts of compacted launches
+static int g_nslots = 0;
 
 bool prof_on() { return g_on; }
 
-ProfScope::ProfScope(const char* name, double units, hipStream_t st) : st_(st), on_(g_on) {
+ProfScope::ProfScope(const char* name, double units, hipStream_t st, const int* dev_units, int mult)
+    : st_(st), on_(g_on) {
   if (!on_) return;
-  ProfRec r{name, units, nullptr, nullptr};
+  ProfRec r{name, units, nullptr, nullptr, -1, mult};
   if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) { on_ = false; return; }
   (void)hipEventRecord(r.a, st);
   std::lock_guard<std::mutex> lk(g_mu);
+  if (dev_units) {
+    if (!g_counts) (void)hipMalloc(&g_counts, sizeof(int) * kCountSlots);
+    if (g_counts && g_nslots < kCountSlots) {
+      r.slot = g_nslots++;
+      (void)hipMemcpyAsync(g_counts + r.slot, dev_units, sizeof(int), hipMemcpyDeviceToDevice, st);
+    }
+  }
   g_recs.push_back(r);
   idx_ = g_recs.size() - 1;
 }
@@ -49,7 +62,16 @@ extern "C" int nr_profile_read(NrKernelStat* out, int max, int* n_out) {
   NR_REQUIRE(n_out, NR_ERR_ARG, "nr_profile_read: null n_out");
   std::lock_guard<std::mutex> lk(g_mu);
   std::vector<NrKernelStat> acc;
+  std::vector<int> counts(g_nslots > 0 ? g_nslots : 1, 0);
+  if (g_nslots > 0) {
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpy(counts.data(), g_counts, sizeof(int) * g_nslots, hipMemcpyDeviceToHost);
+  }
   for (auto& r : g_recs) {
+    if (r.slot >= 0) {
+      const double dev = (double)counts[r.slot] * r.mult;
+      if (dev < r.units) r.units = dev;
+    }
     float ms = 0.f;
     if (hipEventSynchronize(r.b) == hipSuccess) (void)hipEventElapsedTime(&ms, r.a, r.b);
     (void)hipEventDestroy(r.a);
@@ -68,6 +90,7 @@ extern "C" int nr_profile_read(NrKernelStat* out, int max, int* n_out) {
     s->units += r.units;
   }
   g_recs.clear();
+  g_nslots = 0;
   int n = 0;
   for (auto& x : acc)
     if (n < max && out) out[n++] = x;

@@ -276,3 +276,31 @@ def test_multi_chunk_render_is_chunk_invariant(framework):
     assert torch.equal(rgb, torch.cat([p[0] for p in parts], 1))
     assert torch.equal(depth, torch.cat([p[1] for p in parts], 1))
     assert torch.equal(ex['normals_volume'], torch.cat([p[2]['normals_volume'] for p in parts], 1))
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
+@pytest.mark.parametrize('perturb', [False, True])
+def test_neus_zero_alpha_skip_bit_identical(precision, perturb):
+    """The benchmarked render (detailed_output=False) sends only the mid-points whose alpha is not exactly
+    0 through the SDF + radiance nets (neus_mid_compact): rgb / depth / mask / normals must equal the
+    full evaluation bit for bit on the whole config-(b) workload (4096 rays; perturb=True replays the
+    same uniforms in both renders)."""
+    from oracle import rays as orays
+    from neurecon_amd.frameworks.neus import volume_render
+    H, W, f, dist = wg.CAMERAS['b']
+    c2w = wg.look_at_c2w(dist)[None]
+    K = wg.intrinsics(f, H, W)[None]
+    ro, rd, _ = orays.get_rays(c2w, K, H, W)
+    m = neus_model(wg.neus_state(seed=1), precision=precision)
+    kw = dict(obj_bounding_radius=1.0, batched=True, calc_normal=True, detailed_output=False, perturb=perturb,
+              N_samples=64, N_importance=64, N_upsample_iters=4)
+    outs = []
+    for skip in (True, False):
+        torch.manual_seed(7)
+        with torch.no_grad():
+            rgb, depth, ex = volume_render(ro.cuda(), rd.cuda(), m, skip_zero_alpha=skip, **kw)
+        outs.append((rgb, depth, ex['mask_volume'], ex['normals_volume']))
+    torch.cuda.synchronize()
+    for name, a, b in zip(('rgb', 'depth', 'mask', 'normals'), outs[0], outs[1]):
+        assert torch.equal(a, b), (name, float((a - b).abs().max()))
+    print(f'{precision} perturb={perturb}: zero-alpha skip bit-identical on 4096 rays')
