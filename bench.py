@@ -52,6 +52,8 @@ def parse():
     ap.add_argument('--rays', type=int, default=4096)
     ap.add_argument('--precision', default=os.environ.get('NR_PRECISION', 'f16x3'), choices=['f16x3', 'fp32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-full-eval', action='store_true',
+                    help='skip the second timed loop that evaluates every mid-point (profiling runs)')
     ap.add_argument('--workload', default='b', choices=['b', 'frame_d', 'train'],
                     help="b: the BASELINE metric (default); frame_d: config (d) full frame sharded over the GPUs; "
                          "train: NeuS training step")
@@ -383,7 +385,7 @@ def main():
     L.profile_enable(False)
     kstats = L.profile_read()
     full = None
-    if args.workload not in ('frame_d', 'train'):  # the same steps with every mid-point evaluated
+    if args.workload not in ('frame_d', 'train') and not args.no_full_eval:  # every mid-point evaluated
         for _ in range(args.warmup):
             step_full()
         torch.cuda.synchronize()

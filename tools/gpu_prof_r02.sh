@@ -14,8 +14,9 @@ run() {  # tag, timeout, command...
   echo "$tag rc=$rc"; tail -2 $O/$tag/stdout.log | cut -c1-300
   return $rc
 }
-run b 300 python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
-run b_fp32 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --precision fp32 &&
+run b 300 python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-full-eval &&
+run b_full 300 python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
+run b_fp32 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-full-eval --precision fp32 &&
 run frame_d 400 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --workload frame_d &&
 run train 300 python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --workload train &&
 run configs 500 python3 tools/bench_frameworks.py --steps 3 --warmup 1 --configs &&
