@@ -200,8 +200,9 @@ typedef struct {
   int sample_only;
   float* d_all_out;
   /* Mid-points whose alpha is exactly 0 (the SDF does not decrease from sample i to i+1, neus.py:28-35)
-   * contribute w = 0 to every map; without NeRF++ and without the radiance output they skip the SDF
-   * and radiance nets (rgb / depth / mask / normals bit-identical).  no_mid_skip != 0: evaluate every
+   * contribute w = 0 to every map (with NeRF++, mid-points outside the bounding sphere take the
+   * background's colour instead); without the radiance output these skip the SDF and radiance nets
+   * (rgb / depth / mask / normals bit-identical).  no_mid_skip != 0: evaluate every
    * mid-point, as the reference does. */
   int no_mid_skip;
 } NrNeusArgs;

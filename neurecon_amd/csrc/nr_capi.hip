@@ -282,7 +282,7 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
     return rc;
   // SDF + nablas + geometry feature at the mid-points, then the radiance net (neus.py:103-106, :298)
   const int64_t Pm = (int64_t)(c.S - 1) * R;
-  if (a.N_outside > 0 || a.radiance_out || a.no_mid_skip) {  // every mid-point, as the reference
+  if (a.radiance_out || a.no_mid_skip) {  // every mid-point, as the reference
     if ((rc = launch_sdf(SL, a.sdf_packed, c.mids, Pm, c.sdf_m, c.nab_m, c.feat_m, a.sdf->multires, mlp_ws, mlp_bytes,
                          st)))
       return rc;

@@ -536,6 +536,12 @@ __global__ void neus_mid_compact(NeusChunk c, const float* __restrict__ s_dev, f
     const float cn = sigmoidf_ref(fmul(c.sdf_f[(int64_t)(i + 1) * R + r], s_inv));
     const float alpha = fmaxf(fdiv(fsub(cp, cn), fadd(cp, 1e-10f)), 0.0f);
     need = !(alpha == 0.0f);
+    if (need && c.N_out > 0) {  // NeRF++: a mid-point outside the bounding sphere takes the background's
+      const float dm = c.dmid[q];  // alpha and colour (neus_composite_outside's own inside test)
+      const float px = fadd(c.ro[r * 3], fmul(c.rd[r * 3], dm)), py = fadd(c.ro[r * 3 + 1], fmul(c.rd[r * 3 + 1], dm)),
+                  pz = fadd(c.ro[r * 3 + 2], fmul(c.rd[r * 3 + 2], dm));
+      need = norm3_ref(px, py, pz) <= c.r_obj;
+    }
   }
   const uint64_t bal = __ballot(need);
   const int lane = threadIdx.x & 63;

@@ -94,8 +94,9 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
                   upsample_algo='official_solution', N_nograd_samples=2048, N_upsample_iters=4,
                   skip_zero_alpha=True, **dummy_kwargs):
     """neus.py:118-397, render mode.  skip_zero_alpha (not a reference argument): mid-points whose alpha
-    is exactly 0 skip the SDF + radiance nets when no NeRF++ background and no radiance output are
-    asked for -- their weight is an exact 0, so rgb / depth / mask / normals are bit-identical;
+    is exactly 0 (and, with NeRF++, the ones outside the bounding sphere) skip the SDF + radiance nets
+    when the radiance output is not asked for -- their weight is an exact 0 (or their colour is the
+    background's), so rgb / depth / mask / normals are bit-identical;
     False evaluates every mid-point as the reference does.  rays_o/rays_d: [(B,) N_rays, 3]; rays_d need not be normalized.
     perturb=True draws the reference's uniforms (same generators, shapes and order) and hands them
     to the kernels."""
