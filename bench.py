@@ -30,6 +30,9 @@ MAC_SDF_FWD = 524_544             # SURVEY §8(a) A5 (incl. the 257-row last lay
 MAC_SDF_FWD_NOFEAT = 459_008      # the same without the 256 geometry-feature rows (sdf row only)
 MAC_SDF_BWD = 459_008             # SURVEY §8(a) A6 (reverse pass for the nablas)
 MAC_RAD = 271_360                 # SURVEY §8(a) A7, NeuS radiance input 289
+# NeRF++ background net (base.py:395-424, neus.py:38: input 4 -> 84 embedded, view 27, D=8 W=256,
+# skip at layer 5): 84*256 + 6*256*256 + 340*256 + feature 256*256 + alpha 256 + views 283*128 + rgb 128*3
+MAC_NERF = 604_160
 # reference algorithm per ray: 128 no-grad SDF + 255 SDF-with-nabla + 127 radiance.
 # This path evaluates each of the 128 samples once (SDF + nabla when it is drawn):
 # 128 + 127 SDF-with-nabla + 127 radiance; step_tflops counts that executed work.
@@ -176,7 +179,7 @@ def eager_gpu_baseline(dev, n_rays, reps=3):
 # MACs per unit (point) that each library kernel executes (SURVEY.md §8(a) layer shapes): launches
 # without the geometry feature skip its 256 rows of the last layer
 KERNEL_MAC = {'sdf_fwd': MAC_SDF_FWD_NOFEAT, 'sdf_feat': MAC_SDF_FWD, 'sdf_nabla': MAC_SDF_FWD_NOFEAT + MAC_SDF_BWD,
-              'sdf_nabla_feat': MAC_SDF_FWD + MAC_SDF_BWD, 'radiance': MAC_RAD}
+              'sdf_nabla_feat': MAC_SDF_FWD + MAC_SDF_BWD, 'radiance': MAC_RAD, 'nerf': MAC_NERF}
 
 
 def pmc_traffic(kernel, precision):
