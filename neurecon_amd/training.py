@@ -68,6 +68,19 @@ def _wgrad(g, h):
     return torch.bmm(g3.transpose(1, 2), h3).sum(0)
 
 
+def _wgrad2(g1, h1, g2, h2):
+    """g1^T h1 + g2^T h2 as one slab reduction: both split-K products land in one [2C, m, k] buffer"""
+    P = g1.shape[0]
+    C = 16
+    if P < 8192 or P % C:
+        return g1.t() @ h1 + g2.t() @ h2
+    buf = torch.empty(2 * C, g1.shape[1], h1.shape[1], device=g1.device, dtype=g1.dtype)
+    for i, (g, h) in enumerate(((g1, h1), (g2, h2))):
+        torch.bmm(g.contiguous().view(C, P // C, -1).transpose(1, 2), h.contiguous().view(C, P // C, -1),
+                  out=buf[i * C:(i + 1) * C])
+    return buf.sum(0)
+
+
 def _colsum(a):
     """a.sum(0) of a tall [P, n] gradient on the deterministic two-pass HIP reduction (nr_colsum): the
     generic column reduction took ~0.45 ms per [65536, 256] matrix, rocBLAS's GEMV ~1 ms"""
@@ -112,13 +125,13 @@ class SdfNabla(torch.autograd.Function):
         sdf = out[:, 0].contiguous()
         feat = out[:, 1:].contiguous() if want_feat else None
         # nabla chain: g_l = d sdf / d h_l, delta_l = s_l * g_l
-        gs = [None] * D
+        gs, deltas = [None] * D, [None] * D
         g = Ws[D][0:1, :].expand(h.shape[0], -1)
         e_skip = None
         e_first = None
         for l in range(D - 1, -1, -1):
             gs[l] = g.contiguous()
-            delta = _mul(ss[l], gs[l])
+            delta = deltas[l] = _mul(ss[l], gs[l])  # kept: the backward's tangent adjoint
             gin = delta @ Ws[l]
             if l in skips:
                 n_prev = Ws[l - 1].shape[0]
@@ -133,7 +146,7 @@ class SdfNabla(torch.autograd.Function):
                                      0 if e_skip is None else e_skip.shape[1], 1.0, x.shape[0], nfreq, L.ptr(nab),
                                      _st(x)))
         ctx.cfg = cfg
-        ctx.save_for_backward(x, *Ws, *hin, *ss, *gs)
+        ctx.save_for_backward(x, *Ws, *hin, *ss, *gs, *deltas)
         outs = (sdf, nab, feat) if want_feat else (sdf, nab)
         return outs
 
@@ -146,6 +159,7 @@ class SdfNabla(torch.autograd.Function):
         hin = saved[D + 2:2 * D + 3]
         ss = saved[2 * D + 3:3 * D + 3]
         gs = saved[3 * D + 3:4 * D + 3]
+        deltas = saved[4 * D + 3:5 * D + 3]
         g_feat = rest[0] if want_feat else None
         P = x.shape[0]
         dev = x.device
@@ -188,10 +202,10 @@ class SdfNabla(torch.autograd.Function):
                 L.check(lib.nr_softplus_adjoint(L.ptr(hbar), hbar.shape[1], L.ptr(ss[l]),
                                                 L.ptr(gs[l] if tangent else None), L.ptr(zdots[l]), P, n, L.ptr(zbar),
                                                 _st(x)))
-            dW[l] = _wgrad(zbar, hin[l])
-            if tangent:
-                delta = _mul(ss[l], gs[l])  # the tangent's adjoint (= the nabla chain's delta_l)
-                dW[l] += _wgrad(delta, hdins[l])
+            if tangent:  # + the tangent's adjoint (= the nabla chain's delta_l) against hdot
+                dW[l] = _wgrad2(zbar, hin[l], deltas[l], hdins[l])
+            else:
+                dW[l] = _wgrad(zbar, hin[l])
             db[l] = _colsum(zbar)
             if l > 0:
                 hb = zbar @ Ws[l]
