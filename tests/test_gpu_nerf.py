@@ -107,8 +107,9 @@ def test_neus_direct_more_with_nerfpp_vs_oracle(precision):
     assert same.mean() >= 0.8
 
 
+@pytest.mark.parametrize('perturb', [False, True])
 @pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
-def test_neus_nerfpp_compact_background_bit_identical(golden, precision):
+def test_neus_nerfpp_compact_background_bit_identical(golden, precision, perturb):
     """Without detailed outputs the NeRF++ net runs only on the samples the compositing reads (every
     outside sample, mid-points outside the bounding sphere; neus.py:325-343): rgb / depth / mask /
     normals must be bit-identical to the render that evaluates the background at every sample, on the
@@ -123,12 +124,14 @@ def test_neus_nerfpp_compact_background_bit_identical(golden, precision):
     ro = torch.cat([ro, ro[:, :1].repeat(1, 192, 1)], 1)
     rd = torch.cat([rd, rd2], 1)
     kw = dict(obj_bounding_radius=1.0, batched=True, calc_normal=True, N_samples=64, N_importance=64,
-              N_outside=32, N_upsample_iters=4)
-    with torch.no_grad():
+              N_outside=32, N_upsample_iters=4, perturb=perturb)
+    with torch.no_grad():  # perturb: both renders replay the same uniforms (same seed, same draws)
+        torch.manual_seed(11)
         rgb_c, dep_c, ex_c = volume_render(ro, rd, m, detailed_output=False, **kw)
+        torch.manual_seed(11)
         rgb_f, dep_f, ex_f = volume_render(ro, rd, m, detailed_output=True, **kw)
     torch.cuda.synchronize()
     for name, a, b in [('rgb', rgb_c, rgb_f), ('depth', dep_c, dep_f), ('mask', ex_c['mask_volume'], ex_f['mask_volume']),
                        ('normals', ex_c['normals_volume'], ex_f['normals_volume'])]:
         assert torch.equal(a, b), (name, float((a - b).abs().max()))
-    print(f'{precision}: compact-background render bit-identical on {rgb_c.shape[1]} rays')
+    print(f'{precision} perturb={perturb}: compact-background render bit-identical on {rgb_c.shape[1]} rays')
