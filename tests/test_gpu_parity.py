@@ -304,3 +304,32 @@ def test_neus_zero_alpha_skip_bit_identical(precision, perturb):
     for name, a, b in zip(('rgb', 'depth', 'mask', 'normals'), outs[0], outs[1]):
         assert torch.equal(a, b), (name, float((a - b).abs().max()))
     print(f'{precision} perturb={perturb}: zero-alpha skip bit-identical on 4096 rays')
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
+@pytest.mark.parametrize('algo,N_outside', [('direct_use', 0), ('direct_more', 0), ('official_solution', 32),
+                                            ('direct_use', 32)])
+def test_neus_zero_alpha_skip_algos_bit_identical(precision, algo, N_outside):
+    """The mid-point skip behind the other upsamplers (neus.py:215-243) and the NeRF++ background
+    (mid-points outside the bounding sphere also skip the surface nets): maps bit-identical to the
+    render that evaluates every mid-point, on 1024 config-(b) rays."""
+    from oracle import rays as orays
+    from neurecon_amd.frameworks.neus import volume_render
+    H, W, f, dist = wg.CAMERAS['b']
+    c2w = wg.look_at_c2w(dist)[None]
+    K = wg.intrinsics(f, H, W)[None]
+    ro, rd, _ = orays.get_rays(c2w, K, H, W)
+    ro, rd = ro[:, ::4].contiguous(), rd[:, ::4].contiguous()
+    nerf = N_outside > 0
+    m = neus_model(wg.neus_state(seed=1, use_outside_nerf=nerf), use_outside_nerf=nerf, precision=precision)
+    kw = dict(obj_bounding_radius=1.0, batched=True, calc_normal=True, detailed_output=False, perturb=False,
+              N_samples=64, N_importance=64, N_upsample_iters=4, upsample_algo=algo, N_outside=N_outside)
+    outs = []
+    for skip in (True, False):
+        with torch.no_grad():
+            rgb, depth, ex = volume_render(ro.cuda(), rd.cuda(), m, skip_zero_alpha=skip, **kw)
+        outs.append((rgb, depth, ex['mask_volume'], ex['normals_volume']))
+    torch.cuda.synchronize()
+    for name, a, b in zip(('rgb', 'depth', 'mask', 'normals'), outs[0], outs[1]):
+        assert torch.equal(a, b), (name, float((a - b).abs().max()))
+    print(f'{precision} {algo} N_outside={N_outside}: zero-alpha skip bit-identical on {rgb.shape[1]} rays')
