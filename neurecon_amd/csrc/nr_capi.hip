@@ -298,7 +298,8 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
     float* radc = (float*)(wsb + pl.o_mrad);
     NR_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int), st));
     const dim3 g1((unsigned)((Pm + 255) / 256));
-    hipLaunchKernelGGL(neus_mid_compact, g1, dim3(256), 0, st, c, a.s_dev, a.s, cnt, slot, midc, vdc);
+    hipLaunchKernelGGL(neus_mid_compact, dim3((unsigned)((Pm + 1023) / 1024)), dim3(1024), 0, st, c, a.s_dev, a.s, cnt,
+                       slot, midc, vdc);
     NR_HIP_CHECK(hipGetLastError());
     if ((rc = launch_sdf(SL, a.sdf_packed, midc, Pm, c.sdf_m, c.nab_m, c.feat_m, a.sdf->multires, mlp_ws, mlp_bytes,
                          st, cnt, 1)))
@@ -329,7 +330,8 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
       float* radc = (float*)(wsb + pl.o_radc);
       NR_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int), st));
       const dim3 g1((unsigned)((Po + 255) / 256));
-      hipLaunchKernelGGL(neus_outside_compact, g1, dim3(256), 0, st, c, cnt, slot, x4c, vdc);
+      hipLaunchKernelGGL(neus_outside_compact, dim3((unsigned)((Po + 1023) / 1024)), dim3(1024), 0, st, c, cnt, slot,
+                         x4c, vdc);
       NR_HIP_CHECK(hipGetLastError());
       if ((rc = launch_nerf(nerf_layout(*a.nerf), a.nerf_packed, x4c, vdc, 1, INT64_MAX, Po, sigc, radc, st, cnt)))
         return rc;

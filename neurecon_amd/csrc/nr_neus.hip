@@ -469,10 +469,34 @@ __global__ __launch_bounds__(64) void neus_outside_points(NeusChunk c, const flo
   }
 }
 
+// Workgroup-aggregated append (blockDim.x a multiple of 64, at most 1024): one atomicAdd per
+// workgroup instead of one per wave -- the per-wave atomics on the one counter serialised (~8 ns
+// each, 8 k of them per config-(b) mid-point pass).  Returns the lane's compact index when need.
+// Every thread of the block must call it (barriers inside).
+__device__ __forceinline__ int64_t block_append(bool need, int* __restrict__ count) {
+  __shared__ int wcnt[16];
+  __shared__ int bbase;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint64_t bal = __ballot(need);
+  if (lane == 0) wcnt[w] = __popcll(bal);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int i = 0; i < nw; ++i) {
+      const int v = wcnt[i];
+      wcnt[i] = t;
+      t += v;
+    }
+    bbase = t ? atomicAdd(count, t) : 0;
+  }
+  __syncthreads();
+  return (int64_t)bbase + wcnt[w] + __popcll(bal & ((1ull << lane) - 1ull));
+}
+
 // The background values the compositing reads (neus.py:325-343): every inverted-sphere sample, and the
 // mid-points outside the bounding sphere -- the ones inside take the SDF's alpha and radiance, so the
 // reference's background evaluation there is discarded.  Without detailed outputs only these points
-// go through the NeRF++ net: appended (one atomic per wave) to x4c / vdc, slot[q] = compact index or
+// go through the NeRF++ net: appended (one atomic per workgroup) to x4c / vdc, slot[q] = compact index or
 // -1; the inside test is the compositing's own (norm3_ref(o + d dm) <= r_obj).
 __global__ void neus_outside_compact(NeusChunk c, int* __restrict__ count, int* __restrict__ slot,
                                      float* __restrict__ x4c, float* __restrict__ vdc) {
@@ -494,17 +518,10 @@ __global__ void neus_outside_compact(NeusChunk c, int* __restrict__ count, int* 
       need = !(norm3_ref(px, py, pz) <= c.r_obj);
     }
   }
-  const uint64_t bal = __ballot(need);
-  const int lane = threadIdx.x & 63;
-  int base = 0;
-  if (bal) {
-    const int leader = __ffsll((unsigned long long)bal) - 1;
-    if (lane == leader) base = atomicAdd(count, __popcll(bal));
-    base = __shfl(base, leader);
-  }
+  const int64_t ja = block_append(need, count);
   if (!in_range) return;
   if (need) {
-    const int j = base + __popcll(bal & ((1ull << lane) - 1ull));
+    const int j = (int)ja;
     slot[q] = j;
     *(float4*)(x4c + (int64_t)j * 4) = *(const float4*)(c.x4 + q * 4);
     vdc[(int64_t)j * 3 + 0] = c.rd[r * 3 + 0];
@@ -543,17 +560,9 @@ __global__ void neus_mid_compact(NeusChunk c, const float* __restrict__ s_dev, f
       need = norm3_ref(px, py, pz) <= c.r_obj;
     }
   }
-  const uint64_t bal = __ballot(need);
-  const int lane = threadIdx.x & 63;
-  int base = 0;
-  if (bal) {
-    const int leader = __ffsll((unsigned long long)bal) - 1;
-    if (lane == leader) base = atomicAdd(count, __popcll(bal));
-    base = __shfl(base, leader);
-  }
+  const int64_t j = block_append(need, count);
   if (!in_range) return;
   if (need) {
-    const int64_t j = base + __popcll(bal & ((1ull << lane) - 1ull));
     slot[q] = (int)j;
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
