@@ -342,8 +342,13 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
     hipLaunchKernelGGL(neus_composite_outside, grd, blk, 0, st, c, o, a.s_dev, a.s, a.calc_normal, a.white_bkgd);
   } else {
     ProfScope prof("neus_composite", (double)R, st);
-    hipLaunchKernelGGL(neus_composite, dim3((unsigned)R), dim3(64), 8 * c.S * sizeof(float), st, c, o, a.s_dev, a.s,
-                       a.calc_normal, a.white_bkgd);
+    const size_t lds1 = 9 * (size_t)c.S * sizeof(float);  // four rays per wave when four rays' staging fits
+    if (4 * lds1 <= 65536)  // the dynamic-LDS limit per workgroup (nr_neus_render checks lds1 against it)
+      hipLaunchKernelGGL((neus_composite<4>), dim3((unsigned)((R + 3) / 4)), dim3(64), 4 * lds1, st, c, o, a.s_dev, a.s,
+                         a.calc_normal, a.white_bkgd);
+    else
+      hipLaunchKernelGGL((neus_composite<1>), dim3((unsigned)R), dim3(64), lds1, st, c, o, a.s_dev, a.s, a.calc_normal,
+                         a.white_bkgd);
   }
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;
@@ -842,7 +847,7 @@ int nr_neus_render(const NrNeusArgs* a, void* stream) {
     int dev = 0, lds_max = 65536;
     NR_HIP_CHECK(hipGetDevice(&dev));
     NR_HIP_CHECK(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
-    NR_REQUIRE((size_t)8 * S * sizeof(float) <= (size_t)lds_max, NR_ERR_UNSUPPORTED,
+    NR_REQUIRE((size_t)9 * S * sizeof(float) <= (size_t)lds_max, NR_ERR_UNSUPPORTED,
                "nr_neus_render: N_samples + N_importance too large for the per-ray LDS staging of the compositing");
   }
   for (int64_t r0 = 0; r0 < a->n_rays; r0 += Rc) {

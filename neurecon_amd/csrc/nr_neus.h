@@ -61,6 +61,7 @@ __global__ void neus_prologue(NeusChunk c, const float* rays_o, const float* ray
 __global__ void neus_upsample(NeusChunk c, int it, const float* u, int64_t u_stride);
 __global__ void neus_merge(NeusChunk c, int L, float* dv2, float* sv2, int* idv2);
 __global__ void neus_expand(NeusChunk c);
+template <int RPW>
 __global__ void neus_composite(NeusChunk c, NeusOut o, const float* s_dev, float s_val, int calc_normal, int white_bkgd);
 __global__ void neus_outside_points(NeusChunk c, const float* t_rand);
 __global__ void neus_outside_compact(NeusChunk c, int* count, int* slot, float* x4c, float* vdc);

@@ -256,34 +256,41 @@ __global__ void neus_expand(NeusChunk c) {
   }
 }
 
-// compositing (neus.py:296, :346-380), one wave per ray: logistic CDFs, alpha, radiance and unit
-// normals per sample across the lanes (LDS); the transmittance product and the fp64 rgb / acc /
-// normal / depth accumulations on lane 0 in sample order, exactly as the per-ray version did.
+// compositing (neus.py:296, :346-380), RPW rays per wave (64 / RPW lanes each): logistic CDFs,
+// alpha, radiance and unit normals per sample across the ray's lanes (LDS); the transmittance product
+// and the fp64 rgb / acc / normal / depth accumulations on the ray's first lane in sample order,
+// exactly as the per-ray version did.  RPW 4: the serial scans of four rays share one wave's issue.
 // s = exp(ln_s * speed_factor) (neus.py:108-109): *s_dev when given (device scalar, no host sync), else s_val
+template <int RPW>
 __global__ __launch_bounds__(64) void neus_composite(NeusChunk c, NeusOut o, const float* __restrict__ s_dev,
                                                      float s_val, int calc_normal, int white_bkgd) {
   extern __shared__ float lds[];
+  constexpr int NL = 64 / RPW;  // lanes per ray
   const float s_inv = s_dev ? *s_dev : s_val;
-  const int r = blockIdx.x, l = threadIdx.x;
+  const int r = blockIdx.x * RPW + (int)threadIdx.x / NL, l = (int)threadIdx.x % NL;
   const int S = c.S;
   const int64_t R = c.R;
+  const bool live = r < R;
+  const int Sl = live ? S : 0;    // a ray past the chunk's end only joins the barriers
   const int64_t ro = o.ray0 + r;  // global ray index for outputs
-  float* scdf = lds;          // [S]
+  float* scdf = lds + ((int)threadIdx.x / NL) * 9 * S;  // [S]
   float* sal = scdf + S;      // [S-1] alpha, then weights
   float* srad = sal + S;      // [S-1][3]
   float* snrm = srad + 3 * S; // [S-1][3] unit nablas
-  for (int i = l; i < S; i += 64) {
+  float* sdm = snrm + 3 * S;  // [S-1] mid-point depths (the serial depth sum reads LDS, not HBM)
+  for (int i = l; i < Sl; i += NL) {
     const float cdf = sigmoidf_ref(fmul(c.sdf_f[i * R + r], s_inv));
     scdf[i] = cdf;
     if (o.cdf) o.cdf[ro * S + i] = cdf;
   }
   __syncthreads();
-  for (int i = l; i < S - 1; i += 64) {
+  for (int i = l; i < Sl - 1; i += NL) {
     const float cp = scdf[i], cn = scdf[i + 1];
     const float alpha = fmaxf(fdiv(fsub(cp, cn), fadd(cp, 1e-10f)), 0.0f);
     sal[i] = alpha;
     if (o.alpha) o.alpha[ro * (S - 1) + i] = alpha;
     const int64_t q = i * R + r;
+    sdm[i] = c.dmid[q];
 #pragma unroll
     for (int e = 0; e < 3; ++e) srad[i * 3 + e] = c.rad_m[q * 3 + e];
     if (calc_normal) {
@@ -295,7 +302,7 @@ __global__ __launch_bounds__(64) void neus_composite(NeusChunk c, NeusOut o, con
     }
   }
   __syncthreads();
-  if (l == 0) {
+  if (l == 0 && live) {
     double T = 1.0, acc = 0.0, rgb0 = 0.0, rgb1 = 0.0, rgb2 = 0.0, n0 = 0.0, n1 = 0.0, n2 = 0.0;
     for (int i = 0; i < S - 1; ++i) {
       const float alpha = sal[i];
@@ -315,7 +322,7 @@ __global__ __launch_bounds__(64) void neus_composite(NeusChunk c, NeusOut o, con
     const float accf = (float)acc;
     const float denom = fadd(accf, 1e-10f);
     double depth = 0.0;
-    for (int i = 0; i < S - 1; ++i) depth += (double)fmul(fdiv(sal[i], denom), c.dmid[i * R + r]);
+    for (int i = 0; i < S - 1; ++i) depth += (double)fmul(fdiv(sal[i], denom), sdm[i]);
     float r0 = (float)rgb0, r1 = (float)rgb1, r2 = (float)rgb2;
     if (white_bkgd) {
       const float bg = fsub(1.0f, accf);
@@ -334,7 +341,7 @@ __global__ __launch_bounds__(64) void neus_composite(NeusChunk c, NeusOut o, con
   }
   __syncthreads();
   // detailed per-sample outputs, ray-major
-  for (int i = l; i < S; i += 64) {
+  for (int i = l; i < Sl; i += NL) {
     const int64_t q = i * R + r;
     if (o.sdf) o.sdf[ro * S + i] = c.sdf_f[q];
     if (o.nablas) {
@@ -353,6 +360,9 @@ __global__ __launch_bounds__(64) void neus_composite(NeusChunk c, NeusOut o, con
     }
   }
 }
+
+template __global__ void neus_composite<1>(NeusChunk, NeusOut, const float*, float, int, int);
+template __global__ void neus_composite<4>(NeusChunk, NeusOut, const float*, float, int, int);
 
 // ---------------------------------------------------------------------------------------------
 // 'direct_use' / 'direct_more' upsampling (neus.py:215-243): one sample_pdf of N_importance over
