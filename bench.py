@@ -1,14 +1,22 @@
 """Benchmark: NeuS volume rendering, 4096 rays x 128 samples, 8x256 SDF MLP (BASELINE.json).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL)
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...   (same layout)
 
 A step = one `volume_render` call (render mode: torch.no_grad, perturb=False, calc_normal=True,
 detailed_output=False) over one 4096-ray batch of the synthetic config-(b) camera (64x64 pixels,
 f=160, camera at distance 3 looking at a radius-0.5 geometric-init sphere; random-init weights of
 the configs/neus.yaml architecture -- no datasets offline).  Rays are already resident in HBM.
-Multi-GPU: every rank renders its own 4096-ray batch (weak scaling, no data-path collective);
-value = all ranks' rays / max-over-ranks time.  Prints one JSON line on rank 0.
+
+Multi-GPU: one process per GPU over RCCL.  Under torchrun the ranks come from its environment;
+`python bench.py --gpus N` alone spawns the N rank processes itself (before any GPU call) with the
+same environment.  n_gpus is the process group's size (asserted equal to --gpus).
+  * `value`: every rank renders its own 4096-ray batch (weak scaling, no data-path collective);
+    value = all ranks' rays / max-over-ranks time of K steps.
+  * `strong_scaling_frame_d`: one config-(d) 800x600 NeuS+NeRF++ frame per step, its rays split
+    over the ranks (neurecon_amd.dist.render_sharded) and the maps all-gathered inside the timed
+    region; rays/s of the frame at this N (strong scaling).
+Prints one JSON line on rank 0.
 """
 import argparse
 import json
@@ -49,7 +57,8 @@ PMC_KERNEL = {('sdf_nabla', 'f16x3'): ('void nr::sdf4_kernel<true, false>(nr::Sd
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None,
+                    help='number of GPUs (one process each); outside torchrun, N > 1 spawns the N rank processes')
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--rays', type=int, default=4096)
@@ -62,6 +71,10 @@ def parse():
                          "train: NeuS training step")
     ap.add_argument('--train-rays', type=int, default=512)
     ap.add_argument('--cpu-rays', type=int, default=1024)
+    ap.add_argument('--no-frame', action='store_true',
+                    help='skip the strong-scaling config-(d) frame leg of the default workload')
+    ap.add_argument('--frame-steps', type=int, default=3)
+    ap.add_argument('--stub-cpu', action='store_true', help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -331,17 +344,79 @@ def mid_frac(kstats, rays, steps):
     return round(kstats['sdf_nabla_feat'][2] / (127.0 * rays * steps), 4)
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _spawned_rank(rank, argv, world, port):
+    """worker process of `launch`: the torchrun environment for one rank, then the normal bench"""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    sys.argv = [sys.argv[0]] + list(argv)
+    run(parse())
+
+
+def launch(args):
+    """`python bench.py --gpus N` outside torchrun: start N rank processes (spawn: fresh interpreters,
+    started before this parent makes any GPU call) that join one process group, the same layout
+    torchrun gives (one process per GPU, LOCAL_RANK = GPU index).  A failing rank fails the launch."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_spawned_rank, args=(sys.argv[1:], args.gpus, _free_port()), nprocs=args.gpus, join=True,
+                       start_method='spawn')
+
+
+def timed(step, steps, warmup, sync, barrier):
+    """W untimed steps, then K steps bracketed by barrier + device sync on both sides"""
+    for _ in range(warmup):
+        step()
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    barrier()
+    return time.perf_counter() - t0
+
+
 def main():
     args = parse()
+    if 'WORLD_SIZE' not in os.environ and (args.gpus or 1) > 1:
+        return launch(args)
+    run(args)
+
+
+def run(args):
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     dist = world > 1
+    if args.stub_cpu:
+        return run_stub(args, world, rank)
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group('nccl')
+        tdist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        world = tdist.get_world_size()
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f'bench: --gpus {args.gpus} but the process group has {world} ranks')
     dev = torch.device('cuda', local)
+    sync = torch.cuda.synchronize
+    barrier = tdist.barrier if dist else (lambda: None)
+
+    def max_over_ranks(x):
+        if not dist:
+            return x
+        t = torch.tensor([x], device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        return float(t.item())
+
     from neurecon_amd import rend_util
     from neurecon_amd.frameworks.neus import volume_render
     if args.workload == 'frame_d':
@@ -369,51 +444,36 @@ def main():
                 return volume_render(ro, rd, model, skip_zero_alpha=False, **kw)
         n_rays = ro.shape[1] * world
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    torch.cuda.synchronize()
     from neurecon_amd import _lib as L
-    L.profile_read()           # drop warm-up records
-    L.profile_enable(True)     # per-kernel HIP events on the launch stream, inside the timed region
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    dt = time.perf_counter() - t0
-    L.profile_enable(False)
-    kstats = L.profile_read()
+
+    def profiled(fn):
+        """timed region with the library's per-kernel HIP events on the launch stream"""
+        for _ in range(args.warmup):
+            fn()
+        sync()
+        L.profile_read()           # drop warm-up records
+        L.profile_enable(True)
+        try:
+            dt = timed(fn, args.steps, 0, sync, barrier)
+        finally:
+            L.profile_enable(False)
+        return max_over_ranks(dt), L.profile_read()
+
+    dt, kstats = profiled(step)
     full = None
     if args.workload not in ('frame_d', 'train') and not args.no_full_eval:  # every mid-point evaluated
-        for _ in range(args.warmup):
-            step_full()
-        torch.cuda.synchronize()
-        if dist:
-            tdist.barrier()
-        L.profile_read()
-        L.profile_enable(True)
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
-            step_full()
-        torch.cuda.synchronize()
-        if dist:
-            tdist.barrier()
-        dt_full = time.perf_counter() - t1
-        L.profile_enable(False)
-        kstats_full = L.profile_read()
-        if dist:
-            t = torch.tensor([dt_full], device=dev)
-            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-            dt_full = float(t.item())
-        full = (dt_full, kstats_full)
-    if dist:
-        t = torch.tensor([dt], device=dev)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        dt = float(t.item())
+        full = profiled(step_full)
+    frame = None
+    if args.workload == 'b' and not args.no_frame:
+        # strong scaling: one config-(d) 800x600 frame per step split over all ranks, all_gather timed
+        fstep, frame_rays = frame_d_setup(dev, args.precision)
+        fdt = max_over_ranks(timed(fstep, args.frame_steps, 1, sync, barrier))
+        frame = {'metric': 'rays/sec, config (d): NeuS+NeRF++ full 800x600 frame per step, rays sharded over '
+                           'the GPUs (render_sharded + all_gather of the maps inside the timed region)',
+                 'value': round(frame_rays * args.frame_steps / fdt, 1), 'unit': 'rays/s', 'n_gpus': world,
+                 'steps': args.frame_steps, 'warmup': 1, 'ms_per_step': round(fdt / args.frame_steps * 1e3, 3),
+                 'scaling': 'strong', 'rays_per_step': frame_rays, 'rays_per_gpu': frame_rays // world,
+                 'parallelism': f'ray-sharded x{world} + all_gather'}
     total_rays = n_rays * args.steps
     value = total_rays / dt
     if rank == 0:
@@ -464,6 +524,8 @@ def main():
                             'the SDF + radiance nets as the reference does, including the ones whose alpha is exactly 0',
                     'value': round(total_rays / dtf, 1), 'ms_per_step': round(dtf / args.steps * 1e3, 3),
                     'step_tflops': round(executed_flop(kf) / dtf / 1e12, 2), 'roofline': roofline(kf, args.precision)}
+            if frame is not None:
+                out['strong_scaling_frame_d'] = frame
             out['config']['zero_alpha_skip'] = ('mid-points whose alpha is exactly 0 (no SDF decrease between the '
                                                 'two samples, neus.py:28-35) get weight 0 and skip the nets; '
                                                 'rgb/depth/mask/normals bit-identical to full evaluation')
@@ -473,6 +535,35 @@ def main():
                 eg['speedup'] = round(value / eg['value'], 2)
                 out['cpu_baseline']['eager_gpu_reference'] = eg
         print(json.dumps(out), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+def run_stub(args, world, rank):
+    """CPU rehearsal of the launcher and the timing protocol (tests/test_bench_launch.py): gloo process
+    group, a small matmul as the step, the same barrier / max-over-ranks / one-line JSON contract."""
+    import torch.distributed as tdist
+    dist = world > 1
+    if dist:
+        tdist.init_process_group('gloo')
+        world = tdist.get_world_size()
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f'bench: --gpus {args.gpus} but the process group has {world} ranks')
+    a = torch.randn(64, 64)
+    barrier = tdist.barrier if dist else (lambda: None)
+    dt = timed(lambda: a @ a, args.steps, args.warmup, lambda: None, barrier)
+    ranks = [rank]
+    if dist:
+        t = torch.tensor([dt])
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+        got = [None] * world
+        tdist.all_gather_object(got, rank)
+        ranks = got
+    if rank == 0:
+        print(json.dumps({'metric': 'stub', 'value': args.steps * world / dt, 'unit': 'steps/s', 'n_gpus': world,
+                          'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3,
+                          'ranks': ranks, 'pid': os.getpid()}), flush=True)
     if dist:
         tdist.destroy_process_group()
 

@@ -247,13 +247,17 @@ _WS = {}
 
 
 def workspace(device, nbytes):
-    """Scratch for one library call, reused across calls on the device (grow-only): calls are
-    ordered on the caller's stream, so one buffer per device serves them all."""
-    key = str(device)
+    """Scratch for one library call, reused across calls (grow-only) on the same device AND stream:
+    calls enqueued on one stream are ordered, so they can share one buffer; a render on another stream
+    (e.g. a side-stream validation render beside training) gets its own.  A buffer outgrown on its
+    stream is freed through the caching allocator, which reuses the block only in that stream's order.
+    DataParallel replica threads run on their own devices' streams, so they never share a buffer."""
+    dev = torch.device(device)
+    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
     buf = _WS.get(key)
     if buf is None or buf.numel() < nbytes:
         _WS.pop(key, None)
-        buf = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+        buf = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
         _WS[key] = buf
     return buf
 

@@ -103,8 +103,23 @@ def _wn_params(layers):
     return Ws, bs
 
 
+_PARAM_ATTRS = ('weight_v', 'weight_g', 'weight', 'bias')
+
+
 def _version_key(module, precision, device):
-    return (str(device), precision) + tuple((p.data_ptr(), p._version) for p in module.parameters())
+    """Identity of the weights a packed copy was made from: (storage, version) of every layer tensor.
+    Read from the layers' attributes rather than module.parameters(): an nn.DataParallel replica
+    (neus.py:413-414) holds its broadcast copies as plain attributes and has no parameters, so its key
+    names its own copies and a pack made on one device is never served to another."""
+    key = [str(device), precision]
+    for m in module.modules():
+        for name in _PARAM_ATTRS:
+            t = m.__dict__.get(name, None)
+            if t is None:
+                t = m._parameters.get(name, None)
+            if isinstance(t, torch.Tensor):
+                key.append((t.data_ptr(), t._version))
+    return tuple(key)
 
 
 def _ptr_array(ts):

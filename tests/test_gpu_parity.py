@@ -93,6 +93,25 @@ def _neus_render(m, ro, rd, **kw):
                              upsample_algo='official_solution', N_upsample_iters=4, **kw)
 
 
+def _bench_render(m, ro, rd):
+    """the call bench.py times: detailed_output=False, which turns the zero-alpha mid-point skip on"""
+    from neurecon_amd.frameworks.neus import volume_render
+    with torch.no_grad():
+        return volume_render(ro, rd, m, obj_bounding_radius=1.0, batched=True, calc_normal=True,
+                             detailed_output=False, perturb=False, N_samples=64, N_importance=64,
+                             upsample_algo='official_solution', N_upsample_iters=4)
+
+
+def _assert_bench_call_equal(detailed, bench, tag):
+    """rgb / depth / mask / normals of the benchmarked call are the detailed render's, bit for bit"""
+    rgb, depth, ex = detailed
+    rgb_b, depth_b, ex_b = bench
+    for name, a, b in [('rgb', rgb_b, rgb), ('depth', depth_b, depth), ('mask', ex_b['mask_volume'], ex['mask_volume']),
+                       ('normals', ex_b['normals_volume'], ex['normals_volume'])]:
+        assert torch.equal(a, b), (tag, name, float((a - b).abs().max()))
+    print(f'{tag}: benchmarked call (detailed_output=False, zero-alpha skip) bit-identical to the detailed render')
+
+
 def test_neus_render_vs_golden(golden):
     """64 rays of config (b) vs the reference.  rgb/depth/mask must meet the bar on every ray.
     Per-sample values are compared on the rays whose samples did not move: the upsampling's
@@ -105,14 +124,14 @@ def test_neus_render_vs_golden(golden):
     same = ok_d.reshape(ok_d.shape[-2], -1).all(-1)
     print(f'rays with identical samples: {same.sum()} / {same.size}')
     # the reference itself keeps identical samples on only ~85% of config-(b) rays when its SDF is
-    # perturbed by 1e-7 relative noise ("Parity"); require a clear majority here
-    assert same.mean() >= 0.6
+    # perturbed by 1e-7 relative noise ("Parity"); observed here: 0.70 (r02)
+    assert same.mean() >= 0.65
     # per-sample values: rays whose depths agree to 1e-6 relative (d <= 3 -> |dd| <= 3e-6); the
     # sampled field moves by |grad| * |dd| <= ~5e-6 there, so sdf / radiance / weights get atol 1e-5
     dd = np.abs(ex['d_final'].cpu().numpy() - g['d_final'])
     tight = (dd <= 1e-6 * np.abs(g['d_final'])).all(-1).reshape(-1)
     print(f'rays with depths within 1e-6: {tight.sum()} / {tight.size}')
-    assert tight.mean() >= 0.3
+    assert tight.mean() >= 0.55
     sel = lambda t: (t.cpu().numpy() if isinstance(t, torch.Tensor) else t)[0][tight]
     assert report('sdf (same-sample rays)', sel(ex['implicit_surface']), sel(g['sdf']), RT, 1e-5)[0].all()
     assert report('nablas (same-sample rays)', sel(ex['implicit_nablas']), sel(g['nablas']), RT, 1e-4)[0].all()
@@ -139,6 +158,7 @@ def test_neus_full_config_b_vs_oracle():
         ref = NeuSOracle(sd).render(ro, rd)
     m = neus_model(sd)
     rgb, depth, ex = _neus_render(m, ro.cuda(), rd.cuda())
+    _assert_bench_call_equal((rgb, depth, ex), _bench_render(m, ro.cuda(), rd.cuda()), 'fp32 config (b)')
     ok_rgb, _ = report('rgb', rgb, ref['rgb'], RT, AT)
     ok_dep, _ = report('depth', depth, ref['depth_volume'], RT, AT)
     ok_n, _ = report('normals', ex['normals_volume'], ref['normals_volume'], RT, 1e-4)
@@ -187,6 +207,9 @@ def test_f16x3_neus_full_config_b_vs_oracle():
         ref = NeuSOracle(sd).render(ro, rd)
     m = neus_model(sd, precision='f16x3')
     rgb, depth, ex = _neus_render(m, ro.cuda(), rd.cuda())
+    # the benchmarked call (bench.py) is the detailed render bit for bit, so the oracle check below
+    # holds it too
+    _assert_bench_call_equal((rgb, depth, ex), _bench_render(m, ro.cuda(), rd.cuda()), 'f16x3 config (b)')
     ok_rgb, _ = report('f16x3 rgb', rgb, ref['rgb'], RT, AT)
     ok_dep, _ = report('f16x3 depth', depth, ref['depth_volume'], RT, AT)
     ok_m, _ = report('f16x3 mask', ex['mask_volume'], ref['mask_volume'], RT, AT)
@@ -333,3 +356,63 @@ def test_neus_zero_alpha_skip_algos_bit_identical(precision, algo, N_outside):
     for name, a, b in zip(('rgb', 'depth', 'mask', 'normals'), outs[0], outs[1]):
         assert torch.equal(a, b), (name, float((a - b).abs().max()))
     print(f'{precision} {algo} N_outside={N_outside}: zero-alpha skip bit-identical on {rgb.shape[1]} rays')
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
+def test_neus_ray_counts_not_multiple_of_four(precision):
+    """neus_composite packs four rays per wave (16 lanes each); a block's tail lanes are dead when
+    n_rays % 4 != 0.  Ray counts = 1, 2, 3 (mod 4) in one call and as separate calls: bit-identical
+    maps (and the benchmarked call's skip path identical to the detailed render)."""
+    from oracle import rays as orays
+    H, W, f, dist = wg.CAMERAS['b']
+    ro, rd, _ = orays.get_rays(wg.look_at_c2w(dist)[None], wg.intrinsics(f, H, W)[None], H, W)
+    ro, rd = ro[:, 1500:1500 + 1027].contiguous().cuda(), rd[:, 1500:1500 + 1027].contiguous().cuda()  # 1027 = 3 mod 4
+    m = neus_model(wg.neus_state(seed=1), precision=precision)
+    whole = _bench_render(m, ro, rd)
+    _assert_bench_call_equal(_neus_render(m, ro, rd), whole, f'{precision} 1027 rays')
+    cuts = [(0, 513), (513, 1027)]                       # 513 = 1 mod 4, 514 = 2 mod 4
+    parts = [_bench_render(m, ro[:, a:b].contiguous(), rd[:, a:b].contiguous()) for a, b in cuts]
+    single = [_bench_render(m, ro[:, a:a + 1].contiguous(), rd[:, a:a + 1].contiguous()) for a in (0, 700, 1026)]
+    torch.cuda.synchronize()
+    for name, k in [('rgb', 0), ('depth', 1)]:
+        assert torch.equal(whole[k], torch.cat([p[k] for p in parts], 1)), name
+        for a, p in zip((0, 700, 1026), single):
+            assert torch.equal(whole[k][:, a:a + 1], p[k]), (name, a)
+    for name in ('mask_volume', 'normals_volume'):
+        assert torch.equal(whole[2][name], torch.cat([p[2][name] for p in parts], 1)), name
+    print(f'{precision}: 1027 / 513 / 514 / 1-ray renders bit-identical')
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
+def test_neus_many_samples_composite_fallback_vs_oracle(precision):
+    """N_samples + N_importance > 455 samples per ray: the compositing runs its one-ray-per-wave variant
+    (the four-rays-per-wave kernel keeps 4 x S mid-point depths in LDS).  64 config-(b) rays with
+    448 + 64 samples vs the oracle, with the 'only a flipped sampling decision' invariant."""
+    from oracle.neus import NeuSOracle
+    from oracle import rays as orays
+    from neurecon_amd.frameworks.neus import volume_render
+    H, W, f, dist = wg.CAMERAS['b']
+    ro, rd, _ = orays.get_rays(wg.look_at_c2w(dist)[None], wg.intrinsics(f, H, W)[None], H, W)
+    ro, rd = ro[:, 1000:3000:32].contiguous(), rd[:, 1000:3000:32].contiguous()
+    sd = wg.neus_state(seed=1)
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    with torch.no_grad():
+        ref = NeuSOracle(sd).render(ro, rd, N_samples=448, N_importance=64)
+    m = neus_model(sd, precision=precision)
+    kw = dict(obj_bounding_radius=1.0, batched=True, calc_normal=True, perturb=False, N_samples=448, N_importance=64,
+              upsample_algo='official_solution', N_upsample_iters=4)
+    with torch.no_grad():
+        det = volume_render(ro.cuda(), rd.cuda(), m, detailed_output=True, **kw)
+        bench = volume_render(ro.cuda(), rd.cuda(), m, detailed_output=False, **kw)
+    _assert_bench_call_equal(det, bench, f'{precision} S=512')
+    rgb, depth, ex = det
+    assert ex['d_final'].shape[-1] == 511
+    ok_rgb, _ = report(f'{precision} S=512 rgb', rgb, ref['rgb'], RT, AT)
+    ok_dep, _ = report(f'{precision} S=512 depth', depth, ref['depth_volume'], RT, AT)
+    ok_n, _ = report(f'{precision} S=512 normals', ex['normals_volume'], ref['normals_volume'], RT, 1e-4)
+    ray_ok = (ok_rgb.all(-1) & ok_dep).reshape(-1)
+    d_same = (np.abs(ex['d_final'].cpu().numpy() - ref['d_final'].numpy()) <= 1e-5).all(-1).reshape(-1)
+    print(f'{precision} S=512: per-ray pass {ray_ok.mean() * 100:.1f}%, identical samples {d_same.mean() * 100:.1f}%')
+    assert (~ray_ok & d_same).sum() == 0
+    assert (~ok_n.all(-1).reshape(-1) & d_same).sum() == 0
+    assert d_same.mean() >= 0.5

@@ -1,0 +1,136 @@
+"""GPU coverage of the training ray batch: random-pixel get_rays, the target
+gather, and a NeuS training step on a random 512-ray batch (configs/neus.yaml: data.N_rays 512).
+
+The reference draws the pixels with torch's CPU generator (rend_util.py:137-138:
+randint(H) * W + randint(W)); neurecon_amd.rend_util.get_rays makes the same draws, so a seeded call
+replays the reference's batch bit for bit (golden `get_rays.npz`: torch.manual_seed(5), N_rays=37)."""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+import weightgen as wg
+from helpers import neus_model, report, to_gpu
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from neurecon_amd import _lib
+    _lib.lib()
+
+
+def test_get_rays_random_pixels_vs_golden(golden):
+    """rend_util.py:130-142: the reference's seeded random-pixel batch, replayed (indices identical,
+    rays_o bit-exact, rays_d at the full-grid test's bar)."""
+    from neurecon_amd import rend_util
+    g = golden('get_rays')
+    H, W = int(g['H']), int(g['W'])
+    torch.manual_seed(5)
+    ro, rd, si = rend_util.get_rays(to_gpu(g['c2w']), to_gpu(g['K']), H, W, N_rays=37)
+    assert si.dtype == torch.int64 and tuple(si.shape) == g['select_inds'].shape
+    assert np.array_equal(si.cpu().numpy(), g['select_inds'])
+    assert report('rays_o (random pixels)', ro, g['rays_o_sel'], 0, 0)[0].all()
+    assert report('rays_d (random pixels)', rd, g['rays_d_sel'], 1e-6, 1e-7)[0].all()
+    # the selected rays are rows of the full-grid rays
+    full_o, full_d, _ = rend_util.get_rays(to_gpu(g['c2w']), to_gpu(g['K']), H, W)
+    idx = si[0]
+    assert torch.equal(ro[0], full_o[0, idx]) and torch.equal(rd[0], full_d[0, idx])
+
+
+@pytest.mark.parametrize('dtype,tail', [(torch.float32, (3,)), (torch.bool, ()), (torch.float32, ()),
+                                        (torch.uint8, (5,)), (torch.float64, (2,))])
+def test_gather_rays_random_indices(dtype, tail):
+    """neus.py:432-438 target gather (torch.gather of rgb / masks by select_inds) on nr_gather_rows:
+    identical to torch.gather for every row width, two batch rows with their own indices, repeated
+    indices and the first / last pixel."""
+    from neurecon_amd import rend_util
+    B, HW, N = 2, 64 * 48, 1031
+    g = torch.Generator().manual_seed(4)
+    if dtype == torch.bool:
+        src = torch.rand(B, HW, *tail, generator=g) > 0.5
+    elif dtype == torch.uint8:
+        src = torch.randint(0, 256, (B, HW, *tail), generator=g).to(torch.uint8)
+    else:
+        src = torch.randn(B, HW, *tail, generator=g).to(dtype)
+    idx = torch.randint(0, HW, (B, N), generator=g)
+    idx[0, 0], idx[1, -1], idx[1, 5] = 0, HW - 1, idx[1, 4]
+    out = rend_util.gather_rays(src.cuda(), idx.cuda())
+    ref = torch.gather(src, 1, idx.reshape(B, N, *([1] * len(tail))).expand(B, N, *tail))
+    assert out.dtype == src.dtype and tuple(out.shape) == tuple(ref.shape)
+    assert torch.equal(out.cpu(), ref)
+
+
+def _train_kw(H, W):
+    return dict(H=H, W=W, upsample_algo='official_solution', N_nograd_samples=2048, N_upsample_iters=4, N_outside=0,
+                obj_bounding_radius=1.0, batched=True, perturb=False, white_bkgd=False)
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
+def test_neus_train_step_random_batch_vs_oracle(precision):
+    """One NeuS Trainer.forward + backward on a random 512-ray batch of the config-(b) image: the drawn
+    pixels replay torch's CPU generator, and the losses and every parameter gradient match the oracle's
+    autograd (pinned to the reference's Trainer by test_oracle_train_step_vs_golden) on the same
+    pixels, targets and sample depths.  Bar as tests/test_gpu_train.py: losses 1e-5 relative, gradients
+    1e-4 |ref| + 1e-5 max|ref| per tensor."""
+    from neurecon_amd.frameworks.neus import Trainer, _sample_depths
+    from neurecon_amd import rend_util
+    from oracle import rays as orays
+    from oracle.train import neus_train_losses
+    H, W, f, dist = wg.CAMERAS['b']
+    c2w, K = wg.look_at_c2w(dist)[None], wg.intrinsics(f, H, W)[None]
+    sd = wg.neus_state(seed=1)
+    gen = torch.Generator().manual_seed(2)
+    tgt_rgb = torch.rand(1, H * W, 3, generator=gen)
+    tgt_mask = torch.rand(1, H * W, generator=gen) > 0.5
+    m = neus_model(sd, precision=precision)
+    m.train()
+    args = types.SimpleNamespace(data=types.SimpleNamespace(N_rays=512),
+                                 training=types.SimpleNamespace(w_eikonal=0.1, w_mask=1.0, with_mask=True))
+    torch.manual_seed(9)
+    ret = Trainer(m, device_ids=[0]).forward(args, None, {'intrinsics': K.cuda(), 'c2w': c2w.cuda(),
+                                                          'object_mask': tgt_mask.cuda()},
+                                             {'rgb': tgt_rgb.cuda()}, _train_kw(H, W), 0, device='cuda')
+    si = ret['extras']['select_inds'].cpu()
+    torch.manual_seed(9)
+    hs, ws = torch.randint(0, H, size=[512]), torch.randint(0, W, size=[512])
+    assert torch.equal(si.reshape(-1), hs * W + ws), 'random pixels do not replay the CPU generator'
+    losses = {k: torch.mean(v) for k, v in ret['losses'].items()}
+    m.zero_grad()
+    losses['total'].backward()
+    torch.cuda.synchronize()
+    grads = {k: p.grad.detach().cpu() for k, p in m.named_parameters() if p.grad is not None}
+    # the GPU's sample depths for these rays (the no-grad sampling decisions), handed to the oracle
+    ro_g, rd_g, _ = rend_util.get_rays(c2w.cuda(), K.cuda(), H, W)
+    ro_g, rd_g = ro_g[0, si[0].cuda()].contiguous(), rd_g[0, si[0].cuda()].contiguous()
+    with torch.no_grad():
+        d_all, _ = _sample_depths(ro_g, rd_g, m, ro_g.device, 1.0, True, 1, 65536, None, None, False, 1 / 64., 64, 64,
+                                  'official_solution', 2048, 4)
+    d_all = d_all.reshape(1, 512, -1).cpu()
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    sdp = {k: v.clone().requires_grad_(v.is_floating_point() and k != 'implicit_surface.obj_bounding_size')
+           for k, v in sd.items()}
+    ro, rd, _ = orays.get_rays(c2w, K, H, W, select_inds=si)
+    t_rgb = torch.gather(tgt_rgb, 1, si[..., None].expand(1, 512, 3))
+    t_mask = torch.gather(tgt_mask, 1, si)
+    ref_losses, _ = neus_train_losses(sdp, ro, rd, t_rgb, t_mask, d_all=d_all)
+    ref_losses['total'].backward()
+    for k in ('loss_img', 'loss_eikonal', 'loss_mask', 'total'):
+        a, b = float(losses[k]), float(ref_losses[k])
+        print(f'{precision} {k}: gpu {a:.8f} oracle {b:.8f}')
+        assert abs(a - b) <= 1e-5 * abs(b) + 1e-7
+    worst = 0.0
+    for k, v in sdp.items():
+        if v.grad is None:
+            continue
+        ref, mine = v.grad.double(), grads[k].double()
+        scale = float(ref.abs().max()) + 1e-30
+        err = (mine - ref).abs()
+        ok = err <= 1e-4 * ref.abs() + 1e-5 * scale
+        worst = max(worst, float(err.max()) / scale)
+        assert bool(ok.all()), (k, float(err.max()), scale)
+    print(f'{precision}: 512-ray batch, worst gradient error / tensor scale {worst:.3e}')
