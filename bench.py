@@ -152,6 +152,10 @@ def cpu_baseline(n_rays, reps=3):
     cpu = host_cpu()
     return {'value': round(n_rays / dt, 2), 'unit': 'rays/s', 'cores': threads, 'kind': 'port',
             'host_cpu': cpu,
+            'cores_note': 'BASELINE.md section 3 asks for all host cores; the GPU lease grants one GPU\'s CPU share '
+                          f'(OMP_NUM_THREADS={os.environ.get("OMP_NUM_THREADS", "unset")} is set by the box, which '
+                          'forbids using more: the other cores belong to the other GPUs\' jobs), so the oracle runs '
+                          'on that many threads; lscpu\'s count is the whole machine',
             'sample': f'{n_rays} of the 4096 config-(b) rays (evenly spaced), oracle/neus.py, torch {torch.__version__} '
                       f'CPU fp32, {threads} threads of {cpu.get("CPU(s)", "?")} logical CPUs '
                       f'({cpu.get("Model name", "?")}), warm-up + median of {reps}: {dt:.2f} s per run'}

@@ -122,6 +122,9 @@ int check_nerf_desc(const NrNerfDesc* d) {
 static const int kNerfKB[kNerfOps] = {6, 16, 16, 16, 16, 22, 16, 16, 16, 18};
 static const int kNerfNBO[kNerfOps] = {16, 16, 16, 16, 16, 16, 16, 16, 16, 8};
 
+// output blocks of NeRF op i: f16x3's NF also carries alpha_linear (blocks 16-17, row 0 = sigma)
+static int nerf_nbo(int i, int prec) { return (i == NF && prec == NR_PREC_F16X3) ? 18 : kNerfNBO[i]; }
+
 NerfLayout nerf_layout(const NrNerfDesc& d) {
   NerfLayout L{};
   L.prec = d.precision;
@@ -129,10 +132,12 @@ NerfLayout nerf_layout(const NrNerfDesc& d) {
   for (int i = 0; i < kNerfOps; ++i) {
     L.op_bytes[i] = (2 * kNerfKB[i] + 1) * 1024;
     L.op_off[i] = (uint32_t)off;
-    off += (size_t)(kNerfNBO[i] / 2) * L.op_bytes[i];
+    off += (size_t)(nerf_nbo(i, d.precision) / 2) * L.op_bytes[i];
   }
   L.scale_off = (uint32_t)off;
   off = align256(off + kNerfOps * 4);
+  L.bound_off = (uint32_t)off;
+  off = align256(off + kNerfOps * 2 * 4);
   L.alpha_off = (uint32_t)off;
   off = align256(off + 257 * 4);
   L.rgb_off = (uint32_t)off;
@@ -740,11 +745,23 @@ int nr_nerf_pack(const NrNerfDesc* d, const float* const* W, const float* const*
     else
       ops[i] = mkop(W[i], b[i], 256, 256, 0, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + i);
   }
-  ops[NF] = mkop(W[8], b[8], 256, 256, 0, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + NF);
+  if (prec == NR_PREC_F16X3) {  // [feature_linear; alpha_linear]: sigma = row 0 of output block 16
+    ops[NF] = mkop(W[8], b[8], 256, 256, 0, seg(16, 0, 256), seg(2, 0, 1), seg(16, 0, 256), none(), 1.0f, prec,
+                   wmax + NF);
+    ops[NF].W2 = W[10];
+    ops[NF].bias2 = b[10];
+    ops[NF].wn2 = 256;
+    ops[NF].ld2 = 256;
+  } else {
+    ops[NF] = mkop(W[8], b[8], 256, 256, 0, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + NF);
+  }
   ops[NV] = mkop(W[9], b[9], 128, 256 + inv, 0, seg(8, 0, 128), none(), seg(16, 0, 256), seg(2, 256, inv), 1.0f, prec,
                  wmax + NV);
-  for (int i = 0; i < kNerfOps; ++i)
+  float* bound = (float*)(P + L.bound_off);
+  for (int i = 0; i < kNerfOps; ++i) {
+    ops[i].bound = bound + 2 * i;
     if ((rc = launch_pack_op(ops[i], P + L.op_off[i], st))) return rc;
+  }
   if ((rc = launch_pack_vec(W[10], 0, 256, 256, P + L.alpha_off, st))) return rc;
   if ((rc = launch_pack_vec(b[10], 0, 1, 1, P + L.alpha_off + 256 * 4, st))) return rc;
   if ((rc = launch_pack_vec(W[11], 0, 384, 384, P + L.rgb_off, st))) return rc;

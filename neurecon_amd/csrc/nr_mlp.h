@@ -61,12 +61,14 @@ struct RadLayout {
 
 // NeRF++ background MLP (models/base.py:395-453): 8 x (Linear+ReLU) with the input re-injected
 // after layer 4, sigma head, feature Linear, view branch Linear(256+27 -> 128)+ReLU, rgb head.
+// f16x3 (nerf4_kernel): NF carries alpha_linear as output blocks 16-17 (row 0 = sigma), 9 chunks.
 enum NerfOp { N0, N1, N2, N3, N4, N5, N6, N7, NF, NV, kNerfOps };
 
 struct NerfLayout {
   uint32_t op_off[kNerfOps];
   uint32_t op_bytes[kNerfOps];
   uint32_t scale_off;  // [kNerfOps] max |W| per op
+  uint32_t bound_off;  // [kNerfOps][2] max row L1 norm, max |bias| per op (nerf4_kernel's operand scales)
   uint32_t alpha_off;  // [256] weights, [256] = bias
   uint32_t rgb_off;    // [3][128] weights, then [3] bias
   uint32_t total;
@@ -92,6 +94,10 @@ struct PackOp {
   float* wmax;         // device word receiving max |W * scale| (f16x3 scaling)
   const float* aux;    // optional per-output-row vector written to bias-slot floats 64..95 of each chunk
   float* bound;        // optional [2]: max over output rows of sum |W * scale|, max |bias|
+  const float* W2;     // optional second matrix [rows][ld2] (not transposed) for the rows of out[1]
+  const float* bias2;  //   ... and its bias
+  int64_t wn2;
+  int ld2;
 };
 
 int launch_pack_op(const PackOp& op, char* dst, hipStream_t stream);

@@ -19,6 +19,7 @@
 #include <type_traits>
 #include "nr_common.h"
 #include "nr_mlp.h"
+#include "nr_tgemm.h"
 
 namespace nr {
 
@@ -2336,6 +2337,555 @@ __global__ __launch_bounds__(kThreads) void nerf_kernel(NerfKArgs a) {
 }
 
 // =============================================================================================
+// NeRF++ background net on the v3 pipeline (nerf4_kernel, f16x3): the rad4 / sdf4 structure
+// (128-point tile, kNC-column waves, weight ring by LDS-DMA two chunks ahead, per-chunk operand split
+// at a scale fixed from the op's pack-time bound, epilogues staged beside the next chunk's MFMAs) on
+// models/base.py:426-453:
+//   N0 (embed(x4): 84 -> 256) .. N4, ReLU;  N5 on cat([h4, embed(x4)]) (base.py:431-432);  N6, N7;
+//   NF = [feature_linear; alpha_linear](h7): 256 feature rows (no activation) + sigma as row 0 of a
+//   9th chunk (an alpha dot product riding N7's epilogue held 8 more registers and spilled);
+//   NV on cat([feature, embed_view(v)]) -> 128, ReLU, with rgb_linear (128 -> 3) + sigmoid in its
+//   epilogue.
+// The 84-wide embedding stays in registers (fp32) from N0 until N5 re-splits it at N4's output scale;
+// the view embedding is built just before NF and split at NF's output scale.
+// =============================================================================================
+// identity op (feature_linear, with alpha_linear's row as output block 16): chunks 0..7 -> next
+// operand; chunk 8's row 0 is sigma (lane group 0, register 0 of the chunk's first block)
+struct FeatSigmaEpi4 {
+  f16x8 (&oh)[kNC][12];
+  f16x8 (&ol)[kNC][12];
+  const float (&sc)[kNC];
+  float (&mrun)[kNC];
+  float (&sigma)[kNC];
+  __device__ __forceinline__ void operator()(int c, const Z4& zz, int st) {
+    const int q = st >> 2, k = st & 3;
+    if (q >= kNC) return;
+    if (c == 8) {
+      if (k == 3) sigma[q] = zz.z[q][0].x;
+    } else if (k == 2) {
+      mrun[q] = amax8(mrun[q], zz.z[q][0], zz.z[q][1]);
+    } else if (k == 3) {
+      split8a(zz.z[q][0], zz.z[q][1], sc[q], oh[q][c], ol[q][c]);
+    }
+  }
+};
+
+// last hidden op of a net with a [3][ROWS] head in LDS: ReLU, then part[q][o] += y . head[o] over the
+// lane's rows of the chunk (rad4's HeadEpi4 with the head's row length as a parameter)
+template <int ROWS>
+struct HeadEpiN {
+  const float* head;  // LDS
+  float (&part)[kNC][3];
+  int g;
+  float4 y[kNC][2];
+  __device__ __forceinline__ void operator()(int c, const Z4& zz, int st) {
+    const int q = st >> 2, k = st & 3;
+    if (q >= kNC) return;
+    if (k < 2) {
+      const float4 z = zz.z[q][k];
+      y[q][k] = make_float4(fmaxf(z.x, 0.0f), fmaxf(z.y, 0.0f), fmaxf(z.z, 0.0f), fmaxf(z.w, 0.0f));
+    } else {
+#pragma unroll
+      for (int o = 0; o < 3; ++o) {
+        if ((o == 0) != (k == 2)) continue;
+        float p = part[q][o];
+        const uint32_t lo = opaque_lane(4 * g);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const float4 w = *(const float4*)(head + lo + o * ROWS + 16 * (2 * c + b));
+          p = fmaf(y[q][b].x, w.x, p);
+          p = fmaf(y[q][b].y, w.y, p);
+          p = fmaf(y[q][b].z, w.z, p);
+          p = fmaf(y[q][b].w, w.w, p);
+        }
+        asm volatile("" : "+v"(p));
+        part[q][o] = p;
+      }
+    }
+  }
+};
+
+__global__ __attribute__((amdgpu_flat_work_group_size(kT4, kT4), amdgpu_waves_per_eu(kWPE, kWPE)))
+void nerf4_kernel(NerfKArgs a) {
+  constexpr int C6 = chunk_bytes(6), C16 = chunk_bytes(16), C18 = chunk_bytes(18), C22 = chunk_bytes(22);
+  constexpr int kHead = 3 * 128 + 4;  // rgb_linear [3][128], then [3] bias
+  __shared__ __attribute__((aligned(16))) char smem[kRing * C22 + kHead * 4];
+  static_assert(kRing * C22 + kHead * 4 <= 160 * 1024, "LDS budget");
+  WStream4<C22> ws{smem, nullptr, 0, 0, 0};
+  float* head = (float*)(smem + kRing * C22);
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  const NerfLayout& L = a.L;
+  const char* W = a.packed;
+  auto OP = [&](int i) {
+    const char* w = W;
+    asm volatile("" : "+s"(w));
+    return w + L.op_off[i];
+  };
+  {
+    const float* hsrc = (const float*)(W + L.rgb_off);
+    for (int i = threadIdx.x; i < 3 * 128 + 3; i += kT4) head[i] = hsrc[i];
+  }
+  ws.template start<C6, C6>(OP(N0), OP(N0) + C6);  // its barrier also publishes the head
+  Pend4 pd{};
+  NoPre4 nopre;
+  const int64_t Pn = a.P_dev ? min(a.P, (int64_t)*a.P_dev) : a.P;
+  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < Pn; base += (int64_t)gridDim.x * kPointsPerWG) {
+    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < Pn;
+    const int64_t p0 = base + wave * 16 * kNC;
+    f16x8 Uh[kNC][12], Ul[kNC][12], Vh[kNC][12], Vl[kNC][12];
+    float4 E[kNC][6];
+    float m_in[kNC], xinv[kNC], mrun[kNC], mE[kNC];
+    bool valid[kNC];
+    int64_t pcq[kNC];
+#pragma unroll
+    for (int q = 0; q < kNC; ++q) {
+      const int64_t p = p0 + 16 * q + j;
+      valid[q] = p < Pn;
+      pcq[q] = valid[q] ? p : Pn - 1;
+      const float4 xin = *(const float4*)(a.x4 + pcq[q] * 4);
+      const int gq = (int)opaque_lane(g);
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+        const int f = 16 * b + 4 * gq;
+        E[q][b] = make_float4(nerf_embed4(f + 0, xin.x, xin.y, xin.z, xin.w),
+                              nerf_embed4(f + 1, xin.x, xin.y, xin.z, xin.w),
+                              nerf_embed4(f + 2, xin.x, xin.y, xin.z, xin.w),
+                              nerf_embed4(f + 3, xin.x, xin.y, xin.z, xin.w));
+      }
+      mE[q] = max4_groups(amax8(amax8(amax8(0.0f, E[q][0], E[q][1]), E[q][2], E[q][3]), E[q][4], E[q][5]));
+      m_in[q] = mE[q];
+      const float s = bound_scale(mE[q]);  // exact-max scale of N0's operand
+#pragma unroll
+      for (int k = 0; k < 3; ++k) split8a(E[q][2 * k], E[q][2 * k + 1], s, Uh[q][k], Ul[q][k]);
+      xinv[q] = 1.0f / s;
+      mrun[q] = 0.0f;
+    }
+    // output bound of the op about to run (its chunk 0 is the current ring slot): |relu(z)| <= |z| <=
+    // R max|in| + B; floor: the largest value of an input concatenated to that output
+    auto next_scales = [&](int kb, const float (&floor_max)[kNC], float (&sc)[kNC]) {
+      const float4 v = ws.buf()[2 * kb * 64 + 8];
+#pragma unroll
+      for (int q = 0; q < kNC; ++q) sc[q] = bound_scale(fmaxf(fmaf(v.y, m_in[q], v.z), floor_max[q]));
+    };
+    auto finish = [&](const float (&sc)[kNC]) {
+#pragma unroll
+      for (int q = 0; q < kNC; ++q) {
+        m_in[q] = max4_groups(mrun[q]);
+        mrun[q] = 0.0f;
+        xinv[q] = 1.0f / sc[q];
+      }
+    };
+    float zero2[kNC];
+#pragma unroll
+    for (int q = 0; q < kNC; ++q) zero2[q] = 0.0f;
+    {
+      float sc[kNC];
+      next_scales(6, zero2, sc);
+      op4<6, 16, C16, false, false>(ws, OP(N0), OP(N1), Uh, Ul, xinv, pd, nopre, ReluEpi4{Vh, Vl, sc, mrun}, lane);
+      finish(sc);
+    }
+    {
+      float sc[kNC];
+      next_scales(16, zero2, sc);
+      op4<16, 16, C16, false, false>(ws, OP(N1), OP(N2), Vh, Vl, xinv, pd, nopre, ReluEpi4{Uh, Ul, sc, mrun}, lane);
+      finish(sc);
+    }
+    {
+      float sc[kNC];
+      next_scales(16, zero2, sc);
+      op4<16, 16, C16, false, false>(ws, OP(N2), OP(N3), Uh, Ul, xinv, pd, nopre, ReluEpi4{Vh, Vl, sc, mrun}, lane);
+      finish(sc);
+    }
+    {
+      float sc[kNC];
+      next_scales(16, zero2, sc);
+      op4<16, 16, C16, false, false>(ws, OP(N3), OP(N4), Vh, Vl, xinv, pd, nopre, ReluEpi4{Uh, Ul, sc, mrun}, lane);
+      finish(sc);
+    }
+    {
+      // N4's outputs (h4) and the embedding form N5's operand [h4 ; embed(x4)]: one scale per point
+      float sc[kNC];
+      next_scales(16, mE, sc);
+      op4<16, 16, C22, false, false>(ws, OP(N4), OP(N5), Uh, Ul, xinv, pd, nopre, ReluEpi4{Vh, Vl, sc, mrun}, lane);
+#pragma unroll
+      for (int q = 0; q < kNC; ++q) {
+#ifdef NR_NERF4_KEEP_E
+        const float4* Eq = E[q];
+#else  // the embedding again from the point (no 24 registers held across N0..N4)
+        float4 Eq[6];
+        const float4 xin = *(const float4*)(a.x4 + pcq[q] * 4);
+        const int gq = (int)opaque_lane(g);
+#pragma unroll
+        for (int b = 0; b < 6; ++b) {
+          const int f = 16 * b + 4 * gq;
+          Eq[b] = make_float4(nerf_embed4(f + 0, xin.x, xin.y, xin.z, xin.w),
+                              nerf_embed4(f + 1, xin.x, xin.y, xin.z, xin.w),
+                              nerf_embed4(f + 2, xin.x, xin.y, xin.z, xin.w),
+                              nerf_embed4(f + 3, xin.x, xin.y, xin.z, xin.w));
+        }
+#endif
+#pragma unroll
+        for (int k = 0; k < 3; ++k) split8a(Eq[2 * k], Eq[2 * k + 1], sc[q], Vh[q][8 + k], Vl[q][8 + k]);
+        mrun[q] = fmaxf(mrun[q], mE[q]);
+      }
+      finish(sc);
+    }
+    {
+      float sc[kNC];
+      next_scales(22, zero2, sc);
+      op4<22, 16, C16, false, false>(ws, OP(N5), OP(N6), Vh, Vl, xinv, pd, nopre, ReluEpi4{Uh, Ul, sc, mrun}, lane);
+      finish(sc);
+    }
+    {
+      float sc[kNC];
+      next_scales(16, zero2, sc);
+      op4<16, 16, C16, false, false>(ws, OP(N6), OP(N7), Uh, Ul, xinv, pd, nopre, ReluEpi4{Vh, Vl, sc, mrun}, lane);
+      finish(sc);
+    }
+    {
+      float sc[kNC];
+      next_scales(16, zero2, sc);
+      op4<16, 16, C16, false, false>(ws, OP(N7), OP(NF), Vh, Vl, xinv, pd, nopre, ReluEpi4{Uh, Ul, sc, mrun}, lane);
+      finish(sc);
+    }
+    float sig[kNC];
+    // the view embedding (multires_view 4: 27 features in 2 blocks) joins the feature in NV's operand.
+    // Its bound: |sin|, |cos| <= 1 and the raw components |v_i| (3 loads, no embedding held across NF)
+    float mV[kNC];
+#pragma unroll
+    for (int q = 0; q < kNC; ++q) {
+      const int64_t pv = (pcq[q] / a.vdiv) % a.vmod;
+      mV[q] = fmaxf(1.0f, fmaxf(fabsf(a.vdir[pv * 3 + 0]), fmaxf(fabsf(a.vdir[pv * 3 + 1]), fabsf(a.vdir[pv * 3 + 2]))));
+    }
+    {
+      float sc[kNC];
+      next_scales(16, mV, sc);
+      op4<16, 18, C18, false, false>(ws, OP(NF), OP(NV), Uh, Ul, xinv, pd, nopre,
+                                     FeatSigmaEpi4{Vh, Vl, sc, mrun, sig}, lane);
+#pragma unroll
+      for (int q = 0; q < kNC; ++q) {
+        const int64_t pv = (pcq[q] / a.vdiv) % a.vmod;
+        const float v0 = a.vdir[pv * 3 + 0], v1 = a.vdir[pv * 3 + 1], v2 = a.vdir[pv * 3 + 2];
+        const int gq = (int)opaque_lane(g);
+        float4 Ve[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int f = 16 * b + 4 * gq;
+          Ve[b] = make_float4(f + 0 < 27 ? embed_feature(f + 0, v0, v1, v2, 4) : 0.0f,
+                              f + 1 < 27 ? embed_feature(f + 1, v0, v1, v2, 4) : 0.0f,
+                              f + 2 < 27 ? embed_feature(f + 2, v0, v1, v2, 4) : 0.0f,
+                              f + 3 < 27 ? embed_feature(f + 3, v0, v1, v2, 4) : 0.0f);
+        }
+        split8a(Ve[0], Ve[1], sc[q], Vh[q][8], Vl[q][8]);
+        mrun[q] = fmaxf(mrun[q], mV[q]);
+      }
+      finish(sc);
+    }
+    float part[kNC][3];
+#pragma unroll
+    for (int q = 0; q < kNC; ++q) part[q][0] = part[q][1] = part[q][2] = 0.0f;
+    op4<18, 8, C6, false, false>(ws, OP(NV), has_next ? OP(N0) : nullptr, Vh, Vl, xinv, pd, nopre,
+                                 HeadEpiN<128>{head, part, g}, lane);
+#pragma unroll
+    for (int q = 0; q < kNC; ++q) {
+      float r[3];
+#pragma unroll
+      for (int o = 0; o < 3; ++o) r[o] = sigmoidf_ref(wave_sum4(part[q][o]) + head[3 * 128 + o]);
+      if (valid[q] && g == 0) {
+        const int64_t p = p0 + 16 * q + j;
+        a.sigma[p] = sig[q];
+        a.rgb[p * 3 + 0] = r[0];
+        a.rgb[p * 3 + 1] = r[1];
+        a.rgb[p * 3 + 2] = r[2];
+      }
+    }
+  }
+  pd.flush();
+  wait_vmcnt(0);  // a block without tiles still has the prologue's second chunk in flight
+}
+
+// =============================================================================================
+// Training layer GEMM (tgemm_kernel, f16x3): one packed op of the render weight stream applied to a
+// [P, K] fp32 activation matrix with the elementwise step that follows it in the training recipe
+// fused into the epilogue (nr_train.hip header: primal, nabla chain, tangent and adjoint sweeps):
+//   Y[p, o] = epi( sum_i X[p, i] M[o, i] (+ bias[o]) ),  M = the op's packed matrix (W or W^T)
+// 128-point tiles (8 waves x 16 points), the input operand split at the exact per-point max and held
+// in registers, the op's chunks streamed through the LDS ring by LDS-DMA two ahead.  Tensors the
+// epilogue reads (softplus', g, zdot, saved activations) are fetched one chunk ahead by asm loads
+// issued before the chunk's weight DMA, and waited for by count: a compiler-visible load would be
+// waited on behind the in-flight DMA.  Every matrix is row-major with a row stride; the output
+// column layout is the op's block layout (16-column blocks, padded rows computed from zero weights).
+// =============================================================================================
+enum TgMode { TG_NONE = 0, TG_SOFTPLUS = 1, TG_RELU = 2, TG_MUL = 3, TG_SPADJ = 4, TG_RELUMASK = 5 };
+
+// float4 at byte offset off of a wave-uniform base, by asm (not waited on by the compiler)
+__device__ __forceinline__ float4 tg_load(const float* base, uint32_t off) {
+  f32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(v) : "v"(off), "s"(base) : "memory");
+  return fromf(v);
+}
+// pin a loaded value behind the preceding s_waitcnt (uses cannot be scheduled above it)
+__device__ __forceinline__ void tg_pin(float4& v) {
+  f32x4 t = tof(v);
+  asm volatile("" : "+v"(t));
+  v = fromf(t);
+}
+
+// KB input blocks (the last KB2 from x2), NBO output blocks (the last NB2 to yb), epilogue MODE
+template <int KB, int KB2, int NBO, int NB2, int MODE>
+__global__ __attribute__((amdgpu_flat_work_group_size(kT4, kT4), amdgpu_waves_per_eu(kWPE, kWPE)))
+void tgemm_kernel(TGemmArgs a) {
+  static_assert(kNC == 1, "tgemm_kernel: 16-point waves");
+  constexpr int CB = chunk_bytes(KB);
+  constexpr int NCH = NBO / 2, NS = KB / 2, KB1 = KB - KB2, NB1 = NBO - NB2;
+  static_assert(NCH >= 2, "the 2-ahead stream needs >= 2 chunks");
+  static_assert(NB1 % 2 == 0, "the output split falls between chunks");
+  constexpr bool kHead = MODE == TG_RELU;
+  __shared__ __attribute__((aligned(16))) char smem[kRing * CB + (kHead ? 3 * 256 * 4 : 16)];
+  WStream4<CB> ws{smem, nullptr, 0, 0, 0};
+  float* head = (float*)(smem + kRing * CB);  // [3][256] radiance head (TG_RELU with a head)
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  if (kHead && a.head)
+    for (int i = threadIdx.x; i < 3 * 256; i += kT4) head[i] = a.head[i];
+  ws.template start<CB, CB>(uniform_ptr(a.op), uniform_ptr(a.op) + CB);
+  // epilogue tensors by mode: TG_MUL / TG_RELUMASK read a; TG_SPADJ reads a (softplus'), g, zdot
+  constexpr bool kA = MODE == TG_MUL || MODE == TG_SPADJ || MODE == TG_RELUMASK;
+  constexpr bool kG = MODE == TG_SPADJ;
+  constexpr int NA = kG ? 3 : (kA ? 1 : 0);
+  const bool has_g = kG && a.g != nullptr;
+  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < a.P; base += (int64_t)gridDim.x * kPointsPerWG) {
+    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < a.P;
+    const int64_t p = base + wave * 16 + j;
+    const bool valid = p < a.P;
+    const uint32_t pc = (uint32_t)(valid ? p : a.P - 1);
+    // ---- input operand: [x1 blocks ; x2 blocks], split at the exact per-point max ----
+    f16x8 Uh[1][12], Ul[1][12];
+    float xinv[1];
+    {
+      float4 X[KB];
+      auto load_seg = [&](const float* src, int64_t ld, int n, int b0, int nb) {
+        const float* row = src + (int64_t)pc * ld;
+        const bool vec = ((ld | (int64_t)((uintptr_t)src >> 2)) & 3) == 0;
+#pragma unroll
+        for (int b = 0; b < nb; ++b) {
+          const int col = 16 * b + 4 * g;
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (vec && col + 3 < n) v = *(const float4*)(row + col);
+          else {
+            if (col + 0 < n) v.x = row[col + 0];
+            if (col + 1 < n) v.y = row[col + 1];
+            if (col + 2 < n) v.z = row[col + 2];
+            if (col + 3 < n) v.w = row[col + 3];
+          }
+          X[b0 + b] = v;
+        }
+      };
+      load_seg(a.x1, a.ld1, a.n1, 0, KB1);
+      if constexpr (KB2 > 0) load_seg(a.x2, a.ld2, a.n2, KB1, KB2);
+      float m = 0.0f;
+#pragma unroll
+      for (int b = 0; b < KB; b += 2) m = amax8(m, X[b], X[b + 1]);
+      m = max4_groups(m);
+      const float sc = bound_scale(m);
+#pragma unroll
+      for (int k = 0; k < NS; ++k) split8a(X[2 * k], X[2 * k + 1], sc, Uh[0][k], Ul[0][k]);
+      xinv[0] = 1.0f / sc;
+    }
+    // epilogue tensors of chunk c (blocks 2c, 2c+1 < NB1), fetched one chunk ahead
+    float4 aux[2][NA > 0 ? NA : 1][2];
+    auto aux_issue = [&](int c, float4 (&dst)[NA > 0 ? NA : 1][2]) -> int {
+      if constexpr (NA == 0) return 0;
+      if (2 * c >= NB1) return 0;
+      int n = 0;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const uint32_t col = (uint32_t)(16 * (2 * c + b) + 4 * g);
+        dst[0][b] = tg_load(a.a, (pc * (uint32_t)a.lda + col) * 4u);
+        ++n;
+        if constexpr (kG) {
+          if (has_g) {
+            dst[1][b] = tg_load(a.g, (pc * (uint32_t)a.ldg + col) * 4u);
+            dst[2][b] = tg_load(a.zd, (pc * (uint32_t)a.ldzd + col) * 4u);
+            n += 2;
+          }
+        }
+      }
+      return n;
+    };
+    aux_issue(0, aux[0]);
+    float dpart = 0.0f, hpart[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const char* opc = a.op;
+      asm volatile("" : "+s"(opc));
+      int npend = 0;
+      if (c + 1 < NCH) npend += aux_issue(c + 1, aux[(c + 1) & 1]);
+      if (c + 2 < NCH) {
+        ws.template issue<CB>(opc + (c + 2) * CB);
+        npend += WStream4<CB>::template npieces<CB>();
+      } else if (has_next) {
+        ws.template issue<CB>(opc + (c + 2 - NCH) * CB);
+        npend += WStream4<CB>::template npieces<CB>();
+      }
+      const float4* A = ws.buf();
+      f32x4 acc[1][2] = {};
+      mma4<NS>(A, Uh, Ul, acc, lane, [&](int) {});
+      const float inv = xinv[0] * A[2 * KB * 64 + 8].x;
+      float4 z[2];
+      if (a.use_bias) {
+        z[0] = fma4s(acc[0][0], inv, A[2 * KB * 64 + g]);
+        z[1] = fma4s(acc[0][1], inv, A[2 * KB * 64 + 4 + g]);
+      } else {
+        z[0] = fma4s(acc[0][0], inv, make_float4(0.f, 0.f, 0.f, 0.f));
+        z[1] = fma4s(acc[0][1], inv, make_float4(0.f, 0.f, 0.f, 0.f));
+      }
+      // everything issued before this iteration has landed (this chunk's epilogue tensors, chunk c+1's
+      // weights); pinning keeps every use of the asm-loaded registers behind the wait
+      wait_vmcnt(npend);
+      if constexpr (NA > 0) {
+#pragma unroll
+        for (int t = 0; t < NA; ++t) { tg_pin(aux[c & 1][t][0]); tg_pin(aux[c & 1][t][1]); }
+      }
+      const bool lo = 2 * c < NB1;  // this chunk's blocks go to y (else yb)
+      float* dst = lo ? a.y : a.yb;
+      if (dst && valid) {
+        const int64_t ld = lo ? a.ldy : a.ldyb;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int B = 2 * c + b;
+          const int col = 16 * (lo ? B : B - NB1) + 4 * g;
+          const float zz[4] = {z[b].x, z[b].y, z[b].z, z[b].w};
+          float o1[4], o2[4];
+          if constexpr (MODE == TG_SOFTPLUS) {  // torch softplus(beta=100, threshold=20) and softplus'
+            const float4 rvv = A[2 * KB * 64 + 16 + 4 * b + g];  // the op's per-row vector (F7: W8[0, :])
+            const float rv[4] = {rvv.x, rvv.y, rvv.z, rvv.w};
+            float o3[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float t = zz[r] * 144.269504088896341f;  // 100 log2(e) z
+              const float e = __builtin_amdgcn_exp2f(fminf(t, 126.0f));
+              const float u = e + 1.0f;
+              const bool lin = t > 28.8539008f;             // 100 z > 20
+              o1[r] = lin ? zz[r] : __builtin_amdgcn_logf(u) * 0.0069314718055994531f;
+              o2[r] = lin ? 1.0f : e * __builtin_amdgcn_rcpf(u);
+              o3[r] = o2[r] * rv[r];
+              dpart = fmaf(o1[r], rv[r], dpart);
+            }
+            if (a.y3) *(float4*)(a.y3 + p * a.ldy3 + col) = make_float4(o3[0], o3[1], o3[2], o3[3]);
+          } else if constexpr (MODE == TG_RELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o1[r] = fmaxf(zz[r], 0.0f);
+          } else if constexpr (MODE == TG_MUL) {
+            const float av[4] = {aux[c & 1][0][b].x, aux[c & 1][0][b].y, aux[c & 1][0][b].z, aux[c & 1][0][b].w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = zz[r] * a.yscale;
+              o1[r] = v;
+              o2[r] = av[r] * v;
+            }
+          } else if constexpr (MODE == TG_SPADJ) {  // zbar = hbar s + g zdot 100 s (1 - s)
+            const float av[4] = {aux[c & 1][0][b].x, aux[c & 1][0][b].y, aux[c & 1][0][b].z, aux[c & 1][0][b].w};
+            const float gv[4] = {aux[c & 1][1][b].x, aux[c & 1][1][b].y, aux[c & 1][1][b].z, aux[c & 1][1][b].w};
+            const float dv[4] = {aux[c & 1][2][b].x, aux[c & 1][2][b].y, aux[c & 1][2][b].z, aux[c & 1][2][b].w};
+            const float4 rvv = A[2 * KB * 64 + 16 + 4 * b + g];
+            const float rv[4] = {rvv.x, rvv.y, rvv.z, rvv.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float si = av[r];
+              float w = fmul(zz[r] * a.yscale, si);
+              if (has_g) {
+                const float d2 = fmul(fmul(si, fsub(1.0f, si)), 100.0f);
+                w = fadd(w, fmul(fmul(a.g_row ? rv[r] : gv[r], dv[r]), d2));
+              }
+              o1[r] = w;
+            }
+          } else if constexpr (MODE == TG_RELUMASK) {
+            const float av[4] = {aux[c & 1][0][b].x, aux[c & 1][0][b].y, aux[c & 1][0][b].z, aux[c & 1][0][b].w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o1[r] = av[r] > 0.0f ? zz[r] : 0.0f;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o1[r] = zz[r] * a.yscale;
+          }
+          *(float4*)(dst + p * ld + col) = make_float4(o1[0], o1[1], o1[2], o1[3]);
+          if constexpr (MODE == TG_SOFTPLUS || MODE == TG_MUL)
+            if (lo && a.y2) *(float4*)(a.y2 + p * a.ldy2 + col) = make_float4(o2[0], o2[1], o2[2], o2[3]);
+          if constexpr (kHead) {  // radiance head: rgb_o += y . head[o][rows]
+            if (a.head) {
+#pragma unroll
+              for (int o = 0; o < 3; ++o) {
+                const float4 w = *(const float4*)(head + o * 256 + 16 * B + 4 * g);
+                hpart[o] = fmaf(o1[0], w.x, hpart[o]);
+                hpart[o] = fmaf(o1[1], w.y, hpart[o]);
+                hpart[o] = fmaf(o1[2], w.z, hpart[o]);
+                hpart[o] = fmaf(o1[3], w.w, hpart[o]);
+              }
+            }
+          }
+        }
+      }
+      ws.flip(0);  // all older VMEM is complete (waited above): the barrier alone rotates the ring
+    }
+    if constexpr (MODE == TG_SOFTPLUS) {
+      if (a.dot) {
+        const float v = wave_sum4(dpart) + a.dot_bias;
+        if (valid && g == 0) a.dot[p] = v;
+      }
+    }
+    if constexpr (kHead) {
+      if (a.head_out) {
+        float r[3];
+#pragma unroll
+        for (int o = 0; o < 3; ++o) r[o] = wave_sum4(hpart[o]) + a.head_bias[o];
+        if (valid && g == 0) {
+          a.head_out[p * 3 + 0] = sigmoidf_ref(r[0]);
+          a.head_out[p * 3 + 1] = sigmoidf_ref(r[1]);
+          a.head_out[p * 3 + 2] = sigmoidf_ref(r[2]);
+        }
+      }
+    }
+  }
+  wait_vmcnt(0);
+}
+
+// (input blocks, output blocks, epilogue) instances the training path uses (neurecon_amd/training.py)
+#define NR_TG_SHAPES(X)                                                                                  \
+  X(4, 0, 16, 0, TG_SOFTPLUS) X(16, 0, 16, 0, TG_SOFTPLUS) X(16, 0, 14, 0, TG_SOFTPLUS)                   \
+  X(18, 4, 16, 0, TG_SOFTPLUS)                                                                           \
+  X(16, 0, 16, 0, TG_NONE) X(16, 0, 4, 0, TG_NONE) X(16, 0, 18, 2, TG_NONE) X(16, 0, 20, 4, TG_NONE)      \
+  X(16, 0, 16, 0, TG_MUL) X(16, 0, 18, 4, TG_MUL) X(14, 0, 16, 0, TG_MUL) X(4, 0, 16, 0, TG_MUL)          \
+  X(16, 0, 14, 0, TG_MUL) X(18, 4, 16, 0, TG_MUL)                                                        \
+  X(18, 2, 16, 0, TG_SPADJ) X(16, 0, 16, 0, TG_SPADJ) X(16, 0, 18, 4, TG_SPADJ) X(14, 0, 16, 0, TG_SPADJ)  \
+  X(18, 2, 16, 0, TG_RELU) X(20, 4, 16, 0, TG_RELU) X(16, 0, 16, 0, TG_RELU)                              \
+  X(2, 0, 16, 0, TG_RELUMASK) X(16, 0, 16, 0, TG_RELUMASK)
+
+int launch_tgemm(const TGemmArgs& a, int KB, int KB2, int NBO, int NB2, hipStream_t stream) {
+  if (a.P <= 0) return NR_OK;
+  NR_REQUIRE(a.op && a.y, NR_ERR_ARG, "tgemm: null op or output");
+  NR_REQUIRE(a.x1 && (KB2 == 0 || a.x2), NR_ERR_ARG, "tgemm: missing input segment");
+  // 32-bit byte offsets of the epilogue's asm loads
+  const int64_t maxld = std::max(std::max(a.lda, a.ldg), a.ldzd);
+  NR_REQUIRE(a.P * maxld * 4 < ((int64_t)1 << 31), NR_ERR_ARG, "tgemm: epilogue operands exceed 2 GB");
+  const int64_t tiles = (a.P + kPointsPerWG - 1) / kPointsPerWG;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int grid = (int)std::min<int64_t>(tiles, cus);
+  ProfScope prof("train_gemm", (double)a.P, stream);
+#define NR_TG_CASE(kb, kb2, nbo, nb2, md)                                                      \
+  if (KB == kb && KB2 == kb2 && NBO == nbo && NB2 == nb2 && a.mode == md) {                     \
+    hipLaunchKernelGGL((tgemm_kernel<kb, kb2, nbo, nb2, md>), dim3(grid), dim3(kT4), 0, stream, a); \
+    NR_HIP_CHECK(hipGetLastError());                                                            \
+    return NR_OK;                                                                               \
+  }
+  NR_TG_SHAPES(NR_TG_CASE)
+#undef NR_TG_CASE
+  set_error("tgemm: unsupported (input blocks, output blocks) shape");
+  return NR_ERR_UNSUPPORTED;
+}
+
+// =============================================================================================
 // weight packing (device): effective W [rows][ld] -> chunk layout of one GEMM op
 // =============================================================================================
 // source element (W * scale) of A-element (ob, b, fi) of an op, or 0 for padding
@@ -2360,7 +2910,13 @@ __device__ __forceinline__ float pack_src(const PackOp& op, int ob, int i, int b
     b_loc -= op.in[s].nblk;
   }
   if (row < 0 || col < 0) return 0.0f;
+  if (op.W2 && ob >= op.out[0].nblk) return op.W2[(int64_t)row * op.ld2 + col] * op.scale;  // out[1] rows of W2
   return (op.transpose ? op.W[(int64_t)col * op.ld + row] : op.W[(int64_t)row * op.ld + col]) * op.scale;
+}
+
+// bias of a row of output segment s (segment 1 reads bias2 when the op has a second matrix)
+__device__ __forceinline__ float op_bias(const PackOp& op, int s, int row) {
+  return (s == 1 && op.W2) ? op.bias2[row] : op.bias[row];
 }
 
 // weight scale 2^(13 - e) for max |W| = f 2^e (f16x3), 1 for fp32
@@ -2387,7 +2943,7 @@ __global__ void pack_op_kernel(PackOp op, uint32_t* __restrict__ dst, int64_t n)
       for (int s = 0; s < 2; ++s) {
         if (ob_loc < op.out[s].nblk) {
           const int rl = 16 * ob_loc + (idx & 15);
-          if (rl < op.out[s].nvalid) v = op.bias[op.out[s].off + rl];
+          if (rl < op.out[s].nvalid) v = op_bias(op, s, op.out[s].off + rl);
           break;
         }
         ob_loc -= op.out[s].nblk;
@@ -2401,7 +2957,7 @@ __global__ void pack_op_kernel(PackOp op, uint32_t* __restrict__ dst, int64_t n)
       for (int s = 0; s < 2; ++s) {
         if (ob_loc < op.out[s].nblk) {
           const int rl = 16 * ob_loc + (idx & 15);
-          if (rl < op.out[s].nvalid) v = op.bias[op.out[s].off + rl] * kT;
+          if (rl < op.out[s].nvalid) v = op_bias(op, s, op.out[s].off + rl) * kT;
           break;
         }
         ob_loc -= op.out[s].nblk;
@@ -2472,7 +3028,7 @@ __global__ void bound_kernel(PackOp op, unsigned* __restrict__ bound) {
     for (int q = 0; q < 2; ++q) {
       if (ob_loc < op.out[q].nblk) {
         const int rl = 16 * ob_loc + i;
-        if (rl < op.out[q].nvalid) bb = fabsf(op.bias[op.out[q].off + rl]);
+        if (rl < op.out[q].nvalid) bb = fabsf(op_bias(op, q, op.out[q].off + rl));
         break;
       }
       ob_loc -= op.out[q].nblk;
@@ -2499,6 +3055,10 @@ int launch_pack_op(const PackOp& op, char* dst, hipStream_t stream) {
     NR_HIP_CHECK(hipMemsetAsync(op.wmax, 0, sizeof(float), stream));
     hipLaunchKernelGGL(maxabs_kernel, dim3(64), dim3(256), 0, stream, op.W, op.wn, op.scale, (unsigned*)op.wmax);
     NR_HIP_CHECK(hipGetLastError());
+    if (op.W2) {
+      hipLaunchKernelGGL(maxabs_kernel, dim3(64), dim3(256), 0, stream, op.W2, op.wn2, op.scale, (unsigned*)op.wmax);
+      NR_HIP_CHECK(hipGetLastError());
+    }
   }
   if (op.bound) {
     NR_HIP_CHECK(hipMemsetAsync(op.bound, 0, 2 * sizeof(float), stream));
@@ -2572,7 +3132,7 @@ int launch_nerf(const NerfLayout& L, const void* packed, const float* x4, const 
   const int grid = grid_for(P);
   NerfKArgs a{(const char*)packed, L, x4, vdir, vdiv, vmod, P, sigma, rgb, P_dev};
   ProfScope prof("nerf", (double)P, stream, P_dev, 1);
-  if (L.prec == NR_PREC_F16X3) hipLaunchKernelGGL((nerf_kernel<NR_PREC_F16X3>), dim3(grid), dim3(kThreads), 0, stream, a);
+  if (L.prec == NR_PREC_F16X3) hipLaunchKernelGGL(nerf4_kernel, dim3(grid), dim3(kT4), 0, stream, a);  // v3 pipeline
   else hipLaunchKernelGGL((nerf_kernel<NR_PREC_FP32>), dim3(grid), dim3(kThreads), 0, stream, a);
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;
