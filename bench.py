@@ -196,7 +196,12 @@ def eager_gpu_baseline(dev, n_rays, reps=3):
 # MACs per unit (point) that each library kernel executes (SURVEY.md §8(a) layer shapes): launches
 # without the geometry feature skip its 256 rows of the last layer
 KERNEL_MAC = {'sdf_fwd': MAC_SDF_FWD_NOFEAT, 'sdf_feat': MAC_SDF_FWD, 'sdf_nabla': MAC_SDF_FWD_NOFEAT + MAC_SDF_BWD,
-              'sdf_nabla_feat': MAC_SDF_FWD + MAC_SDF_BWD, 'radiance': MAC_RAD, 'nerf': MAC_NERF}
+              'sdf_nabla_feat': MAC_SDF_FWD + MAC_SDF_BWD, 'radiance': MAC_RAD, 'nerf': MAC_NERF,
+              # deferred sample nablas: forward of every sample, reverse pass of the 16-point tiles whose
+              # samples have non-zero weight (units = tile points)
+              'sdf_nabla_fwd': MAC_SDF_FWD_NOFEAT, 'sdf_nabla_bwd': MAC_SDF_BWD,
+              # training GEMMs report MACs (padded 16x16 blocks) as their units
+              'train_gemm': 1}
 
 
 def pmc_traffic(kernel, precision):
@@ -499,7 +504,8 @@ def run(args):
             out = {'metric': 'training rays/sec, NeuS (configs/neus.yaml: 512 rays per GPU, fwd+bwd+Adam)',
                    'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
                    'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
-                   'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32 (gradient GEMMs); sampling ' + dtype,
+                   'scaling': 'weak', 'vs_baseline': None, 'dtype': (dtype + ' layer GEMMs (nr_train_gemm; radiance forward f32), f32 weight gradients'
+                             if args.precision == 'f16x3' else 'f32'),
                    'data': 'synthetic (random 64x64 targets, config-(b) camera, seeded geometric-init weights)',
                    'config': {'workload': 'NeuS Trainer.forward + backward (double backward through the nablas) + '
                                           'Adam step', 'rays_per_gpu': args.train_rays, 'samples_per_ray': 128,

@@ -205,6 +205,12 @@ typedef struct {
    * (rgb / depth / mask / normals bit-identical).  no_mid_skip != 0: evaluate every
    * mid-point, as the reference does. */
   int no_mid_skip;
+  /* Deferred sample nablas (official_solution render without detailed outputs, f16x3 softplus net,
+   * no NeRF++): the sample launches leave their reverse-pass state per 16-sample tile and only the
+   * tiles holding a sample of non-zero interval alpha run the reverse pass; the other samples' nablas
+   * are weighted by exactly 0 in normals_volume (neus.py:364-368).  Maps bit-identical; the workspace
+   * then holds 8 KB per sample of a <= 4096-ray chunk.  no_defer != 0: nablas at every sample when drawn. */
+  int no_defer;
 } NrNeusArgs;
 
 size_t nr_neus_workspace_bytes(const NrNeusArgs* a);
@@ -433,13 +439,16 @@ int nr_sdf_grid(const NrSdfDesc* d, const void* packed, double volume_size, int6
  *   nr_softplus_adjoint  zbar = hbar * s + g * zdot * 100 s (1 - s)  (softplus_double_backward)
  *   nr_mul / nr_activation  elementwise product; ReLU / sigmoid forward (in place) and backward
  *   nr_radiance_input cat([x, embed_view(v), normals, feature]) (base.py:379-384), or cat([x, feature])
- *                     when use_view_dirs = 0 (v / nrm unused)
+ *                     when use_view_dirs = 0 (v / nrm unused); wfeat = 0: without the feature (feat unused)
  *   nr_neus_points    pts / d_mid / pts_mid of the sorted sample depths (neus.py:284-288)
  *   nr_neus_composite_fwd/bwd  sdf_to_alpha, alpha_to_w, rgb / depth / acc (neus.py:28-70, 346-355)
  *                      and their gradient w.r.t. sdf, radiance and s (per-ray partials of d s)
  * ------------------------------------------------------------------------------------------ */
 int nr_embed(const float* x, int64_t P, int nfreq, float* out, void* stream);
 int nr_embed_jvp(const float* x, const float* v, int64_t P, int nfreq, float* out, void* stream);
+/* the same into rows of ldo >= 3+6F floats, zero beyond the features (the training GEMMs' 16-column blocks) */
+int nr_embed_padded(const float* x, int64_t P, int nfreq, float* out, int ldo, void* stream);
+int nr_embed_jvp_padded(const float* x, const float* v, int64_t P, int nfreq, float* out, int ldo, void* stream);
 int nr_embed_vjp(const float* x, const float* e0, int ld0, const float* e1, int ld1, float s1, int64_t P, int nfreq,
                  float* out, void* stream);
 int nr_softplus100(const float* z, int64_t n, float* h, float* s, void* stream);
@@ -544,6 +553,81 @@ int nr_unisurf_composite_bwd(const float* logits, const float* rad, const float*
                              int white_bkgd, const float* g_rgb, const float* g_depth, const float* g_acc,
                              const float* g_weights, float* d_logits, float* d_rad, void* workspace,
                              size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Training layer GEMMs (f16x3 MFMA; the dense layer products of the training step together with the
+ * elementwise step that follows each -- base.py:245-282 forward / nablas with create_graph=True,
+ * base.py:372-391 radiance -- replacing an addmm / mm on hipBLASLt plus one to three elementwise
+ * launches).  One call applies one packed op of a weight stream to a row-major [P, K] activation:
+ *   Y[p, o] = epi( sum_i X[p, i] M[o, i] (+ bias[o]) ),   M = W (forward ops) or W^T (backward ops)
+ * X = [x1 (KB - KB2 blocks of 16 columns) ; x2 (KB2 blocks)], Y = [y (NBO - NB2 blocks) ; yb (NB2)].
+ * epi (mode):
+ *   NR_TG_NONE      y = z * yscale
+ *   NR_TG_SOFTPLUS  y = softplus100(z), y2 = softplus'(z), y3 = y2 * rowvec, dot = y . rowvec + dot_bias
+ *                   (rowvec: the op's per-row vector, e.g. W8[0, :] riding F7: delta_7 and the sdf)
+ *   (2: reserved -- the radiance forward stays on fp32 GEMMs, whose ReLU masks match the reference's;
+ *    the head / head_bias / head_out fields are unused)
+ *   NR_TG_MUL       y = z * yscale, y2 = a * y            (nabla chain delta = s * g, tangent hdot = s * zdot)
+ *   NR_TG_SPADJ     y = hbar s + g zdot 100 s (1 - s), hbar = z * yscale, s = a, g = g (or rowvec with g_row)
+ *   NR_TG_RELUMASK  y = z where a > 0, else 0             (ReLU backward on the saved activation)
+ * Ops come from the render pack (nr_sdf_pack / nr_radiance_pack: forward ops and the SDF net's
+ * transposed ops) and the training pack (nr_sdf_train_pack: W8^T with W8[0, :] as its row vector;
+ * nr_radiance_train_pack: the radiance net's transposed ops); nr_*_op_info give an op's byte offset
+ * in its buffer, input blocks and output blocks.  Supported (KB, KB2, NBO, NB2, mode) shapes are the
+ * training path's own (NR_ERR_UNSUPPORTED otherwise).
+ * ------------------------------------------------------------------------------------------ */
+#define NR_TG_NONE 0
+#define NR_TG_SOFTPLUS 1
+#define NR_TG_MUL 3
+#define NR_TG_SPADJ 4
+#define NR_TG_RELUMASK 5
+
+typedef struct {
+  const char* op;        /* packed op */
+  int64_t P;
+  const float* x1;       /* x1[p * ld1 + col], n1 valid columns (the rest of its blocks read as 0) */
+  int64_t ld1;
+  int n1;
+  const float* x2;
+  int64_t ld2;
+  int n2;
+  int use_bias;
+  int mode;
+  float yscale;
+  float* y;
+  int64_t ldy;
+  float* yb;             /* NULL: those blocks are not stored */
+  int64_t ldyb;
+  float* y2;
+  int64_t ldy2;
+  float* y3;
+  int64_t ldy3;
+  const float* a;
+  int64_t lda;
+  const float* g;
+  int64_t ldg;
+  const float* zd;
+  int64_t ldzd;
+  int g_row;
+  float* dot;
+  float dot_bias;
+  const float* head;     /* [3][256] */
+  const float* head_bias;
+  float* head_out;       /* [P][3] */
+} NrTrainGemm;
+
+int nr_train_gemm(const NrTrainGemm* a, int KB, int KB2, int NBO, int NB2, void* stream);
+/* SDF ops: 0..16 = F0..F8, B7..B0 of the render pack (nr_sdf_pack), 17 = B8 of the training pack */
+int nr_sdf_op_info(const NrSdfDesc* d, int op, int64_t* offset, int* kb, int* nbo);
+size_t nr_sdf_train_packed_bytes(const NrSdfDesc* d);
+int nr_sdf_train_pack(const NrSdfDesc* d, const float* const* W, const float* const* b, void* packed, void* stream);
+/* radiance ops: 0..D-1 = forward ops of the render pack (op 0: [feature ; small inputs]), D = head
+ * offset ([3][256] then [3] bias; kb = nbo = 0); training pack: D+1 = head^T, D+2.. = W_{D-1}^T .. W_1^T,
+ * 2D+1 = W_0^T (output blocks [feature ; small inputs]) */
+int nr_radiance_op_info(const NrRadDesc* d, int op, int64_t* offset, int* kb, int* nbo);
+size_t nr_radiance_train_packed_bytes(const NrRadDesc* d);
+int nr_radiance_train_pack(const NrRadDesc* d, const float* const* W, const float* const* b, void* packed,
+                           void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Opt-in kernel timing (diagnostics / bench roofline).  While enabled, every kernel launch of

@@ -55,7 +55,7 @@ class NrNeusArgs(ctypes.Structure):
         ('upsample_algo', _c_i), ('fixed_s', _c_f), ('N_nograd_samples', _c_i), ('t_nograd', _c_p),
         ('workspace', _c_p), ('workspace_bytes', _c_sz),
         ('u_rand', _c_p), ('t_out_rand', _c_p), ('s_dev', _c_p), ('sample_only', _c_i), ('d_all_out', _c_p),
-        ('no_mid_skip', _c_i),
+        ('no_mid_skip', _c_i), ('no_defer', _c_i),
     ]
 
 
@@ -101,6 +101,22 @@ class NrUnisurfArgs(ctypes.Structure):
 
 
 WINDOW_REDUCE = ctypes.CFUNCTYPE(_c_i, _c_p)
+
+TG_NONE, TG_SOFTPLUS, TG_MUL, TG_SPADJ, TG_RELUMASK = 0, 1, 3, 4, 5
+
+
+class NrTrainGemm(ctypes.Structure):
+    _fields_ = [
+        ('op', _c_p), ('P', _c_i64),
+        ('x1', _c_p), ('ld1', _c_i64), ('n1', _c_i),
+        ('x2', _c_p), ('ld2', _c_i64), ('n2', _c_i),
+        ('use_bias', _c_i), ('mode', _c_i), ('yscale', _c_f),
+        ('y', _c_p), ('ldy', _c_i64), ('yb', _c_p), ('ldyb', _c_i64),
+        ('y2', _c_p), ('ldy2', _c_i64), ('y3', _c_p), ('ldy3', _c_i64),
+        ('a', _c_p), ('lda', _c_i64), ('g', _c_p), ('ldg', _c_i64), ('zd', _c_p), ('ldzd', _c_i64),
+        ('g_row', _c_i), ('dot', _c_p), ('dot_bias', _c_f),
+        ('head', _c_p), ('head_bias', _c_p), ('head_out', _c_p),
+    ]
 
 
 class NrKernelStat(ctypes.Structure):
@@ -148,6 +164,19 @@ _SIGS = {
     'nr_embed': (_c_i, [_c_p, _c_i64, _c_i, _c_p, _c_p]),
     'nr_embed_jvp': (_c_i, [_c_p, _c_p, _c_i64, _c_i, _c_p, _c_p]),
     'nr_embed_vjp': (_c_i, [_c_p, _c_p, _c_i, _c_p, _c_i, _c_f, _c_i64, _c_i, _c_p, _c_p]),
+    'nr_embed_padded': (_c_i, [_c_p, _c_i64, _c_i, _c_p, _c_i, _c_p]),
+    'nr_embed_jvp_padded': (_c_i, [_c_p, _c_p, _c_i64, _c_i, _c_p, _c_i, _c_p]),
+    # training layer GEMMs (nr_mlp.hip tgemm_kernel)
+    'nr_train_gemm': (_c_i, [ctypes.POINTER(NrTrainGemm), _c_i, _c_i, _c_i, _c_i, _c_p]),
+    'nr_sdf_op_info': (_c_i, [ctypes.POINTER(NrSdfDesc), _c_i, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i),
+                              ctypes.POINTER(_c_i)]),
+    'nr_sdf_train_packed_bytes': (_c_sz, [ctypes.POINTER(NrSdfDesc)]),
+    'nr_sdf_train_pack': (_c_i, [ctypes.POINTER(NrSdfDesc), ctypes.POINTER(_c_p), ctypes.POINTER(_c_p), _c_p, _c_p]),
+    'nr_radiance_op_info': (_c_i, [ctypes.POINTER(NrRadDesc), _c_i, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i),
+                                   ctypes.POINTER(_c_i)]),
+    'nr_radiance_train_packed_bytes': (_c_sz, [ctypes.POINTER(NrRadDesc)]),
+    'nr_radiance_train_pack': (_c_i, [ctypes.POINTER(NrRadDesc), ctypes.POINTER(_c_p), ctypes.POINTER(_c_p), _c_p,
+                                      _c_p]),
     'nr_softplus100': (_c_i, [_c_p, _c_i64, _c_p, _c_p, _c_p]),
     'nr_scale_cols': (_c_i, [_c_p, _c_i64, _c_i, _c_i, _c_i, _c_p, _c_f, _c_p, _c_p]),
     'nr_softplus_adjoint': (_c_i, [_c_p, _c_i, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_p, _c_p]),

@@ -1,11 +1,13 @@
 // neurecon_amd — C-ABI entry points (include/neurecon_hip.h): argument checking, packed-weight
 // layouts, and the host-side orchestration of one NeuS ray chunk.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <string>
 
 #include "nr_common.h"
 #include "nr_mlp.h"
+#include "nr_tgemm.h"
 #include "nr_neus.h"
 #include "nr_volsdf.h"
 #include "nr_unisurf.h"
@@ -16,6 +18,7 @@ static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+static int64_t chunk_bytes_host(int KB) { return (int64_t)(2 * KB + 1) * 1024; }
 
 // ---------------------------------------------------------------------------------------------
 // descriptors
@@ -203,10 +206,27 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
     c.sdf_f = c.sv;
     c.nab_f = F(pl.o_nsort);
   }
+  // deferred sample nablas (NeusChunk::slabs): sample launches leave per-tile slabs, the reverse pass
+  // runs after the sampling on the tiles of non-zero weight
+  const bool defer = fused && neus_deferred(a, R);
+  if (defer) {
+    c.slabs = (float4*)(ws + pl.o_slabs);
+    c.tflag = (int*)(ws + pl.o_tflag);
+    c.tiles = (int*)(ws + pl.o_tiles);
+    c.tcnt = (int*)(ws + pl.o_tcnt);
+  }
   void* mlp_ws = ws + pl.o_mlp;
   const size_t mlp_bytes = a.workspace_bytes - pl.o_mlp;
   const SdfLayout SL = sdf_layout(*a.sdf);
   const RadLayout RL = rad_layout(*a.rad);
+  // SDF of P sample points at evaluation slot slot0 (coarse: 0; round it: (N_samples + it n_up) R)
+  auto sample_sdf = [&](const float* pts, int64_t P, float* sdf_out, int64_t slot0) -> int {
+    if (defer)
+      return launch_sdf_deferred(SL, a.sdf_packed, pts, P, sdf_out, nullptr, a.sdf->multires,
+                                 c.slabs + (size_t)(slot0 / 16) * (8 * 16 * 64), nullptr, nullptr, 1, st);
+    return launch_sdf(SL, a.sdf_packed, pts, P, sdf_out, fused ? c.nraw + slot0 * 3 : nullptr, nullptr,
+                      a.sdf->multires, fused ? mlp_ws : nullptr, fused ? mlp_bytes : 0, st);
+  };
   const dim3 blk(64), grd((R + 63) / 64);  // one wave per block: a 4096-ray chunk spreads over 64 CUs
   int rc;
 
@@ -217,9 +237,7 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   }
   NR_HIP_CHECK(hipGetLastError());
   // coarse SDF (no grad, neus.py:220 / :251); direct_more uses its own uniform depths instead
-  if (a.upsample_algo != NR_UPSAMPLE_DIRECT_MORE &&
-      (rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)a.N_samples * R, c.sv, c.nraw, nullptr, a.sdf->multires,
-                       fused ? mlp_ws : nullptr, fused ? mlp_bytes : 0, st)))
+  if (a.upsample_algo != NR_UPSAMPLE_DIRECT_MORE && (rc = sample_sdf(c.pts, (int64_t)a.N_samples * R, c.sv, 0)))
     return rc;
   if (a.upsample_algo == NR_UPSAMPLE_DIRECT_MORE) {  // SDF at N_nograd_samples uniform depths
     hipLaunchKernelGGL(neus_nograd_points, grd, blk, 0, st, c);
@@ -256,20 +274,37 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   };
   for (int it = 0; it < c.n_iters; ++it) {
     if (it > 0 && (rc = merge(a.N_samples + (it - 1) * n_up))) return rc;
+    const int64_t slot0 = (int64_t)(a.N_samples + it * n_up) * R;
+    // deferred: every round's points stay at their evaluation slots (the reverse pass reads them)
+    NeusChunk cu = c;
+    if (defer) cu.pts = c.pts + slot0 * 3;
     {
       ProfScope prof("neus_upsample", (double)R, st);
       // perturb: round it's [n_rays][n_up] block of the caller's uniforms
       const float* u = a.u_rand ? a.u_rand + ((int64_t)it * a.n_rays + ray0) * n_up : a.u_fine;
-      hipLaunchKernelGGL(neus_upsample, dim3((unsigned)R), dim3(64), (4 * c.S + 1) * sizeof(float), st, c, it, u,
+      hipLaunchKernelGGL(neus_upsample, dim3((unsigned)R), dim3(64), (4 * c.S + 1) * sizeof(float), st, cu, it, u,
                          (int64_t)(a.u_rand ? n_up : 0));
     }
     NR_HIP_CHECK(hipGetLastError());
-    float* nslot = fused ? c.nraw + (size_t)(a.N_samples + it * n_up) * R * 3 : nullptr;
-    if ((rc = launch_sdf(SL, a.sdf_packed, c.pts, (int64_t)n_up * R, c.snew, nslot, nullptr, a.sdf->multires,
-                         fused ? mlp_ws : nullptr, fused ? mlp_bytes : 0, st)))
-      return rc;
+    if ((rc = sample_sdf(cu.pts, (int64_t)n_up * R, c.snew, slot0))) return rc;
   }
   if (c.n_iters > 0 && (rc = merge(c.S - n_up))) return rc;
+  if (defer) {  // nablas of the tiles holding a sample of non-zero interval weight; the rest stay 0
+    const int64_t nslot = (int64_t)c.S * R, ntile = nslot / 16;
+    NR_HIP_CHECK(hipMemsetAsync(c.nraw, 0, (size_t)nslot * 3 * sizeof(float), st));
+    if (a.calc_normal) {  // normals_volume is the only reader of the sample nablas here
+      NR_HIP_CHECK(hipMemsetAsync(c.tflag, 0, (size_t)ntile * sizeof(int), st));
+      NR_HIP_CHECK(hipMemsetAsync(c.tcnt, 0, sizeof(int), st));
+      const int64_t nq = (int64_t)(c.S - 1) * R;
+      hipLaunchKernelGGL(neus_sample_need, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, c, a.s_dev, a.s);
+      NR_HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(neus_tile_list, dim3((unsigned)((ntile + 1023) / 1024)), dim3(1024), 0, st, c, ntile);
+      NR_HIP_CHECK(hipGetLastError());
+      if ((rc = launch_sdf_deferred(SL, a.sdf_packed, c.pts, nslot, nullptr, c.nraw, a.sdf->multires, c.slabs, c.tiles,
+                                    c.tcnt, 2, st)))
+        return rc;
+    }
+  }
   if (a.sample_only) {  // training: the sorted depths are the whole output (neus.py:279)
     hipLaunchKernelGGL(neus_write_dall, dim3((unsigned)(((int64_t)c.S * R + 255) / 256)), dim3(256), 0, st, c.dv,
                        (int64_t)R, c.S, ray0, a.d_all_out);
@@ -360,7 +395,10 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
 }
 
 static int64_t neus_chunk_rays(const NrNeusArgs* a) {
-  const int64_t cap = 16384;
+  int64_t cap = 16384;
+  // deferred sample nablas keep 8 KB per sample of the chunk: <= 4096 rays of 128 samples (4.3 GB),
+  // a multiple of 16 rays
+  if (neus_deferred(*a, 16)) cap = std::max<int64_t>(16, (int64_t)(4096 * 128 / std::max(neus_total_samples(*a), 1)) / 16 * 16);
   return a->n_rays < cap ? (a->n_rays > 0 ? a->n_rays : 1) : cap;
 }
 
@@ -816,6 +854,125 @@ int nr_radiance_forward(const NrRadDesc* d, const void* packed, const float* x, 
              "nr_radiance_forward: bad argument");
   return launch_radiance(rad_layout(*d), packed, x, vdir, vdir_div, INT64_MAX, normals, feature, P, rgb,
                          d->multires_view, (hipStream_t)stream);
+}
+
+// ---- training layer GEMMs (nr_mlp.hip tgemm_kernel) ---------------------------------------------
+int nr_train_gemm(const NrTrainGemm* a, int KB, int KB2, int NBO, int NB2, void* stream) {
+  NR_REQUIRE(a, NR_ERR_ARG, "nr_train_gemm: null argument");
+  return launch_tgemm(*a, KB, KB2, NBO, NB2, (hipStream_t)stream);
+}
+
+static int softplus_net(const NrSdfDesc* d) {
+  int rc = check_sdf_desc(d);
+  if (rc) return rc;
+  NR_REQUIRE(!d->siren && d->precision == NR_PREC_F16X3, NR_ERR_UNSUPPORTED,
+             "training GEMMs: f16x3 softplus SDF nets only (SIREN / fp32 nets train on hipBLASLt)");
+  return NR_OK;
+}
+
+int nr_sdf_op_info(const NrSdfDesc* d, int op, int64_t* offset, int* kb, int* nbo) {
+  int rc = softplus_net(d);
+  if (rc) return rc;
+  NR_REQUIRE(offset && kb && nbo && op >= 0 && op <= kSdfOps, NR_ERR_ARG, "nr_sdf_op_info: bad argument");
+  if (op == kSdfOps) {  // B8 = W8^T of the training pack
+    *offset = 0; *kb = 18; *nbo = 16;
+    return NR_OK;
+  }
+  const SdfLayout L = sdf_layout(*d);
+  *offset = L.op_off[op]; *kb = kSdfKB[op]; *nbo = kSdfNBO[op];
+  return NR_OK;
+}
+
+size_t nr_sdf_train_packed_bytes(const NrSdfDesc* d) {
+  if (softplus_net(d)) return 0;
+  return align256((size_t)8 * chunk_bytes_host(18) + 4) + 256;
+}
+
+// W8^T [256 x 257]: output rows = the 256 inputs of layer 8 (h7), input blocks [feature rows (16) ;
+// sdf row (2 blocks, 1 valid)]; per-row vector W8[0, :] (g_7 of the nabla chain, nr_train.hip)
+int nr_sdf_train_pack(const NrSdfDesc* d, const float* const* W, const float* const* b, void* packed, void* stream) {
+  int rc = softplus_net(d);
+  if (rc) return rc;
+  NR_REQUIRE(W && b && packed && W[8], NR_ERR_ARG, "nr_sdf_train_pack: null argument");
+  char* P = (char*)packed;
+  float* wmax = (float*)(P + (size_t)8 * chunk_bytes_host(18));
+  PackOp op = mkop(W[8], nullptr, 257, 256, 1, seg(16, 0, 256), none(), seg(16, 1, 256), seg(2, 0, 1), 1.0f,
+                   NR_PREC_F16X3, wmax);
+  op.aux = W[8];
+  return launch_pack_op(op, P, (hipStream_t)stream);
+}
+
+static int train_radiance(const NrRadDesc* d) {
+  int rc = check_rad_desc(d);
+  if (rc) return rc;
+  NR_REQUIRE(!d->siren && d->D == 4 && d->precision == NR_PREC_F16X3, NR_ERR_UNSUPPORTED,
+             "training GEMMs: f16x3 ReLU radiance nets with D = 4 only");
+  return NR_OK;
+}
+
+// training pack of a radiance net: head^T (KB 2), W3^T, W2^T, W1^T (16 x 16), W0^T (out 16 + kbs)
+static void rad_train_layout(const RadLayout& L, int64_t (&off)[5], int (&kb)[5], int (&nbo)[5], int64_t& total) {
+  const int KBs[5] = {2, 16, 16, 16, 16};
+  const int NBOs[5] = {16, 16, 16, 16, 16 + L.kbs};
+  int64_t o = 0;
+  for (int i = 0; i < 5; ++i) {
+    off[i] = o; kb[i] = KBs[i]; nbo[i] = NBOs[i];
+    o += (int64_t)(NBOs[i] / 2) * chunk_bytes_host(KBs[i]);
+  }
+  total = o;
+}
+
+int nr_radiance_op_info(const NrRadDesc* d, int op, int64_t* offset, int* kb, int* nbo) {
+  int rc = train_radiance(d);
+  if (rc) return rc;
+  NR_REQUIRE(offset && kb && nbo && op >= 0 && op <= 2 * d->D + 1, NR_ERR_ARG, "nr_radiance_op_info: bad argument");
+  const RadLayout L = rad_layout(*d);
+  if (op < d->D) {
+    *offset = L.op_off[op]; *kb = op == 0 ? 16 + L.kbs : 16; *nbo = 16;
+  } else if (op == d->D) {
+    *offset = L.head_off; *kb = 0; *nbo = 0;
+  } else {
+    int64_t off[5], total;
+    int kbs[5], nbos[5];
+    rad_train_layout(L, off, kbs, nbos, total);
+    const int i = op - d->D - 1;
+    *offset = off[i]; *kb = kbs[i]; *nbo = nbos[i];
+  }
+  return NR_OK;
+}
+
+size_t nr_radiance_train_packed_bytes(const NrRadDesc* d) {
+  if (train_radiance(d)) return 0;
+  int64_t off[5], total;
+  int kb[5], nbo[5];
+  rad_train_layout(rad_layout(*d), off, kb, nbo, total);
+  return align256((size_t)total + 5 * 4) + 256;
+}
+
+int nr_radiance_train_pack(const NrRadDesc* d, const float* const* W, const float* const* b, void* packed,
+                           void* stream) {
+  int rc = train_radiance(d);
+  if (rc) return rc;
+  NR_REQUIRE(W && b && packed, NR_ERR_ARG, "nr_radiance_train_pack: null argument");
+  for (int l = 0; l <= d->D; ++l) NR_REQUIRE(W[l], NR_ERR_ARG, "nr_radiance_train_pack: null layer pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const RadLayout L = rad_layout(*d);
+  int64_t off[5], total;
+  int kb[5], nbo[5];
+  rad_train_layout(L, off, kb, nbo, total);
+  char* P = (char*)packed;
+  float* wmax = (float*)(P + total);
+  const int ns = L.n_small, ld0 = ns + 256;
+  PackOp ops[5];
+  ops[0] = mkop(W[4], nullptr, 3, 256, 1, seg(16, 0, 256), none(), seg(2, 0, 3), none(), 1.0f, NR_PREC_F16X3, wmax);
+  for (int i = 1; i <= 3; ++i)  // W3^T, W2^T, W1^T
+    ops[i] = mkop(W[4 - i], nullptr, 256, 256, 1, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f,
+                  NR_PREC_F16X3, wmax + i);
+  ops[4] = mkop(W[0], nullptr, 256, ld0, 1, seg(16, ns, 256), seg(L.kbs, 0, ns), seg(16, 0, 256), none(), 1.0f,
+                NR_PREC_F16X3, wmax + 4);
+  for (int i = 0; i < 5; ++i)
+    if ((rc = launch_pack_op(ops[i], P + off[i], st))) return rc;
+  return NR_OK;
 }
 
 size_t nr_neus_workspace_bytes(const NrNeusArgs* a) {

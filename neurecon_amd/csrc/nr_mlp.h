@@ -105,6 +105,10 @@ int launch_pack_vec(const float* src, int off, int nvalid, int n, char* dst, hip
 int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,
                float* feature, int nfreq, void* ws, size_t ws_bytes, hipStream_t stream,
                const int* P_dev = nullptr, int P_mult = 0);  // P_dev: device count, P_eff = min(P, *P_dev * P_mult)
+// deferred sample nablas (sdf4_kernel STAGE 1 / 2): stage 1 = sdf + slabs per 16-point tile into
+// `slabs` (P/16 x 128 KB); stage 2 = nablas of the tiles tiles[0 .. *n_tiles) from their slabs
+int launch_sdf_deferred(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,
+                        int nfreq, float4* slabs, const int* tiles, const int* n_tiles, int stage, hipStream_t stream);
 int launch_nerf(const NerfLayout& L, const void* packed, const float* x4, const float* vdir, int64_t vdiv,
                 int64_t vmod, int64_t P, float* sigma, float* rgb, hipStream_t stream,
                 const int* P_dev = nullptr);  // P_dev: device count, P_eff = min(P, *P_dev)

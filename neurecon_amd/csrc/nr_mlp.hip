@@ -16,6 +16,7 @@
 //    per-wave scratch slab and applies torch's softplus_backward formula g*e/(e+1).
 //  * Everything per point (embedding, nabla chain rule through sin/cos, sdf row dot product,
 //    sigmoid head) is VALU work in the same kernel.
+#include <algorithm>
 #include <type_traits>
 #include "nr_common.h"
 #include "nr_mlp.h"
@@ -610,6 +611,9 @@ struct SdfKArgs {
   int nfreq;
   const int* P_dev;  // optional device-side point count (x P_mult), bounded by P
   int P_mult;
+  float4* slabs;      // deferred nablas: per 16-point tile of the launch, [tile][8][16][64] float4
+  const int* tiles;   // STAGE 2: 16-point tiles to run the reverse pass on
+  const int* n_tiles; //   ... and their count (device)
 };
 
 template <int P, bool NABLA>
@@ -1498,9 +1502,14 @@ struct NoPre4 {
   __device__ __forceinline__ int operator()(int) const { return 0; }
 };
 
-template <bool NABLA, bool FEAT>
+// STAGE 0: forward (+ reverse pass with NABLA) on consecutive 128-point tiles.  The deferred-nabla
+// pair (NABLA, no feature): STAGE 1 runs the forward and leaves each 16-point tile's slabs (softplus
+// log2 terms, d sdf / d z7) in a.slabs at the tile's index; STAGE 2 runs only the reverse pass, on the
+// 16-point tiles of the device list a.tiles[0 .. *a.n_tiles) (nablas of those points).
+template <bool NABLA, bool FEAT, int STAGE>
 __global__ __attribute__((amdgpu_flat_work_group_size(kT4, kT4), amdgpu_waves_per_eu(kWPE, kWPE)))
 void sdf4_kernel(SdfKArgs a) {
+  static_assert(STAGE == 0 || (NABLA && !FEAT && kNC == 1), "deferred nablas: 16-point waves, no feature");
   constexpr int CB = chunk_bytes(18);  // largest SDF op chunk (F4: 14 + 4 input blocks)
   constexpr int C16 = chunk_bytes(16), C4 = chunk_bytes(4), C14 = chunk_bytes(14), C18 = chunk_bytes(18);
   __shared__ __attribute__((aligned(16))) char smem[kRing * CB + (NABLA ? kSlabRing * kSlab4 : 0)];
@@ -1523,7 +1532,8 @@ void sdf4_kernel(SdfKArgs a) {
     return w + sdf_op_off(i);
   };
   const float b8 = *(const float*)(W + a.L.misc_off);
-  // this wave's slabs: [layer 8][block 16][column kNC][lane 64] float4 (128 KB per column)
+  // this wave's slabs: [layer 8][block 16][column kNC][lane 64] float4 (128 KB per column); the
+  // deferred stages keep them per 16-point tile of the launch (set per tile below)
   float4* escr = uniform_ptr(a.scratch + (size_t)(blockIdx.x * kW4 + wave) * (8 * 16 * kNC * 64));
   auto slab = [&](int l) {
     float4* e = escr;
@@ -1538,23 +1548,35 @@ void sdf4_kernel(SdfKArgs a) {
 #ifdef NR_SDF4_PRIO  // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD)
   if (kWPE == 2 && wave >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
-  ws.template start<C4, C4>(OP(F0), OP(F0) + C4);
+  if constexpr (STAGE == 2) ws.template start<C16, C16>(OP(B7), OP(B7) + C16);
+  else ws.template start<C4, C4>(OP(F0), OP(F0) + C4);
   Pend4 pd{};
   NoPre4 nopre;
   const float kSpSlack = 0.0070f;  // softplus(z) <= max(z, 0) + ln2/100
 
-  const int64_t Pn = a.P_dev ? min(a.P, (int64_t)(*a.P_dev) * a.P_mult) : a.P;
+  // STAGE 2 walks the tile list, 8 tiles (one per wave) per workgroup iteration
+  const int64_t Pn = STAGE == 2 ? (int64_t)(*a.n_tiles) * kPointsPerWG / kW4
+                                : (a.P_dev ? min(a.P, (int64_t)(*a.P_dev) * a.P_mult) : a.P);
   for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < Pn; base += (int64_t)gridDim.x * kPointsPerWG) {
     const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < Pn;
-    const int64_t p0 = base + wave * 16 * kNC;  // this wave's first point
+    int64_t p0 = base + wave * 16 * kNC;  // this wave's first point
+    if constexpr (STAGE == 2) {  // this wave's tile (the last one again past the list's end: nothing stored)
+      const int64_t ti = min(p0 / 16, (int64_t)(*a.n_tiles) - 1);
+      const int64_t tile = a.tiles[ti];
+      escr = uniform_ptr(a.slabs + (size_t)tile * (8 * 16 * 64));
+      p0 = p0 / 16 < (int64_t)(*a.n_tiles) ? tile * 16 : a.P;  // a.P: every point invalid
+    } else if constexpr (STAGE == 1) {
+      escr = uniform_ptr(a.slabs + (size_t)(p0 / 16) * (8 * 16 * 64));
+    }
+    const int64_t Pv = STAGE == 2 ? a.P : Pn;  // points of the launch (validity of this wave's points)
     int64_t pq[kNC];
     bool valid[kNC];
     float xs[kNC][3];
 #pragma unroll
     for (int q = 0; q < kNC; ++q) {
       const int64_t p = p0 + 16 * q + j;
-      valid[q] = p < Pn;
-      pq[q] = valid[q] ? p : Pn - 1;
+      valid[q] = p < Pv;
+      pq[q] = valid[q] ? p : Pv - 1;
       xs[q][0] = a.pts[pq[q] * 3 + 0];
       xs[q][1] = a.pts[pq[q] * 3 + 1];
       xs[q][2] = a.pts[pq[q] * 3 + 2];
@@ -1562,6 +1584,29 @@ void sdf4_kernel(SdfKArgs a) {
     float4 E[kNC][4];
     float mE[kNC], xinv[kNC];
     f16x8 Uh[kNC][12], Ul[kNC][12], Vh[kNC][12], Vl[kNC][12];
+    float mrun[kNC], m_in[kNC];  // running max |output| of the op being computed (lane's values),
+                                 // max |input| of the op being computed (per point)
+    // (R, B) of the op about to run ride in its chunks' bias slot (floats 33, 34); its chunk 0 is
+    // the current ring slot when it starts
+    auto next_scales = [&](int kb, float extra, const float (&floor_max)[kNC], float (&sc)[kNC]) {
+      const float4 v = ws.buf()[2 * kb * 64 + 8];
+#pragma unroll
+      for (int q = 0; q < kNC; ++q) sc[q] = bound_scale(fmaxf(fmaf(v.y, m_in[q], v.z) + extra, floor_max[q]));
+    };
+    // end of an op: its output becomes the next operand; mscale converts the running max to output
+    // units (forward softplus epilogues track max(L, t), i.e. y / (ln2/100))
+    auto finish = [&](const float (&sc)[kNC], float mscale = 1.0f) {
+#pragma unroll
+      for (int q = 0; q < kNC; ++q) {
+        m_in[q] = max4_groups(mrun[q]) * mscale;
+        mrun[q] = 0.0f;
+        xinv[q] = 1.0f / sc[q];
+      }
+    };
+    float zero2[kNC];
+#pragma unroll
+    for (int q = 0; q < kNC; ++q) zero2[q] = 0.0f;
+    if constexpr (STAGE != 2) {
 #pragma unroll
     for (int q = 0; q < kNC; ++q) {
 #pragma unroll
@@ -1592,32 +1637,11 @@ void sdf4_kernel(SdfKArgs a) {
           asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" : : "v"(off), "v"(d), "s"(epark) : "memory");
         }
     }
-    float mrun[kNC], m_in[kNC];  // running max |output| of the op being computed (lane's values),
-#pragma unroll                   // max |input| of the op being computed (per point)
+#pragma unroll
     for (int q = 0; q < kNC; ++q) {
       mrun[q] = 0.0f;
       m_in[q] = mE[q];
     }
-    // (R, B) of the op about to run ride in its chunks' bias slot (floats 33, 34); its chunk 0 is
-    // the current ring slot when it starts
-    auto next_scales = [&](int kb, float extra, const float (&floor_max)[kNC], float (&sc)[kNC]) {
-      const float4 v = ws.buf()[2 * kb * 64 + 8];
-#pragma unroll
-      for (int q = 0; q < kNC; ++q) sc[q] = bound_scale(fmaxf(fmaf(v.y, m_in[q], v.z) + extra, floor_max[q]));
-    };
-    // end of an op: its output becomes the next operand; mscale converts the running max to output
-    // units (forward softplus epilogues track max(L, t), i.e. y / (ln2/100))
-    auto finish = [&](const float (&sc)[kNC], float mscale = 1.0f) {
-#pragma unroll
-      for (int q = 0; q < kNC; ++q) {
-        m_in[q] = max4_groups(mrun[q]) * mscale;
-        mrun[q] = 0.0f;
-        xinv[q] = 1.0f / sc[q];
-      }
-    };
-    float zero2[kNC];
-#pragma unroll
-    for (int q = 0; q < kNC; ++q) zero2[q] = 0.0f;
     auto fwd_epi = [&](f16x8(&oh)[kNC][12], f16x8(&ol)[kNC][12], const float (&sc)[kNC], float4* sl) {
       return FwdEpi4<NABLA>{oh, ol, sc, sl, mrun, pd, lane};
     };
@@ -1688,8 +1712,8 @@ void sdf4_kernel(SdfKArgs a) {
       float sc[kNC];
       next_scales(16, kSpSlack, zero2, sc);
       F7Epi4<NABLA, FEAT> epi{Uh, Ul, sc, slab(7), mrun, sdf_part, pd, lane};
-      constexpr int NXT = (NABLA || FEAT) ? C16 : C4;
-      const char* n = FEAT ? OP(F8) : (NABLA ? OP(B7) : (has_next ? OP(F0) : nullptr));
+      constexpr int NXT = ((NABLA && STAGE == 0) || FEAT) ? C16 : C4;
+      const char* n = FEAT ? OP(F8) : ((NABLA && STAGE == 0) ? OP(B7) : (has_next ? OP(F0) : nullptr));
       op4<16, 16, NXT, true, false>(ws, OP(F7), n, Vh, Vl, xinv, pd, nopre, epi, lane);
       finish(sc);
     }
@@ -1722,7 +1746,11 @@ void sdf4_kernel(SdfKArgs a) {
       const char* n = NABLA ? OP(B7) : (has_next ? OP(F0) : nullptr);
       op4<16, 16, NXT, false, false>(ws, OP(F8), n, Uh, Ul, xinv, pd, nopre, epi, lane);
     }
-    if constexpr (NABLA) {
+    }  // STAGE != 2: forward
+    if constexpr (NABLA && STAGE == 1) {  // the slabs stay for the reverse-pass launch
+      pd.flush();
+    }
+    if constexpr (NABLA && STAGE != 1) {
       // ---- reverse pass (autograd.grad of sdf w.r.t. x, base.py:265-282) ------------------------
       pd.flush();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1779,7 +1807,8 @@ void sdf4_kernel(SdfKArgs a) {
       bwd(I14{}, I16{}, I16{}, IC16{}, B3, OP(B2), Uh, Ul, Vh, Vl, 2, 0, 1);
       bwd(I16{}, I16{}, I16{}, IC16{}, B2, OP(B1), Vh, Vl, Uh, Ul, 1, 0, 0);
       bwd(I16{}, I16{}, I16{}, IC16{}, B1, OP(B0), Uh, Ul, Vh, Vl, 0, 0, -1);
-      bwd(I16{}, I4{}, I0{}, IC4{}, B0, has_next ? OP(F0) : nullptr, Vh, Vl, Uh, Ul, 0, 4, -1);
+      if constexpr (STAGE == 2) bwd(I16{}, I4{}, I0{}, IC16{}, B0, has_next ? OP(B7) : nullptr, Vh, Vl, Uh, Ul, 0, 4, -1);
+      else bwd(I16{}, I4{}, I0{}, IC4{}, B0, has_next ? OP(F0) : nullptr, Vh, Vl, Uh, Ul, 0, 4, -1);
       pd.flush();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // chain rule through the positional encoding (autograd sums both uses of embed(x))
@@ -2617,7 +2646,7 @@ void nerf4_kernel(NerfKArgs a) {
 // waited on behind the in-flight DMA.  Every matrix is row-major with a row stride; the output
 // column layout is the op's block layout (16-column blocks, padded rows computed from zero weights).
 // =============================================================================================
-enum TgMode { TG_NONE = 0, TG_SOFTPLUS = 1, TG_RELU = 2, TG_MUL = 3, TG_SPADJ = 4, TG_RELUMASK = 5 };
+enum TgMode { TG_NONE = 0, TG_SOFTPLUS = 1, TG_MUL = 3, TG_SPADJ = 4, TG_RELUMASK = 5 };  // 2: reserved
 
 // float4 at byte offset off of a wave-uniform base, by asm (not waited on by the compiler)
 __device__ __forceinline__ float4 tg_load(const float* base, uint32_t off) {
@@ -2633,6 +2662,14 @@ __device__ __forceinline__ void tg_pin(float4& v) {
 }
 
 // KB input blocks (the last KB2 from x2), NBO output blocks (the last NB2 to yb), epilogue MODE
+// float4 store at byte offset off of a wave-uniform base, by asm: issued by every lane of the wave (clamped
+// lanes rewrite the last row with that row's own values), so the store count of a chunk is exact for the
+// counted waits (s_nop: the store-data hazard is not tracked through inline asm)
+__device__ __forceinline__ void tg_store(float* base, uint32_t off, float4 v) {
+  const f32x4 d = tof(v);
+  asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" : : "v"(off), "v"(d), "s"(base) : "memory");
+}
+
 template <int KB, int KB2, int NBO, int NB2, int MODE>
 __global__ __attribute__((amdgpu_flat_work_group_size(kT4, kT4), amdgpu_waves_per_eu(kWPE, kWPE)))
 void tgemm_kernel(TGemmArgs a) {
@@ -2641,20 +2678,17 @@ void tgemm_kernel(TGemmArgs a) {
   constexpr int NCH = NBO / 2, NS = KB / 2, KB1 = KB - KB2, NB1 = NBO - NB2;
   static_assert(NCH >= 2, "the 2-ahead stream needs >= 2 chunks");
   static_assert(NB1 % 2 == 0, "the output split falls between chunks");
-  constexpr bool kHead = MODE == TG_RELU;
-  __shared__ __attribute__((aligned(16))) char smem[kRing * CB + (kHead ? 3 * 256 * 4 : 16)];
+  __shared__ __attribute__((aligned(16))) char smem[kRing * CB];
   WStream4<CB> ws{smem, nullptr, 0, 0, 0};
-  float* head = (float*)(smem + kRing * CB);  // [3][256] radiance head (TG_RELU with a head)
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int j = lane & 15, g = lane >> 4;
-  if (kHead && a.head)
-    for (int i = threadIdx.x; i < 3 * 256; i += kT4) head[i] = a.head[i];
   ws.template start<CB, CB>(uniform_ptr(a.op), uniform_ptr(a.op) + CB);
   // epilogue tensors by mode: TG_MUL / TG_RELUMASK read a; TG_SPADJ reads a (softplus'), g, zdot
   constexpr bool kA = MODE == TG_MUL || MODE == TG_SPADJ || MODE == TG_RELUMASK;
   constexpr bool kG = MODE == TG_SPADJ;
   constexpr int NA = kG ? 3 : (kA ? 1 : 0);
-  const bool has_g = kG && a.g != nullptr;
+  // the g zdot term: g from a tensor, or the op's per-row vector (g_row: W8[0, :] for layer 7)
+  const bool has_g = kG && (a.g != nullptr || a.g_row), g_tensor = kG && a.g != nullptr;
   for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < a.P; base += (int64_t)gridDim.x * kPointsPerWG) {
     const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < a.P;
     const int64_t p = base + wave * 16 + j;
@@ -2705,17 +2739,39 @@ void tgemm_kernel(TGemmArgs a) {
         dst[0][b] = tg_load(a.a, (pc * (uint32_t)a.lda + col) * 4u);
         ++n;
         if constexpr (kG) {
-          if (has_g) {
+          if (g_tensor) {
             dst[1][b] = tg_load(a.g, (pc * (uint32_t)a.ldg + col) * 4u);
+            ++n;
+          }
+          if (has_g) {
             dst[2][b] = tg_load(a.zd, (pc * (uint32_t)a.ldzd + col) * 4u);
-            n += 2;
+            ++n;
           }
         }
       }
       return n;
     };
     aux_issue(0, aux[0]);
-    float dpart = 0.0f, hpart[3] = {0.f, 0.f, 0.f};
+    float dpart = 0.0f;
+    // chunk c's outputs (y, y2, y3 per block) are stored at the start of iteration c+1, after that
+    // iteration's loads and DMA: younger than everything its counted wait must see landed
+    float4 pv[3][2];
+    auto flush = [&](int c) -> int {
+      const bool lo = 2 * c < NB1;
+      float* dst = lo ? a.y : a.yb;
+      int n = 0;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int B = 2 * c + b;
+        const uint32_t col = (uint32_t)(16 * (lo ? B : B - NB1) + 4 * g);
+        if (dst) { tg_store(dst, (pc * (uint32_t)(lo ? a.ldy : a.ldyb) + col) * 4u, pv[0][b]); ++n; }
+        if constexpr (MODE == TG_SOFTPLUS || MODE == TG_MUL)
+          if (lo && a.y2) { tg_store(a.y2, (pc * (uint32_t)a.ldy2 + col) * 4u, pv[1][b]); ++n; }
+        if constexpr (MODE == TG_SOFTPLUS)
+          if (lo && a.y3) { tg_store(a.y3, (pc * (uint32_t)a.ldy3 + col) * 4u, pv[2][b]); ++n; }
+      }
+      return n;
+    };
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const char* opc = a.op;
@@ -2729,6 +2785,7 @@ void tgemm_kernel(TGemmArgs a) {
         ws.template issue<CB>(opc + (c + 2 - NCH) * CB);
         npend += WStream4<CB>::template npieces<CB>();
       }
+      if (c > 0) npend += flush(c - 1);
       const float4* A = ws.buf();
       f32x4 acc[1][2] = {};
       mma4<NS>(A, Uh, Ul, acc, lane, [&](int) {});
@@ -2748,16 +2805,11 @@ void tgemm_kernel(TGemmArgs a) {
 #pragma unroll
         for (int t = 0; t < NA; ++t) { tg_pin(aux[c & 1][t][0]); tg_pin(aux[c & 1][t][1]); }
       }
-      const bool lo = 2 * c < NB1;  // this chunk's blocks go to y (else yb)
-      float* dst = lo ? a.y : a.yb;
-      if (dst && valid) {
-        const int64_t ld = lo ? a.ldy : a.ldyb;
+      {
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-          const int B = 2 * c + b;
-          const int col = 16 * (lo ? B : B - NB1) + 4 * g;
           const float zz[4] = {z[b].x, z[b].y, z[b].z, z[b].w};
-          float o1[4], o2[4];
+          float o1[4], o2[4] = {0.f, 0.f, 0.f, 0.f};
           if constexpr (MODE == TG_SOFTPLUS) {  // torch softplus(beta=100, threshold=20) and softplus'
             const float4 rvv = A[2 * KB * 64 + 16 + 4 * b + g];  // the op's per-row vector (F7: W8[0, :])
             const float rv[4] = {rvv.x, rvv.y, rvv.z, rvv.w};
@@ -2773,10 +2825,7 @@ void tgemm_kernel(TGemmArgs a) {
               o3[r] = o2[r] * rv[r];
               dpart = fmaf(o1[r], rv[r], dpart);
             }
-            if (a.y3) *(float4*)(a.y3 + p * a.ldy3 + col) = make_float4(o3[0], o3[1], o3[2], o3[3]);
-          } else if constexpr (MODE == TG_RELU) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o1[r] = fmaxf(zz[r], 0.0f);
+            pv[2][b] = make_float4(o3[0], o3[1], o3[2], o3[3]);
           } else if constexpr (MODE == TG_MUL) {
             const float av[4] = {aux[c & 1][0][b].x, aux[c & 1][0][b].y, aux[c & 1][0][b].z, aux[c & 1][0][b].w};
 #pragma unroll
@@ -2809,41 +2858,17 @@ void tgemm_kernel(TGemmArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) o1[r] = zz[r] * a.yscale;
           }
-          *(float4*)(dst + p * ld + col) = make_float4(o1[0], o1[1], o1[2], o1[3]);
-          if constexpr (MODE == TG_SOFTPLUS || MODE == TG_MUL)
-            if (lo && a.y2) *(float4*)(a.y2 + p * a.ldy2 + col) = make_float4(o2[0], o2[1], o2[2], o2[3]);
-          if constexpr (kHead) {  // radiance head: rgb_o += y . head[o][rows]
-            if (a.head) {
-#pragma unroll
-              for (int o = 0; o < 3; ++o) {
-                const float4 w = *(const float4*)(head + o * 256 + 16 * B + 4 * g);
-                hpart[o] = fmaf(o1[0], w.x, hpart[o]);
-                hpart[o] = fmaf(o1[1], w.y, hpart[o]);
-                hpart[o] = fmaf(o1[2], w.z, hpart[o]);
-                hpart[o] = fmaf(o1[3], w.w, hpart[o]);
-              }
-            }
-          }
+          pv[0][b] = make_float4(o1[0], o1[1], o1[2], o1[3]);
+          pv[1][b] = make_float4(o2[0], o2[1], o2[2], o2[3]);
         }
       }
       ws.flip(0);  // all older VMEM is complete (waited above): the barrier alone rotates the ring
     }
+    flush(NCH - 1);
     if constexpr (MODE == TG_SOFTPLUS) {
       if (a.dot) {
         const float v = wave_sum4(dpart) + a.dot_bias;
         if (valid && g == 0) a.dot[p] = v;
-      }
-    }
-    if constexpr (kHead) {
-      if (a.head_out) {
-        float r[3];
-#pragma unroll
-        for (int o = 0; o < 3; ++o) r[o] = wave_sum4(hpart[o]) + a.head_bias[o];
-        if (valid && g == 0) {
-          a.head_out[p * 3 + 0] = sigmoidf_ref(r[0]);
-          a.head_out[p * 3 + 1] = sigmoidf_ref(r[1]);
-          a.head_out[p * 3 + 2] = sigmoidf_ref(r[2]);
-        }
       }
     }
   }
@@ -2858,7 +2883,6 @@ void tgemm_kernel(TGemmArgs a) {
   X(16, 0, 16, 0, TG_MUL) X(16, 0, 18, 4, TG_MUL) X(14, 0, 16, 0, TG_MUL) X(4, 0, 16, 0, TG_MUL)          \
   X(16, 0, 14, 0, TG_MUL) X(18, 4, 16, 0, TG_MUL)                                                        \
   X(18, 2, 16, 0, TG_SPADJ) X(16, 0, 16, 0, TG_SPADJ) X(16, 0, 18, 4, TG_SPADJ) X(14, 0, 16, 0, TG_SPADJ)  \
-  X(18, 2, 16, 0, TG_RELU) X(20, 4, 16, 0, TG_RELU) X(16, 0, 16, 0, TG_RELU)                              \
   X(2, 0, 16, 0, TG_RELUMASK) X(16, 0, 16, 0, TG_RELUMASK)
 
 int launch_tgemm(const TGemmArgs& a, int KB, int KB2, int NBO, int NB2, hipStream_t stream) {
@@ -2866,13 +2890,13 @@ int launch_tgemm(const TGemmArgs& a, int KB, int KB2, int NBO, int NB2, hipStrea
   NR_REQUIRE(a.op && a.y, NR_ERR_ARG, "tgemm: null op or output");
   NR_REQUIRE(a.x1 && (KB2 == 0 || a.x2), NR_ERR_ARG, "tgemm: missing input segment");
   // 32-bit byte offsets of the epilogue's asm loads
-  const int64_t maxld = std::max(std::max(a.lda, a.ldg), a.ldzd);
+  const int64_t maxld = std::max({a.lda, a.ldg, a.ldzd, a.ldy, a.ldyb, a.ldy2, a.ldy3});
   NR_REQUIRE(a.P * maxld * 4 < ((int64_t)1 << 31), NR_ERR_ARG, "tgemm: epilogue operands exceed 2 GB");
   const int64_t tiles = (a.P + kPointsPerWG - 1) / kPointsPerWG;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int grid = (int)std::min<int64_t>(tiles, cus);
-  ProfScope prof("train_gemm", (double)a.P, stream);
+  ProfScope prof("train_gemm", (double)a.P * KB * NBO * 256.0, stream);  // units: MACs (padded blocks)
 #define NR_TG_CASE(kb, kb2, nbo, nb2, md)                                                      \
   if (KB == kb && KB2 == kb2 && NBO == nbo && NB2 == nb2 && a.mode == md) {                     \
     hipLaunchKernelGGL((tgemm_kernel<kb, kb2, nbo, nb2, md>), dim3(grid), dim3(kT4), 0, stream, a); \
@@ -3089,7 +3113,8 @@ int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t
                int P_mult) {
   if (P <= 0) return NR_OK;
   const int grid = grid_for(P);
-  SdfKArgs a{(const char*)packed, L, pts, P, sdf, nabla, feature, (float4*)ws, nfreq, P_dev, P_mult};
+  SdfKArgs a{(const char*)packed, L, pts, P, sdf, nabla, feature, (float4*)ws, nfreq, P_dev, P_mult, nullptr, nullptr,
+             nullptr};
   ProfScope prof(nabla ? (feature ? "sdf_nabla_feat" : "sdf_nabla") : (feature ? "sdf_feat" : "sdf_fwd"), (double)P,
                  stream, P_dev, P_mult);
   if (L.siren) {
@@ -3111,16 +3136,32 @@ int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t
     const size_t need = (size_t)grid * kScratchPerWG;
     NR_REQUIRE(ws && ws_bytes >= need, NR_ERR_WORKSPACE, "sdf nabla workspace too small");
     if (L.prec == NR_PREC_F16X3) {
-      if (feature) hipLaunchKernelGGL((sdf4_kernel<true, true>), dim3(grid), dim3(kT4), 0, stream, a);
-      else hipLaunchKernelGGL((sdf4_kernel<true, false>), dim3(grid), dim3(kT4), 0, stream, a);
+      if (feature) hipLaunchKernelGGL((sdf4_kernel<true, true, 0>), dim3(grid), dim3(kT4), 0, stream, a);
+      else hipLaunchKernelGGL((sdf4_kernel<true, false, 0>), dim3(grid), dim3(kT4), 0, stream, a);
     }
     else hipLaunchKernelGGL((sdf_kernel<NR_PREC_FP32, true>), dim3(grid), dim3(kThreads), 0, stream, a);
   } else {
     if (L.prec == NR_PREC_F16X3) {
-      if (feature) hipLaunchKernelGGL((sdf4_kernel<false, true>), dim3(grid), dim3(kT4), 0, stream, a);
-      else hipLaunchKernelGGL((sdf4_kernel<false, false>), dim3(grid), dim3(kT4), 0, stream, a);
+      if (feature) hipLaunchKernelGGL((sdf4_kernel<false, true, 0>), dim3(grid), dim3(kT4), 0, stream, a);
+      else hipLaunchKernelGGL((sdf4_kernel<false, false, 0>), dim3(grid), dim3(kT4), 0, stream, a);
     }
     else hipLaunchKernelGGL((sdf_kernel<NR_PREC_FP32, false>), dim3(grid), dim3(kThreads), 0, stream, a);
+  }
+  NR_HIP_CHECK(hipGetLastError());
+  return NR_OK;
+}
+
+int launch_sdf_deferred(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,
+                        int nfreq, float4* slabs, const int* tiles, const int* n_tiles, int stage, hipStream_t stream) {
+  if (P <= 0) return NR_OK;
+  NR_REQUIRE(L.prec == NR_PREC_F16X3 && !L.siren && kNC == 1, NR_ERR_UNSUPPORTED, "deferred nablas: f16x3 softplus nets");
+  SdfKArgs a{(const char*)packed, L, pts, P, sdf, nabla, nullptr, nullptr, nfreq, nullptr, 0, slabs, tiles, n_tiles};
+  if (stage == 1) {
+    ProfScope prof("sdf_nabla_fwd", (double)P, stream);
+    hipLaunchKernelGGL((sdf4_kernel<true, false, 1>), dim3(grid_for(P)), dim3(kT4), 0, stream, a);
+  } else {
+    ProfScope prof("sdf_nabla_bwd", (double)P, stream, n_tiles, 16);
+    hipLaunchKernelGGL((sdf4_kernel<true, false, 2>), dim3(grid_for(P)), dim3(kT4), 0, stream, a);
   }
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;

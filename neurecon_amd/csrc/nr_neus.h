@@ -22,6 +22,11 @@ struct NeusChunk {
   // carry each sample's evaluation slot in idv [S][R] (parallel to dv / sv), and neus_points
   // gathers the sorted nablas once.  idv == NULL: not fused.
   float* nraw; int* idv;
+  // deferred sample nablas (official_solution, no detailed outputs): the sample launches leave each
+  // 16-slot tile's slabs in `slabs` (sdf4_kernel STAGE 1); the tiles holding a sample whose interval
+  // weight can be non-zero are flagged (tflag), listed (tiles / tcnt) and get their nablas in one
+  // reverse-pass launch (STAGE 2); the rest of nraw stays 0 (those samples are weighted by exactly 0)
+  float4* slabs; int* tflag; int* tiles; int* tcnt;
   float* sdf_m; float* nab_m; float* feat_m; float* rad_m;
   // NeRF++ background (N_out = 0: none); M = S-1+N_out samples, sample-major
   int N_out;
@@ -51,10 +56,16 @@ struct NeusPlan {
   size_t o_idv, o_nsort, o_dv2, o_sv2, o_idv2;
   size_t o_slot, o_x4c, o_vdc, o_sigc, o_radc, o_cnt;  // NeRF++: compacted background points
   size_t o_mslot, o_midc, o_mvd, o_mrad, o_mcnt;        // mid-points of non-zero alpha (compacted)
+  size_t o_slabs, o_tflag, o_tiles, o_tcnt;             // deferred sample nablas
   size_t total;
 };
 
 NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc);
+// the sample launches defer their reverse pass (see NeusChunk::slabs) for this chunk of R rays
+bool neus_deferred(const NrNeusArgs& a, int64_t R);
+int neus_total_samples(const NrNeusArgs& a);
+__global__ void neus_sample_need(NeusChunk c, const float* s_dev, float s_val);
+__global__ void neus_tile_list(NeusChunk c, int64_t n_tiles);
 
 __global__ void neus_prologue(NeusChunk c, const float* rays_o, const float* rays_d, const float* t_coarse,
                               float r_obj, float near_bypass, float far_bypass);

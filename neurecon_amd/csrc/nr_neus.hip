@@ -584,6 +584,32 @@ __global__ void neus_mid_compact(NeusChunk c, const float* __restrict__ s_dev, f
   }
 }
 
+// deferred sample nablas: flag the 16-slot tile (evaluation order) of every sorted sample i < S-1 whose
+// interval alpha is not exactly 0 -- neus_composite weights sample i's unit nabla by w_i = alpha_i T_i
+// (neus.py:364-368), so the others contribute exactly 0 (their nablas stay 0, normalize(0) = 0).
+// Same alpha arithmetic as neus_mid_compact / the compositing.
+__global__ void neus_sample_need(NeusChunk c, const float* __restrict__ s_dev, float s_val) {
+  const int64_t R = c.R;
+  const int S1 = c.S - 1;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (int64_t)S1 * R) return;
+  const float s_inv = s_dev ? *s_dev : s_val;
+  const int i = (int)(q / R);
+  const int64_t r = q - (int64_t)i * R;
+  const float cp = sigmoidf_ref(fmul(c.sdf_f[(int64_t)i * R + r], s_inv));
+  const float cn = sigmoidf_ref(fmul(c.sdf_f[(int64_t)(i + 1) * R + r], s_inv));
+  const float alpha = fmaxf(fdiv(fsub(cp, cn), fadd(cp, 1e-10f)), 0.0f);
+  if (!(alpha == 0.0f)) c.tflag[((int64_t)c.idv[q] * R + r) >> 4] = 1;
+}
+
+// flagged tiles -> list (any order: each tile's nablas depend on that tile alone)
+__global__ void neus_tile_list(NeusChunk c, int64_t n_tiles) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool need = t < n_tiles && c.tflag[t] != 0;
+  const int64_t j = block_append(need, c.tcnt);
+  if (need) c.tiles[j] = (int)t;
+}
+
 __global__ void neus_mid_scatter(const int* __restrict__ slot, const float* __restrict__ radc, int64_t n,
                                  float* __restrict__ rad_m) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -801,9 +827,29 @@ NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc) {
   p.o_dv2 = take((size_t)S * Rc);  // merge ping-pong buffers
   p.o_sv2 = take((size_t)S * Rc);
   p.o_idv2 = take((size_t)S * Rc);
+  const size_t tiles = neus_deferred(a, Rc) ? ((size_t)S * Rc + 15) / 16 : 1;
+  p.o_slabs = take(neus_deferred(a, Rc) ? tiles * (8 * 16 * 64 * 4) : 1);  // 128 KB per 16-slot tile
+  p.o_tflag = take(tiles);
+  p.o_tiles = take(tiles);
+  p.o_tcnt = take(1);
   p.o_mlp = off;
   p.total = off + nr_mlp_workspace_bytes(1);
   return p;
+}
+
+int neus_total_samples(const NrNeusArgs& a) {
+  const bool direct = a.upsample_algo != NR_UPSAMPLE_OFFICIAL;
+  const int n_up0 = a.N_upsample_iters > 0 ? a.N_importance / a.N_upsample_iters : 0;
+  return direct ? a.N_samples + a.N_importance : a.N_samples + a.N_upsample_iters * n_up0;
+}
+
+// official_solution, render mode without the per-sample nablas (detailed outputs), no NeRF++ (its
+// compositing weights the samples' nablas by the background's alpha too), the f16x3 softplus net, and
+// slots that tile exactly (R % 16 == 0: every launch starts a tile)
+bool neus_deferred(const NrNeusArgs& a, int64_t R) {
+  return a.upsample_algo == NR_UPSAMPLE_OFFICIAL && !a.sample_only && !a.nablas_out && !a.no_mid_skip &&
+         !a.no_defer && a.N_outside == 0 && a.sdf && a.sdf->precision == NR_PREC_F16X3 && !a.sdf->siren &&
+         R > 0 && R % 16 == 0;
 }
 
 }  // namespace nr

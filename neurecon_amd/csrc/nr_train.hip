@@ -31,24 +31,33 @@ __device__ float emb_f(int f, const float (&x)[3], int nfreq) {
   return m < 3 ? sinf(v) : cosf(v);
 }
 
-__global__ void embed_kernel(const float* __restrict__ x, int64_t P, int nfreq, float* __restrict__ out) {
+// out[p * ldo + f]: features f < nf, zeros up to ldo (ldo >= nf; the training GEMMs' padded blocks)
+__global__ void embed_kernel(const float* __restrict__ x, int64_t P, int nfreq, float* __restrict__ out, int ldo) {
   const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P * nf) return;
-  const int64_t p = i / nf;
-  const int f = (int)(i - p * nf);
+  if (i >= P * ldo) return;
+  const int64_t p = i / ldo;
+  const int f = (int)(i - p * ldo);
+  if (f >= nf) {
+    out[i] = 0.0f;
+    return;
+  }
   const float xs[3] = {x[p * 3], x[p * 3 + 1], x[p * 3 + 2]};
   out[i] = emb_f(f, xs, nfreq);
 }
 
 // J_emb(x) v: d/dt embed(x + t v) (the tangent seed of the double backward)
 __global__ void embed_jvp_kernel(const float* __restrict__ x, const float* __restrict__ v, int64_t P, int nfreq,
-                                 float* __restrict__ out) {
+                                 float* __restrict__ out, int ldo) {
   const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P * nf) return;
-  const int64_t p = i / nf;
-  const int f = (int)(i - p * nf);
+  if (i >= P * ldo) return;
+  const int64_t p = i / ldo;
+  const int f = (int)(i - p * ldo);
+  if (f >= nf) {
+    out[i] = 0.0f;
+    return;
+  }
   if (f < 3) {
     out[i] = v[p * 3 + f];
     return;
@@ -899,19 +908,30 @@ using namespace nr;
 extern "C" {
 
 int nr_embed(const float* x, int64_t P, int nfreq, float* out, void* stream) {
-  NR_REQUIRE(x && out && P >= 0 && nfreq <= 10, NR_ERR_ARG, "nr_embed: bad argument");
   const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
+  return nr_embed_padded(x, P, nfreq, out, nf, stream);
+}
+
+int nr_embed_padded(const float* x, int64_t P, int nfreq, float* out, int ldo, void* stream) {
+  const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
+  NR_REQUIRE(x && out && P >= 0 && nfreq <= 10 && ldo >= nf, NR_ERR_ARG, "nr_embed: bad argument");
   if (P == 0) return NR_OK;
-  hipLaunchKernelGGL(embed_kernel, grid1(P * nf), dim3(kBlk), 0, (hipStream_t)stream, x, P, nfreq, out);
+  hipLaunchKernelGGL(embed_kernel, grid1(P * ldo), dim3(kBlk), 0, (hipStream_t)stream, x, P, nfreq, out, ldo);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
 
 int nr_embed_jvp(const float* x, const float* v, int64_t P, int nfreq, float* out, void* stream) {
-  NR_REQUIRE(x && v && out && P >= 0 && nfreq <= 10, NR_ERR_ARG, "nr_embed_jvp: bad argument");
   const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
+  return nr_embed_jvp_padded(x, v, P, nfreq, out, nf, stream);
+}
+
+int nr_embed_jvp_padded(const float* x, const float* v, int64_t P, int nfreq, float* out, int ldo, void* stream) {
+  const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
+  NR_REQUIRE(x && v && out && P >= 0 && nfreq <= 10 && ldo >= nf, NR_ERR_ARG, "nr_embed_jvp: bad argument");
   if (P == 0) return NR_OK;
-  hipLaunchKernelGGL(embed_jvp_kernel, grid1(P * nf), dim3(kBlk), 0, (hipStream_t)stream, x, v, P, nfreq, out);
+  hipLaunchKernelGGL(embed_jvp_kernel, grid1(P * ldo), dim3(kBlk), 0, (hipStream_t)stream, x, v, P, nfreq, out,
+                     ldo);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
@@ -1007,7 +1027,9 @@ int nr_activation(float* y, float* g, int64_t n, int mode, void* stream) {
 
 int nr_radiance_input(const float* x, const float* v, const float* nrm, const float* feat, int64_t P, int nfreq_view,
                       int use_view_dirs, int wfeat, float* out, void* stream) {
-  NR_REQUIRE(x && (!use_view_dirs || (v && nrm)) && feat && out && P >= 0 && nfreq_view <= 10 && wfeat > 0,
+  // wfeat = 0: the small inputs only (the training GEMM reads the feature from its own tensor)
+  NR_REQUIRE(x && (!use_view_dirs || (v && nrm)) && (feat || wfeat == 0) && out && P >= 0 && nfreq_view <= 10 &&
+                 wfeat >= 0,
              NR_ERR_ARG, "nr_radiance_input: bad argument");
   const int ld = use_view_dirs ? 6 + (nfreq_view < 0 ? 3 : 3 + 6 * nfreq_view) + wfeat : 3 + wfeat;
   if (P == 0) return NR_OK;

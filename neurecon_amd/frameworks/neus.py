@@ -92,12 +92,15 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
                   near_bypass=None, far_bypass=None, detailed_output=True, show_progress=False, perturb=False,
                   fixed_s_recp=1 / 64., N_samples=64, N_importance=64, N_outside=0,
                   upsample_algo='official_solution', N_nograd_samples=2048, N_upsample_iters=4,
-                  skip_zero_alpha=True, **dummy_kwargs):
+                  skip_zero_alpha=True, defer_sample_nablas=True, **dummy_kwargs):
     """neus.py:118-397, render mode.  skip_zero_alpha (not a reference argument): mid-points whose alpha
     is exactly 0 (and, with NeRF++, the ones outside the bounding sphere) skip the SDF + radiance nets
     when the radiance output is not asked for -- their weight is an exact 0 (or their colour is the
     background's), so rgb / depth / mask / normals are bit-identical;
-    False evaluates every mid-point as the reference does.  rays_o/rays_d: [(B,) N_rays, 3]; rays_d need not be normalized.
+    False evaluates every mid-point as the reference does.  defer_sample_nablas (not a reference
+    argument; with skip_zero_alpha, f16x3, no NeRF++, no detailed outputs): the samples' reverse pass
+    (their nablas feed only normals_volume, weighted by w_i) runs after the sampling, only on the
+    16-sample tiles holding a sample of non-zero weight -- bit-identical maps.  rays_o/rays_d: [(B,) N_rays, 3]; rays_d need not be normalized.
     perturb=True draws the reference's uniforms (same generators, shapes and order) and hands them
     to the kernels."""
     L.require_gpu(rays_o, 'rays_o')
@@ -155,6 +158,7 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     a.rad, a.rad_packed = ctypes.pointer(rad_desc), L.ptr(rad_packed)
     a.s, a.s_dev = 0.0, L.ptr(s_dev)
     a.no_mid_skip = 0 if skip_zero_alpha else 1
+    a.no_defer = 0 if defer_sample_nablas else 1
     a.obj_bounding_radius = float(obj_bounding_radius)
     a.near_bypass = float('nan') if near_bypass is None else float(near_bypass)
     a.far_bypass = float('nan') if far_bypass is None else float(far_bypass)

@@ -1,6 +1,10 @@
 """Training path of the render hot loop: autograd Functions whose forward and
-backward run on libnrhip.so's training kernels (nr_train.hip) with the dense layer products on
-hipBLASLt (torch.addmm / mm on the ROCm device -- plain library GEMMs, fp32).
+backward run on libnrhip.so.  f16x3 nets (the default precision; softplus SDF nets and ReLU D=4
+radiance nets) run every layer product on the hand-written training GEMM (nr_train_gemm: f16x3 MFMA
+over the render pack's weight stream, the elementwise step of the recipe fused into its epilogue);
+the weight gradients are hipBLASLt products of those saved activations.  fp32-precision and SIREN
+nets keep the reference-exact path: torch.addmm / mm on hipBLASLt (fp32) and the elementwise
+kernels of nr_train.hip between them.
 
 What the reference differentiates (models/frameworks/neus.py:284-485, models/base.py:265-282):
   * ImplicitSurface.forward_with_nablas with create_graph=True: sdf, nablas = d sdf / d x and the
@@ -521,6 +525,305 @@ class UnisurfComposite(torch.autograd.Function):
         return d_lg, d_rad, None, None
 
 
+
+# ---------------------------------------------------------------------------------------------
+# f16x3 training GEMM path (nr_train_gemm)
+# ---------------------------------------------------------------------------------------------
+def _tg(op, P, shape, mode, x1, ld1, n1, y, ldy, x2=None, ld2=0, n2=0, bias=True, yscale=1.0, yb=None, ldyb=0,
+        y2=None, ldy2=0, y3=None, ldy3=0, a=None, lda=0, g=None, ldg=0, zd=None, ldzd=0, g_row=False, dot=None,
+        dot_bias=0.0, head=None, head_bias=None, head_out=None, stream=None):
+    """one training layer GEMM: shape = (KB, KB2, NBO, NB2) of the packed op at device address `op`"""
+    def _p(v):  # tensor, raw device address or None
+        return None if v is None else (v if isinstance(v, int) else v.data_ptr())
+    t = L.NrTrainGemm()
+    t.op, t.P = op, P
+    t.x1, t.ld1, t.n1 = _p(x1), ld1, n1
+    t.x2, t.ld2, t.n2 = _p(x2), ld2, n2
+    t.use_bias, t.mode, t.yscale = int(bias), mode, float(yscale)
+    t.y, t.ldy, t.yb, t.ldyb = _p(y), ldy, _p(yb), ldyb
+    t.y2, t.ldy2, t.y3, t.ldy3 = _p(y2), ldy2, _p(y3), ldy3
+    t.a, t.lda, t.g, t.ldg, t.zd, t.ldzd = _p(a), lda, _p(g), ldg, _p(zd), ldzd
+    t.g_row, t.dot, t.dot_bias = int(g_row), _p(dot), float(dot_bias)
+    t.head, t.head_bias, t.head_out = _p(head), _p(head_bias), _p(head_out)
+    L.check(L.lib().nr_train_gemm(ctypes.byref(t), *shape, stream))
+
+
+_OPINFO = {}
+
+
+def _op_info(kind, desc, n_ops):
+    """(byte offset, input blocks, output blocks) of every op of a net's render / training pack"""
+    key = (kind, tuple(getattr(desc, f) for f, _ in desc._fields_))
+    info = _OPINFO.get(key)
+    if info is None:
+        fn = L.lib().nr_sdf_op_info if kind == 'sdf' else L.lib().nr_radiance_op_info
+        info = []
+        for i in range(n_ops):
+            off, kb, nbo = ctypes.c_int64(), ctypes.c_int(), ctypes.c_int()
+            L.check(fn(ctypes.byref(desc), i, ctypes.byref(off), ctypes.byref(kb), ctypes.byref(nbo)))
+            info.append((off.value, kb.value, nbo.value))
+        _OPINFO[key] = info
+    return info
+
+
+def _train_pack(module, kind, Ws, bs, device):
+    """the net's training pack (transposed ops the render pack lacks), cached per parameter version"""
+    from .base import _version_key
+    key = _version_key(module, 'train', device)
+    c = getattr(module, '_nr_train_cache', None)
+    if c is not None and c[0] == key:
+        return c[1]
+    lib = L.lib()
+    desc = module.nr_desc()
+    nbytes = (lib.nr_sdf_train_packed_bytes if kind == 'sdf' else lib.nr_radiance_train_packed_bytes)(
+        ctypes.byref(desc))
+    if nbytes == 0:
+        raise NotImplementedError('neurecon_amd: ' + lib.nr_last_error().decode())
+    from .base import _ptr_array
+    W = [w.detach().float().contiguous() for w in Ws]
+    b = [x.detach().float().contiguous() for x in bs]
+    packed = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    fn = lib.nr_sdf_train_pack if kind == 'sdf' else lib.nr_radiance_train_pack
+    L.check(fn(ctypes.byref(desc), _ptr_array(W), _ptr_array(b), L.ptr(packed), L.stream_of(device)))
+    module._nr_train_cache = (key, packed, W, b)
+    return packed
+
+
+def uses_train_gemm(module):
+    """f16x3 softplus SDF nets (D=8, skip 4) and f16x3 ReLU radiance nets with D=4 train on nr_train_gemm"""
+    if getattr(module, 'precision', 'fp32') != 'f16x3' or getattr(module, 'use_siren', False):
+        return False
+    if hasattr(module, 'surface_fc_layers'):
+        return module.D == 8 and list(module.skips) == [4] and module.W == 256 and module.W_geo_feat == 256
+    return module.D == 4 and module.W == 256
+
+
+def _pad16(n):
+    return 16 * ((n + 15) // 16)
+
+
+class SdfNablaTG(torch.autograd.Function):
+    """SdfNabla on nr_train_gemm (f16x3 softplus nets, D=8, skip at layer 4, W=256): the same recipe
+    (nr_train.hip header) with every layer product an op of the render pack (F0..F8 forward, B7..B0
+    transposed) or the training pack (B8 = W8^T), and the elementwise steps in the GEMM epilogues:
+      primal   F_l: h_l, s_l = softplus100 / softplus'(W_l hin_l + b_l); F7 also delta_7 = s_7 W8[0, :]
+               and sdf = h_7 . W8[0, :] + b8;  F8: feature
+      nabla    B_l: g_{l-1} = W_l^T delta_l, delta_{l-1} = s_{l-1} g_{l-1}; B4 splits [g_3 ; e_skip];
+               B0: e_first;  nabla = J_emb^T (e_first + e_skip)
+      tangent  F_l (no bias): zdot_l = W_l hdot_in_l, hdot_l = s_l zdot_l
+      adjoint  B8 then B7..B1: zbar_{l-1} = (W_l^T zbar_l) s_{l-1} + g_{l-1} zdot_{l-1} 100 s (1 - s)
+    Activations are [P, 16-column blocks] row-major (217-wide layer-3 tensors padded to 224, the
+    embedding to 64).  Weight gradients: dW_l = zbar_l^T hin_l + delta_l^T hdot_in_l (hipBLASLt)."""
+
+    @staticmethod
+    def forward(ctx, x, surface, want_feat, *params):
+        D = 8
+        Ws, bs = params[:D + 1], params[D + 1:]
+        dev = x.device
+        st = L.stream_of(dev)
+        x = x.contiguous()
+        P = x.shape[0]
+        desc, packed = surface.nr_packed(dev)
+        info = _op_info('sdf', desc, 18)
+        base = packed.data_ptr()
+        op = lambda i: base + info[i][0]
+        shp = lambda i, kb2=0, nb2=0: (info[i][1], kb2, info[i][2], nb2)
+        nf = surface.input_ch                      # 39
+        h0 = torch.empty(P, 64, device=dev)
+        L.check(L.lib().nr_embed_padded(L.ptr(x), P, surface.embed_multires, L.ptr(h0), 64, st))
+        wd = [256, 256, 256, 224, 256, 256, 256, 256]   # padded widths of the layer outputs h_l
+        nv = [256, 256, 256, 217, 256, 256, 256, 256]
+        H = [torch.empty(P, wd[l], device=dev) for l in range(D)]
+        S = [torch.empty(P, wd[l], device=dev) for l in range(D)]
+        sdf = torch.empty(P, device=dev)
+        delta = [None] * D
+        delta[7] = torch.empty(P, 256, device=dev)
+        for l in range(D):                                                 # F0..F7
+            if l == 0:
+                xin = dict(x1=h0, ld1=64, n1=nf)
+            elif l == 4:
+                xin = dict(x1=H[3], ld1=224, n1=217, x2=h0, ld2=64, n2=nf)
+            else:
+                xin = dict(x1=H[l - 1], ld1=wd[l - 1], n1=nv[l - 1])
+            extra = dict(y3=delta[7], ldy3=256, dot=sdf) if l == 7 else {}
+            _tg(op(l), P, shp(l, 4 if l == 4 else 0), L.TG_SOFTPLUS, y=H[l], ldy=wd[l], y2=S[l], ldy2=wd[l],
+                stream=st, **xin, **extra)
+        sdf.add_(bs[D].detach()[0])                                        # + b8 (no host sync)
+        feat = None
+        if want_feat:                                                      # F8
+            feat = torch.empty(P, 256, device=dev)
+            _tg(op(8), P, shp(8), L.TG_NONE, H[7], 256, 256, feat, 256, stream=st)
+        G = [None] * D                                                     # g_l = d sdf / d h_l (l < 7)
+        for l in range(D - 1, 0, -1):                                      # B7..B1: op index 16 - l
+            i = 16 - l
+            delta[l - 1] = torch.empty(P, wd[l - 1], device=dev)
+            G[l - 1] = torch.empty(P, wd[l - 1], device=dev)
+            if l == 4:  # [g_3 (14 blocks) ; e_skip (4 blocks)]
+                e_skip = torch.empty(P, 64, device=dev)
+                _tg(op(i), P, shp(i, 0, 4), L.TG_MUL, delta[4], 256, 256, G[3], 224, yb=e_skip, ldyb=64,
+                    y2=delta[3], ldy2=224, a=S[3], lda=224, stream=st)
+            else:
+                _tg(op(i), P, shp(i), L.TG_MUL, delta[l], wd[l], nv[l], G[l - 1], wd[l - 1], y2=delta[l - 1],
+                    ldy2=wd[l - 1], a=S[l - 1], lda=wd[l - 1], stream=st)
+        e_first = torch.empty(P, 64, device=dev)                           # B0
+        _tg(op(16), P, shp(16), L.TG_NONE, delta[0], 256, 256, e_first, 64, stream=st)
+        nab = torch.empty(P, 3, device=dev)
+        L.check(L.lib().nr_embed_vjp(L.ptr(x), L.ptr(e_first), 64, L.ptr(e_skip), 64, 1.0, P, surface.embed_multires,
+                                     L.ptr(nab), st))
+        ctx.surface = surface
+        ctx.want_feat = want_feat
+        ctx.save_for_backward(x, h0, *H, *S, *G[:D - 1], *delta, *Ws, *bs)
+        return (sdf, nab, feat) if want_feat else (sdf, nab)
+
+    @staticmethod
+    def backward(ctx, g_sdf, g_nab, *rest):
+        D = 8
+        saved = ctx.saved_tensors
+        x, h0 = saved[0], saved[1]
+        H = saved[2:2 + D]
+        S = saved[2 + D:2 + 2 * D]
+        G = list(saved[2 + 2 * D:2 + 3 * D - 1]) + [None]
+        delta = saved[1 + 3 * D:1 + 4 * D]
+        Ws = saved[1 + 4 * D:1 + 4 * D + D + 1]
+        surface = ctx.surface
+        g_feat = rest[0] if ctx.want_feat else None
+        dev = x.device
+        st = L.stream_of(dev)
+        P = x.shape[0]
+        desc, packed = surface.nr_packed(dev)
+        info = _op_info('sdf', desc, 18)
+        base = packed.data_ptr()
+        op = lambda i: base + info[i][0]
+        shp = lambda i, kb2=0, nb2=0: (info[i][1], kb2, info[i][2], nb2)
+        nf = surface.input_ch
+        wd = [256, 256, 256, 224, 256, 256, 256, 256]
+        nv = [256, 256, 256, 217, 256, 256, 256, 256]
+        tangent = g_nab is not None
+        ZD = [None] * D
+        HD = [None] * D                                                   # hdot_l = s_l zdot_l
+        hd0 = None
+        if tangent:
+            hd0 = torch.empty(P, 64, device=dev)
+            L.check(L.lib().nr_embed_jvp_padded(L.ptr(x), L.ptr(g_nab.contiguous()), P, surface.embed_multires,
+                                                L.ptr(hd0), 64, st))
+            for l in range(D):
+                if l == 0:
+                    xin = dict(x1=hd0, ld1=64, n1=nf)
+                elif l == 4:
+                    xin = dict(x1=HD[3], ld1=224, n1=217, x2=hd0, ld2=64, n2=nf)
+                else:
+                    xin = dict(x1=HD[l - 1], ld1=wd[l - 1], n1=nv[l - 1])
+                ZD[l] = torch.empty(P, wd[l], device=dev)
+                HD[l] = torch.empty(P, wd[l], device=dev)
+                _tg(op(l), P, shp(l, 4 if l == 4 else 0), L.TG_MUL, y=ZD[l], ldy=wd[l], y2=HD[l], ldy2=wd[l],
+                    a=S[l], lda=wd[l], bias=False, stream=st, **xin)
+        # output-layer adjoint ob = [d sdf, d feature] -> zbar_7 through B8 = W8^T (training pack)
+        Wl = [surface.surface_fc_layers[i] for i in range(D + 1)]
+        tp = _train_pack(surface, 'sdf', [l.effective_weight() for l in Wl], [l.bias for l in Wl], dev)
+        gs = torch.zeros(P, device=dev) if g_sdf is None else g_sdf.contiguous()
+        gf = torch.zeros(P, 256, device=dev) if g_feat is None else g_feat.contiguous()
+        Z = [None] * D
+        Z[7] = torch.empty(P, 256, device=dev)
+        _tg(tp.data_ptr() + info[17][0], P, (18, 2, 16, 0), L.TG_SPADJ, gf, 256, 256, Z[7], 256, x2=gs, ld2=1, n2=1,
+            a=S[7], lda=256, zd=ZD[7], ldzd=256, g_row=tangent, stream=st)
+        for l in range(D - 1, 0, -1):                                      # B7..B1 -> zbar_{l-1}
+            i = 16 - l
+            Z[l - 1] = torch.empty(P, wd[l - 1], device=dev)
+            gz = dict(g=G[l - 1], ldg=wd[l - 1], zd=ZD[l - 1], ldzd=wd[l - 1]) if tangent else {}
+            _tg(op(i), P, shp(i, 0, 4 if l == 4 else 0), L.TG_SPADJ, Z[l], wd[l], nv[l], Z[l - 1], wd[l - 1],
+                a=S[l - 1], lda=wd[l - 1], stream=st, **gz)
+        # weight gradients (hipBLASLt): dW_l = zbar_l^T hin_l + delta_l^T hdot_in_l, db_l = sum_p zbar_l
+        dW, db = [None] * (D + 1), [None] * (D + 1)
+        ob = torch.cat([gs[:, None], gf], 1)
+        dW[D] = _wgrad(ob, H[7])
+        db[D] = _colsum(ob)
+        if tangent:
+            dW[D][0] += _colsum(HD[7])
+        for l in range(D):
+            zb = Z[l][:, :nv[l]]
+            if l == 0:
+                dW[0] = _wgrad2(zb, h0[:, :nf], delta[0], hd0[:, :nf]) if tangent else _wgrad(zb, h0[:, :nf])
+            elif l == 4:  # the skip layer's input cat([h3, embed(x)]) / sqrt(2) (base.py:250)
+                hin = torch.cat([H[3][:, :217], h0[:, :nf]], 1).mul_(_ISQ2)
+                hdin = torch.cat([HD[3][:, :217], hd0[:, :nf]], 1).mul_(_ISQ2) if tangent else None
+                dW[4] = _wgrad2(zb, hin, delta[4], hdin) if tangent else _wgrad(zb, hin)
+            else:
+                hin = H[l - 1][:, :nv[l - 1]]
+                dW[l] = (_wgrad2(zb, hin, delta[l][:, :nv[l]], HD[l - 1][:, :nv[l - 1]]) if tangent
+                         else _wgrad(zb, hin))
+            db[l] = _colsum(zb)
+        return (None, None, None, *dW, *db)
+
+
+class RadianceTG(torch.autograd.Function):
+    """RadianceFn with the backward on nr_train_gemm (f16x3 ReLU nets, D=4): head^T and W3^T..W1^T of
+    the training pack with the ReLU mask in the epilogue, W0^T split into d feature / d small inputs
+    (-> d normals); weight gradients on hipBLASLt.  The forward stays on fp32 GEMMs: ReLU'(z) is a
+    step, and the f16x3 forward's ~5e-7 relative error in z flips a few masks per step against the
+    reference's fp32 z -- each flip moves one point's whole contribution to the gradients of every
+    earlier layer (measured: layer-2 bias gradient 3.8e-4 off the float64 truth with the f16x3
+    forward, 9e-8 with the fp32 one; tools/train_diag.py --probe).  The backward has no such decision."""
+
+    @staticmethod
+    def forward(ctx, x, v, nrm, feat, net, *params):
+        Ws, bs = params[:5], params[5:]
+        P = x.shape[0]
+        view = net.use_view_dirs
+        nfv = net.embed_multires_view
+        nvw = (3 if nfv < 0 else 3 + 6 * nfv) if view else 0
+        ns = 3 + nvw + (3 if view else 0)
+        inp = torch.empty(P, ns + 256, device=x.device)  # [x, embed_view(v), normals, feature] (base.py:383-386)
+        L.check(L.lib().nr_radiance_input(L.ptr(x), L.ptr(v), L.ptr(nrm), L.ptr(feat), P, nfv, int(view), 256,
+                                          L.ptr(inp), _st(x)))
+        H = []
+        h = inp
+        for l in range(4):
+            h = torch.addmm(bs[l], h, Ws[l].t())
+            L.check(L.lib().nr_activation(L.ptr(h), None, h.numel(), 0, _st(x)))  # ReLU
+            H.append(h)
+        rgb = torch.addmm(bs[4], h, Ws[4].t())
+        L.check(L.lib().nr_activation(L.ptr(rgb), None, rgb.numel(), 2, _st(x)))  # sigmoid
+        ctx.net = net
+        ctx.cfg = (ns, nvw, view)
+        ctx.save_for_backward(rgb, inp, *H, *Ws)
+        return rgb
+
+    @staticmethod
+    def backward(ctx, gy):
+        ns, nvw, view = ctx.cfg
+        net = ctx.net
+        saved = ctx.saved_tensors
+        rgb, inp = saved[:2]
+        H = saved[2:6]
+        dev = rgb.device
+        st = L.stream_of(dev)
+        P = rgb.shape[0]
+        desc, _ = net.nr_packed(dev)
+        info = _op_info('rad', desc, 10)
+        tp = _train_pack(net, 'rad', [l.effective_weight() for l in net.layers], [l.bias for l in net.layers], dev)
+        tb = tp.data_ptr()
+        g = gy.contiguous().clone()
+        L.check(L.lib().nr_activation(L.ptr(rgb), L.ptr(g), g.numel(), 3, st))  # sigmoid'
+        dW, db = [None] * 5, [None] * 5
+        dW[4], db[4] = _wgrad(g, H[3]), _colsum(g)
+        gz = torch.empty(P, 256, device=dev)
+        _tg(tb + info[5][0], P, (2, 0, 16, 0), L.TG_RELUMASK, g, 3, 3, gz, 256, bias=False, a=H[3], lda=256, stream=st)
+        for l in range(3, 0, -1):  # gz = d z_l  ->  d z_{l-1} through W_l^T (training ops 6, 7, 8)
+            dW[l], db[l] = _wgrad(gz, H[l - 1]), _colsum(gz)
+            gn = torch.empty(P, 256, device=dev)
+            _tg(tb + info[5 + (4 - l)][0], P, (16, 0, 16, 0), L.TG_RELUMASK, gz, 256, 256, gn, 256, bias=False,
+                a=H[l - 1], lda=256, stream=st)
+            gz = gn
+        dW[0], db[0] = _wgrad(gz, inp), _colsum(gz)  # W0 columns [small | feature], as inp
+        nbo0 = info[9][2]
+        d_feat = torch.empty(P, 256, device=dev)
+        d_small = torch.empty(P, 16 * (nbo0 - 16), device=dev)
+        _tg(tb + info[9][0], P, (16, 0, nbo0, nbo0 - 16), L.TG_NONE, gz, 256, 256, d_feat, 256, bias=False,
+            yb=d_small, ldyb=16 * (nbo0 - 16), stream=st)
+        d_nrm = d_small[:, 3 + nvw:3 + nvw + 3].contiguous() if view else None
+        return (None, None, d_nrm, d_feat, None, *dW, *db)
+
+
 def nerf(net, x_emb, v_emb):
     """Differentiable (sigma [P], rgb [P,3]) of a neurecon_amd NeRF background net."""
     Ws = [l.weight for l in net.pts_linears]
@@ -534,6 +837,9 @@ def sdf_nablas(surface, x, want_feat):
     """Differentiable (sdf, nablas, feature) of a neurecon_amd ImplicitSurface at points x [P,3]."""
     Ws = [l.effective_weight() for l in surface.surface_fc_layers]
     bs = [l.bias for l in surface.surface_fc_layers]
+    if uses_train_gemm(surface):
+        out = SdfNablaTG.apply(x.reshape(-1, 3).float().contiguous(), surface, bool(want_feat), *Ws, *bs)
+        return out if want_feat else (out[0], out[1], None)
     cfg = (surface.D, tuple(surface.skips), surface.embed_multires, bool(want_feat), bool(surface.use_siren))
     out = SdfNabla.apply(x.reshape(-1, 3).float().contiguous(), cfg, *Ws, *bs)
     return out if want_feat else (out[0], out[1], None)
@@ -543,5 +849,8 @@ def radiance(net, x, v, nrm, feat):
     Ws = [l.effective_weight() for l in net.layers]
     bs = [l.bias for l in net.layers]
     view = net.use_view_dirs
+    if uses_train_gemm(net):
+        return RadianceTG.apply(x.contiguous(), v.contiguous() if view else None, nrm.contiguous() if view else None,
+                                feat, net, *Ws, *bs)
     return RadianceFn.apply(x.contiguous(), v.contiguous() if view else None, nrm.contiguous() if view else None,
                             feat.contiguous(), (net.D, net.embed_multires_view, view, bool(net.use_siren)), *Ws, *bs)

@@ -418,3 +418,33 @@ def test_neus_many_samples_composite_fallback_vs_oracle(precision):
     assert (~ray_ok & d_same).sum() == 0
     assert (~ok_n.all(-1).reshape(-1) & d_same).sum() == 0
     assert d_same.mean() >= 0.5
+
+
+@pytest.mark.parametrize('perturb', [False, True])
+@pytest.mark.parametrize('calc_normal', [True, False])
+def test_neus_deferred_sample_nablas_bit_identical(perturb, calc_normal):
+    """The benchmarked f16x3 render defers the samples' reverse pass (defer_sample_nablas): sample
+    launches keep per-tile slabs, and only 16-sample tiles holding a sample of non-zero interval alpha
+    get nablas (the others are weighted by exactly 0 in normals_volume, neus.py:364-368).  Maps must
+    equal the render that computes every sample's nabla when drawn, bit for bit (4096 rays of config (b),
+    plus an 8192-ray call that runs two 4096-ray chunks)."""
+    from oracle import rays as orays
+    from neurecon_amd.frameworks.neus import volume_render
+    H, W, f, dist = wg.CAMERAS['b']
+    ro, rd, _ = orays.get_rays(wg.look_at_c2w(dist)[None], wg.intrinsics(f, H, W)[None], H, W)
+    m = neus_model(wg.neus_state(seed=1), precision='f16x3')
+    for rays in (4096, 8192):
+        o = ro.repeat(1, rays // 4096, 1).cuda()
+        d = (rd.repeat(1, rays // 4096, 1) * torch.linspace(0.9, 1.1, rays)[None, :, None]).cuda()
+        kw = dict(obj_bounding_radius=1.0, batched=True, calc_normal=calc_normal, detailed_output=False,
+                  perturb=perturb, N_samples=64, N_importance=64, N_upsample_iters=4)
+        outs = []
+        for defer in (True, False):
+            torch.manual_seed(3)
+            with torch.no_grad():
+                rgb, depth, ex = volume_render(o, d, m, defer_sample_nablas=defer, **kw)
+            outs.append([rgb, depth, ex['mask_volume']] + ([ex['normals_volume']] if calc_normal else []))
+        torch.cuda.synchronize()
+        for name, a, b in zip(('rgb', 'depth', 'mask', 'normals'), outs[0], outs[1]):
+            assert torch.equal(a, b), (rays, name, float((a - b).abs().max()))
+    print(f'deferred sample nablas: bit-identical (perturb={perturb}, calc_normal={calc_normal})')
