@@ -931,7 +931,20 @@ struct Pend4 {
   }
 };
 
-constexpr int kSlabRing = 3;  // softplus' slabs in LDS: one being read, one landing, one being staged
+constexpr int kSlabRing = 3;
+// cache policy of the forward softplus slab stores (read back by the reverse pass of the same tile)
+#ifndef NR_SLAB_NT
+#define NR_SLAB_NT true
+#endif
+// ... of the slab loads staged back into LDS (read once: nt keeps them from evicting the weight
+// stream's lines in L2; 3.80 -> 3.74 ms per 524 k-point nabla + feature launch)
+#ifndef NR_SLAB_LD_POL
+#define NR_SLAB_LD_POL " nt"
+#endif
+// ... of the geometry-feature and d sdf / d z7 stores
+#ifndef NR_FEAT_NT
+#define NR_FEAT_NT false
+#endif  // softplus' slabs in LDS: one being read, one landing, one being staged
 
 template <int CBMAX>
 struct WStream4 {
@@ -1053,8 +1066,8 @@ struct WStream4 {
     else
       asm volatile(
           "s_mov_b32 m0, %2\n\ts_nop 0\n\t"
-          "global_load_lds_dwordx4 %0, %1\n\t"
-          "global_load_lds_dwordx4 %0, %1 offset:1024"
+          "global_load_lds_dwordx4 %0, %1" NR_SLAB_LD_POL "\n\t"
+          "global_load_lds_dwordx4 %0, %1 offset:1024" NR_SLAB_LD_POL
           :
           : "v"(voff), "s"(g), "s"(base)
           : "memory", "m0");
@@ -1410,7 +1423,7 @@ struct FwdEpi4 {
                 oh[kNC - 1][c], ol[kNC - 1][c]);
 #endif
 #ifndef NR_EXP_NO_ESTORE  // timing experiment: softplus' slab not written
-      if constexpr (NABLA) pend_chunk(pd, sl, 2 * c, lane, true);
+      if constexpr (NABLA) pend_chunk(pd, sl, 2 * c, lane, NR_SLAB_NT);
 #endif
     }
   }
@@ -1451,7 +1464,7 @@ struct F7Epi4 {
       }
     }
     if constexpr (NABLA)
-      if (st == 7) pend_chunk(pd, g7, 2 * c, lane, false);
+      if (st == 7) pend_chunk(pd, g7, 2 * c, lane, NR_FEAT_NT);
   }
 };
 
@@ -1740,7 +1753,7 @@ void sdf4_kernel(SdfKArgs a) {
           pd.o[2 * q] = r + (2 * c) * 4;
           pd.o[2 * q + 1] = r + (2 * c + 1) * 4;
         }
-        pd.put(fb, 2 * kNC, false);
+        pd.put(fb, 2 * kNC, NR_FEAT_NT);
       };
       constexpr int NXT = NABLA ? C16 : C4;
       const char* n = NABLA ? OP(B7) : (has_next ? OP(F0) : nullptr);

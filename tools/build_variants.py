@@ -71,6 +71,11 @@ VARIANTS = {
     'nc2s': ['-DNR_DMA_SPREAD'],
     'nc1vnoepi': ['-DNR_SDF4_NC=1', '-DNR_SPLIT_VGPR', '-DNR_EXP_NO_EPI'],
     'nc2noepi': ['-DNR_EXP_NO_EPI'],
+    # slab stores with the default cache policy instead of nt (valid results)
+    'slabt': ['-DNR_SLAB_NT=false'],
+    'sldnt': ['-DNR_SLAB_LD_POL=" nt"'],      # the default since r03
+    'sldt': ['-DNR_SLAB_LD_POL=""'],          # slab loads with the default policy (the r02 build)
+    'sldnt_fnt': ['-DNR_SLAB_LD_POL=" nt"', '-DNR_FEAT_NT=true'],
 }
 
 
