@@ -50,8 +50,12 @@ RAY_FLOP = 2.0 * (255 * (MAC_SDF_FWD + MAC_SDF_BWD) + 127 * MAC_RAD)
 # tools/gpu_pmc.sh); counters cannot be read live, so the latest committed summary is reported.
 PMC_SUMMARY = {'f16x3': 'profiles/r02/f16x3_pmc_summary.json'}  # refreshed with tools/gpu_pmc.sh
 # device kernels behind each merged library kernel name (sdf_nabla = samples + mid-points launches)
-PMC_KERNEL = {('sdf_nabla', 'f16x3'): ('void nr::sdf4_kernel<true, false>(nr::SdfKArgs)',
-                                       'void nr::sdf4_kernel<true, true>(nr::SdfKArgs)'),
+PMC_KERNEL = {('sdf_nabla', 'f16x3'): ('void nr::sdf4_kernel<true, false>(nr::SdfKArgs)',       # r02 names
+                                       'void nr::sdf4_kernel<true, true>(nr::SdfKArgs)',
+                                       # r03: deferred sample nablas (forward + slabs, reverse pass), mid-points
+                                       'void nr::sdf4_kernel<true, false, 1>(nr::SdfKArgs)',
+                                       'void nr::sdf4_kernel<true, false, 2>(nr::SdfKArgs)',
+                                       'void nr::sdf4_kernel<true, true, 0>(nr::SdfKArgs)'),
               ('sdf_nabla', 'fp32'): ('void nr::sdf_kernel<0, true>(nr::SdfKArgs)',)}
 
 
@@ -278,6 +282,29 @@ def roofline(kstats, precision):
             'weight_stream': weight_stream(kstats) if precision == 'f16x3' else None}
 
 
+HBM_PEAK_TBPS = 8.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def train_roofline(kstats, dt, steps):
+    """Training step: the dominant library kernel is the layer GEMM (nr_train_gemm), whose launches
+    stream [P, <=288] fp32 activations: HBM-bound.  achieved = algorithmic bytes of its calls (inputs,
+    outputs, epilogue operands; training.TG_BYTES, counted per call by the host) / their device time.
+    share_of_step: the library kernels' device time / the step time (the rest: hipBLASLt weight
+    gradients and the fp32 radiance forward, torch elementwise, Adam)."""
+    from neurecon_amd import training as T
+    n, ms, _ = kstats.get('train_gemm', (0, 0.0, 0.0))
+    lib_ms = sum(v[1] for v in kstats.values())
+    if not n:
+        return None
+    by = T.TG_BYTES['bytes'] / max(T.TG_BYTES['calls'], 1) * n  # bytes of the timed launches
+    tbps = by / (ms * 1e-3) / 1e12
+    return {'bound': 'hbm', 'achieved': round(tbps, 3), 'peak': HBM_PEAK_TBPS, 'unit': 'TB/s',
+            'frac': round(tbps / HBM_PEAK_TBPS, 4), 'traffic': None, 'kernel': 'train_gemm',
+            'avg_launch_ms': round(ms / n, 4), 'launches': n, 'bytes_per_launch': by / n,
+            'share_of_library_time': round(ms / max(lib_ms, 1e-9), 4),
+            'library_share_of_step': round(lib_ms * 1e-3 / max(dt, 1e-12), 4)}
+
+
 def frame_d_setup(dev, precision):
     """config (d): NeuS + NeRF++ (N_outside=32), full 800x600 frame of the config-(d) camera (H=600,
     W=800, f=800, camera at distance 2), rays sharded over the ranks; the frame's maps are
@@ -501,6 +528,7 @@ def run(args):
                               'parallelism': f'ray-sharded x{world} + all_gather'},
                    'roofline': roof}
         elif args.workload == 'train':
+            roof = train_roofline(kstats, dt, args.steps)
             out = {'metric': 'training rays/sec, NeuS (configs/neus.yaml: 512 rays per GPU, fwd+bwd+Adam)',
                    'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
                    'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,

@@ -292,7 +292,8 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   if (defer) {  // nablas of the tiles holding a sample of non-zero interval weight; the rest stay 0
     const int64_t nslot = (int64_t)c.S * R, ntile = nslot / 16;
     NR_HIP_CHECK(hipMemsetAsync(c.nraw, 0, (size_t)nslot * 3 * sizeof(float), st));
-    if (a.calc_normal) {  // normals_volume is the only reader of the sample nablas here
+    if (a.calc_normal && a.N_outside == 0) {  // normals_volume is the only reader of the sample nablas here
+      // (with NeRF++ the flags need the background's alphas: after the background net, below)
       NR_HIP_CHECK(hipMemsetAsync(c.tflag, 0, (size_t)ntile * sizeof(int), st));
       NR_HIP_CHECK(hipMemsetAsync(c.tcnt, 0, sizeof(int), st));
       const int64_t nq = (int64_t)(c.S - 1) * R;
@@ -313,7 +314,8 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   }
   {
     ProfScope prof("neus_points", (double)R, st);
-    hipLaunchKernelGGL(neus_expand, dim3((unsigned)(((int64_t)c.S * R + 255) / 256)), dim3(256), 0, st, c);
+    hipLaunchKernelGGL(neus_expand, dim3((unsigned)(((int64_t)c.S * R + 255) / 256)), dim3(256), 0, st, c,
+                       (int)!(defer && a.N_outside > 0));
   }
   NR_HIP_CHECK(hipGetLastError());
   // SDF + nablas at the samples (neus.py:294); already in sv / nv on the fused path
@@ -378,8 +380,34 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
       hipLaunchKernelGGL(neus_outside_scatter, g1, dim3(256), 0, st, slot, sigc, radc, Po, c.sig_o, c.rad_o);
       NR_HIP_CHECK(hipGetLastError());
     }
+    if (defer) {  // deferred sample nablas: tiles holding a sample whose (inside or background) alpha != 0
+      const int64_t nslot = (int64_t)c.S * R, ntile = nslot / 16;
+      if (a.calc_normal) {
+        NR_HIP_CHECK(hipMemsetAsync(c.tflag, 0, (size_t)ntile * sizeof(int), st));
+        NR_HIP_CHECK(hipMemsetAsync(c.tcnt, 0, sizeof(int), st));
+        hipLaunchKernelGGL(neus_sample_need_outside, dim3((unsigned)((nslot + 255) / 256)), dim3(256), 0, st, c,
+                           a.s_dev, a.s);
+        NR_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(neus_tile_list, dim3((unsigned)((ntile + 1023) / 1024)), dim3(1024), 0, st, c, ntile);
+        NR_HIP_CHECK(hipGetLastError());
+        if ((rc = launch_sdf_deferred(SL, a.sdf_packed, c.pts, nslot, nullptr, c.nraw, a.sdf->multires, c.slabs,
+                                      c.tiles, c.tcnt, 2, st)))
+          return rc;
+      }
+      hipLaunchKernelGGL(neus_gather_nablas, dim3((unsigned)((nslot + 255) / 256)), dim3(256), 0, st, c);
+      NR_HIP_CHECK(hipGetLastError());
+    }
     ProfScope prof("neus_composite", (double)R, st);
-    hipLaunchKernelGGL(neus_composite_outside, grd, blk, 0, st, c, o, a.s_dev, a.s, a.calc_normal, a.white_bkgd);
+    const int M = c.S - 1 + a.N_outside;
+    const size_t lds1 = (6 * (size_t)M + 4 * (size_t)c.S) * sizeof(float);  // wave-per-ray staging of one ray
+    if (4 * lds1 <= 65536)
+      hipLaunchKernelGGL((neus_composite_outside_w<4>), dim3((unsigned)((R + 3) / 4)), dim3(64), 4 * lds1, st, c, o,
+                         a.s_dev, a.s, a.calc_normal, a.white_bkgd);
+    else if (lds1 <= 65536)
+      hipLaunchKernelGGL((neus_composite_outside_w<1>), dim3((unsigned)R), dim3(64), lds1, st, c, o, a.s_dev, a.s,
+                         a.calc_normal, a.white_bkgd);
+    else
+      hipLaunchKernelGGL(neus_composite_outside, grd, blk, 0, st, c, o, a.s_dev, a.s, a.calc_normal, a.white_bkgd);
   } else {
     ProfScope prof("neus_composite", (double)R, st);
     const size_t lds1 = 9 * (size_t)c.S * sizeof(float);  // four rays per wave when four rays' staging fits
@@ -396,9 +424,9 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
 
 static int64_t neus_chunk_rays(const NrNeusArgs* a) {
   int64_t cap = 16384;
-  // deferred sample nablas keep 8 KB per sample of the chunk: <= 4096 rays of 128 samples (4.3 GB),
-  // a multiple of 16 rays
-  if (neus_deferred(*a, 16)) cap = std::max<int64_t>(16, (int64_t)(4096 * 128 / std::max(neus_total_samples(*a), 1)) / 16 * 16);
+  // deferred sample nablas keep 8 KB per sample of the chunk: <= 16 GB of slabs (16384 rays of 128
+  // samples; smaller chunks leave the per-ray kernels a fraction of the chip), a multiple of 16 rays
+  if (neus_deferred(*a, 16)) cap = std::max<int64_t>(16, (int64_t)(16384 * 128 / std::max(neus_total_samples(*a), 1)) / 16 * 16);
   return a->n_rays < cap ? (a->n_rays > 0 ? a->n_rays : 1) : cap;
 }
 

@@ -66,12 +66,14 @@ bool neus_deferred(const NrNeusArgs& a, int64_t R);
 int neus_total_samples(const NrNeusArgs& a);
 __global__ void neus_sample_need(NeusChunk c, const float* s_dev, float s_val);
 __global__ void neus_tile_list(NeusChunk c, int64_t n_tiles);
+__global__ void neus_sample_need_outside(NeusChunk c, const float* s_dev, float s_val);
+__global__ void neus_gather_nablas(NeusChunk c);
 
 __global__ void neus_prologue(NeusChunk c, const float* rays_o, const float* rays_d, const float* t_coarse,
                               float r_obj, float near_bypass, float far_bypass);
 __global__ void neus_upsample(NeusChunk c, int it, const float* u, int64_t u_stride);
 __global__ void neus_merge(NeusChunk c, int L, float* dv2, float* sv2, int* idv2);
-__global__ void neus_expand(NeusChunk c);
+__global__ void neus_expand(NeusChunk c, int gather);
 template <int RPW>
 __global__ void neus_composite(NeusChunk c, NeusOut o, const float* s_dev, float s_val, int calc_normal, int white_bkgd);
 __global__ void neus_outside_points(NeusChunk c, const float* t_rand);
@@ -85,6 +87,9 @@ __global__ void neus_nograd_points(NeusChunk c);
 __global__ void neus_direct_upsample(NeusChunk c, int more, const float* u, int64_t u_stride);
 __global__ void neus_composite_outside(NeusChunk c, NeusOut o, const float* s_dev, float s_val, int calc_normal,
                                        int white_bkgd);
+template <int RPW>
+__global__ void neus_composite_outside_w(NeusChunk c, NeusOut o, const float* s_dev, float s_val, int calc_normal,
+                                         int white_bkgd);
 __global__ void neus_write_dall(const float* dv, int64_t R, int S, int64_t ray0, float* out);
 __global__ void sample_pdf_kernel(const float* bins, const float* weights, int64_t R, int L, const float* u,
                                   int64_t u_stride, int N, float* out);

@@ -229,7 +229,9 @@ __global__ void neus_merge(NeusChunk c, int L, float* __restrict__ dv2, float* _
 
 // per (sample, ray) after the final merge: sample points (or, fused, the sorted nablas) and the
 // S-1 mid-points d_mid = (d_s + d_{s-1}) / 2 (neus.py:284-288); sample-major, fully parallel
-__global__ void neus_expand(NeusChunk c) {
+// gather = 0: the fused path's nablas are gathered later (neus_gather_nablas: the deferred reverse
+// pass of a NeRF++ render runs after the background net)
+__global__ void neus_expand(NeusChunk c, int gather) {
   const int64_t R = c.R;
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= (int64_t)c.S * R) return;
@@ -238,9 +240,11 @@ __global__ void neus_expand(NeusChunk c) {
   const float dx = c.rd[r * 3], dy = c.rd[r * 3 + 1], dz = c.rd[r * 3 + 2];
   const float d = c.dv[q];
   if (c.idv) {  // fused: nablas of the sorted samples from their evaluation slots
-    const int64_t qs = (int64_t)c.idv[q] * R + r;
+    if (gather) {
+      const int64_t qs = (int64_t)c.idv[q] * R + r;
 #pragma unroll
-    for (int e = 0; e < 3; ++e) c.nab_f[q * 3 + e] = c.nraw[qs * 3 + e];
+      for (int e = 0; e < 3; ++e) c.nab_f[q * 3 + e] = c.nraw[qs * 3 + e];
+    }
   } else {
     c.pts[q * 3 + 0] = fadd(ox, fmul(dx, d));
     c.pts[q * 3 + 1] = fadd(oy, fmul(dy, d));
@@ -254,6 +258,17 @@ __global__ void neus_expand(NeusChunk c) {
     c.mids[qm * 3 + 1] = fadd(oy, fmul(dy, dm));
     c.mids[qm * 3 + 2] = fadd(oz, fmul(dz, dm));
   }
+}
+
+// the fused path's sample nablas into sorted order (neus_expand's gather, run on its own)
+__global__ void neus_gather_nablas(NeusChunk c) {
+  const int64_t R = c.R;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (int64_t)c.S * R) return;
+  const int64_t r = q - (q / R) * R;
+  const int64_t qs = (int64_t)c.idv[q] * R + r;
+#pragma unroll
+  for (int e = 0; e < 3; ++e) c.nab_f[q * 3 + e] = c.nraw[qs * 3 + e];
 }
 
 // compositing (neus.py:296, :346-380), RPW rays per wave (64 / RPW lanes each): logistic CDFs,
@@ -584,6 +599,9 @@ __global__ void neus_mid_compact(NeusChunk c, const float* __restrict__ s_dev, f
   }
 }
 
+// F.softplus (beta 1, threshold 20)
+__device__ __forceinline__ float softplus1(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
+
 // deferred sample nablas: flag the 16-slot tile (evaluation order) of every sorted sample i < S-1 whose
 // interval alpha is not exactly 0 -- neus_composite weights sample i's unit nabla by w_i = alpha_i T_i
 // (neus.py:364-368), so the others contribute exactly 0 (their nablas stay 0, normalize(0) = 0).
@@ -599,6 +617,38 @@ __global__ void neus_sample_need(NeusChunk c, const float* __restrict__ s_dev, f
   const float cp = sigmoidf_ref(fmul(c.sdf_f[(int64_t)i * R + r], s_inv));
   const float cn = sigmoidf_ref(fmul(c.sdf_f[(int64_t)(i + 1) * R + r], s_inv));
   const float alpha = fmaxf(fdiv(fsub(cp, cn), fadd(cp, 1e-10f)), 0.0f);
+  if (!(alpha == 0.0f)) c.tflag[((int64_t)c.idv[q] * R + r) >> 4] = 1;
+}
+
+// the same with the NeRF++ background (neus_composite_outside): sample k < S weights its unit nabla by
+// w_k = alpha_k T_k, alpha_k the SDF alpha of interval k if mid-point k is inside the bounding sphere,
+// else the background's 1 - exp(-softplus(sigma) dist) -- also for k = S-1, whose weight is the first
+// inverted-sphere sample's (neus.py:364-366 pairs min(#weights, #nablas) = S of them).  Runs after the
+// background net (sig_o) with the compositing's own arithmetic; a tile is flagged if any alpha != 0.
+__global__ void neus_sample_need_outside(NeusChunk c, const float* __restrict__ s_dev, float s_val) {
+  const int64_t R = c.R;
+  const int S = c.S, S1 = S - 1, M = S1 + c.N_out;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (int64_t)S * R) return;
+  const int k = (int)(q / R);
+  const int64_t r = q - (int64_t)k * R;
+  bool inside = false;
+  float alpha = 0.0f;
+  if (k < S1) {
+    const float s_inv = s_dev ? *s_dev : s_val;
+    const float cp = sigmoidf_ref(fmul(c.sdf_f[(int64_t)k * R + r], s_inv));
+    const float cn = sigmoidf_ref(fmul(c.sdf_f[(int64_t)(k + 1) * R + r], s_inv));
+    alpha = fmaxf(fdiv(fsub(cp, cn), fadd(cp, 1e-10f)), 0.0f);
+    const float dm = c.dmid[q];
+    const float px = fadd(c.ro[r * 3], fmul(c.rd[r * 3], dm)), py = fadd(c.ro[r * 3 + 1], fmul(c.rd[r * 3 + 1], dm)),
+                pz = fadd(c.ro[r * 3 + 2], fmul(c.rd[r * 3 + 2], dm));
+    inside = norm3_ref(px, py, pz) <= c.r_obj;
+  }
+  if (!inside) {
+    const float dk = c.d_out[q];
+    const float dist = k + 1 < M ? fsub(c.d_out[q + R], dk) : 1e10f;
+    alpha = fsub(1.0f, expf(fmul(-softplus1(c.sig_o[q]), dist)));
+  }
   if (!(alpha == 0.0f)) c.tflag[((int64_t)c.idv[q] * R + r) >> 4] = 1;
 }
 
@@ -632,8 +682,144 @@ __global__ void neus_outside_scatter(const int* __restrict__ slot, const float* 
   rad_o[q * 3 + 2] = radc[(int64_t)j * 3 + 2];
 }
 
-// F.softplus (beta 1, threshold 20)
-__device__ __forceinline__ float softplus1(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
+
+// compositing with the background merged in, RPW rays per wave (neus_composite's structure): the
+// per-sample CDFs, the inside test, the inside / background alphas, radiance and unit nablas across the
+// ray's lanes into LDS; the transmittance product and the fp64 sums on the ray's first lane in sample
+// order with the per-ray version's arithmetic (bit-identical maps; that version, one thread per ray,
+// remains the fallback when the LDS staging does not fit).  LDS per ray: 6 M + 4 S floats.
+template <int RPW>
+__global__ __launch_bounds__(64) void neus_composite_outside_w(NeusChunk c, NeusOut o, const float* __restrict__ s_dev,
+                                                               float s_val, int calc_normal, int white_bkgd) {
+  extern __shared__ float lds[];
+  constexpr int NL = 64 / RPW;
+  const float s_inv = s_dev ? *s_dev : s_val;
+  const int r = blockIdx.x * RPW + (int)threadIdx.x / NL, l = (int)threadIdx.x % NL;
+  const int S = c.S, S1 = S - 1, M = S1 + c.N_out;
+  const int Nn = M < S ? M : S;  // normals use min(#weights, #nablas) samples (neus.py:364-366)
+  const int64_t R = c.R;
+  const bool live = r < R;
+  const int Sl = live ? S : 0, Ml = live ? M : 0, Nl = live ? Nn : 0;
+  const int64_t ro = o.ray0 + r;
+  float* scdf = lds + ((int)threadIdx.x / NL) * (6 * M + 4 * S);  // [S]
+  float* sal = scdf + S;       // [M] alpha, then weights
+  float* srad = sal + M;       // [M][3]
+  float* sdo = srad + 3 * M;   // [M] d_out
+  float* dum = sdo + M;        // [M] (pad)
+  float* snrm = dum + M;       // [S][3] unit nablas
+  for (int i = l; i < Sl; i += NL) {
+    const float cdf = sigmoidf_ref(fmul(c.sdf_f[(int64_t)i * R + r], s_inv));
+    scdf[i] = cdf;
+    if (o.cdf) o.cdf[ro * S + i] = cdf;
+  }
+  __syncthreads();
+  for (int k = l; k < Ml; k += NL) {
+    const int64_t q = (int64_t)k * R + r;
+    const float dk = c.d_out[q];
+    sdo[k] = dk;
+    bool inside = false;
+    float a_in = 0.0f;
+    if (k < S1) {
+      const float cp = scdf[k], cn = scdf[k + 1];
+      a_in = fmaxf(fdiv(fsub(cp, cn), fadd(cp, 1e-10f)), 0.0f);
+      const float dm = c.dmid[q];
+      const float px = fadd(c.ro[r * 3], fmul(c.rd[r * 3], dm)), py = fadd(c.ro[r * 3 + 1], fmul(c.rd[r * 3 + 1], dm)),
+                  pz = fadd(c.ro[r * 3 + 2], fmul(c.rd[r * 3 + 2], dm));
+      inside = norm3_ref(px, py, pz) <= c.r_obj;
+    }
+    float alpha;
+    if (inside) {
+      alpha = a_in;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) srad[k * 3 + e] = c.rad_m[q * 3 + e];
+    } else {
+      const float dist = k + 1 < M ? fsub(c.d_out[q + R], dk) : 1e10f;
+      alpha = fsub(1.0f, expf(fmul(-softplus1(c.sig_o[q]), dist)));
+#pragma unroll
+      for (int e = 0; e < 3; ++e) srad[k * 3 + e] = c.rad_o[q * 3 + e];
+    }
+    sal[k] = alpha;
+    if (o.alpha) o.alpha[ro * M + k] = alpha;
+  }
+  if (calc_normal) {
+    for (int k = l; k < Nl; k += NL) {
+      const int64_t q = (int64_t)k * R + r;
+      float x = c.nab_f[q * 3 + 0], y = c.nab_f[q * 3 + 1], z = c.nab_f[q * 3 + 2];
+      normalize3(x, y, z);
+      snrm[k * 3 + 0] = x;
+      snrm[k * 3 + 1] = y;
+      snrm[k * 3 + 2] = z;
+    }
+  }
+  __syncthreads();
+  if (l == 0 && live) {
+    double T = 1.0, acc = 0.0, rgb0 = 0.0, rgb1 = 0.0, rgb2 = 0.0, n0 = 0.0, n1 = 0.0, n2 = 0.0;
+    for (int k = 0; k < M; ++k) {
+      const float alpha = sal[k];
+      const float w = fmul(alpha, (float)T);
+      T *= (double)fadd(fsub(1.0f, alpha), 1e-10f);
+      rgb0 += (double)fmul(w, srad[k * 3 + 0]);
+      rgb1 += (double)fmul(w, srad[k * 3 + 1]);
+      rgb2 += (double)fmul(w, srad[k * 3 + 2]);
+      acc += (double)w;
+      if (calc_normal && k < Nn) {
+        n0 += (double)fmul(snrm[k * 3 + 0], w);
+        n1 += (double)fmul(snrm[k * 3 + 1], w);
+        n2 += (double)fmul(snrm[k * 3 + 2], w);
+      }
+      sal[k] = w;
+    }
+    const float accf = (float)acc;
+    const float denom = fadd(accf, 1e-10f);
+    double depth = 0.0;
+    for (int k = 0; k < M; ++k) depth += (double)fmul(fdiv(sal[k], denom), sdo[k]);
+    float q0 = (float)rgb0, q1 = (float)rgb1, q2 = (float)rgb2;
+    if (white_bkgd) {
+      const float bg = fsub(1.0f, accf);
+      q0 = fadd(q0, bg); q1 = fadd(q1, bg); q2 = fadd(q2, bg);
+    }
+    o.rgb[ro * 3 + 0] = q0;
+    o.rgb[ro * 3 + 1] = q1;
+    o.rgb[ro * 3 + 2] = q2;
+    o.depth[ro] = (float)depth;
+    o.acc[ro] = accf;
+    if (calc_normal && o.normals) {
+      o.normals[ro * 3 + 0] = (float)n0;
+      o.normals[ro * 3 + 1] = (float)n1;
+      o.normals[ro * 3 + 2] = (float)n2;
+    }
+  }
+  __syncthreads();
+  // detailed per-sample outputs, ray-major
+  for (int k = l; k < Ml; k += NL) {
+    const int64_t q = (int64_t)k * R + r;
+    if (o.weights) o.weights[ro * M + k] = sal[k];
+    if (o.d_final) o.d_final[ro * M + k] = sdo[k];
+    if (o.radiance) {
+      o.radiance[(ro * M + k) * 3 + 0] = srad[k * 3 + 0];
+      o.radiance[(ro * M + k) * 3 + 1] = srad[k * 3 + 1];
+      o.radiance[(ro * M + k) * 3 + 2] = srad[k * 3 + 2];
+    }
+    if (o.sigma_out) o.sigma_out[ro * M + k] = c.sig_o[q];
+    if (o.radiance_bg) {
+      o.radiance_bg[(ro * M + k) * 3 + 0] = c.rad_o[q * 3 + 0];
+      o.radiance_bg[(ro * M + k) * 3 + 1] = c.rad_o[q * 3 + 1];
+      o.radiance_bg[(ro * M + k) * 3 + 2] = c.rad_o[q * 3 + 2];
+    }
+  }
+  for (int i = l; i < Sl; i += NL) {
+    const int64_t q = (int64_t)i * R + r;
+    if (o.sdf) o.sdf[ro * S + i] = c.sdf_f[q];
+    if (o.nablas) {
+      o.nablas[(ro * S + i) * 3 + 0] = c.nab_f[q * 3 + 0];
+      o.nablas[(ro * S + i) * 3 + 1] = c.nab_f[q * 3 + 1];
+      o.nablas[(ro * S + i) * 3 + 2] = c.nab_f[q * 3 + 2];
+    }
+  }
+}
+
+template __global__ void neus_composite_outside_w<1>(NeusChunk, NeusOut, const float*, float, int, int);
+template __global__ void neus_composite_outside_w<4>(NeusChunk, NeusOut, const float*, float, int, int);
 
 // compositing with the background merged in (neus.py:325-343, :346-380)
 __global__ __launch_bounds__(64) void neus_composite_outside(NeusChunk c, NeusOut o, const float* __restrict__ s_dev,
@@ -843,13 +1029,13 @@ int neus_total_samples(const NrNeusArgs& a) {
   return direct ? a.N_samples + a.N_importance : a.N_samples + a.N_upsample_iters * n_up0;
 }
 
-// official_solution, render mode without the per-sample nablas (detailed outputs), no NeRF++ (its
-// compositing weights the samples' nablas by the background's alpha too), the f16x3 softplus net, and
-// slots that tile exactly (R % 16 == 0: every launch starts a tile)
+// official_solution, render mode without the per-sample nablas (detailed outputs), the f16x3 softplus
+// net, and slots that tile exactly (R % 16 == 0: every launch starts a tile).  With NeRF++ the tiles
+// are flagged after the background net (neus_sample_need_outside); not with its detailed outputs.
 bool neus_deferred(const NrNeusArgs& a, int64_t R) {
   return a.upsample_algo == NR_UPSAMPLE_OFFICIAL && !a.sample_only && !a.nablas_out && !a.no_mid_skip &&
-         !a.no_defer && a.N_outside == 0 && a.sdf && a.sdf->precision == NR_PREC_F16X3 && !a.sdf->siren &&
-         R > 0 && R % 16 == 0;
+         !a.no_defer && !(a.N_outside > 0 && (a.sigma_out || a.radiance_bg_out || a.radiance_out)) && a.sdf &&
+         a.sdf->precision == NR_PREC_F16X3 && !a.sdf->siren && R > 0 && R % 16 == 0;
 }
 
 }  // namespace nr

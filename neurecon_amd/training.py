@@ -529,10 +529,27 @@ class UnisurfComposite(torch.autograd.Function):
 # ---------------------------------------------------------------------------------------------
 # f16x3 training GEMM path (nr_train_gemm)
 # ---------------------------------------------------------------------------------------------
+# algorithmic HBM bytes of the nr_train_gemm calls issued since the last reset (the training bench's
+# roofline: these launches stream [P, <=288] fp32 activations, ~4 B per element read or written)
+TG_BYTES = {'bytes': 0.0, 'calls': 0}
+
+
+def _tg_bytes(P, shape, n1, n2, y, yb, y2, y3, a, g, g_row, zd, dot):
+    KB, KB2, NBO, NB2 = shape
+    ny, nyb = 16 * (NBO - NB2), 16 * NB2
+    cols = n1 + n2                                                       # inputs
+    cols += ny * ((y is not None) + (y2 is not None) + (y3 is not None)) + nyb * (yb is not None)  # outputs
+    cols += ny * ((a is not None) + (g is not None and not g_row) + (zd is not None))             # epilogue inputs
+    cols += dot is not None
+    return 4.0 * P * cols
+
+
 def _tg(op, P, shape, mode, x1, ld1, n1, y, ldy, x2=None, ld2=0, n2=0, bias=True, yscale=1.0, yb=None, ldyb=0,
         y2=None, ldy2=0, y3=None, ldy3=0, a=None, lda=0, g=None, ldg=0, zd=None, ldzd=0, g_row=False, dot=None,
         dot_bias=0.0, head=None, head_bias=None, head_out=None, stream=None):
     """one training layer GEMM: shape = (KB, KB2, NBO, NB2) of the packed op at device address `op`"""
+    TG_BYTES['bytes'] += _tg_bytes(P, shape, n1, n2, y, yb, y2, y3, a, g, g_row, zd, dot)
+    TG_BYTES['calls'] += 1
     def _p(v):  # tensor, raw device address or None
         return None if v is None else (v if isinstance(v, int) else v.data_ptr())
     t = L.NrTrainGemm()

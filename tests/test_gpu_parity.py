@@ -422,22 +422,30 @@ def test_neus_many_samples_composite_fallback_vs_oracle(precision):
 
 @pytest.mark.parametrize('perturb', [False, True])
 @pytest.mark.parametrize('calc_normal', [True, False])
-def test_neus_deferred_sample_nablas_bit_identical(perturb, calc_normal):
+@pytest.mark.parametrize('N_outside', [0, 32])
+def test_neus_deferred_sample_nablas_bit_identical(perturb, calc_normal, N_outside):
     """The benchmarked f16x3 render defers the samples' reverse pass (defer_sample_nablas): sample
-    launches keep per-tile slabs, and only 16-sample tiles holding a sample of non-zero interval alpha
-    get nablas (the others are weighted by exactly 0 in normals_volume, neus.py:364-368).  Maps must
-    equal the render that computes every sample's nabla when drawn, bit for bit (4096 rays of config (b),
-    plus an 8192-ray call that runs two 4096-ray chunks)."""
+    launches keep per-tile slabs, and only 16-sample tiles holding a sample of non-zero alpha get
+    nablas (the others are weighted by exactly 0 in normals_volume, neus.py:364-368).  With NeRF++
+    (N_outside 32) a sample's weight uses the background's alpha outside the bounding sphere, and the
+    last sample's the first inverted-sphere sample's, so the tiles are flagged after the background net.
+    Maps must equal the render that computes every sample's nabla when drawn, bit for bit (4096 rays of
+    config (b), or of the config-(d) camera fanned out so that some leave the sphere, plus an 8192-ray
+    call that runs two chunks)."""
     from oracle import rays as orays
     from neurecon_amd.frameworks.neus import volume_render
     H, W, f, dist = wg.CAMERAS['b']
+    if N_outside:
+        dist = wg.CAMERAS['d'][3]
+        f = 80.0  # a wide view: rays that miss the bounding sphere, and rays past its rim
     ro, rd, _ = orays.get_rays(wg.look_at_c2w(dist)[None], wg.intrinsics(f, H, W)[None], H, W)
-    m = neus_model(wg.neus_state(seed=1), precision='f16x3')
+    sd = wg.neus_state(seed=1, use_outside_nerf=bool(N_outside))
+    m = neus_model(sd, precision='f16x3', use_outside_nerf=bool(N_outside))
     for rays in (4096, 8192):
         o = ro.repeat(1, rays // 4096, 1).cuda()
         d = (rd.repeat(1, rays // 4096, 1) * torch.linspace(0.9, 1.1, rays)[None, :, None]).cuda()
         kw = dict(obj_bounding_radius=1.0, batched=True, calc_normal=calc_normal, detailed_output=False,
-                  perturb=perturb, N_samples=64, N_importance=64, N_upsample_iters=4)
+                  perturb=perturb, N_samples=64, N_importance=64, N_upsample_iters=4, N_outside=N_outside)
         outs = []
         for defer in (True, False):
             torch.manual_seed(3)
@@ -447,4 +455,4 @@ def test_neus_deferred_sample_nablas_bit_identical(perturb, calc_normal):
         torch.cuda.synchronize()
         for name, a, b in zip(('rgb', 'depth', 'mask', 'normals'), outs[0], outs[1]):
             assert torch.equal(a, b), (rays, name, float((a - b).abs().max()))
-    print(f'deferred sample nablas: bit-identical (perturb={perturb}, calc_normal={calc_normal})')
+    print(f'deferred sample nablas: bit-identical (perturb={perturb}, calc_normal={calc_normal}, N_outside={N_outside})')
