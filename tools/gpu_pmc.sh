@@ -8,6 +8,6 @@ OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 ${T_PROF:-420} rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/$C -o run \
-    -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-full-eval ${BENCH_ARGS} > $OUT/$C.log 2>&1 || { echo "pmc $C failed"; exit 1; }
+    -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-full-eval --no-frame ${BENCH_ARGS} > $OUT/$C.log 2>&1 || { echo "pmc $C failed"; exit 1; }
 done
 python3 tools/pmc_summary.py $OUT > $OUT/summary.json && cat $OUT/summary.json
