@@ -267,134 +267,175 @@ __global__ void neus_points_kernel(const float* __restrict__ ro, const float* __
 // NeuS compositing with a differentiable graph (neus.py:28-70, :346-355), one thread per ray.
 // sdf [R,S], radiance [R,S-1,3], dmid [R,S-1]; s from the device.  fp64 prefix products / sums
 // rounded per element, as in the render kernels.
-__global__ void neus_composite_fwd_kernel(const float* __restrict__ sdf, const float* __restrict__ s_dev,
+// One ray per 64-lane wave: the per-sample work (CDFs, alphas, staging, the backward's weight
+// adjoints and output stores) across the lanes through LDS, the order-sensitive scans on lane 0 with
+// the per-ray version's arithmetic (512-ray training batches gave the per-thread version 8 waves for
+// the chip).  LDS: fwd 7 S floats, bwd 9 S floats + 4 doubles.
+__global__ __launch_bounds__(64) void neus_composite_fwd_kernel(const float* __restrict__ sdf, const float* __restrict__ s_dev,
                                           const float* __restrict__ rad, const float* __restrict__ dmid, int64_t R,
                                           int S, int white_bkgd, float* __restrict__ rgb, float* __restrict__ depth,
                                           float* __restrict__ acc, float* __restrict__ w_out,
                                           float* __restrict__ alpha_out, float* __restrict__ cdf_out) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R) return;
+  extern __shared__ float lds[];
+  const int64_t r = blockIdx.x;
+  const int l = threadIdx.x, S1 = S - 1;
   const float s = *s_dev;
   const float* sd = sdf + r * S;
-  double T = 1.0, a_acc = 0.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
-  float cp = sigmoidf_ref(fmul(sd[0], s));
-  if (cdf_out) cdf_out[r * S] = cp;
-  for (int i = 0; i < S - 1; ++i) {
-    const float cn = sigmoidf_ref(fmul(sd[i + 1], s));
-    if (cdf_out) cdf_out[r * S + i + 1] = cn;
-    const float al = fmaxf(fdiv(fsub(cp, cn), fadd(cp, 1e-10f)), 0.0f);
-    const float w = fmul(al, (float)T);
-    T *= (double)fadd(fsub(1.0f, al), 1e-10f);
-    const int64_t q = r * (S - 1) + i;
-    c0 += (double)fmul(w, rad[q * 3 + 0]);
-    c1 += (double)fmul(w, rad[q * 3 + 1]);
-    c2 += (double)fmul(w, rad[q * 3 + 2]);
-    a_acc += (double)w;
-    w_out[q] = w;
+  float* lc = lds;           // [S] cdf
+  float* la = lc + S;        // [S] alpha
+  float* lw = la + S;        // [S] weights
+  float* lr = lw + S;        // [3 S] radiance
+  float* ld = lr + 3 * S;    // [S] mid depths
+  for (int i = l; i < S; i += 64) {
+    const float c = sigmoidf_ref(fmul(sd[i], s));
+    lc[i] = c;
+    if (cdf_out) cdf_out[r * S + i] = c;
+  }
+  __syncthreads();
+  for (int i = l; i < S1; i += 64) {
+    const int64_t q = r * S1 + i;
+    const float al = fmaxf(fdiv(fsub(lc[i], lc[i + 1]), fadd(lc[i], 1e-10f)), 0.0f);
+    la[i] = al;
     if (alpha_out) alpha_out[q] = al;
-    cp = cn;
+    lr[i * 3 + 0] = rad[q * 3 + 0];
+    lr[i * 3 + 1] = rad[q * 3 + 1];
+    lr[i * 3 + 2] = rad[q * 3 + 2];
+    ld[i] = dmid[q];
   }
-  const float accf = (float)a_acc;
-  const float den = fadd(accf, 1e-10f);
-  double dep = 0.0;
-  for (int i = 0; i < S - 1; ++i) dep += (double)fmul(fdiv(w_out[r * (S - 1) + i], den), dmid[r * (S - 1) + i]);
-  float o0 = (float)c0, o1 = (float)c1, o2 = (float)c2;
-  if (white_bkgd) {
-    const float bg = fsub(1.0f, accf);
-    o0 = fadd(o0, bg); o1 = fadd(o1, bg); o2 = fadd(o2, bg);
+  __syncthreads();
+  if (l == 0) {
+    double T = 1.0, a_acc = 0.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
+    for (int i = 0; i < S1; ++i) {
+      const float al = la[i];
+      const float w = fmul(al, (float)T);
+      T *= (double)fadd(fsub(1.0f, al), 1e-10f);
+      c0 += (double)fmul(w, lr[i * 3 + 0]);
+      c1 += (double)fmul(w, lr[i * 3 + 1]);
+      c2 += (double)fmul(w, lr[i * 3 + 2]);
+      a_acc += (double)w;
+      lw[i] = w;
+    }
+    const float accf = (float)a_acc;
+    const float den = fadd(accf, 1e-10f);
+    double dep = 0.0;
+    for (int i = 0; i < S1; ++i) dep += (double)fmul(fdiv(lw[i], den), ld[i]);
+    float o0 = (float)c0, o1 = (float)c1, o2 = (float)c2;
+    if (white_bkgd) {
+      const float bg = fsub(1.0f, accf);
+      o0 = fadd(o0, bg); o1 = fadd(o1, bg); o2 = fadd(o2, bg);
+    }
+    rgb[r * 3 + 0] = o0;
+    rgb[r * 3 + 1] = o1;
+    rgb[r * 3 + 2] = o2;
+    depth[r] = (float)dep;
+    acc[r] = accf;
   }
-  rgb[r * 3 + 0] = o0;
-  rgb[r * 3 + 1] = o1;
-  rgb[r * 3 + 2] = o2;
-  depth[r] = (float)dep;
-  acc[r] = accf;
+  __syncthreads();
+  for (int i = l; i < S1; i += 64) w_out[r * S1 + i] = lw[i];
 }
 
 // backward of the above: grads of rgb [R,3], depth [R], acc [R] and (optional) the visibility
 // weights [R,S-1] -> d sdf [R,S], d radiance [R,S-1,3], d s per ray [R] (summed by the host).
 // alpha_i = max((c_i - c_{i+1}) / (c_i + 1e-10), 0) (clamp_min passes the gradient where >= 0);
 // T = exclusive cumprod of (1 - alpha + 1e-10) (cumprod_backward: suffix sums / input).
-__global__ void neus_composite_bwd_kernel(const float* __restrict__ sdf, const float* __restrict__ s_dev,
+__global__ __launch_bounds__(64) void neus_composite_bwd_kernel(const float* __restrict__ sdf, const float* __restrict__ s_dev,
                                           const float* __restrict__ rad, const float* __restrict__ dmid, int64_t R,
                                           int S, int white_bkgd, const float* __restrict__ g_rgb,
                                           const float* __restrict__ g_depth, const float* __restrict__ g_acc,
-                                          const float* __restrict__ g_w, float* __restrict__ work,
-                                          float* __restrict__ d_sdf, float* __restrict__ d_rad,
-                                          float* __restrict__ d_s) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R) return;
-  const int S1 = S - 1;
+                                          const float* __restrict__ g_w, float* __restrict__ d_sdf,
+                                          float* __restrict__ d_rad, float* __restrict__ d_s) {
+  extern __shared__ float lds[];
+  const int64_t r = blockIdx.x;
+  const int l = threadIdx.x, S1 = S - 1;
   const float s = *s_dev;
   const float* sd = sdf + r * S;
-  // work rows: c [S], alpha [S-1], T [S-1], w [S-1], wbar [S-1]
-  float* c = work + r * (5 * S);
-  float* al = c + S;
-  float* Tt = al + S;
-  float* w = Tt + S;
-  float* wb = w + S;
-  for (int i = 0; i < S; ++i) c[i] = sigmoidf_ref(fmul(sd[i], s));
-  double T = 1.0, a_acc = 0.0, wd = 0.0;
-  for (int i = 0; i < S1; ++i) {
-    const float a = fmaxf(fdiv(fsub(c[i], c[i + 1]), fadd(c[i], 1e-10f)), 0.0f);
-    al[i] = a;
-    Tt[i] = (float)T;
-    w[i] = fmul(a, (float)T);
-    T *= (double)fadd(fsub(1.0f, a), 1e-10f);
-    a_acc += (double)w[i];
+  double* ldb = (double*)lds;  // A, wd
+  float* c = lds + 4;          // [S] cdf
+  float* al = c + S;           // [S] alpha
+  float* Tt = al + S;          // [S] T
+  float* w = Tt + S;           // [S] weights
+  float* wb = w + S;           // [S] weight adjoints
+  float* ls = wb + S;          // [S] sdf
+  float* lm = ls + S;          // [S] mid depths
+  float* lo = lm + S;          // [S] d sdf
+  for (int i = l; i < S; i += 64) {
+    const float v = sd[i];
+    ls[i] = v;
+    c[i] = sigmoidf_ref(fmul(v, s));
+    if (i < S1) lm[i] = dmid[r * S1 + i];
   }
-  const float accf = (float)a_acc;
-  const double A = (double)fadd(accf, 1e-10f);
-  for (int i = 0; i < S1; ++i) wd += (double)w[i] * (double)dmid[r * S1 + i];
+  __syncthreads();
+  if (l == 0) {
+    double T = 1.0, a_acc = 0.0, wd = 0.0;
+    for (int i = 0; i < S1; ++i) {
+      const float a = fmaxf(fdiv(fsub(c[i], c[i + 1]), fadd(c[i], 1e-10f)), 0.0f);
+      al[i] = a;
+      Tt[i] = (float)T;
+      w[i] = fmul(a, (float)T);
+      T *= (double)fadd(fsub(1.0f, a), 1e-10f);
+      a_acc += (double)w[i];
+    }
+    const float accf = (float)a_acc;
+    ldb[0] = (double)fadd(accf, 1e-10f);
+    for (int i = 0; i < S1; ++i) wd += (double)w[i] * (double)lm[i];
+    ldb[1] = wd;
+  }
+  __syncthreads();
+  const double A = ldb[0], wd = ldb[1];
   const float gr0 = g_rgb ? g_rgb[r * 3 + 0] : 0.f, gr1 = g_rgb ? g_rgb[r * 3 + 1] : 0.f,
               gr2 = g_rgb ? g_rgb[r * 3 + 2] : 0.f;
   const double gd = g_depth ? (double)g_depth[r] : 0.0;
   // white_bkgd: rgb += 1 - acc -> acc receives -sum(g_rgb)
   const double ga = (g_acc ? (double)g_acc[r] : 0.0) - (white_bkgd ? (double)gr0 + gr1 + gr2 : 0.0);
-  for (int i = 0; i < S1; ++i) {
+  for (int i = l; i < S1; i += 64) {
     const int64_t q = r * S1 + i;
     double v = (double)gr0 * rad[q * 3 + 0] + (double)gr1 * rad[q * 3 + 1] + (double)gr2 * rad[q * 3 + 2] + ga;
-    v += gd * ((double)dmid[q] / A - wd / (A * A));
+    v += gd * ((double)lm[i] / A - wd / (A * A));
     if (g_w) v += (double)g_w[q];
     wb[i] = (float)v;
     d_rad[q * 3 + 0] = fmul(w[i], gr0);
     d_rad[q * 3 + 1] = fmul(w[i], gr1);
     d_rad[q * 3 + 2] = fmul(w[i], gr2);
   }
-  // alpha-bar: w = alpha * T -> alpha gets wbar * T; T_i = prod_{j<i} u_j (u_j = 1 - alpha_j + 1e-10)
-  // -> u_j gets (sum_{k > j} wbar_k alpha_k T_k) / u_j, alpha_j gets minus that
-  double suffix = 0.0;  // sum_{k > i} wbar_k * alpha_k * T_k
-  double sbar = 0.0;
-  for (int i = S - 1; i >= 0; --i) d_sdf[r * S + i] = 0.0f;
-  float cbar_next = 0.0f;  // contribution to c_{i+1} accumulated from alpha_i
-  // walk backwards: alpha_i depends on c_i, c_{i+1}
-  for (int i = S1 - 1; i >= 0; --i) {
-    const double u = (double)fadd(fsub(1.0f, al[i]), 1e-10f);
-    const double abar = (double)wb[i] * Tt[i] - suffix / u;
-    suffix += (double)wb[i] * al[i] * Tt[i];
-    const float num = fsub(c[i], c[i + 1]), den = fadd(c[i], 1e-10f);
-    const bool pass = fdiv(num, den) >= 0.0f;
-    double ci_bar = 0.0, cn_bar = 0.0;
-    if (pass) {
-      ci_bar = abar / den - abar * num / ((double)den * den);
-      cn_bar = -abar / den;
+  __syncthreads();
+  if (l == 0) {
+    // alpha-bar: w = alpha * T -> alpha gets wbar * T; T_i = prod_{j<i} u_j (u_j = 1 - alpha_j + 1e-10)
+    // -> u_j gets (sum_{k > j} wbar_k alpha_k T_k) / u_j, alpha_j gets minus that
+    double suffix = 0.0;  // sum_{k > i} wbar_k * alpha_k * T_k
+    double sbar = 0.0;
+    float cbar_next = 0.0f;  // contribution to c_{i+1} accumulated from alpha_i
+    // walk backwards: alpha_i depends on c_i, c_{i+1}
+    for (int i = S1 - 1; i >= 0; --i) {
+      const double u = (double)fadd(fsub(1.0f, al[i]), 1e-10f);
+      const double abar = (double)wb[i] * Tt[i] - suffix / u;
+      suffix += (double)wb[i] * al[i] * Tt[i];
+      const float num = fsub(c[i], c[i + 1]), den = fadd(c[i], 1e-10f);
+      const bool pass = fdiv(num, den) >= 0.0f;
+      double ci_bar = 0.0, cn_bar = 0.0;
+      if (pass) {
+        ci_bar = abar / den - abar * num / ((double)den * den);
+        cn_bar = -abar / den;
+      }
+      // c_{i+1} collects cn_bar here plus ci_bar from alpha_{i+1} (already in cbar_next)
+      const double cb_next = cn_bar + (double)cbar_next;
+      {
+        const float cc = c[i + 1];
+        const double sg = cb_next * cc * (1.0 - cc);
+        lo[i + 1] = (float)(sg * s);
+        sbar += sg * ls[i + 1];
+      }
+      cbar_next = (float)ci_bar;
     }
-    // c_{i+1} collects cn_bar here plus ci_bar from alpha_{i+1} (already in cbar_next)
-    const double cb_next = cn_bar + (double)cbar_next;
     {
-      const float cc = c[i + 1];
-      const double sg = cb_next * cc * (1.0 - cc);
-      d_sdf[r * S + i + 1] = (float)(sg * s);
-      sbar += sg * sd[i + 1];
+      const float cc = c[0];
+      const double sg = (double)cbar_next * cc * (1.0 - cc);
+      lo[0] = (float)(sg * s);
+      sbar += sg * ls[0];
     }
-    cbar_next = (float)ci_bar;
+    d_s[r] = (float)sbar;
   }
-  {
-    const float cc = c[0];
-    const double sg = (double)cbar_next * cc * (1.0 - cc);
-    d_sdf[r * S] = (float)(sg * s);
-    sbar += sg * sd[0];
-  }
-  d_s[r] = (float)sbar;
+  __syncthreads();
+  for (int i = l; i < S; i += 64) d_sdf[r * S + i] = lo[i];
 }
 
 // ---- VolSDF compositing with a graph (volsdf.py:449-506) ----------------------------------------------
@@ -1056,8 +1097,9 @@ int nr_neus_composite_fwd(const float* sdf, const float* s_dev, const float* rad
   NR_REQUIRE(sdf && s_dev && rad && dmid && rgb && depth && acc && weights && R >= 0 && S >= 2, NR_ERR_ARG,
              "nr_neus_composite_fwd: bad argument");
   if (R == 0) return NR_OK;
-  hipLaunchKernelGGL(neus_composite_fwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream, sdf,
-                     s_dev, rad, dmid, R, S, white_bkgd, rgb, depth, acc, weights, alpha, cdf);
+  NR_REQUIRE((size_t)7 * S * sizeof(float) <= 65536, NR_ERR_UNSUPPORTED, "nr_neus_composite_fwd: S too large");
+  hipLaunchKernelGGL(neus_composite_fwd_kernel, dim3((unsigned)R), dim3(64), 7 * S * sizeof(float), (hipStream_t)stream,
+                     sdf, s_dev, rad, dmid, R, S, white_bkgd, rgb, depth, acc, weights, alpha, cdf);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
@@ -1073,9 +1115,10 @@ int nr_neus_composite_bwd(const float* sdf, const float* s_dev, const float* rad
   if (R == 0) return NR_OK;
   NR_REQUIRE(workspace && workspace_bytes >= nr_neus_composite_bwd_workspace_bytes(R, S), NR_ERR_WORKSPACE,
              "nr_neus_composite_bwd: workspace too small");
-  hipLaunchKernelGGL(neus_composite_bwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream, sdf,
-                     s_dev, rad, dmid, R, S, white_bkgd, g_rgb, g_depth, g_acc, g_weights, (float*)workspace, d_sdf,
-                     d_rad, d_s);
+  NR_REQUIRE((size_t)(8 * S + 4) * sizeof(float) <= 65536, NR_ERR_UNSUPPORTED, "nr_neus_composite_bwd: S too large");
+  hipLaunchKernelGGL(neus_composite_bwd_kernel, dim3((unsigned)R), dim3(64), (8 * S + 4) * sizeof(float),
+                     (hipStream_t)stream, sdf, s_dev, rad, dmid, R, S, white_bkgd, g_rgb, g_depth, g_acc, g_weights,
+                     d_sdf, d_rad, d_s);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
