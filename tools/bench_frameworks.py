@@ -62,7 +62,11 @@ def main():
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--precision', default='f16x3')
     ap.add_argument('--configs', action='store_true', help='also time BASELINE configs (c), (d), (e)')
+    ap.add_argument('--only', default='', help="with --configs: just these of 'c', 'd', 'e' (no framework leg)")
     args = ap.parse_args()
+    if args.only:
+        print(json.dumps(configs(args), default=str), flush=True)
+        return
     import weightgen as wg
     from helpers import unisurf_model, volsdf_model
     dev = torch.device('cuda')
@@ -99,6 +103,21 @@ def configs(args):
     from neurecon_amd.frameworks import neus, unisurf, volsdf
     dev = torch.device('cuda')
     res = {}
+    want = set(args.only) if getattr(args, 'only', '') else {'c', 'd', 'e'}
+    if 'c' in want:
+        res.update(config_c(args, dev))
+    if 'd' in want:
+        res.update(config_d(args, dev))
+    if 'e' in want:
+        res.update(config_e(args, dev))
+    return res
+
+
+def config_c(args, dev):
+    import weightgen as wg
+    from helpers import volsdf_model
+    from neurecon_amd.frameworks import volsdf
+    res = {}
     ro, rd = rays(dev, 'c')
     mv = volsdf_model(wg.volsdf_state(seed=5, beta_init=1e-3), 1e-3, precision=args.precision)
     kw = dict(near=0.0, far=6.0, batched=True, calc_normal=True, detailed_output=False, N_samples=128,
@@ -106,7 +125,15 @@ def configs(args):
     with torch.no_grad():
         dt, ks = timeit(lambda: volsdf.volume_render(ro, rd, mv, **kw), args.steps, args.warmup)
     res['c_volsdf_2048x256'] = {'rays': ro.shape[1], 'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3,
-                                'roofline': mlp_roofline(ks, args.precision, 265)}
+                                'roofline': mlp_roofline(ks, args.precision, 265), 'kernels': ks}
+    return res
+
+
+def config_d(args, dev):
+    import weightgen as wg
+    from helpers import neus_model
+    from neurecon_amd.frameworks import neus
+    res = {}
     ro, rd = rays(dev, 'd')
     mn = neus_model(wg.neus_state(seed=4, use_outside_nerf=True), use_outside_nerf=True, precision=args.precision)
     kw = dict(obj_bounding_radius=1.0, batched=True, calc_normal=True, detailed_output=False, N_samples=64,
@@ -115,6 +142,14 @@ def configs(args):
         dt, ks = timeit(lambda: neus.volume_render(ro, rd, mn, **kw), max(1, args.steps // 2), 1)
     res['d_neus_nerfpp_800x600'] = {'rays': ro.shape[1], 'rays_per_s': ro.shape[1] / dt, 'ms': dt * 1e3,
                                     'roofline': mlp_roofline(ks, args.precision, 289)}
+    return res
+
+
+def config_e(args, dev):
+    import weightgen as wg
+    from helpers import unisurf_model
+    from neurecon_amd.frameworks import unisurf
+    res = {}
     ro, rd = rays(dev, 'e')
     mu = unisurf_model(wg.unisurf_state(seed=3), precision=args.precision)
     with torch.no_grad():
