@@ -282,7 +282,7 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
       ProfScope prof("neus_upsample", (double)R, st);
       // perturb: round it's [n_rays][n_up] block of the caller's uniforms
       const float* u = a.u_rand ? a.u_rand + ((int64_t)it * a.n_rays + ray0) * n_up : a.u_fine;
-      hipLaunchKernelGGL(neus_upsample, dim3((unsigned)R), dim3(64), (4 * c.S + 1) * sizeof(float), st, cu, it, u,
+      hipLaunchKernelGGL(neus_upsample, dim3((unsigned)R), dim3(64), (5 * c.S + 1) * sizeof(float), st, cu, it, u,
                          (int64_t)(a.u_rand ? n_up : 0));
     }
     NR_HIP_CHECK(hipGetLastError());

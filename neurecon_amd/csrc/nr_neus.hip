@@ -120,8 +120,9 @@ __global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const f
   float* sz = lds;           // depths [L]
   float* ss = sz + c.S;      // sdf [L]
   float* sa = ss + c.S;      // alpha, then weights [L-1]
-  float* scdf = sa + c.S;    // cdf [L]
-  float* stot = scdf + c.S;  // [1] weight total
+  float* scdf = sa + c.S;    // (1 - alpha + 1e-10) factors [L-1], then the cdf [L]
+  float* sq = scdf + c.S;    // normalised weights [L-1]
+  float* stot = sq + c.S;    // [1] weight total
   for (int i = l; i < L; i += 64) {
     sz[i] = c.dv[i * R + r];
     ss[i] = c.sv[i * R + r];
@@ -139,25 +140,32 @@ __global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const f
     const float md = fmul(fmul(m, dist), 0.5f);
     const float c0 = sigmoidf_ref(fmul(fsub(mid, md), S));
     const float c1 = sigmoidf_ref(fmul(fadd(mid, md), S));
-    sa[i] = fdiv(fadd(fsub(c0, c1), 1e-5f), fadd(c0, 1e-5f));
+    const float alpha = fdiv(fadd(fsub(c0, c1), 1e-5f), fadd(c0, 1e-5f));
+    sa[i] = alpha;
+    scdf[i] = fadd(fsub(1.0f, alpha), 1e-10f);  // the transmittance factor, off the serial chain
   }
   __syncthreads();
   if (l == 0) {
     double T = 1.0;
     for (int i = 0; i < L - 1; ++i) {
-      const float alpha = sa[i];
-      sa[i] = fmul(alpha, (float)T);
-      T *= (double)fadd(fsub(1.0f, alpha), 1e-10f);
+      sa[i] = fmul(sa[i], (float)T);
+      T *= (double)scdf[i];
     }
-    const float total = aten_row_sum(L - 1, [&](int i) { return fadd(sa[i], 1e-5f); });
-    // sample_pdf's cdf (rend_util.py:259-264): fp64 running sum of the normalised weights
+    stot[0] = aten_row_sum(L - 1, [&](int i) { return fadd(sa[i], 1e-5f); });
+  }
+  __syncthreads();
+  {  // sample_pdf's normalised weights (rend_util.py:259-264) across the lanes
+    const float total = stot[0];
+    for (int i = l; i < L - 1; i += 64) sq[i] = fdiv(fadd(sa[i], 1e-5f), total);
+  }
+  __syncthreads();
+  if (l == 0) {  // ... and their fp64 running sum
     double acc = 0.0;
     scdf[0] = 0.0f;
     for (int i = 0; i < L - 1; ++i) {
-      acc += (double)fdiv(fadd(sa[i], 1e-5f), total);
+      acc += (double)sq[i];
       scdf[i + 1] = (float)acc;
     }
-    stot[0] = total;
   }
   __syncthreads();
   const float ox = c.ro[r * 3], oy = c.ro[r * 3 + 1], oz = c.ro[r * 3 + 2];
@@ -317,8 +325,10 @@ __global__ __launch_bounds__(64) void neus_composite(NeusChunk c, NeusOut o, con
     }
   }
   __syncthreads();
+  double rgb0 = 0.0, rgb1 = 0.0, rgb2 = 0.0, n0 = 0.0, n1 = 0.0, n2 = 0.0;
+  float accf = 0.0f;
   if (l == 0 && live) {
-    double T = 1.0, acc = 0.0, rgb0 = 0.0, rgb1 = 0.0, rgb2 = 0.0, n0 = 0.0, n1 = 0.0, n2 = 0.0;
+    double T = 1.0, acc = 0.0;
     for (int i = 0; i < S - 1; ++i) {
       const float alpha = sal[i];
       const float w = fmul(alpha, (float)T);
@@ -334,10 +344,21 @@ __global__ __launch_bounds__(64) void neus_composite(NeusChunk c, NeusOut o, con
       }
       sal[i] = w;
     }
-    const float accf = (float)acc;
-    const float denom = fadd(accf, 1e-10f);
+    accf = (float)acc;
+    scdf[0] = fadd(accf, 1e-10f);  // the depth normaliser for the ray's lanes (the cdf is no longer read)
+  }
+  __syncthreads();
+  // depth terms w_i / (acc + 1e-10) * d_mid_i across the ray's lanes, into scdf[1 ..] (the CDFs
+  // are no longer read; scdf[0] holds the normaliser)
+  {
+    const float denom = scdf[0];
+    __syncthreads();  // every lane has its normaliser before scdf[1 ..] is overwritten
+    for (int i = l; i < Sl - 1; i += NL) scdf[i + 1] = fmul(fdiv(sal[i], denom), sdm[i]);
+  }
+  __syncthreads();
+  if (l == 0 && live) {
     double depth = 0.0;
-    for (int i = 0; i < S - 1; ++i) depth += (double)fmul(fdiv(sal[i], denom), sdm[i]);
+    for (int i = 0; i < S - 1; ++i) depth += (double)scdf[i + 1];
     float r0 = (float)rgb0, r1 = (float)rgb1, r2 = (float)rgb2;
     if (white_bkgd) {
       const float bg = fsub(1.0f, accf);
