@@ -282,8 +282,13 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
       ProfScope prof("neus_upsample", (double)R, st);
       // perturb: round it's [n_rays][n_up] block of the caller's uniforms
       const float* u = a.u_rand ? a.u_rand + ((int64_t)it * a.n_rays + ray0) * n_up : a.u_fine;
-      hipLaunchKernelGGL(neus_upsample, dim3((unsigned)R), dim3(64), (5 * c.S + 1) * sizeof(float), st, cu, it, u,
-                         (int64_t)(a.u_rand ? n_up : 0));
+      const size_t lds1 = (5 * (size_t)c.S + 1) * sizeof(float);  // four rays per wave when their staging fits
+      if (4 * lds1 <= 65536)
+        hipLaunchKernelGGL((neus_upsample<4>), dim3((unsigned)((R + 3) / 4)), dim3(64), 4 * lds1, st, cu, it, u,
+                           (int64_t)(a.u_rand ? n_up : 0));
+      else
+        hipLaunchKernelGGL((neus_upsample<1>), dim3((unsigned)R), dim3(64), lds1, st, cu, it, u,
+                           (int64_t)(a.u_rand ? n_up : 0));
     }
     NR_HIP_CHECK(hipGetLastError());
     if ((rc = sample_sdf(cu.pts, (int64_t)n_up * R, c.snew, slot0))) return rc;

@@ -71,6 +71,7 @@ __global__ void neus_gather_nablas(NeusChunk c);
 
 __global__ void neus_prologue(NeusChunk c, const float* rays_o, const float* rays_d, const float* t_coarse,
                               float r_obj, float near_bypass, float far_bypass);
+template <int RPW>
 __global__ void neus_upsample(NeusChunk c, int it, const float* u, int64_t u_stride);
 __global__ void neus_merge(NeusChunk c, int L, float* dv2, float* sv2, int* idv2);
 __global__ void neus_expand(NeusChunk c, int gather);

@@ -107,29 +107,33 @@ __device__ void sample_pdf_ray_rand(const float* __restrict__ bins, float* __res
   }
 }
 
-// one "official_solution" upsampling round (neus.py:252-276): one wave per ray.  The per-interval
+// one "official_solution" upsampling round (neus.py:252-276): RPW rays per wave (64 / RPW lanes each).  The per-interval
 // work (slopes, logistic CDFs, alpha) runs across the lanes; the three order-sensitive scans
 // (transmittance cumprod, the ATen-order weight sum, the CDF cumsum) run on lane 0 over LDS with
 // exactly the arithmetic of the per-ray version; the n_up inverse-CDF draws run across lanes.
 // u: the round's uniforms, u[r * u_stride + k] (u_stride 0: the shared deterministic linspace)
+template <int RPW>
 __global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const float* __restrict__ u, int64_t u_stride) {
   extern __shared__ float lds[];
-  const int r = blockIdx.x, l = threadIdx.x;
+  constexpr int NL = 64 / RPW;  // lanes per ray
+  const int r = blockIdx.x * RPW + (int)threadIdx.x / NL, l = (int)threadIdx.x % NL;
   const int L = c.N_samples + it * c.n_up;  // last round's samples were merged by neus_merge
   const int64_t R = c.R;
-  float* sz = lds;           // depths [L]
+  const bool live = r < R;
+  const int Ll = live ? L : 0;  // a ray past the chunk's end only joins the barriers
+  float* sz = lds + ((int)threadIdx.x / NL) * (5 * c.S + 1);  // depths [L]
   float* ss = sz + c.S;      // sdf [L]
   float* sa = ss + c.S;      // alpha, then weights [L-1]
   float* scdf = sa + c.S;    // (1 - alpha + 1e-10) factors [L-1], then the cdf [L]
   float* sq = scdf + c.S;    // normalised weights [L-1]
   float* stot = sq + c.S;    // [1] weight total
-  for (int i = l; i < L; i += 64) {
+  for (int i = l; i < Ll; i += NL) {
     sz[i] = c.dv[i * R + r];
     ss[i] = c.sv[i * R + r];
   }
   __syncthreads();
   const float S = (float)(64 << it);  // 64 * 2**i
-  for (int i = l; i < L - 1; i += 64) {
+  for (int i = l; i < Ll - 1; i += NL) {
     const float s0 = ss[i], s1 = ss[i + 1], z0 = sz[i], z1 = sz[i + 1];
     const float mid = fmul(fadd(s0, s1), 0.5f);
     const float slope = fdiv(fsub(s1, s0), fadd(fsub(z1, z0), 1e-5f));
@@ -145,7 +149,7 @@ __global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const f
     scdf[i] = fadd(fsub(1.0f, alpha), 1e-10f);  // the transmittance factor, off the serial chain
   }
   __syncthreads();
-  if (l == 0) {
+  if (l == 0 && live) {
     double T = 1.0;
     for (int i = 0; i < L - 1; ++i) {
       sa[i] = fmul(sa[i], (float)T);
@@ -156,10 +160,10 @@ __global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const f
   __syncthreads();
   {  // sample_pdf's normalised weights (rend_util.py:259-264) across the lanes
     const float total = stot[0];
-    for (int i = l; i < L - 1; i += 64) sq[i] = fdiv(fadd(sa[i], 1e-5f), total);
+    for (int i = l; i < Ll - 1; i += NL) sq[i] = fdiv(fadd(sa[i], 1e-5f), total);
   }
   __syncthreads();
-  if (l == 0) {  // ... and their fp64 running sum
+  if (l == 0 && live) {  // ... and their fp64 running sum
     double acc = 0.0;
     scdf[0] = 0.0f;
     for (int i = 0; i < L - 1; ++i) {
@@ -168,9 +172,10 @@ __global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const f
     }
   }
   __syncthreads();
+  if (!live) return;
   const float ox = c.ro[r * 3], oy = c.ro[r * 3 + 1], oz = c.ro[r * 3 + 2];
   const float dx = c.rd[r * 3], dy = c.rd[r * 3 + 1], dz = c.rd[r * 3 + 2];
-  for (int k = l; k < c.n_up; k += 64) {
+  for (int k = l; k < c.n_up; k += NL) {
     const float uk = u[r * u_stride + k];
     float d;
     if (uk <= 0.0f) {  // searchsorted -> 0: below = above = 0
@@ -191,6 +196,9 @@ __global__ __launch_bounds__(64) void neus_upsample(NeusChunk c, int it, const f
     c.pts[q * 3 + 2] = fadd(oz, fmul(dz, d));
   }
 }
+
+template __global__ void neus_upsample<1>(NeusChunk, int, const float*, int64_t);
+template __global__ void neus_upsample<4>(NeusChunk, int, const float*, int64_t);
 
 // merge (neus.py:276: cat + sort + gather) of the sorted list (dv, sv, idv)[0..L) with the n_up new
 // samples (dnew, snew) into (dv2, sv2, idv2)[0..L+n_up), one thread per (output element, ray):
