@@ -738,10 +738,12 @@ int nr_sdf_pack(const NrSdfDesc* d, const float* const* W, const float* const* b
       ops[SB4 + (4 - l)] = mkop(W[l], nullptr, 256, 256, 1, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f,
                                 prec, wmax + SB4 + (4 - l));
     ops[SB0] = mkop(W[0], nullptr, 256, 3, 1, seg(4, 0, 3), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + SB0);
+    char* dst[kSirenOps];
     for (int i = 0; i < kSirenOps; ++i) {
       ops[i].bound = bound + 2 * i;
-      if ((rc = launch_pack_op(ops[i], P + L.op_off[i], st))) return rc;
+      dst[i] = P + L.op_off[i];
     }
+    if ((rc = launch_pack_ops(ops, dst, kSirenOps, st))) return rc;
     if ((rc = launch_pack_vec(W[5], 0, 256, 256, P + L.w8row0_off, st))) return rc;
     return launch_pack_vec(b[5], 0, 1, 4, P + L.misc_off, st);
   }
@@ -773,8 +775,9 @@ int nr_sdf_pack(const NrSdfDesc* d, const float* const* W, const float* const* b
   float* bound = (float*)(P + L.bound_off);
   for (int i = 0; i < kSdfOps; ++i) ops[i].bound = bound + 2 * i;
   ops[F7].aux = W[8];  // sdf row W8[0, :] rides with F7's chunks (v2 pipeline's running dot product)
-  for (int i = 0; i < kSdfOps; ++i)
-    if ((rc = launch_pack_op(ops[i], P + L.op_off[i], st))) return rc;
+  char* dst[kSdfOps];
+  for (int i = 0; i < kSdfOps; ++i) dst[i] = P + L.op_off[i];
+  if ((rc = launch_pack_ops(ops, dst, kSdfOps, st))) return rc;
   if ((rc = launch_pack_vec(W[8], 0, 256, 256, P + L.w8row0_off, st))) return rc;
   if ((rc = launch_pack_vec(b[8], 0, 1, 4, P + L.misc_off, st))) return rc;
   return NR_OK;
@@ -829,10 +832,12 @@ int nr_nerf_pack(const NrNerfDesc* d, const float* const* W, const float* const*
   ops[NV] = mkop(W[9], b[9], 128, 256 + inv, 0, seg(8, 0, 128), none(), seg(16, 0, 256), seg(2, 256, inv), 1.0f, prec,
                  wmax + NV);
   float* bound = (float*)(P + L.bound_off);
+  char* dst[kNerfOps];
   for (int i = 0; i < kNerfOps; ++i) {
     ops[i].bound = bound + 2 * i;
-    if ((rc = launch_pack_op(ops[i], P + L.op_off[i], st))) return rc;
+    dst[i] = P + L.op_off[i];
   }
+  if ((rc = launch_pack_ops(ops, dst, kNerfOps, st))) return rc;
   if ((rc = launch_pack_vec(W[10], 0, 256, 256, P + L.alpha_off, st))) return rc;
   if ((rc = launch_pack_vec(b[10], 0, 1, 1, P + L.alpha_off + 256 * 4, st))) return rc;
   if ((rc = launch_pack_vec(W[11], 0, 384, 384, P + L.rgb_off, st))) return rc;
@@ -870,10 +875,12 @@ int nr_radiance_pack(const NrRadDesc* d, const float* const* W, const float* con
   for (int i = 1; i < L.D; ++i)
     ops[i] = mkop(W[i], b[i], 256, 256, 0, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + i);
   float* bound = (float*)(P + L.bound_off);
+  char* dst[5];
   for (int i = 0; i < L.D; ++i) {
     ops[i].bound = bound + 2 * i;
-    if ((rc = launch_pack_op(ops[i], P + L.op_off[i], st))) return rc;
+    dst[i] = P + L.op_off[i];
   }
+  if ((rc = launch_pack_ops(ops, dst, L.D, st))) return rc;
   if ((rc = launch_pack_vec(W[L.D], 0, 768, 768, P + L.head_off, st))) return rc;
   if ((rc = launch_pack_vec(b[L.D], 0, 3, 4, P + L.head_off + 768 * 4, st))) return rc;
   return NR_OK;
@@ -1003,8 +1010,9 @@ int nr_radiance_train_pack(const NrRadDesc* d, const float* const* W, const floa
                   NR_PREC_F16X3, wmax + i);
   ops[4] = mkop(W[0], nullptr, 256, ld0, 1, seg(16, ns, 256), seg(L.kbs, 0, ns), seg(16, 0, 256), none(), 1.0f,
                 NR_PREC_F16X3, wmax + 4);
-  for (int i = 0; i < 5; ++i)
-    if ((rc = launch_pack_op(ops[i], P + off[i], st))) return rc;
+  char* dst[5];
+  for (int i = 0; i < 5; ++i) dst[i] = P + off[i];
+  if ((rc = launch_pack_ops(ops, dst, 5, st))) return rc;
   return NR_OK;
 }
 

@@ -1158,12 +1158,12 @@ struct Z4 {
 //  pre(c): issued right after chunk c's weight DMA (slab staging for a later chunk's epilogue);
 //          returns the DMA instructions it issued
 //  TS:     the epilogue wants t = 100 log2(e) z instead of z (forward softplus ops: the bias slot's
-//          floats 96..127 hold bias * 100 log2(e), packed by pack_op_kernel)
+//          floats 96..127 hold bias * 100 log2(e), packed by pack_ops_kernel)
 // kT ~ 100 log2(e) and kC ~ ln2 / 100 as a float pair whose product is 1 within 2e-10: on softplus'
 // linear branch the value path is t * kC = z * kT * kC, so the correctly rounded constants
 // (product 1 - 4.7e-8) would shrink every positive activation by that factor per layer, a bias that
 // compounds over the network's 8 layers.  kT sits 4.5e-7 relative below 100 log2(e) (softplus' beta
-// moves by that much: <= 3e-9 absolute on its output).  pack_op_kernel packs bias * kT.
+// moves by that much: <= 3e-9 absolute on its output).  pack_ops_kernel packs bias * kT.
 constexpr float kT = 144.26944f;
 constexpr float kC = 0.0069314749f;
 
@@ -2964,10 +2964,8 @@ __device__ __forceinline__ float wscale(const PackOp& op) {
   return __builtin_ldexpf(1.0f, 13 - __builtin_amdgcn_frexp_expf(m));
 }
 
-// one thread per 32-bit word of the packed op
-__global__ void pack_op_kernel(PackOp op, uint32_t* __restrict__ dst, int64_t n) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
+// word e of a packed op
+__device__ __forceinline__ void pack_word(const PackOp& op, uint32_t* __restrict__ dst, int64_t e) {
   const int KB = op.in[0].nblk + op.in[1].nblk;
   const int per_chunk = (2 * KB + 1) * 256;  // words
   const int c = (int)(e / per_chunk);
@@ -3036,43 +3034,84 @@ __global__ void pack_op_kernel(PackOp op, uint32_t* __restrict__ dst, int64_t n)
   }
 }
 
-// max |W * scale| into *out (out zeroed beforehand; non-negative floats order like their bits)
-__global__ void maxabs_kernel(const float* __restrict__ W, int64_t n, float scale, unsigned* __restrict__ out) {
-  float m = 0.0f;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    m = fmaxf(m, fabsf(W[i] * scale));
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+// Packing runs every optimizer step in training (the no-grad sampler's render pack and the training
+// pack follow the weights), for up to 17 ops per network: the ops of one pack call go in batches of
+// kPackBatch through two launches -- pack_prep_kernel (one workgroup per op: max |W * scale| for the
+// f16x3 weight scale, and the op's bound) and pack_ops_kernel (one thread per packed word, blockIdx.y =
+// op) -- instead of two memsets and three launches per op.
+constexpr int kPackBatch = 8;
+struct PackBatch {
+  PackOp op[kPackBatch];
+  uint32_t* dst[kPackBatch];
+  int64_t n[kPackBatch];  // packed words of op i
+};
+
+// one thread per 32-bit word of the packed op
+__global__ void pack_ops_kernel(PackBatch pb) {
+  const int o = blockIdx.y;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= pb.n[o]) return;
+  pack_word(pb.op[o], pb.dst[o], e);
 }
 
-// bound[0] = max over packed output rows of sum_k |W * scale| (row L1 norm of the op's effective
-// matrix), bound[1] = max |bias|; one thread per output row (bound zeroed beforehand)
-// one wave per packed output row (the row's KB x 16 inputs strided over the lanes, then a wave sum):
-// the packing runs every optimizer step in training, where a thread per row took ~85 us per op
-__global__ void bound_kernel(PackOp op, unsigned* __restrict__ bound) {
-  const int KB = op.in[0].nblk + op.in[1].nblk;
-  const int NBO = op.out[0].nblk + op.out[1].nblk;
-  const int r = blockIdx.x;
-  if (r >= NBO * 16) return;
-  const int ob = r >> 4, i = r & 15;
-  float s = 0.0f;
-  for (int e = threadIdx.x; e < KB * 16; e += 64) s += fabsf(pack_src(op, ob, i, e >> 4, e & 15));
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if (threadIdx.x != 0) return;
-  float bb = 0.0f;
-  if (op.bias) {
-    int ob_loc = ob;
-    for (int q = 0; q < 2; ++q) {
-      if (ob_loc < op.out[q].nblk) {
-        const int rl = 16 * ob_loc + i;
-        if (rl < op.out[q].nvalid) bb = fabsf(op_bias(op, q, op.out[q].off + rl));
-        break;
+// One workgroup (16 waves) per op:
+//   *wmax    = max |W * scale| (and of W2) -- f16x3 ops
+//   bound[0] = max over packed output rows of sum_k |W * scale| (row L1 norm of the op's effective
+//              matrix, x 1.0001: margin for the summation's rounding), bound[1] = max |bias|
+// A row's KB x 16 inputs are strided over the lanes of one wave, then wave-summed; the maxima are
+// order-independent, so every op packs bit for bit as one launch per op did.
+__global__ __launch_bounds__(1024) void pack_prep_kernel(PackBatch pb) {
+  const PackOp& op = pb.op[blockIdx.x];
+  __shared__ float red[3][16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float m = 0.0f, best = 0.0f, bb = 0.0f;
+  if (op.prec == NR_PREC_F16X3) {
+    for (int64_t i = threadIdx.x; i < op.wn; i += 1024) m = fmaxf(m, fabsf(op.W[i] * op.scale));
+    if (op.W2)
+      for (int64_t i = threadIdx.x; i < op.wn2; i += 1024) m = fmaxf(m, fabsf(op.W2[i] * op.scale));
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  }
+  if (op.bound) {
+    const int KB = op.in[0].nblk + op.in[1].nblk;
+    const int NBO = op.out[0].nblk + op.out[1].nblk;
+    for (int r = wave; r < NBO * 16; r += 16) {
+      const int ob = r >> 4, i = r & 15;
+      float sr = 0.0f;
+      for (int e = lane; e < KB * 16; e += 64) sr += fabsf(pack_src(op, ob, i, e >> 4, e & 15));
+      for (int o = 32; o > 0; o >>= 1) sr += __shfl_xor(sr, o);
+      best = fmaxf(best, sr * 1.0001f);
+      if (op.bias) {
+        int ob_loc = ob;
+        for (int q = 0; q < 2; ++q) {
+          if (ob_loc < op.out[q].nblk) {
+            const int rl = 16 * ob_loc + i;
+            if (rl < op.out[q].nvalid) bb = fmaxf(bb, fabsf(op_bias(op, q, op.out[q].off + rl)));
+            break;
+          }
+          ob_loc -= op.out[q].nblk;
+        }
       }
-      ob_loc -= op.out[q].nblk;
     }
   }
-  atomicMax(bound, __float_as_uint(s * 1.0001f));  // margin for the summation's rounding
-  atomicMax(bound + 1, __float_as_uint(bb));
+  if (lane == 0) {
+    red[0][wave] = m;
+    red[1][wave] = best;
+    red[2][wave] = bb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.0f, b = 0.0f, c = 0.0f;
+    for (int w = 0; w < 16; ++w) {
+      a = fmaxf(a, red[0][w]);
+      b = fmaxf(b, red[1][w]);
+      c = fmaxf(c, red[2][w]);
+    }
+    if (op.prec == NR_PREC_F16X3) *op.wmax = a;
+    if (op.bound) {
+      op.bound[0] = b;
+      op.bound[1] = c;
+    }
+  }
 }
 
 __global__ void pack_vec_kernel(const float* __restrict__ src, int off, int nvalid, int n, float* __restrict__ dst) {
@@ -3084,29 +3123,30 @@ __global__ void pack_vec_kernel(const float* __restrict__ src, int off, int nval
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
-int launch_pack_op(const PackOp& op, char* dst, hipStream_t stream) {
-  const int KB = op.in[0].nblk + op.in[1].nblk;
-  const int NBO = op.out[0].nblk + op.out[1].nblk;
-  if (op.prec == NR_PREC_F16X3) {
-    NR_REQUIRE(op.wmax, NR_ERR_ARG, "pack: f16x3 needs a max-|W| word");
-    NR_HIP_CHECK(hipMemsetAsync(op.wmax, 0, sizeof(float), stream));
-    hipLaunchKernelGGL(maxabs_kernel, dim3(64), dim3(256), 0, stream, op.W, op.wn, op.scale, (unsigned*)op.wmax);
-    NR_HIP_CHECK(hipGetLastError());
-    if (op.W2) {
-      hipLaunchKernelGGL(maxabs_kernel, dim3(64), dim3(256), 0, stream, op.W2, op.wn2, op.scale, (unsigned*)op.wmax);
-      NR_HIP_CHECK(hipGetLastError());
+int launch_pack_ops(const PackOp* ops, char* const* dst, int nops, hipStream_t stream) {
+  for (int b0 = 0; b0 < nops; b0 += kPackBatch) {
+    const int nb = std::min(kPackBatch, nops - b0);
+    PackBatch pb{};
+    int64_t nmax = 0;
+    for (int i = 0; i < nb; ++i) {
+      const PackOp& op = ops[b0 + i];
+      NR_REQUIRE(op.prec != NR_PREC_F16X3 || op.wmax, NR_ERR_ARG, "pack: f16x3 needs a max-|W| word");
+      const int KB = op.in[0].nblk + op.in[1].nblk;
+      const int NBO = op.out[0].nblk + op.out[1].nblk;
+      pb.op[i] = op;
+      pb.dst[i] = (uint32_t*)dst[b0 + i];
+      pb.n[i] = (int64_t)(NBO / 2) * (2 * KB + 1) * 256;
+      nmax = std::max(nmax, pb.n[i]);
     }
-  }
-  if (op.bound) {
-    NR_HIP_CHECK(hipMemsetAsync(op.bound, 0, 2 * sizeof(float), stream));
-    hipLaunchKernelGGL(bound_kernel, dim3(NBO * 16), dim3(64), 0, stream, op, (unsigned*)op.bound);
+    hipLaunchKernelGGL(pack_prep_kernel, dim3(nb), dim3(1024), 0, stream, pb);
+    NR_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(pack_ops_kernel, dim3((unsigned)((nmax + 255) / 256), nb), dim3(256), 0, stream, pb);
     NR_HIP_CHECK(hipGetLastError());
   }
-  const int64_t n = (int64_t)(NBO / 2) * (2 * KB + 1) * 256;
-  hipLaunchKernelGGL(pack_op_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, op, (uint32_t*)dst, n);
-  NR_HIP_CHECK(hipGetLastError());
   return NR_OK;
 }
+
+int launch_pack_op(const PackOp& op, char* dst, hipStream_t stream) { return launch_pack_ops(&op, &dst, 1, stream); }
 
 int launch_pack_vec(const float* src, int off, int nvalid, int n, char* dst, hipStream_t stream) {
   hipLaunchKernelGGL(pack_vec_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, src, off, nvalid, n, (float*)dst);

@@ -78,7 +78,7 @@ def _neus_uniforms(B, N, batched, rayschunk, direct, n_iters, n_up, N_importance
         elif n_iters > 0:
             ups.append(torch.stack([rend_util.uniform([*pre, nc, n_up], dev) for _ in range(n_iters)], 0))
         if N_outside > 0:
-            outs.append(rend_util.uniform([*pre, nc, N_outside]).float().to(dev))
+            outs.append(rend_util.to_device(rend_util.uniform([*pre, nc, N_outside]).float(), dev))
     u = None
     if ups:
         u = torch.cat(ups, rd)
@@ -306,8 +306,9 @@ def _train_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     L.check(L.lib().nr_neus_points(L.ptr(ro), L.ptr(rd), L.ptr(d_all), n, S, L.ptr(pts), L.ptr(mids), L.ptr(dmid),
                                    L.stream_of(dev)))
     surf = model.implicit_surface
-    sdf, nablas, _ = T.sdf_nablas(surf, pts.reshape(-1, 3), False)            # neus.py:294
-    _, nab_m, feat_m = T.sdf_nablas(surf, mids.reshape(-1, 3), True)           # neus.py:103-106, :298
+    Ws = T.effective_weights(surf)  # one weight_norm per layer, shared by both evaluations
+    sdf, nablas, _ = T.sdf_nablas(surf, pts.reshape(-1, 3), False, Ws)        # neus.py:294
+    _, nab_m, feat_m = T.sdf_nablas(surf, mids.reshape(-1, 3), True, Ws)       # neus.py:103-106, :298
     view = rd[:, None, :].expand(n, S - 1, 3).reshape(-1, 3).contiguous()
     rad = T.radiance(model.radiance_net, mids.reshape(-1, 3), view, nab_m, feat_m)
     s = model.forward_s().float().reshape(-1)[:1]

@@ -104,9 +104,9 @@ def _volsdf_uniforms(B, N, batched, rayschunk, N_importance, N_outside, dev):
         uf.append(rend_util.uniform([(B if batched else 1) * nc, N_importance], dev).reshape(*pre, nc, N_importance))
         if N_outside > 0:
             uo.append(rend_util.uniform([*pre, nc, N_outside], dev))
-    u_rand = torch.cat(uf, len(pre)).reshape(-1, N_importance).float().to(dev)
+    u_rand = rend_util.to_device(torch.cat(uf, len(pre)).reshape(-1, N_importance).float(), dev)
     u_rand = torch.sort(u_rand, dim=-1).values.contiguous()
-    u_out = torch.cat(uo, len(pre)).reshape(-1, N_outside).float().to(dev).contiguous() if uo else None
+    u_out = rend_util.to_device(torch.cat(uo, len(pre)).reshape(-1, N_outside).float(), dev).contiguous() if uo else None
     return u_rand, u_out
 
 

@@ -23,8 +23,8 @@ def get_rays(c2w, intrinsics, H, W, N_rays=-1, device_rng=False):
     if N_rays > 0:
         N_rays = min(N_rays, H * W)
         gen_dev = dev if device_rng else None
-        hs = torch.randint(0, H, size=[N_rays], device=gen_dev).to(dev)
-        ws = torch.randint(0, W, size=[N_rays], device=gen_dev).to(dev)
+        hs = to_device(torch.randint(0, H, size=[N_rays], device=gen_dev), dev)
+        ws = to_device(torch.randint(0, W, size=[N_rays], device=gen_dev), dev)
         select_inds = (hs * W + ws).expand([*prefix, N_rays])
         sel = select_inds.reshape(B, N_rays).contiguous()
         N = N_rays
@@ -51,6 +51,15 @@ def gather_rays(src, select_inds):
     out = torch.empty(B, N, *s.shape[2:], dtype=s.dtype, device=s.device)
     L.check(L.lib().nr_gather_rows(L.ptr(s), B, HW, row_bytes, L.ptr(idx), N, L.ptr(out), L.stream_of(s.device)))
     return out
+
+
+def to_device(t, dev):
+    """t.to(dev) without a host wait: a CPU draw goes up through pinned memory on the current stream
+    (a pageable .to() synchronises the host with the whole queue -- once per training step it left the
+    GPU idle while the host caught up)"""
+    if t.device == torch.device(dev) or t.device.type != 'cpu' or torch.device(dev).type != 'cuda':
+        return t.to(dev)
+    return t.pin_memory().to(dev, non_blocking=True)
 
 
 def uniform(shape, device=None):

@@ -736,7 +736,7 @@ class SdfNablaTG(torch.autograd.Function):
                     a=S[l], lda=wd[l], bias=False, stream=st, **xin)
         # output-layer adjoint ob = [d sdf, d feature] -> zbar_7 through B8 = W8^T (training pack)
         Wl = [surface.surface_fc_layers[i] for i in range(D + 1)]
-        tp = _train_pack(surface, 'sdf', [l.effective_weight() for l in Wl], [l.bias for l in Wl], dev)
+        tp = _train_pack(surface, 'sdf', Ws, [l.bias for l in Wl], dev)  # the forward's effective weights
         gs = torch.zeros(P, device=dev) if g_sdf is None else g_sdf.contiguous()
         gf = torch.zeros(P, 256, device=dev) if g_feat is None else g_feat.contiguous()
         Z = [None] * D
@@ -817,7 +817,7 @@ class RadianceTG(torch.autograd.Function):
         P = rgb.shape[0]
         desc, _ = net.nr_packed(dev)
         info = _op_info('rad', desc, 10)
-        tp = _train_pack(net, 'rad', [l.effective_weight() for l in net.layers], [l.bias for l in net.layers], dev)
+        tp = _train_pack(net, 'rad', saved[6:11], [l.bias for l in net.layers], dev)  # the forward's effective weights
         tb = tp.data_ptr()
         g = gy.contiguous().clone()
         L.check(L.lib().nr_activation(L.ptr(rgb), L.ptr(g), g.numel(), 3, st))  # sigmoid'
@@ -850,9 +850,16 @@ def nerf(net, x_emb, v_emb):
     return NeRFFn.apply(x_emb, v_emb, (len(Ws), tuple(net.skips)), *Ws, *bs, *heads)
 
 
-def sdf_nablas(surface, x, want_feat):
-    """Differentiable (sdf, nablas, feature) of a neurecon_amd ImplicitSurface at points x [P,3]."""
-    Ws = [l.effective_weight() for l in surface.surface_fc_layers]
+def effective_weights(surface):
+    """The SDF layers' weight-normed weights (differentiable), to share between evaluations of one step"""
+    return [l.effective_weight() for l in surface.surface_fc_layers]
+
+
+def sdf_nablas(surface, x, want_feat, Ws=None):
+    """Differentiable (sdf, nablas, feature) of a neurecon_amd ImplicitSurface at points x [P,3]
+    (Ws: effective_weights(surface) of this step, computed here when not given)."""
+    if Ws is None:
+        Ws = effective_weights(surface)
     bs = [l.bias for l in surface.surface_fc_layers]
     if uses_train_gemm(surface):
         out = SdfNablaTG.apply(x.reshape(-1, 3).float().contiguous(), surface, bool(want_feat), *Ws, *bs)
