@@ -59,6 +59,15 @@ def _sine30(z):
     return h, s
 
 
+def _slabs(t, C):
+    """[P, m] (rows possibly strided, e.g. the valid columns of a padded activation) as C row slabs
+    [C, P/C, m] without a copy: hipBLASLt takes the row stride as the leading dimension"""
+    if t.stride(1) != 1:
+        t = t.contiguous()
+    P, m = t.shape
+    return t.as_strided((C, P // C, m), (P // C * t.stride(0), t.stride(0), 1))
+
+
 def _wgrad(g, h):
     """gᵀ h for the weight gradients of a tall batch (g [P, m], h [P, k], P ~ 65 k): split over K into
     a batched GEMM of 16 slabs plus a sum, so the [m, k] output is computed by 16x the tiles (hipBLASLt
@@ -67,9 +76,7 @@ def _wgrad(g, h):
     C = 16
     if P < 8192 or P % C:
         return g.t() @ h
-    g3 = g.contiguous().view(C, P // C, g.shape[1])
-    h3 = h.contiguous().view(C, P // C, h.shape[1])
-    return torch.bmm(g3.transpose(1, 2), h3).sum(0)
+    return torch.bmm(_slabs(g, C).transpose(1, 2), _slabs(h, C)).sum(0)
 
 
 def _wgrad2(g1, h1, g2, h2):
@@ -80,8 +87,7 @@ def _wgrad2(g1, h1, g2, h2):
         return g1.t() @ h1 + g2.t() @ h2
     buf = torch.empty(2 * C, g1.shape[1], h1.shape[1], device=g1.device, dtype=g1.dtype)
     for i, (g, h) in enumerate(((g1, h1), (g2, h2))):
-        torch.bmm(g.contiguous().view(C, P // C, -1).transpose(1, 2), h.contiguous().view(C, P // C, -1),
-                  out=buf[i * C:(i + 1) * C])
+        torch.bmm(_slabs(g, C).transpose(1, 2), _slabs(h, C), out=buf[i * C:(i + 1) * C])
     return buf.sum(0)
 
 
@@ -760,10 +766,10 @@ class SdfNablaTG(torch.autograd.Function):
             zb = Z[l][:, :nv[l]]
             if l == 0:
                 dW[0] = _wgrad2(zb, h0[:, :nf], delta[0], hd0[:, :nf]) if tangent else _wgrad(zb, h0[:, :nf])
-            elif l == 4:  # the skip layer's input cat([h3, embed(x)]) / sqrt(2) (base.py:250)
-                hin = torch.cat([H[3][:, :217], h0[:, :nf]], 1).mul_(_ISQ2)
-                hdin = torch.cat([HD[3][:, :217], hd0[:, :nf]], 1).mul_(_ISQ2) if tangent else None
-                dW[4] = _wgrad2(zb, hin, delta[4], hdin) if tangent else _wgrad(zb, hin)
+            elif l == 4:  # the skip layer's input cat([h3, embed(x)]) / sqrt(2) (base.py:250): per column block
+                parts = [(H[3][:, :217], HD[3][:, :217] if tangent else None), (h0[:, :nf], hd0[:, :nf] if tangent else None)]
+                dW[4] = torch.cat([_wgrad2(zb, a, delta[4], b) if tangent else _wgrad(zb, a) for a, b in parts],
+                                  1).mul_(_ISQ2)
             else:
                 hin = H[l - 1][:, :nv[l - 1]]
                 dW[l] = (_wgrad2(zb, hin, delta[l][:, :nv[l]], HD[l - 1][:, :nv[l - 1]]) if tangent

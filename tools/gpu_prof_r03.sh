@@ -22,4 +22,4 @@ run b_fp32 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-full
 run frame_d 400 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --workload frame_d &&
 run train 300 python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --workload train &&
 run configs 500 python3 tools/bench_frameworks.py --steps 3 --warmup 1 --configs &&
-TAG=r03 bash tools/gpu_pmc.sh > $O/pmc.log 2>&1 && echo pmc ok
+[ -n "$ONLY" ] || TAG=r03 bash tools/gpu_pmc.sh > $O/pmc.log 2>&1 && echo pmc ok
