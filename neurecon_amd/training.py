@@ -774,7 +774,7 @@ class SdfNablaTG(torch.autograd.Function):
                 hin = H[l - 1][:, :nv[l - 1]]
                 dW[l] = (_wgrad2(zb, hin, delta[l][:, :nv[l]], HD[l - 1][:, :nv[l - 1]]) if tangent
                          else _wgrad(zb, hin))
-            db[l] = _colsum(zb)
+            db[l] = _colsum(Z[l])[:nv[l]]  # the padded buffer's columns sum independently: no copy of the view
         return (None, None, None, *dW, *db)
 
 
