@@ -252,10 +252,11 @@ def weight_stream(kstats):
             'frac': round(tbps / LDSDMA_FILL_TBPS, 3)}
 
 
-def roofline(kstats, precision):
+def roofline(kstats, precision, census=None):
     """Dominant kernel (largest device time): executed FLOPs per launch / mean launch duration, both
     launch types of the nabla kernel merged (sample launches without the feature rows, the
-    mid-point launch with them), plus each launch type on its own."""
+    mid-point launch with them), plus each launch type on its own.  kstats: the timed steps (the
+    dominant kernel's launches); census: every library kernel (per-kernel table, device-time share)."""
     peak = FP32_MFMA_PEAK_TFLOPS if precision == 'fp32' else F16X3_PEAK_TFLOPS
     per_type = {}
     for name, (n, ms, units) in kstats.items():
@@ -264,17 +265,21 @@ def roofline(kstats, precision):
             per_type[name] = {'launches': n, 'avg_launch_ms': round(ms / n, 4),
                               'achieved': round(fl / (ms * 1e-3) / 1e12, 2),
                               'frac': round(fl / (ms * 1e-3) / 1e12 / peak, 4)}
-    # the two sdf_kernel<nabla> launches (samples, mid-points) are one kernel
-    merged = {}
-    for name, (n, ms, units) in kstats.items():
-        key = 'sdf_nabla' if name.startswith('sdf_nabla') else name
-        a = merged.setdefault(key, [0, 0.0, 0.0])
-        a[0] += n; a[1] += ms; a[2] += units * 2.0 * KERNEL_MAC.get(name, 0)
-    total_ms = sum(v[1] for v in merged.values())
-    for name, (n, ms, fl) in sorted(merged.items(), key=lambda kv: -kv[1][1]):
+    # the sdf_kernel<nabla> launch types (samples, reverse pass, mid-points) are one kernel
+    def merge(ks):
+        merged = {}
+        for name, (n, ms, units) in ks.items():
+            key = 'sdf_nabla' if name.startswith('sdf_nabla') else name
+            a = merged.setdefault(key, [0, 0.0, 0.0])
+            a[0] += n; a[1] += ms; a[2] += units * 2.0 * KERNEL_MAC.get(name, 0)
+        return merged
+    table = merge(census if census is not None else kstats)
+    total_ms = sum(v[1] for v in table.values())
+    for name, (n, ms, fl) in sorted(table.items(), key=lambda kv: -kv[1][1]):
         print(f'[bench] {name:16s} launches {n:5d}  {ms:9.3f} ms ({100 * ms / max(total_ms, 1e-9):5.1f}%)  '
               f'{fl / max(ms, 1e-9) / 1e9:8.2f} TFLOP/s', file=sys.stderr)
-    dom, (n, ms, fl) = max(merged.items(), key=lambda kv: kv[1][1])
+    dom, (n, ms, fl) = max(merge(kstats).items(), key=lambda kv: kv[1][1])
+    share = table[dom][1] / total_ms if dom in table and total_ms else 1.0
     per_launch_ms = ms / n
     achieved = fl / n / (per_launch_ms * 1e-3) / 1e12
     traffic, src = pmc_traffic(dom, precision)
@@ -282,7 +287,7 @@ def roofline(kstats, precision):
             'frac': round(achieved / peak, 4), 'traffic': traffic, 'traffic_unit': 'bytes/launch',
             'traffic_source': src, 'kernel': dom,
             'avg_launch_ms': round(per_launch_ms, 4), 'launches': n,
-            'flop_per_launch': fl / n, 'share_of_device_time': round(ms / total_ms, 4),
+            'flop_per_launch': fl / n, 'share_of_device_time': round(share, 4),
             'per_launch_type': per_type,
             'weight_stream': weight_stream(kstats) if precision == 'f16x3' else None}
 
@@ -290,7 +295,7 @@ def roofline(kstats, precision):
 HBM_PEAK_TBPS = 8.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
-def train_roofline(kstats, dt, steps):
+def train_roofline(kstats, dt, steps, census=None):
     """Training step: the dominant library kernel is the layer GEMM (nr_train_gemm), whose launches
     stream [P, <=288] fp32 activations: HBM-bound.  achieved = algorithmic bytes of its calls (inputs,
     outputs, epilogue operands; training.TG_BYTES, counted per call by the host) / their device time.
@@ -298,7 +303,7 @@ def train_roofline(kstats, dt, steps):
     gradients and the fp32 radiance forward, torch elementwise, Adam)."""
     from neurecon_amd import training as T
     n, ms, _ = kstats.get('train_gemm', (0, 0.0, 0.0))
-    lib_ms = sum(v[1] for v in kstats.values())
+    lib_ms = sum(v[1] for v in (census if census is not None else kstats).values())
     if not n:
         return None
     by = T.TG_BYTES['bytes'] / max(T.TG_BYTES['calls'], 1) * n  # bytes of the timed launches
@@ -489,20 +494,39 @@ def run(args):
 
     from neurecon_amd import _lib as L
 
+    # HIP events of the timed region bracket only the dominant kernel's launches (the roofline's):
+    # every recorded launch costs two event markers on the stream, ~10 us of idle GPU each at the
+    # kernel boundary, so events around every library launch slowed the step by ~3 %.  The other
+    # library kernels' times (the per-kernel table, the dominant kernel's share, executed FLOPs of the
+    # whole step) come from a census of a few more steps with every launch recorded, after the timing.
+    dom_prefix = 'train_gemm' if args.workload == 'train' else 'sdf_nabla'
+
     def profiled(fn):
-        """timed region with the library's per-kernel HIP events on the launch stream"""
+        """(max-over-ranks time of the timed steps, dominant-kernel stats of the timed steps, every
+        library kernel's stats of a census pass scaled to the timed step count)"""
         for _ in range(args.warmup):
             fn()
         sync()
         L.profile_read()           # drop warm-up records
-        L.profile_enable(True)
+        L.profile_enable(True, dom_prefix)
         try:
             dt = timed(fn, args.steps, 0, sync, barrier)
         finally:
             L.profile_enable(False)
-        return max_over_ranks(dt), L.profile_read()
+        kdom = L.profile_read()
+        n_census = min(3, args.steps)
+        L.profile_enable(True)
+        try:
+            for _ in range(n_census):
+                fn()
+            sync()
+        finally:
+            L.profile_enable(False)
+        f = args.steps / n_census
+        census = {k: (round(n * f), ms * f, u * f) for k, (n, ms, u) in L.profile_read().items()}
+        return max_over_ranks(dt), kdom, census
 
-    dt, kstats = profiled(step)
+    dt, kstats, census = profiled(step)
     full = None
     if args.workload not in ('frame_d', 'train') and not args.no_full_eval:  # every mid-point evaluated
         full = profiled(step_full)
@@ -521,7 +545,7 @@ def run(args):
     value = total_rays / dt
     if rank == 0:
         ms = dt / args.steps * 1e3
-        roof = roofline(kstats, args.precision)
+        roof = roofline(kstats, args.precision, census)
         dtype = 'f32' if args.precision == 'fp32' else args.precision
         if args.workload == 'frame_d':
             out = {'metric': 'rays/sec, config (d): NeuS+NeRF++ full 800x600 frame, rays sharded over the GPUs',
@@ -535,7 +559,7 @@ def run(args):
                               'parallelism': f'ray-sharded x{world} + all_gather'},
                    'roofline': roof}
         elif args.workload == 'train':
-            roof = train_roofline(kstats, dt, args.steps)
+            roof = train_roofline(kstats, dt, args.steps, census)
             out = {'metric': 'training rays/sec, NeuS (configs/neus.yaml: 512 rays per GPU, fwd+bwd+Adam)',
                    'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
                    'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
@@ -560,16 +584,17 @@ def run(args):
                            'parallelism': f'ray-sharded x{world}'},
                 'roofline': roof,
                 # executed MLP FLOPs (fp32-equivalent) per second over the whole step
-                'step_tflops': round(executed_flop(kstats) / args.steps / (dt / args.steps) / 1e12, 2),
+                'step_tflops': round(executed_flop(census) / args.steps / (dt / args.steps) / 1e12, 2),
                 'mid_points_evaluated_frac': mid_frac(kstats, n_rays // world, args.steps),
             }
             if full is not None:
-                dtf, kf = full
+                dtf, kf, kfc = full
                 out['full_evaluation'] = {
                     'note': 'same rays, same outputs bit for bit (tests/test_gpu_parity.py); every mid-point through '
                             'the SDF + radiance nets as the reference does, including the ones whose alpha is exactly 0',
                     'value': round(total_rays / dtf, 1), 'ms_per_step': round(dtf / args.steps * 1e3, 3),
-                    'step_tflops': round(executed_flop(kf) / dtf / 1e12, 2), 'roofline': roofline(kf, args.precision)}
+                    'step_tflops': round(executed_flop(kfc) / dtf / 1e12, 2),
+                    'roofline': roofline(kf, args.precision, kfc)}
             if frame is not None:
                 out['strong_scaling_frame_d'] = frame
             out['config']['zero_alpha_skip'] = ('mid-points whose alpha is exactly 0 (no SDF decrease between the '

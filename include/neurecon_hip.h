@@ -642,6 +642,9 @@ typedef struct {
 } NrKernelStat;
 
 int nr_profile_enable(int on);
+/* record only the launches whose kernel name starts with prefix (NULL or "": every launch); each
+ * recorded launch costs two event markers (and, for compacted launches, a count copy) on the stream */
+int nr_profile_filter(const char* prefix);
 int nr_profile_read(NrKernelStat* out, int max, int* n_out);
 
 #ifdef __cplusplus

@@ -216,6 +216,7 @@ _SIGS = {
     'nr_volsdf_composite_bwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_f, _c_i, _c_p, _c_p, _c_p,
                                        _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
     'nr_profile_enable': (_c_i, [_c_i]),
+    'nr_profile_filter': (_c_i, [ctypes.c_char_p]),
     'nr_profile_read': (_c_i, [ctypes.POINTER(NrKernelStat), _c_i, ctypes.POINTER(_c_i)]),
 }
 
@@ -260,7 +261,9 @@ def stream_of(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
-def profile_enable(on=True):
+def profile_enable(on=True, prefix=''):
+    """library kernel timing on/off; prefix: only kernels whose name starts with it get events"""
+    check(lib().nr_profile_filter(prefix.encode()))
     check(lib().nr_profile_enable(1 if on else 0))
 
 

@@ -19,6 +19,7 @@ struct ProfRec {
 static std::mutex g_mu;
 static std::vector<ProfRec> g_recs;
 static bool g_on = false;
+static std::string g_prefix;  // record only kernels whose name starts with this (empty: all)
 constexpr int kCountSlots = 1 << 16;
 static int* g_counts = nullptr;  // device slots for the device-side unit counts of compacted launches
 static int g_nslots = 0;
@@ -28,6 +29,10 @@ bool prof_on() { return g_on; }
 ProfScope::ProfScope(const char* name, double units, hipStream_t st, const int* dev_units, int mult)
     : st_(st), on_(g_on) {
   if (!on_) return;
+  if (!g_prefix.empty() && std::string(name).compare(0, g_prefix.size(), g_prefix) != 0) {
+    on_ = false;
+    return;
+  }
   ProfRec r{name, units, nullptr, nullptr, -1, mult};
   if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) { on_ = false; return; }
   (void)hipEventRecord(r.a, st);
@@ -55,6 +60,11 @@ using namespace nr;
 
 extern "C" int nr_profile_enable(int on) {
   g_on = on != 0;
+  return NR_OK;
+}
+extern "C" int nr_profile_filter(const char* prefix) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_prefix = prefix ? prefix : "";
   return NR_OK;
 }
 
