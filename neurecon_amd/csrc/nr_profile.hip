@@ -34,7 +34,13 @@ ProfScope::ProfScope(const char* name, double units, hipStream_t st, const int* 
     return;
   }
   ProfRec r{name, units, nullptr, nullptr, -1, mult};
-  if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) { on_ = false; return; }
+  // timing-only events: no system-scope fence (its cache writeback / invalidate put ~10 us of idle GPU
+  // after every recorded launch); nr_profile_read synchronises the device before reading them
+  if (hipEventCreateWithFlags(&r.a, hipEventDisableSystemFence) != hipSuccess ||
+      hipEventCreateWithFlags(&r.b, hipEventDisableSystemFence) != hipSuccess) {
+    on_ = false;
+    return;
+  }
   (void)hipEventRecord(r.a, st);
   std::lock_guard<std::mutex> lk(g_mu);
   if (dev_units) {
@@ -73,8 +79,8 @@ extern "C" int nr_profile_read(NrKernelStat* out, int max, int* n_out) {
   std::lock_guard<std::mutex> lk(g_mu);
   std::vector<NrKernelStat> acc;
   std::vector<int> counts(g_nslots > 0 ? g_nslots : 1, 0);
+  (void)hipDeviceSynchronize();
   if (g_nslots > 0) {
-    (void)hipDeviceSynchronize();
     (void)hipMemcpy(counts.data(), g_counts, sizeof(int) * g_nslots, hipMemcpyDeviceToHost);
   }
   for (auto& r : g_recs) {
