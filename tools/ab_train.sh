@@ -1,6 +1,8 @@
 #!/bin/bash
 # A/B of the training bench on one box: A = neurecon_amd/_exp/head.so (the committed build), B = the
 # working-tree build; alternated so box-to-box variance cancels.  Extra args go to both runs.
+# head.so: compile the changed .hip files of `git archive HEAD neurecon_amd/csrc include` with
+# neurecon_amd/build.py's flags and link them with the other objects of neurecon_amd/_build/.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 for r in 1 2; do
