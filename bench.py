@@ -80,6 +80,9 @@ def parse():
     ap.add_argument('--no-frame', action='store_true',
                     help='skip the strong-scaling config-(d) frame leg of the default workload')
     ap.add_argument('--frame-steps', type=int, default=3)
+    ap.add_argument('--workspace-gb', type=float, default=16.0,
+                    help="render workspace budget (volume_render's max_workspace_gb; the library default is 4 GiB): "
+                         "a 4096-ray config-(b) batch renders as one chunk within 16 GiB")
     ap.add_argument('--stub-cpu', action='store_true', help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -315,7 +318,7 @@ def train_roofline(kstats, dt, steps, census=None):
             'library_share_of_step': round(lib_ms * 1e-3 / max(dt, 1e-12), 4)}
 
 
-def frame_d_setup(dev, precision):
+def frame_d_setup(dev, precision, workspace_gb=None):
     """config (d): NeuS + NeRF++ (N_outside=32), full 800x600 frame of the config-(d) camera (H=600,
     W=800, f=800, camera at distance 2), rays sharded over the ranks; the frame's maps are
     all-gathered (RCCL) inside the timed step."""
@@ -340,7 +343,7 @@ def frame_d_setup(dev, precision):
                                    torch.tensor(K, dtype=torch.float32, device=dev)[None], H, W)
     kw = dict(obj_bounding_radius=1.0, batched=True, calc_normal=True, detailed_output=False, perturb=False,
               N_samples=64, N_importance=64, N_outside=32, upsample_algo='official_solution', N_upsample_iters=4,
-              rayschunk=4096)
+              max_workspace_gb=workspace_gb)
 
     def step():
         with torch.no_grad():
@@ -468,7 +471,7 @@ def run(args):
     from neurecon_amd import rend_util
     from neurecon_amd.frameworks.neus import volume_render
     if args.workload == 'frame_d':
-        step, rays_per_step = frame_d_setup(dev, args.precision)   # all ranks together render one frame
+        step, rays_per_step = frame_d_setup(dev, args.precision, args.workspace_gb)  # all ranks render one frame
         n_rays = rays_per_step
     elif args.workload == 'train':
         step = train_setup(dev, args.precision, args.train_rays, world, args.adam)
@@ -482,6 +485,7 @@ def run(args):
             ro = ro.repeat(1, reps, 1)[:, :args.rays].contiguous()
             rd = rd.repeat(1, reps, 1)[:, :args.rays].contiguous()
         kw = render_kwargs()
+        kw['max_workspace_gb'] = args.workspace_gb
 
         def step():
             with torch.no_grad():
@@ -533,7 +537,7 @@ def run(args):
     frame = None
     if args.workload == 'b' and not args.no_frame:
         # strong scaling: one config-(d) 800x600 frame per step split over all ranks, all_gather timed
-        fstep, frame_rays = frame_d_setup(dev, args.precision)
+        fstep, frame_rays = frame_d_setup(dev, args.precision, args.workspace_gb)
         fdt = max_over_ranks(timed(fstep, args.frame_steps, 1, sync, barrier))
         frame = {'metric': 'rays/sec, config (d): NeuS+NeRF++ full 800x600 frame per step, rays sharded over '
                            'the GPUs (render_sharded + all_gather of the maps inside the timed region)',
@@ -605,6 +609,8 @@ def run(args):
                 eg = eager_gpu_baseline(dev, n_rays)
                 eg['speedup'] = round(value / eg['value'], 2)
                 out['cpu_baseline']['eager_gpu_reference'] = eg
+        out['config']['build_id'] = L.build_id()  # source hash compiled into libnrhip.so (neurecon_amd/build.py)
+        out['config']['workspace_gb'] = args.workspace_gb
         print(json.dumps(out), flush=True)
     if dist:
         tdist.destroy_process_group()

@@ -52,6 +52,9 @@ extern "C" {
 
 int nr_version(void);
 const char* nr_last_error(void);
+/* 16 hex digits: sha256 of the library's sources and flags at build time (neurecon_amd/build.py
+ * source_hash), so a caller can check that the loaded binary is the tree it was built from */
+const char* nr_build_id(void);
 
 /* ------------------------------------------------------------------------------------------
  * NeRF++ background MLP (NeRF, models/base.py:395-453) as used by NeuS / VolSDF outside scenes:
@@ -205,13 +208,23 @@ typedef struct {
    * (rgb / depth / mask / normals bit-identical).  no_mid_skip != 0: evaluate every
    * mid-point, as the reference does. */
   int no_mid_skip;
-  /* Deferred sample nablas (official_solution render without detailed outputs, f16x3 softplus net,
-   * no NeRF++): the sample launches leave their reverse-pass state per 16-sample tile and only the
-   * tiles holding a sample of non-zero interval alpha run the reverse pass; the other samples' nablas
-   * are weighted by exactly 0 in normals_volume (neus.py:364-368).  Maps bit-identical; the workspace
-   * then holds 8 KB per sample of a <= 4096-ray chunk.  no_defer != 0: nablas at every sample when drawn. */
+  /* Deferred sample nablas (official_solution render without the per-sample nablas / radiance outputs,
+   * f16x3 softplus net, chunks of a multiple of 16 rays; with NeRF++ too, flagged after the background
+   * net): the sample launches leave their reverse-pass state per 16-sample tile and only the tiles
+   * holding a sample of non-zero interval weight run the reverse pass; the other samples' nablas are
+   * weighted by exactly 0 in normals_volume (neus.py:364-368).  Maps bit-identical; the workspace then
+   * holds 8 KB per sample of a chunk (sized by max_workspace_bytes below).  no_defer != 0: nablas at
+   * every sample when drawn. */
   int no_defer;
+  /* Memory bound of the render (neus.py:384-397: the reference's `rayschunk` loop is the caller's
+   * memory bound).  Rays per internal chunk <= max_chunk_rays (the caller's rayschunk; <= 0: no
+   * bound), and the chunk is sized so that nr_neus_workspace_bytes() <= max_workspace_bytes
+   * (0: NR_DEFAULT_WORKSPACE_BYTES), down to one 16-ray chunk. */
+  int64_t max_chunk_rays;
+  size_t max_workspace_bytes;
 } NrNeusArgs;
+
+#define NR_DEFAULT_WORKSPACE_BYTES ((size_t)4 << 30) /* 4 GiB */
 
 size_t nr_neus_workspace_bytes(const NrNeusArgs* a);
 int nr_neus_render(const NrNeusArgs* a, void* stream);

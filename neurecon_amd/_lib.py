@@ -55,7 +55,7 @@ class NrNeusArgs(ctypes.Structure):
         ('upsample_algo', _c_i), ('fixed_s', _c_f), ('N_nograd_samples', _c_i), ('t_nograd', _c_p),
         ('workspace', _c_p), ('workspace_bytes', _c_sz),
         ('u_rand', _c_p), ('t_out_rand', _c_p), ('s_dev', _c_p), ('sample_only', _c_i), ('d_all_out', _c_p),
-        ('no_mid_skip', _c_i), ('no_defer', _c_i),
+        ('no_mid_skip', _c_i), ('no_defer', _c_i), ('max_chunk_rays', _c_i64), ('max_workspace_bytes', _c_sz),
     ]
 
 
@@ -127,6 +127,7 @@ class NrKernelStat(ctypes.Structure):
 _SIGS = {
     'nr_version': (_c_i, []),
     'nr_last_error': (ctypes.c_char_p, []),
+    'nr_build_id': (ctypes.c_char_p, []),
     'nr_sdf_packed_bytes': (_c_sz, [ctypes.POINTER(NrSdfDesc)]),
     'nr_sdf_pack': (_c_i, [ctypes.POINTER(NrSdfDesc), ctypes.POINTER(_c_p), ctypes.POINTER(_c_p), _c_p, _c_p]),
     'nr_mlp_workspace_bytes': (_c_sz, [_c_i]),
@@ -248,6 +249,11 @@ def lib():
     return _lib
 
 
+def build_id():
+    """the source hash compiled into the loaded library (neurecon_amd/build.py source_hash)"""
+    return lib().nr_build_id().decode()
+
+
 def check(rc):
     if rc != 0:
         raise NrError(f'libnrhip error {rc}: {lib().nr_last_error().decode()}')
@@ -276,6 +282,21 @@ def profile_read():
 
 
 _WS = {}
+_BUDGET = [None]
+
+
+def set_workspace_budget(gib):
+    """Module-wide cap (GiB) on one render call's workspace; None: $NR_MAX_WORKSPACE_GB, else the
+    library's default (NR_DEFAULT_WORKSPACE_BYTES, 4 GiB).  Renders are chunked to fit it."""
+    _BUDGET[0] = gib
+
+
+def workspace_budget_bytes(override_gib=None):
+    """bytes for NrNeusArgs.max_workspace_bytes (0 = the library's default)"""
+    g = override_gib if override_gib is not None else _BUDGET[0]
+    if g is None:
+        g = os.environ.get('NR_MAX_WORKSPACE_GB')
+    return 0 if g in (None, '') else int(float(g) * (1 << 30))
 
 
 def workspace(device, nbytes):

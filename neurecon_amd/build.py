@@ -4,11 +4,18 @@
 
 Every .hip under neurecon_amd/csrc is compiled for --offload-arch=gfx950 into an object in
 neurecon_amd/_build/, then linked into neurecon_amd/libnrhip.so (git-ignored; it travels to the
-GPU box with the repo snapshot).  Rebuilds only when a source/header is newer than the library.
+GPU box with the repo snapshot).
+
+Build ID: `source_hash()` is a sha256 over the names and bytes of every csrc source/header, the
+public header and the compiler flags.  It is compiled into the library (`nr_build_id()`), and the
+library is rebuilt whenever the ID it carries differs from the tree's (not by file times: a copied
+tree or a reverted edit keeps or changes the hash, never the mtime order).  smoke() and bench.py
+print it and smoke() asserts it equals the tree's.
 """
 import argparse
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -41,16 +48,39 @@ def _deps():
     return _sources() + glob.glob(os.path.join(CSRC, '*.h')) + glob.glob(os.path.join(INC, '*.h'))
 
 
+def source_hash():
+    """16 hex digits identifying the library's sources: csrc/*.hip, csrc/*.h, include/*.h (names and
+    bytes, in name order) and the compile flags (without absolute paths)."""
+    h = hashlib.sha256()
+    for p in sorted(_deps(), key=lambda q: (os.path.basename(os.path.dirname(q)), os.path.basename(q))):
+        h.update(os.path.basename(os.path.dirname(p)).encode() + b'/' + os.path.basename(p).encode() + b'\0')
+        with open(p, 'rb') as f:
+            h.update(f.read())
+        h.update(b'\0')
+    h.update(repr([f for f in FLAGS if f not in (CSRC, INC)]).encode())
+    h.update(repr(sorted(FILE_FLAGS.items())).encode())
+    return h.hexdigest()[:16]
+
+
+def lib_build_id(path=LIB):
+    """The build ID compiled into a library file (read from its bytes; no dlopen), or None."""
+    if not os.path.exists(path):
+        return None
+    with open(path, 'rb') as f:
+        data = f.read()
+    i = data.find(b'NR_BUILD_ID=')
+    if i < 0:
+        return None
+    return data[i + 12:i + 28].decode('ascii', 'replace')
+
+
 def up_to_date():
-    if not os.path.exists(LIB):
-        return False
-    t = os.path.getmtime(LIB)
-    return all(os.path.getmtime(p) <= t for p in _deps())
+    return lib_build_id() == source_hash()
 
 
-def _compile(src):
+def _compile(src, build_id):
     obj = os.path.join(OUT, os.path.basename(src) + '.o')
-    cmd = [HIPCC] + flags_for(src) + ['-c', src, '-o', obj]
+    cmd = [HIPCC] + flags_for(src) + [f'-DNR_BUILD_ID="{build_id}"', '-c', src, '-o', obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f'hipcc failed for {src}:\n{r.stderr}')
@@ -62,9 +92,10 @@ def build(force=False, jobs=None, verbose=False):
         return LIB
     os.makedirs(OUT, exist_ok=True)
     srcs = _sources()
+    bid = source_hash()
     jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 4) // 2), 8)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        results = list(ex.map(_compile, srcs))
+        results = list(ex.map(lambda s: _compile(s, bid), srcs))
     for obj, err in results:
         if verbose and err.strip():
             print(err, file=sys.stderr)
@@ -73,6 +104,8 @@ def build(force=False, jobs=None, verbose=False):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f'link failed:\n{r.stderr}')
+    if lib_build_id(tmp) != bid:
+        raise RuntimeError(f'linked library does not carry build ID {bid}')
     os.replace(tmp, LIB)
     return LIB
 
@@ -83,4 +116,4 @@ if __name__ == '__main__':
     ap.add_argument('--jobs', type=int, default=None)
     ap.add_argument('-v', '--verbose', action='store_true')
     a = ap.parse_args()
-    print(build(force=a.force, jobs=a.jobs, verbose=a.verbose))
+    print(build(force=a.force, jobs=a.jobs, verbose=a.verbose), source_hash())

@@ -427,12 +427,23 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   return NR_OK;
 }
 
+// rays per chunk: at most 16384, the caller's max_chunk_rays (its rayschunk), and as many as keep the
+// workspace within max_workspace_bytes (the plan is affine in the chunk's ray count); deferred
+// chunks (8 KB of slabs per sample) are a multiple of 16 rays, so that every launch starts a tile
 static int64_t neus_chunk_rays(const NrNeusArgs* a) {
+  const int64_t n = a->n_rays > 0 ? a->n_rays : 1;
   int64_t cap = 16384;
-  // deferred sample nablas keep 8 KB per sample of the chunk: <= 16 GB of slabs (16384 rays of 128
-  // samples; smaller chunks leave the per-ray kernels a fraction of the chip), a multiple of 16 rays
-  if (neus_deferred(*a, 16)) cap = std::max<int64_t>(16, (int64_t)(16384 * 128 / std::max(neus_total_samples(*a), 1)) / 16 * 16);
-  return a->n_rays < cap ? (a->n_rays > 0 ? a->n_rays : 1) : cap;
+  if (a->max_chunk_rays > 0) cap = std::min(cap, a->max_chunk_rays);
+  const size_t budget = a->max_workspace_bytes ? a->max_workspace_bytes : NR_DEFAULT_WORKSPACE_BYTES;
+  const bool defer = neus_deferred(*a, 16);
+  NrNeusArgs q = *a;  // plan sizes with deferral decided as for a 16-ray-multiple chunk
+  const size_t t1 = neus_plan(q, 1024).total, t2 = neus_plan(q, 2048).total;
+  const size_t per_ray = (t2 - t1) / 1024 + 1, fixed = t1 > 1024 * per_ray ? t1 - 1024 * per_ray : 0;
+  const int64_t fit = budget > fixed ? (int64_t)((budget - fixed) / per_ray) : 0;
+  cap = std::min(cap, std::max<int64_t>(fit, 16));
+  if (n <= cap) return n;
+  if (defer && cap >= 16) cap = cap / 16 * 16;
+  return std::max<int64_t>(cap, 1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -709,6 +720,12 @@ using namespace nr;
 extern "C" {
 
 int nr_version(void) { return 1; }
+#ifndef NR_BUILD_ID
+#define NR_BUILD_ID "unknown-source00"
+#endif
+// the marker lets neurecon_amd/build.py read the ID from the file without loading it
+__attribute__((used)) static const char kBuildIdMarker[] = "NR_BUILD_ID=" NR_BUILD_ID;
+const char* nr_build_id(void) { return kBuildIdMarker + 12; }
 const char* nr_last_error(void) { return g_err.c_str(); }
 
 size_t nr_sdf_packed_bytes(const NrSdfDesc* d) {

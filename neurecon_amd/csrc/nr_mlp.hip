@@ -1777,6 +1777,7 @@ void sdf4_kernel(SdfKArgs a) {
 #pragma unroll
         for (int b = 0; b < 16; b += 2) m = amax8(m, G[b], G[b + 1]);
         m_in[q] = max4_groups(m);
+        mrun[q] = 0.0f;  // B7's running max starts here (STAGE 2 skips the forward that zeroes it)
         const float sc = bound_scale(m_in[q]);
 #pragma unroll
         for (int s = 0; s < 8; ++s) split8a(G[2 * s], G[2 * s + 1], sc, Uh[q][s], Ul[q][s]);

@@ -1,6 +1,7 @@
 // neurecon_amd — opt-in per-kernel timing with HIP events (bench.py roofline numbers).
 // Disabled by default; when enabled each library kernel launch is bracketed by two events on its
 // own stream, so the measured duration is that kernel's, not the surrounding step's.
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -18,20 +19,23 @@ struct ProfRec {
 };
 static std::mutex g_mu;
 static std::vector<ProfRec> g_recs;
-static bool g_on = false;
+static std::atomic<bool> g_on{false};
 static std::string g_prefix;  // record only kernels whose name starts with this (empty: all)
 constexpr int kCountSlots = 1 << 16;
 static int* g_counts = nullptr;  // device slots for the device-side unit counts of compacted launches
 static int g_nslots = 0;
 
-bool prof_on() { return g_on; }
+bool prof_on() { return g_on.load(); }
 
 ProfScope::ProfScope(const char* name, double units, hipStream_t st, const int* dev_units, int mult)
-    : st_(st), on_(g_on) {
+    : st_(st), on_(g_on.load()) {
   if (!on_) return;
-  if (!g_prefix.empty() && std::string(name).compare(0, g_prefix.size(), g_prefix) != 0) {
-    on_ = false;
-    return;
+  {  // the prefix is written by nr_profile_filter under g_mu (possibly from another thread)
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_prefix.empty() && std::string(name).compare(0, g_prefix.size(), g_prefix) != 0) {
+      on_ = false;
+      return;
+    }
   }
   ProfRec r{name, units, nullptr, nullptr, -1, mult};
   // timing-only events: no system-scope fence (its cache writeback / invalidate put ~10 us of idle GPU

@@ -92,15 +92,19 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
                   near_bypass=None, far_bypass=None, detailed_output=True, show_progress=False, perturb=False,
                   fixed_s_recp=1 / 64., N_samples=64, N_importance=64, N_outside=0,
                   upsample_algo='official_solution', N_nograd_samples=2048, N_upsample_iters=4,
-                  skip_zero_alpha=True, defer_sample_nablas=True, **dummy_kwargs):
+                  skip_zero_alpha=True, defer_sample_nablas=True, max_workspace_gb=None, **dummy_kwargs):
     """neus.py:118-397, render mode.  skip_zero_alpha (not a reference argument): mid-points whose alpha
     is exactly 0 (and, with NeRF++, the ones outside the bounding sphere) skip the SDF + radiance nets
     when the radiance output is not asked for -- their weight is an exact 0 (or their colour is the
     background's), so rgb / depth / mask / normals are bit-identical;
     False evaluates every mid-point as the reference does.  defer_sample_nablas (not a reference
-    argument; with skip_zero_alpha, f16x3, no NeRF++, no detailed outputs): the samples' reverse pass
-    (their nablas feed only normals_volume, weighted by w_i) runs after the sampling, only on the
-    16-sample tiles holding a sample of non-zero weight -- bit-identical maps.  rays_o/rays_d: [(B,) N_rays, 3]; rays_d need not be normalized.
+    argument; with skip_zero_alpha, the f16x3 softplus net, without the per-sample nablas / radiance
+    outputs; with or without NeRF++): the samples' reverse pass (their nablas feed only normals_volume,
+    weighted by w_i) runs after the sampling, only on the 16-sample tiles holding a sample of non-zero
+    weight -- bit-identical maps.  Memory: the library renders chunks of at most `rayschunk` rays (the
+    reference's memory bound, neus.py:384-397) whose workspace fits max_workspace_gb (not a reference
+    argument; None: _lib.set_workspace_budget / $NR_MAX_WORKSPACE_GB / 4 GiB) -- the maps do not depend
+    on the chunking.  rays_o/rays_d: [(B,) N_rays, 3]; rays_d need not be normalized.
     perturb=True draws the reference's uniforms (same generators, shapes and order) and hands them
     to the kernels."""
     L.require_gpu(rays_o, 'rays_o')
@@ -159,6 +163,8 @@ def volume_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
     a.s, a.s_dev = 0.0, L.ptr(s_dev)
     a.no_mid_skip = 0 if skip_zero_alpha else 1
     a.no_defer = 0 if defer_sample_nablas else 1
+    a.max_chunk_rays = int(rayschunk) if rayschunk else 0
+    a.max_workspace_bytes = L.workspace_budget_bytes(max_workspace_gb)
     a.obj_bounding_radius = float(obj_bounding_radius)
     a.near_bypass = float('nan') if near_bypass is None else float(near_bypass)
     a.far_bypass = float('nan') if far_bypass is None else float(far_bypass)
@@ -250,6 +256,8 @@ def _sample_depths(ro, rd, model, dev, obj_bounding_radius, batched, B, rayschun
                                        N_importance, N_outside, dev)
         a.u_rand = L.ptr(u_rand)
     a.sample_only, a.d_all_out = 1, L.ptr(d_all)
+    a.max_chunk_rays = int(rayschunk) if rayschunk else 0
+    a.max_workspace_bytes = L.workspace_budget_bytes()
     lib = L.lib()
     ws_bytes = lib.nr_neus_workspace_bytes(ctypes.byref(a))
     ws = L.workspace(dev, ws_bytes)

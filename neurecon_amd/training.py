@@ -616,9 +616,12 @@ def uses_train_gemm(module):
     """f16x3 softplus SDF nets (D=8, skip 4) and f16x3 ReLU radiance nets with D=4 train on nr_train_gemm"""
     if getattr(module, 'precision', 'fp32') != 'f16x3' or getattr(module, 'use_siren', False):
         return False
-    if hasattr(module, 'surface_fc_layers'):
-        return module.D == 8 and list(module.skips) == [4] and module.W == 256 and module.W_geo_feat == 256
-    return module.D == 4 and module.W == 256
+    if hasattr(module, 'surface_fc_layers'):  # the render pack's SDF shape (check_sdf_desc, nr_capi.hip)
+        return (module.D == 8 and list(module.skips) == [4] and module.W == 256 and module.W_geo_feat == 256
+                and module.embed_multires == 6)
+    # the render pack's radiance shape (check_rad_desc) with RadianceTG's D = 4
+    return (module.D == 4 and module.W == 256 and module.W_geo_feat == 256 and module.embed_multires < 0
+            and module.embed_multires_view <= 7)
 
 
 def _pad16(n):
@@ -881,6 +884,6 @@ def radiance(net, x, v, nrm, feat):
     view = net.use_view_dirs
     if uses_train_gemm(net):
         return RadianceTG.apply(x.contiguous(), v.contiguous() if view else None, nrm.contiguous() if view else None,
-                                feat, net, *Ws, *bs)
+                                feat.contiguous(), net, *Ws, *bs)
     return RadianceFn.apply(x.contiguous(), v.contiguous() if view else None, nrm.contiguous() if view else None,
                             feat.contiguous(), (net.D, net.embed_multires_view, view, bool(net.use_siren)), *Ws, *bs)

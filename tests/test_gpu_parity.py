@@ -456,3 +456,45 @@ def test_neus_deferred_sample_nablas_bit_identical(perturb, calc_normal, N_outsi
         for name, a, b in zip(('rgb', 'depth', 'mask', 'normals'), outs[0], outs[1]):
             assert torch.equal(a, b), (rays, name, float((a - b).abs().max()))
     print(f'deferred sample nablas: bit-identical (perturb={perturb}, calc_normal={calc_normal}, N_outside={N_outside})')
+
+
+@pytest.mark.parametrize('N_outside', [0, 32])
+def test_neus_workspace_bound_by_rayschunk(N_outside):
+    """The caller's memory bound (neus.py:384-397: `rayschunk`, 256 for validation renders, 4096 in
+    tools/render_view.py:529) bounds the library's chunks, and the default workspace is capped at 4 GiB
+    (NR_DEFAULT_WORKSPACE_BYTES): renders with rayschunk=256, the default and a 16 GiB budget are
+    bit-identical, and the peak device memory of each is reported."""
+    from oracle import rays as orays
+    from neurecon_amd.frameworks.neus import volume_render
+    from neurecon_amd import _lib
+    H, W, f, dist = wg.CAMERAS['b']
+    if N_outside:
+        dist, f = wg.CAMERAS['d'][3], 80.0
+    ro, rd, _ = orays.get_rays(wg.look_at_c2w(dist)[None], wg.intrinsics(f, H, W)[None], H, W)
+    sd = wg.neus_state(seed=1, use_outside_nerf=bool(N_outside))
+    m = neus_model(sd, precision='f16x3', use_outside_nerf=bool(N_outside))
+    kw = dict(obj_bounding_radius=1.0, batched=True, calc_normal=True, detailed_output=False, perturb=False,
+              N_samples=64, N_importance=64, N_upsample_iters=4, N_outside=N_outside)
+    o, d = ro.cuda(), rd.cuda()
+    outs = []
+    for name, extra in (('rayschunk=256', dict(rayschunk=256)), ('default (4 GiB)', {}),
+                        ('16 GiB budget', dict(max_workspace_gb=16))):
+        _lib._WS.clear()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats()
+        base = torch.cuda.memory_allocated()
+        with torch.no_grad():
+            rgb, depth, ex = volume_render(o, d, m, **kw, **extra)
+        torch.cuda.synchronize()
+        peak = (torch.cuda.max_memory_allocated() - base) / 2**30
+        print(f'N_outside={N_outside} 4096-ray render, {name}: peak device memory {peak:.3f} GiB')
+        if name.startswith('default'):
+            assert peak <= 4.25, peak
+        if name.startswith('rayschunk'):
+            assert peak <= 1.0, peak
+        outs.append([rgb, depth, ex['mask_volume'], ex['normals_volume']])
+    _lib._WS.clear()
+    for other in outs[1:]:
+        for nm, a, b in zip(('rgb', 'depth', 'mask', 'normals'), outs[0], other):
+            assert torch.equal(a, b), (nm, float((a - b).abs().max()))

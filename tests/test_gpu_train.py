@@ -436,3 +436,29 @@ def test_ddp_gradient_allreduce_world2(fw):
     worst = [m[1] for m in msgs if m[0] == 'diff'][0]
     print(f'DDP-averaged vs single-process mean gradient: worst error / scale {worst:.3e}')
     assert worst <= 1e-5
+
+
+@pytest.mark.parametrize('precision', ['f16x3', 'fp32'])
+def test_radiance_training_strided_feature(precision):
+    """A geometry feature handed over as a strided view (h[..., 1:] of a wider tensor, as a caller
+    slicing the SDF net's output would) gives the same colours and gradients as a contiguous copy
+    (RadianceTG / RadianceFn read raw pointers)."""
+    from neurecon_amd import training as T
+    m = neus_model(wg.neus_state(seed=2), precision=precision)
+    m.train()
+    net = m.radiance_net
+    torch.manual_seed(0)
+    P = 1000
+    x, v, nrm = (torch.randn(P, 3, device='cuda') for _ in range(3))
+    wide = torch.randn(P, 257, device='cuda')
+    outs = []
+    for feat in (wide[:, 1:], wide[:, 1:].contiguous()):
+        f = feat.detach().requires_grad_(True)
+        n = nrm.detach().requires_grad_(True)
+        net.zero_grad()
+        rgb = T.radiance(net, x, v, n, f)
+        (rgb * torch.linspace(0.5, 1.5, 3, device='cuda')).sum().backward()
+        outs.append([rgb.detach(), f.grad, n.grad] + [p.grad.clone() for p in net.parameters()])
+    assert not wide[:, 1:].is_contiguous()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b), float((a - b).abs().max())
