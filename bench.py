@@ -83,6 +83,9 @@ def parse():
     ap.add_argument('--workspace-gb', type=float, default=16.0,
                     help="render workspace budget (volume_render's max_workspace_gb; the library default is 4 GiB): "
                          "a 4096-ray config-(b) batch renders as one chunk within 16 GiB")
+    ap.add_argument('--no-configs', action='store_true',
+                    help='skip the BASELINE configs (c), (e) and the training step in the default line')
+    ap.add_argument('--config-steps', type=int, default=5)
     ap.add_argument('--stub-cpu', action='store_true', help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -383,6 +386,167 @@ def train_setup(dev, precision, n_rays, world, adam='fused'):
     return step
 
 
+def camera_for(device, H, W, f, dist):
+    """SURVEY §8(d) synthetic camera: look_at((0,0,-dist) -> origin, up (0,-1,0)), K = [[f,0,W/2],[0,f,H/2]]"""
+    import numpy as np
+    from neurecon_amd import rend_util
+    cam = np.array([0.0, 0.0, -dist])
+    fwd = -cam / np.linalg.norm(cam)
+    x = np.cross([0.0, -1.0, 0.0], fwd); x /= np.linalg.norm(x)
+    y = np.cross(fwd, x)
+    c2w = np.eye(4); c2w[:3, 0], c2w[:3, 1], c2w[:3, 2], c2w[:3, 3] = x, y, fwd, cam
+    K = np.eye(4); K[0, 0] = K[1, 1] = f; K[0, 2] = W / 2; K[1, 2] = H / 2
+    return rend_util.get_rays(torch.tensor(c2w, dtype=torch.float32, device=device)[None],
+                              torch.tensor(K, dtype=torch.float32, device=device)[None], H, W)[:2]
+
+
+def _census(fn, steps, warmup, sync):
+    """wall time per step of `steps` calls, then one more pass with every library launch timed by HIP
+    events: ({kernel: (launches, ms, units)} per step)"""
+    from neurecon_amd import _lib as L
+    for _ in range(warmup):
+        fn()
+    sync()
+    t = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    sync()
+    dt = (time.perf_counter() - t) / steps
+    L.profile_read()
+    L.profile_enable(True)
+    try:
+        fn()
+        sync()
+    finally:
+        L.profile_enable(False)
+    return dt, L.profile_read()
+
+
+def _kernel_summary(ks, precision, rad_in):
+    """per library kernel: ms per step and share; the dominant MLP kernel's executed-FLOP roofline"""
+    peak = FP32_MFMA_PEAK_TFLOPS if precision == 'fp32' else F16X3_PEAK_TFLOPS
+    mac = dict(KERNEL_MAC, radiance=rad_in * 256 + 3 * 256 * 256 + 3 * 256)
+    total = sum(v[1] for v in ks.values()) or 1e-9
+    table = {k: {'launches': n, 'ms': round(ms, 4), 'share': round(ms / total, 4)}
+             for k, (n, ms, u) in sorted(ks.items(), key=lambda kv: -kv[1][1])}
+    mlp = {k: v for k, v in ks.items() if k in mac and k != 'train_gemm' and v[0]}
+    dom = None
+    if mlp:
+        k, (n, ms, units) = max(mlp.items(), key=lambda kv: kv[1][1])
+        tf = units * 2.0 * mac[k] / (ms * 1e-3) / 1e12
+        dom = {'kernel': k, 'bound': 'mfma', 'launches': n, 'avg_launch_ms': round(ms / n, 4),
+               'achieved': round(tf, 2), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(tf / peak, 4),
+               'share_of_device_time': round(ms / total, 4)}
+    return table, dom
+
+
+def config_c(dev, precision, steps, warmup, sync):
+    """BASELINE config (c): VolSDF (configs/volsdf.yaml architecture, beta_init 1e-3 so the error-bounded
+    loop runs), 2048 rays of the 32x64 camera (f 80, distance 2.7), N_samples 128 + N_importance 128,
+    max_upsample_iter 6, render mode"""
+    from neurecon_amd.frameworks.volsdf import VolSDF, volume_render
+    torch.manual_seed(0)
+    surf = dict(use_siren=False, embed_multires=6, radius_init=1.0, geometric_init=True, D=8, W=256, skips=[4],
+                precision=precision)
+    rad = dict(use_siren=False, embed_multires=-1, embed_multires_view=-1, use_view_dirs=True, D=4, W=256, skips=[],
+               precision=precision)
+    m = VolSDF(beta_init=1e-3, speed_factor=10.0, W_geo_feat=256, obj_bounding_radius=3.0, surface_cfg=surf,
+               radiance_cfg=rad).to(dev).eval()
+    ro, rd = camera_for(dev, 32, 64, 80.0, 2.7)
+    kw = dict(near=0.0, far=6.0, obj_bounding_radius=3.0, batched=True, calc_normal=True, detailed_output=False,
+              N_samples=128, N_importance=128, max_upsample_steps=6, use_nerfplusplus=False)
+
+    def step():
+        with torch.no_grad():
+            return volume_render(ro, rd, m, **kw)
+    dt, ks = _census(step, steps, warmup, sync)
+    with torch.no_grad():
+        _, _, ex = volume_render(ro, rd, m, **dict(kw, detailed_output=True))
+    it = ex['iter_usage'].flatten()
+    table, dom = _kernel_summary(ks, precision, 265)
+    n = ro.shape[1]
+    return {'workload': 'VolSDF render, 2048 rays x (128 + 128) error-bounded samples, beta 1e-3, max_upsample_iter 6',
+            'value': round(n / dt, 1), 'unit': 'rays/s', 'ms_per_step': round(dt * 1e3, 3), 'steps': steps,
+            'iter_usage': {str(int(k)): int((it == k).sum()) for k in it.unique().tolist()},
+            'roofline': dom, 'kernels': table}
+
+
+def config_e(dev, precision, steps, warmup, sync):
+    """BASELINE config (e): UNISURF (configs/unisurf.yaml architecture, tau 0.5 -> logit 0, radius of
+    interest 4), 4096 rays of the 64x64 camera (f 80, distance 3): 256-step march + 8 secant steps,
+    64 interval + 32 free-space samples, render mode"""
+    from neurecon_amd.frameworks.unisurf import UNISURF, volume_render
+    torch.manual_seed(0)
+    surf = dict(use_siren=False, embed_multires=6, radius_init=1.0, geometric_init=True, D=8, W=256, skips=[4],
+                precision=precision)
+    rad = dict(use_siren=False, embed_multires=-1, embed_multires_view=-1, use_view_dirs=True, D=4, W=256, skips=[],
+               precision=precision)
+    m = UNISURF(W_geo_feat=256, surface_cfg=surf, radiance_cfg=rad).to(dev).eval()
+    ro, rd = camera_for(dev, 64, 64, 80.0, 3.0)
+    kw = dict(batched=True, calc_normal=True, detailed_output=False, logit_tau=0.0, radius_of_interest=4.0,
+              method='secant', N_query=64, N_freespace=32)
+
+    def step():
+        with torch.no_grad():
+            return volume_render(ro, rd, m, **kw)
+    dt, ks = _census(step, steps, warmup, sync)
+    with torch.no_grad():
+        _, _, ex = volume_render(ro, rd, m, **dict(kw, detailed_output=True))
+    table, dom = _kernel_summary(ks, precision, 265)
+    n = ro.shape[1]
+    out = {'workload': 'UNISURF render, 4096 rays: 256-step march + 8 secant steps, 64 + 32 samples',
+           'value': round(n / dt, 1), 'unit': 'rays/s', 'ms_per_step': round(dt * 1e3, 3), 'steps': steps,
+           'roofline': dom, 'kernels': table}
+    if 'mask_surface' in ex:
+        out['secant_hit_frac'] = round(float(ex['mask_surface'].float().mean()), 4)
+    return out
+
+
+def config_train(dev, precision, n_rays, steps, warmup, sync, adam='fused'):
+    """NeuS training step, 512 rays (train_setup): wall rays/s, the library's kernel census, and every
+    device kernel of one step by name from torch.profiler (the hipBLASLt `Cijk_*` share included)"""
+    step = train_setup(dev, precision, n_rays, 1, adam)
+    dt, ks = _census(step, steps, warmup, sync)
+    table, _ = _kernel_summary(ks, precision, 289)
+    out = {'workload': 'NeuS Trainer.forward + backward (double backward through the nablas) + Adam, 512 rays x 128 '
+                       'samples', 'value': round(n_rays / dt, 1), 'unit': 'rays/s', 'ms_per_step': round(dt * 1e3, 3),
+           'steps': steps, 'library_kernels': table}
+    try:
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            for _ in range(2):
+                step()
+            sync()
+        groups, by_name = {}, {}
+        for ev in prof.key_averages():
+            t = getattr(ev, 'self_device_time_total', None)
+            if t is None:
+                t = getattr(ev, 'self_cuda_time_total', 0)
+            if not t:
+                continue
+            nm = ev.key
+            if nm.startswith('Cijk_') or 'hipblaslt' in nm.lower():
+                grp = 'hipBLASLt (Cijk_*)'
+            elif 'tgemm_kernel' in nm:
+                grp = 'nr_train_gemm (tgemm_kernel)'
+            elif 'nr::' in nm:
+                grp = 'other libnrhip kernels'
+            else:
+                grp = 'torch / other'
+            groups[grp] = groups.get(grp, 0.0) + t / 2e3   # us over 2 steps -> ms per step
+            by_name[nm] = by_name.get(nm, 0.0) + t / 2e3
+        tot = sum(groups.values()) or 1e-9
+        out['device_time_per_step_ms'] = round(tot, 3)
+        out['device_time_by_group'] = {k: {'ms': round(v, 3), 'share': round(v / tot, 4)}
+                                       for k, v in sorted(groups.items(), key=lambda kv: -kv[1])}
+        top = sorted(by_name.items(), key=lambda kv: -kv[1])[:6]
+        out['top_kernels'] = [{'name': k[:90], 'ms': round(v, 3), 'share': round(v / tot, 4)} for k, v in top]
+        out['device_time_source'] = 'torch.profiler (ROCm kernel trace), 2 steps'
+    except Exception as e:  # the profiler is a diagnostic: its absence does not void the timing
+        out['device_time_by_group'] = f'unavailable: {type(e).__name__}: {e}'
+    return out
+
+
 def executed_flop(kstats):
     """fp32-equivalent FLOPs the MLP launches executed (units = points actually evaluated)"""
     return sum(units * 2.0 * KERNEL_MAC.get(name, 0) for name, (n, ms, units) in kstats.items())
@@ -545,6 +709,12 @@ def run(args):
                  'steps': args.frame_steps, 'warmup': 1, 'ms_per_step': round(fdt / args.frame_steps * 1e3, 3),
                  'scaling': 'strong', 'rays_per_step': frame_rays, 'rays_per_gpu': frame_rays // world,
                  'parallelism': f'ray-sharded x{world} + all_gather'}
+    cfgs = None
+    if args.workload == 'b' and not args.no_configs and world == 1:
+        cs, cw = args.config_steps, 1
+        cfgs = {'c_volsdf_2048x256': config_c(dev, args.precision, cs, cw, sync),
+                'e_unisurf_4096': config_e(dev, args.precision, cs, cw, sync),
+                'train_neus_512': config_train(dev, args.precision, args.train_rays, 2 * cs, 2, sync, args.adam)}
     total_rays = n_rays * args.steps
     value = total_rays / dt
     if rank == 0:
@@ -601,6 +771,8 @@ def run(args):
                     'roofline': roofline(kf, args.precision, kfc)}
             if frame is not None:
                 out['strong_scaling_frame_d'] = frame
+            if cfgs is not None:
+                out['configs'] = cfgs
             out['config']['zero_alpha_skip'] = ('mid-points whose alpha is exactly 0 (no SDF decrease between the '
                                                 'two samples, neus.py:28-35) get weight 0 and skip the nets; '
                                                 'rgb/depth/mask/normals bit-identical to full evaluation')

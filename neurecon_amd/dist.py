@@ -1,8 +1,14 @@
 """Multi-GPU rendering: one process per GPU (torchrun), rays sharded across ranks.
 
 The render path has no data-path exchange: rays are independent (NeuS / VolSDF), so each rank
-renders a contiguous slice of the rays and, when the caller wants the whole frame on every rank,
-the per-ray maps are all-gathered once (RCCL over xGMI with backend 'nccl', gloo on CPU).
+renders its share of the rays and, when the caller wants the whole frame on every rank, the per-ray
+maps are all-gathered once (RCCL over xGMI with backend 'nccl', gloo on CPU).
+Shares are dealt block-cyclically by default (blocks of `block` consecutive rays, block b to rank
+b mod world): per-ray work depends on the scene (rays that miss the object skip most of the nets'
+work: zero-alpha mid-points, deferred sample nablas), so contiguous row bands of a frame differ in
+cost and the slowest band would bound a strong-scaled frame; dealt blocks give every rank a sample
+of every band.  The gather puts each block back at its place.  layout='contiguous' keeps one
+contiguous range per rank (the reference's DataParallel scatter, neus.py:413-414).
 The same driver shards surface_render (sphere tracing / root finding are per ray) and
 `sdf_grid_sharded` splits extract_mesh's voxel grid by contiguous index ranges.
 UNISURF's F.normalize(nablas) couples the points of one `rayschunk` (unisurf.py:36,
@@ -36,6 +42,53 @@ def shard_rays(rays_o, rays_d, rank=None, world_size=None, align=1, dim=-2):
     return rays_o.narrow(dim, lo, hi - lo), rays_d.narrow(dim, lo, hi - lo), (lo, hi)
 
 
+BLOCK = 1024  # rays per dealt block of the cyclic layout
+
+
+def cyclic_index(n, rank, world_size, block=BLOCK):
+    """ray indices of `rank` in the block-cyclic layout, ascending: blocks rank, rank + world_size, ..."""
+    nb = (n + block - 1) // block
+    starts = torch.tensor(list(range(rank, nb, world_size)), dtype=torch.int64) * block
+    if starts.numel() == 0:
+        return torch.empty(0, dtype=torch.int64)
+    idx = (starts[:, None] + torch.arange(block, dtype=torch.int64)[None, :]).reshape(-1)
+    return idx[idx < n]
+
+
+def cyclic_count(n, rank, world_size, block=BLOCK):
+    nb = (n + block - 1) // block
+    full = len(range(rank, nb, world_size)) * block
+    last = nb - 1
+    if nb and last % world_size == rank:
+        full -= nb * block - n
+    return full
+
+
+def gather_cyclic(t, n_total, dim=0, block=BLOCK):
+    """All-gather per-rank shares of the block-cyclic layout and put every ray back at its index."""
+    rank, ws = world()
+    if ws == 1:
+        return t
+    if t.is_cuda and dist.get_backend() == 'gloo':
+        return gather_cyclic(t.cpu(), n_total, dim, block).to(t.device)
+    t = t.contiguous()
+    counts = [cyclic_count(n_total, r, ws, block) for r in range(ws)]
+    cap = max(counts)
+    pad_shape = list(t.shape)
+    pad_shape[dim] = cap
+    buf = torch.zeros(pad_shape, dtype=t.dtype, device=t.device)
+    buf.narrow(dim, 0, t.shape[dim]).copy_(t)
+    parts = [torch.empty_like(buf) for _ in range(ws)]
+    dist.all_gather(parts, buf)
+    out_shape = list(t.shape)
+    out_shape[dim] = n_total
+    out = torch.empty(out_shape, dtype=t.dtype, device=t.device)
+    for r, (p, c) in enumerate(zip(parts, counts)):
+        idx = cyclic_index(n_total, r, ws, block).to(t.device)
+        out.index_copy_(dim, idx, p.narrow(dim, 0, c))
+    return out
+
+
 def gather_rays(t, n_total, dim=0, align=1):
     """All-gather per-rank slices (sharded with shard_bounds) back into the full tensor on every rank."""
     rank, ws = world()
@@ -55,22 +108,35 @@ def gather_rays(t, n_total, dim=0, align=1):
     return torch.cat([p.narrow(dim, 0, hi - lo) for p, (lo, hi) in zip(parts, sizes)], dim)
 
 
-def render_sharded(render_fn, rays_o, rays_d, model, gather=True, align=1, group=None, **kw):
-    """Render this rank's slice of the rays with `render_fn(rays_o, rays_d, model, **kw)` (any of the
+def render_sharded(render_fn, rays_o, rays_d, model, gather=True, align=1, group=None, layout='cyclic',
+                   block=BLOCK, **kw):
+    """Render this rank's share of the rays with `render_fn(rays_o, rays_d, model, **kw)` (any of the
     frameworks' volume_render); with gather=True the per-ray maps (rgb, depth, every extras entry
-    with a ray dimension) are all-gathered so every rank holds the full result.  A render whose
-    batched normalisation couples rays across shards (UNISURF, `render_fn.window_sharded`) is told
-    its slice and reduces those sums over the ranks itself (one small all-reduce per call)."""
+    with a ray dimension) are all-gathered so every rank holds the full result, each ray at its
+    index.  layout 'cyclic' (default): blocks of `block` rays dealt round-robin; 'contiguous': one
+    range per rank (in units of `align` rays).  A render whose batched normalisation couples rays
+    across shards (UNISURF, `render_fn.window_sharded`) needs contiguous slices: it is told its slice
+    and reduces those sums over the ranks itself (one small all-reduce per call)."""
     batched = kw.get('batched', False)
     dim = 1 if batched else 0
     n = rays_o.shape[dim]
-    ro, rd, (lo, hi) = shard_rays(rays_o, rays_d, align=align, dim=dim)
-    if getattr(render_fn, 'window_sharded', False) and batched and world()[1] > 1:
-        kw = dict(kw, shard=(lo, n, group))
-    rgb, depth, extras = render_fn(ro, rd, model, **kw)
-    if not gather:
-        return rgb, depth, extras
-    g = lambda v: gather_rays(v, n, dim=dim, align=align)
+    rank, ws = world()
+    windowed = getattr(render_fn, 'window_sharded', False) and batched and ws > 1
+    if layout == 'cyclic' and not windowed and ws > 1:
+        idx = cyclic_index(n, rank, ws, block).to(rays_o.device)
+        ro, rd = rays_o.index_select(dim, idx), rays_d.index_select(dim, idx)
+        rgb, depth, extras = render_fn(ro, rd, model, **kw)
+        if not gather:
+            return rgb, depth, extras
+        g = lambda v: gather_cyclic(v, n, dim=dim, block=block)
+    else:
+        ro, rd, (lo, hi) = shard_rays(rays_o, rays_d, align=align, dim=dim)
+        if windowed:
+            kw = dict(kw, shard=(lo, n, group))
+        rgb, depth, extras = render_fn(ro, rd, model, **kw)
+        if not gather:
+            return rgb, depth, extras
+        g = lambda v: gather_rays(v, n, dim=dim, align=align)
     rgb_all, depth_all = g(rgb), g(depth)
     out = {}
     for k, v in extras.items():

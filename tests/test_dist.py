@@ -22,16 +22,22 @@ def _fake_render(ro, rd, model, batched=True, **kw):
                         'implicit_surface': ro[..., :1].expand(*ro.shape[:-1], 5).contiguous(), 'scalar': 3}
 
 
-def _worker(rank, ws, port, q, align):
+def _worker(rank, ws, port, q, align, layout='contiguous', block=nd.BLOCK):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=ws)
     try:
         g = torch.Generator().manual_seed(0)
         ro = torch.randn(1, 37, 3, generator=g)
         rd = torch.randn(1, 37, 3, generator=g)
-        rgb, depth, ex = nd.render_sharded(_fake_render, ro, rd, None, batched=True, align=align)
+        seen = []
+        fr = lambda o, d, m, **kw: (seen.append(o.shape[1]), _fake_render(o, d, m, **kw))[1]
+        rgb, depth, ex = nd.render_sharded(fr, ro, rd, None, batched=True, align=align, layout=layout, block=block)
+        if layout == 'cyclic':
+            ok_n = seen == [nd.cyclic_count(37, rank, ws, block)]
+        else:
+            ok_n = True
         ref = _fake_render(ro, rd, None)
-        ok = (torch.equal(rgb, ref[0]) and torch.equal(depth, ref[1]) and
+        ok = (ok_n and torch.equal(rgb, ref[0]) and torch.equal(depth, ref[1]) and
               torch.equal(ex['implicit_surface'], ref[2]['implicit_surface']) and ex['scalar'] == 3)
         lo, hi = nd.shard_bounds(37, rank, ws, align)
         q.put((rank, ok, lo, hi))
@@ -52,7 +58,7 @@ def test_sharded_render_reassembles_world2(align):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, align)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, align, 'contiguous')) for r in range(2)]
     for p in ps:
         p.start()
     res = sorted(q.get(timeout=120) for _ in ps)
@@ -62,6 +68,33 @@ def test_sharded_render_reassembles_world2(align):
     (_, _, lo0, hi0), (_, _, lo1, hi1) = res
     assert lo0 == 0 and hi0 == lo1 and hi1 == 37
     assert hi0 % align == 0
+
+
+@pytest.mark.parametrize('ws,block', [(2, 5), (3, 4), (2, 1024)])
+def test_cyclic_sharded_render_reassembles(ws, block):
+    """block-cyclic shares (the default layout): every rank renders its dealt blocks, the all-gather
+    puts every ray back at its index -- bit-identical to the single-process result"""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, ws, port, q, 1, 'cyclic', block)) for r in range(ws)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _, _ in res), res
+
+
+def test_cyclic_index_partitions():
+    for n in (0, 1, 5, 37, 4096, 4097, 480000):
+        for ws in (1, 2, 3, 8):
+            for block in (1, 5, 1024):
+                parts = [nd.cyclic_index(n, r, ws, block) for r in range(ws)]
+                assert [p.numel() for p in parts] == [nd.cyclic_count(n, r, ws, block) for r in range(ws)]
+                allidx = torch.cat(parts).sort().values if n else torch.empty(0, dtype=torch.int64)
+                assert torch.equal(allidx, torch.arange(n))
+                assert all(bool((p[1:] > p[:-1]).all()) for p in parts if p.numel() > 1)
 
 
 def test_shard_bounds_cover_and_align():
