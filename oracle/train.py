@@ -22,12 +22,16 @@ def nablas_graph(net, x):
 
 def neus_train_losses(sd, rays_o, rays_d, target_rgb, target_mask, w_eikonal=0.1, w_mask=1.0, with_mask=True,
                       d_all=None, speed_factor=10.0, obj_bounding_radius=1.0, N_samples=64, N_importance=64,
-                      N_upsample_iters=4, N_outside=0):
+                      N_upsample_iters=4, N_outside=0, dtype=torch.float32):
     """losses (neus.py:453-478) of one training render of rays [B, N, 3]; d_all [B, N, S] optional
     (the sorted sample depths; computed with the no-grad upsampling when None); N_outside > 0 adds the
-    NeRF++ background (neus.py:303-343, perturb=False) with its parameters in the graph."""
-    o = rays_o.reshape(rays_o.shape[0], -1, 3).float()
-    d = F.normalize(rays_d.reshape(rays_d.shape[0], -1, 3).float(), dim=-1)
+    NeRF++ background (neus.py:303-343, perturb=False) with its parameters in the graph.
+    dtype=torch.float64 (with a float64 state_dict and d_all given): the same function evaluated in
+    float64 on the same inputs -- the truth the fp32 oracle and the GPU are both measured against."""
+    o = rays_o.reshape(rays_o.shape[0], -1, 3).to(dtype)
+    d = F.normalize(rays_d.reshape(rays_d.shape[0], -1, 3).to(dtype), dim=-1)
+    if d_all is not None:
+        d_all = d_all.to(dtype)
     near, far = R.near_far_from_sphere(o, d, r=obj_bounding_radius)
     orc = NeuSOracle({k: v.detach() for k, v in sd.items()}, speed_factor=speed_factor)
     if d_all is None:
@@ -43,14 +47,14 @@ def neus_train_losses(sd, rays_o, rays_d, target_rgb, target_mask, w_eikonal=0.1
     _, n_m, h_m = nablas_graph(sdf_net, pts_mid)                            # neus.py:103-106, :298
     rad = rad_net.forward(pts_mid, d.unsqueeze(-2).expand_as(pts_mid), n_m, h_m)
     if N_outside > 0:                                                       # neus.py:303-343
-        tt = torch.linspace(0, 1, N_outside + 2)[..., 1:-1].float()
+        tt = torch.linspace(0, 1, N_outside + 2)[..., 1:-1].float().to(dtype)
         d_out = torch.cat([d_mid, far / torch.flip(tt, dims=[-1])], -1)
         p_out = o[..., None, :] + d[..., None, :] * d_out[..., :, None]
         r = p_out.norm(dim=-1, keepdim=True)
         x_out = torch.cat([p_out / r, 1. / r], -1)
         sigma_out, rad_out = NeRFNet(sd).forward(x_out, d.unsqueeze(-2).expand_as(x_out[..., :3]))
         dists = d_out[..., 1:] - d_out[..., :-1]
-        dists = torch.cat([dists, 1e10 * torch.ones(dists[..., :1].shape)], -1)
+        dists = torch.cat([dists, 1e10 * torch.ones(dists[..., :1].shape, dtype=dtype)], -1)
         alpha_out = 1 - torch.exp(-F.softplus(sigma_out) * dists)
         n1 = d_mid.shape[-1]
         inside = (pts_mid.norm(dim=-1) <= obj_bounding_radius)
@@ -62,11 +66,13 @@ def neus_train_losses(sd, rays_o, rays_d, target_rgb, target_mask, w_eikonal=0.1
     acc = torch.sum(w, -1)
     nablas_norm = torch.norm(nablas, dim=-1)                                # neus.py:453-478
     mask_volume = torch.clamp(acc, 1e-3, 1 - 1e-3)
+    target_rgb = target_rgb.to(rgb.dtype)
     losses = {'loss_img': F.l1_loss(rgb, target_rgb, reduction='none'),
               'loss_eikonal': w_eikonal * F.mse_loss(nablas_norm, nablas_norm.new_ones(nablas_norm.shape),
                                                      reduction='mean')}
     if with_mask:
-        losses['loss_mask'] = w_mask * F.binary_cross_entropy(mask_volume, target_mask.float(), reduction='mean')
+        losses['loss_mask'] = w_mask * F.binary_cross_entropy(mask_volume, target_mask.to(mask_volume.dtype),
+                                                              reduction='mean')
         losses['loss_img'] = (losses['loss_img'] * target_mask[..., None].float()).sum() / (target_mask.sum() + 1e-10)
     else:
         losses['loss_img'] = losses['loss_img'].mean()

@@ -183,5 +183,10 @@ def test_neus_nerfpp_config_d_frame_vs_oracle(precision):
     # only a flipped sampling decision may take a ray off the bar
     assert (~ray_ok & same).sum() == 0
     assert (~ok_n.all(-1).reshape(-1) & same).sum() == 0
-    # observed (r03): identical samples 83.7 % (fp32) / 84.5 % (f16x3), per-ray pass 99.95 % / 99.85 %
-    assert same.mean() >= 0.8 and ray_ok.mean() >= 0.995
+    # Bar from the reference's own sensitivity (tools/sdf_noise_sensitivity.py, these 2048 rays, 5 noise
+    # seeds, profiles/r04/sdf_noise_sensitivity.txt): the oracle's sampler with absolute SDF noise at
+    # each mode's measured mean |SDF error| vs float64 (fp32 1.2e-7, f16x3 2.0e-7) keeps
+    # identical samples on >= 81.7 % (1e-7) / >= 78.0 % (2e-7) of the rays.  Observed (r03): 83.7 % /
+    # 84.5 %, per-ray pass 99.95 % / 99.85 %.
+    floor = {'fp32': 0.81, 'f16x3': 0.78}[precision]
+    assert same.mean() >= floor and ray_ok.mean() >= 0.995

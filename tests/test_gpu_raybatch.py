@@ -75,11 +75,17 @@ def test_neus_train_step_random_batch_vs_oracle(precision):
     """One NeuS Trainer.forward + backward on a random 512-ray batch of the config-(b) image: the drawn
     pixels replay torch's CPU generator, and the losses and every parameter gradient match the oracle's
     autograd (pinned to the reference's Trainer by test_oracle_train_step_vs_golden) on the same
-    pixels, targets and sample depths.  Bar: losses 1e-5 relative, gradients 1e-4 |ref| + 5e-5 max|ref|
-    per tensor -- the 64-ray golden tests' 1e-5 is too tight for 512 rays: every weight gradient is an
-    fp32 sum over 65 k sample points, and the one element that exceeds 1e-5 (layer-0 weight_g, 2.3e-5
-    of the tensor's largest, identical in fp32 and f16x3 mode, r03) is a cancelling sum whose rounding
-    depends on the summation order."""
+    pixels, targets and sample depths.
+
+    Gradient bar, settled against a float64 truth (the oracle's step evaluated in float64 on the same
+    fp32 inputs, pixels and sample depths): every weight gradient is a sum over 65 k sample points, and
+    the fp32 oracle itself is off that truth by up to a few 1e-5 of the tensor's largest entry.  So
+      (1) element-wise, |gpu - f64| <= |oracle32 - f64| + 1e-5 max|f64|  (the GPU is no further from
+          the truth than the fp32 reference computation, up to 1e-5 of the tensor scale), for every
+          parameter, and
+      (2) the 64-ray golden tests' bar |gpu - oracle32| <= 1e-4 |oracle32| + 1e-5 max|oracle32| for every
+          tensor on which the fp32 oracle itself meets 1e-4 |f64| + 1e-5 max|f64| against the truth.
+    Losses 1e-5 relative."""
     from neurecon_amd.frameworks.neus import Trainer, _sample_depths
     from neurecon_amd import rend_util
     from oracle import rays as orays
@@ -115,26 +121,36 @@ def test_neus_train_step_random_batch_vs_oracle(precision):
                                   'official_solution', 2048, 4)
     d_all = d_all.reshape(1, 512, -1).cpu()
     torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
-    sdp = {k: v.clone().requires_grad_(v.is_floating_point() and k != 'implicit_surface.obj_bounding_size')
-           for k, v in sd.items()}
     ro, rd, _ = orays.get_rays(c2w, K, H, W, select_inds=si)
     t_rgb = torch.gather(tgt_rgb, 1, si[..., None].expand(1, 512, 3))
     t_mask = torch.gather(tgt_mask, 1, si)
-    ref_losses, _ = neus_train_losses(sdp, ro, rd, t_rgb, t_mask, d_all=d_all)
-    ref_losses['total'].backward()
+    ref = {}
+    for dt in (torch.float32, torch.float64):
+        sdp = {k: (v.to(dt) if v.is_floating_point() else v).clone()
+               .requires_grad_(v.is_floating_point() and k != 'implicit_surface.obj_bounding_size') for k, v in sd.items()}
+        rl, _ = neus_train_losses(sdp, ro, rd, t_rgb, t_mask, d_all=d_all, dtype=dt)
+        rl['total'].backward()
+        ref[dt] = (rl, {k: v.grad.double() for k, v in sdp.items() if v.grad is not None})
+    ref_losses, g32 = ref[torch.float32]
+    _, g64 = ref[torch.float64]
     for k in ('loss_img', 'loss_eikonal', 'loss_mask', 'total'):
         a, b = float(losses[k]), float(ref_losses[k])
-        print(f'{precision} {k}: gpu {a:.8f} oracle {b:.8f}')
+        print(f'{precision} {k}: gpu {a:.8f} oracle {b:.8f} f64 {float(ref[torch.float64][0][k]):.10f}')
         assert abs(a - b) <= 1e-5 * abs(b) + 1e-7
-    worst = 0.0
-    for k, v in sdp.items():
-        if v.grad is None:
-            continue
-        ref, mine = v.grad.double(), grads[k].double()
-        scale = float(ref.abs().max()) + 1e-30
-        err = (mine - ref).abs()
-        ok = err <= 1e-4 * ref.abs() + 5e-5 * scale
-        worst = max(worst, float(err.max()) / scale)
-        print(f'{precision} {k}: max err {float(err.max()):.3e} (scale {scale:.3e})')
-        assert bool(ok.all()), (k, float(err.max()), scale)
-    print(f'{precision}: 512-ray batch, worst gradient error / tensor scale {worst:.3e}')
+    worst_gpu, worst_o32, n_tight = 0.0, 0.0, 0
+    for k, t64 in g64.items():
+        mine, o32 = grads[k].double(), g32[k]
+        scale = float(t64.abs().max()) + 1e-30
+        e_gpu, e_o32 = (mine - t64).abs(), (o32 - t64).abs()
+        worst_gpu, worst_o32 = max(worst_gpu, float(e_gpu.max()) / scale), max(worst_o32, float(e_o32.max()) / scale)
+        o32_meets = bool((e_o32 <= 1e-4 * t64.abs() + 1e-5 * scale).all())
+        print(f'{precision} {k}: |gpu-f64| max {float(e_gpu.max()) / scale:.2e}, |oracle32-f64| max '
+              f'{float(e_o32.max()) / scale:.2e} (of the tensor scale {scale:.3e}); oracle32 meets 1e-5: {o32_meets}')
+        assert bool((e_gpu <= e_o32 + 1e-5 * scale).all()), (k, float((e_gpu - e_o32).max()) / scale)
+        if o32_meets:
+            n_tight += 1
+            s32 = float(o32.abs().max()) + 1e-30
+            assert bool(((mine - o32).abs() <= 1e-4 * o32.abs() + 1e-5 * s32).all()), k
+    print(f'{precision}: 512-ray batch, worst |gpu - f64| {worst_gpu:.3e}, worst |oracle32 - f64| {worst_o32:.3e} '
+          f'(of the tensor scale); 1e-5 bar vs the fp32 oracle held on {n_tight} / {len(g64)} tensors '
+          f'(the rest: the fp32 oracle itself misses it against float64)')
