@@ -643,6 +643,39 @@ int nr_radiance_train_pack(const NrRadDesc* d, const float* const* W, const floa
                            void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Weight gradients of the training step (f16x3 MFMA, nr_wgrad.hip): the DenseLayer weight gradients
+ * of models/base.py:118-129 under the double backward (base.py:265-282, train.py:205) -- autograd's
+ * mm(grad_out^T, input) over the sample points -- as
+ *   c[i * ldc + j] = scale * sum_q sum_p a_q[p * lda_q + i] * b_q[p * ldb_q + j]   (i < m, j < n)
+ * for one or two (a, b) pairs (the primal and tangent sweeps of one layer); optional:
+ *   colsum[i] = sum_p a_0[p * lda_0 + i]                  (the bias gradient),
+ *   vec[j]    = vec_scale * sum_p avec[p * ldv] b_0[p * ldb_0 + j]   (one extra output row).
+ * Deterministic (fixed-order slice reduction).  Workspace: nr_wgrad_workspace_bytes(P, m, n, npairs).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  int64_t P;
+  int npairs;
+  const float* a[2];
+  int64_t lda[2];
+  const float* b[2];
+  int64_t ldb[2];
+  int m, n;
+  float scale;
+  float* c;
+  int64_t ldc;
+  float* colsum;      /* [m] or NULL */
+  const float* avec;  /* [P] (stride ldv) or NULL */
+  int64_t ldv;
+  float* vec;         /* [n] or NULL */
+  float vec_scale;
+  void* workspace;
+  size_t workspace_bytes;
+} NrWgrad;
+
+size_t nr_wgrad_workspace_bytes(int64_t P, int m, int n, int npairs);
+int nr_wgrad(const NrWgrad* w, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Opt-in kernel timing (diagnostics / bench roofline).  While enabled, every kernel launch of
  * the library is bracketed by hipEvents on its stream; nr_profile_read() waits for them and
  * returns per-kernel totals (launches, milliseconds, work units: points or rays), then clears.

@@ -119,6 +119,15 @@ class NrTrainGemm(ctypes.Structure):
     ]
 
 
+class NrWgrad(ctypes.Structure):
+    _fields_ = [
+        ('P', _c_i64), ('npairs', _c_i), ('a', _c_p * 2), ('lda', _c_i64 * 2), ('b', _c_p * 2), ('ldb', _c_i64 * 2),
+        ('m', _c_i), ('n', _c_i), ('scale', _c_f), ('c', _c_p), ('ldc', _c_i64), ('colsum', _c_p),
+        ('avec', _c_p), ('ldv', _c_i64), ('vec', _c_p), ('vec_scale', _c_f), ('workspace', _c_p),
+        ('workspace_bytes', _c_sz),
+    ]
+
+
 class NrKernelStat(ctypes.Structure):
     _fields_ = [('name', ctypes.c_char * 32), ('launches', _c_i64), ('ms', ctypes.c_double),
                 ('units', ctypes.c_double)]
@@ -216,6 +225,8 @@ _SIGS = {
     'nr_volsdf_composite_bwd_workspace_bytes': (_c_sz, [_c_i64, _c_i]),
     'nr_volsdf_composite_bwd': (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_i, _c_f, _c_i, _c_p, _c_p, _c_p,
                                        _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
+    'nr_wgrad_workspace_bytes': (_c_sz, [_c_i64, _c_i, _c_i, _c_i]),
+    'nr_wgrad': (_c_i, [ctypes.POINTER(NrWgrad), _c_p]),
     'nr_profile_enable': (_c_i, [_c_i]),
     'nr_profile_filter': (_c_i, [ctypes.c_char_p]),
     'nr_profile_read': (_c_i, [ctypes.POINTER(NrKernelStat), _c_i, ctypes.POINTER(_c_i)]),

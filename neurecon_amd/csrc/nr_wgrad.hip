@@ -1,0 +1,393 @@
+// neurecon_amd -- weight gradients of the training step on MFMA (gfx950): C = scale * sum_q A_q^T B_q.
+//
+// The training step's layer weight gradients (models/base.py:118-129 DenseLayer under the double
+// backward of base.py:265-282 and train.py:205) are products of two tall activation matrices over the
+// sample points: dW_l = zbar_l^T hin_l (+ delta_l^T hdot_in_l for the tangent sweep), A [P, m] and
+// B [P, n] row-major fp32 with P ~ 65 k and m, n <= 289.  The contraction runs over the ROW index of
+// both operands, so each is transposed on its way through LDS:
+//
+//  * grid = S row slices x (m tiles of 256) x (n tiles of 64); a workgroup (8 waves) accumulates its
+//    256 x 64 output tile over its slice, 32 rows (one MFMA k-step) at a time, and writes a partial;
+//    wgrad_reduce sums the S partials in slice order (deterministic) into C.  The n tiles of one slice
+//    run on one XCD back to back (blockIdx -> XCD is round robin), so their shared A rows come from L2.
+//  * k-step: every wave loads its 32 A columns of the 32 rows (4 x 16 B per lane), waves 0-3 the B
+//    block's 16-column groups (2 x 16 B); each wave picks a power-of-two scale for its own group from
+//    the group's max (|v| scale < 2^14), splits v * scale into f16 hi + lo (22 significant bits) and
+//    writes both planes row-major into LDS (row strides 544 / 288 B: the 8 rows a 32-lane half reads
+//    land 8 banks apart).  Double-buffered: the next k-step's global loads are in flight during this
+//    k-step's MFMAs; one barrier per k-step.
+//  * MFMA operands come back with ds_read_b64_tr_b16 (4 rows x 16 columns, delivered column-major):
+//    lane group G of a 16x16x32 operand takes rows {4G..4G+3} and {16+4G..16+4G+3}, the same rows for
+//    A and B, so each k-slot pairs the same point.  Per 16x16 tile and k-step: t = Ah Bh + Ah Bl + Al Bh
+//    (fresh accumulator), then C_tile += t * 2^-(eA + eB) (the two groups' scales; exact).
+//  * optional: column sums of A_0 (the bias gradient) and B_0^T v for a [P] vector v (the sdf row of
+//    the output layer, dW8[0, :]) accumulated in fp32 from the loaded values, reduced in fixed order.
+#include <algorithm>
+#include "nr_common.h"
+
+namespace nr {
+
+constexpr int kWgThreads = 512;   // 8 waves: wave w owns output rows [32 w, 32 w + 32) of the m tile
+constexpr int kWgM = 256, kWgN = 64, kWgK = 32;
+constexpr int kAStride = 272;     // halfs per A row in LDS (544 B)
+constexpr int kBStride = 144;     // halfs per B row (288 B)
+constexpr int kAPlane = kWgK * kAStride;
+constexpr int kBPlane = kWgK * kBStride;
+constexpr int kStage = 2 * kAPlane + 2 * kBPlane;  // halfs: A hi, A lo, B hi, B lo
+
+struct WgKArgs {
+  const float* a[2];
+  int64_t lda[2];
+  const float* b[2];
+  int64_t ldb[2];
+  int npairs;
+  int64_t P;
+  int m, n;
+  int nmt, nnt, S;
+  int64_t KP;        // 32-row steps per pair: ceil(P / 32)
+  float* part;       // [S][nnt * 64][nmt * 256]
+  float* part_cs;    // [S][nmt * 256] column sums of A_0 (nullptr: none)
+  const float* avec; // [P] at avec[p * ldv] (nullptr: none)
+  int64_t ldv;
+  float* part_vec;   // [S][nnt * 64]
+};
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+using lds_v4s = __attribute__((address_space(3))) v4s;
+
+__device__ __forceinline__ v4s tr16(const _Float16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)((__attribute__((address_space(3))) _Float16*)p));
+}
+
+__device__ __forceinline__ f16x8 frag(const _Float16* plane, int stride, int col, int lane) {
+  // rows {4G + q} and {16 + 4G + q} of the 16-column block starting at `col` (T10 addressing: lane
+  // 4q + p' of its 16-lane group supplies row q's columns 4p' .. 4p' + 3)
+  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const v4s lo = tr16(plane + (4 * G + q) * stride + col + 4 * p);
+  const v4s hi = tr16(plane + (16 + 4 * G + q) * stride + col + 4 * p);
+  const short s[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  f16x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = __builtin_bit_cast(_Float16, s[e]);
+  return r;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// power-of-two exponent e with M * 2^e < 2^14 (0 for M = 0 / inf / NaN)
+__device__ __forceinline__ int split_exp(float M) {
+  if (!(M > 0.0f) || __builtin_isinf(M)) return 0;
+  return 14 - __builtin_amdgcn_frexp_expf(M);
+}
+
+// v * 2^e -> (hi, lo) f16 pairs, 4 values: 8 B each plane
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split4(float4 v, float sc, uint2& h, uint2& l) {
+  const float x[4] = {v.x * sc, v.y * sc, v.z * sc, v.w * sc};
+  _Float16 hh[4], ll[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    hh[e] = (_Float16)x[e];
+    ll[e] = (_Float16)(x[e] - (float)hh[e]);
+  }
+  h = make_uint2(__builtin_bit_cast(uint32_t, h2{hh[0], hh[1]}), __builtin_bit_cast(uint32_t, h2{hh[2], hh[3]}));
+  l = make_uint2(__builtin_bit_cast(uint32_t, h2{ll[0], ll[1]}), __builtin_bit_cast(uint32_t, h2{ll[2], ll[3]}));
+}
+
+template <bool VEC>
+__device__ __forceinline__ float4 ld4(const float* base, int64_t ld, int64_t r, int c, int64_t P, int ncol) {
+  if (r >= P || c >= ncol) return make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* p = base + r * ld + c;
+  if (VEC && c + 3 < ncol) return *(const float4*)p;
+  return make_float4(p[0], c + 1 < ncol ? p[1] : 0.f, c + 2 < ncol ? p[2] : 0.f, c + 3 < ncol ? p[3] : 0.f);
+}
+
+__device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+__device__ __forceinline__ float4 fma4(float s, float4 b, float4 c) {
+  return make_float4(fmaf(s, b.x, c.x), fmaf(s, b.y, c.y), fmaf(s, b.z, c.z), fmaf(s, b.w, c.w));
+}
+__device__ __forceinline__ float4 shfl_xor4(float4 v, int o) {
+  return make_float4(__shfl_xor(v.x, o), __shfl_xor(v.y, o), __shfl_xor(v.z, o), __shfl_xor(v.w, o));
+}
+
+template <bool VA, bool VB>
+__global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * kStage];
+  __shared__ float s_inv[2][12];  // per stage: 2^-e of the 8 A groups, then the 4 B groups
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int NT = a.nmt * a.nnt;
+  // block -> (slice, m tile, n tile): with S % 8 == 0 the tiles of one slice share an XCD
+  int slice, t;
+  if (a.S % 8 == 0) {
+    const int xcd = blockIdx.x & 7, seq = blockIdx.x >> 3;
+    slice = (seq / NT) * 8 + xcd;
+    t = seq % NT;
+  } else {
+    slice = blockIdx.x / NT;
+    t = blockIdx.x % NT;
+  }
+  if (slice >= a.S) return;
+  const int mt = t / a.nnt, nt = t % a.nnt;
+  const int m0 = mt * kWgM, n0 = nt * kWgN;
+  const int mloc = min(kWgM, a.m - m0);
+  const bool wvalid = 32 * w < mloc;                   // wave-uniform: this wave has output rows
+  const int64_t KS = a.npairs * a.KP;
+  const int64_t k0 = KS * slice / a.S, k1 = KS * (slice + 1) / a.S;
+
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 cs = make_float4(0.f, 0.f, 0.f, 0.f), vs = make_float4(0.f, 0.f, 0.f, 0.f);
+  const bool want_cs = a.part_cs && nt == 0, want_vec = a.avec && mt == 0;
+
+  // loader geometry: A (all waves) lane -> column quad (lane & 7), rows (lane >> 3) + 8 j;
+  // B (waves 0-3) lane -> column quad (lane & 3), rows (lane >> 2) + 16 j
+  const int ac = 32 * w + 4 * (lane & 7), ar = lane >> 3;
+  const int bc = 16 * w + 4 * (lane & 3), br = lane >> 2;
+  float4 va[4], vb[2];
+  float vv[2];
+  auto load = [&](int64_t ks) {
+    const int q = (int)(ks / a.KP);
+    const int64_t r0 = (ks % a.KP) * kWgK;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      va[j] = wvalid ? ld4<VA>(a.a[q], a.lda[q], r0 + ar + 8 * j, m0 + ac, a.P, a.m) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (w < 4) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int64_t r = r0 + br + 16 * j;
+        vb[j] = ld4<VB>(a.b[q], a.ldb[q], r, n0 + bc, a.P, a.n);
+        vv[j] = (want_vec && q == 0 && r < a.P) ? a.avec[r * a.ldv] : 0.0f;
+      }
+    }
+    return q;
+  };
+  auto store = [&](int stg, int q) {
+    _Float16* S0 = lds + stg * kStage;
+    if (want_cs && q == 0) cs = add4(cs, add4(add4(va[0], va[1]), add4(va[2], va[3])));
+    float m = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m = fmaxf(m, fmaxf(fmaxf(fabsf(va[j].x), fabsf(va[j].y)), fmaxf(fabsf(va[j].z), fabsf(va[j].w))));
+    const int ea = split_exp(wave_max(m));
+    const float sa = __builtin_ldexpf(1.0f, ea);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint2 h, l;
+      split4(va[j], sa, h, l);
+      const int o = (ar + 8 * j) * kAStride + ac;
+      *(uint2*)(S0 + o) = h;
+      *(uint2*)(S0 + kAPlane + o) = l;
+    }
+    if (lane == 0) s_inv[stg][w] = __builtin_ldexpf(1.0f, -ea);
+    if (w < 4) {
+      if (want_vec && q == 0) vs = fma4(vv[1], vb[1], fma4(vv[0], vb[0], vs));
+      float mb = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        mb = fmaxf(mb, fmaxf(fmaxf(fabsf(vb[j].x), fabsf(vb[j].y)), fmaxf(fabsf(vb[j].z), fabsf(vb[j].w))));
+      const int eb = split_exp(wave_max(mb));
+      const float sb = __builtin_ldexpf(1.0f, eb);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        uint2 h, l;
+        split4(vb[j], sb, h, l);
+        const int o = (br + 16 * j) * kBStride + bc;
+        *(uint2*)(S0 + 2 * kAPlane + o) = h;
+        *(uint2*)(S0 + 2 * kAPlane + kBPlane + o) = l;
+      }
+      if (lane == 0) s_inv[stg][8 + w] = __builtin_ldexpf(1.0f, -eb);
+    }
+  };
+
+  int stg = 0;
+  if (k0 < k1) {
+    const int q = load(k0);
+    store(0, q);
+  }
+  __syncthreads();
+  for (int64_t ks = k0; ks < k1; ++ks) {
+    const bool more = ks + 1 < k1;
+    int qn = 0;
+    if (more) qn = load(ks + 1);  // in flight during this k-step's MFMAs
+    if (wvalid) {
+      const _Float16* S0 = lds + stg * kStage;
+      f16x8 ah[2], al[2], bh[4], bl[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        ah[i] = frag(S0, kAStride, 32 * w + 16 * i, lane);
+        al[i] = frag(S0 + kAPlane, kAStride, 32 * w + 16 * i, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bh[j] = frag(S0 + 2 * kAPlane, kBStride, 16 * j, lane);
+        bl[j] = frag(S0 + 2 * kAPlane + kBPlane, kBStride, 16 * j, lane);
+      }
+      const float ia = s_inv[stg][w];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f32x4 tt = f32x4{0.f, 0.f, 0.f, 0.f};
+          tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], tt, 0, 0, 0);
+          tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], tt, 0, 0, 0);
+          tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], tt, 0, 0, 0);
+          const float f = ia * s_inv[stg][8 + j];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = fmaf(tt[r], f, acc[i][j][r]);
+        }
+    }
+    if (more) store(stg ^ 1, qn);
+    __syncthreads();
+    stg ^= 1;
+  }
+
+  // partial tile: lane (G, col) register r holds row 4G + r of each 16 x 16 tile -> part[s][n][m]
+  const int64_t ldp = (int64_t)a.nmt * kWgM;
+  float* P0 = a.part + (int64_t)slice * (a.nnt * kWgN) * ldp;
+  if (wvalid) {
+    const int G = lane >> 4, col = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t nn = n0 + 16 * j + col, mm = m0 + 32 * w + 16 * i + 4 * G;
+        *(float4*)(P0 + nn * ldp + mm) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+  } else {
+    const int G = lane >> 4, col = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t nn = n0 + 16 * j + col, mm = m0 + 32 * w + 16 * i + 4 * G;
+        *(float4*)(P0 + nn * ldp + mm) = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+  }
+  if (want_cs) {  // lanes with equal (lane & 7) hold the same columns: fixed-order butterfly
+    cs = add4(cs, shfl_xor4(cs, 8));
+    cs = add4(cs, shfl_xor4(cs, 16));
+    cs = add4(cs, shfl_xor4(cs, 32));
+    if (lane < 8) *(float4*)(a.part_cs + (int64_t)slice * ldp + m0 + ac) = cs;
+  }
+  if (want_vec && w < 4) {
+    vs = add4(vs, shfl_xor4(vs, 4));
+    vs = add4(vs, shfl_xor4(vs, 8));
+    vs = add4(vs, shfl_xor4(vs, 16));
+    vs = add4(vs, shfl_xor4(vs, 32));
+    if (lane < 4) *(float4*)(a.part_vec + (int64_t)slice * (a.nnt * kWgN) + n0 + bc) = vs;
+  }
+}
+
+// C[i, j] = scale * sum_s part[s][j][i] (i < m, j < n), slices in order; column sums and the vector
+// product likewise
+__global__ void wgrad_reduce(const float* __restrict__ part, int S, int m, int n, int64_t ldp, int64_t ldn, float scale,
+                             float* __restrict__ c, int64_t ldc, const float* __restrict__ part_cs, float* cs,
+                             const float* __restrict__ part_vec, float* vec, float vscale) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)m * n;
+  if (idx < total) {
+    const int64_t j = idx / m, i = idx % m;
+    float s = 0.0f;
+    for (int k = 0; k < S; ++k) s += part[(int64_t)k * ldn * ldp + j * ldp + i];
+    c[i * ldc + j] = s * scale;
+  }
+  if (cs && idx < m) {
+    float s = 0.0f;
+    for (int k = 0; k < S; ++k) s += part_cs[(int64_t)k * ldp + idx];
+    cs[idx] = s;
+  }
+  if (vec && idx < n) {
+    float s = 0.0f;
+    for (int k = 0; k < S; ++k) s += part_vec[(int64_t)k * ldn + idx];
+    vec[idx] = s * vscale;
+  }
+}
+
+struct WgPlan {
+  int nmt, nnt, S;
+  int64_t KP;
+  size_t part_bytes, cs_bytes, vec_bytes;
+};
+
+static WgPlan wgrad_plan(int64_t P, int m, int n, int npairs) {
+  WgPlan p{};
+  p.nmt = (m + kWgM - 1) / kWgM;
+  p.nnt = (n + kWgN - 1) / kWgN;
+  p.KP = (P + kWgK - 1) / kWgK;
+  const int64_t KS = std::max<int64_t>(1, npairs * p.KP);
+  // about one workgroup per CU (256), in whole groups of 8 slices (the XCD mapping), >= 1 k-step each
+  int S = (int)std::max<int64_t>(1, 256 / (p.nmt * p.nnt));
+  S = S >= 8 ? S / 8 * 8 : S;
+  if (S > KS) S = (int)KS;
+  p.S = std::max(S, 1);
+  p.part_bytes = (size_t)p.S * p.nnt * kWgN * p.nmt * kWgM * 4;
+  p.cs_bytes = (size_t)p.S * p.nmt * kWgM * 4;
+  p.vec_bytes = (size_t)p.S * p.nnt * kWgN * 4;
+  return p;
+}
+
+}  // namespace nr
+
+using namespace nr;
+
+extern "C" {
+
+size_t nr_wgrad_workspace_bytes(int64_t P, int m, int n, int npairs) {
+  const WgPlan p = wgrad_plan(P, m, n, npairs);
+  return p.part_bytes + p.cs_bytes + p.vec_bytes + 768;
+}
+
+int nr_wgrad(const NrWgrad* w, void* stream) {
+  NR_REQUIRE(w, NR_ERR_ARG, "nr_wgrad: null args");
+  NR_REQUIRE(w->npairs == 1 || w->npairs == 2, NR_ERR_ARG, "nr_wgrad: npairs must be 1 or 2");
+  NR_REQUIRE(w->m > 0 && w->n > 0 && w->P >= 0, NR_ERR_ARG, "nr_wgrad: bad shape");
+  NR_REQUIRE(w->c && w->ldc >= w->n, NR_ERR_ARG, "nr_wgrad: null output or ldc < n");
+  for (int q = 0; q < w->npairs; ++q)
+    NR_REQUIRE(w->a[q] && w->b[q] && w->lda[q] >= w->m && w->ldb[q] >= w->n, NR_ERR_ARG,
+               "nr_wgrad: null operand or leading dimension below its column count");
+  NR_REQUIRE(!w->vec || w->avec, NR_ERR_ARG, "nr_wgrad: vec output without avec");
+  const WgPlan p = wgrad_plan(w->P, w->m, w->n, w->npairs);
+  NR_REQUIRE(w->workspace && w->workspace_bytes >= p.part_bytes + p.cs_bytes + p.vec_bytes, NR_ERR_WORKSPACE,
+             "nr_wgrad: workspace too small (nr_wgrad_workspace_bytes)");
+  hipStream_t st = (hipStream_t)stream;
+  char* ws = (char*)w->workspace;
+  WgKArgs k{};
+  bool va = true, vb = true;
+  for (int q = 0; q < w->npairs; ++q) {
+    k.a[q] = w->a[q]; k.lda[q] = w->lda[q];
+    k.b[q] = w->b[q]; k.ldb[q] = w->ldb[q];
+    va = va && w->lda[q] % 4 == 0 && ((uintptr_t)w->a[q] & 15) == 0;
+    vb = vb && w->ldb[q] % 4 == 0 && ((uintptr_t)w->b[q] & 15) == 0;
+  }
+  k.npairs = w->npairs; k.P = w->P; k.m = w->m; k.n = w->n;
+  k.nmt = p.nmt; k.nnt = p.nnt; k.S = p.S; k.KP = p.KP;
+  k.part = (float*)ws;
+  k.part_cs = w->colsum ? (float*)(ws + p.part_bytes) : nullptr;
+  k.avec = w->vec ? w->avec : nullptr;
+  k.ldv = w->ldv > 0 ? w->ldv : 1;
+  k.part_vec = w->vec ? (float*)(ws + p.part_bytes + p.cs_bytes) : nullptr;
+  {
+    ProfScope prof("wgrad", (double)w->npairs * w->P * w->m * w->n, st);
+    const dim3 grid((unsigned)(p.S * p.nmt * p.nnt));
+    // S % 8 == 0 needs the grid padded to whole XCD rounds of the mapping (it already is: S * NT)
+    if (va && vb) hipLaunchKernelGGL((wgrad_kernel<true, true>), grid, dim3(kWgThreads), 0, st, k);
+    else if (va) hipLaunchKernelGGL((wgrad_kernel<true, false>), grid, dim3(kWgThreads), 0, st, k);
+    else if (vb) hipLaunchKernelGGL((wgrad_kernel<false, true>), grid, dim3(kWgThreads), 0, st, k);
+    else hipLaunchKernelGGL((wgrad_kernel<false, false>), grid, dim3(kWgThreads), 0, st, k);
+    NR_HIP_CHECK(hipGetLastError());
+  }
+  const int64_t ldp = (int64_t)p.nmt * kWgM, ldn = (int64_t)p.nnt * kWgN;
+  const int64_t total = std::max<int64_t>({(int64_t)w->m * w->n, (int64_t)w->m, (int64_t)w->n});
+  hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, k.part, p.S, w->m, w->n,
+                     ldp, ldn, w->scale, w->c, w->ldc, k.part_cs, w->colsum, k.part_vec, w->vec, w->vec_scale);
+  NR_HIP_CHECK(hipGetLastError());
+  return NR_OK;
+}
+
+}  // extern "C"

@@ -91,6 +91,36 @@ def _wgrad2(g1, h1, g2, h2):
     return buf.sum(0)
 
 
+def _wg(pairs, out=None, scale=1.0, colsum=None, avec=None, vec=None):
+    """sum_q a_q^T b_q on the hand-written MFMA weight-gradient kernel (nr_wgrad, f16x3): pairs of
+    row-major views a [P, m], b [P, n] (unit column stride; any row stride); out [m, n] (a view with
+    unit column stride, e.g. a column range of the gradient) = scale * the sum.  colsum: [m] <- the
+    column sums of a_0 (the bias gradient); avec [P] / vec [n]: vec <- avec^T b_0 (an extra row)."""
+    a0, b0 = pairs[0]
+    P, m = a0.shape
+    n = b0.shape[1]
+    dev = a0.device
+    if out is None:
+        out = torch.empty(m, n, device=dev)
+    w = L.NrWgrad()
+    w.P, w.npairs, w.m, w.n, w.scale = P, len(pairs), m, n, float(scale)
+    for q, (a, b) in enumerate(pairs):
+        assert a.shape == (P, m) and b.shape == (P, n) and a.stride(1) == 1 and b.stride(1) == 1
+        w.a[q], w.lda[q], w.b[q], w.ldb[q] = a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0)
+    assert out.shape == (m, n) and out.stride(1) == 1
+    w.c, w.ldc = out.data_ptr(), out.stride(0)
+    if colsum is not None:
+        w.colsum = colsum.data_ptr()
+    if avec is not None:
+        w.avec, w.ldv, w.vec, w.vec_scale = avec.data_ptr(), avec.stride(0), vec.data_ptr(), 1.0
+    lib = L.lib()
+    nb = lib.nr_wgrad_workspace_bytes(P, m, n, len(pairs))
+    ws = L.workspace(dev, nb)
+    w.workspace, w.workspace_bytes = ws.data_ptr(), nb
+    L.check(lib.nr_wgrad(ctypes.byref(w), _st(a0)))
+    return out
+
+
 def _colsum(a):
     """a.sum(0) of a tall [P, n] gradient on the deterministic two-pass HIP reduction (nr_colsum): the
     generic column reduction took ~0.45 ms per [65536, 256] matrix, rocBLAS's GEMV ~1 ms"""
@@ -758,26 +788,36 @@ class SdfNablaTG(torch.autograd.Function):
             gz = dict(g=G[l - 1], ldg=wd[l - 1], zd=ZD[l - 1], ldzd=wd[l - 1]) if tangent else {}
             _tg(op(i), P, shp(i, 0, 4 if l == 4 else 0), L.TG_SPADJ, Z[l], wd[l], nv[l], Z[l - 1], wd[l - 1],
                 a=S[l - 1], lda=wd[l - 1], stream=st, **gz)
-        # weight gradients (hipBLASLt): dW_l = zbar_l^T hin_l + delta_l^T hdot_in_l, db_l = sum_p zbar_l
+        # weight gradients on nr_wgrad (f16x3 MFMA): dW_l = zbar_l^T hin_l + delta_l^T hdot_in_l (one
+        # launch for both sweeps), db_l = sum_p zbar_l fused into it
         dW, db = [None] * (D + 1), [None] * (D + 1)
-        ob = torch.cat([gs[:, None], gf], 1)
-        dW[D] = _wgrad(ob, H[7])
-        db[D] = _colsum(ob)
+        dW[D] = torch.empty(257, 256, device=dev)  # rows [d sdf ; d feature] x h7
+        db[D] = torch.empty(257, device=dev)
+        if g_feat is not None:
+            _wg([(gf, H[7])], out=dW[D][1:], colsum=db[D][1:], avec=gs, vec=dW[D][0])
+        else:  # no feature gradient: only the sdf row
+            dW[D][1:].zero_()
+            db[D][1:].zero_()
+            _wg([(gs[:, None], H[7])], out=dW[D][:1])
+        db[D][:1] = _colsum(gs[:, None])
         if tangent:
             dW[D][0] += _colsum(HD[7])
         for l in range(D):
             zb = Z[l][:, :nv[l]]
+            db[l] = torch.empty(nv[l], device=dev)
             if l == 0:
-                dW[0] = _wgrad2(zb, h0[:, :nf], delta[0], hd0[:, :nf]) if tangent else _wgrad(zb, h0[:, :nf])
+                pr = [(zb, h0[:, :nf])] + ([(delta[0][:, :nv[0]], hd0[:, :nf])] if tangent else [])
+                dW[0] = _wg(pr, colsum=db[0])
             elif l == 4:  # the skip layer's input cat([h3, embed(x)]) / sqrt(2) (base.py:250): per column block
-                parts = [(H[3][:, :217], HD[3][:, :217] if tangent else None), (h0[:, :nf], hd0[:, :nf] if tangent else None)]
-                dW[4] = torch.cat([_wgrad2(zb, a, delta[4], b) if tangent else _wgrad(zb, a) for a, b in parts],
-                                  1).mul_(_ISQ2)
+                dW[4] = torch.empty(256, 217 + nf, device=dev)
+                _wg([(zb, H[3][:, :217])] + ([(delta[4][:, :nv[4]], HD[3][:, :217])] if tangent else []),
+                    out=dW[4][:, :217], scale=_ISQ2, colsum=db[4])
+                _wg([(zb, h0[:, :nf])] + ([(delta[4][:, :nv[4]], hd0[:, :nf])] if tangent else []),
+                    out=dW[4][:, 217:], scale=_ISQ2)
             else:
                 hin = H[l - 1][:, :nv[l - 1]]
-                dW[l] = (_wgrad2(zb, hin, delta[l][:, :nv[l]], HD[l - 1][:, :nv[l - 1]]) if tangent
-                         else _wgrad(zb, hin))
-            db[l] = _colsum(Z[l])[:nv[l]]  # the padded buffer's columns sum independently: no copy of the view
+                pr = [(zb, hin)] + ([(delta[l][:, :nv[l]], HD[l - 1][:, :nv[l - 1]])] if tangent else [])
+                dW[l] = _wg(pr, colsum=db[l])
         return (None, None, None, *dW, *db)
 
 
@@ -831,16 +871,19 @@ class RadianceTG(torch.autograd.Function):
         g = gy.contiguous().clone()
         L.check(L.lib().nr_activation(L.ptr(rgb), L.ptr(g), g.numel(), 3, st))  # sigmoid'
         dW, db = [None] * 5, [None] * 5
-        dW[4], db[4] = _wgrad(g, H[3]), _colsum(g)
+        db[4] = torch.empty(3, device=dev)
+        dW[4] = _wg([(g, H[3])], colsum=db[4])      # weight gradients on nr_wgrad (bias gradient fused)
         gz = torch.empty(P, 256, device=dev)
         _tg(tb + info[5][0], P, (2, 0, 16, 0), L.TG_RELUMASK, g, 3, 3, gz, 256, bias=False, a=H[3], lda=256, stream=st)
         for l in range(3, 0, -1):  # gz = d z_l  ->  d z_{l-1} through W_l^T (training ops 6, 7, 8)
-            dW[l], db[l] = _wgrad(gz, H[l - 1]), _colsum(gz)
+            db[l] = torch.empty(256, device=dev)
+            dW[l] = _wg([(gz, H[l - 1])], colsum=db[l])
             gn = torch.empty(P, 256, device=dev)
             _tg(tb + info[5 + (4 - l)][0], P, (16, 0, 16, 0), L.TG_RELUMASK, gz, 256, 256, gn, 256, bias=False,
                 a=H[l - 1], lda=256, stream=st)
             gz = gn
-        dW[0], db[0] = _wgrad(gz, inp), _colsum(gz)  # W0 columns [small | feature], as inp
+        db[0] = torch.empty(256, device=dev)
+        dW[0] = _wg([(gz, inp)], colsum=db[0])  # W0 columns [small | feature], as inp
         nbo0 = info[9][2]
         d_feat = torch.empty(P, 256, device=dev)
         d_small = torch.empty(P, 16 * (nbo0 - 16), device=dev)
