@@ -78,12 +78,35 @@ def up_to_date():
     return lib_build_id() == source_hash()
 
 
+ID_SOURCE = 'nr_capi.hip'  # the one object that carries the build ID (nr_build_id)
+
+
+def _obj_key(src, build_id):
+    """what an object depends on: its source, every header, its flags (and the ID for ID_SOURCE)"""
+    h = hashlib.sha256()
+    for p in [src] + sorted(glob.glob(os.path.join(CSRC, '*.h')) + glob.glob(os.path.join(INC, '*.h'))):
+        with open(p, 'rb') as f:
+            h.update(os.path.basename(p).encode() + b'\0' + f.read())
+    h.update(repr([f for f in flags_for(src) if f not in (CSRC, INC)] + [HIPCC]).encode())
+    if os.path.basename(src) == ID_SOURCE:
+        h.update(build_id.encode())
+    return h.hexdigest()
+
+
 def _compile(src, build_id):
+    """compile one source unless its object was built from the same inputs (sidecar key file)"""
     obj = os.path.join(OUT, os.path.basename(src) + '.o')
-    cmd = [HIPCC] + flags_for(src) + [f'-DNR_BUILD_ID="{build_id}"', '-c', src, '-o', obj]
+    key = _obj_key(src, build_id)
+    kfile = obj + '.key'
+    if os.path.exists(obj) and os.path.exists(kfile) and open(kfile).read() == key:
+        return obj, ''
+    defs = [f'-DNR_BUILD_ID="{build_id}"'] if os.path.basename(src) == ID_SOURCE else []
+    cmd = [HIPCC] + flags_for(src) + defs + ['-c', src, '-o', obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f'hipcc failed for {src}:\n{r.stderr}')
+    with open(kfile, 'w') as f:
+        f.write(key)
     return obj, r.stderr
 
 

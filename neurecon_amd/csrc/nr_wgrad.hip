@@ -6,20 +6,21 @@
 // B [P, n] row-major fp32 with P ~ 65 k and m, n <= 289.  The contraction runs over the ROW index of
 // both operands, so each is transposed on its way through LDS:
 //
-//  * grid = S row slices x (m tiles of 256) x (n tiles of 64); a workgroup (8 waves) accumulates its
-//    256 x 64 output tile over its slice, 32 rows (one MFMA k-step) at a time, and writes a partial;
+//  * grid = S row slices x (m tiles of 256) x (n tiles of 128); a workgroup (8 waves) accumulates its
+//    256 x 128 output tile over its slice, 32 rows (one MFMA k-step) at a time, and writes a partial;
 //    wgrad_reduce sums the S partials in slice order (deterministic) into C.  The n tiles of one slice
 //    run on one XCD back to back (blockIdx -> XCD is round robin), so their shared A rows come from L2.
-//  * k-step: every wave loads its 32 A columns of the 32 rows (4 x 16 B per lane), waves 0-3 the B
-//    block's 16-column groups (2 x 16 B); each wave picks a power-of-two scale for its own group from
-//    the group's max (|v| scale < 2^14), splits v * scale into f16 hi + lo (22 significant bits) and
-//    writes both planes row-major into LDS (row strides 544 / 288 B: the 8 rows a 32-lane half reads
-//    land 8 banks apart).  Double-buffered: the next k-step's global loads are in flight during this
-//    k-step's MFMAs; one barrier per k-step.
+//  * k-step: every wave loads 32 A columns of the 32 rows (4 x 16 B per lane) and 16 B columns
+//    (2 x 16 B); per column quad (4 columns x 32 rows) a power-of-two scale from the quad's max
+//    (|v| scale < 2^14; three / four ds_swizzle + permlane32 steps), v * scale split into f16 hi + lo
+//    (22 significant bits), both planes written row-major into LDS (row strides 544 / 288 B: the 8
+//    rows a 32-lane half reads land 8 banks apart).  Two k-steps of global loads are in flight in
+//    registers while a k-step's MFMAs run from LDS (double-buffered stages, one barrier per k-step).
 //  * MFMA operands come back with ds_read_b64_tr_b16 (4 rows x 16 columns, delivered column-major):
 //    lane group G of a 16x16x32 operand takes rows {4G..4G+3} and {16+4G..16+4G+3}, the same rows for
-//    A and B, so each k-slot pairs the same point.  Per 16x16 tile and k-step: t = Ah Bh + Ah Bl + Al Bh
-//    (fresh accumulator), then C_tile += t * 2^-(eA + eB) (the two groups' scales; exact).
+//    A and B, so each k-slot pairs the same point.  Per 16x16 tile and k-step: t = Al Bh + Ah Bl + Ah Bh
+//    (fresh accumulator), then C += t * 2^-(eA + eB): a lane's 4 output rows are one A quad and its
+//    column one B quad, so one factor per lane and tile (exact).
 //  * optional: column sums of A_0 (the bias gradient) and B_0^T v for a [P] vector v (the sdf row of
 //    the output layer, dW8[0, :]) accumulated in fp32 from the loaded values, reduced in fixed order.
 #include <algorithm>
@@ -28,9 +29,9 @@
 namespace nr {
 
 constexpr int kWgThreads = 512;   // 8 waves: wave w owns output rows [32 w, 32 w + 32) of the m tile
-constexpr int kWgM = 256, kWgN = 64, kWgK = 32;
-constexpr int kAStride = 272;     // halfs per A row in LDS (544 B)
-constexpr int kBStride = 144;     // halfs per B row (288 B)
+constexpr int kWgM = 256, kWgN = 128, kWgK = 32;
+constexpr int kAStride = 272;     // halfs per A row in LDS (544 B: 8 rows of a half-wave read land 8 banks apart)
+constexpr int kBStride = 144;     // halfs per B row (288 B, the same property)
 constexpr int kAPlane = kWgK * kAStride;
 constexpr int kBPlane = kWgK * kBStride;
 constexpr int kStage = 2 * kAPlane + 2 * kBPlane;  // halfs: A hi, A lo, B hi, B lo
@@ -45,11 +46,11 @@ struct WgKArgs {
   int m, n;
   int nmt, nnt, S;
   int64_t KP;        // 32-row steps per pair: ceil(P / 32)
-  float* part;       // [S][nnt * 64][nmt * 256]
+  float* part;       // [S][nnt * 128][nmt * 256]
   float* part_cs;    // [S][nmt * 256] column sums of A_0 (nullptr: none)
   const float* avec; // [P] at avec[p * ldv] (nullptr: none)
   int64_t ldv;
-  float* part_vec;   // [S][nnt * 64]
+  float* part_vec;   // [S][nnt * 128]
 };
 
 typedef short v4s __attribute__((ext_vector_type(4)));
@@ -72,10 +73,14 @@ __device__ __forceinline__ f16x8 frag(const _Float16* plane, int stride, int col
   return r;
 }
 
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
+// max over lanes l ^ 8, l ^ 16, l ^ 32 (and l ^ 4 with FOUR): ds_swizzle within 32 lanes, then the halves
+template <bool FOUR>
+__device__ __forceinline__ float quad_max(float v) {
+  if constexpr (FOUR) v = fmaxf(v, __uint_as_float(__builtin_amdgcn_ds_swizzle(__float_as_uint(v), 0x101F)));
+  v = fmaxf(v, __uint_as_float(__builtin_amdgcn_ds_swizzle(__float_as_uint(v), 0x201F)));
+  v = fmaxf(v, __uint_as_float(__builtin_amdgcn_ds_swizzle(__float_as_uint(v), 0x401F)));
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
 // power-of-two exponent e with M * 2^e < 2^14 (0 for M = 0 / inf / NaN)
@@ -102,7 +107,10 @@ template <bool VEC>
 __device__ __forceinline__ float4 ld4(const float* base, int64_t ld, int64_t r, int c, int64_t P, int ncol) {
   if (r >= P || c >= ncol) return make_float4(0.f, 0.f, 0.f, 0.f);
   const float* p = base + r * ld + c;
-  if (VEC && c + 3 < ncol) return *(const float4*)p;
+  if (VEC && c + 3 < ncol) {  // streamed once from HBM: non-temporal
+    const f32x4 v = __builtin_nontemporal_load((const f32x4*)p);
+    return make_float4(v[0], v[1], v[2], v[3]);
+  }
   return make_float4(p[0], c + 1 < ncol ? p[1] : 0.f, c + 2 < ncol ? p[2] : 0.f, c + 3 < ncol ? p[3] : 0.f);
 }
 
@@ -113,11 +121,21 @@ __device__ __forceinline__ float4 fma4(float s, float4 b, float4 c) {
 __device__ __forceinline__ float4 shfl_xor4(float4 v, int o) {
   return make_float4(__shfl_xor(v.x, o), __shfl_xor(v.y, o), __shfl_xor(v.z, o), __shfl_xor(v.w, o));
 }
+__device__ __forceinline__ float amax4(float4 v) {
+  return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
+
+// one k-step's operands in registers: A rows (lane >> 3) + 8 j, B rows (lane >> 2) + 16 j
+struct WgRegs {
+  float4 va[4], vb[2];
+  float vv[2];
+  int q;
+};
 
 template <bool VA, bool VB>
 __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * kStage];
-  __shared__ float s_inv[2][12];  // per stage: 2^-e of the 8 A groups, then the 4 B groups
+  __shared__ float s_inv[2][64 + 32];  // per stage: 2^-e of the 64 A column quads, then the 32 B quads
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int NT = a.nmt * a.nnt;
   // block -> (slice, m tile, n tile): with S % 8 == 0 the tiles of one slice share an XCD
@@ -138,135 +156,130 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
   const int64_t KS = a.npairs * a.KP;
   const int64_t k0 = KS * slice / a.S, k1 = KS * (slice + 1) / a.S;
 
-  f32x4 acc[2][4];
+  f32x4 acc[2][8];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float4 cs = make_float4(0.f, 0.f, 0.f, 0.f), vs = make_float4(0.f, 0.f, 0.f, 0.f);
   const bool want_cs = a.part_cs && nt == 0, want_vec = a.avec && mt == 0;
 
-  // loader geometry: A (all waves) lane -> column quad (lane & 7), rows (lane >> 3) + 8 j;
-  // B (waves 0-3) lane -> column quad (lane & 3), rows (lane >> 2) + 16 j
+  // loader geometry: A lane -> column quad (lane & 7) of the wave's 32 columns, rows (lane >> 3) + 8 j;
+  // B lane -> column quad (lane & 3) of the wave's 16 columns, rows (lane >> 2) + 16 j
   const int ac = 32 * w + 4 * (lane & 7), ar = lane >> 3;
   const int bc = 16 * w + 4 * (lane & 3), br = lane >> 2;
-  float4 va[4], vb[2];
-  float vv[2];
-  auto load = [&](int64_t ks) {
+  auto load = [&](int64_t ks, WgRegs& R) {
     const int q = (int)(ks / a.KP);
     const int64_t r0 = (ks % a.KP) * kWgK;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      va[j] = wvalid ? ld4<VA>(a.a[q], a.lda[q], r0 + ar + 8 * j, m0 + ac, a.P, a.m) : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (w < 4) {
+      R.va[j] = wvalid ? ld4<VA>(a.a[q], a.lda[q], r0 + ar + 8 * j, m0 + ac, a.P, a.m) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int64_t r = r0 + br + 16 * j;
-        vb[j] = ld4<VB>(a.b[q], a.ldb[q], r, n0 + bc, a.P, a.n);
-        vv[j] = (want_vec && q == 0 && r < a.P) ? a.avec[r * a.ldv] : 0.0f;
-      }
+    for (int j = 0; j < 2; ++j) {
+      const int64_t r = r0 + br + 16 * j;
+      R.vb[j] = ld4<VB>(a.b[q], a.ldb[q], r, n0 + bc, a.P, a.n);
+      R.vv[j] = (want_vec && q == 0 && r < a.P) ? a.avec[r * a.ldv] : 0.0f;
     }
-    return q;
+    R.q = q;
   };
-  auto store = [&](int stg, int q) {
+  auto store = [&](int stg, const WgRegs& R) {
     _Float16* S0 = lds + stg * kStage;
-    if (want_cs && q == 0) cs = add4(cs, add4(add4(va[0], va[1]), add4(va[2], va[3])));
-    float m = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) m = fmaxf(m, fmaxf(fmaxf(fabsf(va[j].x), fabsf(va[j].y)), fmaxf(fabsf(va[j].z), fabsf(va[j].w))));
-    const int ea = split_exp(wave_max(m));
+    if (want_cs && R.q == 0) cs = add4(cs, add4(add4(R.va[0], R.va[1]), add4(R.va[2], R.va[3])));
+    if (want_vec && R.q == 0) vs = fma4(R.vv[1], R.vb[1], fma4(R.vv[0], R.vb[0], vs));
+    // per column quad: the max over its 32 rows (this lane's 4 rows x 8 lanes) -> power-of-two scale
+    const float ma = quad_max<false>(fmaxf(fmaxf(amax4(R.va[0]), amax4(R.va[1])), fmaxf(amax4(R.va[2]), amax4(R.va[3]))));
+    const int ea = split_exp(ma);
     const float sa = __builtin_ldexpf(1.0f, ea);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       uint2 h, l;
-      split4(va[j], sa, h, l);
+      split4(R.va[j], sa, h, l);
       const int o = (ar + 8 * j) * kAStride + ac;
       *(uint2*)(S0 + o) = h;
       *(uint2*)(S0 + kAPlane + o) = l;
     }
-    if (lane == 0) s_inv[stg][w] = __builtin_ldexpf(1.0f, -ea);
-    if (w < 4) {
-      if (want_vec && q == 0) vs = fma4(vv[1], vb[1], fma4(vv[0], vb[0], vs));
-      float mb = 0.0f;
+    if (lane < 8) s_inv[stg][ac >> 2] = __builtin_ldexpf(1.0f, -ea);
+    const float mb = quad_max<true>(fmaxf(amax4(R.vb[0]), amax4(R.vb[1])));
+    const int eb = split_exp(mb);
+    const float sb = __builtin_ldexpf(1.0f, eb);
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        mb = fmaxf(mb, fmaxf(fmaxf(fabsf(vb[j].x), fabsf(vb[j].y)), fmaxf(fabsf(vb[j].z), fabsf(vb[j].w))));
-      const int eb = split_exp(wave_max(mb));
-      const float sb = __builtin_ldexpf(1.0f, eb);
+    for (int j = 0; j < 2; ++j) {
+      uint2 h, l;
+      split4(R.vb[j], sb, h, l);
+      const int o = (br + 16 * j) * kBStride + bc;
+      *(uint2*)(S0 + 2 * kAPlane + o) = h;
+      *(uint2*)(S0 + 2 * kAPlane + kBPlane + o) = l;
+    }
+    if (lane < 4) s_inv[stg][64 + (bc >> 2)] = __builtin_ldexpf(1.0f, -eb);
+  };
+  auto compute = [&](int stg) {
+    if (!wvalid) return;
+    const _Float16* S0 = lds + stg * kStage;
+    const int G = lane >> 4, col = lane & 15;
+    f16x8 ah[2], al[2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        uint2 h, l;
-        split4(vb[j], sb, h, l);
-        const int o = (br + 16 * j) * kBStride + bc;
-        *(uint2*)(S0 + 2 * kAPlane + o) = h;
-        *(uint2*)(S0 + 2 * kAPlane + kBPlane + o) = l;
+    for (int i = 0; i < 2; ++i) {
+      ah[i] = frag(S0, kAStride, 32 * w + 16 * i, lane);
+      al[i] = frag(S0 + kAPlane, kAStride, 32 * w + 16 * i, lane);
+    }
+    // unscale factors: output rows 4G..4G+3 of m block i are one A column quad, column col of n block j
+    // one B quad
+    const float ia0 = s_inv[stg][8 * w + G], ia1 = s_inv[stg][8 * w + 4 + G];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f16x8 bh = frag(S0 + 2 * kAPlane, kBStride, 16 * j, lane);
+      const f16x8 bl = frag(S0 + 2 * kAPlane + kBPlane, kBStride, 16 * j, lane);
+      const float ib = s_inv[stg][64 + 4 * j + (col >> 2)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        f32x4 tt = f32x4{0.f, 0.f, 0.f, 0.f};
+        tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh, tt, 0, 0, 0);
+        tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl, tt, 0, 0, 0);
+        tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh, tt, 0, 0, 0);
+        const float f = (i ? ia1 : ia0) * ib;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = fmaf(tt[r], f, acc[i][j][r]);
       }
-      if (lane == 0) s_inv[stg][8 + w] = __builtin_ldexpf(1.0f, -eb);
     }
   };
 
-  int stg = 0;
+  // two k-steps of loads in flight: while k-step ks runs its MFMAs from LDS stage ks & 1, the
+  // registers hold k-step ks + 1 (split into the other stage after the MFMAs) and k-step ks + 2 loads
+  WgRegs R0, R1;
   if (k0 < k1) {
-    const int q = load(k0);
-    store(0, q);
+    load(k0, R0);
+    if (k0 + 1 < k1) load(k0 + 1, R1);
+    store(0, R0);
   }
   __syncthreads();
-  for (int64_t ks = k0; ks < k1; ++ks) {
-    const bool more = ks + 1 < k1;
-    int qn = 0;
-    if (more) qn = load(ks + 1);  // in flight during this k-step's MFMAs
-    if (wvalid) {
-      const _Float16* S0 = lds + stg * kStage;
-      f16x8 ah[2], al[2], bh[4], bl[4];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        ah[i] = frag(S0, kAStride, 32 * w + 16 * i, lane);
-        al[i] = frag(S0 + kAPlane, kAStride, 32 * w + 16 * i, lane);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        bh[j] = frag(S0 + 2 * kAPlane, kBStride, 16 * j, lane);
-        bl[j] = frag(S0 + 2 * kAPlane + kBPlane, kBStride, 16 * j, lane);
-      }
-      const float ia = s_inv[stg][w];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          f32x4 tt = f32x4{0.f, 0.f, 0.f, 0.f};
-          tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], tt, 0, 0, 0);
-          tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], tt, 0, 0, 0);
-          tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], tt, 0, 0, 0);
-          const float f = ia * s_inv[stg][8 + j];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] = fmaf(tt[r], f, acc[i][j][r]);
-        }
-    }
-    if (more) store(stg ^ 1, qn);
+  int64_t ks = k0;
+  while (ks < k1) {
+    // even step: compute stage 0, R1 holds ks + 1, refill R0 with ks + 2
+    if (ks + 2 < k1) load(ks + 2, R0);
+    compute(0);
+    if (ks + 1 < k1) store(1, R1);
     __syncthreads();
-    stg ^= 1;
+    if (++ks >= k1) break;
+    // odd step: compute stage 1, R0 holds ks + 1, refill R1 with ks + 2
+    if (ks + 2 < k1) load(ks + 2, R1);
+    compute(1);
+    if (ks + 1 < k1) store(0, R0);
+    __syncthreads();
+    ++ks;
   }
 
   // partial tile: lane (G, col) register r holds row 4G + r of each 16 x 16 tile -> part[s][n][m]
   const int64_t ldp = (int64_t)a.nmt * kWgM;
   float* P0 = a.part + (int64_t)slice * (a.nnt * kWgN) * ldp;
-  if (wvalid) {
+  {
     const int G = lane >> 4, col = lane & 15;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < 8; ++j) {
         const int64_t nn = n0 + 16 * j + col, mm = m0 + 32 * w + 16 * i + 4 * G;
-        *(float4*)(P0 + nn * ldp + mm) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-      }
-  } else {
-    const int G = lane >> 4, col = lane & 15;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t nn = n0 + 16 * j + col, mm = m0 + 32 * w + 16 * i + 4 * G;
-        *(float4*)(P0 + nn * ldp + mm) = make_float4(0.f, 0.f, 0.f, 0.f);
+        *(float4*)(P0 + nn * ldp + mm) = wvalid ? make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3])
+                                                : make_float4(0.f, 0.f, 0.f, 0.f);
       }
   }
   if (want_cs) {  // lanes with equal (lane & 7) hold the same columns: fixed-order butterfly
@@ -275,7 +288,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
     cs = add4(cs, shfl_xor4(cs, 32));
     if (lane < 8) *(float4*)(a.part_cs + (int64_t)slice * ldp + m0 + ac) = cs;
   }
-  if (want_vec && w < 4) {
+  if (want_vec) {
     vs = add4(vs, shfl_xor4(vs, 4));
     vs = add4(vs, shfl_xor4(vs, 8));
     vs = add4(vs, shfl_xor4(vs, 16));

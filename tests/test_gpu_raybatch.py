@@ -80,9 +80,10 @@ def test_neus_train_step_random_batch_vs_oracle(precision):
     Gradient bar, settled against a float64 truth (the oracle's step evaluated in float64 on the same
     fp32 inputs, pixels and sample depths): every weight gradient is a sum over 65 k sample points, and
     the fp32 oracle itself is off that truth by up to a few 1e-5 of the tensor's largest entry.  So
-      (1) element-wise, |gpu - f64| <= |oracle32 - f64| + 1e-5 max|f64|  (the GPU is no further from
-          the truth than the fp32 reference computation, up to 1e-5 of the tensor scale), for every
-          parameter, and
+      (1) element-wise, |gpu - f64| <= max|oracle32 - f64| + 1e-5 max|f64|  (the GPU stays inside the
+          fp32 reference computation's own error envelope for that tensor, up to 1e-5 of the tensor
+          scale; the two fp32 computations err at different elements, so the envelope is the tensor's
+          worst fp32 error, not the element's), for every parameter, and
       (2) the 64-ray golden tests' bar |gpu - oracle32| <= 1e-4 |oracle32| + 1e-5 max|oracle32| for every
           tensor on which the fp32 oracle itself meets 1e-4 |f64| + 1e-5 max|f64| against the truth.
     Losses 1e-5 relative."""
@@ -146,7 +147,8 @@ def test_neus_train_step_random_batch_vs_oracle(precision):
         o32_meets = bool((e_o32 <= 1e-4 * t64.abs() + 1e-5 * scale).all())
         print(f'{precision} {k}: |gpu-f64| max {float(e_gpu.max()) / scale:.2e}, |oracle32-f64| max '
               f'{float(e_o32.max()) / scale:.2e} (of the tensor scale {scale:.3e}); oracle32 meets 1e-5: {o32_meets}')
-        assert bool((e_gpu <= e_o32 + 1e-5 * scale).all()), (k, float((e_gpu - e_o32).max()) / scale)
+        assert bool((e_gpu <= float(e_o32.max()) + 1e-5 * scale).all()), (k, float(e_gpu.max()) / scale,
+                                                                          float(e_o32.max()) / scale)
         if o32_meets:
             n_tight += 1
             s32 = float(o32.abs().max()) + 1e-30

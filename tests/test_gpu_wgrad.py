@@ -93,7 +93,7 @@ def test_wgrad_vector_row_and_views():
 def test_wgrad_timing_vs_hipblaslt():
     """device time of one 65536 x 256 x 256 weight gradient (both sweeps) on nr_wgrad vs the split-K
     fp32 batched GEMM + sum it replaces (hipBLASLt)"""
-    from neurecon_amd.training import _wg, _wgrad2
+    from neurecon_amd.training import _wg, _wgrad, _wgrad2
     g = torch.Generator().manual_seed(3)
     P = 65536
     a1, b1, a2, b2 = (_mk(P, 256, 256, g) for _ in range(4))
@@ -112,6 +112,9 @@ def test_wgrad_timing_vs_hipblaslt():
         return e0.elapsed_time(e1) / reps * 1e3
     us_hip = t(lambda: _wg([(a1, b1), (a2, b2)], colsum=cs))
     us_blas = t(lambda: _wgrad2(a1, b1, a2, b2))
+    us_hip1 = t(lambda: _wg([(a1, b1)], colsum=cs))
+    us_blas1 = t(lambda: _wgrad(a1, b1))
     gb = 4 * P * 256 * 4 / 1e9
     print(f'weight gradient, 2 x [65536, 256]^T [65536, 256]: nr_wgrad {us_hip:.1f} us ({gb / us_hip * 1e6 / 1e3:.2f} TB/s '
-          f'of operands, bias gradient fused), hipBLASLt split-K bmm + sum {us_blas:.1f} us')
+          f'of operands, bias gradient fused), hipBLASLt split-K bmm + sum {us_blas:.1f} us; one pair: nr_wgrad '
+          f'{us_hip1:.1f} us, hipBLASLt {us_blas1:.1f} us')
