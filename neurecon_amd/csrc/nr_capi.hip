@@ -223,7 +223,8 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   auto sample_sdf = [&](const float* pts, int64_t P, float* sdf_out, int64_t slot0) -> int {
     if (defer)
       return launch_sdf_deferred(SL, a.sdf_packed, pts, P, sdf_out, nullptr, a.sdf->multires,
-                                 c.slabs + (size_t)(slot0 / 16) * (8 * 16 * 64), nullptr, nullptr, 1, st);
+                                 (float4*)((char*)c.slabs + (size_t)(slot0 / 16) * kSlabColBytes), nullptr, nullptr,
+                                 1, st);
     return launch_sdf(SL, a.sdf_packed, pts, P, sdf_out, fused ? c.nraw + slot0 * 3 : nullptr, nullptr,
                       a.sdf->multires, fused ? mlp_ws : nullptr, fused ? mlp_bytes : 0, st);
   };

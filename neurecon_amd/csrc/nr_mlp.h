@@ -10,6 +10,13 @@ constexpr int kTile = 16;                       // points per wave (MFMA N dimen
 constexpr int kPointsPerWG = kTile * kWaves;    // 128
 constexpr int kMaxChunkBytes = 48 * 1024;       // LDS chunk: 2 output blocks x <=24 input blocks x 1 KB
 constexpr size_t kScratchPerWG = (size_t)kWaves * 8 * 16 * 64 * 16;  // exp(100z) slabs, 1 MiB
+// sdf4_kernel reverse-pass slabs of one 16-point column: layers 0..6 hold 24-bit codes of
+// 2^-L = 1 - softplus'(z) (per chunk [block 2][column][lane] x 12 B: 8 chunks x 1536 B = 12 KB per
+// layer), layer 7 holds d sdf / d z7 (and, during the forward, the parked embedding) in fp32
+// ([block 16][column][lane] x 16 B); 100 KB instead of 8 x 16 KB of fp32 slabs
+constexpr int kSlab24Chunk = 2 * 64 * 12;               // one chunk of one column: 1536 B
+constexpr int kSlab24Layer = 8 * kSlab24Chunk;          // 12 KB
+constexpr int kSlabColBytes = 7 * kSlab24Layer + 16 * 64 * 16;  // 100 KB per column (deferred tile)
 
 // SDF GEMM ops in stream order (forward F*, feature F8, backward B*)
 enum SdfOp { F0, F1, F2, F3, F4, F5, F6, F7, F8, B7, B6, B5, B4, B3, B2, B1, B0, kSdfOps };
@@ -108,7 +115,7 @@ int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t
                float* feature, int nfreq, void* ws, size_t ws_bytes, hipStream_t stream,
                const int* P_dev = nullptr, int P_mult = 0);  // P_dev: device count, P_eff = min(P, *P_dev * P_mult)
 // deferred sample nablas (sdf4_kernel STAGE 1 / 2): stage 1 = sdf + slabs per 16-point tile into
-// `slabs` (P/16 x 128 KB); stage 2 = nablas of the tiles tiles[0 .. *n_tiles) from their slabs
+// `slabs` (P/16 x kSlabColBytes); stage 2 = nablas of the tiles tiles[0 .. *n_tiles) from their slabs
 int launch_sdf_deferred(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,
                         int nfreq, float4* slabs, const int* tiles, const int* n_tiles, int stage, hipStream_t stream);
 int launch_nerf(const NerfLayout& L, const void* packed, const float* x4, const float* vdir, int64_t vdiv,

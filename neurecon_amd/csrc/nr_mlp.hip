@@ -611,7 +611,7 @@ struct SdfKArgs {
   int nfreq;
   const int* P_dev;  // optional device-side point count (x P_mult), bounded by P
   int P_mult;
-  float4* slabs;      // deferred nablas: per 16-point tile of the launch, [tile][8][16][64] float4
+  float4* slabs;      // deferred nablas: per 16-point tile of the launch, kSlabColBytes (nr_mlp.h layout)
   const int* tiles;   // STAGE 2: 16-point tiles to run the reverse pass on
   const int* n_tiles; //   ... and their count (device)
 };
@@ -885,8 +885,8 @@ static_assert(kNC == 1 || kNC == 2, "columns per wave");
 constexpr int kW4 = 8 / kNC;      // waves per workgroup: the tile stays 128 points
 constexpr int kT4 = 64 * kW4;
 constexpr int kWPE = kW4 / 4;     // waves per SIMD
-constexpr int kSlabW = 2 * kNC * 1024;  // one chunk's slab values of one wave (2 blocks x kNC columns)
-constexpr int kSlab4 = kW4 * kSlabW;    // ... of the workgroup: 16 KB
+constexpr int kSlabW = kNC * kSlab24Chunk;  // one chunk's slab codes of one wave (2 blocks x kNC columns x 64 x 12 B)
+constexpr int kSlab4 = kW4 * kSlabW;        // ... of the workgroup: 12 KB
 #ifndef NR_DMA_LOADERS
 #define NR_DMA_LOADERS (8 / NR_SDF4_NC)
 #endif
@@ -896,12 +896,14 @@ static_assert(kLoad >= 1 && kLoad <= kW4, "loader waves");
 // Deferred stores of one chunk (up to 4 x 16 B per lane), issued at the start of the next chunk
 // before its weight DMA, so flip()'s counted wait never stands behind a store younger than the
 // weights it waits for.  Wave-uniform base (SGPR) + per-lane 32-bit float4 offsets.
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 struct Pend4 {
   float4* base;  // null: nothing pending
-  uint32_t o[4];
-  float4 v[4];
+  uint32_t o[4];  // float4 index, or with b96 a byte offset
+  float4 v[4];    // with b96: the 3 dwords in .x .y .z (bit patterns)
   int n;
   bool nt;
+  bool b96;       // 12-byte stores (24-bit slab codes)
   // global_store_dwordx4 with an SGPR base and a 32-bit VGPR byte offset (saddr form), from asm:
   // compiler-built 64-bit per-lane addresses get hoisted out of the tile loop and spilled
   __device__ __forceinline__ int pending() const { return base ? n : 0; }
@@ -912,22 +914,30 @@ struct Pend4 {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if (i < n) {
-          const uint32_t off = o[i] * 16u;
-          const f32x4 d = tof(v[i]);
           // s_nop: the store-data hazard (a VALU may not overwrite a >8-byte store's data VGPRs in
           // the next cycle) is not tracked through inline asm
-          if (nt) asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" : : "v"(off), "v"(d), "s"(base) : "memory");
-          else asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" : : "v"(off), "v"(d), "s"(base) : "memory");
+          if (b96) {
+            const uint32_t off = o[i];
+            const u32x3 d = {__float_as_uint(v[i].x), __float_as_uint(v[i].y), __float_as_uint(v[i].z)};
+            if (nt) asm volatile("global_store_dwordx3 %0, %1, %2 nt\n\ts_nop 1" : : "v"(off), "v"(d), "s"(base) : "memory");
+            else asm volatile("global_store_dwordx3 %0, %1, %2\n\ts_nop 1" : : "v"(off), "v"(d), "s"(base) : "memory");
+          } else {
+            const uint32_t off = o[i] * 16u;
+            const f32x4 d = tof(v[i]);
+            if (nt) asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" : : "v"(off), "v"(d), "s"(base) : "memory");
+            else asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" : : "v"(off), "v"(d), "s"(base) : "memory");
+          }
         }
       }
       base = nullptr;
     }
     return issued;
   }
-  __device__ __forceinline__ void put(float4* b, int cnt, bool nontemporal) {
+  __device__ __forceinline__ void put(float4* b, int cnt, bool nontemporal, bool bytes96 = false) {
     base = b;
     n = cnt;
     nt = nontemporal;
+    b96 = bytes96;
   }
 };
 
@@ -1045,29 +1055,30 @@ struct WStream4 {
   // this wave's softplus' slab of chunk c (blocks 2c, 2c+1, all kNC columns: 2 or 4 KB contiguous) ->
   // the next slab slot; one M0 setting, the instruction offset steps global and LDS address together.
   // Staged two chunk-iterations before the epilogue that reads it.  Returns the DMA instructions issued.
+  // e: byte base of the layer's slab (24-bit codes, kSlab24Chunk per column and chunk)
   __device__ __forceinline__ int stage_slab(const float4* e, int c) {
 #ifdef NR_EXP_NO_ELOAD  // timing experiment: softplus' slab not read back
     return 0;
 #endif
-    const uint32_t voff = (threadIdx.x & 63) * 16;
-    const char* g = (const char*)uniform_ptr(e + 2 * kNC * c * 64);
+    const uint32_t voff = (threadIdx.x & 63) * 12;
+    const char* g = uniform_ptr((const char*)e + kNC * kSlab24Chunk * c);
     const uint32_t base =
         __builtin_amdgcn_readfirstlane(lds_u32(slab) + (uint32_t)(es * kSlab4 + wave_id() * kSlabW));
     if constexpr (kNC == 2)
       asm volatile(
           "s_mov_b32 m0, %2\n\ts_nop 0\n\t"
-          "global_load_lds_dwordx4 %0, %1\n\t"
-          "global_load_lds_dwordx4 %0, %1 offset:1024\n\t"
-          "global_load_lds_dwordx4 %0, %1 offset:2048\n\t"
-          "global_load_lds_dwordx4 %0, %1 offset:3072"
+          "global_load_lds_dwordx3 %0, %1" NR_SLAB_LD_POL "\n\t"
+          "global_load_lds_dwordx3 %0, %1 offset:768" NR_SLAB_LD_POL "\n\t"
+          "global_load_lds_dwordx3 %0, %1 offset:1536" NR_SLAB_LD_POL "\n\t"
+          "global_load_lds_dwordx3 %0, %1 offset:2304" NR_SLAB_LD_POL
           :
           : "v"(voff), "s"(g), "s"(base)
           : "memory", "m0");
     else
       asm volatile(
           "s_mov_b32 m0, %2\n\ts_nop 0\n\t"
-          "global_load_lds_dwordx4 %0, %1" NR_SLAB_LD_POL "\n\t"
-          "global_load_lds_dwordx4 %0, %1 offset:1024" NR_SLAB_LD_POL
+          "global_load_lds_dwordx3 %0, %1" NR_SLAB_LD_POL "\n\t"
+          "global_load_lds_dwordx3 %0, %1 offset:768" NR_SLAB_LD_POL
           :
           : "v"(voff), "s"(g), "s"(base)
           : "memory", "m0");
@@ -1337,6 +1348,35 @@ __device__ __forceinline__ void pend_chunk(Pend4& pd, float4* base, int first_bl
   for (int i = 0; i < 2 * kNC; ++i) pd.o[i] = (kNC * first_blk + i) * 64 + l;
   pd.put(base, 2 * kNC, nt);
 }
+// 24-bit slab codes of chunk c: pd.v[o * kNC + q] (3 dwords: block 2c + o, column q) -> byte offset
+// c kNC 1536 + ((o kNC + q) 64 + lane) 12 of the layer's slab (the chunk's kNC x 1536 B stay contiguous
+// for the reverse pass's staging DMA)
+__device__ __forceinline__ void pend_chunk24(Pend4& pd, float4* layer, int c, int lane, bool nt) {
+  const uint32_t l = opaque_lane(lane);
+#pragma unroll
+  for (int i = 0; i < 2 * kNC; ++i) pd.o[i] = (uint32_t)(c * kNC * kSlab24Chunk) + ((uint32_t)i * 64 + l) * 12u;
+  pd.put(layer, 2 * kNC, nt, true);
+}
+// softplus' = 1 - 2^-L is kept as the 24-bit code of c = 2^-L = 1 / (1 + 2^t): u = floor(c 2^23 + 0.5)
+// (c in [0, 1], 2^23 fits in 24 bits).  The code's absolute error 2^-24 matches fp32's rounding of
+// softplus' near 1 (and of the old 1 - 2^-L cancellation near 0); exact 1 (u = 0) wherever 2^-L < 2^-24,
+// which covers torch's linear branch (100 z > 20: 2^-L < 2^-28.8).  4 codes -> 3 dwords.
+__device__ __forceinline__ uint32_t code24(float c) { return (uint32_t)__builtin_fmaf(c, 8388608.0f, 0.5f); }
+__device__ __forceinline__ float4 pack24(float c0, float c1, float c2, float c3) {
+  const uint32_t u0 = code24(c0), u1 = code24(c1), u2 = code24(c2), u3 = code24(c3);
+  return make_float4(__uint_as_float(u0 | (u1 << 24)), __uint_as_float((u1 >> 8) | (u2 << 16)),
+                     __uint_as_float((u2 >> 16) | (u3 << 8)), 0.0f);
+}
+// g * softplus' = g - g c for the 4 codes in (w0, w1, w2)
+__device__ __forceinline__ float4 unpack24_mul(uint32_t w0, uint32_t w1, uint32_t w2, float4 g) {
+  const float u0 = (float)(w0 & 0xFFFFFFu);
+  const float u1 = (float)(__builtin_amdgcn_alignbit(w1, w0, 24) & 0xFFFFFFu);
+  const float u2 = (float)(__builtin_amdgcn_alignbit(w2, w1, 16) & 0xFFFFFFu);
+  const float u3 = (float)(w2 >> 8);
+  constexpr float k = 1.0f / 8388608.0f;
+  return make_float4(__builtin_fmaf(-(g.x * k), u0, g.x), __builtin_fmaf(-(g.y * k), u1, g.y),
+                     __builtin_fmaf(-(g.z * k), u2, g.z), __builtin_fmaf(-(g.w * k), u3, g.w));
+}
 
 // forward softplus op: out -> next operand (k-step c of oh/ol), slab <- L = log2(1 + 2^t).
 // Staged by operation, not by value: each stage applies one step to all 16 values of the chunk
@@ -1388,9 +1428,17 @@ struct FwdEpi4 {
     } else if (st == 3) {
 #pragma unroll
       for (int i = NV / 2; i < NV; ++i) L[i] = NR_LOG2(e[i]);
+      if constexpr (NABLA) {  // c = 2^-L = 1 / (1 + 2^t) for the slab codes (e no longer needed)
+#pragma unroll
+        for (int i = 0; i < NV / 2; ++i) e[i] = __builtin_amdgcn_rcpf(e[i]);
+      }
     } else if (st == 4) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) m[i] = fmaxf(L[i], zval(zz, i));
+      if constexpr (NABLA) {
+#pragma unroll
+        for (int i = NV / 2; i < NV; ++i) e[i] = __builtin_amdgcn_rcpf(e[i]);
+      }
     } else if (st == 5) {
 #pragma unroll
       for (int q = 0; q < kNC; ++q) {
@@ -1402,13 +1450,13 @@ struct FwdEpi4 {
         r = __builtin_fmaxf(r, __builtin_fmaxf(m[i + 6], m[i + 7]));
         mrun[q] = r;
       }
-      if constexpr (NABLA) {  // L straight into the pending-store slots ([block][column])
+      if constexpr (NABLA) {  // 24-bit codes of 2^-L straight into the pending-store slots ([block][column])
 #pragma unroll
         for (int q = 0; q < kNC; ++q)
 #pragma unroll
           for (int o = 0; o < 2; ++o) {
             const int i = (2 * q + o) * 4;
-            pd.v[kNC * o + q] = make_float4(L[i], L[i + 1], L[i + 2], L[i + 3]);
+            pd.v[kNC * o + q] = pack24(e[i], e[i + 1], e[i + 2], e[i + 3]);
           }
       }
     } else if (st == 6) {
@@ -1423,7 +1471,7 @@ struct FwdEpi4 {
                 oh[kNC - 1][c], ol[kNC - 1][c]);
 #endif
 #ifndef NR_EXP_NO_ESTORE  // timing experiment: softplus' slab not written
-      if constexpr (NABLA) pend_chunk(pd, sl, 2 * c, lane, NR_SLAB_NT);
+      if constexpr (NABLA) pend_chunk24(pd, sl, c, lane, NR_SLAB_NT);
 #endif
     }
   }
@@ -1487,11 +1535,9 @@ struct BwdEpi4 {
     if (2 * c < NMAIN) {
       const int q = st >> 2, k = st & 3;
       if (q >= kNC) return;
-      if (k < 2) {  // g * softplus'(z) = g - g 2^-L  (FwdEpi4's slab)
-        const float4 Lv = ws.slab_read()[(kNC * k + q) * 64 + lane];
-        const float4 gv = zz.z[q][k];
-        y[q][k] = make_float4(__builtin_fmaf(-gv.x, NR_EXP2(-Lv.x), gv.x), __builtin_fmaf(-gv.y, NR_EXP2(-Lv.y), gv.y),
-                              __builtin_fmaf(-gv.z, NR_EXP2(-Lv.z), gv.z), __builtin_fmaf(-gv.w, NR_EXP2(-Lv.w), gv.w));
+      if (k < 2) {  // g * softplus'(z) = g - g 2^-L  (FwdEpi4's 24-bit codes of 2^-L)
+        const uint32_t* sw = (const uint32_t*)((const char*)ws.slab_read() + ((kNC * k + q) * 64 + lane) * 12);
+        y[q][k] = unpack24_mul(sw[0], sw[1], sw[2], zz.z[q][k]);
       } else if (k == 2) {
         mrun[q] = amax8(mrun[q], y[q][0], y[q][1]);
       } else {
@@ -1547,11 +1593,12 @@ void sdf4_kernel(SdfKArgs a) {
   const float b8 = *(const float*)(W + a.L.misc_off);
   // this wave's slabs: [layer 8][block 16][column kNC][lane 64] float4 (128 KB per column); the
   // deferred stages keep them per 16-point tile of the launch (set per tile below)
-  float4* escr = uniform_ptr(a.scratch + (size_t)(blockIdx.x * kW4 + wave) * (8 * 16 * kNC * 64));
+  float4* escr = uniform_ptr((float4*)((char*)a.scratch + (size_t)(blockIdx.x * kW4 + wave) * (kNC * kSlabColBytes)));
+  // layer l's slab (byte base): layers 0..6 24-bit codes (kNC x 12 KB), layer 7 fp32 (kNC x 16 KB)
   auto slab = [&](int l) {
-    float4* e = escr;
+    char* e = (char*)escr;
     asm volatile("" : "+s"(e));
-    return e + l * 16 * kNC * 64;
+    return (float4*)(e + l * kNC * kSlab24Layer);
   };
 
 #ifdef NR_EXP_STAMPS
@@ -1576,10 +1623,10 @@ void sdf4_kernel(SdfKArgs a) {
     if constexpr (STAGE == 2) {  // this wave's tile (the last one again past the list's end: nothing stored)
       const int64_t ti = min(p0 / 16, (int64_t)(*a.n_tiles) - 1);
       const int64_t tile = a.tiles[ti];
-      escr = uniform_ptr(a.slabs + (size_t)tile * (8 * 16 * 64));
+      escr = uniform_ptr((float4*)((char*)a.slabs + (size_t)tile * kSlabColBytes));
       p0 = p0 / 16 < (int64_t)(*a.n_tiles) ? tile * 16 : a.P;  // a.P: every point invalid
     } else if constexpr (STAGE == 1) {
-      escr = uniform_ptr(a.slabs + (size_t)(p0 / 16) * (8 * 16 * 64));
+      escr = uniform_ptr((float4*)((char*)a.slabs + (size_t)(p0 / 16) * kSlabColBytes));
     }
     const int64_t Pv = STAGE == 2 ? a.P : Pn;  // points of the launch (validity of this wave's points)
     int64_t pq[kNC];

@@ -1043,7 +1043,7 @@ NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc) {
   p.o_sv2 = take((size_t)S * Rc);
   p.o_idv2 = take((size_t)S * Rc);
   const size_t tiles = neus_deferred(a, Rc) ? ((size_t)S * Rc + 15) / 16 : 1;
-  p.o_slabs = take(neus_deferred(a, Rc) ? tiles * (8 * 16 * 64 * 4) : 1);  // 128 KB per 16-slot tile
+  p.o_slabs = take(neus_deferred(a, Rc) ? tiles * (kSlabColBytes / 4) : 1);  // 100 KB per 16-slot tile
   p.o_tflag = take(tiles);
   p.o_tiles = take(tiles);
   p.o_tcnt = take(1);
