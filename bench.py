@@ -80,9 +80,12 @@ def parse():
     ap.add_argument('--no-frame', action='store_true',
                     help='skip the strong-scaling config-(d) frame leg of the default workload')
     ap.add_argument('--frame-steps', type=int, default=3)
-    ap.add_argument('--workspace-gb', type=float, default=16.0,
-                    help="render workspace budget (volume_render's max_workspace_gb; the library default is 4 GiB): "
-                         "a 4096-ray config-(b) batch renders as one chunk within 16 GiB")
+    ap.add_argument('--workspace-gb', type=float, default=None,
+                    help="config-(b) render workspace budget (volume_render's max_workspace_gb); default: the "
+                         "library's 4 GiB, within which the 4096-ray batch renders as one chunk")
+    ap.add_argument('--frame-workspace-gb', type=float, default=16.0,
+                    help="workspace budget of the 480,000-ray config-(d) frame render (chunks of up to 16384 rays "
+                         "keep the per-ray kernels on the whole chip; the caller's choice on a 288 GB GPU)")
     ap.add_argument('--no-configs', action='store_true',
                     help='skip the BASELINE configs (c), (e) and the training step in the default line')
     ap.add_argument('--config-steps', type=int, default=5)
@@ -635,7 +638,7 @@ def run(args):
     from neurecon_amd import rend_util
     from neurecon_amd.frameworks.neus import volume_render
     if args.workload == 'frame_d':
-        step, rays_per_step = frame_d_setup(dev, args.precision, args.workspace_gb)  # all ranks render one frame
+        step, rays_per_step = frame_d_setup(dev, args.precision, args.frame_workspace_gb)  # one frame, all ranks
         n_rays = rays_per_step
     elif args.workload == 'train':
         step = train_setup(dev, args.precision, args.train_rays, world, args.adam)
@@ -701,7 +704,7 @@ def run(args):
     frame = None
     if args.workload == 'b' and not args.no_frame:
         # strong scaling: one config-(d) 800x600 frame per step split over all ranks, all_gather timed
-        fstep, frame_rays = frame_d_setup(dev, args.precision, args.workspace_gb)
+        fstep, frame_rays = frame_d_setup(dev, args.precision, args.frame_workspace_gb)
         fdt = max_over_ranks(timed(fstep, args.frame_steps, 1, sync, barrier))
         frame = {'metric': 'rays/sec, config (d): NeuS+NeRF++ full 800x600 frame per step, rays sharded over '
                            'the GPUs (render_sharded + all_gather of the maps inside the timed region)',
@@ -782,7 +785,9 @@ def run(args):
                 eg['speedup'] = round(value / eg['value'], 2)
                 out['cpu_baseline']['eager_gpu_reference'] = eg
         out['config']['build_id'] = L.build_id()  # source hash compiled into libnrhip.so (neurecon_amd/build.py)
-        out['config']['workspace_gb'] = args.workspace_gb
+        out['config']['workspace_gb'] = args.workspace_gb if args.workspace_gb is not None else 'library default (4 GiB)'
+        if args.workload == 'b' and not args.no_frame:
+            out['strong_scaling_frame_d']['workspace_gb'] = args.frame_workspace_gb
         print(json.dumps(out), flush=True)
     if dist:
         tdist.destroy_process_group()

@@ -442,6 +442,9 @@ static int64_t neus_chunk_rays(const NrNeusArgs* a) {
   const size_t per_ray = (t2 - t1) / 1024 + 1, fixed = t1 > 1024 * per_ray ? t1 - 1024 * per_ray : 0;
   const int64_t fit = budget > fixed ? (int64_t)((budget - fixed) / per_ray) : 0;
   cap = std::min(cap, std::max<int64_t>(fit, 16));
+  // deferred chunks tile exactly: a ray count that is not a multiple of 16 renders as 16-multiple
+  // chunks (deferred) plus a < 16-ray tail (nablas when drawn)
+  if (defer && n > 16 && n % 16) cap = std::min(cap, n / 16 * 16);
   if (n <= cap) return n;
   if (defer && cap >= 16) cap = cap / 16 * 16;
   return std::max<int64_t>(cap, 1);
