@@ -304,6 +304,24 @@ def roofline(kstats, precision, census=None):
 HBM_PEAK_TBPS = 8.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
+TRAIN_PMC_SUMMARY = 'profiles/r04/train_pmc_summary.json'  # tools/gpu_prof_r04.sh (PMC passes of --workload train)
+
+
+def train_pmc_traffic(prefix):
+    """HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) averaged over the training bench's launches
+    of every device kernel whose name contains `prefix`, from the committed PMC summary"""
+    path = os.path.join(ROOT, TRAIN_PMC_SUMMARY)
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        summary = json.load(f)
+    recs = [r for k, r in summary.items() if prefix in k]
+    n = sum(r['launches'] for r in recs)
+    if not n:
+        return None, None
+    return sum(r['hbm_bytes_per_launch'] * r['launches'] for r in recs) / n, TRAIN_PMC_SUMMARY
+
+
 def train_roofline(kstats, dt, steps, census=None):
     """Training step: the dominant library kernel is the layer GEMM (nr_train_gemm), whose launches
     stream [P, <=288] fp32 activations: HBM-bound.  achieved = algorithmic bytes of its calls (inputs,
@@ -317,11 +335,24 @@ def train_roofline(kstats, dt, steps, census=None):
         return None
     by = T.TG_BYTES['bytes'] / max(T.TG_BYTES['calls'], 1) * n  # bytes of the timed launches
     tbps = by / (ms * 1e-3) / 1e12
-    return {'bound': 'hbm', 'achieved': round(tbps, 3), 'peak': HBM_PEAK_TBPS, 'unit': 'TB/s',
-            'frac': round(tbps / HBM_PEAK_TBPS, 4), 'traffic': None, 'kernel': 'train_gemm',
-            'avg_launch_ms': round(ms / n, 4), 'launches': n, 'bytes_per_launch': by / n,
-            'share_of_library_time': round(ms / max(lib_ms, 1e-9), 4),
-            'library_share_of_step': round(lib_ms * 1e-3 / max(dt, 1e-12), 4)}
+    traffic, src = train_pmc_traffic('tgemm_kernel')
+    out = {'bound': 'hbm', 'achieved': round(tbps, 3), 'peak': HBM_PEAK_TBPS, 'unit': 'TB/s',
+           'frac': round(tbps / HBM_PEAK_TBPS, 4), 'traffic': traffic, 'traffic_unit': 'bytes/launch',
+           'traffic_source': src, 'kernel': 'train_gemm',
+           'avg_launch_ms': round(ms / n, 4), 'launches': n, 'bytes_per_launch': by / n,
+           'share_of_library_time': round(ms / max(lib_ms, 1e-9), 4),
+           'library_share_of_step': round(lib_ms * 1e-3 / max(dt, 1e-12), 4)}
+    # the weight-gradient kernel (nr_wgrad): units = operand bytes (npairs P (m + n) 4), HBM-bound
+    wc = (census if census is not None else kstats).get('wgrad')
+    if wc and wc[0]:
+        nw, msw, byw = wc
+        wtraffic, wsrc = train_pmc_traffic('wgrad_kernel')
+        out['wgrad'] = {'bound': 'hbm', 'achieved': round(byw / (msw * 1e-3) / 1e12, 3), 'peak': HBM_PEAK_TBPS,
+                        'unit': 'TB/s', 'frac': round(byw / (msw * 1e-3) / 1e12 / HBM_PEAK_TBPS, 4),
+                        'launches_per_step': round(nw / steps, 1), 'avg_launch_ms': round(msw / nw, 4),
+                        'bytes_per_launch': byw / nw, 'traffic': wtraffic, 'traffic_source': wsrc,
+                        'share_of_library_time': round(msw / max(lib_ms, 1e-9), 4)}
+    return out
 
 
 def frame_d_setup(dev, precision, workspace_gb=None):

@@ -386,7 +386,8 @@ int nr_wgrad(const NrWgrad* w, void* stream) {
   k.ldv = w->ldv > 0 ? w->ldv : 1;
   k.part_vec = w->vec ? (float*)(ws + p.part_bytes + p.cs_bytes) : nullptr;
   {
-    ProfScope prof("wgrad", (double)w->npairs * w->P * w->m * w->n, st);
+    // units: the operands' bytes (the HBM-bound roofline's algorithmic traffic)
+    ProfScope prof("wgrad", (double)w->npairs * w->P * (w->m + w->n) * 4.0, st);
     const dim3 grid((unsigned)(p.S * p.nmt * p.nnt));
     // S % 8 == 0 needs the grid padded to whole XCD rounds of the mapping (it already is: S * NT)
     if (va && vb) hipLaunchKernelGGL((wgrad_kernel<true, true>), grid, dim3(kWgThreads), 0, st, k);
