@@ -885,8 +885,10 @@ static_assert(kNC == 1 || kNC == 2, "columns per wave");
 constexpr int kW4 = 8 / kNC;      // waves per workgroup: the tile stays 128 points
 constexpr int kT4 = 64 * kW4;
 constexpr int kWPE = kW4 / 4;     // waves per SIMD
-constexpr int kSlabW = kNC * kSlab24Chunk;  // one chunk's slab codes of one wave (2 blocks x kNC columns x 64 x 12 B)
-constexpr int kSlab4 = kW4 * kSlabW;        // ... of the workgroup: 12 KB
+// one chunk's slab codes of one wave in LDS: 2 blocks x kNC columns x 64 lanes x 16 B (the LDS-DMA of
+// global_load_lds_dwordx3 lands lane l's 12 B at l x 16, the 4th dword untouched: tools/probes/ldsdma_x3)
+constexpr int kSlabW = 2 * kNC * 1024;
+constexpr int kSlab4 = kW4 * kSlabW;        // ... of the workgroup: 16 KB
 #ifndef NR_DMA_LOADERS
 #define NR_DMA_LOADERS (8 / NR_SDF4_NC)
 #endif
@@ -1060,28 +1062,22 @@ struct WStream4 {
 #ifdef NR_EXP_NO_ELOAD  // timing experiment: softplus' slab not read back
     return 0;
 #endif
+    // global: 768 B per piece (64 lanes x 12 B); LDS: 1 KB per piece (lane stride 16 B), so each piece
+    // gets its own global base and M0 (the instruction offset would step both by the same amount)
     const uint32_t voff = (threadIdx.x & 63) * 12;
     const char* g = uniform_ptr((const char*)e + kNC * kSlab24Chunk * c);
     const uint32_t base =
         __builtin_amdgcn_readfirstlane(lds_u32(slab) + (uint32_t)(es * kSlab4 + wave_id() * kSlabW));
-    if constexpr (kNC == 2)
+#pragma unroll
+    for (int piece = 0; piece < 2 * kNC; ++piece) {
+      const char* gp = g + piece * 768;
       asm volatile(
           "s_mov_b32 m0, %2\n\ts_nop 0\n\t"
-          "global_load_lds_dwordx3 %0, %1" NR_SLAB_LD_POL "\n\t"
-          "global_load_lds_dwordx3 %0, %1 offset:768" NR_SLAB_LD_POL "\n\t"
-          "global_load_lds_dwordx3 %0, %1 offset:1536" NR_SLAB_LD_POL "\n\t"
-          "global_load_lds_dwordx3 %0, %1 offset:2304" NR_SLAB_LD_POL
+          "global_load_lds_dwordx3 %0, %1" NR_SLAB_LD_POL
           :
-          : "v"(voff), "s"(g), "s"(base)
+          : "v"(voff), "s"(gp), "s"(base + piece * 1024)
           : "memory", "m0");
-    else
-      asm volatile(
-          "s_mov_b32 m0, %2\n\ts_nop 0\n\t"
-          "global_load_lds_dwordx3 %0, %1" NR_SLAB_LD_POL "\n\t"
-          "global_load_lds_dwordx3 %0, %1 offset:768" NR_SLAB_LD_POL
-          :
-          : "v"(voff), "s"(g), "s"(base)
-          : "memory", "m0");
+    }
     es = next3(es);
     return 2 * kNC;
   }
@@ -1536,8 +1532,8 @@ struct BwdEpi4 {
       const int q = st >> 2, k = st & 3;
       if (q >= kNC) return;
       if (k < 2) {  // g * softplus'(z) = g - g 2^-L  (FwdEpi4's 24-bit codes of 2^-L)
-        const uint32_t* sw = (const uint32_t*)((const char*)ws.slab_read() + ((kNC * k + q) * 64 + lane) * 12);
-        y[q][k] = unpack24_mul(sw[0], sw[1], sw[2], zz.z[q][k]);
+        const uint4 sw = *(const uint4*)((const char*)ws.slab_read() + ((kNC * k + q) * 64 + lane) * 16);
+        y[q][k] = unpack24_mul(sw.x, sw.y, sw.z, zz.z[q][k]);
       } else if (k == 2) {
         mrun[q] = amax8(mrun[q], y[q][0], y[q][1]);
       } else {
