@@ -24,6 +24,7 @@
 //  * optional: column sums of A_0 (the bias gradient) and B_0^T v for a [P] vector v (the sdf row of
 //    the output layer, dW8[0, :]) accumulated in fp32 from the loaded values, reduced in fixed order.
 #include <algorithm>
+#include <cstdlib>
 #include "nr_common.h"
 
 namespace nr {
@@ -83,10 +84,13 @@ __device__ __forceinline__ float quad_max(float v) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
-// power-of-two exponent e with M * 2^e < 2^14 (0 for M = 0 / inf / NaN)
+// power-of-two exponent e with M * 2^e < 2^14 (0 for M = 0 / inf / NaN), at most 100: a quad of tiny
+// values (|v| < 2^-86, e.g. adjoints of points the loss does not see) would otherwise get an
+// infinite scale 2^e (and 0 * inf = NaN); capped, such values flush to zero in f16 -- contributions
+// below 2^-86 of the operand scale
 __device__ __forceinline__ int split_exp(float M) {
   if (!(M > 0.0f) || __builtin_isinf(M)) return 0;
-  return 14 - __builtin_amdgcn_frexp_expf(M);
+  return min(14 - __builtin_amdgcn_frexp_expf(M), 100);
 }
 
 // v * 2^e -> (hi, lo) f16 pairs, 4 values: 8 B each plane
@@ -365,7 +369,11 @@ int nr_wgrad(const NrWgrad* w, void* stream) {
     NR_REQUIRE(w->a[q] && w->b[q] && w->lda[q] >= w->m && w->ldb[q] >= w->n, NR_ERR_ARG,
                "nr_wgrad: null operand or leading dimension below its column count");
   NR_REQUIRE(!w->vec || w->avec, NR_ERR_ARG, "nr_wgrad: vec output without avec");
-  const WgPlan p = wgrad_plan(w->P, w->m, w->n, w->npairs);
+  WgPlan p = wgrad_plan(w->P, w->m, w->n, w->npairs);
+  if (const char* e = getenv("NR_WGRAD_SLICES")) {  // measurement knob (tools/wgrad_bench.py): fewer slices
+    const int s = atoi(e);
+    if (s > 0 && s < p.S) p.S = s;
+  }
   NR_REQUIRE(w->workspace && w->workspace_bytes >= p.part_bytes + p.cs_bytes + p.vec_bytes, NR_ERR_WORKSPACE,
              "nr_wgrad: workspace too small (nr_wgrad_workspace_bytes)");
   hipStream_t st = (hipStream_t)stream;

@@ -118,3 +118,26 @@ def test_wgrad_timing_vs_hipblaslt():
     print(f'weight gradient, 2 x [65536, 256]^T [65536, 256]: nr_wgrad {us_hip:.1f} us ({gb / us_hip * 1e6 / 1e3:.2f} TB/s '
           f'of operands, bias gradient fused), hipBLASLt split-K bmm + sum {us_blas:.1f} us; one pair: nr_wgrad '
           f'{us_hip1:.1f} us, hipBLASLt {us_blas1:.1f} us')
+
+
+def test_wgrad_tiny_and_zero_quads():
+    """column quads whose values are all zero, tiny (1e-30, below the scale cap) or denormal in some
+    32-row blocks (adjoints of points the loss does not see): finite results equal to the float64 product
+    up to the tiny values' share"""
+    from neurecon_amd.training import _wg
+    g = torch.Generator().manual_seed(11)
+    P = 4096
+    a = torch.randn(P, 256, generator=g)
+    b = torch.randn(P, 256, generator=g)
+    a[:, 4:8] = 0.0                      # a zero quad
+    a[:64, 8:12] *= 1e-30                # tiny in two k-steps, normal elsewhere
+    a[:, 12:16] = 1e-40                  # denormal everywhere
+    b[32:96, 16:20] = 0.0
+    b[:, 20:24] *= 1e-35
+    a, b = a.cuda(), b.cuda()
+    out = _wg([(a, b)])
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    ref = a.double().t() @ b.double()
+    sc = float(ref.abs().max())
+    assert float((out.double() - ref).abs().max()) <= 1e-5 * sc

@@ -1,0 +1,43 @@
+"""nr_wgrad timing on the training step's main shape (P = 65536, 256 x 256, one and two pairs) vs the
+split-K hipBLASLt product it replaces; run under rocprofv3 --kernel-trace --stats to split the
+kernel from its reduction.  NR_WGRAD_SLICES=<S> overrides the slice count (fewer, larger slices)."""
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    from neurecon_amd.training import _wg, _wgrad, _wgrad2
+    g = torch.Generator().manual_seed(3)
+    P = 65536
+    a1, b1, a2, b2 = (torch.randn(P, 256, generator=g).cuda() for _ in range(4))
+    cs = torch.empty(256, device='cuda')
+
+    def t(fn, reps=20):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e3
+    for name, fn in (('nr_wgrad 1 pair', lambda: _wg([(a1, b1)], colsum=cs)),
+                     ('nr_wgrad 2 pairs', lambda: _wg([(a1, b1), (a2, b2)], colsum=cs)),
+                     ('hipBLASLt 1 pair', lambda: _wgrad(a1, b1)),
+                     ('hipBLASLt 2 pairs', lambda: _wgrad2(a1, b1, a2, b2))):
+        us = t(fn)
+        npairs = 2 if '2' in name else 1
+        print(f'{name}: {us:.1f} us, {npairs * 2 * P * 256 * 4 / us / 1e6:.2f} TB/s of operands '
+              f'(NR_WGRAD_SLICES={os.environ.get("NR_WGRAD_SLICES", "-")})', flush=True)
+
+
+if __name__ == '__main__':
+    main()
