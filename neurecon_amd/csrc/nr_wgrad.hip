@@ -107,15 +107,34 @@ __device__ __forceinline__ void split4(float4 v, float sc, uint2& h, uint2& l) {
   l = make_uint2(__builtin_bit_cast(uint32_t, h2{ll[0], ll[1]}), __builtin_bit_cast(uint32_t, h2{ll[2], ll[3]}));
 }
 
+// Operand loads go through buffer resources: an offset past the resource's size reads as zero, so
+// rows past P, columns past the operand's width and idle waves cost one v_cndmask on the offset and no
+// branch (a divergent branch around a load makes the compiler wait for every load in flight, which
+// defeats the two-k-step prefetch).  Each operand spans < 2^31 bytes (checked on the host).
+constexpr uint32_t kOob = 0x80000000u;
+constexpr int kRsrcFlags = 0x00020000;  // gfx9 buffer resource word 3 (32-bit dword format)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, kRsrcFlags);
+}
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// 4 consecutive columns [c, c + 4) of row r, zero outside [0, P) x [0, ncol).  VEC: ncol % 4 == 0 and
+// 16-byte aligned rows (one dwordx4); otherwise four dwords
 template <bool VEC>
-__device__ __forceinline__ float4 ld4(const float* base, int64_t ld, int64_t r, int c, int64_t P, int ncol) {
-  if (r >= P || c >= ncol) return make_float4(0.f, 0.f, 0.f, 0.f);
-  const float* p = base + r * ld + c;
-  if (VEC && c + 3 < ncol) {  // streamed once from HBM: non-temporal
-    const f32x4 v = __builtin_nontemporal_load((const f32x4*)p);
+__device__ __forceinline__ float4 ld4(__amdgpu_buffer_rsrc_t rs, int64_t ld, int64_t r, int c, int64_t P, int ncol,
+                                      bool on) {
+  const bool ok = on && r < P && c < ncol;
+  const uint32_t o = (uint32_t)(r * ld + c) * 4u;
+  if constexpr (VEC) {
+    const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? o : kOob, 0, 0);
+    return make_float4(__int_as_float(v[0]), __int_as_float(v[1]), __int_as_float(v[2]), __int_as_float(v[3]));
+  } else {
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      v[e] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ok && c + e < ncol ? o + 4u * e : kOob, 0, 0));
     return make_float4(v[0], v[1], v[2], v[3]);
   }
-  return make_float4(p[0], c + 1 < ncol ? p[1] : 0.f, c + 2 < ncol ? p[2] : 0.f, c + 3 < ncol ? p[3] : 0.f);
 }
 
 __device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
@@ -172,17 +191,22 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
   // B lane -> column quad (lane & 3) of the wave's 16 columns, rows (lane >> 2) + 16 j
   const int ac = 32 * w + 4 * (lane & 7), ar = lane >> 3;
   const int bc = 16 * w + 4 * (lane & 3), br = lane >> 2;
+  const __amdgpu_buffer_rsrc_t ra0 = rsrc(a.a[0], a.P * a.lda[0] * 4), rb0 = rsrc(a.b[0], a.P * a.ldb[0] * 4);
+  const __amdgpu_buffer_rsrc_t ra1 = a.npairs > 1 ? rsrc(a.a[1], a.P * a.lda[1] * 4) : ra0;
+  const __amdgpu_buffer_rsrc_t rb1 = a.npairs > 1 ? rsrc(a.b[1], a.P * a.ldb[1] * 4) : rb0;
+  const __amdgpu_buffer_rsrc_t rv = rsrc(a.avec ? a.avec : a.a[0], a.avec ? a.P * a.ldv * 4 : 0);
   auto load = [&](int64_t ks, WgRegs& R) {
-    const int q = (int)(ks / a.KP);
-    const int64_t r0 = (ks % a.KP) * kWgK;
+    const int q = ks >= a.KP;
+    const int64_t r0 = (ks - (q ? a.KP : 0)) * kWgK;
+    const int64_t lda = q ? a.lda[1] : a.lda[0], ldb = q ? a.ldb[1] : a.ldb[0];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      R.va[j] = wvalid ? ld4<VA>(a.a[q], a.lda[q], r0 + ar + 8 * j, m0 + ac, a.P, a.m) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = 0; j < 4; ++j) R.va[j] = ld4<VA>(q ? ra1 : ra0, lda, r0 + ar + 8 * j, m0 + ac, a.P, a.m, wvalid);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int64_t r = r0 + br + 16 * j;
-      R.vb[j] = ld4<VB>(a.b[q], a.ldb[q], r, n0 + bc, a.P, a.n);
-      R.vv[j] = (want_vec && q == 0 && r < a.P) ? a.avec[r * a.ldv] : 0.0f;
+      R.vb[j] = ld4<VB>(q ? rb1 : rb0, ldb, r, n0 + bc, a.P, a.n, true);
+      R.vv[j] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          rv, want_vec && q == 0 && r < a.P ? (uint32_t)(r * a.ldv) * 4u : kOob, 0, 0));
     }
     R.q = q;
   };
@@ -301,28 +325,73 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
   }
 }
 
-// C[i, j] = scale * sum_s part[s][j][i] (i < m, j < n), slices in order; column sums and the vector
-// product likewise
-__global__ void wgrad_reduce(const float* __restrict__ part, int S, int m, int n, int64_t ldp, int64_t ldn, float scale,
-                             float* __restrict__ c, int64_t ldc, const float* __restrict__ part_cs, float* cs,
-                             const float* __restrict__ part_vec, float* vec, float vscale) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t total = (int64_t)m * n;
-  if (idx < total) {
-    const int64_t j = idx / m, i = idx % m;
-    float s = 0.0f;
-    for (int k = 0; k < S; ++k) s += part[(int64_t)k * ldn * ldp + j * ldp + i];
-    c[i * ldc + j] = s * scale;
+// C[i, j] = scale * sum_s part[s][j][i] (i < m, j < n), deterministic: a block takes 32 float4 groups of
+// (j, 4 consecutive i); its 8 thread groups sum the slices s = g, g + 8, g + 16, ... in order, then the
+// 8 group sums are added in group order.  The last blocks do the same for the column sums of A_0 and
+// the vector row (one float per thread instead of a float4).
+constexpr int kRedGroups = 8;
+struct WgRedArgs {
+  const float* part;
+  int S, m, n;
+  int64_t ldp, ldn;
+  float scale;
+  float* c;
+  int64_t ldc;
+  int nb_c, nb_cs;          // blocks for C, then for the column sums; the rest for the vector row
+  const float* part_cs;
+  float* cs;
+  const float* part_vec;
+  float* vec;
+  float vscale;
+};
+
+__global__ __launch_bounds__(256) void wgrad_reduce(WgRedArgs r) {
+  __shared__ float4 acc[kRedGroups][32];
+  const int t = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int b = blockIdx.x;
+  if (b < r.nb_c) {
+    const int64_t q = (int64_t)b * 32 + t;  // float4 group: j = q / (ldp / 4), i = 4 (q % (ldp / 4))
+    const int64_t qpr = r.ldp / 4, nq = (int64_t)r.n * qpr;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (q < nq) {
+      const float4* p = (const float4*)r.part + q;
+      const int64_t stride = r.ldn * qpr;  // one slice, in float4
+#pragma unroll 4
+      for (int k = g; k < r.S; k += kRedGroups) s = add4(s, p[(int64_t)k * stride]);
+    }
+    acc[g][t] = s;
+    __syncthreads();
+    if (g == 0 && q < nq) {
+      float4 v = acc[0][t];
+#pragma unroll
+      for (int k = 1; k < kRedGroups; ++k) v = add4(v, acc[k][t]);
+      const int64_t j = q / qpr, i = 4 * (q % qpr);
+      const float e4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (i + e < r.m) r.c[(i + e) * r.ldc + j] = e4[e] * r.scale;
+    }
+    return;
   }
-  if (cs && idx < m) {
-    float s = 0.0f;
-    for (int k = 0; k < S; ++k) s += part_cs[(int64_t)k * ldp + idx];
-    cs[idx] = s;
+  // a column sum (index < m, slices ldp apart) or a vector-row entry (index < n, slices ldn apart)
+  const bool is_cs = b < r.nb_c + r.nb_cs;
+  const int64_t idx = (int64_t)(b - (is_cs ? r.nb_c : r.nb_c + r.nb_cs)) * 32 + t;
+  const int len = is_cs ? r.m : r.n;
+  const int64_t ld = is_cs ? r.ldp : r.ldn;
+  const float* p = is_cs ? r.part_cs : r.part_vec;
+  float s = 0.0f;
+  if (idx < len) {
+#pragma unroll 4
+    for (int k = g; k < r.S; k += kRedGroups) s += p[(int64_t)k * ld + idx];
   }
-  if (vec && idx < n) {
-    float s = 0.0f;
-    for (int k = 0; k < S; ++k) s += part_vec[(int64_t)k * ldn + idx];
-    vec[idx] = s * vscale;
+  acc[g][t].x = s;
+  __syncthreads();
+  if (g == 0 && idx < len) {
+    float v = acc[0][t].x;
+#pragma unroll
+    for (int k = 1; k < kRedGroups; ++k) v += acc[k][t].x;
+    if (is_cs) r.cs[idx] = v;
+    else r.vec[idx] = v * r.vscale;
   }
 }
 
@@ -369,6 +438,12 @@ int nr_wgrad(const NrWgrad* w, void* stream) {
     NR_REQUIRE(w->a[q] && w->b[q] && w->lda[q] >= w->m && w->ldb[q] >= w->n, NR_ERR_ARG,
                "nr_wgrad: null operand or leading dimension below its column count");
   NR_REQUIRE(!w->vec || w->avec, NR_ERR_ARG, "nr_wgrad: vec output without avec");
+  {  // operands are read through buffer resources with 32-bit byte offsets
+    const int64_t lim = (int64_t)1 << 31;
+    bool fits = !w->avec || w->P * std::max<int64_t>(w->ldv, 1) * 4 < lim;
+    for (int q = 0; q < w->npairs; ++q) fits = fits && w->P * w->lda[q] * 4 < lim && w->P * w->ldb[q] * 4 < lim;
+    NR_REQUIRE(fits, NR_ERR_ARG, "nr_wgrad: an operand spans 2 GiB or more (split the rows over calls)");
+  }
   WgPlan p = wgrad_plan(w->P, w->m, w->n, w->npairs);
   if (const char* e = getenv("NR_WGRAD_SLICES")) {  // measurement knob (tools/wgrad_bench.py): fewer slices
     const int s = atoi(e);
@@ -383,8 +458,8 @@ int nr_wgrad(const NrWgrad* w, void* stream) {
   for (int q = 0; q < w->npairs; ++q) {
     k.a[q] = w->a[q]; k.lda[q] = w->lda[q];
     k.b[q] = w->b[q]; k.ldb[q] = w->ldb[q];
-    va = va && w->lda[q] % 4 == 0 && ((uintptr_t)w->a[q] & 15) == 0;
-    vb = vb && w->ldb[q] % 4 == 0 && ((uintptr_t)w->b[q] & 15) == 0;
+    va = va && w->m % 4 == 0 && w->lda[q] % 4 == 0 && ((uintptr_t)w->a[q] & 15) == 0;
+    vb = vb && w->n % 4 == 0 && w->ldb[q] % 4 == 0 && ((uintptr_t)w->b[q] & 15) == 0;
   }
   k.npairs = w->npairs; k.P = w->P; k.m = w->m; k.n = w->n;
   k.nmt = p.nmt; k.nnt = p.nnt; k.S = p.S; k.KP = p.KP;
@@ -405,9 +480,14 @@ int nr_wgrad(const NrWgrad* w, void* stream) {
     NR_HIP_CHECK(hipGetLastError());
   }
   const int64_t ldp = (int64_t)p.nmt * kWgM, ldn = (int64_t)p.nnt * kWgN;
-  const int64_t total = std::max<int64_t>({(int64_t)w->m * w->n, (int64_t)w->m, (int64_t)w->n});
-  hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, k.part, p.S, w->m, w->n,
-                     ldp, ldn, w->scale, w->c, w->ldc, k.part_cs, w->colsum, k.part_vec, w->vec, w->vec_scale);
+  WgRedArgs r{};
+  r.part = k.part; r.S = p.S; r.m = w->m; r.n = w->n; r.ldp = ldp; r.ldn = ldn;
+  r.scale = w->scale; r.c = w->c; r.ldc = w->ldc;
+  r.nb_c = (int)((w->n * (ldp / 4) + 31) / 32);
+  r.nb_cs = w->colsum ? (w->m + 31) / 32 : 0;
+  const int nb_vec = w->vec ? (w->n + 31) / 32 : 0;
+  r.part_cs = k.part_cs; r.cs = w->colsum; r.part_vec = k.part_vec; r.vec = w->vec; r.vscale = w->vec_scale;
+  hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)(r.nb_c + r.nb_cs + nb_vec)), dim3(256), 0, st, r);
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;
 }
