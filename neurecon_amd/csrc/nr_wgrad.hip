@@ -74,23 +74,29 @@ __device__ __forceinline__ f16x8 frag(const _Float16* plane, int stride, int col
   return r;
 }
 
-// max over lanes l ^ 8, l ^ 16, l ^ 32 (and l ^ 4 with FOUR): ds_swizzle within 32 lanes, then the halves
+// max over lanes l ^ 8, l ^ 16, l ^ 32 (and l ^ 4 with FOUR), all VALU: DPP row rotations within each
+// 16-lane row (by 4 and 8: the set {l, l +- 4, l + 8}; by 8: {l, l ^ 8}), then permlane16 / permlane32
+// swaps (a wave-wide max of the pair (v, swapped v) is the max over l and l ^ 16, resp. l ^ 32)
 template <bool FOUR>
 __device__ __forceinline__ float quad_max(float v) {
-  if constexpr (FOUR) v = fmaxf(v, __uint_as_float(__builtin_amdgcn_ds_swizzle(__float_as_uint(v), 0x101F)));
-  v = fmaxf(v, __uint_as_float(__builtin_amdgcn_ds_swizzle(__float_as_uint(v), 0x201F)));
-  v = fmaxf(v, __uint_as_float(__builtin_amdgcn_ds_swizzle(__float_as_uint(v), 0x401F)));
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  if constexpr (FOUR)
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false)));
+  const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+  const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
 }
 
-// power-of-two exponent e with M * 2^e < 2^14 (0 for M = 0 / inf / NaN), at most 100: a quad of tiny
-// values (|v| < 2^-86, e.g. adjoints of points the loss does not see) would otherwise get an
+// power-of-two exponent e with M * 2^e < 2^14, at most kExpCap (also for M = 0 / inf / NaN): a quad of
+// tiny values (|v| < 2^-86, e.g. adjoints of points the loss does not see) would otherwise get an
 // infinite scale 2^e (and 0 * inf = NaN); capped, such values flush to zero in f16 -- contributions
 // below 2^-86 of the operand scale
+constexpr int kExpCap = 100;
+constexpr int kHeadroom = 4;
 __device__ __forceinline__ int split_exp(float M) {
-  if (!(M > 0.0f) || __builtin_isinf(M)) return 0;
-  return min(14 - __builtin_amdgcn_frexp_expf(M), 100);
+  if (!(M > 0.0f) || __builtin_isinf(M)) return kExpCap;
+  return min(14 - __builtin_amdgcn_frexp_expf(M), kExpCap);
 }
 
 // v * 2^e -> (hi, lo) f16 pairs, 4 values: 8 B each plane
@@ -107,10 +113,12 @@ __device__ __forceinline__ void split4(float4 v, float sc, uint2& h, uint2& l) {
   l = make_uint2(__builtin_bit_cast(uint32_t, h2{ll[0], ll[1]}), __builtin_bit_cast(uint32_t, h2{ll[2], ll[3]}));
 }
 
-// Operand loads go through buffer resources: an offset past the resource's size reads as zero, so
-// rows past P, columns past the operand's width and idle waves cost one v_cndmask on the offset and no
-// branch (a divergent branch around a load makes the compiler wait for every load in flight, which
-// defeats the two-k-step prefetch).  Each operand spans < 2^31 bytes (checked on the host).
+// Operand loads go through buffer resources rebased at each k-step's first row and sized to the rows
+// left before P: an offset past the size reads as zero, so rows past P need no test; a lane whose
+// columns lie past the operand's width (or an idle wave) uses an out-of-range offset.  The per-lane
+// offsets are loop invariant, so a k-step's loads cost no vector ALU and no branch (a divergent branch
+// around a load makes the compiler wait for every load in flight, which defeats the prefetch).  Each
+// operand spans < 2^31 bytes (checked on the host).
 constexpr uint32_t kOob = 0x80000000u;
 constexpr int kRsrcFlags = 0x00020000;  // gfx9 buffer resource word 3 (32-bit dword format)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int64_t bytes) {
@@ -118,21 +126,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int64_t b
 }
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-// 4 consecutive columns [c, c + 4) of row r, zero outside [0, P) x [0, ncol).  VEC: ncol % 4 == 0 and
-// 16-byte aligned rows (one dwordx4); otherwise four dwords
+// byte offset of (row, col) in a row-major operand, or kOob when the lane is off / col >= ncol
+__device__ __forceinline__ uint32_t lane_off(int row, int col, int64_t ld, int ncol, bool on) {
+  return on && col < ncol ? (uint32_t)(row * ld + col) * 4u : kOob;
+}
+
+// 4 consecutive columns at byte offset o (kOob: zeros).  VEC: ncol % 4 == 0 and 16-byte aligned rows
+// (one dwordx4); otherwise four dwords, each tested against ncol (c = the first column)
 template <bool VEC>
-__device__ __forceinline__ float4 ld4(__amdgpu_buffer_rsrc_t rs, int64_t ld, int64_t r, int c, int64_t P, int ncol,
-                                      bool on) {
-  const bool ok = on && r < P && c < ncol;
-  const uint32_t o = (uint32_t)(r * ld + c) * 4u;
+__device__ __forceinline__ float4 ld4(__amdgpu_buffer_rsrc_t rs, uint32_t o, int c, int ncol) {
   if constexpr (VEC) {
-    const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? o : kOob, 0, 0);
+    const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
     return make_float4(__int_as_float(v[0]), __int_as_float(v[1]), __int_as_float(v[2]), __int_as_float(v[3]));
   } else {
     float v[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-      v[e] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ok && c + e < ncol ? o + 4u * e : kOob, 0, 0));
+      v[e] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o != kOob && c + e < ncol ? o + 4u * e : kOob, 0, 0));
     return make_float4(v[0], v[1], v[2], v[3]);
   }
 }
@@ -158,7 +168,10 @@ struct WgRegs {
 template <bool VA, bool VB>
 __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * kStage];
-  __shared__ float s_inv[2][64 + 32];  // per stage: 2^-e of the 64 A column quads, then the 32 B quads
+  // per stage: the rescale ratios 2^(e_new - e_old) of the 64 A column quads, then the 32 B quads, and
+  // one byte per wave: "a B quad this wave loads lowered its exponent"; [2]: the final 2^-e
+  __shared__ float s_rat[3][64 + 32];
+  __shared__ __attribute__((aligned(8))) unsigned char s_chg[2][8];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int NT = a.nmt * a.nnt;
   // block -> (slice, m tile, n tile): with S % 8 == 0 the tiles of one slice share an XCD
@@ -191,32 +204,67 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
   // B lane -> column quad (lane & 3) of the wave's 16 columns, rows (lane >> 2) + 16 j
   const int ac = 32 * w + 4 * (lane & 7), ar = lane >> 3;
   const int bc = 16 * w + 4 * (lane & 3), br = lane >> 2;
-  const __amdgpu_buffer_rsrc_t ra0 = rsrc(a.a[0], a.P * a.lda[0] * 4), rb0 = rsrc(a.b[0], a.P * a.ldb[0] * 4);
-  const __amdgpu_buffer_rsrc_t ra1 = a.npairs > 1 ? rsrc(a.a[1], a.P * a.lda[1] * 4) : ra0;
-  const __amdgpu_buffer_rsrc_t rb1 = a.npairs > 1 ? rsrc(a.b[1], a.P * a.ldb[1] * 4) : rb0;
-  const __amdgpu_buffer_rsrc_t rv = rsrc(a.avec ? a.avec : a.a[0], a.avec ? a.P * a.ldv * 4 : 0);
-  auto load = [&](int64_t ks, WgRegs& R) {
+  // loop-invariant lane offsets within a k-step's rows, per pair (the pairs may differ in leading dims)
+  uint32_t oa[2][4], ob[2][2], ov[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int qq = q < a.npairs ? q : 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) oa[q][j] = lane_off(ar + 8 * j, m0 + ac, a.lda[qq], a.m, wvalid);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) ob[q][j] = lane_off(br + 16 * j, n0 + bc, a.ldb[qq], a.n, true);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) ov[j] = want_vec ? (uint32_t)((br + 16 * j) * a.ldv) * 4u : kOob;
+  // live = false (past the slice's last k-step): zero-sized resources, the loads return zeros and touch
+  // no memory.  Issued unconditionally, so the compiler counts the loads in flight exactly (a
+  // conditional prefetch makes it wait for all of them)
+  auto load = [&](int64_t ks, WgRegs& R, bool live) {
+#ifdef NR_WG_EXP_NO_LOAD
+    const float x = (float)(ks & 7) + 0.5f;
+    for (int j = 0; j < 4; ++j) R.va[j] = make_float4(x, x, x, x);
+    for (int j = 0; j < 2; ++j) { R.vb[j] = make_float4(x, x, x, x); R.vv[j] = x; }
+    R.q = 0;
+    return;
+#endif
+    ks = live ? ks : 0;
     const int q = ks >= a.KP;
     const int64_t r0 = (ks - (q ? a.KP : 0)) * kWgK;
     const int64_t lda = q ? a.lda[1] : a.lda[0], ldb = q ? a.ldb[1] : a.ldb[0];
+    const int64_t rows = live ? a.P - r0 : 0;
+    const __amdgpu_buffer_rsrc_t ra = rsrc((q ? a.a[1] : a.a[0]) + r0 * lda, rows * lda * 4);
+    const __amdgpu_buffer_rsrc_t rb = rsrc((q ? a.b[1] : a.b[0]) + r0 * ldb, rows * ldb * 4);
+    const __amdgpu_buffer_rsrc_t rv = rsrc(a.avec ? a.avec + r0 * a.ldv : a.a[0], a.avec && q == 0 ? rows * a.ldv * 4 : 0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) R.va[j] = ld4<VA>(q ? ra1 : ra0, lda, r0 + ar + 8 * j, m0 + ac, a.P, a.m, wvalid);
+    for (int j = 0; j < 4; ++j) R.va[j] = ld4<VA>(ra, q ? oa[1][j] : oa[0][j], m0 + ac, a.m);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int64_t r = r0 + br + 16 * j;
-      R.vb[j] = ld4<VB>(q ? rb1 : rb0, ldb, r, n0 + bc, a.P, a.n, true);
-      R.vv[j] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-          rv, want_vec && q == 0 && r < a.P ? (uint32_t)(r * a.ldv) * 4u : kOob, 0, 0));
+      R.vb[j] = ld4<VB>(rb, q ? ob[1][j] : ob[0][j], n0 + bc, a.n);
+      R.vv[j] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rv, ov[j], 0, 0));
     }
     R.q = q;
   };
+  [[maybe_unused]] float sink = 0.0f;  // timing experiments only (NR_WG_EXP_NO_STORE keeps the loads alive)
+  // Running per-quad exponents: a quad keeps one scale over the slice (e only decreases), so MFMAs
+  // accumulate straight into acc.  A k-step whose quad max M would reach 2^14 at the current scale
+  // lowers it to put M at 2^(14 - kHeadroom) (16x headroom: later maxima rarely force another change),
+  // and the accumulated tiles of that quad are multiplied by 2^(e_new - e_old); the final 2^-(eA + eB)
+  // is applied once.  A value below the running scale keeps its absolute precision: |error| < 2^-35 of
+  // the quad's running max (the f16 subnormal quantum at a 2^10 scale).
+  int ea_cur = kExpCap, eb_cur = kExpCap;
+  bool cha[2] = {false, false};
   auto store = [&](int stg, const WgRegs& R) {
+#ifdef NR_WG_EXP_NO_STORE
+    sink += R.va[0].x + R.va[1].y + R.va[2].z + R.va[3].w + R.vb[0].x + R.vb[1].w + R.vv[0] + R.vv[1];
+    return;
+#endif
     _Float16* S0 = lds + stg * kStage;
     if (want_cs && R.q == 0) cs = add4(cs, add4(add4(R.va[0], R.va[1]), add4(R.va[2], R.va[3])));
     if (want_vec && R.q == 0) vs = fma4(R.vv[1], R.vb[1], fma4(R.vv[0], R.vb[0], vs));
     // per column quad: the max over its 32 rows (this lane's 4 rows x 8 lanes) -> power-of-two scale
     const float ma = quad_max<false>(fmaxf(fmaxf(amax4(R.va[0]), amax4(R.va[1])), fmaxf(amax4(R.va[2]), amax4(R.va[3]))));
-    const int ea = split_exp(ma);
+    const int ta = split_exp(ma);
+    const int ea = ta < ea_cur ? ta - kHeadroom : ea_cur;
     const float sa = __builtin_ldexpf(1.0f, ea);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -226,9 +274,12 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
       *(uint2*)(S0 + o) = h;
       *(uint2*)(S0 + kAPlane + o) = l;
     }
-    if (lane < 8) s_inv[stg][ac >> 2] = __builtin_ldexpf(1.0f, -ea);
+    if (lane < 8) s_rat[stg][ac >> 2] = __builtin_ldexpf(1.0f, ea - ea_cur);
+    cha[stg] = __builtin_amdgcn_ballot_w64(ea != ea_cur) != 0;  // this wave's A quads = its output rows
+    ea_cur = ea;
     const float mb = quad_max<true>(fmaxf(amax4(R.vb[0]), amax4(R.vb[1])));
-    const int eb = split_exp(mb);
+    const int tb = split_exp(mb);
+    const int eb = tb < eb_cur ? tb - kHeadroom : eb_cur;
     const float sb = __builtin_ldexpf(1.0f, eb);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -238,74 +289,99 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
       *(uint2*)(S0 + 2 * kAPlane + o) = h;
       *(uint2*)(S0 + 2 * kAPlane + kBPlane + o) = l;
     }
-    if (lane < 4) s_inv[stg][64 + (bc >> 2)] = __builtin_ldexpf(1.0f, -eb);
+    if (lane < 4) s_rat[stg][64 + (bc >> 2)] = __builtin_ldexpf(1.0f, eb - eb_cur);
+    const bool chb = __builtin_amdgcn_ballot_w64(eb != eb_cur) != 0;
+    if (lane == 0) s_chg[stg][w] = chb ? 1 : 0;
+    eb_cur = eb;
+  };
+  const int G = lane >> 4, col = lane & 15;
+  // multiply each output tile by its A quad's and its B quad's factor in table s_rat[tab]
+  auto rescale = [&](int tab) {
+    const float fa0 = s_rat[tab][8 * w + G], fa1 = s_rat[tab][8 * w + 4 + G];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float fb = s_rat[tab][64 + 4 * j + (col >> 2)];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        acc[0][j][r] = acc[0][j][r] * fa0 * fb;
+        acc[1][j][r] = acc[1][j][r] * fa1 * fb;
+      }
+    }
   };
   auto compute = [&](int stg) {
     if (!wvalid) return;
+#ifdef NR_WG_EXP_NO_MFMA
+    return;
+#endif
+    uint64_t chb;
+    __builtin_memcpy(&chb, s_chg[stg], 8);
+    if (cha[stg] || chb != 0) rescale(stg);  // wave-uniform
     const _Float16* S0 = lds + stg * kStage;
-    const int G = lane >> 4, col = lane & 15;
     f16x8 ah[2], al[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       ah[i] = frag(S0, kAStride, 32 * w + 16 * i, lane);
       al[i] = frag(S0 + kAPlane, kAStride, 32 * w + 16 * i, lane);
     }
-    // unscale factors: output rows 4G..4G+3 of m block i are one A column quad, column col of n block j
-    // one B quad
-    const float ia0 = s_inv[stg][8 * w + G], ia1 = s_inv[stg][8 * w + 4 + G];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const f16x8 bh = frag(S0 + 2 * kAPlane, kBStride, 16 * j, lane);
       const f16x8 bl = frag(S0 + 2 * kAPlane + kBPlane, kBStride, 16 * j, lane);
-      const float ib = s_inv[stg][64 + 4 * j + (col >> 2)];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        f32x4 tt = f32x4{0.f, 0.f, 0.f, 0.f};
-        tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh, tt, 0, 0, 0);
-        tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl, tt, 0, 0, 0);
-        tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh, tt, 0, 0, 0);
-        const float f = (i ? ia1 : ia0) * ib;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = fmaf(tt[r], f, acc[i][j][r]);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh, acc[i][j], 0, 0, 0);
       }
     }
   };
 
-  // two k-steps of loads in flight: while k-step ks runs its MFMAs from LDS stage ks & 1, the
-  // registers hold k-step ks + 1 (split into the other stage after the MFMAs) and k-step ks + 2 loads
-  WgRegs R0, R1;
-  if (k0 < k1) {
-    load(k0, R0);
-    if (k0 + 1 < k1) load(k0 + 1, R1);
-    store(0, R0);
-  }
+  // three k-steps of loads in flight: while k-step ks runs its MFMAs from LDS stage ks & 1, register set
+  // (ks + 1) % 3 holds k-step ks + 1 (split into the other stage after the MFMAs) and the two other sets
+  // k-steps ks + 2 and ks + 3 (the set k-step ks came from is refilled first).  Unrolled by 6 = lcm(2, 3).
+  // Loads past the slice's end are dead (zeros, no memory); stores past it fill a stage nobody reads.
+  WgRegs R0, R1, R2;
+  load(k0, R0, k0 < k1);
+  load(k0 + 1, R1, k0 + 1 < k1);
+  load(k0 + 2, R2, k0 + 2 < k1);
+  store(0, R0);
   __syncthreads();
   int64_t ks = k0;
+  auto step = [&](int stg, WgRegs& refill, WgRegs& next) {
+    load(ks + 3, refill, ks + 3 < k1);
+    compute(stg);
+    store(stg ^ 1, next);
+    __syncthreads();
+    return ++ks < k1;
+  };
   while (ks < k1) {
-    // even step: compute stage 0, R1 holds ks + 1, refill R0 with ks + 2
-    if (ks + 2 < k1) load(ks + 2, R0);
-    compute(0);
-    if (ks + 1 < k1) store(1, R1);
-    __syncthreads();
-    if (++ks >= k1) break;
-    // odd step: compute stage 1, R0 holds ks + 1, refill R1 with ks + 2
-    if (ks + 2 < k1) load(ks + 2, R1);
-    compute(1);
-    if (ks + 1 < k1) store(0, R0);
-    __syncthreads();
-    ++ks;
+    if (!step(0, R0, R1)) break;
+    if (!step(1, R1, R2)) break;
+    if (!step(0, R2, R0)) break;
+    if (!step(1, R0, R1)) break;
+    if (!step(0, R1, R2)) break;
+    if (!step(1, R2, R0)) break;
   }
+  // the final exponents -> 2^-e per quad, applied once (two factors: 2^-(eA + eB) can underflow)
+  if (lane < 8) s_rat[2][ac >> 2] = __builtin_ldexpf(1.0f, -ea_cur);
+  if (lane < 4) s_rat[2][64 + (bc >> 2)] = __builtin_ldexpf(1.0f, -eb_cur);
+  __syncthreads();
+#ifndef NR_WG_EXP_NO_MFMA
+  if (wvalid) rescale(2);
+#endif
 
   // partial tile: lane (G, col) register r holds row 4G + r of each 16 x 16 tile -> part[s][n][m]
   const int64_t ldp = (int64_t)a.nmt * kWgM;
   float* P0 = a.part + (int64_t)slice * (a.nnt * kWgN) * ldp;
   {
-    const int G = lane >> 4, col = lane & 15;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int64_t nn = n0 + 16 * j + col, mm = m0 + 32 * w + 16 * i + 4 * G;
+#ifdef NR_WG_EXP_NO_STORE
+        acc[i][j][0] += sink;
+#endif
         *(float4*)(P0 + nn * ldp + mm) = wvalid ? make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3])
                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
       }

@@ -76,6 +76,11 @@ VARIANTS = {
     'sldnt': ['-DNR_SLAB_LD_POL=" nt"'],      # the default since r03
     'sldt': ['-DNR_SLAB_LD_POL=""'],          # slab loads with the default policy (the r02 build)
     'sldnt_fnt': ['-DNR_SLAB_LD_POL=" nt"', '-DNR_FEAT_NT=true'],
+    # nr_wgrad cost split (results NOT valid): no MFMA / no split+LDS store / no global loads
+    'wg_nomfma': ['-DNR_WG_EXP_NO_MFMA'],
+    'wg_nostore': ['-DNR_WG_EXP_NO_STORE'],
+    'wg_loadonly': ['-DNR_WG_EXP_NO_MFMA', '-DNR_WG_EXP_NO_STORE'],
+    'wg_noload': ['-DNR_WG_EXP_NO_LOAD'],
 }
 
 

@@ -1,5 +1,6 @@
 #!/bin/bash
-# SQ/GRBM counter passes (<= 8 SQ counters per pass, kernel-trace only) over tools/mlp_driver.py.
+# SQ/GRBM counter passes (<= 8 SQ counters per pass, kernel-trace only) over tools/mlp_driver.py
+# (DRIVER=tools/wgrad_bench.py for another driver script).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 TAG=${TAG:-sq}
@@ -13,6 +14,6 @@ for SET in \
   "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum SQ_WAIT_INST_LDS SQ_INSTS_FLAT SQ_WAVES SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_LDS" ; do
   i=$((i+1))
   timeout -k 10 ${T_PROF:-300} rocprofv3 --pmc $SET --kernel-trace --output-format csv -d $OUT/p$i -o run \
-    -- python3 tools/mlp_driver.py ${DRIVER_ARGS} > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+    -- python3 ${DRIVER:-tools/mlp_driver.py} ${DRIVER_ARGS} > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
 python3 tools/pmc_sq_summary.py $OUT > $OUT/summary.txt && cat $OUT/summary.txt
