@@ -48,7 +48,7 @@ RAY_FLOP_REF = 704.8e6
 RAY_FLOP = 2.0 * (255 * (MAC_SDF_FWD + MAC_SDF_BWD) + 127 * MAC_RAD)
 # HBM-side bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc passes of this bench,
 # tools/gpu_pmc.sh); counters cannot be read live, so the latest committed summary is reported.
-PMC_SUMMARY = {'f16x3': 'profiles/r03/f16x3_pmc_summary.json'}  # refreshed with tools/gpu_pmc.sh (TAG=r03)
+PMC_SUMMARY = {'f16x3': 'profiles/r04/f16x3_pmc_summary.json'}  # tools/gpu_prof_r04.sh (PMC passes of the default bench)
 # device kernels behind each merged library kernel name (sdf_nabla = samples + mid-points launches)
 PMC_KERNEL = {('sdf_nabla', 'f16x3'): ('void nr::sdf4_kernel<true, false>(nr::SdfKArgs)',       # r02 names
                                        'void nr::sdf4_kernel<true, true>(nr::SdfKArgs)',
