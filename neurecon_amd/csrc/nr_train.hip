@@ -71,25 +71,52 @@ __global__ void embed_jvp_kernel(const float* __restrict__ x, const float* __res
 
 // J_emb(x)^T (e0 + s1 e1) -> [P, 3] (autograd's Sin/Cos backward then the Mul by the frequency,
 // contributions summed in feature order)
+// one feature's contribution to the point's d x (summed in feature order by the caller)
+__device__ __forceinline__ void embed_vjp_acc(int f, float gf, const float (&xp)[3], float (&n)[3]) {
+  if (f < 3) {
+    n[f] = fadd(n[f], gf);
+    return;
+  }
+  const int fp = f - 3, band = fp / 6, m = fp - band * 6, c = m % 3;
+  const float freq = (float)(1 << band);
+  const float a = fmul(xp[c], freq);
+  const float contrib = m < 3 ? fmul(fmul(gf, cosf(a)), freq) : fmul(fmul(gf, -sinf(a)), freq);
+  n[c] = fadd(n[c], contrib);
+}
+
+// VEC: rows read as float4 (ld0 / ld1 multiples of 4 covering the features rounded up to 4, 16-byte
+// aligned): a thread per point walks its own row, so scalar loads touched 64 rows' cache lines per
+// instruction (r04: 62 us for 65 k points); the arithmetic and its order are the same either way
+template <bool VEC>
 __global__ void embed_vjp_kernel(const float* __restrict__ x, const float* __restrict__ e0, int ld0,
                                  const float* __restrict__ e1, int ld1, float s1, int64_t P, int nfreq,
                                  float* __restrict__ out) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
   const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
+  const float xp[3] = {x[p * 3], x[p * 3 + 1], x[p * 3 + 2]};
   float n[3] = {0.f, 0.f, 0.f};
-  for (int f = 0; f < nf; ++f) {
-    float gf = e0[p * ld0 + f];
-    if (e1) gf = fadd(gf, fmul(e1[p * ld1 + f], s1));
-    if (f < 3) {
-      n[f] = fadd(n[f], gf);
-      continue;
+  if constexpr (VEC) {
+    const float4* r0 = (const float4*)(e0 + p * ld0);
+    const float4* r1 = e1 ? (const float4*)(e1 + p * ld1) : nullptr;
+    for (int f4 = 0; f4 < nf; f4 += 4) {
+      const float4 v = r0[f4 >> 2];
+      const float4 u = r1 ? r1[f4 >> 2] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float vv[4] = {v.x, v.y, v.z, v.w}, uu[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (f4 + e >= nf) break;
+        float gf = vv[e];
+        if (r1) gf = fadd(gf, fmul(uu[e], s1));
+        embed_vjp_acc(f4 + e, gf, xp, n);
+      }
     }
-    const int fp = f - 3, band = fp / 6, m = fp - band * 6, c = m % 3;
-    const float freq = (float)(1 << band);
-    const float a = fmul(x[p * 3 + c], freq);
-    const float contrib = m < 3 ? fmul(fmul(gf, cosf(a)), freq) : fmul(fmul(gf, -sinf(a)), freq);
-    n[c] = fadd(n[c], contrib);
+  } else {
+    for (int f = 0; f < nf; ++f) {
+      float gf = e0[p * ld0 + f];
+      if (e1) gf = fadd(gf, fmul(e1[p * ld1 + f], s1));
+      embed_vjp_acc(f, gf, xp, n);
+    }
   }
   out[p * 3 + 0] = n[0];
   out[p * 3 + 1] = n[1];
@@ -981,8 +1008,15 @@ int nr_embed_vjp(const float* x, const float* e0, int ld0, const float* e1, int 
                  float* out, void* stream) {
   NR_REQUIRE(x && e0 && out && P >= 0 && nfreq <= 10, NR_ERR_ARG, "nr_embed_vjp: bad argument");
   if (P == 0) return NR_OK;
-  hipLaunchKernelGGL(embed_vjp_kernel, grid1(P), dim3(kBlk), 0, (hipStream_t)stream, x, e0, ld0, e1, ld1, s1, P,
-                     nfreq, out);
+  const int nf4 = ((nfreq < 0 ? 3 : 3 + 6 * nfreq) + 3) / 4 * 4;
+  const bool vec = ld0 % 4 == 0 && ld0 >= nf4 && ((uintptr_t)e0 & 15) == 0 &&
+                   (!e1 || (ld1 % 4 == 0 && ld1 >= nf4 && ((uintptr_t)e1 & 15) == 0));
+  if (vec)
+    hipLaunchKernelGGL(embed_vjp_kernel<true>, grid1(P), dim3(kBlk), 0, (hipStream_t)stream, x, e0, ld0, e1, ld1, s1,
+                       P, nfreq, out);
+  else
+    hipLaunchKernelGGL(embed_vjp_kernel<false>, grid1(P), dim3(kBlk), 0, (hipStream_t)stream, x, e0, ld0, e1, ld1, s1,
+                       P, nfreq, out);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

@@ -31,6 +31,12 @@ namespace nr {
 
 constexpr int kWgThreads = 512;   // 8 waves: wave w owns output rows [32 w, 32 w + 32) of the m tile
 constexpr int kWgM = 256, kWgN = 128, kWgK = 32;
+#ifndef NR_WG_PP_BIT
+#define NR_WG_PP_BIT 0
+#endif
+// waves w with (w & bit) run the split before the MFMAs; 0 = none (measured r04: splitting the phases
+// between the two waves of a SIMD, bit 4, took 114 us per two-pair call against 104-107 without)
+constexpr int kPingPongBit = NR_WG_PP_BIT;
 constexpr int kAStride = 272;     // halfs per A row in LDS (544 B: 8 rows of a half-wave read land 8 banks apart)
 constexpr int kBStride = 144;     // halfs per B row (288 B, the same property)
 constexpr int kAPlane = kWgK * kAStride;
@@ -219,7 +225,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
   // live = false (past the slice's last k-step): zero-sized resources, the loads return zeros and touch
   // no memory.  Issued unconditionally, so the compiler counts the loads in flight exactly (a
   // conditional prefetch makes it wait for all of them)
-  auto load = [&](int64_t ks, WgRegs& R, bool live) {
+  auto load = [&](int64_t ks, WgRegs& R, bool live) __attribute__((always_inline)) {
 #ifdef NR_WG_EXP_NO_LOAD
     const float x = (float)(ks & 7) + 0.5f;
     for (int j = 0; j < 4; ++j) R.va[j] = make_float4(x, x, x, x);
@@ -253,7 +259,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
   // the quad's running max (the f16 subnormal quantum at a 2^10 scale).
   int ea_cur = kExpCap, eb_cur = kExpCap;
   bool cha[2] = {false, false};
-  auto store = [&](int stg, const WgRegs& R) {
+  auto store = [&](int stg, const WgRegs& R) __attribute__((always_inline)) {
 #ifdef NR_WG_EXP_NO_STORE
     sink += R.va[0].x + R.va[1].y + R.va[2].z + R.va[3].w + R.vb[0].x + R.vb[1].w + R.vv[0] + R.vv[1];
     return;
@@ -296,7 +302,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
   };
   const int G = lane >> 4, col = lane & 15;
   // multiply each output tile by its A quad's and its B quad's factor in table s_rat[tab]
-  auto rescale = [&](int tab) {
+  auto rescale = [&](int tab) __attribute__((always_inline)) {
     const float fa0 = s_rat[tab][8 * w + G], fa1 = s_rat[tab][8 * w + 4 + G];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -308,7 +314,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
       }
     }
   };
-  auto compute = [&](int stg) {
+  auto compute = [&](int stg) __attribute__((always_inline)) {
     if (!wvalid) return;
 #ifdef NR_WG_EXP_NO_MFMA
     return;
@@ -347,10 +353,18 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
   store(0, R0);
   __syncthreads();
   int64_t ks = k0;
-  auto step = [&](int stg, WgRegs& refill, WgRegs& next) {
+  // Within a barrier interval the MFMAs read stage stg and the split writes stage stg ^ 1, so their
+  // order is free (the kPingPongBit experiment: the two waves of a SIMD in different phases).
+  const bool split_first = (w & kPingPongBit) != 0;
+  auto step = [&](int stg, WgRegs& refill, WgRegs& next) __attribute__((always_inline)) {
     load(ks + 3, refill, ks + 3 < k1);
-    compute(stg);
-    store(stg ^ 1, next);
+    if (split_first) {
+      store(stg ^ 1, next);
+      compute(stg);
+    } else {
+      compute(stg);
+      store(stg ^ 1, next);
+    }
     __syncthreads();
     return ++ks < k1;
   };

@@ -81,6 +81,9 @@ VARIANTS = {
     'wg_nostore': ['-DNR_WG_EXP_NO_STORE'],
     'wg_loadonly': ['-DNR_WG_EXP_NO_MFMA', '-DNR_WG_EXP_NO_STORE'],
     'wg_noload': ['-DNR_WG_EXP_NO_LOAD'],
+    # nr_wgrad phase split between the two waves of a SIMD (valid results): waves w & 4 / adjacent waves
+    'wg_pp4': ['-DNR_WG_PP_BIT=4'],
+    'wg_pp1': ['-DNR_WG_PP_BIT=1'],
 }
 
 
