@@ -90,3 +90,52 @@ def test_struct_layouts_match_the_c_compiler(tmp_path):
         assert int(got[S.__name__]) == ctypes.sizeof(S), S.__name__
         for f, _ in S._fields_:
             assert int(got[f'{S.__name__}.{f}']) == getattr(S, f).offset, (S.__name__, f)
+
+
+def _wgrad_args(P=1000, m=256, n=256, npairs=1, ld=None):
+    from neurecon_amd import _lib
+    w = _lib.NrWgrad()
+    w.P, w.npairs, w.m, w.n, w.scale = P, npairs, m, n, 1.0
+    for q in range(2):  # fake non-null device pointers: argument checks run before any HIP call
+        w.a[q], w.b[q] = 0x1000, 0x2000
+        w.lda[q], w.ldb[q] = ld or m, ld or n
+    w.c, w.ldc = 0x3000, n
+    w.workspace = 0x4000
+    w.workspace_bytes = 1 << 40
+    return w
+
+
+@pytest.mark.parametrize('case, code, text', [
+    ('npairs', -1, 'npairs'),
+    ('lda', -1, 'leading dimension'),
+    ('null_out', -1, 'null output'),
+    ('vec_without_avec', -1, 'avec'),
+    ('operand_2gib', -1, '2 GiB'),
+    ('workspace', -4, 'workspace'),
+])
+def test_wgrad_rejects_bad_arguments(lib, case, code, text):
+    """nr_wgrad's argument checks (include/neurecon_hip.h NrWgrad) fail loudly before touching the GPU"""
+    w = _wgrad_args()
+    if case == 'npairs':
+        w.npairs = 3
+    elif case == 'lda':
+        w.lda[0] = 100
+    elif case == 'null_out':
+        w.c = 0
+    elif case == 'vec_without_avec':
+        w.vec = 0x5000
+    elif case == 'operand_2gib':
+        w = _wgrad_args(P=1 << 22, m=256, n=256)  # 4 M rows x 256 x 4 B = 4 GiB
+    elif case == 'workspace':
+        w.workspace_bytes = 16
+    rc = lib.nr_wgrad(ctypes.byref(w), None)
+    assert rc == code, (rc, lib.nr_last_error())
+    assert text in lib.nr_last_error().decode()
+
+
+def test_wgrad_workspace_sizes(lib):
+    """partials [S][n tiles x 128][m tiles x 256] + column-sum / vector partials, S ~ 256 / tiles"""
+    one = lib.nr_wgrad_workspace_bytes(65536, 256, 256, 1)
+    assert one >= 256 * 256 * 4 * 8
+    assert lib.nr_wgrad_workspace_bytes(65536, 3, 256, 1) <= one
+    assert lib.nr_wgrad_workspace_bytes(33, 17, 5, 1) > 0
