@@ -627,7 +627,22 @@ typedef struct {
   const float* head;     /* [3][256] */
   const float* head_bias;
   float* head_out;       /* [P][3] */
+  int blocked;           /* NR_BLK_* bits: those tensors are 16 x 16 blocked (below), the rest row-major */
 } NrTrainGemm;
+
+/* 16 x 16 blocked layout of a [P, ld] tensor (ld and P multiples of 16): element (p, c) at float
+ * ((p / 16) * (ld / 16) + c / 16) * 256 + (p % 16) * 16 + c % 16 -- a 16-point x 16-column block is one
+ * contiguous 1 KB run, which is what one wave-instruction of the training GEMMs' epilogues and of
+ * nr_wgrad's loaders reads or writes (row-major: 16 rows x 64 B).  Same size as the row-major tensor. */
+#define NR_BLK_X1 1
+#define NR_BLK_X2 2
+#define NR_BLK_Y 4
+#define NR_BLK_YB 8
+#define NR_BLK_Y2 16
+#define NR_BLK_Y3 32
+#define NR_BLK_A 64
+#define NR_BLK_G 128
+#define NR_BLK_ZD 256
 
 int nr_train_gemm(const NrTrainGemm* a, int KB, int KB2, int NBO, int NB2, void* stream);
 /* SDF ops: 0..16 = F0..F8, B7..B0 of the render pack (nr_sdf_pack), 17 = B8 of the training pack */
@@ -670,7 +685,13 @@ typedef struct {
   float vec_scale;
   void* workspace;
   size_t workspace_bytes;
+  int blocked;        /* NR_WG_BLK_* bits: those operands are 16 x 16 blocked (NR_BLK_* comment above:
+                         lda / ldb and P multiples of 16), the rest row-major */
 } NrWgrad;
+#define NR_WG_BLK_A0 1
+#define NR_WG_BLK_A1 2
+#define NR_WG_BLK_B0 4
+#define NR_WG_BLK_B1 8
 
 size_t nr_wgrad_workspace_bytes(int64_t P, int m, int n, int npairs);
 int nr_wgrad(const NrWgrad* w, void* stream);

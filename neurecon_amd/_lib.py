@@ -103,6 +103,9 @@ class NrUnisurfArgs(ctypes.Structure):
 WINDOW_REDUCE = ctypes.CFUNCTYPE(_c_i, _c_p)
 
 TG_NONE, TG_SOFTPLUS, TG_MUL, TG_SPADJ, TG_RELUMASK = 0, 1, 3, 4, 5
+# NrTrainGemm.blocked / NrWgrad.blocked bits (include/neurecon_hip.h: 16 x 16 blocked tensors)
+BLK_X1, BLK_X2, BLK_Y, BLK_YB, BLK_Y2, BLK_Y3, BLK_A, BLK_G, BLK_ZD = 1, 2, 4, 8, 16, 32, 64, 128, 256
+WG_BLK_A0, WG_BLK_A1, WG_BLK_B0, WG_BLK_B1 = 1, 2, 4, 8
 
 
 class NrTrainGemm(ctypes.Structure):
@@ -115,7 +118,7 @@ class NrTrainGemm(ctypes.Structure):
         ('y2', _c_p), ('ldy2', _c_i64), ('y3', _c_p), ('ldy3', _c_i64),
         ('a', _c_p), ('lda', _c_i64), ('g', _c_p), ('ldg', _c_i64), ('zd', _c_p), ('ldzd', _c_i64),
         ('g_row', _c_i), ('dot', _c_p), ('dot_bias', _c_f),
-        ('head', _c_p), ('head_bias', _c_p), ('head_out', _c_p),
+        ('head', _c_p), ('head_bias', _c_p), ('head_out', _c_p), ('blocked', _c_i),
     ]
 
 
@@ -124,7 +127,7 @@ class NrWgrad(ctypes.Structure):
         ('P', _c_i64), ('npairs', _c_i), ('a', _c_p * 2), ('lda', _c_i64 * 2), ('b', _c_p * 2), ('ldb', _c_i64 * 2),
         ('m', _c_i), ('n', _c_i), ('scale', _c_f), ('c', _c_p), ('ldc', _c_i64), ('colsum', _c_p),
         ('avec', _c_p), ('ldv', _c_i64), ('vec', _c_p), ('vec_scale', _c_f), ('workspace', _c_p),
-        ('workspace_bytes', _c_sz),
+        ('workspace_bytes', _c_sz), ('blocked', _c_i),
     ]
 
 

@@ -2727,6 +2727,14 @@ __device__ __forceinline__ void tg_store(float* base, uint32_t off, float4 v) {
   asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" : : "v"(off), "v"(d), "s"(base) : "memory");
 }
 
+// float index of element (p, c) of a [P, ld] tensor, row-major or 16 x 16 blocked (NR_BLK_* in
+// include/neurecon_hip.h: a 16-point x 16-column block is one contiguous 1 KB run, which is what one
+// wave-instruction of the epilogue reads or writes; row-major it is 16 rows x 64 B).  c % 4 == 0 keeps
+// c .. c + 3 inside one block in both layouts.
+__device__ __forceinline__ uint32_t tg_elem(bool blk, uint32_t p, uint32_t ld, uint32_t c) {
+  return blk ? (((p >> 4) * (ld >> 4) + (c >> 4)) << 8) + ((p & 15u) << 4) + (c & 15u) : p * ld + c;
+}
+
 template <int KB, int KB2, int NBO, int NB2, int MODE>
 __global__ __attribute__((amdgpu_flat_work_group_size(kT4, kT4), amdgpu_waves_per_eu(kWPE, kWPE)))
 void tgemm_kernel(TGemmArgs a) {
@@ -2756,25 +2764,25 @@ void tgemm_kernel(TGemmArgs a) {
     float xinv[1];
     {
       float4 X[KB];
-      auto load_seg = [&](const float* src, int64_t ld, int n, int b0, int nb) {
-        const float* row = src + (int64_t)pc * ld;
-        const bool vec = ((ld | (int64_t)((uintptr_t)src >> 2)) & 3) == 0;
+      auto load_seg = [&](const float* src, int64_t ld, int n, int b0, int nb, bool blk) {
+        const bool vec = blk || ((ld | (int64_t)((uintptr_t)src >> 2)) & 3) == 0;
 #pragma unroll
         for (int b = 0; b < nb; ++b) {
           const int col = 16 * b + 4 * g;
+          const float* e = src + tg_elem(blk, pc, (uint32_t)ld, (uint32_t)col);
           float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (vec && col + 3 < n) v = *(const float4*)(row + col);
+          if (vec && col + 3 < n) v = *(const float4*)e;
           else {
-            if (col + 0 < n) v.x = row[col + 0];
-            if (col + 1 < n) v.y = row[col + 1];
-            if (col + 2 < n) v.z = row[col + 2];
-            if (col + 3 < n) v.w = row[col + 3];
+            if (col + 0 < n) v.x = e[0];
+            if (col + 1 < n) v.y = e[1];
+            if (col + 2 < n) v.z = e[2];
+            if (col + 3 < n) v.w = e[3];
           }
           X[b0 + b] = v;
         }
       };
-      load_seg(a.x1, a.ld1, a.n1, 0, KB1);
-      if constexpr (KB2 > 0) load_seg(a.x2, a.ld2, a.n2, KB1, KB2);
+      load_seg(a.x1, a.ld1, a.n1, 0, KB1, (a.blocked & NR_BLK_X1) != 0);
+      if constexpr (KB2 > 0) load_seg(a.x2, a.ld2, a.n2, KB1, KB2, (a.blocked & NR_BLK_X2) != 0);
       float m = 0.0f;
 #pragma unroll
       for (int b = 0; b < KB; b += 2) m = amax8(m, X[b], X[b + 1]);
@@ -2793,15 +2801,15 @@ void tgemm_kernel(TGemmArgs a) {
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const uint32_t col = (uint32_t)(16 * (2 * c + b) + 4 * g);
-        dst[0][b] = tg_load(a.a, (pc * (uint32_t)a.lda + col) * 4u);
+        dst[0][b] = tg_load(a.a, tg_elem(a.blocked & NR_BLK_A, pc, (uint32_t)a.lda, col) * 4u);
         ++n;
         if constexpr (kG) {
           if (g_tensor) {
-            dst[1][b] = tg_load(a.g, (pc * (uint32_t)a.ldg + col) * 4u);
+            dst[1][b] = tg_load(a.g, tg_elem(a.blocked & NR_BLK_G, pc, (uint32_t)a.ldg, col) * 4u);
             ++n;
           }
           if (has_g) {
-            dst[2][b] = tg_load(a.zd, (pc * (uint32_t)a.ldzd + col) * 4u);
+            dst[2][b] = tg_load(a.zd, tg_elem(a.blocked & NR_BLK_ZD, pc, (uint32_t)a.ldzd, col) * 4u);
             ++n;
           }
         }
@@ -2821,11 +2829,21 @@ void tgemm_kernel(TGemmArgs a) {
       for (int b = 0; b < 2; ++b) {
         const int B = 2 * c + b;
         const uint32_t col = (uint32_t)(16 * (lo ? B : B - NB1) + 4 * g);
-        if (dst) { tg_store(dst, (pc * (uint32_t)(lo ? a.ldy : a.ldyb) + col) * 4u, pv[0][b]); ++n; }
+        if (dst) {
+          const bool blk = (a.blocked & (lo ? NR_BLK_Y : NR_BLK_YB)) != 0;
+          tg_store(dst, tg_elem(blk, pc, (uint32_t)(lo ? a.ldy : a.ldyb), col) * 4u, pv[0][b]);
+          ++n;
+        }
         if constexpr (MODE == TG_SOFTPLUS || MODE == TG_MUL)
-          if (lo && a.y2) { tg_store(a.y2, (pc * (uint32_t)a.ldy2 + col) * 4u, pv[1][b]); ++n; }
+          if (lo && a.y2) {
+            tg_store(a.y2, tg_elem(a.blocked & NR_BLK_Y2, pc, (uint32_t)a.ldy2, col) * 4u, pv[1][b]);
+            ++n;
+          }
         if constexpr (MODE == TG_SOFTPLUS)
-          if (lo && a.y3) { tg_store(a.y3, (pc * (uint32_t)a.ldy3 + col) * 4u, pv[2][b]); ++n; }
+          if (lo && a.y3) {
+            tg_store(a.y3, tg_elem(a.blocked & NR_BLK_Y3, pc, (uint32_t)a.ldy3, col) * 4u, pv[2][b]);
+            ++n;
+          }
       }
       return n;
     };
@@ -2949,6 +2967,12 @@ int launch_tgemm(const TGemmArgs& a, int KB, int KB2, int NBO, int NB2, hipStrea
   // 32-bit byte offsets of the epilogue's asm loads
   const int64_t maxld = std::max({a.lda, a.ldg, a.ldzd, a.ldy, a.ldyb, a.ldy2, a.ldy3});
   NR_REQUIRE(a.P * maxld * 4 < ((int64_t)1 << 31), NR_ERR_ARG, "tgemm: epilogue operands exceed 2 GB");
+  if (a.blocked) {  // 16 x 16 blocked tensors: whole blocks of points and columns
+    const int64_t lds[9] = {a.ld1, a.ld2, a.ldy, a.ldyb, a.ldy2, a.ldy3, a.lda, a.ldg, a.ldzd};
+    bool ok = a.P % 16 == 0 && (a.blocked & ~0x1ff) == 0;
+    for (int i = 0; i < 9; ++i) ok = ok && (!(a.blocked & (1 << i)) || (lds[i] > 0 && lds[i] % 16 == 0));
+    NR_REQUIRE(ok, NR_ERR_ARG, "tgemm: a blocked tensor needs P and its leading dimension multiples of 16");
+  }
   const int64_t tiles = (a.P + kPointsPerWG - 1) / kPointsPerWG;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

@@ -58,6 +58,7 @@ struct WgKArgs {
   const float* avec; // [P] at avec[p * ldv] (nullptr: none)
   int64_t ldv;
   float* part_vec;   // [S][nnt * 128]
+  int blocked;       // NR_WG_BLK_* bits
 };
 
 typedef short v4s __attribute__((ext_vector_type(4)));
@@ -132,9 +133,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int64_t b
 }
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-// byte offset of (row, col) in a row-major operand, or kOob when the lane is off / col >= ncol
-__device__ __forceinline__ uint32_t lane_off(int row, int col, int64_t ld, int ncol, bool on) {
-  return on && col < ncol ? (uint32_t)(row * ld + col) * 4u : kOob;
+// byte offset of (row, col) in a row-major or 16 x 16 blocked operand (include/neurecon_hip.h NR_BLK_*;
+// rows relative to a 16-aligned k-step start), or kOob when the lane is off / col >= ncol
+__device__ __forceinline__ uint32_t lane_off(int row, int col, int64_t ld, int ncol, bool on, bool blk) {
+  if (!(on && col < ncol)) return kOob;
+  if (blk)
+    return ((((uint32_t)row >> 4) * (uint32_t)(ld >> 4) + ((uint32_t)col >> 4)) * 256u + ((uint32_t)row & 15u) * 16u +
+            ((uint32_t)col & 15u)) * 4u;
+  return (uint32_t)(row * ld + col) * 4u;
 }
 
 // 4 consecutive columns at byte offset o (kOob: zeros).  VEC: ncol % 4 == 0 and 16-byte aligned rows
@@ -215,10 +221,11 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int qq = q < a.npairs ? q : 0;
+    const bool blka = (a.blocked & (NR_WG_BLK_A0 << qq)) != 0, blkb = (a.blocked & (NR_WG_BLK_B0 << qq)) != 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) oa[q][j] = lane_off(ar + 8 * j, m0 + ac, a.lda[qq], a.m, wvalid);
+    for (int j = 0; j < 4; ++j) oa[q][j] = lane_off(ar + 8 * j, m0 + ac, a.lda[qq], a.m, wvalid, blka);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) ob[q][j] = lane_off(br + 16 * j, n0 + bc, a.ldb[qq], a.n, true);
+    for (int j = 0; j < 2; ++j) ob[q][j] = lane_off(br + 16 * j, n0 + bc, a.ldb[qq], a.n, true, blkb);
   }
 #pragma unroll
   for (int j = 0; j < 2; ++j) ov[j] = want_vec ? (uint32_t)((br + 16 * j) * a.ldv) * 4u : kOob;
@@ -534,6 +541,14 @@ int nr_wgrad(const NrWgrad* w, void* stream) {
     for (int q = 0; q < w->npairs; ++q) fits = fits && w->P * w->lda[q] * 4 < lim && w->P * w->ldb[q] * 4 < lim;
     NR_REQUIRE(fits, NR_ERR_ARG, "nr_wgrad: an operand spans 2 GiB or more (split the rows over calls)");
   }
+  if (w->blocked) {  // 16 x 16 blocked operands: whole blocks of rows and columns
+    bool ok = w->P % 16 == 0 && (w->blocked & ~0xf) == 0;
+    for (int q = 0; q < w->npairs; ++q) {
+      if (w->blocked & (NR_WG_BLK_A0 << q)) ok = ok && w->lda[q] % 16 == 0;
+      if (w->blocked & (NR_WG_BLK_B0 << q)) ok = ok && w->ldb[q] % 16 == 0;
+    }
+    NR_REQUIRE(ok, NR_ERR_ARG, "nr_wgrad: a blocked operand needs P and its leading dimension multiples of 16");
+  }
   WgPlan p = wgrad_plan(w->P, w->m, w->n, w->npairs);
   if (const char* e = getenv("NR_WGRAD_SLICES")) {  // measurement knob (tools/wgrad_bench.py): fewer slices
     const int s = atoi(e);
@@ -558,6 +573,7 @@ int nr_wgrad(const NrWgrad* w, void* stream) {
   k.avec = w->vec ? w->avec : nullptr;
   k.ldv = w->ldv > 0 ? w->ldv : 1;
   k.part_vec = w->vec ? (float*)(ws + p.part_bytes + p.cs_bytes) : nullptr;
+  k.blocked = w->blocked;
   {
     // units: the operands' bytes (the HBM-bound roofline's algorithmic traffic)
     ProfScope prof("wgrad", (double)w->npairs * w->P * (w->m + w->n) * 4.0, st);

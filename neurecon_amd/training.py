@@ -18,6 +18,7 @@ equals the nabla chain's own gradients, one tangent sweep and one adjoint sweep 
 gradient: dW_l = zbar_l^T hin_l + delta_l^T hdot_in_l.
 """
 import ctypes
+import os
 import math
 
 import torch
@@ -91,11 +92,13 @@ def _wgrad2(g1, h1, g2, h2):
     return buf.sum(0)
 
 
-def _wg(pairs, out=None, scale=1.0, colsum=None, avec=None, vec=None):
+def _wg(pairs, out=None, scale=1.0, colsum=None, avec=None, vec=None, blocked=0):
     """sum_q a_q^T b_q on the hand-written MFMA weight-gradient kernel (nr_wgrad, f16x3): pairs of
     row-major views a [P, m], b [P, n] (unit column stride; any row stride); out [m, n] (a view with
     unit column stride, e.g. a column range of the gradient) = scale * the sum.  colsum: [m] <- the
-    column sums of a_0 (the bias gradient); avec [P] / vec [n]: vec <- avec^T b_0 (an extra row)."""
+    column sums of a_0 (the bias gradient); avec [P] / vec [n]: vec <- avec^T b_0 (an extra row).
+    blocked: NR_WG_BLK_* bits of the operands stored 16 x 16 blocked (a column view [:, :n] of a
+    blocked tensor keeps its pointer and leading dimension, which is all the kernel needs)."""
     a0, b0 = pairs[0]
     P, m = a0.shape
     n = b0.shape[1]
@@ -113,6 +116,7 @@ def _wg(pairs, out=None, scale=1.0, colsum=None, avec=None, vec=None):
         w.colsum = colsum.data_ptr()
     if avec is not None:
         w.avec, w.ldv, w.vec, w.vec_scale = avec.data_ptr(), avec.stride(0), vec.data_ptr(), 1.0
+    w.blocked = blocked
     lib = L.lib()
     nb = lib.nr_wgrad_workspace_bytes(P, m, n, len(pairs))
     ws = L.workspace(dev, nb)
@@ -582,7 +586,7 @@ def _tg_bytes(P, shape, n1, n2, y, yb, y2, y3, a, g, g_row, zd, dot):
 
 def _tg(op, P, shape, mode, x1, ld1, n1, y, ldy, x2=None, ld2=0, n2=0, bias=True, yscale=1.0, yb=None, ldyb=0,
         y2=None, ldy2=0, y3=None, ldy3=0, a=None, lda=0, g=None, ldg=0, zd=None, ldzd=0, g_row=False, dot=None,
-        dot_bias=0.0, head=None, head_bias=None, head_out=None, stream=None):
+        dot_bias=0.0, head=None, head_bias=None, head_out=None, stream=None, blocked=0):
     """one training layer GEMM: shape = (KB, KB2, NBO, NB2) of the packed op at device address `op`"""
     TG_BYTES['bytes'] += _tg_bytes(P, shape, n1, n2, y, yb, y2, y3, a, g, g_row, zd, dot)
     TG_BYTES['calls'] += 1
@@ -598,6 +602,7 @@ def _tg(op, P, shape, mode, x1, ld1, n1, y, ldy, x2=None, ld2=0, n2=0, bias=True
     t.a, t.lda, t.g, t.ldg, t.zd, t.ldzd = _p(a), lda, _p(g), ldg, _p(zd), ldzd
     t.g_row, t.dot, t.dot_bias = int(g_row), _p(dot), float(dot_bias)
     t.head, t.head_bias, t.head_out = _p(head), _p(head_bias), _p(head_out)
+    t.blocked = blocked
     L.check(L.lib().nr_train_gemm(ctypes.byref(t), *shape, stream))
 
 
@@ -658,6 +663,19 @@ def _pad16(n):
     return 16 * ((n + 15) // 16)
 
 
+def _blk_bits(P):
+    """NrTrainGemm.blocked bits from role names, or always 0 when P is not a multiple of 16 (the blocked
+    layout tiles whole 16-point blocks) or NR_TRAIN_BLOCKED=0 (row-major everywhere: the bit-identity
+    test's reference)"""
+    on = P % 16 == 0 and os.environ.get('NR_TRAIN_BLOCKED', '1') != '0'
+    return lambda roles: sum(getattr(L, 'BLK_' + r) for r in roles) if on else 0
+
+
+def _WG_BLK(a_blocked, b_blocked):
+    """NrWgrad.blocked bits for operand pairs whose A (resp. B) operands are all blocked or all not"""
+    return (L.WG_BLK_A0 | L.WG_BLK_A1) * bool(a_blocked) | (L.WG_BLK_B0 | L.WG_BLK_B1) * bool(b_blocked)
+
+
 class SdfNablaTG(torch.autograd.Function):
     """SdfNabla on nr_train_gemm (f16x3 softplus nets, D=8, skip at layer 4, W=256): the same recipe
     (nr_train.hip header) with every layer product an op of the render pack (F0..F8 forward, B7..B0
@@ -668,8 +686,12 @@ class SdfNablaTG(torch.autograd.Function):
                B0: e_first;  nabla = J_emb^T (e_first + e_skip)
       tangent  F_l (no bias): zdot_l = W_l hdot_in_l, hdot_l = s_l zdot_l
       adjoint  B8 then B7..B1: zbar_{l-1} = (W_l^T zbar_l) s_{l-1} + g_{l-1} zdot_{l-1} 100 s (1 - s)
-    Activations are [P, 16-column blocks] row-major (217-wide layer-3 tensors padded to 224, the
-    embedding to 64).  Weight gradients: dW_l = zbar_l^T hin_l + delta_l^T hdot_in_l (hipBLASLt)."""
+    Activations are [P, 16-column blocks] (217-wide layer-3 tensors padded to 224, the embedding to
+    64); the layer tensors (H, S, delta, G, ZD, HD, Z) are stored 16 x 16 blocked when P % 16 == 0
+    (include/neurecon_hip.h NR_BLK_*: one contiguous 1 KB run per wave-instruction of the GEMM epilogues
+    and the weight-gradient loaders, instead of 16 rows x 64 B), the embedding tensors, the feature and
+    hdot_7 (a torch-side column sum) row-major.  Weight gradients: dW_l = zbar_l^T hin_l + delta_l^T
+    hdot_in_l (nr_wgrad)."""
 
     @staticmethod
     def forward(ctx, x, surface, want_feat, *params):
@@ -694,6 +716,7 @@ class SdfNablaTG(torch.autograd.Function):
         sdf = torch.empty(P, device=dev)
         delta = [None] * D
         delta[7] = torch.empty(P, 256, device=dev)
+        bk = _blk_bits(P)
         for l in range(D):                                                 # F0..F7
             if l == 0:
                 xin = dict(x1=h0, ld1=64, n1=nf)
@@ -703,12 +726,12 @@ class SdfNablaTG(torch.autograd.Function):
                 xin = dict(x1=H[l - 1], ld1=wd[l - 1], n1=nv[l - 1])
             extra = dict(y3=delta[7], ldy3=256, dot=sdf) if l == 7 else {}
             _tg(op(l), P, shp(l, 4 if l == 4 else 0), L.TG_SOFTPLUS, y=H[l], ldy=wd[l], y2=S[l], ldy2=wd[l],
-                stream=st, **xin, **extra)
+                stream=st, blocked=bk(('X1',) * (l > 0) + ('Y', 'Y2') + ('Y3',) * (l == 7)), **xin, **extra)
         sdf.add_(bs[D].detach()[0])                                        # + b8 (no host sync)
         feat = None
         if want_feat:                                                      # F8
             feat = torch.empty(P, 256, device=dev)
-            _tg(op(8), P, shp(8), L.TG_NONE, H[7], 256, 256, feat, 256, stream=st)
+            _tg(op(8), P, shp(8), L.TG_NONE, H[7], 256, 256, feat, 256, stream=st, blocked=bk(('X1',)))
         G = [None] * D                                                     # g_l = d sdf / d h_l (l < 7)
         for l in range(D - 1, 0, -1):                                      # B7..B1: op index 16 - l
             i = 16 - l
@@ -717,12 +740,12 @@ class SdfNablaTG(torch.autograd.Function):
             if l == 4:  # [g_3 (14 blocks) ; e_skip (4 blocks)]
                 e_skip = torch.empty(P, 64, device=dev)
                 _tg(op(i), P, shp(i, 0, 4), L.TG_MUL, delta[4], 256, 256, G[3], 224, yb=e_skip, ldyb=64,
-                    y2=delta[3], ldy2=224, a=S[3], lda=224, stream=st)
+                    y2=delta[3], ldy2=224, a=S[3], lda=224, stream=st, blocked=bk(('X1', 'Y', 'Y2', 'A')))
             else:
                 _tg(op(i), P, shp(i), L.TG_MUL, delta[l], wd[l], nv[l], G[l - 1], wd[l - 1], y2=delta[l - 1],
-                    ldy2=wd[l - 1], a=S[l - 1], lda=wd[l - 1], stream=st)
+                    ldy2=wd[l - 1], a=S[l - 1], lda=wd[l - 1], stream=st, blocked=bk(('X1', 'Y', 'Y2', 'A')))
         e_first = torch.empty(P, 64, device=dev)                           # B0
-        _tg(op(16), P, shp(16), L.TG_NONE, delta[0], 256, 256, e_first, 64, stream=st)
+        _tg(op(16), P, shp(16), L.TG_NONE, delta[0], 256, 256, e_first, 64, stream=st, blocked=bk(('X1',)))
         nab = torch.empty(P, 3, device=dev)
         L.check(L.lib().nr_embed_vjp(L.ptr(x), L.ptr(e_first), 64, L.ptr(e_skip), 64, 1.0, P, surface.embed_multires,
                                      L.ptr(nab), st))
@@ -755,6 +778,8 @@ class SdfNablaTG(torch.autograd.Function):
         wd = [256, 256, 256, 224, 256, 256, 256, 256]
         nv = [256, 256, 256, 217, 256, 256, 256, 256]
         tangent = g_nab is not None
+        bk = _blk_bits(P)
+        wb = _WG_BLK if bk(('Y',)) else (lambda a, b: 0)
         ZD = [None] * D
         HD = [None] * D                                                   # hdot_l = s_l zdot_l
         hd0 = None
@@ -771,8 +796,10 @@ class SdfNablaTG(torch.autograd.Function):
                     xin = dict(x1=HD[l - 1], ld1=wd[l - 1], n1=nv[l - 1])
                 ZD[l] = torch.empty(P, wd[l], device=dev)
                 HD[l] = torch.empty(P, wd[l], device=dev)
+                # hdot_7 stays row-major: its consumer is the torch-side column sum of dW8[0]
                 _tg(op(l), P, shp(l, 4 if l == 4 else 0), L.TG_MUL, y=ZD[l], ldy=wd[l], y2=HD[l], ldy2=wd[l],
-                    a=S[l], lda=wd[l], bias=False, stream=st, **xin)
+                    a=S[l], lda=wd[l], bias=False, stream=st,
+                    blocked=bk(('X1',) * (l > 0) + ('Y', 'A') + ('Y2',) * (l < 7)), **xin)
         # output-layer adjoint ob = [d sdf, d feature] -> zbar_7 through B8 = W8^T (training pack)
         Wl = [surface.surface_fc_layers[i] for i in range(D + 1)]
         tp = _train_pack(surface, 'sdf', Ws, [l.bias for l in Wl], dev)  # the forward's effective weights
@@ -781,24 +808,25 @@ class SdfNablaTG(torch.autograd.Function):
         Z = [None] * D
         Z[7] = torch.empty(P, 256, device=dev)
         _tg(tp.data_ptr() + info[17][0], P, (18, 2, 16, 0), L.TG_SPADJ, gf, 256, 256, Z[7], 256, x2=gs, ld2=1, n2=1,
-            a=S[7], lda=256, zd=ZD[7], ldzd=256, g_row=tangent, stream=st)
+            a=S[7], lda=256, zd=ZD[7], ldzd=256, g_row=tangent, stream=st,
+            blocked=bk(('Y', 'A') + ('ZD',) * tangent))
         for l in range(D - 1, 0, -1):                                      # B7..B1 -> zbar_{l-1}
             i = 16 - l
             Z[l - 1] = torch.empty(P, wd[l - 1], device=dev)
             gz = dict(g=G[l - 1], ldg=wd[l - 1], zd=ZD[l - 1], ldzd=wd[l - 1]) if tangent else {}
             _tg(op(i), P, shp(i, 0, 4 if l == 4 else 0), L.TG_SPADJ, Z[l], wd[l], nv[l], Z[l - 1], wd[l - 1],
-                a=S[l - 1], lda=wd[l - 1], stream=st, **gz)
+                a=S[l - 1], lda=wd[l - 1], stream=st, blocked=bk(('X1', 'Y', 'A') + ('G', 'ZD') * tangent), **gz)
         # weight gradients on nr_wgrad (f16x3 MFMA): dW_l = zbar_l^T hin_l + delta_l^T hdot_in_l (one
         # launch for both sweeps), db_l = sum_p zbar_l fused into it
         dW, db = [None] * (D + 1), [None] * (D + 1)
         dW[D] = torch.empty(257, 256, device=dev)  # rows [d sdf ; d feature] x h7
         db[D] = torch.empty(257, device=dev)
         if g_feat is not None:
-            _wg([(gf, H[7])], out=dW[D][1:], colsum=db[D][1:], avec=gs, vec=dW[D][0])
+            _wg([(gf, H[7])], out=dW[D][1:], colsum=db[D][1:], avec=gs, vec=dW[D][0], blocked=wb(False, True))
         else:  # no feature gradient: only the sdf row
             dW[D][1:].zero_()
             db[D][1:].zero_()
-            _wg([(gs[:, None], H[7])], out=dW[D][:1])
+            _wg([(gs[:, None], H[7])], out=dW[D][:1], blocked=wb(False, True))
         db[D][:1] = _colsum(gs[:, None])
         if tangent:
             dW[D][0] += _colsum(HD[7])
@@ -807,17 +835,17 @@ class SdfNablaTG(torch.autograd.Function):
             db[l] = torch.empty(nv[l], device=dev)
             if l == 0:
                 pr = [(zb, h0[:, :nf])] + ([(delta[0][:, :nv[0]], hd0[:, :nf])] if tangent else [])
-                dW[0] = _wg(pr, colsum=db[0])
+                dW[0] = _wg(pr, colsum=db[0], blocked=wb(True, False))
             elif l == 4:  # the skip layer's input cat([h3, embed(x)]) / sqrt(2) (base.py:250): per column block
                 dW[4] = torch.empty(256, 217 + nf, device=dev)
                 _wg([(zb, H[3][:, :217])] + ([(delta[4][:, :nv[4]], HD[3][:, :217])] if tangent else []),
-                    out=dW[4][:, :217], scale=_ISQ2, colsum=db[4])
+                    out=dW[4][:, :217], scale=_ISQ2, colsum=db[4], blocked=wb(True, True))
                 _wg([(zb, h0[:, :nf])] + ([(delta[4][:, :nv[4]], hd0[:, :nf])] if tangent else []),
-                    out=dW[4][:, 217:], scale=_ISQ2)
+                    out=dW[4][:, 217:], scale=_ISQ2, blocked=wb(True, False))
             else:
                 hin = H[l - 1][:, :nv[l - 1]]
                 pr = [(zb, hin)] + ([(delta[l][:, :nv[l]], HD[l - 1][:, :nv[l - 1]])] if tangent else [])
-                dW[l] = _wg(pr, colsum=db[l])
+                dW[l] = _wg(pr, colsum=db[l], blocked=wb(True, True))
         return (None, None, None, *dW, *db)
 
 

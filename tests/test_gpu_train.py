@@ -462,3 +462,20 @@ def test_radiance_training_strided_feature(precision):
     assert not wide[:, 1:].is_contiguous()
     for a, b in zip(*outs):
         assert torch.equal(a, b), float((a - b).abs().max())
+
+
+@pytest.mark.parametrize('name', ['neus_train', 'neus_train_nerfpp'])
+def test_blocked_layout_training_step_bit_identical(golden, name, monkeypatch):
+    """the f16x3 SDF training path's layer tensors in the 16 x 16 blocked layout (NR_BLK_*, the default
+    when P % 16 == 0) give bit-identical losses and gradients to the same step with every tensor
+    row-major (NR_TRAIN_BLOCKED=0): only the addressing of the GEMM epilogues and the weight-gradient
+    loaders differs"""
+    g = golden(name)
+    monkeypatch.setenv('NR_TRAIN_BLOCKED', '0')
+    _, l_row, g_row, _ = _gpu_step(g, 'f16x3')
+    monkeypatch.setenv('NR_TRAIN_BLOCKED', '1')
+    _, l_blk, g_blk, _ = _gpu_step(g, 'f16x3')
+    for k in l_row:
+        assert torch.equal(l_row[k], l_blk[k]), k
+    for k in g_row:
+        assert torch.equal(g_row[k], g_blk[k]), (k, float((g_row[k] - g_blk[k]).abs().max()))

@@ -141,3 +141,34 @@ def test_wgrad_tiny_and_zero_quads():
     ref = a.double().t() @ b.double()
     sc = float(ref.abs().max())
     assert float((out.double() - ref).abs().max()) <= 1e-5 * sc
+
+
+def _blocked(t):
+    """the 16 x 16 blocked storage (include/neurecon_hip.h NR_BLK_*) of a row-major [P, C] tensor, as a
+    [P, C]-shaped tensor whose memory is in blocked order"""
+    P, C = t.shape
+    return t.reshape(P // 16, 16, C // 16, 16).permute(0, 2, 1, 3).contiguous().reshape(P, C)
+
+
+@pytest.mark.parametrize('m, lda, n, ldb, npairs', [(256, 256, 256, 256, 2), (217, 224, 256, 256, 2),
+                                                    (256, 256, 217, 224, 1), (256, 256, 39, 64, 2)])
+def test_wgrad_blocked_operands_bit_identical(m, lda, n, ldb, npairs):
+    """operands in the 16 x 16 blocked layout give bit-identical results to the same operands
+    row-major (only the addressing differs), A and B blocked independently; column views [:, :n] of a
+    blocked tensor keep the pointer and leading dimension the kernel needs"""
+    from neurecon_amd import _lib as L
+    from neurecon_amd.training import _wg
+    g = torch.Generator().manual_seed(m + n)
+    P = 4096 + 48
+    A = [_mk(P, lda, lda, g, heavy=True) for _ in range(npairs)]
+    B = [_mk(P, ldb, ldb, g) for _ in range(npairs)]
+    ref = _wg([(a[:, :m], b[:, :n]) for a, b in zip(A, B)], colsum=(cs0 := torch.empty(m, device='cuda')))
+    for ba, bb in ((True, False), (False, True), (True, True)):
+        AA = [_blocked(a) if ba else a for a in A]
+        BB = [_blocked(b) if bb else b for b in B]
+        bits = (L.WG_BLK_A0 | L.WG_BLK_A1) * ba | (L.WG_BLK_B0 | L.WG_BLK_B1) * bb
+        cs = torch.empty(m, device='cuda')
+        out = _wg([(a[:, :m], b[:, :n]) for a, b in zip(AA, BB)], colsum=cs, blocked=bits)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), (ba, bb, float((out - ref).abs().max()))
+        assert torch.equal(cs, cs0), (ba, bb)
