@@ -607,7 +607,7 @@ typedef struct {
   int use_bias;
   int mode;
   float yscale;
-  float* y;
+  float* y;              /* NULL: those blocks are not stored (at least one output must be given) */
   int64_t ldy;
   float* yb;             /* NULL: those blocks are not stored */
   int64_t ldyb;
@@ -628,6 +628,8 @@ typedef struct {
   const float* head_bias;
   float* head_out;       /* [P][3] */
   int blocked;           /* NR_BLK_* bits: those tensors are 16 x 16 blocked (below), the rest row-major */
+  int g_scaled;          /* NR_TG_SPADJ: g holds s * g (the nabla chain's delta) and the g zdot term uses
+                            100 (1 - s) -- the nabla sweep then need not store g at all */
 } NrTrainGemm;
 
 /* 16 x 16 blocked layout of a [P, ld] tensor (ld and P multiples of 16): element (p, c) at float

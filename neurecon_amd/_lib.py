@@ -119,6 +119,7 @@ class NrTrainGemm(ctypes.Structure):
         ('a', _c_p), ('lda', _c_i64), ('g', _c_p), ('ldg', _c_i64), ('zd', _c_p), ('ldzd', _c_i64),
         ('g_row', _c_i), ('dot', _c_p), ('dot_bias', _c_f),
         ('head', _c_p), ('head_bias', _c_p), ('head_out', _c_p), ('blocked', _c_i),
+        ('g_scaled', _c_i),
     ]
 
 

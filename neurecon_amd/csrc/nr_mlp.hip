@@ -2920,7 +2920,9 @@ void tgemm_kernel(TGemmArgs a) {
               const float si = av[r];
               float w = fmul(zz[r] * a.yscale, si);
               if (has_g) {
-                const float d2 = fmul(fmul(si, fsub(1.0f, si)), 100.0f);
+                // s' = 100 s (1 - s); with g_scaled the tensor holds s g already
+                const float d2 = a.g_scaled && !a.g_row ? fmul(fsub(1.0f, si), 100.0f)
+                                                        : fmul(fmul(si, fsub(1.0f, si)), 100.0f);
                 w = fadd(w, fmul(fmul(a.g_row ? rv[r] : gv[r], dv[r]), d2));
               }
               o1[r] = w;
@@ -2962,7 +2964,7 @@ void tgemm_kernel(TGemmArgs a) {
 
 int launch_tgemm(const TGemmArgs& a, int KB, int KB2, int NBO, int NB2, hipStream_t stream) {
   if (a.P <= 0) return NR_OK;
-  NR_REQUIRE(a.op && a.y, NR_ERR_ARG, "tgemm: null op or output");
+  NR_REQUIRE(a.op && (a.y || a.yb || a.y2 || a.y3 || a.dot), NR_ERR_ARG, "tgemm: null op or no output");
   NR_REQUIRE(a.x1 && (KB2 == 0 || a.x2), NR_ERR_ARG, "tgemm: missing input segment");
   // 32-bit byte offsets of the epilogue's asm loads
   const int64_t maxld = std::max({a.lda, a.ldg, a.ldzd, a.ldy, a.ldyb, a.ldy2, a.ldy3});

@@ -586,7 +586,7 @@ def _tg_bytes(P, shape, n1, n2, y, yb, y2, y3, a, g, g_row, zd, dot):
 
 def _tg(op, P, shape, mode, x1, ld1, n1, y, ldy, x2=None, ld2=0, n2=0, bias=True, yscale=1.0, yb=None, ldyb=0,
         y2=None, ldy2=0, y3=None, ldy3=0, a=None, lda=0, g=None, ldg=0, zd=None, ldzd=0, g_row=False, dot=None,
-        dot_bias=0.0, head=None, head_bias=None, head_out=None, stream=None, blocked=0):
+        dot_bias=0.0, head=None, head_bias=None, head_out=None, stream=None, blocked=0, g_scaled=False):
     """one training layer GEMM: shape = (KB, KB2, NBO, NB2) of the packed op at device address `op`"""
     TG_BYTES['bytes'] += _tg_bytes(P, shape, n1, n2, y, yb, y2, y3, a, g, g_row, zd, dot)
     TG_BYTES['calls'] += 1
@@ -602,7 +602,7 @@ def _tg(op, P, shape, mode, x1, ld1, n1, y, ldy, x2=None, ld2=0, n2=0, bias=True
     t.a, t.lda, t.g, t.ldg, t.zd, t.ldzd = _p(a), lda, _p(g), ldg, _p(zd), ldzd
     t.g_row, t.dot, t.dot_bias = int(g_row), _p(dot), float(dot_bias)
     t.head, t.head_bias, t.head_out = _p(head), _p(head_bias), _p(head_out)
-    t.blocked = blocked
+    t.blocked, t.g_scaled = blocked, int(g_scaled)
     L.check(L.lib().nr_train_gemm(ctypes.byref(t), *shape, stream))
 
 
@@ -682,10 +682,12 @@ class SdfNablaTG(torch.autograd.Function):
     transposed) or the training pack (B8 = W8^T), and the elementwise steps in the GEMM epilogues:
       primal   F_l: h_l, s_l = softplus100 / softplus'(W_l hin_l + b_l); F7 also delta_7 = s_7 W8[0, :]
                and sdf = h_7 . W8[0, :] + b8;  F8: feature
-      nabla    B_l: g_{l-1} = W_l^T delta_l, delta_{l-1} = s_{l-1} g_{l-1}; B4 splits [g_3 ; e_skip];
+      nabla    B_l: g_{l-1} = W_l^T delta_l, delta_{l-1} = s_{l-1} g_{l-1} (only delta stored); B4 splits
+               [g_3 ; e_skip];
                B0: e_first;  nabla = J_emb^T (e_first + e_skip)
       tangent  F_l (no bias): zdot_l = W_l hdot_in_l, hdot_l = s_l zdot_l
-      adjoint  B8 then B7..B1: zbar_{l-1} = (W_l^T zbar_l) s_{l-1} + g_{l-1} zdot_{l-1} 100 s (1 - s)
+      adjoint  B8 then B7..B1: zbar_{l-1} = (W_l^T zbar_l) s_{l-1} + delta_{l-1} zdot_{l-1} 100 (1 - s)
+               (= g zdot 100 s (1 - s), torch's softplus double backward)
     Activations are [P, 16-column blocks] (217-wide layer-3 tensors padded to 224, the embedding to
     64); the layer tensors (H, S, delta, G, ZD, HD, Z) are stored 16 x 16 blocked when P % 16 == 0
     (include/neurecon_hip.h NR_BLK_*: one contiguous 1 KB run per wave-instruction of the GEMM epilogues
@@ -732,18 +734,18 @@ class SdfNablaTG(torch.autograd.Function):
         if want_feat:                                                      # F8
             feat = torch.empty(P, 256, device=dev)
             _tg(op(8), P, shp(8), L.TG_NONE, H[7], 256, 256, feat, 256, stream=st, blocked=bk(('X1',)))
-        G = [None] * D                                                     # g_l = d sdf / d h_l (l < 7)
+        # g_l = d sdf / d h_l (l < 7) is not stored: only delta_l = s_l g_l is, and the adjoint's
+        # g zdot s' term reads delta (NrTrainGemm.g_scaled: s' / s = 100 (1 - s))
         for l in range(D - 1, 0, -1):                                      # B7..B1: op index 16 - l
             i = 16 - l
             delta[l - 1] = torch.empty(P, wd[l - 1], device=dev)
-            G[l - 1] = torch.empty(P, wd[l - 1], device=dev)
-            if l == 4:  # [g_3 (14 blocks) ; e_skip (4 blocks)]
+            if l == 4:  # [g_3 (14 blocks, not stored) ; e_skip (4 blocks)]
                 e_skip = torch.empty(P, 64, device=dev)
-                _tg(op(i), P, shp(i, 0, 4), L.TG_MUL, delta[4], 256, 256, G[3], 224, yb=e_skip, ldyb=64,
-                    y2=delta[3], ldy2=224, a=S[3], lda=224, stream=st, blocked=bk(('X1', 'Y', 'Y2', 'A')))
+                _tg(op(i), P, shp(i, 0, 4), L.TG_MUL, delta[4], 256, 256, None, 0, yb=e_skip, ldyb=64,
+                    y2=delta[3], ldy2=224, a=S[3], lda=224, stream=st, blocked=bk(('X1', 'Y2', 'A')))
             else:
-                _tg(op(i), P, shp(i), L.TG_MUL, delta[l], wd[l], nv[l], G[l - 1], wd[l - 1], y2=delta[l - 1],
-                    ldy2=wd[l - 1], a=S[l - 1], lda=wd[l - 1], stream=st, blocked=bk(('X1', 'Y', 'Y2', 'A')))
+                _tg(op(i), P, shp(i), L.TG_MUL, delta[l], wd[l], nv[l], None, 0, y2=delta[l - 1],
+                    ldy2=wd[l - 1], a=S[l - 1], lda=wd[l - 1], stream=st, blocked=bk(('X1', 'Y2', 'A')))
         e_first = torch.empty(P, 64, device=dev)                           # B0
         _tg(op(16), P, shp(16), L.TG_NONE, delta[0], 256, 256, e_first, 64, stream=st, blocked=bk(('X1',)))
         nab = torch.empty(P, 3, device=dev)
@@ -751,7 +753,7 @@ class SdfNablaTG(torch.autograd.Function):
                                      L.ptr(nab), st))
         ctx.surface = surface
         ctx.want_feat = want_feat
-        ctx.save_for_backward(x, h0, *H, *S, *G[:D - 1], *delta, *Ws, *bs)
+        ctx.save_for_backward(x, h0, *H, *S, *delta, *Ws, *bs)
         return (sdf, nab, feat) if want_feat else (sdf, nab)
 
     @staticmethod
@@ -761,9 +763,8 @@ class SdfNablaTG(torch.autograd.Function):
         x, h0 = saved[0], saved[1]
         H = saved[2:2 + D]
         S = saved[2 + D:2 + 2 * D]
-        G = list(saved[2 + 2 * D:2 + 3 * D - 1]) + [None]
-        delta = saved[1 + 3 * D:1 + 4 * D]
-        Ws = saved[1 + 4 * D:1 + 4 * D + D + 1]
+        delta = saved[2 + 2 * D:2 + 3 * D]
+        Ws = saved[2 + 3 * D:2 + 3 * D + D + 1]
         surface = ctx.surface
         g_feat = rest[0] if ctx.want_feat else None
         dev = x.device
@@ -813,7 +814,7 @@ class SdfNablaTG(torch.autograd.Function):
         for l in range(D - 1, 0, -1):                                      # B7..B1 -> zbar_{l-1}
             i = 16 - l
             Z[l - 1] = torch.empty(P, wd[l - 1], device=dev)
-            gz = dict(g=G[l - 1], ldg=wd[l - 1], zd=ZD[l - 1], ldzd=wd[l - 1]) if tangent else {}
+            gz = dict(g=delta[l - 1], ldg=wd[l - 1], g_scaled=True, zd=ZD[l - 1], ldzd=wd[l - 1]) if tangent else {}
             _tg(op(i), P, shp(i, 0, 4 if l == 4 else 0), L.TG_SPADJ, Z[l], wd[l], nv[l], Z[l - 1], wd[l - 1],
                 a=S[l - 1], lda=wd[l - 1], stream=st, blocked=bk(('X1', 'Y', 'A') + ('G', 'ZD') * tangent), **gz)
         # weight gradients on nr_wgrad (f16x3 MFMA): dW_l = zbar_l^T hin_l + delta_l^T hdot_in_l (one
