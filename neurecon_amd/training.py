@@ -902,22 +902,26 @@ class RadianceTG(torch.autograd.Function):
         dW, db = [None] * 5, [None] * 5
         db[4] = torch.empty(3, device=dev)
         dW[4] = _wg([(g, H[3])], colsum=db[4])      # weight gradients on nr_wgrad (bias gradient fused)
+        # the pre-activation adjoints gz stay inside this function: 16 x 16 blocked (SdfNablaTG's note)
+        bk = _blk_bits(P)
+        wb = _WG_BLK if bk(('Y',)) else (lambda a, b: 0)
         gz = torch.empty(P, 256, device=dev)
-        _tg(tb + info[5][0], P, (2, 0, 16, 0), L.TG_RELUMASK, g, 3, 3, gz, 256, bias=False, a=H[3], lda=256, stream=st)
+        _tg(tb + info[5][0], P, (2, 0, 16, 0), L.TG_RELUMASK, g, 3, 3, gz, 256, bias=False, a=H[3], lda=256, stream=st,
+            blocked=bk(('Y',)))
         for l in range(3, 0, -1):  # gz = d z_l  ->  d z_{l-1} through W_l^T (training ops 6, 7, 8)
             db[l] = torch.empty(256, device=dev)
-            dW[l] = _wg([(gz, H[l - 1])], colsum=db[l])
+            dW[l] = _wg([(gz, H[l - 1])], colsum=db[l], blocked=wb(True, False))
             gn = torch.empty(P, 256, device=dev)
             _tg(tb + info[5 + (4 - l)][0], P, (16, 0, 16, 0), L.TG_RELUMASK, gz, 256, 256, gn, 256, bias=False,
-                a=H[l - 1], lda=256, stream=st)
+                a=H[l - 1], lda=256, stream=st, blocked=bk(('X1', 'Y')))
             gz = gn
         db[0] = torch.empty(256, device=dev)
-        dW[0] = _wg([(gz, inp)], colsum=db[0])  # W0 columns [small | feature], as inp
+        dW[0] = _wg([(gz, inp)], colsum=db[0], blocked=wb(True, False))  # W0 columns [small | feature], as inp
         nbo0 = info[9][2]
         d_feat = torch.empty(P, 256, device=dev)
         d_small = torch.empty(P, 16 * (nbo0 - 16), device=dev)
         _tg(tb + info[9][0], P, (16, 0, nbo0, nbo0 - 16), L.TG_NONE, gz, 256, 256, d_feat, 256, bias=False,
-            yb=d_small, ldyb=16 * (nbo0 - 16), stream=st)
+            yb=d_small, ldyb=16 * (nbo0 - 16), stream=st, blocked=bk(('X1',)))
         d_nrm = d_small[:, 3 + nvw:3 + nvw + 3].contiguous() if view else None
         return (None, None, d_nrm, d_feat, None, *dW, *db)
 
