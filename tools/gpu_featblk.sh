@@ -1,4 +1,6 @@
 #!/bin/bash
+# (record of an r04 measurement: the experiment build it compares was removed after it was measured;
+#  results and reading in profiles/r04/ and DESIGN.md -- rerunning needs that variant restored)
 # blocked geometry feature (sdf4 -> rad4) experiment: config-(b) bench, default build vs featblk, alternated;
 # then the render parity tests on the featblk build (its results are valid: producer and consumer agree)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (record of an r04 measurement: the experiment build it compares was removed after it was measured;
+#  results and reading in profiles/r04/ and DESIGN.md -- rerunning needs that variant restored)
 # tgemm epilogue access-pattern experiment: training bench with the default build vs NR_EXP_TG_LINEAR
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (record of an r04 measurement: the experiment build it compares was removed after it was measured;
+#  results and reading in profiles/r04/ and DESIGN.md -- rerunning needs that variant restored)
 # nr_wgrad ping-pong phase split: base (waves w & 4 split first) vs none vs adjacent waves; parity
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp

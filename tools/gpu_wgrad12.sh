@@ -1,4 +1,6 @@
 #!/bin/bash
+# (record of an r04 measurement: the experiment build it compares was removed after it was measured;
+#  results and reading in profiles/r04/ and DESIGN.md -- rerunning needs that variant restored)
 # nr_wgrad 256-wide n tile vs 128 (NR_WGRAD_NB), parity of both, training bench
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
