@@ -315,8 +315,14 @@ def _train_render(rays_o, rays_d, model, obj_bounding_radius=1.0, batched=False,
                                    L.stream_of(dev)))
     surf = model.implicit_surface
     Ws = T.effective_weights(surf)  # one weight_norm per layer, shared by both evaluations
-    sdf, nablas, _ = T.sdf_nablas(surf, pts.reshape(-1, 3), False, Ws)        # neus.py:294
-    _, nab_m, feat_m = T.sdf_nablas(surf, mids.reshape(-1, 3), True, Ws)       # neus.py:103-106, :298
+    if T.uses_train_gemm(surf):  # samples and mid-points in one evaluation (feature for the mid-points only)
+        Ps = n * S
+        sdf_all, nab_all, feat_m = T.sdf_nablas(surf, torch.cat([pts.reshape(-1, 3), mids.reshape(-1, 3)]), True,
+                                                Ws, feat_from=Ps)
+        sdf, nablas, nab_m = sdf_all[:Ps], nab_all[:Ps], nab_all[Ps:]
+    else:
+        sdf, nablas, _ = T.sdf_nablas(surf, pts.reshape(-1, 3), False, Ws)    # neus.py:294
+        _, nab_m, feat_m = T.sdf_nablas(surf, mids.reshape(-1, 3), True, Ws)   # neus.py:103-106, :298
     view = rd[:, None, :].expand(n, S - 1, 3).reshape(-1, 3).contiguous()
     rad = T.radiance(model.radiance_net, mids.reshape(-1, 3), view, nab_m, feat_m)
     s = model.forward_s().float().reshape(-1)[:1]

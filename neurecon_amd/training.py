@@ -663,11 +663,11 @@ def _pad16(n):
     return 16 * ((n + 15) // 16)
 
 
-def _blk_bits(P):
-    """NrTrainGemm.blocked bits from role names, or always 0 when P is not a multiple of 16 (the blocked
-    layout tiles whole 16-point blocks) or NR_TRAIN_BLOCKED=0 (row-major everywhere: the bit-identity
-    test's reference)"""
-    on = P % 16 == 0 and os.environ.get('NR_TRAIN_BLOCKED', '1') != '0'
+def _blk_bits(P, row0=0):
+    """NrTrainGemm.blocked bits from role names, or always 0 when P (or a row offset row0 the caller
+    addresses) is not a multiple of 16 (the blocked layout tiles whole 16-point blocks) or
+    NR_TRAIN_BLOCKED=0 (row-major everywhere: the bit-identity test's reference)"""
+    on = P % 16 == 0 and row0 % 16 == 0 and os.environ.get('NR_TRAIN_BLOCKED', '1') != '0'
     return lambda roles: sum(getattr(L, 'BLK_' + r) for r in roles) if on else 0
 
 
@@ -696,13 +696,14 @@ class SdfNablaTG(torch.autograd.Function):
     hdot_in_l (nr_wgrad)."""
 
     @staticmethod
-    def forward(ctx, x, surface, want_feat, *params):
+    def forward(ctx, x, surface, want_feat, feat_from, *params):
         D = 8
         Ws, bs = params[:D + 1], params[D + 1:]
         dev = x.device
         st = L.stream_of(dev)
         x = x.contiguous()
         P = x.shape[0]
+        assert 0 <= feat_from < P or not want_feat
         desc, packed = surface.nr_packed(dev)
         info = _op_info('sdf', desc, 18)
         base = packed.data_ptr()
@@ -718,7 +719,7 @@ class SdfNablaTG(torch.autograd.Function):
         sdf = torch.empty(P, device=dev)
         delta = [None] * D
         delta[7] = torch.empty(P, 256, device=dev)
-        bk = _blk_bits(P)
+        bk = _blk_bits(P, feat_from)
         for l in range(D):                                                 # F0..F7
             if l == 0:
                 xin = dict(x1=h0, ld1=64, n1=nf)
@@ -731,9 +732,10 @@ class SdfNablaTG(torch.autograd.Function):
                 stream=st, blocked=bk(('X1',) * (l > 0) + ('Y', 'Y2') + ('Y3',) * (l == 7)), **xin, **extra)
         sdf.add_(bs[D].detach()[0])                                        # + b8 (no host sync)
         feat = None
-        if want_feat:                                                      # F8
-            feat = torch.empty(P, 256, device=dev)
-            _tg(op(8), P, shp(8), L.TG_NONE, H[7], 256, 256, feat, 256, stream=st, blocked=bk(('X1',)))
+        if want_feat:                                                      # F8 on points [feat_from, P)
+            feat = torch.empty(P - feat_from, 256, device=dev)
+            _tg(op(8), P - feat_from, shp(8), L.TG_NONE, H[7].data_ptr() + feat_from * 256 * 4, 256, 256, feat, 256,
+                stream=st, blocked=bk(('X1',)))  # a row offset of a multiple of 16: the same in both layouts
         # g_l = d sdf / d h_l (l < 7) is not stored: only delta_l = s_l g_l is, and the adjoint's
         # g zdot s' term reads delta (NrTrainGemm.g_scaled: s' / s = 100 (1 - s))
         for l in range(D - 1, 0, -1):                                      # B7..B1: op index 16 - l
@@ -753,6 +755,7 @@ class SdfNablaTG(torch.autograd.Function):
                                      L.ptr(nab), st))
         ctx.surface = surface
         ctx.want_feat = want_feat
+        ctx.feat_from = feat_from
         ctx.save_for_backward(x, h0, *H, *S, *delta, *Ws, *bs)
         return (sdf, nab, feat) if want_feat else (sdf, nab)
 
@@ -779,7 +782,7 @@ class SdfNablaTG(torch.autograd.Function):
         wd = [256, 256, 256, 224, 256, 256, 256, 256]
         nv = [256, 256, 256, 217, 256, 256, 256, 256]
         tangent = g_nab is not None
-        bk = _blk_bits(P)
+        bk = _blk_bits(P, ctx.feat_from)
         wb = _WG_BLK if bk(('Y',)) else (lambda a, b: 0)
         ZD = [None] * D
         HD = [None] * D                                                   # hdot_l = s_l zdot_l
@@ -805,7 +808,14 @@ class SdfNablaTG(torch.autograd.Function):
         Wl = [surface.surface_fc_layers[i] for i in range(D + 1)]
         tp = _train_pack(surface, 'sdf', Ws, [l.bias for l in Wl], dev)  # the forward's effective weights
         gs = torch.zeros(P, device=dev) if g_sdf is None else g_sdf.contiguous()
-        gf = torch.zeros(P, 256, device=dev) if g_feat is None else g_feat.contiguous()
+        if g_feat is None:
+            gf = torch.zeros(P, 256, device=dev)
+        elif ctx.feat_from:  # no feature (zero gradient) on the points before feat_from
+            gf = torch.empty(P, 256, device=dev)
+            gf[:ctx.feat_from].zero_()
+            gf[ctx.feat_from:].copy_(g_feat)
+        else:
+            gf = g_feat.contiguous()
         Z = [None] * D
         Z[7] = torch.empty(P, 256, device=dev)
         _tg(tp.data_ptr() + info[17][0], P, (18, 2, 16, 0), L.TG_SPADJ, gf, 256, 256, Z[7], 256, x2=gs, ld2=1, n2=1,
@@ -847,7 +857,7 @@ class SdfNablaTG(torch.autograd.Function):
                 hin = H[l - 1][:, :nv[l - 1]]
                 pr = [(zb, hin)] + ([(delta[l][:, :nv[l]], HD[l - 1][:, :nv[l - 1]])] if tangent else [])
                 dW[l] = _wg(pr, colsum=db[l], blocked=wb(True, True))
-        return (None, None, None, *dW, *db)
+        return (None, None, None, None, *dW, *db)
 
 
 class RadianceTG(torch.autograd.Function):
@@ -940,15 +950,19 @@ def effective_weights(surface):
     return [l.effective_weight() for l in surface.surface_fc_layers]
 
 
-def sdf_nablas(surface, x, want_feat, Ws=None):
+def sdf_nablas(surface, x, want_feat, Ws=None, feat_from=0):
     """Differentiable (sdf, nablas, feature) of a neurecon_amd ImplicitSurface at points x [P,3]
-    (Ws: effective_weights(surface) of this step, computed here when not given)."""
+    (Ws: effective_weights(surface) of this step, computed here when not given).  feat_from (the
+    nr_train_gemm path only): the feature is computed for points [feat_from, P) only, so one call can
+    evaluate two point sets that need it and do not (NeuS's samples and mid-points)."""
     if Ws is None:
         Ws = effective_weights(surface)
     bs = [l.bias for l in surface.surface_fc_layers]
     if uses_train_gemm(surface):
-        out = SdfNablaTG.apply(x.reshape(-1, 3).float().contiguous(), surface, bool(want_feat), *Ws, *bs)
+        out = SdfNablaTG.apply(x.reshape(-1, 3).float().contiguous(), surface, bool(want_feat), int(feat_from),
+                               *Ws, *bs)
         return out if want_feat else (out[0], out[1], None)
+    assert feat_from == 0, 'feat_from: nr_train_gemm path only'
     cfg = (surface.D, tuple(surface.skips), surface.embed_multires, bool(want_feat), bool(surface.use_siren))
     out = SdfNabla.apply(x.reshape(-1, 3).float().contiguous(), cfg, *Ws, *bs)
     return out if want_feat else (out[0], out[1], None)
