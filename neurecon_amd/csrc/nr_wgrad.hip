@@ -11,16 +11,20 @@
 //    wgrad_reduce sums the S partials in slice order (deterministic) into C.  The n tiles of one slice
 //    run on one XCD back to back (blockIdx -> XCD is round robin), so their shared A rows come from L2.
 //  * k-step: every wave loads 32 A columns of the 32 rows (4 x 16 B per lane) and 16 B columns
-//    (2 x 16 B); per column quad (4 columns x 32 rows) a power-of-two scale from the quad's max
-//    (|v| scale < 2^14; three / four ds_swizzle + permlane32 steps), v * scale split into f16 hi + lo
-//    (22 significant bits), both planes written row-major into LDS (row strides 544 / 288 B: the 8
-//    rows a 32-lane half reads land 8 banks apart).  Two k-steps of global loads are in flight in
-//    registers while a k-step's MFMAs run from LDS (double-buffered stages, one barrier per k-step).
+//    (2 x 16 B) through buffer resources rebased per k-step (rows past P read as zero; loop-invariant
+//    lane offsets; operands row-major or 16 x 16 blocked, NrWgrad.blocked), three k-steps in flight in
+//    registers, every load issued unconditionally (no branch around a load).
+//  * per column quad (4 columns x 32 rows) a running power-of-two scale: the quad's max (DPP row
+//    rotations + permlane16/32 swaps) only lowers the exponent, with 16x headroom, when it would reach
+//    2^14; v * scale split into f16 hi + lo (22 significant bits), both planes written row-major into
+//    LDS (row strides 544 / 288 B: the 8 rows a 32-lane half reads land 8 banks apart);
+//    double-buffered stages, one barrier per k-step.
 //  * MFMA operands come back with ds_read_b64_tr_b16 (4 rows x 16 columns, delivered column-major):
 //    lane group G of a 16x16x32 operand takes rows {4G..4G+3} and {16+4G..16+4G+3}, the same rows for
-//    A and B, so each k-slot pairs the same point.  Per 16x16 tile and k-step: t = Al Bh + Ah Bl + Ah Bh
-//    (fresh accumulator), then C += t * 2^-(eA + eB): a lane's 4 output rows are one A quad and its
-//    column one B quad, so one factor per lane and tile (exact).
+//    A and B, so each k-slot pairs the same point.  Per 16x16 tile and k-step Al Bh + Ah Bl + Ah Bh
+//    accumulate in place (a lane's 4 output rows are one A quad and its column one B quad); a k-step that
+//    lowered an exponent rescales the affected tiles by 2^(e_new - e_old) first, and 2^-(eA + eB) is
+//    applied once at the end.
 //  * optional: column sums of A_0 (the bias gradient) and B_0^T v for a [P] vector v (the sdf row of
 //    the output layer, dW8[0, :]) accumulated in fp32 from the loaded values, reduced in fixed order.
 #include <algorithm>
