@@ -544,7 +544,9 @@ def config_train(dev, precision, n_rays, steps, warmup, sync, adam='fused'):
     table, _ = _kernel_summary(ks, precision, 289)
     out = {'workload': 'NeuS Trainer.forward + backward (double backward through the nablas) + Adam, 512 rays x 128 '
                        'samples', 'value': round(n_rays / dt, 1), 'unit': 'rays/s', 'ms_per_step': round(dt * 1e3, 3),
-           'steps': steps, 'library_kernels': table}
+           'steps': steps, 'library_kernels': table,
+           # the dominant kernel (the layer GEMM, HBM-bound) and nr_wgrad, from the census step's HIP events
+           'roofline': train_roofline(ks, dt, 1, ks) if precision == 'f16x3' else None}
     try:
         from torch.profiler import ProfilerActivity, profile
         with profile(activities=[ProfilerActivity.CUDA]) as prof:
@@ -771,7 +773,7 @@ def run(args):
             out = {'metric': 'training rays/sec, NeuS (configs/neus.yaml: 512 rays per GPU, fwd+bwd+Adam)',
                    'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
                    'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
-                   'scaling': 'weak', 'vs_baseline': None, 'dtype': (dtype + ' layer GEMMs (nr_train_gemm; radiance forward f32), f32 weight gradients'
+                   'scaling': 'weak', 'vs_baseline': None, 'dtype': (dtype + ' layer GEMMs (nr_train_gemm) and weight gradients (nr_wgrad); radiance forward f32'
                              if args.precision == 'f16x3' else 'f32'),
                    'data': 'synthetic (random 64x64 targets, config-(b) camera, seeded geometric-init weights)',
                    'config': {'workload': 'NeuS Trainer.forward + backward (double backward through the nablas) + '
