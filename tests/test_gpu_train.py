@@ -479,3 +479,26 @@ def test_blocked_layout_training_step_bit_identical(golden, name, monkeypatch):
         assert torch.equal(l_row[k], l_blk[k]), k
     for k in g_row:
         assert torch.equal(g_row[k], g_blk[k]), (k, float((g_row[k] - g_blk[k]).abs().max()))
+
+
+def test_merged_sample_and_midpoint_evaluation_matches_separate():
+    """NeuS training evaluates its samples and mid-points in one SdfNablaTG call (feat_from: the feature
+    for the mid-points only): sdf, nablas and features are per point, so they equal the two separate
+    evaluations bit for bit; the weight gradients are sums over both point sets either way (checked
+    against the oracle by the training-step tests)"""
+    from neurecon_amd import training as T
+    m = neus_model(wg.neus_state(seed=3), precision='f16x3')
+    surf = m.implicit_surface
+    if not T.uses_train_gemm(surf):
+        pytest.skip('not on the nr_train_gemm path')
+    g = torch.Generator().manual_seed(4)
+    pts = (torch.rand(4096, 3, generator=g) * 2 - 1).cuda()
+    mids = (torch.rand(4064, 3, generator=g) * 2 - 1).cuda()
+    with torch.no_grad():
+        Ws = T.effective_weights(surf)
+        s1, n1, _ = T.sdf_nablas(surf, pts, False, Ws)
+        _, n2, f2 = T.sdf_nablas(surf, mids, True, Ws)
+        s_all, n_all, f_m = T.sdf_nablas(surf, torch.cat([pts, mids]), True, Ws, feat_from=pts.shape[0])
+    torch.cuda.synchronize()
+    assert torch.equal(s_all[:4096], s1) and torch.equal(n_all[:4096], n1)
+    assert torch.equal(n_all[4096:], n2) and torch.equal(f_m, f2)
