@@ -1,4 +1,6 @@
 #!/bin/bash
+# (record of an r04 measurement: both the built-out change and the comparison library were removed after
+#  it was measured; results in profiles/r04/feat_blocked_experiment.txt)
 # blocked geometry feature between the render's SDF and radiance launches: render parity suites, then
 # the config-(b) bench against the previous build (neurecon_amd/prev_cmp.so), alternated
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
