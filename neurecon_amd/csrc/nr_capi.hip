@@ -6,6 +6,7 @@
 #include <string>
 
 #include "nr_common.h"
+#include <cstdlib>
 #include "nr_mlp.h"
 #include "nr_tgemm.h"
 #include "nr_neus.h"
@@ -638,9 +639,39 @@ static int unisurf_chunk(const NrUnisurfArgs& a, const UniPlan& pl, int64_t ray0
     hipLaunchKernelGGL(uni_prologue, grd, blk, 0, st, c, a.rays_o + ray0 * 3, a.rays_d + ray0 * 3);
   }
   NR_HIP_CHECK(hipGetLastError());
-  if ((rc = launch_sdf(SL, a.sdf_packed, c.pts_m, (int64_t)a.N_steps * R, c.sm, nullptr, nullptr, a.sdf->multires,
-                       nullptr, 0, st)))
-    return rc;
+  {  // the march (ray_casting.py:88-101) in chunks of kMarchK steps over the rays still without a crossing
+    // NR_UNISURF_FULL_MARCH=1: every step of every ray in one launch (the bit-identity test's reference)
+    const char* fm = getenv("NR_UNISURF_FULL_MARCH");
+    const bool full = fm && atoi(fm) != 0;
+    const int N = a.N_steps, K0 = (full || N < kMarchK) ? N : kMarchK;
+    if ((rc = launch_sdf(SL, a.sdf_packed, c.pts_m, (int64_t)K0 * R, c.sm, nullptr, nullptr, a.sdf->multires, nullptr,
+                         0, st)))
+      return rc;
+    int* act[2] = {(int*)(ws + pl.o_act0), (int*)(ws + pl.o_act1)};
+    int* cnt = (int*)(ws + pl.o_acnt);
+    float* ptsc = F(pl.o_ptsc);
+    float* sc = F(pl.o_sc);
+    NR_HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int), st));
+    hipLaunchKernelGGL(uni_march_scan, grd, blk, 0, st, c, 0, K0, nullptr, nullptr, act[0], cnt);
+    NR_HIP_CHECK(hipGetLastError());
+    int cur = 0;
+    for (int s0 = K0; s0 < N; s0 += kMarchK) {
+      const int Kc = N - s0 < kMarchK ? N - s0 : kMarchK;
+      const dim3 gq((unsigned)(((int64_t)Kc * R + 255) / 256));
+      hipLaunchKernelGGL(uni_march_gather, gq, dim3(256), 0, st, c, s0, Kc, act[cur], cnt + cur, ptsc);
+      NR_HIP_CHECK(hipGetLastError());
+      if ((rc = launch_sdf(SL, a.sdf_packed, ptsc, (int64_t)Kc * R, sc, nullptr, nullptr, a.sdf->multires, nullptr, 0,
+                           st, cnt + cur, Kc)))
+        return rc;
+      hipLaunchKernelGGL(uni_march_scatter, gq, dim3(256), 0, st, c, s0, Kc, act[cur], cnt + cur, sc);
+      NR_HIP_CHECK(hipGetLastError());
+      NR_HIP_CHECK(hipMemsetAsync(cnt + (cur ^ 1), 0, sizeof(int), st));
+      hipLaunchKernelGGL(uni_march_scan, grd, blk, 0, st, c, s0, s0 + Kc, act[cur], cnt + cur, act[cur ^ 1],
+                         cnt + (cur ^ 1));
+      NR_HIP_CHECK(hipGetLastError());
+      cur ^= 1;
+    }
+  }
   hipLaunchKernelGGL(uni_root, grd, blk, 0, st, c);
   NR_HIP_CHECK(hipGetLastError());
   for (int i = 0; i < (a.no_secant ? 0 : a.N_secant_steps); ++i) {

@@ -48,10 +48,16 @@ struct UniOut {
   float* radiance; float* sdf; float* nablas; float* alpha; float* weights;
 };
 
+// The root-finding march evaluates its steps in chunks of kMarchK: a ray leaves the march at its first
+// sign change (uni_root only reads up to there), so later chunks run on the device-compacted rays
+// still without one.  Same values at every step uni_root reads: the maps are bit-identical.
+constexpr int kMarchK = 32;
+
 struct UniPlan {
   int64_t Rc;
   size_t o_ro, o_rd, o_near, o_far, o_thr, o_ptsm, o_sm, o_sec, o_ptss, o_ss, o_dall, o_ptsf, o_sdff, o_nabf;
   size_t o_featf, o_nrmf, o_radf, o_wss, o_mlp;
+  size_t o_act0, o_act1, o_acnt, o_ptsc, o_sc;  // chunked march: active lists, counts, compacted points / sdf
   size_t total;
   int64_t max_windows;
 };
@@ -64,6 +70,10 @@ void unisurf_windows(const NrUnisurfArgs& a, int64_t& rc_rays, int64_t& nw_full,
 
 __global__ void uni_prologue(UniChunk c, const float* rays_o, const float* rays_d);
 __global__ void uni_root(UniChunk c);
+__global__ void uni_march_scan(UniChunk c, int s0, int s1, const int* act_in, const int* n_in, int* act_out,
+                               int* n_out);
+__global__ void uni_march_gather(UniChunk c, int s0, int K, const int* act, const int* n, float* pts);
+__global__ void uni_march_scatter(UniChunk c, int s0, int K, const int* act, const int* n, const float* v);
 __global__ void rf_prologue(UniChunk c, const float* rays_o, const float* rays_d, float near, float far,
                             const float* near_rays, const float* far_rays);
 __global__ void rf_finish(UniChunk c, int64_t ray0, float* d_out, float* pts, uint8_t* mask, uint8_t* msc,

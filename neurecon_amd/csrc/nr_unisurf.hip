@@ -143,6 +143,47 @@ __global__ void uni_root(UniChunk c) {
   c.pts_s[r * 3 + 2] = fadd(c.ro[r * 3 + 2], fmul(dp, c.rd[r * 3 + 2]));
 }
 
+// chunked march (kMarchK): after steps [s0, s1) are evaluated, the rays without a sign change among the
+// pairs (i, i + 1) with i + 1 in [max(s0, 1), s1) -- uni_root's test, in its order -- and steps left
+// are appended to act_out (order free: each ray's points go back to its own slots)
+__global__ void uni_march_scan(UniChunk c, int s0, int s1, const int* __restrict__ act_in,
+                               const int* __restrict__ n_in, int* __restrict__ act_out, int* __restrict__ n_out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = act_in ? *n_in : c.R;
+  if (j >= n) return;
+  const int r = act_in ? act_in[j] : j;
+  const float tau = c.logit_tau;
+  const int i0 = s0 > 0 ? s0 - 1 : 0;
+  float vi = fsub(c.sm[(int64_t)i0 * c.R + r], tau);
+  for (int i = i0; i + 1 < s1; ++i) {
+    const float vn = fsub(c.sm[(int64_t)(i + 1) * c.R + r], tau);
+    if (fmul(vi, vn) < 0.0f) return;  // its first crossing: uni_root stops here
+    vi = vn;
+  }
+  if (s1 < c.N_steps) act_out[atomicAdd(n_out, 1)] = r;
+}
+
+// steps [s0, s0 + K) of the active rays -> compacted points q = j K + t
+__global__ void uni_march_gather(UniChunk c, int s0, int K, const int* __restrict__ act, const int* __restrict__ n,
+                                 float* __restrict__ pts) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (int64_t)*n * K) return;
+  const int j = (int)(q / K), t = (int)(q - (int64_t)j * K);
+  const int64_t src = (int64_t)(s0 + t) * c.R + act[j];
+  pts[q * 3 + 0] = c.pts_m[src * 3 + 0];
+  pts[q * 3 + 1] = c.pts_m[src * 3 + 1];
+  pts[q * 3 + 2] = c.pts_m[src * 3 + 2];
+}
+
+// ... and their sdf back into the march array
+__global__ void uni_march_scatter(UniChunk c, int s0, int K, const int* __restrict__ act, const int* __restrict__ n,
+                                  const float* __restrict__ v) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (int64_t)*n * K) return;
+  const int j = (int)(q / K), t = (int)(q - (int64_t)j * K);
+  c.sm[(int64_t)(s0 + t) * c.R + act[j]] = v[q];
+}
+
 // one secant step (ray_casting.py:17-29) given f at the current estimate
 __global__ void uni_secant(UniChunk c, int last) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -440,6 +481,11 @@ UniPlan unisurf_plan(const NrUnisurfArgs& a, int64_t Rc) {
   p.o_nrmf = take((size_t)P * Rc * 3);
   p.o_radf = take((size_t)P * Rc * 3);
   p.o_wss = take((size_t)p.max_windows * 6);
+  p.o_act0 = take(Rc);
+  p.o_act1 = take(Rc);
+  p.o_acnt = take(2);
+  p.o_ptsc = take((size_t)kMarchK * Rc * 3);
+  p.o_sc = take((size_t)kMarchK * Rc);
   p.o_mlp = off;
   p.total = off + nr_mlp_workspace_bytes(1);
   return p;
