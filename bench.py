@@ -16,6 +16,11 @@ same environment.  n_gpus is the process group's size (asserted equal to --gpus)
   * `strong_scaling_frame_d`: one config-(d) 800x600 NeuS+NeRF++ frame per step, its rays split
     over the ranks (neurecon_amd.dist.render_sharded) and the maps all-gathered inside the timed
     region; rays/s of the frame at this N (strong scaling).
+  * `weak_scaling_e`: config (e) UNISURF, 4096 rays per rank as the rank's contiguous share of one
+    N x 4096-ray batch row: the windowed F.normalize spans ranks, so every render all-reduces the
+    per-window sums of nabla^2 (RCCL) inside the timed region.
+  * `weak_scaling_train`: the NeuS training step, 512 rays per rank, DDP (RCCL gradient all-reduce
+    in backward) at N > 1.
 Prints one JSON line on rank 0.
 """
 import argparse
@@ -49,6 +54,12 @@ RAY_FLOP = 2.0 * (255 * (MAC_SDF_FWD + MAC_SDF_BWD) + 127 * MAC_RAD)
 # HBM-side bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc passes of this bench,
 # tools/gpu_pmc.sh); counters cannot be read live, so the latest committed summary is reported.
 PMC_SUMMARY = {'f16x3': 'profiles/r04/f16x3_pmc_summary.json'}  # tools/gpu_prof_r04.sh (PMC passes of the default bench)
+# matrix-pipe occupancy and effective clock per nabla launch type (rocprofv3 GRBM_GUI_ACTIVE and
+# SQ_VALU_MFMA_BUSY_CYCLES passes of this bench, tools/gpu_mfma_r05.sh -> tools/mfma_summary.py)
+MFMA_SUMMARY = 'profiles/r05/mfma_summary.json'
+MFMA_KERNEL = {'sdf_nabla_fwd': 'void nr::sdf4_kernel<true, false, 1>(nr::SdfKArgs)',
+               'sdf_nabla_bwd': 'void nr::sdf4_kernel<true, false, 2>(nr::SdfKArgs)',
+               'sdf_nabla_feat': 'void nr::sdf4_kernel<true, true, 0>(nr::SdfKArgs)'}
 # device kernels behind each merged library kernel name (sdf_nabla = samples + mid-points launches)
 PMC_KERNEL = {('sdf_nabla', 'f16x3'): ('void nr::sdf4_kernel<true, false>(nr::SdfKArgs)',       # r02 names
                                        'void nr::sdf4_kernel<true, true>(nr::SdfKArgs)',
@@ -89,6 +100,11 @@ def parse():
     ap.add_argument('--no-configs', action='store_true',
                     help='skip the BASELINE configs (c), (e) and the training step in the default line')
     ap.add_argument('--config-steps', type=int, default=5)
+    ap.add_argument('--no-scaling-legs', action='store_true',
+                    help='skip the weak-scaling config-(e) and DDP-training legs of the default workload')
+    ap.add_argument('--leg-steps', type=int, default=5)
+    ap.add_argument('--no-fp32-mode', action='store_true',
+                    help='skip the exact-fp32 rate of config (b) beside the f16x3 headline')
     ap.add_argument('--stub-cpu', action='store_true', help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -292,13 +308,43 @@ def roofline(kstats, precision, census=None):
     per_launch_ms = ms / n
     achieved = fl / n / (per_launch_ms * 1e-3) / 1e12
     traffic, src = pmc_traffic(dom, precision)
+    ev = mfma_evidence(per_type) if precision == 'f16x3' else None
     return {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': peak, 'unit': 'TFLOP/s',
             'frac': round(achieved / peak, 4), 'traffic': traffic, 'traffic_unit': 'bytes/launch',
             'traffic_source': src, 'kernel': dom,
             'avg_launch_ms': round(per_launch_ms, 4), 'launches': n,
             'flop_per_launch': fl / n, 'share_of_device_time': round(share, 4),
+            'mfma_busy': ev['mfma_busy'] if ev else None, 'clock_ghz': ev['clock_ghz'] if ev else None,
+            'mfma_evidence': ev,
             'per_launch_type': per_type,
             'weight_stream': weight_stream(kstats) if precision == 'f16x3' else None}
+
+
+def mfma_evidence(per_type):
+    """per launch type: mfma_busy (fraction of SIMD-cycles the matrix pipe was busy) and clock_ghz from
+    the committed counter summary; the merged kernel's values weighted by each type's device time"""
+    path = os.path.join(ROOT, MFMA_SUMMARY)
+    if not os.path.exists(path) or not per_type:
+        return None
+    with open(path) as f:
+        summary = json.load(f)
+    out, wsum, busy, clk = {}, 0.0, 0.0, 0.0
+    for name, rec in per_type.items():
+        r = summary.get(MFMA_KERNEL.get(name, '-'))
+        if not r or 'mfma_busy' not in r:
+            continue
+        out[name] = {'mfma_busy': round(r['mfma_busy'], 4), 'clock_ghz': round(r['clock_ghz'], 3)}
+        w = rec['avg_launch_ms'] * rec['launches']
+        wsum += w
+        busy += w * r['mfma_busy']
+        clk += w * r['clock_ghz']
+    if not wsum:
+        return None
+    return {'mfma_busy': round(busy / wsum, 4), 'clock_ghz': round(clk / wsum, 3), 'per_launch_type': out,
+            'source': MFMA_SUMMARY,
+            'note': 'rocprofv3 --pmc passes of this bench (GRBM_GUI_ACTIVE; SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x '
+                    'cycles)); counters cannot be read inside the timed run, so the committed summary of the same '
+                    'build is reported'}
 
 
 HBM_PEAK_TBPS = 8.0  # MI355X HBM3E (MI355X_MICROARCH.md)
@@ -536,6 +582,90 @@ def config_e(dev, precision, steps, warmup, sync):
     return out
 
 
+def e_sharded_setup(dev, precision, world):
+    """config (e) at N ranks (weak scaling): the 4096 rays of the config-(e) camera repeated N times as
+    one batch row of N x 4096 rays; each rank renders its contiguous 4096-ray share
+    (neurecon_amd.dist.render_sharded; UNISURF's windowed F.normalize spans the ranks, so the render
+    all-reduces the per-window sums of nabla^2 over the process group, RCCL, inside the step)"""
+    from neurecon_amd import dist as nd
+    from neurecon_amd.frameworks.unisurf import UNISURF, volume_render
+    torch.manual_seed(0)
+    surf = dict(use_siren=False, embed_multires=6, radius_init=1.0, geometric_init=True, D=8, W=256, skips=[4],
+                precision=precision)
+    rad = dict(use_siren=False, embed_multires=-1, embed_multires_view=-1, use_view_dirs=True, D=4, W=256, skips=[],
+               precision=precision)
+    m = UNISURF(W_geo_feat=256, surface_cfg=surf, radiance_cfg=rad).to(dev).eval()
+    ro, rd = camera_for(dev, 64, 64, 80.0, 3.0)
+    ro, rd = ro.repeat(1, world, 1).contiguous(), rd.repeat(1, world, 1).contiguous()
+    kw = dict(batched=True, calc_normal=True, detailed_output=False, logit_tau=0.0, radius_of_interest=4.0,
+              method='secant', N_query=64, N_freespace=32)
+
+    def step():
+        with torch.no_grad():
+            return nd.render_sharded(volume_render, ro, rd, m, gather=False, layout='contiguous', **kw)
+    return step, ro.shape[1]
+
+
+def scaling_legs(args, dev, world, sync, barrier, max_over_ranks):
+    """the weak-scaling legs of the default N-GPU line: config (e) with its window all-reduce, and the
+    DDP training step (gradient all-reduce in backward); barrier + sync around K steps, max over ranks"""
+    legs = {}
+    estep, e_rays = e_sharded_setup(dev, args.precision, world)
+    edt = max_over_ranks(timed(estep, args.leg_steps, 1, sync, barrier))
+    legs['weak_scaling_e'] = {
+        'metric': 'rays/sec, config (e): UNISURF 4096 rays per GPU (256-step march + 8 secant steps, 64 + 32 samples)',
+        'value': round(e_rays * args.leg_steps / edt, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.leg_steps,
+        'warmup': 1, 'ms_per_step': round(edt / args.leg_steps * 1e3, 3), 'scaling': 'weak',
+        'rays_per_step': e_rays, 'rays_per_gpu': e_rays // world,
+        'parallelism': f'contiguous ray shares x{world}' + (' + per-window nabla^2 all-reduce (RCCL) per render'
+                                                            if world > 1 else ''),
+        'collective_in_step': world > 1}
+    tsteps = 2 * args.leg_steps
+    tstep = train_setup(dev, args.precision, args.train_rays, world, args.adam)
+    tdt = max_over_ranks(timed(tstep, tsteps, 2, sync, barrier))
+    legs['weak_scaling_train'] = {
+        'metric': 'training rays/sec, NeuS (configs/neus.yaml: 512 rays per GPU, forward + double backward + Adam)',
+        'value': round(args.train_rays * world * tsteps / tdt, 1), 'unit': 'rays/s', 'n_gpus': world,
+        'steps': tsteps, 'warmup': 2, 'ms_per_step': round(tdt / tsteps * 1e3, 3), 'scaling': 'weak',
+        'rays_per_gpu': args.train_rays,
+        'parallelism': f'DDP x{world} (RCCL gradient all-reduce in backward)' if world > 1 else 'single GPU',
+        'collective_in_step': world > 1}
+    return legs
+
+
+def fp32_mode(args, dev, sync):
+    """config (b) in the exact-fp32 precision mode (v_mfma_f32_16x16x4_f32): rays/s, ms/step, and the
+    nabla kernel's fraction of the 157.3 TF/s fp32 MFMA peak (HIP events of the timed steps)"""
+    from neurecon_amd import _lib as L
+    from neurecon_amd import rend_util
+    from neurecon_amd.frameworks.neus import volume_render
+    model = make_model(dev, 'fp32')
+    c2w, K = camera(dev)
+    ro, rd, _ = rend_util.get_rays(c2w, K, 64, 64)
+    kw = render_kwargs()
+
+    def step():
+        with torch.no_grad():
+            return volume_render(ro, rd, model, **kw)
+    steps = args.leg_steps
+    for _ in range(2):
+        step()
+    sync()
+    L.profile_read()
+    L.profile_enable(True, 'sdf_nabla')
+    try:
+        dt = timed(step, steps, 0, sync, lambda: None)
+    finally:
+        L.profile_enable(False)
+    ks = L.profile_read()
+    roof = roofline(ks, 'fp32')
+    return {'workload': 'config (b), precision fp32 (exact fp32 MFMA v_mfma_f32_16x16x4_f32; same render and kernels)',
+            'value': round(ro.shape[1] * steps / dt, 1), 'unit': 'rays/s', 'ms_per_step': round(dt / steps * 1e3, 3),
+            'steps': steps, 'dtype': 'f32',
+            'roofline': {k: roof[k] for k in ('kernel', 'achieved', 'peak', 'unit', 'frac', 'avg_launch_ms',
+                                               'launches', 'per_launch_type')}}
+
+
 def config_train(dev, precision, n_rays, steps, warmup, sync, adam='fused'):
     """NeuS training step, 512 rays (train_setup): wall rays/s, the library's kernel census, and every
     device kernel of one step by name from torch.profiler (the hipBLASLt `Cijk_*` share included)"""
@@ -745,6 +875,12 @@ def run(args):
                  'steps': args.frame_steps, 'warmup': 1, 'ms_per_step': round(fdt / args.frame_steps * 1e3, 3),
                  'scaling': 'strong', 'rays_per_step': frame_rays, 'rays_per_gpu': frame_rays // world,
                  'parallelism': f'ray-sharded x{world} + all_gather'}
+    legs = None
+    if args.workload == 'b' and not args.no_scaling_legs:
+        legs = scaling_legs(args, dev, world, sync, barrier, max_over_ranks)
+    f32 = None
+    if args.workload == 'b' and args.precision == 'f16x3' and not args.no_fp32_mode and world == 1:
+        f32 = fp32_mode(args, dev, sync)
     cfgs = None
     if args.workload == 'b' and not args.no_configs and world == 1:
         cs, cw = args.config_steps, 1
@@ -807,6 +943,10 @@ def run(args):
                     'roofline': roofline(kf, args.precision, kfc)}
             if frame is not None:
                 out['strong_scaling_frame_d'] = frame
+            if legs is not None:
+                out.update(legs)
+            if f32 is not None:
+                out['fp32_mode'] = f32
             if cfgs is not None:
                 out['configs'] = cfgs
             out['config']['zero_alpha_skip'] = ('mid-points whose alpha is exactly 0 (no SDF decrease between the '
@@ -838,21 +978,69 @@ def run_stub(args, world, rank):
         raise SystemExit(f'bench: --gpus {args.gpus} but the process group has {world} ranks')
     a = torch.randn(64, 64)
     barrier = tdist.barrier if dist else (lambda: None)
-    dt = timed(lambda: a @ a, args.steps, args.warmup, lambda: None, barrier)
+
+    def max_over_ranks(x):
+        if not dist:
+            return x
+        t = torch.tensor([x])
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        return float(t.item())
+    dt = max_over_ranks(timed(lambda: a @ a, args.steps, args.warmup, lambda: None, barrier))
     ranks = [rank]
     if dist:
-        t = torch.tensor([dt])
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        dt = float(t.item())
         got = [None] * world
         tdist.all_gather_object(got, rank)
         ranks = got
+    out = {'metric': 'stub', 'value': args.steps * world / dt, 'unit': 'steps/s', 'n_gpus': world,
+           'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3,
+           'ranks': ranks, 'pid': os.getpid()}
+    if not args.no_scaling_legs:
+        out.update(stub_legs(args, world, barrier, max_over_ranks))
     if rank == 0:
-        print(json.dumps({'metric': 'stub', 'value': args.steps * world / dt, 'unit': 'steps/s', 'n_gpus': world,
-                          'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3,
-                          'ranks': ranks, 'pid': os.getpid()}), flush=True)
+        print(json.dumps(out), flush=True)
     if dist:
         tdist.destroy_process_group()
+
+
+def stub_legs(args, world, barrier, max_over_ranks):
+    """CPU rehearsal of scaling_legs(): the same sharding driver and collectives with stand-in compute.
+    weak_scaling_e: render_sharded over a window-sharded stand-in render whose step all-reduces its
+    per-window partial sums (as UNISURF's window_reduce does); weak_scaling_train: a DDP-wrapped linear
+    model's forward + backward (gradient all-reduce) + Adam."""
+    import torch.distributed as tdist
+    from neurecon_amd import dist as nd
+    n_per = 64
+    ro = torch.randn(1, n_per * world, 3)
+    rd = torch.randn(1, n_per * world, 3)
+    seen = {}
+
+    def fake_unisurf(o, d, model, shard=None, **kw):
+        ss = (o * d).sum(dim=(0, 1)).double()          # this share's partial window sums
+        if shard is not None and tdist.is_initialized():
+            tdist.all_reduce(ss, op=tdist.ReduceOp.SUM)
+        seen['shard'] = shard is not None
+        rgb = o * ss.float().norm()
+        return rgb, rgb[..., 0], {'rgb': rgb}
+    fake_unisurf.window_sharded = True
+    estep = lambda: nd.render_sharded(fake_unisurf, ro, rd, None, gather=False, layout='contiguous', batched=True)
+    edt = max_over_ranks(timed(estep, args.leg_steps, 1, lambda: None, barrier))
+    net = torch.nn.Linear(16, 16)
+    model = torch.nn.parallel.DistributedDataParallel(net) if world > 1 else net
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    x = torch.randn(32, 16)
+
+    def tstep():
+        loss = model(x).square().mean()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    tdt = max_over_ranks(timed(tstep, 2 * args.leg_steps, 2, lambda: None, barrier))
+    return {'weak_scaling_e': {'value': n_per * world * args.leg_steps / edt, 'unit': 'rays/s', 'n_gpus': world,
+                               'scaling': 'weak', 'rays_per_gpu': n_per, 'steps': args.leg_steps,
+                               'collective_in_step': bool(seen.get('shard'))},
+            'weak_scaling_train': {'value': 32 * world * 2 * args.leg_steps / tdt, 'unit': 'rays/s', 'n_gpus': world,
+                                   'scaling': 'weak', 'steps': 2 * args.leg_steps,
+                                   'collective_in_step': world > 1}}
 
 
 if __name__ == '__main__':

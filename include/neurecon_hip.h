@@ -217,14 +217,17 @@ typedef struct {
    * every sample when drawn. */
   int no_defer;
   /* Memory bound of the render (neus.py:384-397: the reference's `rayschunk` loop is the caller's
-   * memory bound).  Rays per internal chunk <= max_chunk_rays (the caller's rayschunk; <= 0: no
-   * bound), and the chunk is sized so that nr_neus_workspace_bytes() <= max_workspace_bytes
-   * (0: NR_DEFAULT_WORKSPACE_BYTES), down to one 16-ray chunk. */
+   * memory bound).  Rays per internal chunk <= max(max_chunk_rays, NR_MIN_CHUNK_RAYS) (the
+   * caller's rayschunk is a hint: a 256-ray validation chunk would leave the per-ray kernels a few
+   * CUs; <= 0: no bound), and the chunk is sized so that nr_neus_workspace_bytes() <=
+   * max_workspace_bytes (0: NR_DEFAULT_WORKSPACE_BYTES), down to one 16-ray chunk: the workspace
+   * budget is the memory bound. */
   int64_t max_chunk_rays;
   size_t max_workspace_bytes;
 } NrNeusArgs;
 
 #define NR_DEFAULT_WORKSPACE_BYTES ((size_t)4 << 30) /* 4 GiB */
+#define NR_MIN_CHUNK_RAYS 4096 /* floor of max_chunk_rays */
 
 size_t nr_neus_workspace_bytes(const NrNeusArgs* a);
 int nr_neus_render(const NrNeusArgs* a, void* stream);
@@ -367,6 +370,10 @@ typedef struct {
    * depth_surface are still written when given) -- rgb / depth / acc may then be NULL */
   float* d_all_out;
   int sample_only;
+  /* full_march != 0: the root-finding march evaluates every step of every ray in one launch (the
+   * reference's schedule, ray_casting.py:88-101; bit-identical outputs, slower).  0 (default): in
+   * chunks of 32 steps over the rays still without a sign change */
+  int full_march;
 } NrUnisurfArgs;
 
 size_t nr_unisurf_workspace_bytes(const NrUnisurfArgs* a);
@@ -417,14 +424,16 @@ int nr_sphere_trace(const NrSdfDesc* d, const void* packed, const float* rays_o,
  * depth 1 on hits).  near / far: scalars, or per-ray [R] device arrays near_rays / far_rays when
  * non-null (the reference's tensor near/far, :53-54, :70-73).  Outputs d_pred [R] (inf if fill_inf,
  * else far, on misses; 0 when the first sample is occupied), pts [R,3] (1 on misses), mask [R],
- * mask_sign_change [R] (u8, optional).  rays_d as given (already normalised).  Workspace:
- * nr_root_find_workspace_bytes. */
+ * mask_sign_change [R] (u8, optional).  rays_d as given (already normalised).  The march runs in
+ * chunks of 32 steps over the rays still without a sign change (a ray's march is read only up to its
+ * first crossing: bit-identical outputs); full_march != 0 evaluates every step of every ray in one
+ * launch (the reference's schedule).  Workspace: nr_root_find_workspace_bytes. */
 size_t nr_root_find_workspace_bytes(int64_t n_rays, int N_steps);
 int nr_root_find(const NrSdfDesc* d, const void* packed, const float* rays_o, const float* rays_d, int64_t n_rays,
                  float near, float far, const float* near_rays, const float* far_rays, int N_steps,
-                 const float* t_march, int N_secant_steps, int no_secant, float logit_tau, int fill_inf, float* d_pred,
-                 float* pts, uint8_t* mask, uint8_t* mask_sign_change, void* workspace, size_t workspace_bytes,
-                 void* stream);
+                 const float* t_march, int N_secant_steps, int no_secant, float logit_tau, int fill_inf,
+                 int full_march, float* d_pred, float* pts, uint8_t* mask, uint8_t* mask_sign_change, void* workspace,
+                 size_t workspace_bytes, void* stream);
 int nr_normalize3(const float* v, int64_t n, float* out, void* stream);
 int nr_surface_finish(float* rgb, const float* nablas, const uint8_t* mask, int64_t n, float* normals, void* stream);
 
@@ -689,6 +698,8 @@ typedef struct {
   size_t workspace_bytes;
   int blocked;        /* NR_WG_BLK_* bits: those operands are 16 x 16 blocked (NR_BLK_* comment above:
                          lda / ldb and P multiples of 16), the rest row-major */
+  int fp32;           /* 0: f16x3 products (hi*hi + hi*lo + lo*hi, running per-quad exponents);
+                         1: exact fp32 products (v_mfma_f32_16x16x4_f32), the fp32-precision nets' path */
 } NrWgrad;
 #define NR_WG_BLK_A0 1
 #define NR_WG_BLK_A1 2

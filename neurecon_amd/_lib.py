@@ -97,6 +97,7 @@ class NrUnisurfArgs(ctypes.Structure):
         ('u_query', _c_p), ('u_free', _c_p),
         ('shard_ray0', _c_i64), ('shard_row_rays', _c_i64), ('window_ss', _c_p), ('window_reduce', _c_p),
         ('window_user', _c_p), ('no_secant', _c_i), ('d_all_out', _c_p), ('sample_only', _c_i),
+        ('full_march', _c_i),
     ]
 
 
@@ -128,7 +129,7 @@ class NrWgrad(ctypes.Structure):
         ('P', _c_i64), ('npairs', _c_i), ('a', _c_p * 2), ('lda', _c_i64 * 2), ('b', _c_p * 2), ('ldb', _c_i64 * 2),
         ('m', _c_i), ('n', _c_i), ('scale', _c_f), ('c', _c_p), ('ldc', _c_i64), ('colsum', _c_p),
         ('avec', _c_p), ('ldv', _c_i64), ('vec', _c_p), ('vec_scale', _c_f), ('workspace', _c_p),
-        ('workspace_bytes', _c_sz), ('blocked', _c_i),
+        ('workspace_bytes', _c_sz), ('blocked', _c_i), ('fp32', _c_i),
     ]
 
 
@@ -167,8 +168,8 @@ _SIGS = {
                                _c_p, _c_p, _c_i, _c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
     'nr_root_find_workspace_bytes': (_c_sz, [_c_i64, _c_i]),
     'nr_root_find': (_c_i, [ctypes.POINTER(NrSdfDesc), _c_p, _c_p, _c_p, _c_i64, ctypes.c_float, ctypes.c_float, _c_p,
-                            _c_p, _c_i, _c_p, _c_i, _c_i, ctypes.c_float, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_sz,
-                            _c_p]),
+                            _c_p, _c_i, _c_p, _c_i, _c_i, ctypes.c_float, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p,
+                            _c_sz, _c_p]),
     'nr_normalize3': (_c_i, [_c_p, _c_i64, _c_p, _c_p]),
     'nr_surface_finish': (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_p, _c_p]),
     'nr_sdf_grid_workspace_bytes': (_c_sz, [_c_i64]),

@@ -429,13 +429,15 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   return NR_OK;
 }
 
-// rays per chunk: at most 16384, the caller's max_chunk_rays (its rayschunk), and as many as keep the
-// workspace within max_workspace_bytes (the plan is affine in the chunk's ray count); deferred
-// chunks (8 KB of slabs per sample) are a multiple of 16 rays, so that every launch starts a tile
+// rays per chunk: at most 16384, the caller's max_chunk_rays (its rayschunk) as a hint floored at
+// NR_MIN_CHUNK_RAYS (the reference's validation rayschunk of 256 would leave the per-ray kernels a
+// few CUs; memory is bounded by the workspace budget), and as many as keep the workspace within
+// max_workspace_bytes (the plan is affine in the chunk's ray count); deferred chunks (8 KB of slabs
+// per sample) are a multiple of 16 rays, so that every launch starts a tile
 static int64_t neus_chunk_rays(const NrNeusArgs* a) {
   const int64_t n = a->n_rays > 0 ? a->n_rays : 1;
   int64_t cap = 16384;
-  if (a->max_chunk_rays > 0) cap = std::min(cap, a->max_chunk_rays);
+  if (a->max_chunk_rays > 0) cap = std::min(cap, std::max<int64_t>(a->max_chunk_rays, NR_MIN_CHUNK_RAYS));
   const size_t budget = a->max_workspace_bytes ? a->max_workspace_bytes : NR_DEFAULT_WORKSPACE_BYTES;
   const bool defer = neus_deferred(*a, 16);
   NrNeusArgs q = *a;  // plan sizes with deferral decided as for a 16-ray-multiple chunk
@@ -639,39 +641,11 @@ static int unisurf_chunk(const NrUnisurfArgs& a, const UniPlan& pl, int64_t ray0
     hipLaunchKernelGGL(uni_prologue, grd, blk, 0, st, c, a.rays_o + ray0 * 3, a.rays_d + ray0 * 3);
   }
   NR_HIP_CHECK(hipGetLastError());
-  {  // the march (ray_casting.py:88-101) in chunks of kMarchK steps over the rays still without a crossing
-    // NR_UNISURF_FULL_MARCH=1: every step of every ray in one launch (the bit-identity test's reference)
-    const char* fm = getenv("NR_UNISURF_FULL_MARCH");
-    const bool full = fm && atoi(fm) != 0;
-    const int N = a.N_steps, K0 = (full || N < kMarchK) ? N : kMarchK;
-    if ((rc = launch_sdf(SL, a.sdf_packed, c.pts_m, (int64_t)K0 * R, c.sm, nullptr, nullptr, a.sdf->multires, nullptr,
-                         0, st)))
-      return rc;
-    int* act[2] = {(int*)(ws + pl.o_act0), (int*)(ws + pl.o_act1)};
-    int* cnt = (int*)(ws + pl.o_acnt);
-    float* ptsc = F(pl.o_ptsc);
-    float* sc = F(pl.o_sc);
-    NR_HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int), st));
-    hipLaunchKernelGGL(uni_march_scan, grd, blk, 0, st, c, 0, K0, nullptr, nullptr, act[0], cnt);
-    NR_HIP_CHECK(hipGetLastError());
-    int cur = 0;
-    for (int s0 = K0; s0 < N; s0 += kMarchK) {
-      const int Kc = N - s0 < kMarchK ? N - s0 : kMarchK;
-      const dim3 gq((unsigned)(((int64_t)Kc * R + 255) / 256));
-      hipLaunchKernelGGL(uni_march_gather, gq, dim3(256), 0, st, c, s0, Kc, act[cur], cnt + cur, ptsc);
-      NR_HIP_CHECK(hipGetLastError());
-      if ((rc = launch_sdf(SL, a.sdf_packed, ptsc, (int64_t)Kc * R, sc, nullptr, nullptr, a.sdf->multires, nullptr, 0,
-                           st, cnt + cur, Kc)))
-        return rc;
-      hipLaunchKernelGGL(uni_march_scatter, gq, dim3(256), 0, st, c, s0, Kc, act[cur], cnt + cur, sc);
-      NR_HIP_CHECK(hipGetLastError());
-      NR_HIP_CHECK(hipMemsetAsync(cnt + (cur ^ 1), 0, sizeof(int), st));
-      hipLaunchKernelGGL(uni_march_scan, grd, blk, 0, st, c, s0, s0 + Kc, act[cur], cnt + cur, act[cur ^ 1],
-                         cnt + (cur ^ 1));
-      NR_HIP_CHECK(hipGetLastError());
-      cur ^= 1;
-    }
-  }
+  // the march (ray_casting.py:88-101) in chunks of kMarchK steps over the rays still without a crossing
+  // (full_march: every step of every ray in one launch, the bit-identity test's reference)
+  if ((rc = run_march(SL, a.sdf_packed, a.sdf->multires, c, a.full_march != 0, (int*)(ws + pl.o_act0),
+                      (int*)(ws + pl.o_act1), (int*)(ws + pl.o_acnt), F(pl.o_ptsc), F(pl.o_sc), st)))
+    return rc;
   hipLaunchKernelGGL(uni_root, grd, blk, 0, st, c);
   NR_HIP_CHECK(hipGetLastError());
   for (int i = 0; i < (a.no_secant ? 0 : a.N_secant_steps); ++i) {

@@ -14,9 +14,17 @@ constexpr size_t kScratchPerWG = (size_t)kWaves * 8 * 16 * 64 * 16;  // exp(100z
 // 2^-L = 1 - softplus'(z) (per chunk [block 2][column][lane] x 12 B: 8 chunks x 1536 B = 12 KB per
 // layer), layer 7 holds d sdf / d z7 (and, during the forward, the parked embedding) in fp32
 // ([block 16][column][lane] x 16 B); 100 KB instead of 8 x 16 KB of fp32 slabs
-constexpr int kSlab24Chunk = 2 * 64 * 12;               // one chunk of one column: 1536 B
-constexpr int kSlab24Layer = 8 * kSlab24Chunk;          // 12 KB
-constexpr int kSlabColBytes = 7 * kSlab24Layer + 16 * 64 * 16;  // 100 KB per column (deferred tile)
+// NR_SLAB32: each code as the fp32 F = 2^23 + round(c 2^23) (bits 0x4B000000 | code), 16 B per 4 codes:
+// the forward forms it with one fma and the reverse pass softplus' = 2 - F 2^-23 with one more, instead
+// of packing / unpacking 24-bit fields (128 KB per column)
+#ifdef NR_SLAB32
+constexpr int kSlabVB = 16;                             // slab bytes per lane and 4 codes
+#else
+constexpr int kSlabVB = 12;
+#endif
+constexpr int kSlab24Chunk = 2 * 64 * kSlabVB;          // one chunk of one column: 1536 B (2 KB with NR_SLAB32)
+constexpr int kSlab24Layer = 8 * kSlab24Chunk;          // 12 KB (16 KB)
+constexpr int kSlabColBytes = 7 * kSlab24Layer + 16 * 64 * 16;  // 100 KB (128 KB) per column (deferred tile)
 
 // SDF GEMM ops in stream order (forward F*, feature F8, backward B*)
 enum SdfOp { F0, F1, F2, F3, F4, F5, F6, F7, F8, B7, B6, B5, B4, B3, B2, B1, B0, kSdfOps };

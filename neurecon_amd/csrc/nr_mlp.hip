@@ -944,6 +944,10 @@ struct Pend4 {
 };
 
 constexpr int kSlabRing = 3;
+// weight-ring slots of the forward-only sdf4_kernel launches (4; 3 = the r04 build, for A/B)
+#ifndef NR_FWD_RING
+#define NR_FWD_RING 4
+#endif
 // cache policy of the forward softplus slab stores (read back by the reverse pass of the same tile)
 #ifndef NR_SLAB_NT
 #define NR_SLAB_NT true
@@ -958,15 +962,25 @@ constexpr int kSlabRing = 3;
 #define NR_FEAT_NT false
 #endif  // softplus' slabs in LDS: one being read, one landing, one being staged
 
-template <int CBMAX>
+// RING: weight-ring slots, issued RING - 1 chunks ahead of the chunk being computed.  3 wherever the
+// slab ring shares the LDS (reverse passes); 4 in the forward-only launches, whose LDS holds the
+// weight ring alone (a 37 KB chunk x 4 = 148 KB): three chunks in flight instead of two against the
+// L2 latency of the stream
+template <int CBMAX, int RING = 3>
 struct WStream4 {
+  static_assert(RING == 3 || RING == 4, "weight ring depth");
+  static constexpr int kRingN = RING;
   char* lds;
   char* slab;  // kSlabRing x kSlab4
   int cur;     // ring slot of the chunk being computed
   int es;      // slab slot the next stage_slab() writes
   int er;      // slab slot the next consumed chunk's epilogue reads
+  int prev;    // RING 4: VMEM instructions this wave issued in the previous chunk iteration
   __device__ __forceinline__ static int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
   __device__ __forceinline__ static int next3(int i) { return i == 2 ? 0 : i + 1; }
+  __device__ __forceinline__ static int nextr(int i) { return i == RING - 1 ? 0 : i + 1; }
+  // the slot chunk c + RING - 1 goes into: the one chunk c - 1 left (every wave is past it)
+  __device__ __forceinline__ int ahead_slot() const { return cur == 0 ? RING - 1 : cur - 1; }
   // BYTES/1 KB pieces; every loader wave (the last kLoad of the workgroup) issues ceil(pieces/kLoad)
   // (a wave past the end repeats the last piece: identical bytes to the same LDS address) so the
   // count is one constant in every loader wave
@@ -1035,25 +1049,43 @@ struct WStream4 {
     constexpr int NB = BYTES / 1024, NPW = pieces<BYTES>();
     if (loader() < 0) return;
     const int first = __builtin_amdgcn_readfirstlane(min(loader() * NPW, NB - NPW)) + j;
-    const int slot = cur == 0 ? 2 : cur - 1;
+    const int slot = ahead_slot();
     glds16m(uniform_ptr(gsrc) + first * 1024, (threadIdx.x & 63) * 16,
             __builtin_amdgcn_readfirstlane(lds_u32(lds) + (uint32_t)(slot * CBMAX) + (uint32_t)(first * 1024)));
   }
   template <int B0, int B1>
   __device__ __forceinline__ void start(const char* g0, const char* g1) {
+    static_assert(RING == 3, "start: the first RING - 1 chunks");
     cur = 0;
     es = 0;
     er = 0;
+    prev = 0;
     dma<B0>(g0, 0);
     dma<B1>(g1, 1);
     wait_vmcnt(npieces<B1>());
     __syncthreads();
   }
+  template <int B0, int B1, int B2>
+  __device__ __forceinline__ void start(const char* g0, const char* g1, const char* g2) {
+    static_assert(RING == 4, "start: the first RING - 1 chunks");
+    cur = 0;
+    es = 0;
+    er = 0;
+    dma<B0>(g0, 0);
+    dma<B1>(g1, 1);
+    dma<B2>(g2, 2);
+    prev = npieces<B2>();
+    wait_vmcnt(npieces<B1>() + npieces<B2>());
+    __syncthreads();
+  }
   template <int BYTES>
-  __device__ __forceinline__ void issue(const char* gsrc) { dma<BYTES>(gsrc, cur == 0 ? 2 : cur - 1); }
+  __device__ __forceinline__ void issue(const char* gsrc) { dma<BYTES>(gsrc, ahead_slot()); }
   // after a mid-chunk flip (cur already names the next chunk's slot): the chunk after that
   template <int BYTES>
-  __device__ __forceinline__ void issue_next(const char* gsrc) { dma<BYTES>(gsrc, next3(cur)); }
+  __device__ __forceinline__ void issue_next(const char* gsrc) {
+    static_assert(RING == 3, "NR_MID_FLIP: 3-slot ring");
+    dma<BYTES>(gsrc, next3(cur));
+  }
   // this wave's softplus' slab of chunk c (blocks 2c, 2c+1, all kNC columns: 2 or 4 KB contiguous) ->
   // the next slab slot; one M0 setting, the instruction offset steps global and LDS address together.
   // Staged two chunk-iterations before the epilogue that reads it.  Returns the DMA instructions issued.
@@ -1064,12 +1096,21 @@ struct WStream4 {
 #endif
     // global: 768 B per piece (64 lanes x 12 B); LDS: 1 KB per piece (lane stride 16 B), so each piece
     // gets its own global base and M0 (the instruction offset would step both by the same amount)
-    const uint32_t voff = (threadIdx.x & 63) * 12;
+    const uint32_t voff = (threadIdx.x & 63) * kSlabVB;
     const char* g = uniform_ptr((const char*)e + kNC * kSlab24Chunk * c);
     const uint32_t base =
         __builtin_amdgcn_readfirstlane(lds_u32(slab) + (uint32_t)(es * kSlab4 + wave_id() * kSlabW));
 #pragma unroll
     for (int piece = 0; piece < 2 * kNC; ++piece) {
+#ifdef NR_SLAB32
+      const char* gp = g + piece * 1024;
+      asm volatile(
+          "s_mov_b32 m0, %2\n\ts_nop 0\n\t"
+          "global_load_lds_dwordx4 %0, %1" NR_SLAB_LD_POL
+          :
+          : "v"(voff), "s"(gp), "s"(base + piece * 1024)
+          : "memory", "m0");
+#else
       const char* gp = g + piece * 768;
       asm volatile(
           "s_mov_b32 m0, %2\n\ts_nop 0\n\t"
@@ -1077,6 +1118,7 @@ struct WStream4 {
           :
           : "v"(voff), "s"(gp), "s"(base + piece * 1024)
           : "memory", "m0");
+#endif
     }
     es = next3(es);
     return 2 * kNC;
@@ -1094,13 +1136,20 @@ struct WStream4 {
     return (const float4*)(lds + off);
   }
   // n: DMA / store instructions this wave issued in the current iteration (vmcnt retires in issue
-  // order: everything older -- the current-plus-one chunk's weights and slab -- has landed after it)
+  // order: everything older -- the current-plus-one chunk's weights and slab -- has landed after it).
+  // RING 4: chunk c+1 went out two iterations ago, so the previous iteration's instructions may stay
+  // in flight too (after a vmcnt(0) drain the count only over-allows instructions that have landed)
   __device__ __forceinline__ void flip(int n) {
-    wait_vmcnt(n);
+    if constexpr (RING == 4) {
+      wait_vmcnt(n + prev);
+      prev = n;
+    } else {
+      wait_vmcnt(n);
+    }
 #ifndef NR_EXP_NO_BARRIER
     __syncthreads();
 #endif
-    cur = next3(cur);
+    cur = nextr(cur);
   }
 };
 
@@ -1198,7 +1247,9 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
                                     Epi&& epi, int lane) {
   constexpr int CB = chunk_bytes(KB);
   constexpr int NCH = NBO / 2;
+  constexpr int LA = WS::kRingN - 1;  // chunks issued ahead of the one being computed
   static_assert(NCH >= 2, "the 2-ahead stream needs >= 2 chunks per op");
+  // (a 4-slot ring's lookahead reaches chunk 2 of the next op: forward ops only, all >= 7 chunks)
   const int g = lane >> 4;
   Z4 zq{};
 #pragma unroll
@@ -1210,6 +1261,7 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
     NR_STAMP(t0);
     int npend = 0;
 #ifdef NR_DMA_SPREAD  // the chunk-two-ahead's pieces go out one per k-step region, beside the MFMAs
+    static_assert(LA == 2, "NR_DMA_SPREAD: 3-slot ring");
     const char* dsrc = nullptr;
     int dkind = 0;
     if (c + 2 < NCH) {
@@ -1222,11 +1274,11 @@ __device__ __forceinline__ void op4(WS& ws, const char* __restrict__ op, const c
       npend = WS::template npieces<NXT_CB>();
     }
 #elif !defined(NR_MID_FLIP)
-    if (c + 2 < NCH) {
-      ws.template issue<CB>(opc + (c + 2) * CB);
+    if (c + LA < NCH) {
+      ws.template issue<CB>(opc + (c + LA) * CB);
       npend = WS::template npieces<CB>();
     } else if (nxc) {
-      ws.template issue<NXT_CB>(nxc + (c + 2 - NCH) * NXT_CB);
+      ws.template issue<NXT_CB>(nxc + (c + LA - NCH) * NXT_CB);
       npend = WS::template npieces<NXT_CB>();
     }
 #endif
@@ -1349,15 +1401,34 @@ __device__ __forceinline__ void pend_chunk(Pend4& pd, float4* base, int first_bl
 // for the reverse pass's staging DMA)
 __device__ __forceinline__ void pend_chunk24(Pend4& pd, float4* layer, int c, int lane, bool nt) {
   const uint32_t l = opaque_lane(lane);
+#ifdef NR_SLAB32  // float4 indices, 16 B stores
+#pragma unroll
+  for (int i = 0; i < 2 * kNC; ++i) pd.o[i] = (uint32_t)(c * kNC * kSlab24Chunk / 16) + (uint32_t)i * 64 + l;
+  pd.put(layer, 2 * kNC, nt, false);
+#else
 #pragma unroll
   for (int i = 0; i < 2 * kNC; ++i) pd.o[i] = (uint32_t)(c * kNC * kSlab24Chunk) + ((uint32_t)i * 64 + l) * 12u;
   pd.put(layer, 2 * kNC, nt, true);
+#endif
 }
 // softplus' = 1 - 2^-L is kept as the 24-bit code of c = 2^-L = 1 / (1 + 2^t): u = floor(c 2^23 + 0.5)
 // (c in [0, 1], 2^23 fits in 24 bits).  The code's absolute error 2^-24 matches fp32's rounding of
 // softplus' near 1 (and of the old 1 - 2^-L cancellation near 0); exact 1 (u = 0) wherever 2^-L < 2^-24,
 // which covers torch's linear branch (100 z > 20: 2^-L < 2^-28.8).  4 codes -> 3 dwords.
 __device__ __forceinline__ uint32_t code24(float c) { return (uint32_t)__builtin_fmaf(c, 8388608.0f, 0.5f); }
+// NR_SLAB32: F = 2^23 + round(c 2^23) in one fma (c 2^23 + 2^23 lies in [2^23, 2^24], where fp32's spacing
+// is 1; c = 1 gives 2^24); the reverse pass's softplus' = 2 - F 2^-23 = 1 - round(c 2^23) 2^-23 is exact
+// (F 2^-23 in [1, 2], Sterbenz), then one multiply by g
+__device__ __forceinline__ float4 code32(float c0, float c1, float c2, float c3) {
+  constexpr float k = 8388608.0f;
+  return make_float4(__builtin_fmaf(c0, k, k), __builtin_fmaf(c1, k, k), __builtin_fmaf(c2, k, k),
+                     __builtin_fmaf(c3, k, k));
+}
+__device__ __forceinline__ float4 code32_mul(float4 F, float4 g) {
+  constexpr float k = -1.0f / 8388608.0f;
+  return make_float4(g.x * __builtin_fmaf(F.x, k, 2.0f), g.y * __builtin_fmaf(F.y, k, 2.0f),
+                     g.z * __builtin_fmaf(F.z, k, 2.0f), g.w * __builtin_fmaf(F.w, k, 2.0f));
+}
 __device__ __forceinline__ float4 pack24(float c0, float c1, float c2, float c3) {
   const uint32_t u0 = code24(c0), u1 = code24(c1), u2 = code24(c2), u3 = code24(c3);
   return make_float4(__uint_as_float(u0 | (u1 << 24)), __uint_as_float((u1 >> 8) | (u2 << 16)),
@@ -1452,7 +1523,11 @@ struct FwdEpi4 {
 #pragma unroll
           for (int o = 0; o < 2; ++o) {
             const int i = (2 * q + o) * 4;
+#ifdef NR_SLAB32
+            pd.v[kNC * o + q] = code32(e[i], e[i + 1], e[i + 2], e[i + 3]);
+#else
             pd.v[kNC * o + q] = pack24(e[i], e[i + 1], e[i + 2], e[i + 3]);
+#endif
           }
       }
     } else if (st == 6) {
@@ -1532,8 +1607,13 @@ struct BwdEpi4 {
       const int q = st >> 2, k = st & 3;
       if (q >= kNC) return;
       if (k < 2) {  // g * softplus'(z) = g - g 2^-L  (FwdEpi4's 24-bit codes of 2^-L)
+#ifdef NR_SLAB32
+        const float4 F = *(const float4*)((const char*)ws.slab_read() + ((kNC * k + q) * 64 + lane) * 16);
+        y[q][k] = code32_mul(F, zz.z[q][k]);
+#else
         const uint4 sw = *(const uint4*)((const char*)ws.slab_read() + ((kNC * k + q) * 64 + lane) * 16);
         y[q][k] = unpack24_mul(sw.x, sw.y, sw.z, zz.z[q][k]);
+#endif
       } else if (k == 2) {
         mrun[q] = amax8(mrun[q], y[q][0], y[q][1]);
       } else {
@@ -1567,9 +1647,14 @@ void sdf4_kernel(SdfKArgs a) {
   static_assert(STAGE == 0 || (NABLA && !FEAT && kNC == 1), "deferred nablas: 16-point waves, no feature");
   constexpr int CB = chunk_bytes(18);  // largest SDF op chunk (F4: 14 + 4 input blocks)
   constexpr int C16 = chunk_bytes(16), C4 = chunk_bytes(4), C14 = chunk_bytes(14), C18 = chunk_bytes(18);
-  __shared__ __attribute__((aligned(16))) char smem[kRing * CB + (NABLA ? kSlabRing * kSlab4 : 0)];
-  static_assert(kRing * CB + kSlabRing * kSlab4 <= 160 * 1024, "LDS budget");
-  WStream4<CB> ws{smem, NABLA ? smem + kRing * CB : nullptr, 0, 0, 0};
+  // launches with a reverse pass share the LDS with the slab ring (3 weight slots); forward-only
+  // launches (STAGE 1 included: its slabs go straight to HBM) stream through a 4-slot ring
+  static_assert((size_t)kW4 * kNC * kSlabColBytes <= kScratchPerWG, "per-workgroup slab scratch");
+  constexpr bool SLABS = NABLA && STAGE != 1;
+  constexpr int RING = SLABS ? 3 : NR_FWD_RING;
+  __shared__ __attribute__((aligned(16))) char smem[RING * CB + (SLABS ? kSlabRing * kSlab4 : 0)];
+  static_assert(RING * CB + (SLABS ? kSlabRing * kSlab4 : 0) <= 160 * 1024, "LDS budget");
+  WStream4<CB, RING> ws{smem, SLABS ? smem + RING * CB : nullptr, 0, 0, 0, 0};
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int j = lane & 15, g = lane >> 4;
   const char* W = a.packed;
@@ -1605,6 +1690,7 @@ void sdf4_kernel(SdfKArgs a) {
   if (kWPE == 2 && wave >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
   if constexpr (STAGE == 2) ws.template start<C16, C16>(OP(B7), OP(B7) + C16);
+  else if constexpr (RING == 4) ws.template start<C4, C4, C4>(OP(F0), OP(F0) + C4, OP(F0) + 2 * C4);
   else ws.template start<C4, C4>(OP(F0), OP(F0) + C4);
   Pend4 pd{};
   NoPre4 nopre;
@@ -1844,7 +1930,7 @@ void sdf4_kernel(SdfKArgs a) {
           if (c + 1 == NBOo / 2 && lnext >= 0) return ws.stage_slab(slab(lnext), 0);
           return 0;
         };
-        BwdEpi4<NMAIN, WStream4<CB>> epi{oh, ol, sc, ws, park, park_blk, mrun, pd, lane};
+        BwdEpi4<NMAIN, decltype(ws)> epi{oh, ol, sc, ws, park, park_blk, mrun, pd, lane};
         op4<KBo, NBOo, NXC, false, false>(ws, OP(opi), nxt, ih, il, xinv, pd, pre, epi, lane);
         finish(sc);
       };

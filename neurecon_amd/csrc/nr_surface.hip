@@ -161,7 +161,9 @@ constexpr int kSecFloats = 8;          // per-ray secant state (nr_unisurf.hip k
 
 struct RootPlan {
   int64_t Rc;
-  size_t o_ro, o_rd, o_near, o_far, o_ptsm, o_sm, o_sec, o_ptss, o_ss, total;
+  size_t o_ro, o_rd, o_near, o_far, o_ptsm, o_sm, o_sec, o_ptss, o_ss;
+  size_t o_act0, o_act1, o_acnt, o_ptsc, o_sc;  // chunked march (run_march): active lists, counts, compacted points
+  size_t total;
 };
 
 static RootPlan root_plan(int64_t n_rays, int N_steps) {
@@ -178,6 +180,11 @@ static RootPlan root_plan(int64_t n_rays, int N_steps) {
   p.o_sec = o; o += a256(R * kSecFloats * 4);
   p.o_ptss = o; o += a256(R * 12);
   p.o_ss = o; o += a256(R * 4);
+  p.o_act0 = o; o += a256(R * 4);
+  p.o_act1 = o; o += a256(R * 4);
+  p.o_acnt = o; o += a256(2 * 4);
+  p.o_ptsc = o; o += a256(R * (size_t)kMarchK * 12);
+  p.o_sc = o; o += a256(R * (size_t)kMarchK * 4);
   p.total = o;
   return p;
 }
@@ -258,9 +265,9 @@ size_t nr_root_find_workspace_bytes(int64_t n_rays, int N_steps) {
 
 int nr_root_find(const NrSdfDesc* d, const void* packed, const float* rays_o, const float* rays_d, int64_t n_rays,
                  float near, float far, const float* near_rays, const float* far_rays, int N_steps,
-                 const float* t_march, int N_secant_steps, int no_secant, float logit_tau, int fill_inf, float* d_pred,
-                 float* pts, uint8_t* mask, uint8_t* mask_sign_change, void* workspace, size_t workspace_bytes,
-                 void* stream) {
+                 const float* t_march, int N_secant_steps, int no_secant, float logit_tau, int fill_inf,
+                 int full_march, float* d_pred, float* pts, uint8_t* mask, uint8_t* mask_sign_change, void* workspace,
+                 size_t workspace_bytes, void* stream) {
   int rc = check_sdf_desc(d);
   if (rc) return rc;
   NR_REQUIRE(n_rays >= 0 && N_steps >= 2 && N_secant_steps >= 0, NR_ERR_ARG,
@@ -290,8 +297,10 @@ int nr_root_find(const NrSdfDesc* d, const void* packed, const float* rays_o, co
                          near_rays ? near_rays + r0 : nullptr, far_rays ? far_rays + r0 : nullptr);
     }
     NR_HIP_CHECK(hipGetLastError());
-    if ((rc = launch_sdf(SL, packed, c.pts_m, (int64_t)N_steps * R, c.sm, nullptr, nullptr, d->multires, nullptr, 0,
-                         st)))
+    // the march in chunks of kMarchK steps over the rays still without a sign change (uni_root reads a
+    // ray's march only up to its first crossing); full_march: every step of every ray in one launch
+    if ((rc = run_march(SL, packed, d->multires, c, full_march != 0, (int*)(ws + pl.o_act0), (int*)(ws + pl.o_act1),
+                        (int*)(ws + pl.o_acnt), F(pl.o_ptsc), F(pl.o_sc), st)))
       return rc;
     hipLaunchKernelGGL(uni_root, grd, blk, 0, st, c);
     NR_HIP_CHECK(hipGetLastError());

@@ -74,6 +74,13 @@ __global__ void uni_march_scan(UniChunk c, int s0, int s1, const int* act_in, co
                                int* n_out);
 __global__ void uni_march_gather(UniChunk c, int s0, int K, const int* act, const int* n, float* pts);
 __global__ void uni_march_scatter(UniChunk c, int s0, int K, const int* act, const int* n, const float* v);
+// The root-finding march of one chunk (ray_casting.py:88-101) into c.sm: steps [0, kMarchK) of every ray,
+// then chunks of kMarchK steps over the rays still without a sign change (full: every step of every
+// ray in one launch).  act0 / act1: [R] ints, cnt: 2 ints, ptsc: [kMarchK R, 3], sc: [kMarchK R] floats
+// of workspace.  Used by UNISURF's render and by nr_root_find.
+struct SdfLayout;
+int run_march(const SdfLayout& SL, const void* packed, int multires, const UniChunk& c, bool full, int* act0,
+              int* act1, int* cnt, float* ptsc, float* sc, hipStream_t st);
 __global__ void rf_prologue(UniChunk c, const float* rays_o, const float* rays_d, float near, float far,
                             const float* near_rays, const float* far_rays);
 __global__ void rf_finish(UniChunk c, int64_t ray0, float* d_out, float* pts, uint8_t* mask, uint8_t* msc,

@@ -491,4 +491,37 @@ UniPlan unisurf_plan(const NrUnisurfArgs& a, int64_t Rc) {
   return p;
 }
 
+int run_march(const SdfLayout& SL, const void* packed, int multires, const UniChunk& c, bool full, int* act0,
+              int* act1, int* cnt, float* ptsc, float* sc, hipStream_t st) {
+  const int R = c.R;
+  const dim3 blk(64), grd((R + 63) / 64);
+  const int N = c.N_steps, K0 = (full || N < kMarchK) ? N : kMarchK;
+  int rc;
+  if ((rc = launch_sdf(SL, packed, c.pts_m, (int64_t)K0 * R, c.sm, nullptr, nullptr, multires, nullptr, 0, st)))
+    return rc;
+  if (K0 == N) return NR_OK;
+  int* act[2] = {act0, act1};
+  NR_HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int), st));
+  hipLaunchKernelGGL(uni_march_scan, grd, blk, 0, st, c, 0, K0, nullptr, nullptr, act[0], cnt);
+  NR_HIP_CHECK(hipGetLastError());
+  int cur = 0;
+  for (int s0 = K0; s0 < N; s0 += kMarchK) {
+    const int Kc = N - s0 < kMarchK ? N - s0 : kMarchK;
+    const dim3 gq((unsigned)(((int64_t)Kc * R + 255) / 256));
+    hipLaunchKernelGGL(uni_march_gather, gq, dim3(256), 0, st, c, s0, Kc, act[cur], cnt + cur, ptsc);
+    NR_HIP_CHECK(hipGetLastError());
+    if ((rc = launch_sdf(SL, packed, ptsc, (int64_t)Kc * R, sc, nullptr, nullptr, multires, nullptr, 0, st, cnt + cur,
+                         Kc)))
+      return rc;
+    hipLaunchKernelGGL(uni_march_scatter, gq, dim3(256), 0, st, c, s0, Kc, act[cur], cnt + cur, sc);
+    NR_HIP_CHECK(hipGetLastError());
+    NR_HIP_CHECK(hipMemsetAsync(cnt + (cur ^ 1), 0, sizeof(int), st));
+    hipLaunchKernelGGL(uni_march_scan, grd, blk, 0, st, c, s0, s0 + Kc, act[cur], cnt + cur, act[cur ^ 1],
+                       cnt + (cur ^ 1));
+    NR_HIP_CHECK(hipGetLastError());
+    cur ^= 1;
+  }
+  return NR_OK;
+}
+
 }  // namespace nr

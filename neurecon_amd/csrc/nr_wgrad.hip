@@ -27,6 +27,13 @@
 //    applied once at the end.
 //  * optional: column sums of A_0 (the bias gradient) and B_0^T v for a [P] vector v (the sdf row of
 //    the output layer, dW8[0, :]) accumulated in fp32 from the loaded values, reduced in fixed order.
+//  * NrWgrad.fp32 (the fp32-precision nets' training step): the same loaders, slices and reduction with
+//    exact fp32 products on v_mfma_f32_16x16x4_f32.  The k-step's rows are stored into LDS as fp32 (the
+//    A / B row images take the bytes of the hi + lo planes: 272 / 144 floats per row, 16 banks apart
+//    per row, so a fragment's 2 x 16 consecutive floats per 32 lanes read conflict-free) and each
+//    16 x 16 tile accumulates 8 k-substeps of 4 rows in order: A[i][k] = a[p0 + k][m0 + i] is lane
+//    (k, i)'s ds_read_b32, B[k][j] likewise.  Each slice sums its rows in order, the slices are summed
+//    in fixed order: a deterministic fp32 reduction in place of hipBLASLt's split-K products.
 #include <algorithm>
 #include <cstdlib>
 #include "nr_common.h"
@@ -181,7 +188,7 @@ struct WgRegs {
   int q;
 };
 
-template <bool VA, bool VB>
+template <bool VA, bool VB, bool F32 = false>
 __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * kStage];
   // per stage: the rescale ratios 2^(e_new - e_old) of the 64 A column quads, then the 32 B quads, and
@@ -278,6 +285,15 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
     _Float16* S0 = lds + stg * kStage;
     if (want_cs && R.q == 0) cs = add4(cs, add4(add4(R.va[0], R.va[1]), add4(R.va[2], R.va[3])));
     if (want_vec && R.q == 0) vs = fma4(R.vv[1], R.vb[1], fma4(R.vv[0], R.vb[0], vs));
+    if constexpr (F32) {  // fp32 row images: A [32][kAStride floats], B [32][kBStride floats] (no split)
+      float* A32 = (float*)S0;
+      float* B32 = (float*)(S0 + 2 * kAPlane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *(float4*)(A32 + (ar + 8 * j) * kAStride + ac) = R.va[j];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) *(float4*)(B32 + (br + 16 * j) * kBStride + bc) = R.vb[j];
+      return;
+    }
     // per column quad: the max over its 32 rows (this lane's 4 rows x 8 lanes) -> power-of-two scale
     const float ma = quad_max<false>(fmaxf(fmaxf(amax4(R.va[0]), amax4(R.va[1])), fmaxf(amax4(R.va[2]), amax4(R.va[3]))));
     const int ta = split_exp(ma);
@@ -330,6 +346,24 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
 #ifdef NR_WG_EXP_NO_MFMA
     return;
 #endif
+    if constexpr (F32) {
+      const float* A32 = (const float*)(lds + stg * kStage);
+      const float* B32 = (const float*)(lds + stg * kStage + 2 * kAPlane);
+#pragma unroll
+      for (int s = 0; s < kWgK / 4; ++s) {
+        const int r = 4 * s + G;
+        float av[2], bv[8];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) av[i] = A32[r * kAStride + 32 * w + 16 * i + col];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bv[j] = B32[r * kBStride + 16 * j + col];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+      }
+      return;
+    }
     uint64_t chb;
     __builtin_memcpy(&chb, s_chg[stg], 8);
     if (cha[stg] || chb != 0) rescale(stg);  // wave-uniform
@@ -388,12 +422,14 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
     if (!step(1, R2, R0)) break;
   }
   // the final exponents -> 2^-e per quad, applied once (two factors: 2^-(eA + eB) can underflow)
-  if (lane < 8) s_rat[2][ac >> 2] = __builtin_ldexpf(1.0f, -ea_cur);
-  if (lane < 4) s_rat[2][64 + (bc >> 2)] = __builtin_ldexpf(1.0f, -eb_cur);
-  __syncthreads();
+  if constexpr (!F32) {
+    if (lane < 8) s_rat[2][ac >> 2] = __builtin_ldexpf(1.0f, -ea_cur);
+    if (lane < 4) s_rat[2][64 + (bc >> 2)] = __builtin_ldexpf(1.0f, -eb_cur);
+    __syncthreads();
 #ifndef NR_WG_EXP_NO_MFMA
-  if (wvalid) rescale(2);
+    if (wvalid) rescale(2);
 #endif
+  }
 
   // partial tile: lane (G, col) register r holds row 4G + r of each 16 x 16 tile -> part[s][n][m]
   const int64_t ldp = (int64_t)a.nmt * kWgM;
@@ -554,10 +590,12 @@ int nr_wgrad(const NrWgrad* w, void* stream) {
     NR_REQUIRE(ok, NR_ERR_ARG, "nr_wgrad: a blocked operand needs P and its leading dimension multiples of 16");
   }
   WgPlan p = wgrad_plan(w->P, w->m, w->n, w->npairs);
-  if (const char* e = getenv("NR_WGRAD_SLICES")) {  // measurement knob (tools/wgrad_bench.py): fewer slices
+#ifdef NR_WG_EXP_SLICES_ENV  // measurement builds only (tools/wgrad_bench.py): fewer slices
+  if (const char* e = getenv("NR_WGRAD_SLICES")) {
     const int s = atoi(e);
     if (s > 0 && s < p.S) p.S = s;
   }
+#endif
   NR_REQUIRE(w->workspace && w->workspace_bytes >= p.part_bytes + p.cs_bytes + p.vec_bytes, NR_ERR_WORKSPACE,
              "nr_wgrad: workspace too small (nr_wgrad_workspace_bytes)");
   hipStream_t st = (hipStream_t)stream;
@@ -583,10 +621,17 @@ int nr_wgrad(const NrWgrad* w, void* stream) {
     ProfScope prof("wgrad", (double)w->npairs * w->P * (w->m + w->n) * 4.0, st);
     const dim3 grid((unsigned)(p.S * p.nmt * p.nnt));
     // S % 8 == 0 needs the grid padded to whole XCD rounds of the mapping (it already is: S * NT)
-    if (va && vb) hipLaunchKernelGGL((wgrad_kernel<true, true>), grid, dim3(kWgThreads), 0, st, k);
-    else if (va) hipLaunchKernelGGL((wgrad_kernel<true, false>), grid, dim3(kWgThreads), 0, st, k);
-    else if (vb) hipLaunchKernelGGL((wgrad_kernel<false, true>), grid, dim3(kWgThreads), 0, st, k);
-    else hipLaunchKernelGGL((wgrad_kernel<false, false>), grid, dim3(kWgThreads), 0, st, k);
+    if (w->fp32) {
+      if (va && vb) hipLaunchKernelGGL((wgrad_kernel<true, true, true>), grid, dim3(kWgThreads), 0, st, k);
+      else if (va) hipLaunchKernelGGL((wgrad_kernel<true, false, true>), grid, dim3(kWgThreads), 0, st, k);
+      else if (vb) hipLaunchKernelGGL((wgrad_kernel<false, true, true>), grid, dim3(kWgThreads), 0, st, k);
+      else hipLaunchKernelGGL((wgrad_kernel<false, false, true>), grid, dim3(kWgThreads), 0, st, k);
+    } else {
+      if (va && vb) hipLaunchKernelGGL((wgrad_kernel<true, true>), grid, dim3(kWgThreads), 0, st, k);
+      else if (va) hipLaunchKernelGGL((wgrad_kernel<true, false>), grid, dim3(kWgThreads), 0, st, k);
+      else if (vb) hipLaunchKernelGGL((wgrad_kernel<false, true>), grid, dim3(kWgThreads), 0, st, k);
+      else hipLaunchKernelGGL((wgrad_kernel<false, false>), grid, dim3(kWgThreads), 0, st, k);
+    }
     NR_HIP_CHECK(hipGetLastError());
   }
   const int64_t ldp = (int64_t)p.nmt * kWgM, ldn = (int64_t)p.nnt * kWgN;

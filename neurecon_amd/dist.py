@@ -15,6 +15,8 @@ UNISURF's F.normalize(nablas) couples the points of one `rayschunk` (unisurf.py:
 train_util.py:23-71): its shards exchange the per-window sums of nabla^2 (3 doubles per window, one
 all-reduce per render call) so the result equals a single-process render at any shard split.
 """
+import math
+
 import torch
 import torch.distributed as dist
 
@@ -42,7 +44,18 @@ def shard_rays(rays_o, rays_d, rank=None, world_size=None, align=1, dim=-2):
     return rays_o.narrow(dim, lo, hi - lo), rays_d.narrow(dim, lo, hi - lo), (lo, hi)
 
 
-BLOCK = 1024  # rays per dealt block of the cyclic layout
+BLOCK = 1024  # rays per dealt block of the cyclic layout (the largest; see cyclic_block)
+MIN_BLOCKS_PER_RANK = 4
+
+
+def cyclic_block(n, world_size, align=1, block=BLOCK):
+    """Block size of the cyclic layout for n rays: BLOCK, shrunk so that every rank gets at least
+    MIN_BLOCKS_PER_RANK blocks (4096 rays on 8 ranks: 128-ray blocks, not 4 busy ranks of 1024), a
+    multiple of 16 rays (whole 16-sample tiles in the NeuS chunks) and of `align`."""
+    q = 16 * align // math.gcd(16, align)
+    want = -(-n // (world_size * MIN_BLOCKS_PER_RANK))
+    b = min(block, max(want, 1))
+    return max(q, b // q * q)
 
 
 def cyclic_index(n, rank, world_size, block=BLOCK):
@@ -109,24 +122,30 @@ def gather_rays(t, n_total, dim=0, align=1):
 
 
 def render_sharded(render_fn, rays_o, rays_d, model, gather=True, align=1, group=None, layout='cyclic',
-                   block=BLOCK, **kw):
+                   block=None, **kw):
     """Render this rank's share of the rays with `render_fn(rays_o, rays_d, model, **kw)` (any of the
     frameworks' volume_render); with gather=True the per-ray maps (rgb, depth, every extras entry
     with a ray dimension) are all-gathered so every rank holds the full result, each ray at its
-    index.  layout 'cyclic' (default): blocks of `block` rays dealt round-robin; 'contiguous': one
-    range per rank (in units of `align` rays).  A render whose batched normalisation couples rays
-    across shards (UNISURF, `render_fn.window_sharded`) needs contiguous slices: it is told its slice
-    and reduces those sums over the ranks itself (one small all-reduce per call)."""
+    index.  layout 'cyclic' (default): blocks of `block` rays dealt round-robin (default
+    cyclic_block(n, world, align)); 'contiguous': one range per rank (in units of `align` rays).  A
+    render whose batched normalisation couples rays across shards (UNISURF, `render_fn.window_sharded`)
+    needs contiguous slices: it is told its slice and reduces those sums over the ranks itself (one
+    small all-reduce per call).  With gather=False the rank's own maps are returned and
+    extras['ray_index'] holds the indices (along the ray dimension) of the rays it rendered."""
     batched = kw.get('batched', False)
     dim = 1 if batched else 0
     n = rays_o.shape[dim]
     rank, ws = world()
     windowed = getattr(render_fn, 'window_sharded', False) and batched and ws > 1
     if layout == 'cyclic' and not windowed and ws > 1:
+        if block is None:
+            block = cyclic_block(n, ws, align)
+        assert block % align == 0, f'render_sharded: block {block} is not a multiple of align {align}'
         idx = cyclic_index(n, rank, ws, block).to(rays_o.device)
         ro, rd = rays_o.index_select(dim, idx), rays_d.index_select(dim, idx)
         rgb, depth, extras = render_fn(ro, rd, model, **kw)
         if not gather:
+            extras['ray_index'] = idx
             return rgb, depth, extras
         g = lambda v: gather_cyclic(v, n, dim=dim, block=block)
     else:
@@ -135,6 +154,7 @@ def render_sharded(render_fn, rays_o, rays_d, model, gather=True, align=1, group
             kw = dict(kw, shard=(lo, n, group))
         rgb, depth, extras = render_fn(ro, rd, model, **kw)
         if not gather:
+            extras['ray_index'] = torch.arange(lo, hi, device=rays_o.device)
             return rgb, depth, extras
         g = lambda v: gather_rays(v, n, dim=dim, align=align)
     rgb_all, depth_all = g(rgb), g(depth)

@@ -65,11 +65,14 @@ def sphere_tracing_surface_points(implicit_surface, rays_o, rays_d, near=0.0, fa
 
 
 def root_finding_surface_points(surface_query_fn, rays_o, rays_d, near=0.0, far=6.0, batched=True, batched_info={},
-                                N_steps=256, logit_tau=0.0, method='secant', N_secant_steps=8, fill_inf=True):
+                                N_steps=256, logit_tau=0.0, method='secant', N_secant_steps=8, fill_inf=True,
+                                _full_march=False):
     """ray_casting.py:35-160 -> (d_pred_out, pt_pred, mask, mask_sign_change); rays_d already
     normalised.  `surface_query_fn` must be a neurecon_amd ImplicitSurface (its forward SDF runs in
     the library); near / far floats or per-ray [(B), N_rays] tensors; a method other than 'secant'
-    skips the refinement and reports depth 1 on hits (ray_casting.py:128-135)."""
+    skips the refinement and reports depth 1 on hits (ray_casting.py:128-135).  The march runs in
+    chunks of 32 steps over the rays without a sign change so far; _full_march=True evaluates every
+    step of every ray (the reference's schedule, the same outputs bit for bit)."""
     from .frameworks.neus import _linspace_table
     if not hasattr(surface_query_fn, 'nr_packed'):
         raise NotImplementedError('neurecon_amd: root finding needs a neurecon_amd ImplicitSurface as surface_query_fn')
@@ -93,7 +96,8 @@ def root_finding_surface_points(surface_query_fn, rays_o, rays_d, near=0.0, far=
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     L.check(lib.nr_root_find(ctypes.byref(desc), L.ptr(packed), L.ptr(ro), L.ptr(rd), n, ctypes.c_float(near),
                              ctypes.c_float(far), L.ptr(near_r), L.ptr(far_r), int(N_steps), L.ptr(t),
-                             int(N_secant_steps), int(method != 'secant'), ctypes.c_float(logit_tau), int(bool(fill_inf)), L.ptr(d), L.ptr(pts), L.ptr(mask), L.ptr(msc), L.ptr(ws), ws_bytes,
+                             int(N_secant_steps), int(method != 'secant'), ctypes.c_float(logit_tau), int(bool(fill_inf)),
+                             int(bool(_full_march)), L.ptr(d), L.ptr(pts), L.ptr(mask), L.ptr(msc), L.ptr(ws), ws_bytes,
                              L.stream_of(dev)))
     return (d.reshape(shape), pts.reshape(*shape, 3), mask.view(torch.bool).reshape(shape),
             msc.view(torch.bool).reshape(shape))

@@ -2,9 +2,10 @@
 backward run on libnrhip.so.  f16x3 nets (the default precision; softplus SDF nets and ReLU D=4
 radiance nets) run every layer product on the hand-written training GEMM (nr_train_gemm: f16x3 MFMA
 over the render pack's weight stream, the elementwise step of the recipe fused into its epilogue);
-the weight gradients are hipBLASLt products of those saved activations.  fp32-precision and SIREN
-nets keep the reference-exact path: torch.addmm / mm on hipBLASLt (fp32) and the elementwise
-kernels of nr_train.hip between them.
+the weight gradients run on nr_wgrad (hand-written MFMA, f16x3 products).  fp32-precision and SIREN
+nets keep the reference-exact path: torch.addmm / mm on hipBLASLt (fp32) for the layer products, the
+elementwise kernels of nr_train.hip between them, and nr_wgrad with exact fp32 products (fixed-order
+reduction) for the weight gradients.
 
 What the reference differentiates (models/frameworks/neus.py:284-485, models/base.py:265-282):
   * ImplicitSurface.forward_with_nablas with create_graph=True: sdf, nablas = d sdf / d x and the
@@ -60,40 +61,29 @@ def _sine30(z):
     return h, s
 
 
-def _slabs(t, C):
-    """[P, m] (rows possibly strided, e.g. the valid columns of a padded activation) as C row slabs
-    [C, P/C, m] without a copy: hipBLASLt takes the row stride as the leading dimension"""
-    if t.stride(1) != 1:
-        t = t.contiguous()
-    P, m = t.shape
-    return t.as_strided((C, P // C, m), (P // C * t.stride(0), t.stride(0), 1))
+def _wgrad(g, h, fp32=True):
+    """gᵀ h for the weight gradients of a tall batch (g [P, m], h [P, k], P ~ 65 k) on nr_wgrad: exact
+    fp32 products (v_mfma_f32_16x16x4_f32) summed per row slice in order and over the slices in fixed
+    order -- the fp32 nets' path (r05; r04 ran hipBLASLt's split-K batched GEMM + a sum, whose error
+    was 1.4x the fp32 oracle's own on the training step's layer-0 / layer-4 weights); fp32=False: the
+    f16x3 products of the default nets"""
+    return _wg([(g, h)], fp32=fp32)
 
 
-def _wgrad(g, h):
-    """gᵀ h for the weight gradients of a tall batch (g [P, m], h [P, k], P ~ 65 k): split over K into
-    a batched GEMM of 16 slabs plus a sum, so the [m, k] output is computed by 16x the tiles (hipBLASLt
-    otherwise runs a handful of 32x64 tiles over the whole of K: ~37 TF/s)"""
-    P = g.shape[0]
-    C = 16
-    if P < 8192 or P % C:
-        return g.t() @ h
-    return torch.bmm(_slabs(g, C).transpose(1, 2), _slabs(h, C)).sum(0)
+def _wgrad2(g1, h1, g2, h2, fp32=True):
+    """g1^T h1 + g2^T h2 in one nr_wgrad launch (both sweeps of a layer)"""
+    return _wg([(g1, h1), (g2, h2)], fp32=fp32)
 
 
-def _wgrad2(g1, h1, g2, h2):
-    """g1^T h1 + g2^T h2 as one slab reduction: both split-K products land in one [2C, m, k] buffer"""
-    P = g1.shape[0]
-    C = 16
-    if P < 8192 or P % C:
-        return g1.t() @ h1 + g2.t() @ h2
-    buf = torch.empty(2 * C, g1.shape[1], h1.shape[1], device=g1.device, dtype=g1.dtype)
-    for i, (g, h) in enumerate(((g1, h1), (g2, h2))):
-        torch.bmm(_slabs(g, C).transpose(1, 2), _slabs(h, C), out=buf[i * C:(i + 1) * C])
-    return buf.sum(0)
+def _wgb(g, h, fp32=True):
+    """(gᵀ h, column sums of g): a layer's weight and bias gradients in one nr_wgrad launch"""
+    db = torch.empty(g.shape[1], device=g.device)
+    return _wg([(g, h)], colsum=db, fp32=fp32), db
 
 
-def _wg(pairs, out=None, scale=1.0, colsum=None, avec=None, vec=None, blocked=0):
-    """sum_q a_q^T b_q on the hand-written MFMA weight-gradient kernel (nr_wgrad, f16x3): pairs of
+def _wg(pairs, out=None, scale=1.0, colsum=None, avec=None, vec=None, blocked=0, fp32=False):
+    """sum_q a_q^T b_q on the hand-written MFMA weight-gradient kernel (nr_wgrad; f16x3 products, or
+    exact fp32 products on v_mfma_f32_16x16x4_f32 with fp32=True -- the fp32 nets' path): pairs of
     row-major views a [P, m], b [P, n] (unit column stride; any row stride); out [m, n] (a view with
     unit column stride, e.g. a column range of the gradient) = scale * the sum.  colsum: [m] <- the
     column sums of a_0 (the bias gradient); avec [P] / vec [n]: vec <- avec^T b_0 (an extra row).
@@ -117,6 +107,7 @@ def _wg(pairs, out=None, scale=1.0, colsum=None, avec=None, vec=None, blocked=0)
     if avec is not None:
         w.avec, w.ldv, w.vec, w.vec_scale = avec.data_ptr(), avec.stride(0), vec.data_ptr(), 1.0
     w.blocked = blocked
+    w.fp32 = int(bool(fp32))
     lib = L.lib()
     nb = lib.nr_wgrad_workspace_bytes(P, m, n, len(pairs))
     ws = L.workspace(dev, nb)
@@ -303,8 +294,7 @@ class RadianceFn(torch.autograd.Function):
         L.check(L.lib().nr_activation(L.ptr(y), L.ptr(g), g.numel(), 3, _st(g)))
         dW, db = [None] * (D + 1), [None] * (D + 1)
         for l in range(D, -1, -1):
-            dW[l] = _wgrad(g, hs[l])
-            db[l] = _colsum(g)
+            dW[l], db[l] = _wgb(g, hs[l])
             g = g @ Ws[l]
             if l > 0:
                 if siren:
@@ -367,7 +357,7 @@ class NeRFFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xe, ve, cfg, *params):
-        D, skips = cfg
+        D, skips, ctx.fp32 = cfg
         Ws, bs = params[:D], params[D:2 * D]
         Wa, ba, Wf, bf, Wv, bv, Wr, br = params[2 * D:]
         st = _st(xe)
@@ -405,21 +395,22 @@ class NeRFFn(torch.autograd.Function):
         P = rgb.shape[0]
         g = torch.zeros_like(rgb) if g_rgb is None else g_rgb.contiguous().clone()
         L.check(lib.nr_activation(L.ptr(rgb), L.ptr(g), g.numel(), 3, st))          # sigmoid'
-        dWr, dbr = _wgrad(g, hv), _colsum(g)
+        f32 = ctx.fp32  # weight gradients on nr_wgrad: exact fp32 products (fp32 nets) or f16x3
+        dWr, dbr = _wgb(g, hv, f32)
         ghv = g @ Wr
         L.check(lib.nr_activation(L.ptr(hv), L.ptr(ghv), ghv.numel(), 1, st))      # ReLU'
-        dWv, dbv = _wgrad(ghv, hv_in), _colsum(ghv)
+        dWv, dbv = _wgb(ghv, hv_in, f32)
         g_feat = (ghv @ Wv)[:, :Wf.shape[0]].contiguous()                           # views: no gradient
-        dWf, dbf = _wgrad(g_feat, h), _colsum(g_feat)
+        dWf, dbf = _wgb(g_feat, h, f32)
         gh = g_feat @ Wf
         gs = (torch.zeros(P, 1, device=rgb.device) if g_sigma is None else g_sigma.reshape(P, 1).contiguous())
-        dWa, dba = _wgrad(gs, h), _colsum(gs)
+        dWa, dba = _wgb(gs, h, f32)
         gh = torch.addmm(gh, gs, Wa)
         dW, db = [None] * D, [None] * D
         for i in range(D - 1, -1, -1):
             gz = gh.contiguous()
             L.check(lib.nr_activation(L.ptr(outs[i]), L.ptr(gz), gz.numel(), 1, st))  # ReLU'
-            dW[i], db[i] = _wgrad(gz, ins[i]), _colsum(gz)
+            dW[i], db[i] = _wgb(gz, ins[i], f32)
             if i > 0:
                 gin = gz @ Ws[i]
                 gh = gin[:, nx:] if (i - 1) in skips else gin                          # drop the re-injected input
@@ -663,11 +654,16 @@ def _pad16(n):
     return 16 * ((n + 15) // 16)
 
 
-def _blk_bits(P, row0=0):
-    """NrTrainGemm.blocked bits from role names, or always 0 when P (or a row offset row0 the caller
-    addresses) is not a multiple of 16 (the blocked layout tiles whole 16-point blocks) or
-    NR_TRAIN_BLOCKED=0 (row-major everywhere: the bit-identity test's reference)"""
-    on = P % 16 == 0 and row0 % 16 == 0 and os.environ.get('NR_TRAIN_BLOCKED', '1') != '0'
+def _blk_on(P, row0=0):
+    """whether a training step stores its layer tensors 16 x 16 blocked: not when P (or a row offset
+    row0 the caller addresses) is not a multiple of 16 (the blocked layout tiles whole 16-point
+    blocks) or NR_TRAIN_BLOCKED=0 (row-major everywhere: the bit-identity test's reference).  Decided
+    once per forward and kept on the autograd context: backward reads what forward wrote."""
+    return P % 16 == 0 and row0 % 16 == 0 and os.environ.get('NR_TRAIN_BLOCKED', '1') != '0'
+
+
+def _blk_bits(on):
+    """NrTrainGemm.blocked bits from role names (all 0 when the layout is row-major)"""
     return lambda roles: sum(getattr(L, 'BLK_' + r) for r in roles) if on else 0
 
 
@@ -703,7 +699,7 @@ class SdfNablaTG(torch.autograd.Function):
         st = L.stream_of(dev)
         x = x.contiguous()
         P = x.shape[0]
-        assert 0 <= feat_from < P or not want_feat
+        assert 0 <= feat_from <= P or not want_feat
         desc, packed = surface.nr_packed(dev)
         info = _op_info('sdf', desc, 18)
         base = packed.data_ptr()
@@ -719,7 +715,8 @@ class SdfNablaTG(torch.autograd.Function):
         sdf = torch.empty(P, device=dev)
         delta = [None] * D
         delta[7] = torch.empty(P, 256, device=dev)
-        bk = _blk_bits(P, feat_from)
+        ctx.blk_on = _blk_on(P, feat_from)
+        bk = _blk_bits(ctx.blk_on)
         for l in range(D):                                                 # F0..F7
             if l == 0:
                 xin = dict(x1=h0, ld1=64, n1=nf)
@@ -782,7 +779,7 @@ class SdfNablaTG(torch.autograd.Function):
         wd = [256, 256, 256, 224, 256, 256, 256, 256]
         nv = [256, 256, 256, 217, 256, 256, 256, 256]
         tangent = g_nab is not None
-        bk = _blk_bits(P, ctx.feat_from)
+        bk = _blk_bits(ctx.blk_on)  # the layout forward wrote
         wb = _WG_BLK if bk(('Y',)) else (lambda a, b: 0)
         ZD = [None] * D
         HD = [None] * D                                                   # hdot_l = s_l zdot_l
@@ -913,7 +910,7 @@ class RadianceTG(torch.autograd.Function):
         db[4] = torch.empty(3, device=dev)
         dW[4] = _wg([(g, H[3])], colsum=db[4])      # weight gradients on nr_wgrad (bias gradient fused)
         # the pre-activation adjoints gz stay inside this function: 16 x 16 blocked (SdfNablaTG's note)
-        bk = _blk_bits(P)
+        bk = _blk_bits(_blk_on(P))  # gz is written and read inside this backward
         wb = _WG_BLK if bk(('Y',)) else (lambda a, b: 0)
         gz = torch.empty(P, 256, device=dev)
         _tg(tb + info[5][0], P, (2, 0, 16, 0), L.TG_RELUMASK, g, 3, 3, gz, 256, bias=False, a=H[3], lda=256, stream=st,
@@ -942,7 +939,8 @@ def nerf(net, x_emb, v_emb):
     bs = [l.bias for l in net.pts_linears]
     heads = [net.alpha_linear.weight, net.alpha_linear.bias, net.feature_linear.weight, net.feature_linear.bias,
              net.views_linears[0].weight, net.views_linears[0].bias, net.rgb_linear.weight, net.rgb_linear.bias]
-    return NeRFFn.apply(x_emb, v_emb, (len(Ws), tuple(net.skips)), *Ws, *bs, *heads)
+    return NeRFFn.apply(x_emb, v_emb, (len(Ws), tuple(net.skips), getattr(net, 'precision', 'fp32') == 'fp32'), *Ws,
+                        *bs, *heads)
 
 
 def effective_weights(surface):

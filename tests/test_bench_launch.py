@@ -26,11 +26,17 @@ def test_bench_spawns_n_ranks():
     out = _run([sys.executable, 'bench.py', '--gpus', '2', '--steps', '2', '--warmup', '1', '--stub-cpu'])
     assert out['n_gpus'] == 2 and sorted(out['ranks']) == [0, 1]
     assert out['steps'] == 2 and out['warmup'] == 1
+    # the weak-scaling legs of the default N-GPU line: config (e)'s sharded render with its window
+    # all-reduce in the step, and the DDP training step
+    for leg in ('weak_scaling_e', 'weak_scaling_train'):
+        assert out[leg]['n_gpus'] == 2 and out[leg]['scaling'] == 'weak' and out[leg]['value'] > 0, out[leg]
+        assert out[leg]['collective_in_step'], leg
 
 
 def test_bench_single_process_default():
     out = _run([sys.executable, 'bench.py', '--steps', '2', '--warmup', '1', '--stub-cpu'])
     assert out['n_gpus'] == 1 and out['ranks'] == [0]
+    assert out['weak_scaling_e']['n_gpus'] == 1 and not out['weak_scaling_e']['collective_in_step']
 
 
 def _free_port():

@@ -33,12 +33,21 @@ def _worker(rank, ws, port, q, align, layout='contiguous', block=nd.BLOCK):
         fr = lambda o, d, m, **kw: (seen.append(o.shape[1]), _fake_render(o, d, m, **kw))[1]
         rgb, depth, ex = nd.render_sharded(fr, ro, rd, None, batched=True, align=align, layout=layout, block=block)
         if layout == 'cyclic':
-            ok_n = seen == [nd.cyclic_count(37, rank, ws, block)]
+            b = block if block is not None else nd.cyclic_block(37, ws, align)
+            ok_n = seen == [nd.cyclic_count(37, rank, ws, b)]
         else:
             ok_n = True
         ref = _fake_render(ro, rd, None)
         ok = (ok_n and torch.equal(rgb, ref[0]) and torch.equal(depth, ref[1]) and
               torch.equal(ex['implicit_surface'], ref[2]['implicit_surface']) and ex['scalar'] == 3)
+        # gather=False: the rank's own maps and the indices of its rays
+        rgb_s, _, ex_s = nd.render_sharded(_fake_render, ro, rd, None, batched=True, align=align, layout=layout,
+                                           block=block, gather=False)
+        idx = ex_s['ray_index']
+        ok = ok and torch.equal(rgb_s, ref[0][:, idx])
+        if layout == 'cyclic':
+            b = block if block is not None else nd.cyclic_block(37, ws, align)
+            ok = ok and torch.equal(idx, nd.cyclic_index(37, rank, ws, b))
         lo, hi = nd.shard_bounds(37, rank, ws, align)
         q.put((rank, ok, lo, hi))
     finally:
@@ -70,7 +79,7 @@ def test_sharded_render_reassembles_world2(align):
     assert hi0 % align == 0
 
 
-@pytest.mark.parametrize('ws,block', [(2, 5), (3, 4), (2, 1024)])
+@pytest.mark.parametrize('ws,block', [(2, 5), (3, 4), (2, 1024), (3, None)])
 def test_cyclic_sharded_render_reassembles(ws, block):
     """block-cyclic shares (the default layout): every rank renders its dealt blocks, the all-gather
     puts every ray back at its index -- bit-identical to the single-process result"""
@@ -95,6 +104,20 @@ def test_cyclic_index_partitions():
                 allidx = torch.cat(parts).sort().values if n else torch.empty(0, dtype=torch.int64)
                 assert torch.equal(allidx, torch.arange(n))
                 assert all(bool((p[1:] > p[:-1]).all()) for p in parts if p.numel() > 1)
+
+
+def test_cyclic_block_keeps_every_rank_busy():
+    """the default block (cyclic_block) deals every rank >= MIN_BLOCKS_PER_RANK blocks on small frames,
+    stays at BLOCK on large ones, and is a multiple of 16 and of align"""
+    assert nd.cyclic_block(480000, 8) == nd.BLOCK
+    for n in (37, 4096, 4097, 65536, 480000):
+        for ws in (2, 3, 8):
+            for align in (1, 8, 48):
+                b = nd.cyclic_block(n, ws, align)
+                assert b % 16 == 0 and b % align == 0 and b <= max(nd.BLOCK, 48)
+                if n >= ws * nd.MIN_BLOCKS_PER_RANK * 48:
+                    assert all(nd.cyclic_count(n, r, ws, b) > 0 for r in range(ws)), (n, ws, b)
+    assert nd.cyclic_block(4096, 8) == 128   # 4096 rays on 8 ranks: 512 rays per rank
 
 
 def test_shard_bounds_cover_and_align():

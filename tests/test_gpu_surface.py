@@ -212,3 +212,34 @@ def test_sdf_grid_range_matches_full_grid():
     assert torch.equal(part, full[1000:6001])
     with pytest.raises(ValueError):
         sdf_grid_range(m.implicit_surface, 1.5, N, N ** 3 - 3, 4)
+
+
+@pytest.mark.parametrize('precision', ['f16x3', 'fp32'])
+def test_root_finding_chunked_march_bit_identical(precision):
+    """nr_root_find's march runs in chunks of 32 steps over the rays still without a sign change
+    (run_march, shared with UNISURF): d_pred / pts / mask / mask_sign_change and the surface_render
+    maps equal the single-launch march over every step of every ray (_full_march=True) bit for bit,
+    on a wide-angle camera where rays hit, miss and graze the surface; plus N_steps that are not a
+    multiple of 32 and fewer than 32 steps."""
+    from oracle.rays import get_rays
+    from neurecon_amd.ray_casting import root_finding_surface_points, surface_render
+    sd = wg.neus_state(seed=1)
+    H, W, f, dist = 48, 64, 40.0, 2.0
+    ro, rd, _ = get_rays(wg.look_at_c2w(dist)[None], wg.intrinsics(f, H, W)[None], H, W)
+    ro, rd = ro.cuda(), rd.cuda()
+    rdn = torch.nn.functional.normalize(rd, dim=-1)
+    m = neus_model(sd, precision=precision)
+    with torch.no_grad():
+        for kw in (dict(), dict(N_steps=100, N_secant_steps=4), dict(N_steps=20), dict(near=0.5, far=4.0)):
+            outs = [root_finding_surface_points(m.implicit_surface, ro, rdn, _full_march=full, **kw)
+                    for full in (True, False)]
+            for name, a, b in zip(('d_pred', 'pts', 'mask', 'mask_sign_change'), *outs):
+                assert torch.equal(a, b), (kw, name)
+            print(f'[{precision}] {kw}: {int(outs[0][2].sum())} / {outs[0][2].numel()} hits, bit-identical')
+        maps = [surface_render(ro, rd, m, calc_normal=True, batched=True, ray_casting_algo='root_finding',
+                               ray_casting_cfgs={'_full_march': full}) for full in (True, False)]
+    (c0, d0, e0), (c1, d1, e1) = maps
+    assert torch.equal(c0, c1) and torch.equal(d0, d1)
+    for k in e0:
+        if torch.is_tensor(e0[k]):
+            assert torch.equal(e0[k], e1[k]), k

@@ -118,21 +118,21 @@ def test_unisurf_full_config_e_vs_oracle(precision):
 
 
 @pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
-def test_unisurf_chunked_march_bit_identical(precision, monkeypatch):
+def test_unisurf_chunked_march_bit_identical(precision):
     """the root-finding march runs in chunks of 32 steps over the rays still without a sign change
     (nr_unisurf.h kMarchK): every output equals the single-launch march over all steps of all rays
-    (NR_UNISURF_FULL_MARCH=1) bit for bit -- uni_root only reads the march up to a ray's first crossing"""
+    (NrUnisurfArgs.full_march, volume_render(_full_march=True)) bit for bit -- uni_root only reads the march up to a ray's first crossing"""
     from oracle import rays as orays
     from neurecon_amd.frameworks.unisurf import volume_render
     H, W, f, dist = wg.CAMERAS['e']
     ro, rd, _ = orays.get_rays(wg.look_at_c2w(dist)[None], wg.intrinsics(f, H, W)[None], H, W)
     m = unisurf_model(wg.unisurf_state(seed=3), precision=precision)
     outs = []
-    for full in ('1', '0'):
-        monkeypatch.setenv('NR_UNISURF_FULL_MARCH', full)
+    for full in (True, False):
         with torch.no_grad():
             rgb, depth, ex = volume_render(ro.cuda(), rd.cuda(), m, batched=True, calc_normal=True,
-                                           detailed_output=True, logit_tau=0.0, N_query=64, N_freespace=32)
+                                           detailed_output=True, logit_tau=0.0, N_query=64, N_freespace=32,
+                                           _full_march=full)
         torch.cuda.synchronize()
         outs.append((rgb.clone(), depth.clone(), {k: v.clone() for k, v in ex.items() if torch.is_tensor(v)}))
     (r0, d0, e0), (r1, d1, e1) = outs

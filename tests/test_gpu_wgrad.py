@@ -43,15 +43,18 @@ CASES = {
 }
 
 
+@pytest.mark.parametrize('fp32', [False, True], ids=['f16x3', 'fp32'])
 @pytest.mark.parametrize('name', list(CASES))
-def test_wgrad_vs_float64(name):
+def test_wgrad_vs_float64(name, fp32):
+    """both product modes: f16x3 (the default nets) and exact fp32 products (NrWgrad.fp32, the fp32 nets'
+    training path in place of hipBLASLt's split-K GEMMs)"""
     from neurecon_amd.training import _wg
     P, m, lda, n, ldb, npairs = CASES[name]
     g = torch.Generator().manual_seed(sum(map(ord, name)))
     pairs = [(_mk(P, m, lda, g, heavy=True), _mk(P, n, ldb, g, scale=0.3)) for _ in range(npairs)]
     cs = torch.empty(m, device='cuda')
-    out = _wg(pairs, colsum=cs, scale=0.5)
-    out2 = _wg(pairs, colsum=torch.empty(m, device='cuda'), scale=0.5)
+    out = _wg(pairs, colsum=cs, scale=0.5, fp32=fp32)
+    out2 = _wg(pairs, colsum=torch.empty(m, device='cuda'), scale=0.5, fp32=fp32)
     torch.cuda.synchronize()
     assert torch.equal(out, out2), 'not deterministic'
     ref64 = sum(a.double().t() @ b.double() for a, b in pairs) * 0.5
@@ -59,7 +62,7 @@ def test_wgrad_vs_float64(name):
     scale = float(ref64.abs().max())
     e_hip = (out.double() - ref64).abs()
     e_32 = (ref32.double() - ref64).abs()
-    print(f'{name}: max |hip - f64| {float(e_hip.max()) / scale:.2e}, max |fp32 GEMM - f64| '
+    print(f'{name} [{"fp32" if fp32 else "f16x3"}]: max |hip - f64| {float(e_hip.max()) / scale:.2e}, max |fp32 GEMM - f64| '
           f'{float(e_32.max()) / scale:.2e} (of max |C| = {scale:.3e})')
     assert bool((e_hip <= e_32 + 2e-6 * scale).all()), float((e_hip - e_32).max()) / scale
     cref = pairs[0][0].double().sum(0)

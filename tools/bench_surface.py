@@ -1,5 +1,6 @@
 """Throughput of the §8f widening rows on one GPU (not the headline bench):
   * surface_render (sphere tracing, 20 iterations) of a full 800x600 frame (480,000 rays, config-(d) camera);
+  * surface_render (root finding: 256-step march + secant) of the same frame, chunked and full march;
   * extract_mesh's SDF grid query at N=512 (134 M forward SDF evaluations).
 Prints one JSON line per workload with per-kernel HIP-event timings from the library.
 
@@ -61,6 +62,19 @@ def main():
         print(json.dumps(dict(workload='surface_render sphere_tracing 800x600 (480000 rays, 20 iters)', rays=H * W,
                               hit_rays=hits, ms=round(dt * 1e3, 3), rays_per_s=round(H * W / dt, 1),
                               kernels={k: dict(launches=v[0], ms=round(v[1], 3)) for k, v in prof.items()})))
+        # root finding (ray_casting.py:35-160): the 256-step march evaluated in chunks of 32 steps over the
+        # rays without a sign change so far, against the single launch over every step (_full_march)
+        for full in (True, False):
+            (rgb, depth, ex), dt, prof = timed(
+                lambda: surface_render(ro, rd, m, calc_normal=True, batched=True, ray_casting_algo='root_finding',
+                                       ray_casting_cfgs={'_full_march': full}), args.reps)
+            hits = int(ex['mask_surface'].sum().item())
+            print(json.dumps(dict(workload='surface_render root_finding 800x600 (480000 rays, 256-step march + 8 '
+                                           'secant steps), ' + ('full march (every step of every ray)' if full else
+                                                                'chunked march (32-step chunks over rays without a '
+                                                                'crossing)'),
+                                  rays=H * W, hit_rays=hits, ms=round(dt * 1e3, 3), rays_per_s=round(H * W / dt, 1),
+                                  kernels={k: dict(launches=v[0], ms=round(v[1], 3)) for k, v in prof.items()})))
         N = args.grid_n
         out, dt, prof = timed(lambda: sdf_grid(m.implicit_surface, 2.0, N), args.reps)
         kms = sum(v[1] for k, v in prof.items() if k.startswith('sdf'))

@@ -84,11 +84,18 @@ VARIANTS = {
     # nr_wgrad phase split between the two waves of a SIMD (valid results): waves w & 4 / adjacent waves
     'wg_pp4': ['-DNR_WG_PP_BIT=4'],
     'wg_pp1': ['-DNR_WG_PP_BIT=1'],
+    # r05: the forward-only sdf4_kernel launches with the r04 3-slot weight ring (valid results)
+    'ring3': ['-DNR_FWD_RING=3'],
+    # r05: fp32 magic-number slab codes (one fma to write, one fma + mul to read; 8 instead of 6 KB / point)
+    'slab32': ['-DNR_SLAB32'],
+    'slab32prio': ['-DNR_SLAB32', '-DNR_SDF4_PRIO'],
+    # nr_wgrad slice count from $NR_WGRAD_SLICES (tools/wgrad_bench.py)
+    'wg_slices_env': ['-DNR_WG_EXP_SLICES_ENV'],
 }
 
 
 def one(name):
-    out_dir = os.path.join(ROOT, 'neurecon_amd', '_exp')
+    out_dir = os.environ.get('NR_EXP_DIR', os.path.join(ROOT, 'neurecon_amd', '_exp'))
     objs = []
     for src in B._sources():
         obj = os.path.join(out_dir, f'{name}_{os.path.basename(src)}.o')
@@ -101,7 +108,7 @@ def one(name):
 
 def main(names):
     import concurrent.futures as cf
-    os.makedirs(os.path.join(ROOT, 'neurecon_amd', '_exp'), exist_ok=True)
+    os.makedirs(os.environ.get('NR_EXP_DIR', os.path.join(ROOT, 'neurecon_amd', '_exp')), exist_ok=True)
     with cf.ThreadPoolExecutor(4) as ex:
         for lib in ex.map(one, names):
             print(lib)

@@ -1,6 +1,7 @@
 """nr_wgrad timing on the training step's main shape (P = 65536, 256 x 256, one and two pairs) vs the
 split-K hipBLASLt product it replaces; run under rocprofv3 --kernel-trace --stats to split the
-kernel from its reduction.  NR_WGRAD_SLICES=<S> overrides the slice count (fewer, larger slices)."""
+kernel from its reduction.  NR_WGRAD_SLICES=<S> overrides the slice count (fewer, larger slices) in the wg_slices_env variant build
+(tools/build_variants.py; NR_LIB=neurecon_amd/_exp/libnrhip_wg_slices_env.so)."""
 import os
 import sys
 import time
