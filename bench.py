@@ -109,14 +109,14 @@ def parse():
     return ap.parse_args()
 
 
-def make_model(device, precision):
+def make_model(device, precision, outside=False):
     from neurecon_amd.frameworks.neus import NeuS
     torch.manual_seed(0)
     surf = dict(use_siren=False, embed_multires=6, radius_init=0.5, geometric_init=True, D=8, W=256, skips=[4],
                 precision=precision)
     rad = dict(use_siren=False, embed_multires=-1, embed_multires_view=4, use_view_dirs=True, D=4, W=256, skips=[],
                precision=precision)
-    m = NeuS(variance_init=0.05, speed_factor=10.0, W_geo_feat=256, use_outside_nerf=False, obj_bounding_radius=1.0,
+    m = NeuS(variance_init=0.05, speed_factor=10.0, W_geo_feat=256, use_outside_nerf=outside, obj_bounding_radius=1.0,
              surface_cfg=surf, radiance_cfg=rad)
     return m.to(device).eval()
 
@@ -434,13 +434,14 @@ def frame_d_setup(dev, precision, workspace_gb=None):
     return step, H * W
 
 
-def train_setup(dev, precision, n_rays, world, adam='fused'):
+def train_setup(dev, precision, n_rays, world, adam='fused', nerfpp=False):
     """NeuS training step (configs/neus.yaml: N_rays=512 per rank, perturb=True, with_mask): random
     rays of a synthetic 64x64 image, render with the autograd graph (neurecon_amd.training), the
-    reference's losses, backward (DDP gradient all-reduce over RCCL when world > 1), Adam."""
+    reference's losses, backward (DDP gradient all-reduce over RCCL when world > 1), Adam.
+    nerfpp=True: configs/neus_nomask_blended.yaml's model (NeRF++ background, N_outside 32, no mask loss)."""
     import types
     from neurecon_amd.frameworks.neus import Trainer
-    model = make_model(dev, precision)
+    model = make_model(dev, precision, outside=nerfpp)
     model.train()
     trainer = Trainer(model, device_ids=[dev.index or 0])
     if world > 1:
@@ -454,9 +455,10 @@ def train_setup(dev, precision, n_rays, world, adam='fused'):
     mi = {'intrinsics': K, 'c2w': c2w, 'object_mask': (torch.rand(1, 4096, generator=g) > 0.5).to(dev)}
     gt = {'rgb': torch.rand(1, 4096, 3, generator=g).to(dev)}
     a = types.SimpleNamespace(data=types.SimpleNamespace(N_rays=n_rays),
-                              training=types.SimpleNamespace(w_eikonal=0.1, w_mask=1.0, with_mask=True))
-    kw = dict(H=64, W=64, upsample_algo='official_solution', N_nograd_samples=2048, N_upsample_iters=4, N_outside=0,
-              obj_bounding_radius=1.0, batched=True, perturb=True, white_bkgd=False)
+                              training=types.SimpleNamespace(w_eikonal=0.1, w_mask=0.0 if nerfpp else 1.0,
+                                                             with_mask=not nerfpp))
+    kw = dict(H=64, W=64, upsample_algo='official_solution', N_nograd_samples=2048, N_upsample_iters=4,
+              N_outside=32 if nerfpp else 0, obj_bounding_radius=1.0, batched=True, perturb=True, white_bkgd=False)
 
     def step():
         ret = trainer(a, None, mi, gt, kw, 0, device=dev)
@@ -666,14 +668,15 @@ def fp32_mode(args, dev, sync):
                                                'launches', 'per_launch_type')}}
 
 
-def config_train(dev, precision, n_rays, steps, warmup, sync, adam='fused'):
+def config_train(dev, precision, n_rays, steps, warmup, sync, adam='fused', nerfpp=False):
     """NeuS training step, 512 rays (train_setup): wall rays/s, the library's kernel census, and every
     device kernel of one step by name from torch.profiler (the hipBLASLt `Cijk_*` share included)"""
-    step = train_setup(dev, precision, n_rays, 1, adam)
+    step = train_setup(dev, precision, n_rays, 1, adam, nerfpp)
     dt, ks = _census(step, steps, warmup, sync)
     table, _ = _kernel_summary(ks, precision, 289)
-    out = {'workload': 'NeuS Trainer.forward + backward (double backward through the nablas) + Adam, 512 rays x 128 '
-                       'samples', 'value': round(n_rays / dt, 1), 'unit': 'rays/s', 'ms_per_step': round(dt * 1e3, 3),
+    wl = ('NeuS Trainer.forward + backward (double backward through the nablas) + Adam, 512 rays x 128 samples' +
+          (' + NeRF++ background (configs/neus_nomask_blended.yaml: N_outside 32, no mask loss)' if nerfpp else ''))
+    out = {'workload': wl, 'value': round(n_rays / dt, 1), 'unit': 'rays/s', 'ms_per_step': round(dt * 1e3, 3),
            'steps': steps, 'library_kernels': table,
            # the dominant kernel (the layer GEMM, HBM-bound) and nr_wgrad, from the census step's HIP events
            'roofline': train_roofline(ks, dt, 1, ks) if precision == 'f16x3' else None}
@@ -886,7 +889,9 @@ def run(args):
         cs, cw = args.config_steps, 1
         cfgs = {'c_volsdf_2048x256': config_c(dev, args.precision, cs, cw, sync),
                 'e_unisurf_4096': config_e(dev, args.precision, cs, cw, sync),
-                'train_neus_512': config_train(dev, args.precision, args.train_rays, 2 * cs, 2, sync, args.adam)}
+                'train_neus_512': config_train(dev, args.precision, args.train_rays, 2 * cs, 2, sync, args.adam),
+                'train_neus_nerfpp_512': config_train(dev, args.precision, args.train_rays, 2 * cs, 2, sync, args.adam,
+                                                      nerfpp=True)}
     total_rays = n_rays * args.steps
     value = total_rays / dt
     if rank == 0:

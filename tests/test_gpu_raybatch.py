@@ -80,15 +80,15 @@ def test_neus_train_step_random_batch_vs_oracle(precision):
     Gradient bar, settled against a float64 truth (the oracle's step evaluated in float64 on the same
     fp32 inputs, pixels and sample depths): every weight gradient is a sum over 65 k sample points, and
     the fp32 oracle itself is off that truth by up to a few 1e-5 of the tensor's largest entry.  So
-      (1) element-wise, |gpu - f64| <= 2 E + 1e-5 max|f64| for every parameter, E the tensor's fp32
+      (1) element-wise, |gpu - f64| <= E + 1e-5 max|f64| for every parameter, E the tensor's fp32
           error envelope: the largest max|oracle32 - f64| of three fp32 evaluations of the same step --
           point sums in two orders (the rays as drawn, and reversed; the loss is a mean over rays), and
           one with one-ulp relative noise on the points entering the positional encoding (the GPU
           forms o + t d with fused multiply-adds; sin(2^5 x) amplifies an ulp of x 32-fold).  Two fp32
           computations err at different elements (an element-wise bound fails on uncorrelated
-          rounding) and by different amounts (r04: layer 0 weight_v 6.9e-5 on
-          the GPU's fp32 path against 4.8e-5 for all three oracle variants: hipBLASLt's split-K sums are
-          one more order), so the bar is twice the spread of fp32 evaluations, and
+          rounding), hence the envelope's max.  (r04 needed 2 E: layer 0 weight_v was 6.9e-5 off on the
+          fp32 path against 4.8e-5 for all three oracle variants, from hipBLASLt's split-K sums; r05 runs
+          those weight gradients on nr_wgrad's exact-fp32 fixed-order reduction), and
       (2) the 64-ray golden tests' bar |gpu - oracle32| <= 1e-4 |oracle32| + 1e-5 max|oracle32| for every
           tensor on which the fp32 oracle itself meets 1e-4 |f64| + 1e-5 max|f64| against the truth.
     Losses 1e-5 relative."""
@@ -134,12 +134,13 @@ def test_neus_train_step_random_batch_vs_oracle(precision):
     rev = torch.arange(511, -1, -1)
     from oracle import nets as onets
     embed0 = onets.embed
-    variants = (('f32', torch.float32, None, 0.0), ('f32rev', torch.float32, rev, 0.0),
-                ('f32ulp', torch.float32, None, 2.0 ** -24), ('f64', torch.float64, None, 0.0))
-    for tag, dt, perm, noise in variants:
-        sdp = {k: (v.to(dt) if v.is_floating_point() else v).clone()
+    variants = (('f32', torch.float32, None, 0.0, 'cpu'), ('f32rev', torch.float32, rev, 0.0, 'cpu'),
+                ('f32ulp', torch.float32, None, 2.0 ** -24, 'cpu'), ('f32gpu', torch.float32, None, 0.0, 'cuda'),
+                ('f64', torch.float64, None, 0.0, 'cpu'))
+    for tag, dt, perm, noise, dv in variants:
+        sdp = {k: (v.to(dt) if v.is_floating_point() else v).clone().to(dv)
                .requires_grad_(v.is_floating_point() and k != 'implicit_surface.obj_bounding_size') for k, v in sd.items()}
-        P_ = (lambda t: t) if perm is None else (lambda t: t[:, perm])
+        P_ = (lambda t: t.to(dv)) if perm is None else (lambda t: t[:, perm].to(dv))
         if noise:  # one-ulp relative noise on the encoded points (the GPU forms o + t d with fused multiply-adds)
             eg = torch.Generator().manual_seed(5)
             onets.embed = lambda x, n: embed0(x * (1 + noise * (torch.rand(x.shape, generator=eg, dtype=x.dtype) * 2 - 1)), n)
@@ -148,9 +149,10 @@ def test_neus_train_step_random_batch_vs_oracle(precision):
         finally:
             onets.embed = embed0
         rl['total'].backward()
-        ref[tag] = (rl, {k: v.grad.double() for k, v in sdp.items() if v.grad is not None})
+        ref[tag] = ({k: v.cpu() for k, v in rl.items()}, {k: v.grad.double().cpu() for k, v in sdp.items()
+                                                          if v.grad is not None})
     ref_losses, g32 = ref['f32']
-    g32x = [ref['f32rev'][1], ref['f32ulp'][1]]
+    g32x = [ref['f32rev'][1], ref['f32ulp'][1], ref['f32gpu'][1]]
     _, g64 = ref['f64']
     for k in ('loss_img', 'loss_eikonal', 'loss_mask', 'total'):
         a, b = float(losses[k]), float(ref_losses[k])
@@ -162,11 +164,15 @@ def test_neus_train_step_random_batch_vs_oracle(precision):
         scale = float(t64.abs().max()) + 1e-30
         e_gpu, e_o32 = (mine - t64).abs(), (o32 - t64).abs()
         env = max([float(e_o32.max())] + [float((g[k] - t64).abs().max()) for g in g32x])
+        e_gpu_oracle = float((g32x[2][k] - t64).abs().max())
         worst_gpu, worst_o32 = max(worst_gpu, float(e_gpu.max()) / scale), max(worst_o32, env / scale)
         o32_meets = bool((e_o32 <= 1e-4 * t64.abs() + 1e-5 * scale).all())
-        print(f'{precision} {k}: |gpu-f64| max {float(e_gpu.max()) / scale:.2e}, fp32 envelope (3 variants) '
-              f'{env / scale:.2e} (of the tensor scale {scale:.3e}); oracle32 meets 1e-5: {o32_meets}')
-        assert bool((e_gpu <= 2 * env + 1e-5 * scale).all()), (k, float(e_gpu.max()) / scale, env / scale)
+        print(f'{precision} {k}: |gpu-f64| max {float(e_gpu.max()) / scale:.2e}, fp32 envelope (4 variants) '
+              f'{env / scale:.2e} (the oracle in fp32 on the GPU: {e_gpu_oracle / scale:.2e}; of the tensor scale '
+              f'{scale:.3e}); oracle32 meets 1e-5: {o32_meets}')
+        # r05: the fp32 mode's weight gradients run on nr_wgrad's exact-fp32 fixed-order reduction (r04:
+        # hipBLASLt split-K, 1.43x the envelope on layers 0 / 4): the single-envelope bar holds in both modes
+        assert bool((e_gpu <= env + 1e-5 * scale).all()), (k, float(e_gpu.max()) / scale, env / scale)
         if o32_meets:
             n_tight += 1
             s32 = float(o32.abs().max()) + 1e-30
