@@ -664,6 +664,15 @@ int nr_sdf_train_pack(const NrSdfDesc* d, const float* const* W, const float* co
  * offset ([3][256] then [3] bias; kb = nbo = 0); training pack: D+1 = head^T, D+2.. = W_{D-1}^T .. W_1^T,
  * 2D+1 = W_0^T (output blocks [feature ; small inputs]) */
 int nr_radiance_op_info(const NrRadDesc* d, int op, int64_t* offset, int* kb, int* nbo);
+/* Training forward of a ReLU D=4 radiance net (RadianceNet.forward with a graph, base.py:372-391) with
+ * exact fp32 products: `packed` is the net's pack for a desc with precision NR_PREC_FP32 (nr_radiance_pack),
+ * feat [P][256], small[p * ld_small + f] the small inputs [x, embed_view(v), normals] (nr_radiance_input's
+ * first columns); outputs the hidden activations h0..h3 [P][256] (after the ReLU, for the backward) and
+ * rgb [P][3] (sigmoid).  The layers chain in registers in one launch; the ReLU masks come from fp32
+ * pre-activations as the reference's.  NR_ERR_UNSUPPORTED for SIREN / D != 4 / f16x3 packs. */
+int nr_radiance_train_fwd32(const NrRadDesc* d, const void* packed, const float* feat, const float* small,
+                            int64_t ld_small, int64_t P, float* h0, float* h1, float* h2, float* h3, float* rgb,
+                            void* stream);
 size_t nr_radiance_train_packed_bytes(const NrRadDesc* d);
 int nr_radiance_train_pack(const NrRadDesc* d, const float* const* W, const float* const* b, void* packed,
                            void* stream);

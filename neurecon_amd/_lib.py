@@ -166,6 +166,8 @@ _SIGS = {
     'nr_sphere_trace_workspace_bytes': (_c_sz, [_c_i64]),
     'nr_sphere_trace': (_c_i, [ctypes.POINTER(NrSdfDesc), _c_p, _c_p, _c_p, _c_i64, ctypes.c_float, ctypes.c_float,
                                _c_p, _c_p, _c_i, _c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
+    'nr_radiance_train_fwd32': (_c_i, [ctypes.POINTER(NrRadDesc), _c_p, _c_p, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_p,
+                                        _c_p, _c_p, _c_p]),
     'nr_root_find_workspace_bytes': (_c_sz, [_c_i64, _c_i]),
     'nr_root_find': (_c_i, [ctypes.POINTER(NrSdfDesc), _c_p, _c_p, _c_p, _c_i64, ctypes.c_float, ctypes.c_float, _c_p,
                             _c_p, _c_i, _c_p, _c_i, _c_i, ctypes.c_float, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p,

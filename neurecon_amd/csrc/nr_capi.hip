@@ -922,6 +922,21 @@ int nr_radiance_forward(const NrRadDesc* d, const void* packed, const float* x, 
                          d->multires_view, (hipStream_t)stream);
 }
 
+int nr_radiance_train_fwd32(const NrRadDesc* d, const void* packed, const float* feat, const float* small,
+                            int64_t ld_small, int64_t P, float* h0, float* h1, float* h2, float* h3, float* rgb,
+                            void* stream) {
+  int rc = check_rad_desc(d);
+  if (rc) return rc;
+  NR_REQUIRE(P >= 0, NR_ERR_ARG, "nr_radiance_train_fwd32: negative P");
+  if (P == 0) return NR_OK;
+  NR_REQUIRE(packed && feat && small && h0 && h1 && h2 && h3 && rgb, NR_ERR_ARG,
+             "nr_radiance_train_fwd32: null argument");
+  const RadLayout L = rad_layout(*d);
+  NR_REQUIRE(ld_small >= L.n_small, NR_ERR_ARG, "nr_radiance_train_fwd32: ld_small below the small-input count");
+  float* const h[4] = {h0, h1, h2, h3};
+  return launch_radiance_train32(L, packed, feat, small, ld_small, L.n_small, P, h, rgb, (hipStream_t)stream);
+}
+
 // ---- training layer GEMMs (nr_mlp.hip tgemm_kernel) ---------------------------------------------
 int nr_train_gemm(const NrTrainGemm* a, int KB, int KB2, int NBO, int NB2, void* stream) {
   NR_REQUIRE(a, NR_ERR_ARG, "nr_train_gemm: null argument");

@@ -133,6 +133,9 @@ int launch_radiance(const RadLayout& L, const void* packed, const float* x, cons
                     int64_t vmod, const float* normals, const float* feature, int64_t P, float* rgb, int nfreq_view,
                     hipStream_t stream, const int* P_dev = nullptr);  // P_dev: device count, P_eff = min(P, *P_dev)
 
+// training forward of a ReLU D=4 radiance net on its fp32 pack: h[0..3] [P][256], rgb [P][3]
+int launch_radiance_train32(const RadLayout& L, const void* packed, const float* feat, const float* small,
+                            int64_t ld_small, int n_small, int64_t P, float* const* h, float* rgb, hipStream_t stream);
 SdfLayout sdf_layout(const NrSdfDesc& d);
 RadLayout rad_layout(const NrRadDesc& d);
 int check_sdf_desc(const NrSdfDesc* d);

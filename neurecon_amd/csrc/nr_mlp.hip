@@ -2204,6 +2204,102 @@ __global__ __launch_bounds__(kThreads) void radiance_kernel(RadKArgs a) {
 }
 
 // =============================================================================================
+// Training forward of the ReLU radiance net with exact fp32 products (RadianceTG.forward,
+// base.py:372-391 with a graph): the fp32 render kernel's layer chain (radiance_kernel<FP32>: the
+// activations stay in registers from layer to layer, v_mfma_f32_16x16x4_f32 over an fp32 pack) with
+// every hidden activation h_l stored ([P, 256] row-major, after the ReLU) for the backward, the small
+// inputs read from the training input tensor (nr_radiance_input's [x, embed_view(v), normals] columns,
+// the same values the backward's weight gradient of layer 0 reads) and the feature from its own
+// [P, 256] tensor; rgb = sigmoid(head).  The ReLU masks come from fp32 pre-activations as in the
+// reference (an f16x3 z flips a few masks per step); one launch replaces the four
+// hipBLASLt GEMMs, their ReLU launches and the head.
+// =============================================================================================
+struct RadTrainArgs {
+  const char* packed;
+  RadLayout L;
+  const float* feat;   // [P][256]
+  const float* small;  // small[p * ld_small + f], f < n_small
+  int64_t ld_small;
+  int n_small;
+  int64_t P;
+  float* h[4];         // [P][256] each
+  float* rgb;          // [P][3]
+};
+
+template <int KBS>
+__global__ __launch_bounds__(kThreads) void radiance_train32_kernel(RadTrainArgs a) {
+  constexpr int CB = chunk_bytes(16 + KBS);
+  __shared__ __attribute__((aligned(16))) char smem[kRing * CB];
+  WStream<CB> ws{smem, nullptr, 0, 0, 0};
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  const RadLayout& L = a.L;
+  const char* W = a.packed;
+  auto OP = [&](int i) { return W + L.op_off[i]; };
+  auto OPB = [&](int i) { return (int)L.op_bytes[i]; };
+  const float* head = (const float*)(W + L.head_off);  // [3][256] weights then [3] bias
+
+  ws.start(OP(0), OPB(0), OP(0) + OPB(0), OPB(0));
+  const int64_t Pn = a.P;
+  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < Pn; base += (int64_t)gridDim.x * kPointsPerWG) {
+    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < Pn;
+    const int64_t p = base + wave * kTile + j;
+    const bool valid = p < Pn;
+    const int64_t pc = valid ? p : Pn - 1;
+    float4 S[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = 16 * b + 4 * g + r;
+        v[r] = (b < KBS && f < a.n_small) ? a.small[pc * a.ld_small + f] : 0.0f;
+      }
+      S[b] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    float4 X[16], Y[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) X[b] = *(const float4*)(a.feat + pc * 256 + 16 * b + 4 * g);
+    auto store = [&](int l, const float4 (&H)[16]) {
+      if (!valid) return;
+      float* h = a.h[l] + p * 256 + 4 * g;
+#pragma unroll
+      for (int b = 0; b < 16; ++b) *(float4*)(h + 16 * b) = H[b];
+    };
+    gemm_fwd<NR_PREC_FP32, 16, KBS, 16, ACT_RELU>(ws, OP(0), OP(1), OPB(1), X, S, Y, nullptr, nullptr, false, lane);
+    store(0, Y);
+    gemm_fwd<NR_PREC_FP32, 16, 0, 16, ACT_RELU>(ws, OP(1), OP(2), OPB(2), Y, S, X, nullptr, nullptr, false, lane);
+    store(1, X);
+    gemm_fwd<NR_PREC_FP32, 16, 0, 16, ACT_RELU>(ws, OP(2), OP(3), OPB(3), X, S, Y, nullptr, nullptr, false, lane);
+    store(2, Y);
+    gemm_fwd<NR_PREC_FP32, 16, 0, 16, ACT_RELU>(ws, OP(3), has_next ? OP(0) : nullptr, OPB(0), Y, S, X, nullptr,
+                                                nullptr, false, lane);
+    store(3, X);
+    // head: Linear(256 -> 3) + sigmoid (VALU dot products, as radiance_kernel)
+    float r[3];
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      float part = 0.f;
+#pragma unroll
+      for (int b = 0; b < 16; ++b) {
+        const float4 w = *(const float4*)(head + o * 256 + 16 * b + 4 * g);
+        part = fmaf(X[b].x, w.x, part);
+        part = fmaf(X[b].y, w.y, part);
+        part = fmaf(X[b].z, w.z, part);
+        part = fmaf(X[b].w, w.w, part);
+      }
+      r[o] = sigmoidf_ref(wave_sum4(part) + head[3 * 256 + o]);
+    }
+    if (valid && g == 0) {
+      a.rgb[p * 3 + 0] = r[0];
+      a.rgb[p * 3 + 1] = r[1];
+      a.rgb[p * 3 + 2] = r[2];
+    }
+  }
+  wait_vmcnt(0);
+}
+
+// =============================================================================================
 // Radiance net on the v3 pipeline (rad4_kernel, f16x3, ReLU, D = 4): the sdf4_kernel structure
 // (128-point tile, kNC-column waves, weight ring by LDS-DMA two chunks ahead, per-chunk operand
 // split at a scale fixed from the op's pack-time bound, epilogue staged beside the next chunk's
@@ -3384,6 +3480,21 @@ int launch_nerf(const NerfLayout& L, const void* packed, const float* x4, const 
   ProfScope prof("nerf", (double)P, stream, P_dev, 1);
   if (L.prec == NR_PREC_F16X3) hipLaunchKernelGGL(nerf4_kernel, dim3(grid), dim3(kT4), 0, stream, a);  // v3 pipeline
   else hipLaunchKernelGGL((nerf_kernel<NR_PREC_FP32>), dim3(grid), dim3(kThreads), 0, stream, a);
+  NR_HIP_CHECK(hipGetLastError());
+  return NR_OK;
+}
+
+int launch_radiance_train32(const RadLayout& L, const void* packed, const float* feat, const float* small,
+                            int64_t ld_small, int n_small, int64_t P, float* const* h, float* rgb, hipStream_t stream) {
+  if (P <= 0) return NR_OK;
+  if (L.prec != NR_PREC_FP32 || L.siren || L.D != 4 || (L.kbs != 2 && L.kbs != 4)) {
+    set_error("nr_radiance_train_fwd32: needs the fp32 pack of a ReLU D=4 radiance net");
+    return NR_ERR_UNSUPPORTED;
+  }
+  RadTrainArgs a{(const char*)packed, L, feat, small, ld_small, n_small, P, {h[0], h[1], h[2], h[3]}, rgb};
+  ProfScope prof("radiance_train32", (double)P, stream);
+  if (L.kbs == 2) hipLaunchKernelGGL((radiance_train32_kernel<2>), dim3(grid_for(P)), dim3(kThreads), 0, stream, a);
+  else hipLaunchKernelGGL((radiance_train32_kernel<4>), dim3(grid_for(P)), dim3(kThreads), 0, stream, a);
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;
 }

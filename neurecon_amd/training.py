@@ -638,6 +638,29 @@ def _train_pack(module, kind, Ws, bs, device):
     return packed
 
 
+def _fp32_pack(net, Ws, bs, device):
+    """the radiance net's render pack built for exact fp32 products (the NR_PREC_FP32 layout of
+    nr_radiance_pack) from the step's effective weights, cached per parameter version: the operand of
+    the fp32 training forward (nr_radiance_train_fwd32)"""
+    from .base import _version_key, _ptr_array
+    key = _version_key(net, 'fp32pack', device)
+    c = getattr(net, '_nr_fp32_cache', None)
+    if c is not None and c[0] == key:
+        return c[1], c[2]
+    lib = L.lib()
+    desc = net.nr_desc()
+    desc.precision = L.PREC_FP32
+    nbytes = lib.nr_radiance_packed_bytes(ctypes.byref(desc))
+    if nbytes == 0:
+        raise NotImplementedError('neurecon_amd: ' + lib.nr_last_error().decode())
+    W = [w.detach().float().contiguous() for w in Ws]
+    b = [x.detach().float().contiguous() for x in bs]
+    packed = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    L.check(lib.nr_radiance_pack(ctypes.byref(desc), _ptr_array(W), _ptr_array(b), L.ptr(packed), L.stream_of(device)))
+    net._nr_fp32_cache = (key, desc, packed, W, b)
+    return desc, packed
+
+
 def uses_train_gemm(module):
     """f16x3 softplus SDF nets (D=8, skip 4) and f16x3 ReLU radiance nets with D=4 train on nr_train_gemm"""
     if getattr(module, 'precision', 'fp32') != 'f16x3' or getattr(module, 'use_siren', False):
@@ -860,11 +883,14 @@ class SdfNablaTG(torch.autograd.Function):
 class RadianceTG(torch.autograd.Function):
     """RadianceFn with the backward on nr_train_gemm (f16x3 ReLU nets, D=4): head^T and W3^T..W1^T of
     the training pack with the ReLU mask in the epilogue, W0^T split into d feature / d small inputs
-    (-> d normals); weight gradients on hipBLASLt.  The forward stays on fp32 GEMMs: ReLU'(z) is a
-    step, and the f16x3 forward's ~5e-7 relative error in z flips a few masks per step against the
+    (-> d normals); weight gradients on nr_wgrad.  The forward keeps exact fp32 products: ReLU'(z) is
+    a step, and the f16x3 forward's ~5e-7 relative error in z flips a few masks per step against the
     reference's fp32 z -- each flip moves one point's whole contribution to the gradients of every
     earlier layer (measured: layer-2 bias gradient 3.8e-4 off the float64 truth with the f16x3
-    forward, 9e-8 with the fp32 one; tools/train_diag.py --probe).  The backward has no such decision."""
+    forward, 9e-8 with the fp32 one; tools/train_diag.py --probe).  r05: that fp32 forward is one
+    launch of nr_radiance_train_fwd32 (the four layers chained in registers on v_mfma_f32_16x16x4_f32
+    over the net's fp32 pack, every h_l stored, sigmoid head) instead of four hipBLASLt GEMMs, their
+    ReLU launches and the head.  The backward has no such decision."""
 
     @staticmethod
     def forward(ctx, x, v, nrm, feat, net, *params):
@@ -877,14 +903,12 @@ class RadianceTG(torch.autograd.Function):
         inp = torch.empty(P, ns + 256, device=x.device)  # [x, embed_view(v), normals, feature] (base.py:383-386)
         L.check(L.lib().nr_radiance_input(L.ptr(x), L.ptr(v), L.ptr(nrm), L.ptr(feat), P, nfv, int(view), 256,
                                           L.ptr(inp), _st(x)))
-        H = []
-        h = inp
-        for l in range(4):
-            h = torch.addmm(bs[l], h, Ws[l].t())
-            L.check(L.lib().nr_activation(L.ptr(h), None, h.numel(), 0, _st(x)))  # ReLU
-            H.append(h)
-        rgb = torch.addmm(bs[4], h, Ws[4].t())
-        L.check(L.lib().nr_activation(L.ptr(rgb), None, rgb.numel(), 2, _st(x)))  # sigmoid
+        desc32, pk32 = _fp32_pack(net, Ws, bs, x.device)
+        H = [torch.empty(P, 256, device=x.device) for _ in range(4)]
+        rgb = torch.empty(P, 3, device=x.device)
+        feat = feat.contiguous()
+        L.check(L.lib().nr_radiance_train_fwd32(ctypes.byref(desc32), L.ptr(pk32), L.ptr(feat), L.ptr(inp), ns + 256, P,
+                                                *[L.ptr(h) for h in H], L.ptr(rgb), _st(x)))
         ctx.net = net
         ctx.cfg = (ns, nvw, view)
         ctx.save_for_backward(rgb, inp, *H, *Ws)

@@ -82,7 +82,10 @@ class RadianceNet:
         self.act = sine30 if siren else torch.relu
         self.layers = [(wn_weight(sd, f'{prefix}layers.{l}'), sd[f'{prefix}layers.{l}.bias']) for l in range(D + 1)]
 
-    def forward(self, x, v, normals, feature):
+    def forward(self, x, v, normals, feature, masks=None, z_out=None):
+        """masks (test instrumentation, ReLU nets): per hidden layer a bool tensor [..., 256] that
+        replaces relu(z) by z * mask -- the ReLU decisions pinned to another evaluation's, as the tests
+        pin the sample depths; z_out: a list that receives every hidden layer's pre-activation."""
         xe = embed(x, self.multires)
         if self.use_view_dirs:
             h = torch.cat([xe, embed(v, self.multires_view), normals, feature], dim=-1)
@@ -90,7 +93,14 @@ class RadianceNet:
             h = torch.cat([xe, feature], dim=-1)
         for i, (W, b) in enumerate(self.layers):
             z = F.linear(h, W, b)
-            h = torch.sigmoid(z) if i == self.D else self.act(z)
+            if i < self.D and z_out is not None:
+                z_out.append(z.detach())
+            if i == self.D:
+                h = torch.sigmoid(z)
+            elif masks is not None:
+                h = z * masks[i].reshape(z.shape).to(z.dtype)
+            else:
+                h = self.act(z)
         return h
 
 

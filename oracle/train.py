@@ -22,12 +22,14 @@ def nablas_graph(net, x):
 
 def neus_train_losses(sd, rays_o, rays_d, target_rgb, target_mask, w_eikonal=0.1, w_mask=1.0, with_mask=True,
                       d_all=None, speed_factor=10.0, obj_bounding_radius=1.0, N_samples=64, N_importance=64,
-                      N_upsample_iters=4, N_outside=0, dtype=torch.float32):
+                      N_upsample_iters=4, N_outside=0, dtype=torch.float32, rad_masks=None, rad_z=None):
     """losses (neus.py:453-478) of one training render of rays [B, N, 3]; d_all [B, N, S] optional
     (the sorted sample depths; computed with the no-grad upsampling when None); N_outside > 0 adds the
     NeRF++ background (neus.py:303-343, perturb=False) with its parameters in the graph.
     dtype=torch.float64 (with a float64 state_dict and d_all given): the same function evaluated in
-    float64 on the same inputs -- the truth the fp32 oracle and the GPU are both measured against."""
+    float64 on the same inputs -- the truth the fp32 oracle and the GPU are both measured against.
+    rad_masks / rad_z: RadianceNet.forward's masks / z_out on the mid-points [B, N, S-1] (test
+    instrumentation: the radiance net's ReLU decisions pinned to the GPU's)."""
     o = rays_o.reshape(rays_o.shape[0], -1, 3).to(dtype)
     d = F.normalize(rays_d.reshape(rays_d.shape[0], -1, 3).to(dtype), dim=-1)
     if d_all is not None:
@@ -45,7 +47,7 @@ def neus_train_losses(sd, rays_o, rays_d, target_rgb, target_mask, w_eikonal=0.1
     s = torch.exp(sd['ln_s'] * speed_factor)
     cdf, alpha = sdf_to_alpha(sdf, s)
     _, n_m, h_m = nablas_graph(sdf_net, pts_mid)                            # neus.py:103-106, :298
-    rad = rad_net.forward(pts_mid, d.unsqueeze(-2).expand_as(pts_mid), n_m, h_m)
+    rad = rad_net.forward(pts_mid, d.unsqueeze(-2).expand_as(pts_mid), n_m, h_m, masks=rad_masks, z_out=rad_z)
     if N_outside > 0:                                                       # neus.py:303-343
         tt = torch.linspace(0, 1, N_outside + 2)[..., 1:-1].float().to(dtype)
         d_out = torch.cat([d_mid, far / torch.flip(tt, dims=[-1])], -1)

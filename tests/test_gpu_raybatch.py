@@ -79,16 +79,23 @@ def test_neus_train_step_random_batch_vs_oracle(precision):
 
     Gradient bar, settled against a float64 truth (the oracle's step evaluated in float64 on the same
     fp32 inputs, pixels and sample depths): every weight gradient is a sum over 65 k sample points, and
-    the fp32 oracle itself is off that truth by up to a few 1e-5 of the tensor's largest entry.  So
+    the fp32 oracle itself is off that truth by up to a few 1e-5 of the tensor's largest entry.  The
+    discrete decisions of the step are pinned to the GPU's, as in every parity test here: the sample
+    depths, and (r05) the radiance net's ReLU decisions -- every oracle evaluation multiplies its hidden
+    pre-activations by the GPU's masks instead of applying relu.  A decision taken on a z within
+    rounding of 0 flips between any two fp32 evaluations (about 67 M of them per step) and moves one
+    point's whole contribution in every earlier layer's gradient, so without the pinning the bar
+    measured which evaluation happened to flip where.  The pinned decisions are checked against
+    float64's: at most 1e-5 of them differ, each at |z64| <= 1e-5 of the layer's largest |z|.  Then
       (1) element-wise, |gpu - f64| <= E + 1e-5 max|f64| for every parameter, E the tensor's fp32
-          error envelope: the largest max|oracle32 - f64| of three fp32 evaluations of the same step --
-          point sums in two orders (the rays as drawn, and reversed; the loss is a mean over rays), and
-          one with one-ulp relative noise on the points entering the positional encoding (the GPU
-          forms o + t d with fused multiply-adds; sin(2^5 x) amplifies an ulp of x 32-fold).  Two fp32
-          computations err at different elements (an element-wise bound fails on uncorrelated
-          rounding), hence the envelope's max.  (r04 needed 2 E: layer 0 weight_v was 6.9e-5 off on the
-          fp32 path against 4.8e-5 for all three oracle variants, from hipBLASLt's split-K sums; r05 runs
-          those weight gradients on nr_wgrad's exact-fp32 fixed-order reduction), and
+          error envelope: the largest max|oracle32 - f64| of four fp32 evaluations of the same step --
+          point sums in two orders (the rays as drawn, and reversed; the loss is a mean over rays), one
+          with one-ulp relative noise on the points entering the positional encoding (the GPU forms
+          o + t d with fused multiply-adds; sin(2^5 x) amplifies an ulp of x 32-fold), and the oracle
+          run on the GPU (torch eager, ROCm's fp32 kernels).  Two fp32 computations err at different
+          elements (an element-wise bound fails on uncorrelated rounding), hence the envelope's max.
+          (r04 needed 2 E; r05 runs the fp32 weight gradients on nr_wgrad's exact-fp32 fixed-order
+          reduction), and
       (2) the 64-ray golden tests' bar |gpu - oracle32| <= 1e-4 |oracle32| + 1e-5 max|oracle32| for every
           tensor on which the fp32 oracle itself meets 1e-4 |f64| + 1e-5 max|f64| against the truth.
     Losses 1e-5 relative."""
@@ -106,10 +113,27 @@ def test_neus_train_step_random_batch_vs_oracle(precision):
     m.train()
     args = types.SimpleNamespace(data=types.SimpleNamespace(N_rays=512),
                                  training=types.SimpleNamespace(w_eikonal=0.1, w_mask=1.0, with_mask=True))
+    # the radiance net's ReLU decisions on the GPU (its saved post-ReLU activations), to pin the
+    # oracle's to them below
+    from neurecon_amd import training as ntr
+    rad0, rad_h = ntr.radiance, []
+
+    def rad_rec(net, *a):
+        y = rad0(net, *a)
+        sv, D = y.grad_fn.saved_tensors, net.D
+        rad_h[:] = sv[2:2 + D] if ntr.uses_train_gemm(net) else sv[D + 3:2 * D + 3]  # RadianceTG / RadianceFn
+        return y
+    ntr.radiance = rad_rec
     torch.manual_seed(9)
-    ret = Trainer(m, device_ids=[0]).forward(args, None, {'intrinsics': K.cuda(), 'c2w': c2w.cuda(),
+    try:
+        ret = Trainer(m, device_ids=[0]).forward(args, None, {'intrinsics': K.cuda(), 'c2w': c2w.cuda(),
                                                           'object_mask': tgt_mask.cuda()},
-                                             {'rgb': tgt_rgb.cuda()}, _train_kw(H, W), 0, device='cuda')
+                                                 {'rgb': tgt_rgb.cuda()}, _train_kw(H, W), 0, device='cuda')
+    finally:
+        ntr.radiance = rad0
+    assert len(rad_h) == 4
+    rad_masks = [(h > 0).reshape(1, 512, -1, h.shape[-1]).cpu() for h in rad_h]
+    del rad_h
     si = ret['extras']['select_inds'].cpu()
     torch.manual_seed(9)
     hs, ws = torch.randint(0, H, size=[512]), torch.randint(0, W, size=[512])
@@ -130,7 +154,7 @@ def test_neus_train_step_random_batch_vs_oracle(precision):
     ro, rd, _ = orays.get_rays(c2w, K, H, W, select_inds=si)
     t_rgb = torch.gather(tgt_rgb, 1, si[..., None].expand(1, 512, 3))
     t_mask = torch.gather(tgt_mask, 1, si)
-    ref = {}
+    ref, z64 = {}, []
     rev = torch.arange(511, -1, -1)
     from oracle import nets as onets
     embed0 = onets.embed
@@ -145,12 +169,23 @@ def test_neus_train_step_random_batch_vs_oracle(precision):
             eg = torch.Generator().manual_seed(5)
             onets.embed = lambda x, n: embed0(x * (1 + noise * (torch.rand(x.shape, generator=eg, dtype=x.dtype) * 2 - 1)), n)
         try:
-            rl, _ = neus_train_losses(sdp, P_(ro), P_(rd), P_(t_rgb), P_(t_mask), d_all=P_(d_all), dtype=dt)
+            rl, _ = neus_train_losses(sdp, P_(ro), P_(rd), P_(t_rgb), P_(t_mask), d_all=P_(d_all), dtype=dt,
+                                      rad_masks=[P_(mk) for mk in rad_masks], rad_z=z64 if tag == 'f64' else None)
         finally:
             onets.embed = embed0
         rl['total'].backward()
         ref[tag] = ({k: v.cpu() for k, v in rl.items()}, {k: v.grad.double().cpu() for k, v in sdp.items()
                                                           if v.grad is not None})
+    # the pinned ReLU decisions against float64's: a decision differs only where z is within rounding
+    # of 0 (a wrong mask would differ at |z| ~ 1 and in bulk)
+    for l, (mk, z) in enumerate(zip(rad_masks, z64)):
+        z = z.reshape(mk.shape)
+        dis = (z > 0) != mk
+        zmax = float(z.abs().max())
+        zd = float(z[dis].abs().max()) if bool(dis.any()) else 0.0
+        print(f'{precision} radiance layer {l}: {int(dis.sum())} of {mk.numel()} ReLU decisions differ from '
+              f'float64, max |z64| there {zd:.2e} (layer max {zmax:.2e})')
+        assert int(dis.sum()) <= 1e-5 * mk.numel() and zd <= 1e-5 * zmax, (l, int(dis.sum()), zd)
     ref_losses, g32 = ref['f32']
     g32x = [ref['f32rev'][1], ref['f32ulp'][1], ref['f32gpu'][1]]
     _, g64 = ref['f64']

@@ -502,3 +502,49 @@ def test_merged_sample_and_midpoint_evaluation_matches_separate():
     torch.cuda.synchronize()
     assert torch.equal(s_all[:4096], s1) and torch.equal(n_all[:4096], n1)
     assert torch.equal(n_all[4096:], n2) and torch.equal(f_m, f2)
+
+
+def test_radiance_train_fwd32_vs_fp64():
+    """nr_radiance_train_fwd32 (RadianceTG's forward: the four ReLU layers chained in registers with exact
+    fp32 products over the net's fp32 pack, every hidden activation stored, sigmoid head) against the
+    same layers in float64 on 32 k points: hidden activations and rgb within 1e-5 of the tensor scale,
+    no further from float64 than torch's fp32 GEMMs (2x + 1e-6), and ReLU masks equal to the fp32
+    GEMMs' except where |z| is at fp32 rounding level; the config-(b) net (view embedding 4, normals)."""
+    import ctypes
+    from neurecon_amd import _lib as L
+    from neurecon_amd.base import RadianceNet
+    from neurecon_amd.training import _fp32_pack
+    torch.manual_seed(3)
+    net = RadianceNet(D=4, W=256, W_geo_feat=256, embed_multires=-1, embed_multires_view=4,
+                      precision='f16x3').cuda()
+    P = 32768
+    x = torch.rand(P, 3, device='cuda') * 2 - 1
+    v = torch.nn.functional.normalize(torch.randn(P, 3, device='cuda'), dim=-1)
+    nrm = torch.randn(P, 3, device='cuda')
+    feat = torch.randn(P, 256, device='cuda')
+    ns = 3 + 27 + 3
+    inp = torch.empty(P, ns + 256, device='cuda')
+    L.check(L.lib().nr_radiance_input(L.ptr(x), L.ptr(v), L.ptr(nrm), L.ptr(feat), P, 4, 1, 256, L.ptr(inp),
+                                      L.stream_of(x.device)))
+    with torch.no_grad():
+        Ws = [l.effective_weight() for l in net.layers]
+        bs = [l.bias for l in net.layers]
+        desc, pk = _fp32_pack(net, Ws, bs, x.device)
+        H = [torch.empty(P, 256, device='cuda') for _ in range(4)]
+        rgb = torch.empty(P, 3, device='cuda')
+        L.check(L.lib().nr_radiance_train_fwd32(ctypes.byref(desc), L.ptr(pk), L.ptr(feat), L.ptr(inp), ns + 256, P,
+                                                *[L.ptr(h) for h in H], L.ptr(rgb), L.stream_of(x.device)))
+        h64, h32 = inp.double(), inp
+        for l in range(4):
+            z64 = h64 @ Ws[l].double().t() + bs[l].double()
+            z32 = torch.addmm(bs[l], h32, Ws[l].t())
+            h64, h32 = z64.clamp_min(0), z32.clamp_min(0)
+            scale = float(h64.abs().max())
+            e_hip = float((H[l].double() - h64).abs().max())
+            e_32 = float((h32.double() - h64).abs().max())
+            print(f'h{l}: max |hip - f64| {e_hip / scale:.2e}, |fp32 GEMM - f64| {e_32 / scale:.2e} of {scale:.3e}')
+            assert e_hip <= 2 * e_32 + 1e-6 * scale and e_hip <= 1e-5 * scale, l
+            flip = (H[l] > 0) != (h32 > 0)
+            assert bool((z64.abs()[flip] <= 1e-5 * scale).all()), (l, int(flip.sum()))
+        y64 = torch.sigmoid(h64 @ Ws[4].double().t() + bs[4].double())
+        assert float((rgb.double() - y64).abs().max()) <= 1e-6
