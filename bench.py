@@ -85,6 +85,8 @@ def parse():
                     help="b: the BASELINE metric (default); frame_d: config (d) full frame sharded over the GPUs; "
                          "train: NeuS training step")
     ap.add_argument('--train-rays', type=int, default=512)
+    ap.add_argument('--train-nerfpp', action='store_true',
+                    help='--workload train with the NeRF++ background (configs/neus_nomask_blended.yaml)')
     ap.add_argument('--adam', default='fused', choices=['fused', 'foreach'],
                     help='torch.optim.Adam implementation of the training workload')
     ap.add_argument('--cpu-rays', type=int, default=1024)
@@ -807,7 +809,7 @@ def run(args):
         step, rays_per_step = frame_d_setup(dev, args.precision, args.frame_workspace_gb)  # one frame, all ranks
         n_rays = rays_per_step
     elif args.workload == 'train':
-        step = train_setup(dev, args.precision, args.train_rays, world, args.adam)
+        step = train_setup(dev, args.precision, args.train_rays, world, args.adam, nerfpp=args.train_nerfpp)
         n_rays = args.train_rays * world
     else:
         model = make_model(dev, args.precision)
@@ -911,10 +913,12 @@ def run(args):
                    'roofline': roof}
         elif args.workload == 'train':
             roof = train_roofline(kstats, dt, args.steps, census)
-            out = {'metric': 'training rays/sec, NeuS (configs/neus.yaml: 512 rays per GPU, fwd+bwd+Adam)',
+            out = {'metric': ('training rays/sec, NeuS + NeRF++ (configs/neus_nomask_blended.yaml: 512 rays per GPU, '
+                              'fwd+bwd+Adam)' if args.train_nerfpp else
+                              'training rays/sec, NeuS (configs/neus.yaml: 512 rays per GPU, fwd+bwd+Adam)'),
                    'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
                    'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
-                   'scaling': 'weak', 'vs_baseline': None, 'dtype': (dtype + ' layer GEMMs (nr_train_gemm) and weight gradients (nr_wgrad); radiance forward f32'
+                   'scaling': 'weak', 'vs_baseline': None, 'dtype': (dtype + ' layer GEMMs (nr_train_gemm) and weight gradients (nr_wgrad); radiance forward fp32 MFMA'
                              if args.precision == 'f16x3' else 'f32'),
                    'data': 'synthetic (random 64x64 targets, config-(b) camera, seeded geometric-init weights)',
                    'config': {'workload': 'NeuS Trainer.forward + backward (double backward through the nablas) + '

@@ -709,116 +709,155 @@ __device__ __forceinline__ double sp1_grad(float x) { return x > 20.0f ? 1.0 : 1
 // composite with the background merged (neus.py:325-352): sample k < S-1 takes the SDF alpha and the
 // radiance net's colour where inside[k], else the background's; k >= S-1 are background samples.
 // alpha_out = 1 - exp(-softplus(sigma) dist), dist = d_{k+1} - d_k (1e10 for the last).
-__global__ void neus_composite_bg_fwd_kernel(const float* __restrict__ sdf, const float* __restrict__ s_dev,
-                                             const float* __restrict__ rad, const float* __restrict__ sig_o,
-                                             const float* __restrict__ rad_o, const float* __restrict__ d_out,
-                                             const uint8_t* __restrict__ inside, int64_t R, int S, int M,
-                                             int white_bkgd, float* __restrict__ rgb, float* __restrict__ depth,
-                                             float* __restrict__ acc, float* __restrict__ w_out,
-                                             float* __restrict__ alpha_out, float* __restrict__ cdf_out) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R) return;
+// One ray per 64-lane wave, as neus_composite_fwd_kernel (r05; one thread per ray gave a 512-ray
+// training batch 8 waves for the chip: 0.35 ms fwd + 0.52 ms bwd per step): the per-sample CDFs,
+// alphas (softplus, exp) and colour staging across the lanes, the prefix product and sums on lane 0
+// in the per-ray order.  LDS floats: S + 6 M.
+__global__ __launch_bounds__(64) void neus_composite_bg_fwd_kernel(
+    const float* __restrict__ sdf, const float* __restrict__ s_dev, const float* __restrict__ rad,
+    const float* __restrict__ sig_o, const float* __restrict__ rad_o, const float* __restrict__ d_out,
+    const uint8_t* __restrict__ inside, int64_t R, int S, int M, int white_bkgd, float* __restrict__ rgb,
+    float* __restrict__ depth, float* __restrict__ acc, float* __restrict__ w_out, float* __restrict__ alpha_out,
+    float* __restrict__ cdf_out) {
+  extern __shared__ float lds[];
+  const int64_t r = blockIdx.x;
+  const int l = threadIdx.x, S1 = S - 1;
   const float s = *s_dev;
-  const int S1 = S - 1;
   const float* sd = sdf + r * S;
   const float* dk = d_out + r * M;
-  double T = 1.0, a_acc = 0.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
-  float cp = sigmoidf_ref(fmul(sd[0], s));
-  if (cdf_out) cdf_out[r * S] = cp;
-  for (int k = 0; k < M; ++k) {
-    const float dist = k + 1 < M ? fsub(dk[k + 1], dk[k]) : 1e10f;
-    const float a_o = fsub(1.0f, expf(fmul(-sp1(sig_o[r * M + k]), dist)));
-    float al = a_o;
+  float* c = lds;            // [S] cdf
+  float* la = c + S;         // [M] alpha
+  float* lw = la + M;        // [M] weights
+  float* lcol = lw + M;      // [3 M] colour
+  float* ld = lcol + 3 * M;  // [M] depths
+  for (int i = l; i < S; i += 64) {
+    const float v = sigmoidf_ref(fmul(sd[i], s));
+    c[i] = v;
+    if (cdf_out) cdf_out[r * S + i] = v;
+  }
+  __syncthreads();
+  for (int k = l; k < M; k += 64) {
+    const float d0 = dk[k];
     const float* col = rad_o + (r * M + k) * 3;
-    if (k < S1) {
-      const float cn = sigmoidf_ref(fmul(sd[k + 1], s));
-      if (cdf_out) cdf_out[r * S + k + 1] = cn;
-      const float a_in = fmaxf(fdiv(fsub(cp, cn), fadd(cp, 1e-10f)), 0.0f);
-      cp = cn;
-      if (inside[r * S1 + k]) {
-        al = a_in;
-        col = rad + (r * S1 + k) * 3;
-      }
+    float al;
+    if (k < S1 && inside[r * S1 + k]) {
+      al = fmaxf(fdiv(fsub(c[k], c[k + 1]), fadd(c[k], 1e-10f)), 0.0f);
+      col = rad + (r * S1 + k) * 3;
+    } else {
+      const float dist = k + 1 < M ? fsub(dk[k + 1], d0) : 1e10f;
+      al = fsub(1.0f, expf(fmul(-sp1(sig_o[r * M + k]), dist)));
     }
-    const float w = fmul(al, (float)T);
-    T *= (double)fadd(fsub(1.0f, al), 1e-10f);
-    c0 += (double)fmul(w, col[0]);
-    c1 += (double)fmul(w, col[1]);
-    c2 += (double)fmul(w, col[2]);
-    a_acc += (double)w;
-    w_out[r * M + k] = w;
+    la[k] = al;
+    lcol[3 * k + 0] = col[0];
+    lcol[3 * k + 1] = col[1];
+    lcol[3 * k + 2] = col[2];
+    ld[k] = d0;
     if (alpha_out) alpha_out[r * M + k] = al;
   }
-  const float accf = (float)a_acc;
-  const float den = fadd(accf, 1e-10f);
-  double dep = 0.0;
-  for (int k = 0; k < M; ++k) dep += (double)fmul(fdiv(w_out[r * M + k], den), dk[k]);
-  float o0 = (float)c0, o1 = (float)c1, o2 = (float)c2;
-  if (white_bkgd) {
-    const float bg = fsub(1.0f, accf);
-    o0 = fadd(o0, bg); o1 = fadd(o1, bg); o2 = fadd(o2, bg);
+  __syncthreads();
+  if (l == 0) {
+    double T = 1.0, a_acc = 0.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
+    for (int k = 0; k < M; ++k) {
+      const float al = la[k];
+      const float w = fmul(al, (float)T);
+      T *= (double)fadd(fsub(1.0f, al), 1e-10f);
+      c0 += (double)fmul(w, lcol[3 * k + 0]);
+      c1 += (double)fmul(w, lcol[3 * k + 1]);
+      c2 += (double)fmul(w, lcol[3 * k + 2]);
+      a_acc += (double)w;
+      lw[k] = w;
+    }
+    const float accf = (float)a_acc;
+    const float den = fadd(accf, 1e-10f);
+    double dep = 0.0;
+    for (int k = 0; k < M; ++k) dep += (double)fmul(fdiv(lw[k], den), ld[k]);
+    float o0 = (float)c0, o1 = (float)c1, o2 = (float)c2;
+    if (white_bkgd) {
+      const float bg = fsub(1.0f, accf);
+      o0 = fadd(o0, bg); o1 = fadd(o1, bg); o2 = fadd(o2, bg);
+    }
+    rgb[r * 3 + 0] = o0;
+    rgb[r * 3 + 1] = o1;
+    rgb[r * 3 + 2] = o2;
+    depth[r] = (float)dep;
+    acc[r] = accf;
   }
-  rgb[r * 3 + 0] = o0;
-  rgb[r * 3 + 1] = o1;
-  rgb[r * 3 + 2] = o2;
-  depth[r] = (float)dep;
-  acc[r] = accf;
+  __syncthreads();
+  for (int k = l; k < M; k += 64) w_out[r * M + k] = lw[k];
 }
 
 // backward of the above -> d sdf [R,S], d radiance [R,S-1,3], d sigma_out [R,M], d radiance_out
-// [R,M,3], d s per ray [R].  Work rows (floats): c [S], alpha [M], T [M], w [M], wbar [M], a_in [S-1]
-__global__ void neus_composite_bg_bwd_kernel(const float* __restrict__ sdf, const float* __restrict__ s_dev,
-                                             const float* __restrict__ rad, const float* __restrict__ sig_o,
-                                             const float* __restrict__ rad_o, const float* __restrict__ d_out,
-                                             const uint8_t* __restrict__ inside, int64_t R, int S, int M,
-                                             int white_bkgd, const float* __restrict__ g_rgb,
-                                             const float* __restrict__ g_depth, const float* __restrict__ g_acc,
-                                             const float* __restrict__ g_w, float* __restrict__ work,
-                                             float* __restrict__ d_sdf, float* __restrict__ d_rad,
-                                             float* __restrict__ d_sig, float* __restrict__ d_rad_o,
-                                             float* __restrict__ d_s) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R) return;
-  const int S1 = S - 1;
+// [R,M,3], d s per ray [R].  One ray per wave: the elementwise parts (alphas, weight adjoints, the
+// colour gradients, d sigma from the stored alpha adjoints) across the lanes, the prefix product and
+// the reverse suffix walk on lane 0.  LDS: 8 (M + 2) + 4 (3 S + 5 M) bytes.
+__global__ __launch_bounds__(64) void neus_composite_bg_bwd_kernel(
+    const float* __restrict__ sdf, const float* __restrict__ s_dev, const float* __restrict__ rad,
+    const float* __restrict__ sig_o, const float* __restrict__ rad_o, const float* __restrict__ d_out,
+    const uint8_t* __restrict__ inside, int64_t R, int S, int M, int white_bkgd, const float* __restrict__ g_rgb,
+    const float* __restrict__ g_depth, const float* __restrict__ g_acc, const float* __restrict__ g_w,
+    float* __restrict__ d_sdf, float* __restrict__ d_rad, float* __restrict__ d_sig, float* __restrict__ d_rad_o,
+    float* __restrict__ d_s) {
+  extern __shared__ double ldsd[];
+  const int64_t r = blockIdx.x;
+  const int l = threadIdx.x, S1 = S - 1;
   const float s = *s_dev;
   const float* sd = sdf + r * S;
   const float* dk = d_out + r * M;
-  float* c = work + r * (size_t)(2 * S + 4 * M);
-  float* al = c + S;
-  float* Tt = al + M;
-  float* w = Tt + M;
-  float* wb = w + M;
-  float* ain = wb + M;
-  for (int i = 0; i < S; ++i) c[i] = sigmoidf_ref(fmul(sd[i], s));
+  double* lab = ldsd;              // [M] alpha adjoints
+  double* ldb = lab + M;           // A, wd
+  float* c = (float*)(ldb + 2);    // [S] cdf
+  float* ls = c + S;               // [S] sdf
+  float* lo = ls + S;              // [S] d sdf
+  float* al = lo + S;              // [M] alpha
+  float* Tt = al + M;              // [M] T
+  float* w = Tt + M;               // [M] weights
+  float* wb = w + M;               // [M] weight adjoints
+  float* ld = wb + M;              // [M] depths
   auto is_in = [&](int k) { return k < S1 && inside[r * S1 + k] != 0; };
-  double T = 1.0, a_acc = 0.0, wd = 0.0;
-  for (int k = 0; k < M; ++k) {
+  for (int i = l; i < S; i += 64) {
+    const float v = sd[i];
+    ls[i] = v;
+    c[i] = sigmoidf_ref(fmul(v, s));
+  }
+  __syncthreads();
+  for (int k = l; k < M; k += 64) {
+    const float d0 = dk[k];
     float a;
-    if (k < S1) ain[k] = fmaxf(fdiv(fsub(c[k], c[k + 1]), fadd(c[k], 1e-10f)), 0.0f);
     if (is_in(k)) {
-      a = ain[k];
+      a = fmaxf(fdiv(fsub(c[k], c[k + 1]), fadd(c[k], 1e-10f)), 0.0f);
     } else {
-      const float dist = k + 1 < M ? fsub(dk[k + 1], dk[k]) : 1e10f;
+      const float dist = k + 1 < M ? fsub(dk[k + 1], d0) : 1e10f;
       a = fsub(1.0f, expf(fmul(-sp1(sig_o[r * M + k]), dist)));
     }
     al[k] = a;
-    Tt[k] = (float)T;
-    w[k] = fmul(a, (float)T);
-    T *= (double)fadd(fsub(1.0f, a), 1e-10f);
-    a_acc += (double)w[k];
+    ld[k] = d0;
   }
-  const float accf = (float)a_acc;
-  const double A = (double)fadd(accf, 1e-10f);
-  for (int k = 0; k < M; ++k) wd += (double)w[k] * (double)dk[k];
+  __syncthreads();
+  if (l == 0) {
+    double T = 1.0, a_acc = 0.0, wd = 0.0;
+    for (int k = 0; k < M; ++k) {
+      const float a = al[k];
+      Tt[k] = (float)T;
+      w[k] = fmul(a, (float)T);
+      T *= (double)fadd(fsub(1.0f, a), 1e-10f);
+      a_acc += (double)w[k];
+    }
+    const float accf = (float)a_acc;
+    ldb[0] = (double)fadd(accf, 1e-10f);
+    for (int k = 0; k < M; ++k) wd += (double)w[k] * (double)ld[k];
+    ldb[1] = wd;
+  }
+  __syncthreads();
+  const double A = ldb[0], wd = ldb[1];
   const float gr0 = g_rgb ? g_rgb[r * 3 + 0] : 0.f, gr1 = g_rgb ? g_rgb[r * 3 + 1] : 0.f,
               gr2 = g_rgb ? g_rgb[r * 3 + 2] : 0.f;
   const double gd = g_depth ? (double)g_depth[r] : 0.0;
   const double ga = (g_acc ? (double)g_acc[r] : 0.0) - (white_bkgd ? (double)gr0 + gr1 + gr2 : 0.0);
-  for (int k = 0; k < M; ++k) {
+  for (int k = l; k < M; k += 64) {
     const bool in = is_in(k);
     const float* col = in ? rad + (r * S1 + k) * 3 : rad_o + (r * M + k) * 3;
     double v = (double)gr0 * col[0] + (double)gr1 * col[1] + (double)gr2 * col[2] + ga;
-    v += gd * ((double)dk[k] / A - wd / (A * A));
+    v += gd * ((double)ld[k] / A - wd / (A * A));
     if (g_w) v += (double)g_w[r * M + k];
     wb[k] = (float)v;
     float* dro = d_rad_o + (r * M + k) * 3;
@@ -832,45 +871,51 @@ __global__ void neus_composite_bg_bwd_kernel(const float* __restrict__ sdf, cons
       dri[2] = in ? fmul(w[k], gr2) : 0.f;
     }
   }
-  double suffix = 0.0, sbar = 0.0;
-  float cbar_next = 0.0f;  // gradient reaching c_{k+1} from alpha_{k+1}'s c_i term
-  for (int k = M - 1; k >= 0; --k) {
-    const double u = (double)fadd(fsub(1.0f, al[k]), 1e-10f);
-    const double abar = (double)wb[k] * Tt[k] - suffix / u;
-    suffix += (double)wb[k] * al[k] * Tt[k];
+  __syncthreads();
+  if (l == 0) {
+    double suffix = 0.0, sbar = 0.0;
+    float cbar_next = 0.0f;  // gradient reaching c_{k+1} from alpha_{k+1}'s c_i term
+    for (int k = M - 1; k >= 0; --k) {
+      const double u = (double)fadd(fsub(1.0f, al[k]), 1e-10f);
+      const double abar = (double)wb[k] * Tt[k] - suffix / u;
+      suffix += (double)wb[k] * al[k] * Tt[k];
+      lab[k] = abar;
+      if (k < S1) {
+        double ci_bar = 0.0, cn_bar = 0.0;
+        if (is_in(k)) {
+          const float num = fsub(c[k], c[k + 1]), den = fadd(c[k], 1e-10f);
+          if (fdiv(num, den) >= 0.0f) {
+            ci_bar = abar / den - abar * num / ((double)den * den);
+            cn_bar = -abar / den;
+          }
+        }
+        const double cb_next = cn_bar + (double)cbar_next;
+        const float cc = c[k + 1];
+        const double sg = cb_next * cc * (1.0 - cc);
+        lo[k + 1] = (float)(sg * s);
+        sbar += sg * ls[k + 1];
+        cbar_next = (float)ci_bar;
+      }
+    }
+    const float cc = c[0];
+    const double sg = (double)cbar_next * cc * (1.0 - cc);
+    lo[0] = (float)(sg * s);
+    sbar += sg * ls[0];
+    d_s[r] = (float)sbar;
+  }
+  __syncthreads();
+  for (int k = l; k < M; k += 64) {
     if (is_in(k)) {
       d_sig[r * M + k] = 0.f;
     } else {
-      const float dist = k + 1 < M ? fsub(dk[k + 1], dk[k]) : 1e10f;
-      const float x = sig_o[r * M + k];
       // d alpha_out / d sigma = exp(-softplus(sigma) dist) dist softplus'(sigma)
+      const float dist = k + 1 < M ? fsub(ld[k + 1], ld[k]) : 1e10f;
+      const float x = sig_o[r * M + k];
       const double e = exp(-(double)sp1(x) * (double)dist);
-      d_sig[r * M + k] = (float)(abar * e * (double)dist * sp1_grad(x));
-    }
-    if (k < S1) {
-      double ci_bar = 0.0, cn_bar = 0.0;
-      if (is_in(k)) {
-        const float num = fsub(c[k], c[k + 1]), den = fadd(c[k], 1e-10f);
-        if (fdiv(num, den) >= 0.0f) {
-          ci_bar = abar / den - abar * num / ((double)den * den);
-          cn_bar = -abar / den;
-        }
-      }
-      const double cb_next = cn_bar + (double)cbar_next;
-      const float cc = c[k + 1];
-      const double sg = cb_next * cc * (1.0 - cc);
-      d_sdf[r * S + k + 1] = (float)(sg * s);
-      sbar += sg * sd[k + 1];
-      cbar_next = (float)ci_bar;
+      d_sig[r * M + k] = (float)(lab[k] * e * (double)dist * sp1_grad(x));
     }
   }
-  {
-    const float cc = c[0];
-    const double sg = (double)cbar_next * cc * (1.0 - cc);
-    d_sdf[r * S] = (float)(sg * s);
-    sbar += sg * sd[0];
-  }
-  d_s[r] = (float)sbar;
+  for (int i = l; i < S; i += 64) d_sdf[r * S + i] = lo[i];
 }
 
 // ---- UNISURF compositing with a graph (unisurf.py:219-236, get_opacity_from_surface :53-62) ------------
@@ -1176,9 +1221,10 @@ int nr_neus_composite_bg_fwd(const float* sdf, const float* s_dev, const float* 
                  R >= 0 && S >= 2 && M >= S - 1,
              NR_ERR_ARG, "nr_neus_composite_bg_fwd: bad argument");
   if (R == 0) return NR_OK;
-  hipLaunchKernelGGL(neus_composite_bg_fwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
-                     sdf, s_dev, rad, sigma_out, rad_out, d_out, inside, R, S, M, white_bkgd, rgb, depth, acc, weights,
-                     alpha, cdf);
+  const size_t lds = (size_t)(S + 6 * M) * sizeof(float);
+  NR_REQUIRE(lds <= 65536, NR_ERR_UNSUPPORTED, "nr_neus_composite_bg_fwd: S + M too large");
+  hipLaunchKernelGGL(neus_composite_bg_fwd_kernel, dim3((unsigned)R), dim3(64), lds, (hipStream_t)stream, sdf, s_dev,
+                     rad, sigma_out, rad_out, d_out, inside, R, S, M, white_bkgd, rgb, depth, acc, weights, alpha, cdf);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
@@ -1198,9 +1244,11 @@ int nr_neus_composite_bg_bwd(const float* sdf, const float* s_dev, const float* 
   if (R == 0) return NR_OK;
   NR_REQUIRE(workspace && workspace_bytes >= nr_neus_composite_bg_bwd_workspace_bytes(R, S, M), NR_ERR_WORKSPACE,
              "nr_neus_composite_bg_bwd: workspace too small");
-  hipLaunchKernelGGL(neus_composite_bg_bwd_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
-                     sdf, s_dev, rad, sigma_out, rad_out, d_out, inside, R, S, M, white_bkgd, g_rgb, g_depth, g_acc,
-                     g_weights, (float*)workspace, d_sdf, d_rad, d_sigma_out, d_rad_out, d_s);
+  const size_t lds = (size_t)(M + 2) * sizeof(double) + (size_t)(3 * S + 5 * M) * sizeof(float);
+  NR_REQUIRE(lds <= 65536, NR_ERR_UNSUPPORTED, "nr_neus_composite_bg_bwd: S + M too large");
+  hipLaunchKernelGGL(neus_composite_bg_bwd_kernel, dim3((unsigned)R), dim3(64), lds, (hipStream_t)stream, sdf, s_dev,
+                     rad, sigma_out, rad_out, d_out, inside, R, S, M, white_bkgd, g_rgb, g_depth, g_acc, g_weights,
+                     d_sdf, d_rad, d_sigma_out, d_rad_out, d_s);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
