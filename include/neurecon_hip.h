@@ -673,6 +673,25 @@ int nr_radiance_op_info(const NrRadDesc* d, int op, int64_t* offset, int* kb, in
 int nr_radiance_train_fwd32(const NrRadDesc* d, const void* packed, const float* feat, const float* small,
                             int64_t ld_small, int64_t P, float* h0, float* h1, float* h2, float* h3, float* rgb,
                             void* stream);
+/* NeRF++ background net in the training step (NeRF.forward with a graph, base.py:426-453), exact fp32
+ * products, replacing NeRFFn's hipBLASLt GEMMs (neurecon_amd/training.py):
+ *   nr_nerf_train_fwd32  `packed` = nr_nerf_pack for a desc with precision NR_PREC_FP32; x_emb [P][84]
+ *                        (16-byte aligned) and v_emb [P][27] from nr_nerf_train_input; outputs the 8 ReLU
+ *                        activations h[0..7] [P][256], the feature [P][256], the view branch's ReLU output
+ *                        hv [P][128], sigma [P] and rgb [P][3] in one launch
+ *   nr_nerf_train_pack   the backward's transposed fp32 ops (views^T, feature^T, W7^T .. W1^T) and the
+ *                        rgb / alpha rows; W / b as nr_nerf_pack's 12 layers (biases unused)
+ *   nr_nerf_train_bwd32  the data gradients in one launch: g3 = g_rgb * sigmoid' [P][3], ghv = (g3 Wr) *
+ *                        [hv > 0] [P][128], g_feat = Wv[:, :256]^T ghv [P][256], gz[7] = (Wf^T g_feat +
+ *                        g_sigma Wa) * [h7 > 0], gz[i-1] = (W_i^T gz[i])[h columns] * [h_{i-1} > 0]; g_rgb /
+ *                        g_sigma may be null (zero).  The weight gradients are nr_wgrad products of these. */
+int nr_nerf_train_fwd32(const NrNerfDesc* d, const void* packed, const float* x_emb, const float* v_emb, int64_t P,
+                        float* const* h, float* feat, float* hv, float* sigma, float* rgb, void* stream);
+size_t nr_nerf_train_packed_bytes(const NrNerfDesc* d);
+int nr_nerf_train_pack(const NrNerfDesc* d, const float* const* W, const float* const* b, void* packed, void* stream);
+int nr_nerf_train_bwd32(const NrNerfDesc* d, const void* train_packed, const float* rgb, const float* hv,
+                        const float* const* h, const float* g_rgb, const float* g_sigma, int64_t P, float* g3,
+                        float* ghv, float* g_feat, float* const* gz, void* stream);
 size_t nr_radiance_train_packed_bytes(const NrRadDesc* d);
 int nr_radiance_train_pack(const NrRadDesc* d, const float* const* W, const float* const* b, void* packed,
                            void* stream);

@@ -153,6 +153,12 @@ _SIGS = {
     'nr_nerf_packed_bytes': (_c_sz, [ctypes.POINTER(NrNerfDesc)]),
     'nr_nerf_pack': (_c_i, [ctypes.POINTER(NrNerfDesc), ctypes.POINTER(_c_p), ctypes.POINTER(_c_p), _c_p, _c_p]),
     'nr_nerf_forward': (_c_i, [ctypes.POINTER(NrNerfDesc), _c_p, _c_p, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_p]),
+    'nr_nerf_train_fwd32': (_c_i, [ctypes.POINTER(NrNerfDesc), _c_p, _c_p, _c_p, _c_i64, ctypes.POINTER(_c_p), _c_p,
+                                   _c_p, _c_p, _c_p, _c_p]),
+    'nr_nerf_train_packed_bytes': (_c_sz, [ctypes.POINTER(NrNerfDesc)]),
+    'nr_nerf_train_pack': (_c_i, [ctypes.POINTER(NrNerfDesc), ctypes.POINTER(_c_p), ctypes.POINTER(_c_p), _c_p, _c_p]),
+    'nr_nerf_train_bwd32': (_c_i, [ctypes.POINTER(NrNerfDesc), _c_p, _c_p, _c_p, ctypes.POINTER(_c_p), _c_p, _c_p,
+                                   _c_i64, _c_p, _c_p, _c_p, ctypes.POINTER(_c_p), _c_p]),
     'nr_neus_workspace_bytes': (_c_sz, [ctypes.POINTER(NrNeusArgs)]),
     'nr_neus_render': (_c_i, [ctypes.POINTER(NrNeusArgs), _c_p]),
     'nr_volsdf_workspace_bytes': (_c_sz, [ctypes.POINTER(NrVolsdfArgs)]),

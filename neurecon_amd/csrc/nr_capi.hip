@@ -937,6 +937,91 @@ int nr_radiance_train_fwd32(const NrRadDesc* d, const void* packed, const float*
   return launch_radiance_train32(L, packed, feat, small, ld_small, L.n_small, P, h, rgb, (hipStream_t)stream);
 }
 
+// ---- NeRF++ net in the training step (nr_mlp.hip nerf_train32_*_kernel) ---------------------------
+static NerfBwdLayout nerf_bwd_layout() {
+  NerfBwdLayout B{};
+  size_t off = 0;
+  for (int i = 0; i < kNerfBwdOps; ++i) {
+    B.op_bytes[i] = (2 * (i == NBV ? 8 : 16) + 1) * 1024;
+    B.op_off[i] = (uint32_t)off;
+    off += 8 * (size_t)B.op_bytes[i];  // 16 output blocks = 8 chunks
+  }
+  B.scale_off = (uint32_t)off;
+  off = align256(off + kNerfBwdOps * 4);
+  B.wr_off = (uint32_t)off;
+  off = align256(off + 3 * 128 * 4);
+  B.wa_off = (uint32_t)off;
+  off = align256(off + 256 * 4);
+  B.total = (uint32_t)off;
+  return B;
+}
+
+size_t nr_nerf_train_packed_bytes(const NrNerfDesc* d) {
+  if (check_nerf_desc(d)) return 0;
+  return nerf_bwd_layout().total;
+}
+
+int nr_nerf_train_pack(const NrNerfDesc* d, const float* const* W, const float* const* b, void* packed, void* stream) {
+  int rc = check_nerf_desc(d);
+  if (rc) return rc;
+  NR_REQUIRE(W && b && packed, NR_ERR_ARG, "nr_nerf_train_pack: null argument");
+  for (int l = 0; l < 12; ++l) NR_REQUIRE(W[l], NR_ERR_ARG, "nr_nerf_train_pack: null layer pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const NerfBwdLayout B = nerf_bwd_layout();
+  char* P = (char*)packed;
+  float* wmax = (float*)(P + B.scale_off);
+  const int prec = NR_PREC_FP32, in0 = 84, inv = 27;
+  PackOp ops[kNerfBwdOps];
+  // views_linears[0]^T restricted to the feature columns: [128][256 + 27] -> out 256 (feature), in 128
+  ops[NBV] = mkop(W[9], nullptr, 128, 256 + inv, 1, seg(16, 0, 256), none(), seg(8, 0, 128), none(), 1.0f, prec,
+                  wmax + NBV);
+  ops[NBF] = mkop(W[8], nullptr, 256, 256, 1, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec,
+                  wmax + NBF);
+  for (int i = 7; i >= 1; --i) {
+    const int o = NB7 + (7 - i);
+    if (i == 5)  // input cat([x_emb(84), h4(256)]): the h4 columns 84..339
+      ops[o] = mkop(W[5], nullptr, 256, 256 + in0, 1, seg(16, in0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec,
+                    wmax + o);
+    else
+      ops[o] = mkop(W[i], nullptr, 256, 256, 1, seg(16, 0, 256), none(), seg(16, 0, 256), none(), 1.0f, prec, wmax + o);
+  }
+  char* dst[kNerfBwdOps];
+  for (int i = 0; i < kNerfBwdOps; ++i) dst[i] = P + B.op_off[i];
+  if ((rc = launch_pack_ops(ops, dst, kNerfBwdOps, st))) return rc;
+  if ((rc = launch_pack_vec(W[11], 0, 384, 384, P + B.wr_off, st))) return rc;
+  if ((rc = launch_pack_vec(W[10], 0, 256, 256, P + B.wa_off, st))) return rc;
+  return NR_OK;
+}
+
+int nr_nerf_train_fwd32(const NrNerfDesc* d, const void* packed, const float* x_emb, const float* v_emb, int64_t P,
+                        float* const* h, float* feat, float* hv, float* sigma, float* rgb, void* stream) {
+  int rc = check_nerf_desc(d);
+  if (rc) return rc;
+  NR_REQUIRE(d->precision == NR_PREC_FP32, NR_ERR_ARG, "nr_nerf_train_fwd32: the desc / pack must be NR_PREC_FP32");
+  NR_REQUIRE(P >= 0, NR_ERR_ARG, "nr_nerf_train_fwd32: negative P");
+  if (P == 0) return NR_OK;
+  NR_REQUIRE(packed && x_emb && v_emb && h && feat && hv && sigma && rgb, NR_ERR_ARG,
+             "nr_nerf_train_fwd32: null argument");
+  for (int i = 0; i < 8; ++i) NR_REQUIRE(h[i], NR_ERR_ARG, "nr_nerf_train_fwd32: null activation pointer");
+  NR_REQUIRE(((uintptr_t)x_emb & 15) == 0, NR_ERR_ARG, "nr_nerf_train_fwd32: x_emb must be 16-byte aligned");
+  return launch_nerf_train32_fwd(nerf_layout(*d), packed, x_emb, v_emb, P, h, feat, hv, sigma, rgb,
+                                 (hipStream_t)stream);
+}
+
+int nr_nerf_train_bwd32(const NrNerfDesc* d, const void* train_packed, const float* rgb, const float* hv,
+                        const float* const* h, const float* g_rgb, const float* g_sigma, int64_t P, float* g3,
+                        float* ghv, float* g_feat, float* const* gz, void* stream) {
+  int rc = check_nerf_desc(d);
+  if (rc) return rc;
+  NR_REQUIRE(P >= 0, NR_ERR_ARG, "nr_nerf_train_bwd32: negative P");
+  if (P == 0) return NR_OK;
+  NR_REQUIRE(train_packed && rgb && hv && h && g3 && ghv && g_feat && gz, NR_ERR_ARG,
+             "nr_nerf_train_bwd32: null argument");
+  for (int i = 0; i < 8; ++i) NR_REQUIRE(h[i] && gz[i], NR_ERR_ARG, "nr_nerf_train_bwd32: null layer pointer");
+  return launch_nerf_train32_bwd(nerf_bwd_layout(), train_packed, rgb, hv, h, g_rgb, g_sigma, P, g3, ghv, g_feat, gz,
+                                 (hipStream_t)stream);
+}
+
 // ---- training layer GEMMs (nr_mlp.hip tgemm_kernel) ---------------------------------------------
 int nr_train_gemm(const NrTrainGemm* a, int KB, int KB2, int NBO, int NB2, void* stream) {
   NR_REQUIRE(a, NR_ERR_ARG, "nr_train_gemm: null argument");

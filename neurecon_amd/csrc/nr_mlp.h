@@ -90,6 +90,20 @@ struct NerfLayout {
   int prec;
 };
 
+// NeRF++ training pack (nr_nerf_train_pack, fp32): the transposed ops of the backward data gradients,
+// chained by nerf_train32_bwd_kernel: views (Wv[:, :256]^T: 128 -> 256), feature (Wf^T), then W7^T ..
+// W1^T (W5^T restricted to its h columns 84..339); Wr [3][128] and Wa [256] for the VALU heads
+enum NerfBwdOp { NBV, NBF, NB7, NB6, NB5, NB4, NB3, NB2, NB1, kNerfBwdOps };
+
+struct NerfBwdLayout {
+  uint32_t op_off[kNerfBwdOps];
+  uint32_t op_bytes[kNerfBwdOps];
+  uint32_t scale_off;  // [kNerfBwdOps] max |W| per op (written by the pack scan)
+  uint32_t wr_off;     // [3][128] rgb_linear weights
+  uint32_t wa_off;     // [256] alpha_linear weights
+  uint32_t total;
+};
+
 struct PackSeg {
   int nblk;    // 16-feature blocks
   int off;     // first source index
@@ -136,6 +150,13 @@ int launch_radiance(const RadLayout& L, const void* packed, const float* x, cons
 // training forward of a ReLU D=4 radiance net on its fp32 pack: h[0..3] [P][256], rgb [P][3]
 int launch_radiance_train32(const RadLayout& L, const void* packed, const float* feat, const float* small,
                             int64_t ld_small, int n_small, int64_t P, float* const* h, float* rgb, hipStream_t stream);
+// NeRF++ training forward on the fp32 render pack (xe [P][84], ve [P][27] -> h[0..7] [P][256], feat
+// [P][256], hv [P][128], sigma [P], rgb [P][3]) and the data gradients on the training pack
+int launch_nerf_train32_fwd(const NerfLayout& L, const void* packed, const float* xe, const float* ve, int64_t P,
+                            float* const* h, float* feat, float* hv, float* sigma, float* rgb, hipStream_t stream);
+int launch_nerf_train32_bwd(const NerfBwdLayout& B, const void* packed, const float* rgb, const float* hv,
+                            const float* const* h, const float* g_rgb, const float* g_sigma, int64_t P, float* g3,
+                            float* ghv, float* g_feat, float* const* gz, hipStream_t stream);
 SdfLayout sdf_layout(const NrSdfDesc& d);
 RadLayout rad_layout(const NrRadDesc& d);
 int check_sdf_desc(const NrSdfDesc* d);

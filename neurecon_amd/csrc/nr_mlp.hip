@@ -2605,6 +2605,245 @@ __global__ __launch_bounds__(kThreads) void nerf_kernel(NerfKArgs a) {
 }
 
 // =============================================================================================
+// NeRF++ background net in the training step (NeRFFn, models/base.py:426-453 with a graph), exact fp32
+// products on v_mfma_f32_16x16x4_f32, the layer chain in registers (nerf_kernel<FP32>'s structure):
+// * nerf_train32_fwd_kernel, over the fp32 render pack (nerf_layout): the embedded inputs read from the
+//   training tensors (x_emb [P,84], v_emb [P,27], nr_nerf_train_input), every tensor the backward needs
+//   stored -- the 8 ReLU outputs h_i [P,256], the feature [P,256], the view branch's ReLU output hv
+//   [P,128] -- plus sigma [P] and rgb [P,3].  The ReLU decisions come from fp32 pre-activations, as the
+//   reference's (the radiance net's note).
+// * nerf_train32_bwd_kernel, over the training pack (nerf_bwd_layout: transposed ops): the data
+//   gradients in one launch -- g3 = g_rgb sigmoid'(rgb) [P,3]; ghv = (g3 Wr) [hv > 0] [P,128];
+//   g_feat = Wv[:, :256]^T ghv [P,256] (the view embedding takes no gradient); gz7 = (Wf^T g_feat +
+//   g_sigma Wa) [h7 > 0]; gz_{i-1} = (W_i^T gz_i) [h_{i-1} > 0] for i = 7..1, W5^T restricted to the
+//   h columns 84..339 of its input cat([x_emb, h4]) (base.py:431-432).  Each gz is stored for the
+//   weight gradients (nr_wgrad).
+// One launch each replaces 12 hipBLASLt GEMMs + 3 activation launches (forward) and 11 GEMMs + 10
+// activation launches (backward).
+// =============================================================================================
+struct NerfTrainFwdArgs {
+  const char* packed;
+  NerfLayout L;
+  const float* xe;  // [P][84]
+  const float* ve;  // [P][27]
+  int64_t P;
+  float* h[8];      // [P][256]
+  float* feat;      // [P][256]
+  float* hv;        // [P][128]
+  float* sigma;     // [P]
+  float* rgb;       // [P][3]
+};
+
+__global__ __launch_bounds__(kThreads) void nerf_train32_fwd_kernel(NerfTrainFwdArgs a) {
+  constexpr int CB = chunk_bytes(22);  // N5: 16 + 6 input blocks
+  __shared__ __attribute__((aligned(16))) char smem[kRing * CB];
+  WStream<CB> ws{smem, nullptr, 0, 0, 0};
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  const NerfLayout& L = a.L;
+  const char* W = a.packed;
+  auto OP = [&](int i) { return W + L.op_off[i]; };
+  auto OPB = [&](int i) { return (int)L.op_bytes[i]; };
+  const float* wa = (const float*)(W + L.alpha_off);
+  const float* wr = (const float*)(W + L.rgb_off);
+  constexpr int F32 = NR_PREC_FP32;
+
+  ws.start(OP(N0), OPB(N0), OP(N0) + OPB(N0), OPB(N0));
+  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < a.P; base += (int64_t)gridDim.x * kPointsPerWG) {
+    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < a.P;
+    const int64_t p = base + wave * kTile + j;
+    const bool valid = p < a.P;
+    const int64_t pc = valid ? p : a.P - 1;
+    float4 E[6], V[2];
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {  // 84 = 21 float4s: feature f < 84 covers f .. f + 3
+      const int f = 16 * b + 4 * g;
+      E[b] = f < 84 ? *(const float4*)(a.xe + pc * 84 + f) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int f = 16 * b + 4 * g;
+      const float* v = a.ve + pc * 27;
+      V[b] = make_float4(f + 0 < 27 ? v[f + 0] : 0.f, f + 1 < 27 ? v[f + 1] : 0.f, f + 2 < 27 ? v[f + 2] : 0.f,
+                         f + 3 < 27 ? v[f + 3] : 0.f);
+    }
+    auto store = [&](float* dst, const float4 (&H)[16]) {  // [P][256] row p
+      if (!valid) return;
+      float* h = dst + p * 256 + 4 * g;
+#pragma unroll
+      for (int b = 0; b < 16; ++b) *(float4*)(h + 16 * b) = H[b];
+    };
+    float4 X[16], Y[16];
+    gemm_fwd<F32, 0, 6, 16, ACT_RELU>(ws, OP(N0), OP(N1), OPB(N1), X, E, Y, nullptr, nullptr, false, lane);
+    store(a.h[0], Y);
+    gemm_fwd<F32, 16, 0, 16, ACT_RELU>(ws, OP(N1), OP(N2), OPB(N2), Y, E, X, nullptr, nullptr, false, lane);
+    store(a.h[1], X);
+    gemm_fwd<F32, 16, 0, 16, ACT_RELU>(ws, OP(N2), OP(N3), OPB(N3), X, E, Y, nullptr, nullptr, false, lane);
+    store(a.h[2], Y);
+    gemm_fwd<F32, 16, 0, 16, ACT_RELU>(ws, OP(N3), OP(N4), OPB(N4), Y, E, X, nullptr, nullptr, false, lane);
+    store(a.h[3], X);
+    gemm_fwd<F32, 16, 0, 16, ACT_RELU>(ws, OP(N4), OP(N5), OPB(N5), X, E, Y, nullptr, nullptr, false, lane);
+    store(a.h[4], Y);
+    // skip: cat([input_pts, h]) (base.py:431-432); K blocks packed as [h ; embedding]
+    gemm_fwd<F32, 16, 6, 16, ACT_RELU>(ws, OP(N5), OP(N6), OPB(N6), Y, E, X, nullptr, nullptr, false, lane);
+    store(a.h[5], X);
+    gemm_fwd<F32, 16, 0, 16, ACT_RELU>(ws, OP(N6), OP(N7), OPB(N7), X, E, Y, nullptr, nullptr, false, lane);
+    store(a.h[6], Y);
+    gemm_fwd<F32, 16, 0, 16, ACT_RELU>(ws, OP(N7), OP(NF), OPB(NF), Y, E, X, nullptr, nullptr, false, lane);
+    store(a.h[7], X);
+    float part = 0.f;  // sigma = alpha_linear(h7)
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const float4 w = *(const float4*)(wa + 16 * b + 4 * g);
+      part = fmaf(X[b].x, w.x, part);
+      part = fmaf(X[b].y, w.y, part);
+      part = fmaf(X[b].z, w.z, part);
+      part = fmaf(X[b].w, w.w, part);
+    }
+    const float sigma = wave_sum4(part) + wa[256];
+    // feature = feature_linear(h7), stored by the op's drain; hv = relu(views_linears[0](cat([feature, v])))
+    gemm_fwd<F32, 16, 0, 16, ACT_NONE>(ws, OP(NF), OP(NV), OPB(NV), X, E, Y, nullptr, a.feat + p * 256, valid, lane);
+    gemm_fwd<F32, 16, 2, 8, ACT_RELU>(ws, OP(NV), has_next ? OP(N0) : nullptr, OPB(N0), Y, V, X, nullptr, nullptr,
+                                      false, lane);
+    if (valid) {
+      float* hv = a.hv + p * 128 + 4 * g;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) *(float4*)(hv + 16 * b) = X[b];
+    }
+    float r[3];
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      float q = 0.f;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const float4 w = *(const float4*)(wr + o * 128 + 16 * b + 4 * g);
+        q = fmaf(X[b].x, w.x, q);
+        q = fmaf(X[b].y, w.y, q);
+        q = fmaf(X[b].z, w.z, q);
+        q = fmaf(X[b].w, w.w, q);
+      }
+      r[o] = sigmoidf_ref(wave_sum4(q) + wr[3 * 128 + o]);
+    }
+    if (valid && g == 0) {
+      a.sigma[p] = sigma;
+      a.rgb[p * 3 + 0] = r[0];
+      a.rgb[p * 3 + 1] = r[1];
+      a.rgb[p * 3 + 2] = r[2];
+    }
+  }
+  wait_vmcnt(0);
+}
+
+struct NerfTrainBwdArgs {
+  const char* packed;
+  NerfBwdLayout B;
+  const float* rgb;      // [P][3]
+  const float* hv;       // [P][128]
+  const float* h[8];     // [P][256]
+  const float* g_rgb;    // [P][3] or null (zero)
+  const float* g_sigma;  // [P] or null (zero)
+  int64_t P;
+  float* g3;             // [P][3]
+  float* ghv;            // [P][128]
+  float* g_feat;         // [P][256]
+  float* gz[8];          // [P][256]
+};
+
+__global__ __launch_bounds__(kThreads) void nerf_train32_bwd_kernel(NerfTrainBwdArgs a) {
+  constexpr int CB = chunk_bytes(16);
+  __shared__ __attribute__((aligned(16))) char smem[kRing * CB];
+  WStream<CB> ws{smem, nullptr, 0, 0, 0};
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  const NerfBwdLayout& L = a.B;
+  const char* W = a.packed;
+  auto OP = [&](int i) { return W + L.op_off[i]; };
+  auto OPB = [&](int i) { return (int)L.op_bytes[i]; };
+  const float* wr = (const float*)(W + L.wr_off);  // [3][128]
+  const float* wa = (const float*)(W + L.wa_off);  // [256]
+  constexpr int F32 = NR_PREC_FP32;
+  const float4 E0[1] = {make_float4(0.f, 0.f, 0.f, 0.f)};  // no second input segment
+
+  ws.start(OP(NBV), OPB(NBV), OP(NBV) + OPB(NBV), OPB(NBV));
+  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < a.P; base += (int64_t)gridDim.x * kPointsPerWG) {
+    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < a.P;
+    const int64_t p = base + wave * kTile + j;
+    const bool valid = p < a.P;
+    const int64_t pc = valid ? p : a.P - 1;
+    // rgb = sigmoid(y): g3 = g_rgb y (1 - y) (act_kernel mode 3's arithmetic)
+    float g3[3];
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      const float y = a.rgb[pc * 3 + o];
+      const float gy = a.g_rgb ? a.g_rgb[pc * 3 + o] : 0.0f;
+      g3[o] = fmul(gy, fmul(y, fsub(1.0f, y)));
+    }
+    if (valid && g == 0) {
+      a.g3[p * 3 + 0] = g3[0];
+      a.g3[p * 3 + 1] = g3[1];
+      a.g3[p * 3 + 2] = g3[2];
+    }
+    const float gs = a.g_sigma ? a.g_sigma[pc] : 0.0f;
+    float4 X[16], Y[16];
+    // ghv = (g3 Wr) where hv > 0 (views_linears' ReLU)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int f = 16 * b + 4 * g;
+      const float4 w0 = *(const float4*)(wr + f), w1 = *(const float4*)(wr + 128 + f),
+                   w2 = *(const float4*)(wr + 256 + f);
+      const float4 m = *(const float4*)(a.hv + pc * 128 + f);
+      float4 v;
+      v.x = m.x > 0.0f ? fmaf(g3[2], w2.x, fmaf(g3[1], w1.x, g3[0] * w0.x)) : 0.0f;
+      v.y = m.y > 0.0f ? fmaf(g3[2], w2.y, fmaf(g3[1], w1.y, g3[0] * w0.y)) : 0.0f;
+      v.z = m.z > 0.0f ? fmaf(g3[2], w2.z, fmaf(g3[1], w1.z, g3[0] * w0.z)) : 0.0f;
+      v.w = m.w > 0.0f ? fmaf(g3[2], w2.w, fmaf(g3[1], w1.w, g3[0] * w0.w)) : 0.0f;
+      X[b] = v;
+      if (valid) *(float4*)(a.ghv + p * 128 + f) = v;
+    }
+#pragma unroll
+    for (int b = 8; b < 16; ++b) X[b] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // (W_i^T gz)[h part] masked by h_{i-1} > 0, stored as gz_{i-1}
+    auto mask_store = [&](float4 (&H)[16], const float* hprev, float* gz) {
+#pragma unroll
+      for (int b = 0; b < 16; ++b) {
+        const int f = 16 * b + 4 * g;
+        const float4 m = *(const float4*)(hprev + pc * 256 + f);
+        H[b] = make_float4(m.x > 0.0f ? H[b].x : 0.0f, m.y > 0.0f ? H[b].y : 0.0f, m.z > 0.0f ? H[b].z : 0.0f,
+                           m.w > 0.0f ? H[b].w : 0.0f);
+        if (valid) *(float4*)(gz + p * 256 + f) = H[b];
+      }
+    };
+    // g_feat = Wv[:, :256]^T ghv, stored by the op's drain
+    gemm_fwd<F32, 8, 0, 16, ACT_NONE>(ws, OP(NBV), OP(NBF), OPB(NBF), X, E0, Y, nullptr, a.g_feat + p * 256, valid,
+                                      lane);
+    // gz7 = (Wf^T g_feat + g_sigma Wa) where h7 > 0
+    gemm_fwd<F32, 16, 0, 16, ACT_NONE>(ws, OP(NBF), OP(NB7), OPB(NB7), Y, E0, X, nullptr, nullptr, false, lane);
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const float4 w = *(const float4*)(wa + 16 * b + 4 * g);
+      X[b] = make_float4(fmaf(gs, w.x, X[b].x), fmaf(gs, w.y, X[b].y), fmaf(gs, w.z, X[b].z), fmaf(gs, w.w, X[b].w));
+    }
+    mask_store(X, a.h[7], a.gz[7]);
+    gemm_fwd<F32, 16, 0, 16, ACT_NONE>(ws, OP(NB7), OP(NB6), OPB(NB6), X, E0, Y, nullptr, nullptr, false, lane);
+    mask_store(Y, a.h[6], a.gz[6]);
+    gemm_fwd<F32, 16, 0, 16, ACT_NONE>(ws, OP(NB6), OP(NB5), OPB(NB5), Y, E0, X, nullptr, nullptr, false, lane);
+    mask_store(X, a.h[5], a.gz[5]);
+    gemm_fwd<F32, 16, 0, 16, ACT_NONE>(ws, OP(NB5), OP(NB4), OPB(NB4), X, E0, Y, nullptr, nullptr, false, lane);
+    mask_store(Y, a.h[4], a.gz[4]);
+    gemm_fwd<F32, 16, 0, 16, ACT_NONE>(ws, OP(NB4), OP(NB3), OPB(NB3), Y, E0, X, nullptr, nullptr, false, lane);
+    mask_store(X, a.h[3], a.gz[3]);
+    gemm_fwd<F32, 16, 0, 16, ACT_NONE>(ws, OP(NB3), OP(NB2), OPB(NB2), X, E0, Y, nullptr, nullptr, false, lane);
+    mask_store(Y, a.h[2], a.gz[2]);
+    gemm_fwd<F32, 16, 0, 16, ACT_NONE>(ws, OP(NB2), OP(NB1), OPB(NB1), Y, E0, X, nullptr, nullptr, false, lane);
+    mask_store(X, a.h[1], a.gz[1]);
+    gemm_fwd<F32, 16, 0, 16, ACT_NONE>(ws, OP(NB1), has_next ? OP(NBV) : nullptr, OPB(NBV), X, E0, Y, nullptr, nullptr,
+                                       false, lane);
+    mask_store(Y, a.h[0], a.gz[0]);
+  }
+  wait_vmcnt(0);
+}
+
+// =============================================================================================
 // NeRF++ background net on the v3 pipeline (nerf4_kernel, f16x3): the rad4 / sdf4 structure
 // (128-point tile, kNC-column waves, weight ring by LDS-DMA two chunks ahead, per-chunk operand split
 // at a scale fixed from the op's pack-time bound, epilogues staged beside the next chunk's MFMAs) on
@@ -3480,6 +3719,50 @@ int launch_nerf(const NerfLayout& L, const void* packed, const float* x4, const 
   ProfScope prof("nerf", (double)P, stream, P_dev, 1);
   if (L.prec == NR_PREC_F16X3) hipLaunchKernelGGL(nerf4_kernel, dim3(grid), dim3(kT4), 0, stream, a);  // v3 pipeline
   else hipLaunchKernelGGL((nerf_kernel<NR_PREC_FP32>), dim3(grid), dim3(kThreads), 0, stream, a);
+  NR_HIP_CHECK(hipGetLastError());
+  return NR_OK;
+}
+
+int launch_nerf_train32_fwd(const NerfLayout& L, const void* packed, const float* xe, const float* ve, int64_t P,
+                            float* const* h, float* feat, float* hv, float* sigma, float* rgb, hipStream_t stream) {
+  if (P <= 0) return NR_OK;
+  NR_REQUIRE(L.prec == NR_PREC_FP32, NR_ERR_ARG, "nerf train forward: needs the fp32 render pack");
+  NerfTrainFwdArgs a{};
+  a.packed = (const char*)packed;
+  a.L = L;
+  a.xe = xe;
+  a.ve = ve;
+  a.P = P;
+  for (int i = 0; i < 8; ++i) a.h[i] = h[i];
+  a.feat = feat;
+  a.hv = hv;
+  a.sigma = sigma;
+  a.rgb = rgb;
+  ProfScope prof("nerf_train32_fwd", (double)P, stream);
+  hipLaunchKernelGGL(nerf_train32_fwd_kernel, dim3(grid_for(P)), dim3(kThreads), 0, stream, a);
+  NR_HIP_CHECK(hipGetLastError());
+  return NR_OK;
+}
+
+int launch_nerf_train32_bwd(const NerfBwdLayout& B, const void* packed, const float* rgb, const float* hv,
+                            const float* const* h, const float* g_rgb, const float* g_sigma, int64_t P, float* g3,
+                            float* ghv, float* g_feat, float* const* gz, hipStream_t stream) {
+  if (P <= 0) return NR_OK;
+  NerfTrainBwdArgs a{};
+  a.packed = (const char*)packed;
+  a.B = B;
+  a.rgb = rgb;
+  a.hv = hv;
+  for (int i = 0; i < 8; ++i) a.h[i] = h[i];
+  a.g_rgb = g_rgb;
+  a.g_sigma = g_sigma;
+  a.P = P;
+  a.g3 = g3;
+  a.ghv = ghv;
+  a.g_feat = g_feat;
+  for (int i = 0; i < 8; ++i) a.gz[i] = gz[i];
+  ProfScope prof("nerf_train32_bwd", (double)P, stream);
+  hipLaunchKernelGGL(nerf_train32_bwd_kernel, dim3(grid_for(P)), dim3(kThreads), 0, stream, a);
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;
 }

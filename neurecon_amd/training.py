@@ -348,73 +348,103 @@ class NeuSComposite(torch.autograd.Function):
         return d_sdf, d_s.sum().reshape(1), d_rad, None, None
 
 
+def _nerf_packs(net, Ws, bs, device):
+    """(fp32 desc, the fp32 render pack, the training pack) of a NeRF++ net built from the step's
+    weights (12 layers: pts_linears 0..7, feature, views, alpha, rgb), cached per parameter version"""
+    from .base import _version_key, _ptr_array
+    key = _version_key(net, 'nerf_train32', device)
+    c = getattr(net, '_nr_train32_cache', None)
+    if c is not None and c[0] == key:
+        return c[1], c[2], c[3]
+    lib = L.lib()
+    desc = net.nr_desc()
+    desc.precision = L.PREC_FP32
+    W = [w.detach().float().contiguous() for w in Ws]
+    b = [x.detach().float().contiguous() for x in bs]
+    pk = torch.empty(lib.nr_nerf_packed_bytes(ctypes.byref(desc)), dtype=torch.uint8, device=device)
+    L.check(lib.nr_nerf_pack(ctypes.byref(desc), _ptr_array(W), _ptr_array(b), L.ptr(pk), L.stream_of(device)))
+    tp = torch.empty(lib.nr_nerf_train_packed_bytes(ctypes.byref(desc)), dtype=torch.uint8, device=device)
+    L.check(lib.nr_nerf_train_pack(ctypes.byref(desc), _ptr_array(W), _ptr_array(b), L.ptr(tp), L.stream_of(device)))
+    net._nr_train32_cache = (key, desc, pk, tp, W, b)
+    return desc, pk, tp
+
+
+def _ptrs(ts):
+    return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+
 class NeRFFn(torch.autograd.Function):
     """NeRF.forward (base.py:426-453, NeRF++ background: 8 x ReLU(256) with cat([input, h]) after the
     skip layer, alpha / feature heads, views Linear(256+27 -> 128) + ReLU, rgb Linear + sigmoid) with a
-    graph: GEMMs on hipBLASLt (torch.addmm), activations in libnrhip.  Inputs are the embedded points
-    x_emb [P,84] and views v_emb [P,27] (no gradient: they depend on the rays and the no-grad depths).
-    Returns sigma [P], rgb [P,3]; gradients reach every parameter."""
+    graph.  Inputs are the embedded points x_emb [P,84] and views v_emb [P,27] (no gradient: they depend
+    on the rays and the no-grad depths).  Returns sigma [P], rgb [P,3]; gradients reach every parameter.
+    r05: the forward is one launch of nr_nerf_train_fwd32 (exact fp32 products, the layers chained in
+    registers, every activation the backward needs stored) and the backward's data gradients one launch
+    of nr_nerf_train_bwd32 (the transposed fp32 ops chained, each layer's ReLU mask applied and its
+    pre-activation gradient stored), in place of 23 hipBLASLt GEMMs and 13 activation launches; the
+    weight gradients are nr_wgrad products (exact fp32 for fp32 nets, f16x3 otherwise), the skip
+    layer's and the views layer's per input column block (no [P, 340] / [P, 283] concatenations)."""
 
     @staticmethod
-    def forward(ctx, xe, ve, cfg, *params):
-        D, skips, ctx.fp32 = cfg
-        Ws, bs = params[:D], params[D:2 * D]
-        Wa, ba, Wf, bf, Wv, bv, Wr, br = params[2 * D:]
-        st = _st(xe)
-        lib = L.lib()
-        ins, outs = [], []
-        h = xe
-        for i in range(D):
-            ins.append(h)
-            z = torch.addmm(bs[i], h, Ws[i].t())
-            L.check(lib.nr_activation(L.ptr(z), None, z.numel(), 0, st))
-            outs.append(z)
-            h = torch.cat([xe, z], -1) if i in skips else z
-        sigma = torch.addmm(ba, h, Wa.t())
-        feat = torch.addmm(bf, h, Wf.t())
-        hv_in = torch.cat([feat, ve], -1)
-        hv = torch.addmm(bv, hv_in, Wv.t())
-        L.check(lib.nr_activation(L.ptr(hv), None, hv.numel(), 0, st))
-        rgb = torch.addmm(br, hv, Wr.t())
-        L.check(lib.nr_activation(L.ptr(rgb), None, rgb.numel(), 2, st))
-        ctx.cfg = (D, tuple(skips), xe.shape[1])
-        ctx.save_for_backward(rgb, hv, hv_in, h, *ins, *outs, *params)
-        return sigma[:, 0], rgb
+    def forward(ctx, xe, ve, net, *params):
+        Ws, bs = params[:12], params[12:]
+        dev = xe.device
+        P = xe.shape[0]
+        xe, ve = xe.contiguous(), ve.contiguous()
+        desc, pk, _ = _nerf_packs(net, Ws, bs, dev)
+        H = [torch.empty(P, 256, device=dev) for _ in range(8)]
+        feat = torch.empty(P, 256, device=dev)
+        hv = torch.empty(P, 128, device=dev)
+        sigma = torch.empty(P, device=dev)
+        rgb = torch.empty(P, 3, device=dev)
+        L.check(L.lib().nr_nerf_train_fwd32(ctypes.byref(desc), L.ptr(pk), L.ptr(xe), L.ptr(ve), P, _ptrs(H),
+                                            L.ptr(feat), L.ptr(hv), L.ptr(sigma), L.ptr(rgb), _st(xe)))
+        ctx.net = net
+        ctx.fp32 = getattr(net, 'precision', 'fp32') == 'fp32'
+        ctx.save_for_backward(xe, ve, rgb, hv, feat, *H, *params)
+        return sigma, rgb
 
     @staticmethod
     def backward(ctx, g_sigma, g_rgb):
-        D, skips, nx = ctx.cfg
         saved = ctx.saved_tensors
-        rgb, hv, hv_in, h = saved[:4]
-        ins, outs = saved[4:4 + D], saved[4 + D:4 + 2 * D]
-        params = saved[4 + 2 * D:]
-        Ws = params[:D]
-        Wa, ba, Wf, bf, Wv, bv, Wr, br = params[2 * D:]
-        st = _st(rgb)
-        lib = L.lib()
+        xe, ve, rgb, hv, feat = saved[:5]
+        H = saved[5:13]
+        params = saved[13:]
+        Ws, bs = params[:12], params[12:]
+        dev = rgb.device
         P = rgb.shape[0]
-        g = torch.zeros_like(rgb) if g_rgb is None else g_rgb.contiguous().clone()
-        L.check(lib.nr_activation(L.ptr(rgb), L.ptr(g), g.numel(), 3, st))          # sigmoid'
+        nx = xe.shape[1]
+        desc, _, tp = _nerf_packs(ctx.net, Ws, bs, dev)
+        g3 = torch.empty(P, 3, device=dev)
+        ghv = torch.empty(P, 128, device=dev)
+        g_feat = torch.empty(P, 256, device=dev)
+        GZ = [torch.empty(P, 256, device=dev) for _ in range(8)]
+        g_rgb = None if g_rgb is None else g_rgb.contiguous()
+        gs = torch.zeros(P, device=dev) if g_sigma is None else g_sigma.reshape(P).contiguous()
+        L.check(L.lib().nr_nerf_train_bwd32(ctypes.byref(desc), L.ptr(tp), L.ptr(rgb), L.ptr(hv), _ptrs(H),
+                                            None if g_rgb is None else L.ptr(g_rgb), L.ptr(gs), P, L.ptr(g3),
+                                            L.ptr(ghv), L.ptr(g_feat), _ptrs(GZ), _st(rgb)))
         f32 = ctx.fp32  # weight gradients on nr_wgrad: exact fp32 products (fp32 nets) or f16x3
-        dWr, dbr = _wgb(g, hv, f32)
-        ghv = g @ Wr
-        L.check(lib.nr_activation(L.ptr(hv), L.ptr(ghv), ghv.numel(), 1, st))      # ReLU'
-        dWv, dbv = _wgb(ghv, hv_in, f32)
-        g_feat = (ghv @ Wv)[:, :Wf.shape[0]].contiguous()                           # views: no gradient
-        dWf, dbf = _wgb(g_feat, h, f32)
-        gh = g_feat @ Wf
-        gs = (torch.zeros(P, 1, device=rgb.device) if g_sigma is None else g_sigma.reshape(P, 1).contiguous())
-        dWa, dba = _wgb(gs, h, f32)
-        gh = torch.addmm(gh, gs, Wa)
-        dW, db = [None] * D, [None] * D
-        for i in range(D - 1, -1, -1):
-            gz = gh.contiguous()
-            L.check(lib.nr_activation(L.ptr(outs[i]), L.ptr(gz), gz.numel(), 1, st))  # ReLU'
-            dW[i], db[i] = _wgb(gz, ins[i], f32)
-            if i > 0:
-                gin = gz @ Ws[i]
-                gh = gin[:, nx:] if (i - 1) in skips else gin                          # drop the re-injected input
-        return (None, None, None, *dW, *db, dWa, dba, dWf, dbf, dWv, dbv, dWr, dbr)
+        dWr, dbr = _wgb(g3, hv, f32)
+        dWv = torch.empty(128, 256 + ve.shape[1], device=dev)
+        dbv = torch.empty(128, device=dev)
+        _wg([(ghv, feat)], out=dWv[:, :256], colsum=dbv, fp32=f32)                  # cat([feature, v_emb])
+        _wg([(ghv, ve)], out=dWv[:, 256:], fp32=f32)
+        dWf, dbf = _wgb(g_feat, H[7], f32)
+        dWa, dba = _wgb(gs[:, None], H[7], f32)
+        dW, db = [None] * 8, [None] * 8
+        for i in range(8):
+            db[i] = torch.empty(256, device=dev)
+            if i == 0:
+                dW[0] = _wg([(GZ[0], xe)], colsum=db[0], fp32=f32)
+            elif i == 5:  # the skip layer's input cat([x_emb, h4]) (base.py:431-432): per column block
+                dW[5] = torch.empty(256, nx + 256, device=dev)
+                _wg([(GZ[5], xe)], out=dW[5][:, :nx], colsum=db[5], fp32=f32)
+                _wg([(GZ[5], H[4])], out=dW[5][:, nx:], fp32=f32)
+            else:
+                dW[i] = _wg([(GZ[i], H[i - 1])], colsum=db[i], fp32=f32)
+        # params: pts_linears W0..W7, feature, views, alpha, rgb, then the biases in the same order
+        return (None, None, None, *dW, dWf, dWv, dWa, dWr, *db, dbf, dbv, dba, dbr)
 
 
 class NeuSCompositeBG(torch.autograd.Function):
@@ -958,13 +988,10 @@ class RadianceTG(torch.autograd.Function):
 
 
 def nerf(net, x_emb, v_emb):
-    """Differentiable (sigma [P], rgb [P,3]) of a neurecon_amd NeRF background net."""
-    Ws = [l.weight for l in net.pts_linears]
-    bs = [l.bias for l in net.pts_linears]
-    heads = [net.alpha_linear.weight, net.alpha_linear.bias, net.feature_linear.weight, net.feature_linear.bias,
-             net.views_linears[0].weight, net.views_linears[0].bias, net.rgb_linear.weight, net.rgb_linear.bias]
-    return NeRFFn.apply(x_emb, v_emb, (len(Ws), tuple(net.skips), getattr(net, 'precision', 'fp32') == 'fp32'), *Ws,
-                        *bs, *heads)
+    """Differentiable (sigma [P], rgb [P,3]) of a neurecon_amd NeRF background net (the NeRF++
+    configuration, NeRF.nr_desc)."""
+    layers = list(net.pts_linears) + [net.feature_linear, net.views_linears[0], net.alpha_linear, net.rgb_linear]
+    return NeRFFn.apply(x_emb, v_emb, net, *[l.weight for l in layers], *[l.bias for l in layers])
 
 
 def effective_weights(surface):

@@ -548,3 +548,80 @@ def test_radiance_train_fwd32_vs_fp64():
             assert bool((z64.abs()[flip] <= 1e-5 * scale).all()), (l, int(flip.sum()))
         y64 = torch.sigmoid(h64 @ Ws[4].double().t() + bs[4].double())
         assert float((rgb.double() - y64).abs().max()) <= 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('precision', ['fp32', 'f16x3'])
+def test_nerf_train32_fwd_bwd_vs_fp64(precision):
+    """NeRFFn on nr_nerf_train_fwd32 / nr_nerf_train_bwd32 (the NeRF++ background net of the training
+    step, base.py:426-453: one launch each way, exact fp32 products, layers chained in registers) against
+    the same net in float64 on 20 000 points (not a multiple of the 128-point tile):
+      forward: every stored activation, sigma and rgb within 1e-5 of the tensor scale; the ReLU decisions
+        equal float64's except at |z64| <= 1e-5 of the layer scale (fp32 rounding of a z near 0);
+      backward: with float64's ReLU decisions pinned to the GPU's (as the 512-ray step test pins them),
+        every parameter gradient within 1e-5 (fp32 nets: exact-fp32 weight gradients) / 2e-5 (f16x3 nets:
+        f16x3 weight-gradient products) of the tensor's largest entry."""
+    from neurecon_amd.base import NeRF
+    from neurecon_amd import training as T
+    torch.manual_seed(5)
+    net = NeRF(D=8, W=256, input_ch=4, input_ch_view=3, multires=10, multires_view=4, output_ch=4, skips=[4],
+               use_view_dirs=True, precision=precision).cuda()
+    P = 20000
+    xe = (torch.rand(P, 84, device='cuda') * 2 - 1)
+    ve = (torch.rand(P, 27, device='cuda') * 2 - 1)
+    sigma, rgb = T.nerf(net, xe, ve)
+    sv = rgb.grad_fn.saved_tensors
+    hv_gpu, feat_gpu, H = sv[3], sv[4], sv[5:13]
+    layers = list(net.pts_linears) + [net.feature_linear, net.views_linears[0], net.alpha_linear, net.rgb_linear]
+    P64 = [p.detach().double().requires_grad_(True) for l in layers for p in (l.weight, l.bias)]
+
+    def ref(masks=None, zs=None):
+        W = P64[0::2]
+        b = P64[1::2]
+        x64, v64 = xe.double(), ve.double()
+        h, hs = x64, []
+        for i in range(8):
+            z = h @ W[i].t() + b[i]
+            if zs is not None:
+                zs.append(z.detach())
+            h = z * masks[i] if masks is not None else z.clamp_min(0)
+            hs.append(h)
+            if i == 4:
+                h = torch.cat([x64, h], -1)
+        sig = (h @ W[10].t() + b[10])[:, 0]
+        feat = h @ W[8].t() + b[8]
+        zv = torch.cat([feat, v64], -1) @ W[9].t() + b[9]
+        hv = zv * masks[8] if masks is not None else zv.clamp_min(0)
+        return sig, torch.sigmoid(hv @ W[11].t() + b[11]), hs, feat, hv
+
+    zs = []
+    with torch.no_grad():
+        s64, r64, h64, f64, hv64 = ref(zs=zs)
+    for name, a, b in [('sigma', sigma, s64), ('rgb', rgb, r64), ('feature', feat_gpu, f64), ('hv', hv_gpu, hv64)] + \
+            [(f'h{i}', H[i], h64[i]) for i in range(8)]:
+        sc = float(b.abs().max())
+        e = float((a.detach().double() - b).abs().max())
+        print(f'{precision} {name}: max |hip - f64| {e / sc:.2e} of {sc:.3e}')
+        assert e <= 1e-5 * sc, name
+    for i in range(8):
+        flip = (H[i] > 0) != (zs[i] > 0)
+        zd = float(zs[i].abs()[flip].max()) if bool(flip.any()) else 0.0
+        assert zd <= 1e-5 * float(zs[i].abs().max()), (i, int(flip.sum()), zd)
+    g_s = torch.randn(P, device='cuda')
+    g_r = torch.randn(P, 3, device='cuda')
+    net.zero_grad()
+    ((sigma * g_s).sum() + (rgb * g_r).sum()).backward()
+    masks = [(h > 0).double() for h in H] + [(hv_gpu > 0).double()]
+    s64, r64, _, _, _ = ref(masks=masks)
+    ((s64 * g_s.double()).sum() + (r64 * g_r.double()).sum()).backward()
+    bar = 1e-5 if precision == 'fp32' else 2e-5
+    names = [f'{n}.{k}' for n in [f'pts{i}' for i in range(8)] + ['feature', 'views', 'alpha', 'rgb']
+             for k in ('weight', 'bias')]
+    mine = [p.grad for l in layers for p in (l.weight, l.bias)]
+    worst = 0.0
+    for name, a, b in zip(names, mine, P64):
+        sc = float(b.grad.abs().max()) + 1e-30
+        e = float((a.double() - b.grad).abs().max()) / sc
+        worst = max(worst, e)
+        assert e <= bar, (name, e)
+    print(f'{precision}: worst parameter-gradient error {worst:.2e} of the tensor scale')
