@@ -491,6 +491,25 @@ int nr_sine_adjoint(const float* hbar, int ldh, const float* s, const float* h, 
 int nr_mul(const float* a, const float* b, int64_t n, float* out, void* stream);
 /* mode 0: y = relu(y); 1: g *= (y > 0); 2: y = sigmoid(y); 3: g *= y (1 - y) */
 int nr_activation(float* y, float* g, int64_t n, int mode, void* stream);
+/* weight_norm(dim=0) of up to NR_WN_MAX layers in one launch (torch._weight_norm, models/base.py:118-129,
+ * 226-227): w = v * (g / ||v_row||), norm[row] saved for the backward; backward (torch's
+ * weight_norm_bwd_first_dim): dot = sum grad_w * v per row, grad_g = dot / norm, grad_v = (g / norm) *
+ * (grad_w - v * dot / norm^2).  v / w / grad_w / grad_v [rows][cols] row-major, g / norm / grad_g [rows];
+ * a null grad_w is a zero gradient.  One 64-lane wave per row, fp32 sums in a fixed order. */
+#define NR_WN_MAX 16
+typedef struct {
+  const float* v;
+  const float* g;
+  float* w;          /* forward output */
+  float* norm;       /* forward output / backward input */
+  const float* grad_w;
+  float* grad_v;
+  float* grad_g;
+  int rows;
+  int cols;
+} NrWnLayer;
+int nr_weight_norm_fwd(const NrWnLayer* layers, int n, void* stream);
+int nr_weight_norm_bwd(const NrWnLayer* layers, int n, void* stream);
 int nr_radiance_input(const float* x, const float* v, const float* nrm, const float* feat, int64_t P, int nfreq_view,
                       int use_view_dirs, int wfeat, float* out, void* stream);
 int nr_neus_points(const float* rays_o, const float* rays_d, const float* d_all, int64_t R, int S, float* pts,

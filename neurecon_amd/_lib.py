@@ -107,6 +107,7 @@ TG_NONE, TG_SOFTPLUS, TG_MUL, TG_SPADJ, TG_RELUMASK = 0, 1, 3, 4, 5
 # NrTrainGemm.blocked / NrWgrad.blocked bits (include/neurecon_hip.h: 16 x 16 blocked tensors)
 BLK_X1, BLK_X2, BLK_Y, BLK_YB, BLK_Y2, BLK_Y3, BLK_A, BLK_G, BLK_ZD = 1, 2, 4, 8, 16, 32, 64, 128, 256
 WG_BLK_A0, WG_BLK_A1, WG_BLK_B0, WG_BLK_B1 = 1, 2, 4, 8
+WN_MAX = 16  # NR_WN_MAX: layers per nr_weight_norm_* call
 
 
 class NrTrainGemm(ctypes.Structure):
@@ -133,6 +134,11 @@ class NrWgrad(ctypes.Structure):
     ]
 
 
+class NrWnLayer(ctypes.Structure):
+    _fields_ = [('v', _c_p), ('g', _c_p), ('w', _c_p), ('norm', _c_p), ('grad_w', _c_p), ('grad_v', _c_p),
+                ('grad_g', _c_p), ('rows', _c_i), ('cols', _c_i)]
+
+
 class NrKernelStat(ctypes.Structure):
     _fields_ = [('name', ctypes.c_char * 32), ('launches', _c_i64), ('ms', ctypes.c_double),
                 ('units', ctypes.c_double)]
@@ -156,6 +162,8 @@ _SIGS = {
     'nr_nerf_train_fwd32': (_c_i, [ctypes.POINTER(NrNerfDesc), _c_p, _c_p, _c_p, _c_i64, ctypes.POINTER(_c_p), _c_p,
                                    _c_p, _c_p, _c_p, _c_p]),
     'nr_nerf_train_packed_bytes': (_c_sz, [ctypes.POINTER(NrNerfDesc)]),
+    'nr_weight_norm_fwd': (_c_i, [ctypes.POINTER(NrWnLayer), _c_i, _c_p]),
+    'nr_weight_norm_bwd': (_c_i, [ctypes.POINTER(NrWnLayer), _c_i, _c_p]),
     'nr_nerf_train_pack': (_c_i, [ctypes.POINTER(NrNerfDesc), ctypes.POINTER(_c_p), ctypes.POINTER(_c_p), _c_p, _c_p]),
     'nr_nerf_train_bwd32': (_c_i, [ctypes.POINTER(NrNerfDesc), _c_p, _c_p, _c_p, ctypes.POINTER(_c_p), _c_p, _c_p,
                                    _c_i64, _c_p, _c_p, _c_p, ctypes.POINTER(_c_p), _c_p]),

@@ -31,47 +31,54 @@ __device__ float emb_f(int f, const float (&x)[3], int nfreq) {
   return m < 3 ? sinf(v) : cosf(v);
 }
 
+// The embedding kernels run one 64-lane wave per point, a lane per feature (r05: one thread per
+// element indexed p = i / ldo paid a 64-bit division per element, one thread per point for the vjp
+// walked its row serially: 23 / 31 / 46 us per 131 k-point training step)
+constexpr int kEmbPts = 4;  // points (waves) per 256-thread block
+// grid-stride over points: ~2 k workgroups, each wave walking its points (one wave per point as a
+// launch was wave-dispatch bound)
+inline dim3 emb_grid(int64_t P) { return dim3((unsigned)std::min<int64_t>((P + kEmbPts - 1) / kEmbPts, 2048)); }
+__device__ __forceinline__ float emb_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
 // out[p * ldo + f]: features f < nf, zeros up to ldo (ldo >= nf; the training GEMMs' padded blocks)
-__global__ void embed_kernel(const float* __restrict__ x, int64_t P, int nfreq, float* __restrict__ out, int ldo) {
+__global__ __launch_bounds__(256) void embed_kernel(const float* __restrict__ x, int64_t P, int nfreq,
+                                                    float* __restrict__ out, int ldo) {
   const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P * ldo) return;
-  const int64_t p = i / ldo;
-  const int f = (int)(i - p * ldo);
-  if (f >= nf) {
-    out[i] = 0.0f;
-    return;
+  const int lane = threadIdx.x & 63;
+  for (int64_t p = (int64_t)blockIdx.x * kEmbPts + (threadIdx.x >> 6); p < P; p += (int64_t)gridDim.x * kEmbPts) {
+    const float xs[3] = {x[p * 3], x[p * 3 + 1], x[p * 3 + 2]};
+    for (int f = lane; f < ldo; f += 64) out[p * ldo + f] = f < nf ? emb_f(f, xs, nfreq) : 0.0f;
   }
-  const float xs[3] = {x[p * 3], x[p * 3 + 1], x[p * 3 + 2]};
-  out[i] = emb_f(f, xs, nfreq);
 }
 
 // J_emb(x) v: d/dt embed(x + t v) (the tangent seed of the double backward)
-__global__ void embed_jvp_kernel(const float* __restrict__ x, const float* __restrict__ v, int64_t P, int nfreq,
-                                 float* __restrict__ out, int ldo) {
+__global__ __launch_bounds__(256) void embed_jvp_kernel(const float* __restrict__ x, const float* __restrict__ v,
+                                                        int64_t P, int nfreq, float* __restrict__ out, int ldo) {
   const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P * ldo) return;
-  const int64_t p = i / ldo;
-  const int f = (int)(i - p * ldo);
-  if (f >= nf) {
-    out[i] = 0.0f;
-    return;
+  const int lane = threadIdx.x & 63;
+  for (int64_t p = (int64_t)blockIdx.x * kEmbPts + (threadIdx.x >> 6); p < P; p += (int64_t)gridDim.x * kEmbPts)
+  for (int f = lane; f < ldo; f += 64) {
+    float o = 0.0f;
+    if (f < 3) {
+      o = v[p * 3 + f];
+    } else if (f < nf) {
+      const int fp = f - 3, band = fp / 6, m = fp - band * 6, c = m % 3;
+      const float freq = (float)(1 << band);
+      const float a = fmul(x[p * 3 + c], freq);
+      const float d = m < 3 ? cosf(a) : -sinf(a);
+      o = fmul(fmul(v[p * 3 + c], d), freq);
+    }
+    out[p * ldo + f] = o;
   }
-  if (f < 3) {
-    out[i] = v[p * 3 + f];
-    return;
-  }
-  const int fp = f - 3, band = fp / 6, m = fp - band * 6, c = m % 3;
-  const float freq = (float)(1 << band);
-  const float a = fmul(x[p * 3 + c], freq);
-  const float d = m < 3 ? cosf(a) : -sinf(a);
-  out[i] = fmul(fmul(v[p * 3 + c], d), freq);
 }
 
-// J_emb(x)^T (e0 + s1 e1) -> [P, 3] (autograd's Sin/Cos backward then the Mul by the frequency,
-// contributions summed in feature order)
-// one feature's contribution to the point's d x (summed in feature order by the caller)
+// J_emb(x)^T (e0 + s1 e1) -> [P, 3] (autograd's Sin/Cos backward then the Mul by the frequency): each
+// lane forms its feature's contribution, the three components are summed over the wave by a fixed
+// butterfly
 __device__ __forceinline__ void embed_vjp_acc(int f, float gf, const float (&xp)[3], float (&n)[3]) {
   if (f < 3) {
     n[f] = fadd(n[f], gf);
@@ -84,43 +91,28 @@ __device__ __forceinline__ void embed_vjp_acc(int f, float gf, const float (&xp)
   n[c] = fadd(n[c], contrib);
 }
 
-// VEC: rows read as float4 (ld0 / ld1 multiples of 4 covering the features rounded up to 4, 16-byte
-// aligned): a thread per point walks its own row, so scalar loads touched 64 rows' cache lines per
-// instruction (r04: 62 us for 65 k points); the arithmetic and its order are the same either way
-template <bool VEC>
-__global__ void embed_vjp_kernel(const float* __restrict__ x, const float* __restrict__ e0, int ld0,
-                                 const float* __restrict__ e1, int ld1, float s1, int64_t P, int nfreq,
-                                 float* __restrict__ out) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P) return;
+__global__ __launch_bounds__(256) void embed_vjp_kernel(const float* __restrict__ x, const float* __restrict__ e0,
+                                                        int ld0, const float* __restrict__ e1, int ld1, float s1,
+                                                        int64_t P, int nfreq, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
   const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
+  for (int64_t p = (int64_t)blockIdx.x * kEmbPts + (threadIdx.x >> 6); p < P; p += (int64_t)gridDim.x * kEmbPts) {
   const float xp[3] = {x[p * 3], x[p * 3 + 1], x[p * 3 + 2]};
   float n[3] = {0.f, 0.f, 0.f};
-  if constexpr (VEC) {
-    const float4* r0 = (const float4*)(e0 + p * ld0);
-    const float4* r1 = e1 ? (const float4*)(e1 + p * ld1) : nullptr;
-    for (int f4 = 0; f4 < nf; f4 += 4) {
-      const float4 v = r0[f4 >> 2];
-      const float4 u = r1 ? r1[f4 >> 2] : make_float4(0.f, 0.f, 0.f, 0.f);
-      const float vv[4] = {v.x, v.y, v.z, v.w}, uu[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (f4 + e >= nf) break;
-        float gf = vv[e];
-        if (r1) gf = fadd(gf, fmul(uu[e], s1));
-        embed_vjp_acc(f4 + e, gf, xp, n);
-      }
-    }
-  } else {
-    for (int f = 0; f < nf; ++f) {
-      float gf = e0[p * ld0 + f];
-      if (e1) gf = fadd(gf, fmul(e1[p * ld1 + f], s1));
-      embed_vjp_acc(f, gf, xp, n);
-    }
+  for (int f = lane; f < nf; f += 64) {
+    float gf = e0[p * ld0 + f];
+    if (e1) gf = fadd(gf, fmul(e1[p * ld1 + f], s1));
+    embed_vjp_acc(f, gf, xp, n);
   }
-  out[p * 3 + 0] = n[0];
-  out[p * 3 + 1] = n[1];
-  out[p * 3 + 2] = n[2];
+  n[0] = emb_wave_sum(n[0]);
+  n[1] = emb_wave_sum(n[1]);
+  n[2] = emb_wave_sum(n[2]);
+  if (lane == 0) {
+    out[p * 3 + 0] = n[0];
+    out[p * 3 + 1] = n[1];
+    out[p * 3 + 2] = n[2];
+  }
+  }
 }
 
 // Softplus(beta=100, threshold=20) (base.py:202) and torch's softplus_backward factor
@@ -245,6 +237,61 @@ __global__ void act_kernel(float* __restrict__ y, float* __restrict__ g, int64_t
   }
 }
 
+// weight_norm(dim=0) of a batch of layers: one wave per row (rows of all layers concatenated)
+struct WnBatch {
+  NrWnLayer l[NR_WN_MAX];
+  int row0[NR_WN_MAX + 1];
+  int n;
+};
+__device__ __forceinline__ int wn_layer(const WnBatch& b, int row) {
+  int i = 0;
+  while (i + 1 < b.n && row >= b.row0[i + 1]) ++i;
+  return i;
+}
+// lane-strided sum, then a fixed butterfly over the wave
+__device__ __forceinline__ float wave_sum64(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__global__ __launch_bounds__(256) void weight_norm_fwd_kernel(WnBatch b) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= b.row0[b.n]) return;
+  const int li = wn_layer(b, row);
+  const NrWnLayer& L = b.l[li];
+  const int r = row - b.row0[li];
+  const float* v = L.v + (int64_t)r * L.cols;
+  float ss = 0.0f;
+  for (int c = lane; c < L.cols; c += 64) ss = fmaf(v[c], v[c], ss);
+  const float nrm = __fsqrt_rn(wave_sum64(ss));
+  const float s = fdiv(L.g[r], nrm);
+  float* w = L.w + (int64_t)r * L.cols;
+  for (int c = lane; c < L.cols; c += 64) w[c] = fmul(v[c], s);
+  if (lane == 0) L.norm[r] = nrm;
+}
+__global__ __launch_bounds__(256) void weight_norm_bwd_kernel(WnBatch b) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= b.row0[b.n]) return;
+  const int li = wn_layer(b, row);
+  const NrWnLayer& L = b.l[li];
+  const int r = row - b.row0[li];
+  const float* v = L.v + (int64_t)r * L.cols;
+  float* gv = L.grad_v + (int64_t)r * L.cols;
+  if (!L.grad_w) {
+    for (int c = lane; c < L.cols; c += 64) gv[c] = 0.0f;
+    if (lane == 0) L.grad_g[r] = 0.0f;
+    return;
+  }
+  const float* gw = L.grad_w + (int64_t)r * L.cols;
+  float dot = 0.0f;
+  for (int c = lane; c < L.cols; c += 64) dot = fmaf(gw[c], v[c], dot);
+  dot = wave_sum64(dot);
+  const float nrm = L.norm[r];
+  const float a = fdiv(L.g[r], nrm), bcoef = fdiv(dot, fmul(nrm, nrm));
+  for (int c = lane; c < L.cols; c += 64) gv[c] = fmul(a, fsub(gw[c], fmul(v[c], bcoef)));
+  if (lane == 0) L.grad_g[r] = fdiv(dot, nrm);
+}
+
 // RadianceNet input cat([x, embed_view(v), normals, feature]) (base.py:379-384), one row per point;
 // v is indexed per point.  Without view dirs (view = 0): cat([x, feature]) (base.py:383-384)
 __global__ void radiance_input_kernel(const float* __restrict__ x, const float* __restrict__ v,
@@ -294,10 +341,34 @@ __global__ void neus_points_kernel(const float* __restrict__ ro, const float* __
 // NeuS compositing with a differentiable graph (neus.py:28-70, :346-355), one thread per ray.
 // sdf [R,S], radiance [R,S-1,3], dmid [R,S-1]; s from the device.  fp64 prefix products / sums
 // rounded per element, as in the render kernels.
-// One ray per 64-lane wave: the per-sample work (CDFs, alphas, staging, the backward's weight
-// adjoints and output stores) across the lanes through LDS, the order-sensitive scans on lane 0 with
-// the per-ray version's arithmetic (512-ray training batches gave the per-thread version 8 waves for
-// the chip).  LDS: fwd 7 S floats, bwd 9 S floats + 4 doubles.
+// One ray per 64-lane wave, everything across the lanes (r05; r03-r04 ran the scans on lane 0: 26 + 78
+// us per 512-ray step): the transmittance T_i = prod_{j<i} (1 - alpha_j + 1e-10) is a wave prefix
+// product in fp64 over 64-sample segments with a carried running product, the colour / opacity / depth
+// sums are per-lane fp64 partials reduced by a fixed butterfly; the backward's suffix sums likewise.
+// The association of the fp64 products and sums differs from a sequential walk (relative 1e-16, below
+// the per-element fp32 rounding).  LDS: fwd 2 S floats, bwd S doubles + 5 S floats.
+__device__ __forceinline__ double wave_incl_prod(double x, int l) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const double t = __shfl_up(x, d);
+    if (l >= d) x *= t;
+  }
+  return x;
+}
+__device__ __forceinline__ double wave_incl_sum_rev(double x, int l) {  // sum over lanes >= l
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const double t = __shfl_down(x, d);
+    if (l + d < 64) x += t;
+  }
+  return x;
+}
+__device__ __forceinline__ double wave_sum_d(double x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
 __global__ __launch_bounds__(64) void neus_composite_fwd_kernel(const float* __restrict__ sdf, const float* __restrict__ s_dev,
                                           const float* __restrict__ rad, const float* __restrict__ dmid, int64_t R,
                                           int S, int white_bkgd, float* __restrict__ rgb, float* __restrict__ depth,
@@ -308,44 +379,49 @@ __global__ __launch_bounds__(64) void neus_composite_fwd_kernel(const float* __r
   const int l = threadIdx.x, S1 = S - 1;
   const float s = *s_dev;
   const float* sd = sdf + r * S;
-  float* lc = lds;           // [S] cdf
-  float* la = lc + S;        // [S] alpha
-  float* lw = la + S;        // [S] weights
-  float* lr = lw + S;        // [3 S] radiance
-  float* ld = lr + 3 * S;    // [S] mid depths
+  float* lc = lds;      // [S] cdf
+  float* lw = lc + S;   // [S] weights
   for (int i = l; i < S; i += 64) {
     const float c = sigmoidf_ref(fmul(sd[i], s));
     lc[i] = c;
     if (cdf_out) cdf_out[r * S + i] = c;
   }
   __syncthreads();
-  for (int i = l; i < S1; i += 64) {
-    const int64_t q = r * S1 + i;
-    const float al = fmaxf(fdiv(fsub(lc[i], lc[i + 1]), fadd(lc[i], 1e-10f)), 0.0f);
-    la[i] = al;
-    if (alpha_out) alpha_out[q] = al;
-    lr[i * 3 + 0] = rad[q * 3 + 0];
-    lr[i * 3 + 1] = rad[q * 3 + 1];
-    lr[i * 3 + 2] = rad[q * 3 + 2];
-    ld[i] = dmid[q];
-  }
-  __syncthreads();
-  if (l == 0) {
-    double T = 1.0, a_acc = 0.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
-    for (int i = 0; i < S1; ++i) {
-      const float al = la[i];
-      const float w = fmul(al, (float)T);
-      T *= (double)fadd(fsub(1.0f, al), 1e-10f);
-      c0 += (double)fmul(w, lr[i * 3 + 0]);
-      c1 += (double)fmul(w, lr[i * 3 + 1]);
-      c2 += (double)fmul(w, lr[i * 3 + 2]);
-      a_acc += (double)w;
+  double Tc = 1.0, c0 = 0.0, c1 = 0.0, c2 = 0.0, a_acc = 0.0;
+  for (int b = 0; b < S1; b += 64) {
+    const int i = b + l;
+    const bool ok = i < S1;
+    const int64_t q = r * S1 + (ok ? i : 0);
+    const float al = ok ? fmaxf(fdiv(fsub(lc[i], lc[i + 1]), fadd(lc[i], 1e-10f)), 0.0f) : 0.0f;
+    const double u = ok ? (double)fadd(fsub(1.0f, al), 1e-10f) : 1.0;
+    const double incl = wave_incl_prod(u, l);
+    const double excl = __shfl_up(incl, 1);
+    const double T = Tc * (l == 0 ? 1.0 : excl);
+    const float w = fmul(al, (float)T);
+    if (ok) {
       lw[i] = w;
+      if (alpha_out) alpha_out[q] = al;
+      c0 += (double)fmul(w, rad[q * 3 + 0]);
+      c1 += (double)fmul(w, rad[q * 3 + 1]);
+      c2 += (double)fmul(w, rad[q * 3 + 2]);
+      a_acc += (double)w;
     }
-    const float accf = (float)a_acc;
-    const float den = fadd(accf, 1e-10f);
-    double dep = 0.0;
-    for (int i = 0; i < S1; ++i) dep += (double)fmul(fdiv(lw[i], den), ld[i]);
+    Tc *= __shfl(incl, 63);
+  }
+  c0 = wave_sum_d(c0);
+  c1 = wave_sum_d(c1);
+  c2 = wave_sum_d(c2);
+  a_acc = wave_sum_d(a_acc);
+  __syncthreads();
+  const float accf = (float)a_acc;
+  const float den = fadd(accf, 1e-10f);
+  double dep = 0.0;
+  for (int i = l; i < S1; i += 64) {
+    dep += (double)fmul(fdiv(lw[i], den), dmid[r * S1 + i]);
+    w_out[r * S1 + i] = lw[i];
+  }
+  dep = wave_sum_d(dep);
+  if (l == 0) {
     float o0 = (float)c0, o1 = (float)c1, o2 = (float)c2;
     if (white_bkgd) {
       const float bg = fsub(1.0f, accf);
@@ -357,112 +433,110 @@ __global__ __launch_bounds__(64) void neus_composite_fwd_kernel(const float* __r
     depth[r] = (float)dep;
     acc[r] = accf;
   }
-  __syncthreads();
-  for (int i = l; i < S1; i += 64) w_out[r * S1 + i] = lw[i];
 }
 
 // backward of the above: grads of rgb [R,3], depth [R], acc [R] and (optional) the visibility
 // weights [R,S-1] -> d sdf [R,S], d radiance [R,S-1,3], d s per ray [R] (summed by the host).
 // alpha_i = max((c_i - c_{i+1}) / (c_i + 1e-10), 0) (clamp_min passes the gradient where >= 0);
-// T = exclusive cumprod of (1 - alpha + 1e-10) (cumprod_backward: suffix sums / input).
+// T = exclusive cumprod of (1 - alpha + 1e-10) (cumprod_backward: suffix sums / input):
+//   alpha-bar_i = wbar_i T_i - (sum_{k > i} wbar_k alpha_k T_k) / u_i, then c_i and c_{i+1} receive the
+//   quotient rule's terms; c_{i+1}'s total is cn_bar_i + ci_bar_{i+1} (rounded to fp32 as before).
 __global__ __launch_bounds__(64) void neus_composite_bwd_kernel(const float* __restrict__ sdf, const float* __restrict__ s_dev,
                                           const float* __restrict__ rad, const float* __restrict__ dmid, int64_t R,
                                           int S, int white_bkgd, const float* __restrict__ g_rgb,
                                           const float* __restrict__ g_depth, const float* __restrict__ g_acc,
                                           const float* __restrict__ g_w, float* __restrict__ d_sdf,
                                           float* __restrict__ d_rad, float* __restrict__ d_s) {
-  extern __shared__ float lds[];
+  extern __shared__ double ldsd[];
   const int64_t r = blockIdx.x;
   const int l = threadIdx.x, S1 = S - 1;
   const float s = *s_dev;
   const float* sd = sdf + r * S;
-  double* ldb = (double*)lds;  // A, wd
-  float* c = lds + 4;          // [S] cdf
-  float* al = c + S;           // [S] alpha
-  float* Tt = al + S;          // [S] T
-  float* w = Tt + S;           // [S] weights
-  float* wb = w + S;           // [S] weight adjoints
-  float* ls = wb + S;          // [S] sdf
-  float* lm = ls + S;          // [S] mid depths
-  float* lo = lm + S;          // [S] d sdf
-  for (int i = l; i < S; i += 64) {
-    const float v = sd[i];
-    ls[i] = v;
-    c[i] = sigmoidf_ref(fmul(v, s));
-    if (i < S1) lm[i] = dmid[r * S1 + i];
-  }
+  double* cnb = ldsd;     // [S] cn_bar_{k-1} at k (fp64, as the sequential walk adds it)
+  float* c = (float*)(cnb + S);  // [S] cdf
+  float* al = c + S;      // [S] alpha
+  float* Tt = al + S;     // [S] T (fp32, as the weights use it)
+  float* wb = Tt + S;     // [S] weight adjoints
+  float* cib = wb + S;    // [S] ci_bar (fp32)
+  for (int i = l; i < S; i += 64) c[i] = sigmoidf_ref(fmul(sd[i], s));
   __syncthreads();
-  if (l == 0) {
-    double T = 1.0, a_acc = 0.0, wd = 0.0;
-    for (int i = 0; i < S1; ++i) {
-      const float a = fmaxf(fdiv(fsub(c[i], c[i + 1]), fadd(c[i], 1e-10f)), 0.0f);
+  // forward recompute: alpha, T, weights; acc and sum w d
+  double Tc = 1.0, a_acc = 0.0, wd = 0.0;
+  for (int b = 0; b < S1; b += 64) {
+    const int i = b + l;
+    const bool ok = i < S1;
+    const float a = ok ? fmaxf(fdiv(fsub(c[i], c[i + 1]), fadd(c[i], 1e-10f)), 0.0f) : 0.0f;
+    const double u = ok ? (double)fadd(fsub(1.0f, a), 1e-10f) : 1.0;
+    const double incl = wave_incl_prod(u, l);
+    const double excl = __shfl_up(incl, 1);
+    const float T = (float)(Tc * (l == 0 ? 1.0 : excl));
+    if (ok) {
       al[i] = a;
-      Tt[i] = (float)T;
-      w[i] = fmul(a, (float)T);
-      T *= (double)fadd(fsub(1.0f, a), 1e-10f);
-      a_acc += (double)w[i];
+      Tt[i] = T;
+      const float w = fmul(a, T);
+      a_acc += (double)w;
+      wd += (double)w * (double)dmid[r * S1 + i];
     }
-    const float accf = (float)a_acc;
-    ldb[0] = (double)fadd(accf, 1e-10f);
-    for (int i = 0; i < S1; ++i) wd += (double)w[i] * (double)lm[i];
-    ldb[1] = wd;
+    Tc *= __shfl(incl, 63);
   }
-  __syncthreads();
-  const double A = ldb[0], wd = ldb[1];
+  a_acc = wave_sum_d(a_acc);
+  wd = wave_sum_d(wd);
+  const double A = (double)fadd((float)a_acc, 1e-10f);
   const float gr0 = g_rgb ? g_rgb[r * 3 + 0] : 0.f, gr1 = g_rgb ? g_rgb[r * 3 + 1] : 0.f,
               gr2 = g_rgb ? g_rgb[r * 3 + 2] : 0.f;
   const double gd = g_depth ? (double)g_depth[r] : 0.0;
   // white_bkgd: rgb += 1 - acc -> acc receives -sum(g_rgb)
   const double ga = (g_acc ? (double)g_acc[r] : 0.0) - (white_bkgd ? (double)gr0 + gr1 + gr2 : 0.0);
+  __syncthreads();
   for (int i = l; i < S1; i += 64) {
     const int64_t q = r * S1 + i;
+    const float w = fmul(al[i], Tt[i]);
     double v = (double)gr0 * rad[q * 3 + 0] + (double)gr1 * rad[q * 3 + 1] + (double)gr2 * rad[q * 3 + 2] + ga;
-    v += gd * ((double)lm[i] / A - wd / (A * A));
+    v += gd * ((double)dmid[q] / A - wd / (A * A));
     if (g_w) v += (double)g_w[q];
     wb[i] = (float)v;
-    d_rad[q * 3 + 0] = fmul(w[i], gr0);
-    d_rad[q * 3 + 1] = fmul(w[i], gr1);
-    d_rad[q * 3 + 2] = fmul(w[i], gr2);
+    d_rad[q * 3 + 0] = fmul(w, gr0);
+    d_rad[q * 3 + 1] = fmul(w, gr1);
+    d_rad[q * 3 + 2] = fmul(w, gr2);
   }
   __syncthreads();
-  if (l == 0) {
-    // alpha-bar: w = alpha * T -> alpha gets wbar * T; T_i = prod_{j<i} u_j (u_j = 1 - alpha_j + 1e-10)
-    // -> u_j gets (sum_{k > j} wbar_k alpha_k T_k) / u_j, alpha_j gets minus that
-    double suffix = 0.0;  // sum_{k > i} wbar_k * alpha_k * T_k
-    double sbar = 0.0;
-    float cbar_next = 0.0f;  // contribution to c_{i+1} accumulated from alpha_i
-    // walk backwards: alpha_i depends on c_i, c_{i+1}
-    for (int i = S1 - 1; i >= 0; --i) {
+  // alpha-bar from the reverse suffix sums (segments from the end, carried), then the quotient rule
+  double carry = 0.0;  // sum over the later segments
+  double sbar = 0.0;
+  const int nseg = (S1 + 63) / 64;
+  for (int sg = nseg - 1; sg >= 0; --sg) {
+    const int i = sg * 64 + l;
+    const bool ok = i < S1;
+    const double t = ok ? (double)wb[i] * al[i] * Tt[i] : 0.0;
+    const double incl = wave_incl_sum_rev(t, l);          // sum over lanes >= l of this segment
+    const double suffix = carry + (incl - t);              // sum_{k > i}
+    if (ok) {
       const double u = (double)fadd(fsub(1.0f, al[i]), 1e-10f);
       const double abar = (double)wb[i] * Tt[i] - suffix / u;
-      suffix += (double)wb[i] * al[i] * Tt[i];
       const float num = fsub(c[i], c[i + 1]), den = fadd(c[i], 1e-10f);
-      const bool pass = fdiv(num, den) >= 0.0f;
       double ci_bar = 0.0, cn_bar = 0.0;
-      if (pass) {
+      if (fdiv(num, den) >= 0.0f) {
         ci_bar = abar / den - abar * num / ((double)den * den);
         cn_bar = -abar / den;
       }
-      // c_{i+1} collects cn_bar here plus ci_bar from alpha_{i+1} (already in cbar_next)
-      const double cb_next = cn_bar + (double)cbar_next;
-      {
-        const float cc = c[i + 1];
-        const double sg = cb_next * cc * (1.0 - cc);
-        lo[i + 1] = (float)(sg * s);
-        sbar += sg * ls[i + 1];
-      }
-      cbar_next = (float)ci_bar;
+      cib[i] = (float)ci_bar;
+      cnb[i + 1] = cn_bar;  // c_{i+1}'s term from alpha_i (completed below)
     }
-    {
-      const float cc = c[0];
-      const double sg = (double)cbar_next * cc * (1.0 - cc);
-      lo[0] = (float)(sg * s);
-      sbar += sg * ls[0];
-    }
-    d_s[r] = (float)sbar;
+    carry += __shfl(incl, 0);
   }
   __syncthreads();
-  for (int i = l; i < S; i += 64) d_sdf[r * S + i] = lo[i];
+  // c_{i+1} collects cn_bar_i plus ci_bar_{i+1} (rounded to fp32); c_0 only ci_bar_0
+  for (int k = l; k < S; k += 64) {
+    double cb;
+    if (k == 0) cb = (double)cib[0];
+    else cb = cnb[k] + (k < S1 ? (double)cib[k] : 0.0);
+    const float cc = c[k];
+    const double g = cb * cc * (1.0 - cc);
+    d_sdf[r * S + k] = (float)(g * s);
+    sbar += g * sd[k];
+  }
+  sbar = wave_sum_d(sbar);
+  if (l == 0) d_s[r] = (float)sbar;
 }
 
 // ---- VolSDF compositing with a graph (volsdf.py:449-506) ----------------------------------------------
@@ -1029,7 +1103,8 @@ int nr_embed_padded(const float* x, int64_t P, int nfreq, float* out, int ldo, v
   const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
   NR_REQUIRE(x && out && P >= 0 && nfreq <= 10 && ldo >= nf, NR_ERR_ARG, "nr_embed: bad argument");
   if (P == 0) return NR_OK;
-  hipLaunchKernelGGL(embed_kernel, grid1(P * ldo), dim3(kBlk), 0, (hipStream_t)stream, x, P, nfreq, out, ldo);
+  hipLaunchKernelGGL(embed_kernel, emb_grid(P), dim3(256), 0, (hipStream_t)stream, x,
+                     P, nfreq, out, ldo);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
@@ -1043,8 +1118,8 @@ int nr_embed_jvp_padded(const float* x, const float* v, int64_t P, int nfreq, fl
   const int nf = nfreq < 0 ? 3 : 3 + 6 * nfreq;
   NR_REQUIRE(x && v && out && P >= 0 && nfreq <= 10 && ldo >= nf, NR_ERR_ARG, "nr_embed_jvp: bad argument");
   if (P == 0) return NR_OK;
-  hipLaunchKernelGGL(embed_jvp_kernel, grid1(P * ldo), dim3(kBlk), 0, (hipStream_t)stream, x, v, P, nfreq, out,
-                     ldo);
+  hipLaunchKernelGGL(embed_jvp_kernel, emb_grid(P), dim3(256), 0,
+                     (hipStream_t)stream, x, v, P, nfreq, out, ldo);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
@@ -1053,15 +1128,8 @@ int nr_embed_vjp(const float* x, const float* e0, int ld0, const float* e1, int 
                  float* out, void* stream) {
   NR_REQUIRE(x && e0 && out && P >= 0 && nfreq <= 10, NR_ERR_ARG, "nr_embed_vjp: bad argument");
   if (P == 0) return NR_OK;
-  const int nf4 = ((nfreq < 0 ? 3 : 3 + 6 * nfreq) + 3) / 4 * 4;
-  const bool vec = ld0 % 4 == 0 && ld0 >= nf4 && ((uintptr_t)e0 & 15) == 0 &&
-                   (!e1 || (ld1 % 4 == 0 && ld1 >= nf4 && ((uintptr_t)e1 & 15) == 0));
-  if (vec)
-    hipLaunchKernelGGL(embed_vjp_kernel<true>, grid1(P), dim3(kBlk), 0, (hipStream_t)stream, x, e0, ld0, e1, ld1, s1,
-                       P, nfreq, out);
-  else
-    hipLaunchKernelGGL(embed_vjp_kernel<false>, grid1(P), dim3(kBlk), 0, (hipStream_t)stream, x, e0, ld0, e1, ld1, s1,
-                       P, nfreq, out);
+  hipLaunchKernelGGL(embed_vjp_kernel, emb_grid(P), dim3(256), 0,
+                     (hipStream_t)stream, x, e0, ld0, e1, ld1, s1, P, nfreq, out);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
@@ -1145,6 +1213,27 @@ int nr_activation(float* y, float* g, int64_t n, int mode, void* stream) {
   return NR_OK;
 }
 
+static int wn_launch(const NrWnLayer* layers, int n, void* stream, bool bwd) {
+  NR_REQUIRE(layers && n >= 1 && n <= NR_WN_MAX, NR_ERR_ARG, "nr_weight_norm: 1..NR_WN_MAX layers");
+  WnBatch b{};
+  b.n = n;
+  b.row0[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    const NrWnLayer& L = layers[i];
+    NR_REQUIRE(L.v && L.g && L.norm && L.rows > 0 && L.cols > 0, NR_ERR_ARG, "nr_weight_norm: bad layer");
+    NR_REQUIRE(bwd ? (L.grad_v && L.grad_g) : (L.w != nullptr), NR_ERR_ARG, "nr_weight_norm: null output");
+    b.l[i] = L;
+    b.row0[i + 1] = b.row0[i] + L.rows;
+  }
+  const unsigned blocks = (unsigned)((b.row0[n] + 3) / 4);
+  if (bwd) hipLaunchKernelGGL(weight_norm_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, b);
+  else hipLaunchKernelGGL(weight_norm_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, b);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+int nr_weight_norm_fwd(const NrWnLayer* layers, int n, void* stream) { return wn_launch(layers, n, stream, false); }
+int nr_weight_norm_bwd(const NrWnLayer* layers, int n, void* stream) { return wn_launch(layers, n, stream, true); }
+
 int nr_radiance_input(const float* x, const float* v, const float* nrm, const float* feat, int64_t P, int nfreq_view,
                       int use_view_dirs, int wfeat, float* out, void* stream) {
   // wfeat = 0: the small inputs only (the training GEMM reads the feature from its own tensor)
@@ -1176,8 +1265,8 @@ int nr_neus_composite_fwd(const float* sdf, const float* s_dev, const float* rad
   NR_REQUIRE(sdf && s_dev && rad && dmid && rgb && depth && acc && weights && R >= 0 && S >= 2, NR_ERR_ARG,
              "nr_neus_composite_fwd: bad argument");
   if (R == 0) return NR_OK;
-  NR_REQUIRE((size_t)7 * S * sizeof(float) <= 65536, NR_ERR_UNSUPPORTED, "nr_neus_composite_fwd: S too large");
-  hipLaunchKernelGGL(neus_composite_fwd_kernel, dim3((unsigned)R), dim3(64), 7 * S * sizeof(float), (hipStream_t)stream,
+  NR_REQUIRE((size_t)2 * S * sizeof(float) <= 65536, NR_ERR_UNSUPPORTED, "nr_neus_composite_fwd: S too large");
+  hipLaunchKernelGGL(neus_composite_fwd_kernel, dim3((unsigned)R), dim3(64), 2 * S * sizeof(float), (hipStream_t)stream,
                      sdf, s_dev, rad, dmid, R, S, white_bkgd, rgb, depth, acc, weights, alpha, cdf);
   NR_LAUNCH_CHECK();
   return NR_OK;
@@ -1194,8 +1283,9 @@ int nr_neus_composite_bwd(const float* sdf, const float* s_dev, const float* rad
   if (R == 0) return NR_OK;
   NR_REQUIRE(workspace && workspace_bytes >= nr_neus_composite_bwd_workspace_bytes(R, S), NR_ERR_WORKSPACE,
              "nr_neus_composite_bwd: workspace too small");
-  NR_REQUIRE((size_t)(8 * S + 4) * sizeof(float) <= 65536, NR_ERR_UNSUPPORTED, "nr_neus_composite_bwd: S too large");
-  hipLaunchKernelGGL(neus_composite_bwd_kernel, dim3((unsigned)R), dim3(64), (8 * S + 4) * sizeof(float),
+  const size_t lds = (size_t)S * sizeof(double) + (size_t)5 * S * sizeof(float);
+  NR_REQUIRE(lds <= 65536, NR_ERR_UNSUPPORTED, "nr_neus_composite_bwd: S too large");
+  hipLaunchKernelGGL(neus_composite_bwd_kernel, dim3((unsigned)R), dim3(64), lds,
                      (hipStream_t)stream, sdf, s_dev, rad, dmid, R, S, white_bkgd, g_rgb, g_depth, g_acc, g_weights,
                      d_sdf, d_rad, d_s);
   NR_LAUNCH_CHECK();

@@ -994,9 +994,56 @@ def nerf(net, x_emb, v_emb):
     return NeRFFn.apply(x_emb, v_emb, net, *[l.weight for l in layers], *[l.bias for l in layers])
 
 
+class _WeightNormAll(torch.autograd.Function):
+    """torch._weight_norm(v, g, 0) (base.py:118-129, 226-227) of a net's layers in one nr_weight_norm_fwd
+    launch, the backward in one nr_weight_norm_bwd launch (torch: one weight_norm_fwd / _bwd_first_dim
+    launch per layer, ~5 us each; 28 per NeuS training step)"""
+
+    @staticmethod
+    def forward(ctx, n, *vg):
+        vs = [v.contiguous() for v in vg[:n]]
+        gs = [g.contiguous() for g in vg[n:]]
+        dev = vs[0].device
+        ws = [torch.empty_like(v) for v in vs]
+        norms = [torch.empty(v.shape[0], device=dev) for v in vs]
+        arr = (L.NrWnLayer * n)()
+        for i in range(n):
+            arr[i].v, arr[i].g, arr[i].w, arr[i].norm = L.ptr(vs[i]), L.ptr(gs[i]), L.ptr(ws[i]), L.ptr(norms[i])
+            arr[i].rows, arr[i].cols = vs[i].shape
+        L.check(L.lib().nr_weight_norm_fwd(arr, n, _st(vs[0])))
+        ctx.n = n
+        ctx.save_for_backward(*vs, *gs, *norms)
+        return tuple(ws)
+
+    @staticmethod
+    def backward(ctx, *gws):
+        n = ctx.n
+        sv = ctx.saved_tensors
+        vs, gs, norms = sv[:n], sv[n:2 * n], sv[2 * n:]
+        gv = [torch.empty_like(v) for v in vs]
+        gg = [torch.empty_like(g) for g in gs]
+        gw = [None if t is None else t.contiguous() for t in gws]
+        arr = (L.NrWnLayer * n)()
+        for i in range(n):
+            arr[i].v, arr[i].g, arr[i].norm = L.ptr(vs[i]), L.ptr(gs[i]), L.ptr(norms[i])
+            arr[i].grad_w = None if gw[i] is None else L.ptr(gw[i])
+            arr[i].grad_v, arr[i].grad_g = L.ptr(gv[i]), L.ptr(gg[i])
+            arr[i].rows, arr[i].cols = vs[i].shape
+        L.check(L.lib().nr_weight_norm_bwd(arr, n, _st(vs[0])))
+        return (None, *gv, *gg)
+
+
+def weight_norm_all(layers):
+    """[l.effective_weight() for l in layers] (weight-normed WNLinear layers) with one launch each way"""
+    ls = list(layers)
+    if len(ls) > L.WN_MAX:
+        return [l.effective_weight() for l in ls]
+    return list(_WeightNormAll.apply(len(ls), *[l.weight_v for l in ls], *[l.weight_g for l in ls]))
+
+
 def effective_weights(surface):
     """The SDF layers' weight-normed weights (differentiable), to share between evaluations of one step"""
-    return [l.effective_weight() for l in surface.surface_fc_layers]
+    return weight_norm_all(surface.surface_fc_layers)
 
 
 def sdf_nablas(surface, x, want_feat, Ws=None, feat_from=0):
@@ -1018,7 +1065,7 @@ def sdf_nablas(surface, x, want_feat, Ws=None, feat_from=0):
 
 
 def radiance(net, x, v, nrm, feat):
-    Ws = [l.effective_weight() for l in net.layers]
+    Ws = weight_norm_all(net.layers)
     bs = [l.bias for l in net.layers]
     view = net.use_view_dirs
     if uses_train_gemm(net):
