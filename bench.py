@@ -374,8 +374,8 @@ def train_roofline(kstats, dt, steps, census=None):
     """Training step: the dominant library kernel is the layer GEMM (nr_train_gemm), whose launches
     stream [P, <=288] fp32 activations: HBM-bound.  achieved = algorithmic bytes of its calls (inputs,
     outputs, epilogue operands; training.TG_BYTES, counted per call by the host) / their device time.
-    share_of_step: the library kernels' device time / the step time (the rest: hipBLASLt weight
-    gradients and the fp32 radiance forward, torch elementwise, Adam)."""
+    share_of_step: the library kernels' device time / the step time (the rest: torch elementwise and
+    the losses, Adam; r05: no hipBLASLt GEMM is left in the step)."""
     from neurecon_amd import training as T
     n, ms, _ = kstats.get('train_gemm', (0, 0.0, 0.0))
     lib_ms = sum(v[1] for v in (census if census is not None else kstats).values())
