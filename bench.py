@@ -53,7 +53,7 @@ RAY_FLOP_REF = 704.8e6
 RAY_FLOP = 2.0 * (255 * (MAC_SDF_FWD + MAC_SDF_BWD) + 127 * MAC_RAD)
 # HBM-side bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc passes of this bench,
 # tools/gpu_pmc.sh); counters cannot be read live, so the latest committed summary is reported.
-PMC_SUMMARY = {'f16x3': 'profiles/r04/f16x3_pmc_summary.json'}  # tools/gpu_prof_r04.sh (PMC passes of the default bench)
+PMC_SUMMARY = {'f16x3': 'profiles/r05/f16x3_pmc_summary.json'}  # tools/gpu_final_r05.sh PROFILES=1 (PMC passes of the default bench)
 # matrix-pipe occupancy and effective clock per nabla launch type (rocprofv3 GRBM_GUI_ACTIVE and
 # SQ_VALU_MFMA_BUSY_CYCLES passes of this bench, tools/gpu_mfma_r05.sh -> tools/mfma_summary.py)
 MFMA_SUMMARY = 'profiles/r05/mfma_summary.json'
@@ -352,7 +352,7 @@ def mfma_evidence(per_type):
 HBM_PEAK_TBPS = 8.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
-TRAIN_PMC_SUMMARY = 'profiles/r04/train_pmc_summary.json'  # tools/gpu_prof_r04.sh (PMC passes of --workload train)
+TRAIN_PMC_SUMMARY = 'profiles/r05/train_pmc_summary.json'  # tools/gpu_final_r05.sh PROFILES=1 (PMC passes of --workload train)
 
 
 def train_pmc_traffic(prefix):

@@ -139,3 +139,37 @@ def test_wgrad_workspace_sizes(lib):
     assert one >= 256 * 256 * 4 * 8
     assert lib.nr_wgrad_workspace_bytes(65536, 3, 256, 1) <= one
     assert lib.nr_wgrad_workspace_bytes(33, 17, 5, 1) > 0
+
+
+def test_r05_training_entries_reject_bad_arguments(lib):
+    """nr_weight_norm_*, nr_nerf_train_* and nr_radiance_train_fwd32 check their arguments before any HIP
+    call (fake device pointers: nothing is dereferenced on the error paths)"""
+    from neurecon_amd import _lib
+    P = ctypes.c_void_p
+    # weight norm: layer count, shapes, outputs
+    assert lib.nr_weight_norm_fwd(None, 0, None) == -1 and 'NR_WN_MAX' in lib.nr_last_error().decode()
+    arr = (_lib.NrWnLayer * 17)()
+    assert lib.nr_weight_norm_fwd(arr, 17, None) == -1
+    one = (_lib.NrWnLayer * 1)()
+    one[0].v, one[0].g, one[0].norm, one[0].w, one[0].rows, one[0].cols = 0x1000, 0x2000, 0x3000, 0x4000, 0, 8
+    assert lib.nr_weight_norm_fwd(one, 1, None) == -1 and 'bad layer' in lib.nr_last_error().decode()
+    one[0].rows = 4
+    assert lib.nr_weight_norm_bwd(one, 1, None) == -1 and 'null output' in lib.nr_last_error().decode()
+    # NeRF++ training: the forward needs the fp32 pack and an aligned embedding; the backward every pointer
+    nd = _lib.NrNerfDesc(8, 256, 4, 4, 10, 4, _lib.PREC_F16X3)
+    assert lib.nr_nerf_train_packed_bytes(ctypes.byref(nd)) > 8 * 8 * 33 * 1024  # 8 ops of 8 x 33 KB chunks + views^T
+    h8 = (P * 8)(*([0x10000] * 8))
+    rc = lib.nr_nerf_train_fwd32(ctypes.byref(nd), 0x1000, 0x2000, 0x3000, 64, h8, 0x4000, 0x5000, 0x6000, 0x7000, None)
+    assert rc == -1 and 'NR_PREC_FP32' in lib.nr_last_error().decode()
+    nd.precision = _lib.PREC_FP32
+    rc = lib.nr_nerf_train_fwd32(ctypes.byref(nd), 0x1000, 0x2004, 0x3000, 64, h8, 0x4000, 0x5000, 0x6000, 0x7000, None)
+    assert rc == -1 and '16-byte' in lib.nr_last_error().decode()
+    gz = (P * 8)(*([0x20000] * 7 + [0]))
+    rc = lib.nr_nerf_train_bwd32(ctypes.byref(nd), 0x1000, 0x2000, 0x3000, h8, None, None, 64, 0x4000, 0x5000, 0x6000,
+                                 gz, None)
+    assert rc == -1 and 'null layer pointer' in lib.nr_last_error().decode()
+    # the radiance training forward: the small-input stride covers the small inputs
+    rd = _lib.NrRadDesc(4, 256, -1, 4, 256, _lib.PREC_FP32)
+    rc = lib.nr_radiance_train_fwd32(ctypes.byref(rd), 0x1000, 0x2000, 0x3000, 8, 64, 0x4000, 0x5000, 0x6000, 0x7000,
+                                     0x8000, None)
+    assert rc == -1 and 'ld_small' in lib.nr_last_error().decode()
