@@ -1226,7 +1226,7 @@ constexpr float kC = 0.0069314749f;
 #ifdef NR_EXP_STAMPS
 // timing experiment: per-wave shader-clock totals of the four phases of a chunk iteration (VMEM
 // issue, MFMA loop + epilogue stages, bias + vmcnt wait, barrier), copied out at the end of the launch
-constexpr int kStampPh = 5;  // 4 phases + iteration count
+constexpr int kStampPh = 6;  // 4 phases + iteration count (tgemm_kernel: tile start) + tgemm's epilogue
 __device__ unsigned long long g_nr_stamps[2048 * 8 * kStampPh];
 __device__ __forceinline__ unsigned long long* stamp_lds() {
   __shared__ unsigned long long s_stamp[kW4 * kStampPh];
@@ -3156,6 +3156,18 @@ __device__ __forceinline__ uint32_t tg_elem(bool blk, uint32_t p, uint32_t ld, u
   return blk ? (((p >> 4) * (ld >> 4) + (c >> 4)) << 8) + ((p & 15u) << 4) + (c & 15u) : p * ld + c;
 }
 
+// NR_TG_XPF: the next tile's input blocks are loaded during this tile's chunk loop (two per chunk, asm
+// loads counted with the chunk's other VMEM), so a tile starts from registers instead of a chip-wide
+// load burst (tools/tg_driver.py --stamps: the tile start was 27-37 % of the wave time)
+#ifndef NR_TG_XPF
+#define NR_TG_XPF 1
+#endif
+#ifndef NR_TG_XPF_PER  // prefetched blocks issued per chunk iteration
+#define NR_TG_XPF_PER 2
+#endif
+#ifndef NR_TG_XPF_SPADJ  // blocks the adjoint GEMMs prefetch (their three epilogue tensors fill the registers)
+#define NR_TG_XPF_SPADJ 8
+#endif
 template <int KB, int KB2, int NBO, int NB2, int MODE>
 __global__ __attribute__((amdgpu_flat_work_group_size(kT4, kT4), amdgpu_waves_per_eu(kWPE, kWPE)))
 void tgemm_kernel(TGemmArgs a) {
@@ -3175,20 +3187,50 @@ void tgemm_kernel(TGemmArgs a) {
   constexpr int NA = kG ? 3 : (kA ? 1 : 0);
   // the g zdot term: g from a tensor, or the op's per-row vector (g_row: W8[0, :] for layer 7)
   const bool has_g = kG && (a.g != nullptr || a.g_row), g_tensor = kG && a.g != nullptr;
+#ifdef NR_EXP_STAMPS  // timing experiment: phases 0-3 of the chunk iterations as sdf4_kernel's, 4 = tile start
+  if (lane == 0)
+    for (int i = 0; i < kStampPh; ++i) stamp_lds()[wave * kStampPh + i] = 0;
+#endif
+  // next-tile prefetch: x1 blocks [0, NPF) (single-segment inputs; SPADJ holds 3 epilogue tensors in
+  // registers and prefetches half)
+  constexpr int NPF = (NR_TG_XPF && KB2 == 0) ? ((MODE == TG_SPADJ ? NR_TG_XPF_SPADJ : (KB1 < 2 * NCH ? KB1 : 2 * NCH)) & ~1) : 0;
+  const bool blk1 = (a.blocked & NR_BLK_X1) != 0;
+  const bool pf_ok = NPF > 0 && (blk1 || ((a.ld1 | (int64_t)((uintptr_t)a.x1 >> 2)) & 3) == 0);
+  float4 Xn[NPF > 0 ? NPF : 1];
+  bool have_pf = false;
+  int nst_prev = 0;  // stores the previous tile's last flush issued (younger than its prefetch)
   for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < a.P; base += (int64_t)gridDim.x * kPointsPerWG) {
+    NR_STAMP(ts0);
     const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < a.P;
     const int64_t p = base + wave * 16 + j;
     const bool valid = p < a.P;
     const uint32_t pc = (uint32_t)(valid ? p : a.P - 1);
+    // this lane's row of the next tile (clamped: the last tile's rows are re-read, never stored)
+    const uint32_t pcn = (uint32_t)min(p + (int64_t)gridDim.x * kPointsPerWG, a.P - 1);
     // ---- input operand: [x1 blocks ; x2 blocks], split at the exact per-point max ----
     f16x8 Uh[1][12], Ul[1][12];
     float xinv[1];
     {
       float4 X[KB];
-      auto load_seg = [&](const float* src, int64_t ld, int n, int b0, int nb, bool blk) {
+      int b_first = 0;  // first x1 block loaded here (the ones before came with the previous tile)
+      if constexpr (NPF > 0) {
+        if (have_pf) {
+          wait_vmcnt(nst_prev);  // the prefetch has landed; the final flush's stores may still fly
+#pragma unroll
+          for (int b = 0; b < NPF; ++b) {
+            tg_pin(Xn[b]);
+            const int col = 16 * b + 4 * g;  // columns past n1 read as zeros, as load_seg's
+            X[b] = make_float4(col + 0 < a.n1 ? Xn[b].x : 0.f, col + 1 < a.n1 ? Xn[b].y : 0.f,
+                               col + 2 < a.n1 ? Xn[b].z : 0.f, col + 3 < a.n1 ? Xn[b].w : 0.f);
+          }
+          b_first = NPF;
+        }
+      }
+      auto load_seg = [&](const float* src, int64_t ld, int n, int b0, int nb, bool blk, int bs = 0) {
         const bool vec = blk || ((ld | (int64_t)((uintptr_t)src >> 2)) & 3) == 0;
 #pragma unroll
         for (int b = 0; b < nb; ++b) {
+          if (b < bs) continue;
           const int col = 16 * b + 4 * g;
           const float* e = src + tg_elem(blk, pc, (uint32_t)ld, (uint32_t)col);
           float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -3202,7 +3244,7 @@ void tgemm_kernel(TGemmArgs a) {
           X[b0 + b] = v;
         }
       };
-      load_seg(a.x1, a.ld1, a.n1, 0, KB1, (a.blocked & NR_BLK_X1) != 0);
+      load_seg(a.x1, a.ld1, a.n1, 0, KB1, blk1, b_first);
       if constexpr (KB2 > 0) load_seg(a.x2, a.ld2, a.n2, KB1, KB2, (a.blocked & NR_BLK_X2) != 0);
       float m = 0.0f;
 #pragma unroll
@@ -3238,6 +3280,9 @@ void tgemm_kernel(TGemmArgs a) {
       return n;
     };
     aux_issue(0, aux[0]);
+#ifdef NR_EXP_STAMPS
+    stamp_add(4, stamp_now() - ts0);
+#endif
     float dpart = 0.0f;
     // chunk c's outputs (y, y2, y3 per block) are stored at the start of iteration c+1, after that
     // iteration's loads and DMA: younger than everything its counted wait must see landed
@@ -3272,6 +3317,7 @@ void tgemm_kernel(TGemmArgs a) {
     for (int c = 0; c < NCH; ++c) {
       const char* opc = a.op;
       asm volatile("" : "+s"(opc));
+      NR_STAMP(t0);
       int npend = 0;
       if (c + 1 < NCH) npend += aux_issue(c + 1, aux[(c + 1) & 1]);
       if (c + 2 < NCH) {
@@ -3282,9 +3328,24 @@ void tgemm_kernel(TGemmArgs a) {
         npend += WStream4<CB>::template npieces<CB>();
       }
       if (c > 0) npend += flush(c - 1);
+      if constexpr (NPF > 0) {  // the next tile's x1 blocks 2c, 2c+1
+        constexpr int PER = NR_TG_XPF_PER;
+        if (pf_ok && has_next && PER * c < NPF) {
+#pragma unroll
+          for (int bb = 0; bb < PER; ++bb) {
+            const int b = PER * c + bb;
+            if (b < NPF) {
+              Xn[b] = tg_load(a.x1, tg_elem(blk1, pcn, (uint32_t)a.ld1, (uint32_t)(16 * b + 4 * g)) * 4u);
+              ++npend;
+            }
+          }
+        }
+      }
+      NR_STAMP(t1);
       const float4* A = ws.buf();
       f32x4 acc[1][2] = {};
       mma4<NS>(A, Uh, Ul, acc, lane, [&](int) {});
+      NR_STAMP(t2);
       const float inv = xinv[0] * A[2 * KB * 64 + 8].x;
       float4 z[2];
       if (a.use_bias) {
@@ -3297,6 +3358,7 @@ void tgemm_kernel(TGemmArgs a) {
       // everything issued before this iteration has landed (this chunk's epilogue tensors, chunk c+1's
       // weights); pinning keeps every use of the asm-loaded registers behind the wait
       wait_vmcnt(npend);
+      NR_STAMP(t3);
       if constexpr (NA > 0) {
 #pragma unroll
         for (int t = 0; t < NA; ++t) { tg_pin(aux[c & 1][t][0]); tg_pin(aux[c & 1][t][1]); }
@@ -3360,17 +3422,32 @@ void tgemm_kernel(TGemmArgs a) {
           pv[1][b] = make_float4(o2[0], o2[1], o2[2], o2[3]);
         }
       }
+      NR_STAMP(t3e);
       ws.flip(0);  // all older VMEM is complete (waited above): the barrier alone rotates the ring
+#ifdef NR_EXP_STAMPS
+      const uint64_t t4 = stamp_now();
+      stamp_add(0, t1 - t0);   // VMEM issue: epilogue operands, weight DMA, previous chunk's stores
+      stamp_add(1, t2 - t1);   // MFMA loop
+      stamp_add(2, t3 - t2);   // bias + counted vmcnt wait
+      stamp_add(5, t3e - t3);  // epilogue VALU
+      stamp_add(3, t4 - t3e);  // barrier
+#endif
     }
-    flush(NCH - 1);
+    nst_prev = flush(NCH - 1);
     if constexpr (MODE == TG_SOFTPLUS) {
       if (a.dot) {
         const float v = wave_sum4(dpart) + a.dot_bias;
         if (valid && g == 0) a.dot[p] = v;
       }
     }
+    have_pf = pf_ok && has_next;
   }
   wait_vmcnt(0);
+#ifdef NR_EXP_STAMPS
+  if (lane == 0 && blockIdx.x < 2048)
+    for (int i = 0; i < kStampPh; ++i)
+      g_nr_stamps[(blockIdx.x * kW4 + wave) * kStampPh + i] = stamp_lds()[wave * kStampPh + i];
+#endif
 }
 
 // (input blocks, output blocks, epilogue) instances the training path uses (neurecon_amd/training.py)

@@ -89,6 +89,10 @@ VARIANTS = {
     # r05: fp32 magic-number slab codes (one fma to write, one fma + mul to read; 8 instead of 6 KB / point)
     'slab32': ['-DNR_SLAB32'],
     'slab32prio': ['-DNR_SLAB32', '-DNR_SDF4_PRIO'],
+    # r05: tgemm_kernel without the next-tile input prefetch (the r04 schedule; valid results)
+    'tgxpf0': ['-DNR_TG_XPF=0'],
+    'tgxpf4': ['-DNR_TG_XPF_PER=4'],
+    'tgxpf_p4s12': ['-DNR_TG_XPF_PER=4', '-DNR_TG_XPF_SPADJ=12'],
     # nr_wgrad slice count from $NR_WGRAD_SLICES (tools/wgrad_bench.py)
     'wg_slices_env': ['-DNR_WG_EXP_SLICES_ENV'],
 }

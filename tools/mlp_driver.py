@@ -47,13 +47,13 @@ def main():
         import ctypes
         import numpy as np
         from neurecon_amd import _lib as L
-        buf = np.zeros(2048 * 8 * 5, dtype=np.uint64)
+        buf = np.zeros(2048 * 8 * 6, dtype=np.uint64)
         nw = L.lib().nr_exp_stamps(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(buf.size))
-        v = buf.reshape(-1, 5)
+        v = buf.reshape(-1, 6)
         v = v[v[:, 4] > 0]
         tot = v[:, :4].sum(1)
         names = ['vmem issue', 'mfma loop', 'bias+vmcnt', 'barrier']
-        print(f'waves {len(v)} (per WG {nw // 5}), chunk iterations/wave {v[:, 4].mean():.0f}, '
+        print(f'waves {len(v)} (per WG {nw // 6}), chunk iterations/wave {v[:, 4].mean():.0f}, '
               f'clocks/iteration {tot.mean() / v[:, 4].mean():.0f}')
         for i, n in enumerate(names):
             print(f'  {n:12s} {v[:, i].mean() / v[:, 4].mean():8.0f} clk/iter  {100 * v[:, i].sum() / tot.sum():5.1f} %')
