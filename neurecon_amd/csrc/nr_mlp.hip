@@ -1151,6 +1151,13 @@ struct WStream4 {
 #endif
     cur = nextr(cur);
   }
+  // the caller has waited for everything the next chunk needs (tgemm_kernel's counted waits)
+  __device__ __forceinline__ void flip_nowait() {
+#ifndef NR_EXP_NO_BARRIER
+    __syncthreads();
+#endif
+    cur = nextr(cur);
+  }
 };
 
 // one k-step pair of output blocks x kNC point columns: 6 kNC MFMAs per k-step
@@ -3168,6 +3175,12 @@ __device__ __forceinline__ uint32_t tg_elem(bool blk, uint32_t p, uint32_t ld, u
 #ifndef NR_TG_XPF_SPADJ  // blocks the adjoint GEMMs prefetch (their three epilogue tensors fill the registers)
 #define NR_TG_XPF_SPADJ 8
 #endif
+#ifndef NR_TG_RING  // weight-ring slots (4: three chunks in flight, ops of >= 4 chunks)
+#define NR_TG_RING 3
+#endif
+#ifndef NR_TG_DRAIN
+#define NR_TG_DRAIN 0
+#endif
 template <int KB, int KB2, int NBO, int NB2, int MODE>
 __global__ __attribute__((amdgpu_flat_work_group_size(kT4, kT4), amdgpu_waves_per_eu(kWPE, kWPE)))
 void tgemm_kernel(TGemmArgs a) {
@@ -3176,11 +3189,17 @@ void tgemm_kernel(TGemmArgs a) {
   constexpr int NCH = NBO / 2, NS = KB / 2, KB1 = KB - KB2, NB1 = NBO - NB2;
   static_assert(NCH >= 2, "the 2-ahead stream needs >= 2 chunks");
   static_assert(NB1 % 2 == 0, "the output split falls between chunks");
-  __shared__ __attribute__((aligned(16))) char smem[kRing * CB];
-  WStream4<CB> ws{smem, nullptr, 0, 0, 0};
+  constexpr int TRING = (NR_TG_RING == 4 && NCH >= 4 && 4 * CB <= 160 * 1024) ? 4 : 3;
+  constexpr int LA = TRING - 1;  // chunks issued ahead of the one being computed
+  using WS = WStream4<CB, TRING>;
+  __shared__ __attribute__((aligned(16))) char smem[TRING * CB];
+  WS ws{smem, nullptr, 0, 0, 0, 0};
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int j = lane & 15, g = lane >> 4;
-  ws.template start<CB, CB>(uniform_ptr(a.op), uniform_ptr(a.op) + CB);
+  if constexpr (TRING == 4)
+    ws.template start<CB, CB, CB>(uniform_ptr(a.op), uniform_ptr(a.op) + CB, uniform_ptr(a.op) + 2 * CB);
+  else
+    ws.template start<CB, CB>(uniform_ptr(a.op), uniform_ptr(a.op) + CB);
   // epilogue tensors by mode: TG_MUL / TG_RELUMASK read a; TG_SPADJ reads a (softplus'), g, zdot
   constexpr bool kA = MODE == TG_MUL || MODE == TG_SPADJ || MODE == TG_RELUMASK;
   constexpr bool kG = MODE == TG_SPADJ;
@@ -3199,6 +3218,7 @@ void tgemm_kernel(TGemmArgs a) {
   float4 Xn[NPF > 0 ? NPF : 1];
   bool have_pf = false;
   int nst_prev = 0;  // stores the previous tile's last flush issued (younger than its prefetch)
+  int rest_prev = 0;  // VMEM the previous chunk iteration issued after its epilogue-operand loads
   for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < a.P; base += (int64_t)gridDim.x * kPointsPerWG) {
     NR_STAMP(ts0);
     const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < a.P;
@@ -3320,12 +3340,13 @@ void tgemm_kernel(TGemmArgs a) {
       NR_STAMP(t0);
       int npend = 0;
       if (c + 1 < NCH) npend += aux_issue(c + 1, aux[(c + 1) & 1]);
-      if (c + 2 < NCH) {
-        ws.template issue<CB>(opc + (c + 2) * CB);
-        npend += WStream4<CB>::template npieces<CB>();
+      const int naux = npend;  // what this iteration issues after its epilogue-operand loads
+      if (c + LA < NCH) {
+        ws.template issue<CB>(opc + (c + LA) * CB);
+        npend += WS::template npieces<CB>();
       } else if (has_next) {
-        ws.template issue<CB>(opc + (c + 2 - NCH) * CB);
-        npend += WStream4<CB>::template npieces<CB>();
+        ws.template issue<CB>(opc + (c + LA - NCH) * CB);
+        npend += WS::template npieces<CB>();
       }
       if (c > 0) npend += flush(c - 1);
       if constexpr (NPF > 0) {  // the next tile's x1 blocks 2c, 2c+1
@@ -3356,8 +3377,11 @@ void tgemm_kernel(TGemmArgs a) {
         z[1] = fma4s(acc[0][1], inv, make_float4(0.f, 0.f, 0.f, 0.f));
       }
       // everything issued before this iteration has landed (this chunk's epilogue tensors, chunk c+1's
-      // weights); pinning keeps every use of the asm-loaded registers behind the wait
-      wait_vmcnt(npend);
+      // weights); pinning keeps every use of the asm-loaded registers behind the wait.  With the 4-slot
+      // ring the previous iteration's weight DMA, stores and prefetch may still fly (issued after its
+      // epilogue-operand loads; chunk c+1's weights went out one iteration before that)
+      wait_vmcnt(npend + (TRING == 4 && c > 0 ? rest_prev : 0));
+      rest_prev = npend - naux;
       NR_STAMP(t3);
       if constexpr (NA > 0) {
 #pragma unroll
@@ -3423,7 +3447,11 @@ void tgemm_kernel(TGemmArgs a) {
         }
       }
       NR_STAMP(t3e);
-      ws.flip(0);  // all older VMEM is complete (waited above): the barrier alone rotates the ring
+      // the counted wait above covered the next chunk's weights, so this iteration's DMA, stores and
+      // prefetch stay in flight across the barrier (r05 with the prefetch: +0.8 % on the training step
+      // alternated; NR_TG_DRAIN=1 drains them here as r04 did; the 4-slot ring, NR_TG_RING=4, +0.7 %)
+      if constexpr (TRING == 3 && NR_TG_DRAIN) ws.flip(0);
+      else ws.flip_nowait();
 #ifdef NR_EXP_STAMPS
       const uint64_t t4 = stamp_now();
       stamp_add(0, t1 - t0);   // VMEM issue: epilogue operands, weight DMA, previous chunk's stores

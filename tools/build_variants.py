@@ -93,6 +93,9 @@ VARIANTS = {
     'tgxpf0': ['-DNR_TG_XPF=0'],
     'tgxpf4': ['-DNR_TG_XPF_PER=4'],
     'tgxpf_p4s12': ['-DNR_TG_XPF_PER=4', '-DNR_TG_XPF_SPADJ=12'],
+    # r05: tgemm weight ring of 4 slots (three chunks in flight) / 3 slots drained at every barrier (r04)
+    'tgring4': ['-DNR_TG_RING=4'],
+    'tgdrain': ['-DNR_TG_DRAIN=1'],
     # nr_wgrad slice count from $NR_WGRAD_SLICES (tools/wgrad_bench.py)
     'wg_slices_env': ['-DNR_WG_EXP_SLICES_ENV'],
 }
