@@ -87,8 +87,9 @@ def parse():
     ap.add_argument('--train-rays', type=int, default=512)
     ap.add_argument('--train-nerfpp', action='store_true',
                     help='--workload train with the NeRF++ background (configs/neus_nomask_blended.yaml)')
-    ap.add_argument('--adam', default='fused', choices=['fused', 'foreach'],
-                    help='torch.optim.Adam implementation of the training workload')
+    ap.add_argument('--adam', default='nr', choices=['nr', 'fused', 'foreach'],
+                    help="the training workload's Adam: nr = neurecon_amd.optim.Adam (one nr_adam_step launch), "
+                         "fused / foreach = torch.optim.Adam's implementations")
     ap.add_argument('--cpu-rays', type=int, default=1024)
     ap.add_argument('--no-frame', action='store_true',
                     help='skip the strong-scaling config-(d) frame leg of the default workload')
@@ -436,7 +437,7 @@ def frame_d_setup(dev, precision, workspace_gb=None):
     return step, H * W
 
 
-def train_setup(dev, precision, n_rays, world, adam='fused', nerfpp=False):
+def train_setup(dev, precision, n_rays, world, adam='nr', nerfpp=False):
     """NeuS training step (configs/neus.yaml: N_rays=512 per rank, perturb=True, with_mask): random
     rays of a synthetic 64x64 image, render with the autograd graph (neurecon_amd.training), the
     reference's losses, backward (DDP gradient all-reduce over RCCL when world > 1), Adam.
@@ -449,9 +450,14 @@ def train_setup(dev, precision, n_rays, world, adam='fused', nerfpp=False):
     if world > 1:
         from torch.nn.parallel import DistributedDataParallel as DDP
         trainer = DDP(trainer, device_ids=[dev.index or 0])
-    # the reference's optimizer (torch.optim.Adam, train.py); fused=True: its single-kernel CUDA/ROCm
-    # implementation of the same update (the default foreach form costs ~0.3 ms of Python per step here)
-    opt = torch.optim.Adam(model.parameters(), lr=5e-4, fused=(adam == 'fused'))
+    # the reference's optimizer (torch.optim.Adam, models/base.py:488): by default neurecon_amd.optim.Adam,
+    # the same update in one nr_adam_step launch (torch's fused form: two multi-tensor launches, ~90 us;
+    # its default foreach form costs ~0.3 ms of Python per step here)
+    if adam == 'nr':
+        from neurecon_amd.optim import Adam
+        opt = Adam(model.parameters(), lr=5e-4)
+    else:
+        opt = torch.optim.Adam(model.parameters(), lr=5e-4, fused=(adam == 'fused'))
     c2w, K = camera(dev)
     g = torch.Generator().manual_seed(1)
     mi = {'intrinsics': K, 'c2w': c2w, 'object_mask': (torch.rand(1, 4096, generator=g) > 0.5).to(dev)}
@@ -670,7 +676,7 @@ def fp32_mode(args, dev, sync):
                                                'launches', 'per_launch_type')}}
 
 
-def config_train(dev, precision, n_rays, steps, warmup, sync, adam='fused', nerfpp=False):
+def config_train(dev, precision, n_rays, steps, warmup, sync, adam='nr', nerfpp=False):
     """NeuS training step, 512 rays (train_setup): wall rays/s, the library's kernel census, and every
     device kernel of one step by name from torch.profiler (the hipBLASLt `Cijk_*` share included)"""
     step = train_setup(dev, precision, n_rays, 1, adam, nerfpp)
@@ -924,7 +930,8 @@ def run(args):
                    'config': {'workload': 'NeuS Trainer.forward + backward (double backward through the nablas) + '
                                           'Adam step', 'rays_per_gpu': args.train_rays, 'samples_per_ray': 128,
                               'parallelism': f'DDP x{world}' if world > 1 else 'single GPU',
-                              'optimizer': f'torch.optim.Adam ({args.adam})'},
+                              'optimizer': 'neurecon_amd.optim.Adam (nr_adam_step)' if args.adam == 'nr' else
+                              f'torch.optim.Adam ({args.adam})'},
                    'roofline': roof}
         else:
             out = {

@@ -510,6 +510,22 @@ typedef struct {
 } NrWnLayer;
 int nr_weight_norm_fwd(const NrWnLayer* layers, int n, void* stream);
 int nr_weight_norm_bwd(const NrWnLayer* layers, int n, void* stream);
+/* One torch.optim.Adam step (train.py:main's optimizer; amsgrad = maximize = False) over up to
+ * NR_ADAM_MAX fp32 parameter tensors in one launch, in place: g += weight_decay * p; m = b1 m + (1 - b1) g;
+ * v = b2 v + (1 - b2) g^2; p -= lr / (1 - b1^step) * m / (sqrt(v) / sqrt(1 - b2^step) + eps) -- the
+ * update of torch's fused Adam (replaces its multi-tensor launches, ~45 us each for the NeuS nets).
+ * step = the step count after this update (>= 1), shared by every tensor of the call.  The hyper-parameters
+ * are doubles (as torch passes them): 1 - beta and the bias corrections are formed in double, then rounded. */
+#define NR_ADAM_MAX 64
+typedef struct {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t n;
+} NrAdamTensor;
+int nr_adam_step(const NrAdamTensor* tensors, int n, int64_t step, double lr, double beta1, double beta2, double eps,
+                 double weight_decay, void* stream);
 int nr_radiance_input(const float* x, const float* v, const float* nrm, const float* feat, int64_t P, int nfreq_view,
                       int use_view_dirs, int wfeat, float* out, void* stream);
 int nr_neus_points(const float* rays_o, const float* rays_d, const float* d_all, int64_t R, int S, float* pts,

@@ -20,6 +20,7 @@ _c_p = ctypes.c_void_p
 _c_i = ctypes.c_int
 _c_i64 = ctypes.c_int64
 _c_f = ctypes.c_float
+_c_d = ctypes.c_double
 _c_sz = ctypes.c_size_t
 
 
@@ -108,6 +109,7 @@ TG_NONE, TG_SOFTPLUS, TG_MUL, TG_SPADJ, TG_RELUMASK = 0, 1, 3, 4, 5
 BLK_X1, BLK_X2, BLK_Y, BLK_YB, BLK_Y2, BLK_Y3, BLK_A, BLK_G, BLK_ZD = 1, 2, 4, 8, 16, 32, 64, 128, 256
 WG_BLK_A0, WG_BLK_A1, WG_BLK_B0, WG_BLK_B1 = 1, 2, 4, 8
 WN_MAX = 16  # NR_WN_MAX: layers per nr_weight_norm_* call
+ADAM_MAX = 64  # NR_ADAM_MAX: tensors per nr_adam_step call
 
 
 class NrTrainGemm(ctypes.Structure):
@@ -139,6 +141,10 @@ class NrWnLayer(ctypes.Structure):
                 ('grad_g', _c_p), ('rows', _c_i), ('cols', _c_i)]
 
 
+class NrAdamTensor(ctypes.Structure):
+    _fields_ = [('param', _c_p), ('grad', _c_p), ('exp_avg', _c_p), ('exp_avg_sq', _c_p), ('n', _c_i64)]
+
+
 class NrKernelStat(ctypes.Structure):
     _fields_ = [('name', ctypes.c_char * 32), ('launches', _c_i64), ('ms', ctypes.c_double),
                 ('units', ctypes.c_double)]
@@ -164,6 +170,7 @@ _SIGS = {
     'nr_nerf_train_packed_bytes': (_c_sz, [ctypes.POINTER(NrNerfDesc)]),
     'nr_weight_norm_fwd': (_c_i, [ctypes.POINTER(NrWnLayer), _c_i, _c_p]),
     'nr_weight_norm_bwd': (_c_i, [ctypes.POINTER(NrWnLayer), _c_i, _c_p]),
+    'nr_adam_step': (_c_i, [ctypes.POINTER(NrAdamTensor), _c_i, _c_i64, _c_d, _c_d, _c_d, _c_d, _c_d, _c_p]),
     'nr_nerf_train_pack': (_c_i, [ctypes.POINTER(NrNerfDesc), ctypes.POINTER(_c_p), ctypes.POINTER(_c_p), _c_p, _c_p]),
     'nr_nerf_train_bwd32': (_c_i, [ctypes.POINTER(NrNerfDesc), _c_p, _c_p, _c_p, ctypes.POINTER(_c_p), _c_p, _c_p,
                                    _c_i64, _c_p, _c_p, _c_p, ctypes.POINTER(_c_p), _c_p]),

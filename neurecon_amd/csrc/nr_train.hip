@@ -13,6 +13,8 @@
 //   adjoint  zbar_l = hbar_l * s_l + g_l * zdot_l * s'_l   (s'_l = 100 s_l (1 - s_l), 0 on torch's
 //            linear branch: softplus_double_backward), dW_l = zbar_l^T hin_l + delta_l^T hdot_in_l
 // This file holds every elementwise step of that recipe plus the NeuS compositing forward/backward.
+#include <cmath>
+
 #include "nr_common.h"
 
 namespace nr {
@@ -290,6 +292,36 @@ __global__ __launch_bounds__(256) void weight_norm_bwd_kernel(WnBatch b) {
   const float a = fdiv(L.g[r], nrm), bcoef = fdiv(dot, fmul(nrm, nrm));
   for (int c = lane; c < L.cols; c += 64) gv[c] = fmul(a, fsub(gw[c], fmul(v[c], bcoef)));
   if (lane == 0) L.grad_g[r] = fdiv(dot, nrm);
+}
+
+// Adam over a batch of parameter tensors: each workgroup owns kAdamChunk consecutive elements of one
+// tensor (chunk0[i] = first chunk of tensor i), thread t updates elements t, t + 256, ... of the chunk
+// (coalesced), the update in the order of torch's fused Adam (FusedAdamKernel, ADAM_MODE::ORIGINAL)
+constexpr int kAdamChunk = 4096;
+struct AdamBatch {
+  NrAdamTensor t[NR_ADAM_MAX];
+  int chunk0[NR_ADAM_MAX + 1];
+  int n;
+  float beta1, beta2, omb1, omb2, eps, wd, step_size, bc2_sqrt;  // omb = 1 - beta, formed in double as torch
+};
+__global__ __launch_bounds__(256) void adam_kernel(AdamBatch b) {
+  const int c = blockIdx.x;
+  int i = 0;
+  while (i + 1 < b.n && c >= b.chunk0[i + 1]) ++i;
+  const NrAdamTensor& T = b.t[i];
+  const int64_t e0 = (int64_t)(c - b.chunk0[i]) * kAdamChunk;
+  const int64_t e1 = e0 + kAdamChunk < T.n ? e0 + kAdamChunk : T.n;
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) {
+    const float p = T.param[e];
+    float g = T.grad[e];
+    if (b.wd != 0.0f) g = fadd(g, fmul(b.wd, p));
+    const float m = fadd(fmul(b.beta1, T.exp_avg[e]), fmul(b.omb1, g));
+    const float v = fadd(fmul(b.beta2, T.exp_avg_sq[e]), fmul(fmul(b.omb2, g), g));
+    const float denom = fadd(fdiv(__fsqrt_rn(v), b.bc2_sqrt), b.eps);
+    T.exp_avg[e] = m;
+    T.exp_avg_sq[e] = v;
+    T.param[e] = fsub(p, fdiv(fmul(b.step_size, m), denom));
+  }
 }
 
 // RadianceNet input cat([x, embed_view(v), normals, feature]) (base.py:379-384), one row per point;
@@ -1233,6 +1265,36 @@ static int wn_launch(const NrWnLayer* layers, int n, void* stream, bool bwd) {
 }
 int nr_weight_norm_fwd(const NrWnLayer* layers, int n, void* stream) { return wn_launch(layers, n, stream, false); }
 int nr_weight_norm_bwd(const NrWnLayer* layers, int n, void* stream) { return wn_launch(layers, n, stream, true); }
+
+int nr_adam_step(const NrAdamTensor* tensors, int n, int64_t step, double lr, double beta1, double beta2, double eps,
+                 double weight_decay, void* stream) {
+  NR_REQUIRE(tensors && n >= 1 && n <= NR_ADAM_MAX && step >= 1, NR_ERR_ARG, "nr_adam_step: 1..NR_ADAM_MAX tensors, step >= 1");
+  NR_REQUIRE(beta1 >= 0.0 && beta1 < 1.0 && beta2 >= 0.0 && beta2 < 1.0 && eps >= 0.0 && lr >= 0.0,
+             NR_ERR_ARG, "nr_adam_step: bad hyper-parameter");
+  AdamBatch b{};
+  b.n = n;
+  b.chunk0[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    const NrAdamTensor& T = tensors[i];
+    NR_REQUIRE(T.param && T.grad && T.exp_avg && T.exp_avg_sq && T.n > 0, NR_ERR_ARG, "nr_adam_step: bad tensor");
+    const int64_t nc = (T.n + kAdamChunk - 1) / kAdamChunk;
+    NR_REQUIRE(b.chunk0[i] + nc < (int64_t)1 << 30, NR_ERR_ARG, "nr_adam_step: too many elements");
+    b.t[i] = T;
+    b.chunk0[i + 1] = b.chunk0[i] + (int)nc;
+  }
+  // torch's fused Adam: step_size = lr / (1 - beta1^step), denom = sqrt(v) / sqrt(1 - beta2^step) + eps
+  b.beta1 = (float)beta1;
+  b.beta2 = (float)beta2;
+  b.omb1 = (float)(1.0 - beta1);
+  b.omb2 = (float)(1.0 - beta2);
+  b.eps = (float)eps;
+  b.wd = (float)weight_decay;
+  b.step_size = (float)(lr / (1.0 - std::pow(beta1, (double)step)));
+  b.bc2_sqrt = (float)std::sqrt(1.0 - std::pow(beta2, (double)step));
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)b.chunk0[n]), dim3(256), 0, (hipStream_t)stream, b);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
 
 int nr_radiance_input(const float* x, const float* v, const float* nrm, const float* feat, int64_t P, int nfreq_view,
                       int use_view_dirs, int wfeat, float* out, void* stream) {

@@ -173,3 +173,29 @@ def test_r05_training_entries_reject_bad_arguments(lib):
     rc = lib.nr_radiance_train_fwd32(ctypes.byref(rd), 0x1000, 0x2000, 0x3000, 8, 64, 0x4000, 0x5000, 0x6000, 0x7000,
                                      0x8000, None)
     assert rc == -1 and 'ld_small' in lib.nr_last_error().decode()
+
+
+def test_adam_step_rejects_bad_arguments(lib):
+    """nr_adam_step checks its table and hyper-parameters before any HIP call"""
+    from neurecon_amd import _lib
+    assert lib.nr_adam_step(None, 0, 1, 1e-3, 0.9, 0.999, 1e-8, 0.0, None) == -1
+    assert 'NR_ADAM_MAX' in lib.nr_last_error().decode()
+    arr = (_lib.NrAdamTensor * 1)()
+    arr[0].param, arr[0].grad, arr[0].exp_avg, arr[0].exp_avg_sq, arr[0].n = 0x1000, 0x2000, 0x3000, 0x4000, 0
+    assert lib.nr_adam_step(arr, 1, 1, 1e-3, 0.9, 0.999, 1e-8, 0.0, None) == -1
+    assert 'bad tensor' in lib.nr_last_error().decode()
+    arr[0].n = 10
+    assert lib.nr_adam_step(arr, 1, 0, 1e-3, 0.9, 0.999, 1e-8, 0.0, None) == -1      # step counts from 1
+    assert lib.nr_adam_step(arr, 1, 1, 1e-3, 1.0, 0.999, 1e-8, 0.0, None) == -1      # beta1 < 1
+    assert 'hyper-parameter' in lib.nr_last_error().decode()
+    assert lib.nr_adam_step(arr, _lib.ADAM_MAX + 1, 1, 1e-3, 0.9, 0.999, 1e-8, 0.0, None) == -1
+
+
+def test_adam_optimizer_rejects_cpu_parameters():
+    """neurecon_amd.optim.Adam has no CPU path: a CPU parameter raises instead of falling back"""
+    import torch
+    from neurecon_amd.optim import Adam
+    p = torch.nn.Parameter(torch.zeros(4))
+    p.grad = torch.ones(4)
+    with pytest.raises(RuntimeError, match='GPU'):
+        Adam([p]).step()

@@ -656,3 +656,54 @@ def test_weight_norm_all_vs_torch():
         l.zero_grad()
     (w2[0] * gw[0]).sum().backward()
     assert float(layers[1].weight_v.grad.abs().max()) == 0.0 and float(layers[1].weight_g.grad.abs().max()) == 0.0
+
+
+@pytest.mark.parametrize('weight_decay', [0.0, 1e-2])
+def test_adam_matches_torch_adam(weight_decay):
+    """neurecon_amd.optim.Adam (nr_adam_step: every tensor in one launch) against torch.optim.Adam's fused
+    and default forms over 6 steps on the NeuS nets' tensor shapes (incl. a scalar, a size just past a
+    4096-element chunk and > 64 tensors, so two launches), two parameter groups at different lr: every
+    parameter and moment within 2e-6 of its scale (fp32, the same update in another rounding order);
+    the state_dicts load into each other and the run continues identically."""
+    from neurecon_amd.optim import Adam
+    torch.manual_seed(5)
+    shapes = [(256, 39), (256,), (257, 256), (1,), (), (4097,), (3, 289)] + [(17, 5)] * 60
+    init = [torch.randn(s, device='cuda') for s in shapes]
+    grads = [[torch.randn(s, device='cuda') for s in shapes] for _ in range(8)]
+
+    def run(make, steps, state=None, start=0):
+        ps = [torch.nn.Parameter(t.clone()) for t in init]
+        opt = make([{'params': ps[:40], 'lr': 1e-3}, {'params': ps[40:], 'lr': 3e-4}])
+        if state is not None:
+            for p, q in zip(ps, state[0]):
+                p.data.copy_(q)
+            opt.load_state_dict(state[1])
+        for k in range(start, start + steps):
+            for p, g in zip(ps, grads[k]):
+                p.grad = g.clone()
+            if k % 3 == 2:
+                ps[5].grad = None  # a parameter without a gradient this step: untouched
+            opt.step()
+        return ps, opt
+
+    kw = dict(betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay)
+    mine, om = run(lambda g: Adam(g, **kw), 6)
+    for ref_kw in (dict(fused=True), dict(foreach=False)):
+        ref, orf = run(lambda g: torch.optim.Adam(g, **kw, **ref_kw), 6)
+        for i, (a, b) in enumerate(zip(mine, ref)):
+            sa, sb = om.state[a], orf.state[b]
+            assert float(sa['step']) == float(sb['step']), i
+            for x, y in ((a, b), (sa['exp_avg'], sb['exp_avg']), (sa['exp_avg_sq'], sb['exp_avg_sq'])):
+                sc = float(y.abs().max()) + 1e-30
+                assert float((x - y).abs().max()) / sc <= 2e-6, (ref_kw, i)
+    # checkpoint interchange: torch's state continues on nr_adam_step and vice versa
+    # (deep copies: load_state_dict keeps tensors already on the parameter's device and dtype by reference)
+    import copy
+    ref, orf = run(lambda g: torch.optim.Adam(g, **kw), 4)
+    a, _ = run(lambda g: Adam(g, **kw), 2, state=([p.detach() for p in ref], copy.deepcopy(orf.state_dict())), start=4)
+    b, _ = run(lambda g: torch.optim.Adam(g, **kw), 2, state=([p.detach() for p in ref], copy.deepcopy(orf.state_dict())),
+               start=4)
+    for x, y in zip(a, b):
+        assert float((x - y).abs().max()) / (float(y.abs().max()) + 1e-30) <= 2e-6
+    with pytest.raises(NotImplementedError):
+        Adam(mine, amsgrad=True)
