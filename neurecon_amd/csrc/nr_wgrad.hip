@@ -188,7 +188,14 @@ struct WgRegs {
   int q;
 };
 
-template <bool VA, bool VB, bool F32 = false>
+// VEC: the B_0^T v row is wanted (a.avec set).  A template parameter, not a runtime test: its loads and
+// accumulators (10 VGPRs) pushed the common launches to the 256-VGPR limit, where the compiler's
+// temporaries land on in-flight load destinations (each such hazard is a vmcnt wait on the prefetch)
+// SAME: both pairs have one geometry (leading dims, blocked bits; every call of the training step), so
+// one set of lane offsets serves both and a k-step's loads need no per-lane select (whose VGPR
+// temporaries at the loop head aliased registers the prologue's loads were still filling: a vmcnt(0)
+// drain once per unrolled iteration)
+template <bool VA, bool VB, bool F32 = false, bool VEC = false, bool SAME = false>
 __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * kStage];
   // per stage: the rescale ratios 2^(e_new - e_old) of the 64 A column quads, then the 32 B quads, and
@@ -212,8 +219,11 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
   const int m0 = mt * kWgM, n0 = nt * kWgN;
   const int mloc = min(kWgM, a.m - m0);
   const bool wvalid = 32 * w < mloc;                   // wave-uniform: this wave has output rows
-  const int64_t KS = a.npairs * a.KP;
-  const int64_t k0 = KS * slice / a.S, k1 = KS * (slice + 1) / a.S;
+  // k-step indices are 32-bit (the host caps P): a 64-bit compare has no scalar form on gfx9, so the
+  // compiler copies an operand into a VGPR -- at this kernel's register budget one an in-flight prefetch
+  // load writes, and the hazard wait (vmcnt(2) at the loop head) drained the 3-deep prefetch every k-step
+  const int KP = (int)a.KP, KS = a.npairs * KP;
+  const int k0 = (int)((int64_t)KS * slice / a.S), k1 = (int)((int64_t)KS * (slice + 1) / a.S);
 
   f32x4 acc[2][8];
 #pragma unroll
@@ -221,16 +231,17 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float4 cs = make_float4(0.f, 0.f, 0.f, 0.f), vs = make_float4(0.f, 0.f, 0.f, 0.f);
-  const bool want_cs = a.part_cs && nt == 0, want_vec = a.avec && mt == 0;
+  const bool want_cs = a.part_cs && nt == 0, want_vec = VEC && mt == 0;
 
   // loader geometry: A lane -> column quad (lane & 7) of the wave's 32 columns, rows (lane >> 3) + 8 j;
   // B lane -> column quad (lane & 3) of the wave's 16 columns, rows (lane >> 2) + 16 j
   const int ac = 32 * w + 4 * (lane & 7), ar = lane >> 3;
   const int bc = 16 * w + 4 * (lane & 3), br = lane >> 2;
   // loop-invariant lane offsets within a k-step's rows, per pair (the pairs may differ in leading dims)
-  uint32_t oa[2][4], ob[2][2], ov[2];
+  constexpr int NQ = SAME ? 1 : 2;
+  uint32_t oa[NQ][4], ob[NQ][2], ov[2];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < NQ; ++q) {
     const int qq = q < a.npairs ? q : 0;
     const bool blka = (a.blocked & (NR_WG_BLK_A0 << qq)) != 0, blkb = (a.blocked & (NR_WG_BLK_B0 << qq)) != 0;
 #pragma unroll
@@ -239,11 +250,11 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
     for (int j = 0; j < 2; ++j) ob[q][j] = lane_off(br + 16 * j, n0 + bc, a.ldb[qq], a.n, true, blkb);
   }
 #pragma unroll
-  for (int j = 0; j < 2; ++j) ov[j] = want_vec ? (uint32_t)((br + 16 * j) * a.ldv) * 4u : kOob;
+  for (int j = 0; j < 2; ++j) ov[j] = VEC && want_vec ? (uint32_t)((br + 16 * j) * a.ldv) * 4u : kOob;
   // live = false (past the slice's last k-step): zero-sized resources, the loads return zeros and touch
   // no memory.  Issued unconditionally, so the compiler counts the loads in flight exactly (a
   // conditional prefetch makes it wait for all of them)
-  auto load = [&](int64_t ks, WgRegs& R, bool live) __attribute__((always_inline)) {
+  auto load = [&](int ks, WgRegs& R, bool live) __attribute__((always_inline)) {
 #ifdef NR_WG_EXP_NO_LOAD
     const float x = (float)(ks & 7) + 0.5f;
     for (int j = 0; j < 4; ++j) R.va[j] = make_float4(x, x, x, x);
@@ -252,19 +263,20 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
     return;
 #endif
     ks = live ? ks : 0;
-    const int q = ks >= a.KP;
-    const int64_t r0 = (ks - (q ? a.KP : 0)) * kWgK;
+    const int q = ks >= KP;
+    const int64_t r0 = (int64_t)(ks - (q ? KP : 0)) * kWgK;
     const int64_t lda = q ? a.lda[1] : a.lda[0], ldb = q ? a.ldb[1] : a.ldb[0];
     const int64_t rows = live ? a.P - r0 : 0;
     const __amdgpu_buffer_rsrc_t ra = rsrc((q ? a.a[1] : a.a[0]) + r0 * lda, rows * lda * 4);
     const __amdgpu_buffer_rsrc_t rb = rsrc((q ? a.b[1] : a.b[0]) + r0 * ldb, rows * ldb * 4);
-    const __amdgpu_buffer_rsrc_t rv = rsrc(a.avec ? a.avec + r0 * a.ldv : a.a[0], a.avec && q == 0 ? rows * a.ldv * 4 : 0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) R.va[j] = ld4<VA>(ra, q ? oa[1][j] : oa[0][j], m0 + ac, a.m);
+    for (int j = 0; j < 4; ++j) R.va[j] = ld4<VA>(ra, SAME ? oa[0][j] : q ? oa[NQ - 1][j] : oa[0][j], m0 + ac, a.m);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      R.vb[j] = ld4<VB>(rb, q ? ob[1][j] : ob[0][j], n0 + bc, a.n);
-      R.vv[j] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rv, ov[j], 0, 0));
+    for (int j = 0; j < 2; ++j) R.vb[j] = ld4<VB>(rb, SAME ? ob[0][j] : q ? ob[NQ - 1][j] : ob[0][j], n0 + bc, a.n);
+    if constexpr (VEC) {
+      const __amdgpu_buffer_rsrc_t rv = rsrc(a.avec + r0 * a.ldv, q == 0 ? rows * a.ldv * 4 : 0);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) R.vv[j] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rv, ov[j], 0, 0));
     }
     R.q = q;
   };
@@ -284,7 +296,8 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
 #endif
     _Float16* S0 = lds + stg * kStage;
     if (want_cs && R.q == 0) cs = add4(cs, add4(add4(R.va[0], R.va[1]), add4(R.va[2], R.va[3])));
-    if (want_vec && R.q == 0) vs = fma4(R.vv[1], R.vb[1], fma4(R.vv[0], R.vb[0], vs));
+    if constexpr (VEC)
+      if (want_vec && R.q == 0) vs = fma4(R.vv[1], R.vb[1], fma4(R.vv[0], R.vb[0], vs));
     if constexpr (F32) {  // fp32 row images: A [32][kAStride floats], B [32][kBStride floats] (no split)
       float* A32 = (float*)S0;
       float* B32 = (float*)(S0 + 2 * kAPlane);
@@ -397,7 +410,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
   load(k0 + 2, R2, k0 + 2 < k1);
   store(0, R0);
   __syncthreads();
-  int64_t ks = k0;
+  int ks = k0;
   // Within a barrier interval the MFMAs read stage stg and the split writes stage stg ^ 1, so their
   // order is free (the kPingPongBit experiment: the two waves of a SIMD in different phases).
   const bool split_first = (w & kPingPongBit) != 0;
@@ -453,7 +466,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(WgKArgs a) {
     cs = add4(cs, shfl_xor4(cs, 32));
     if (lane < 8) *(float4*)(a.part_cs + (int64_t)slice * ldp + m0 + ac) = cs;
   }
-  if (want_vec) {
+  if (VEC && want_vec) {
     vs = add4(vs, shfl_xor4(vs, 4));
     vs = add4(vs, shfl_xor4(vs, 8));
     vs = add4(vs, shfl_xor4(vs, 16));
@@ -530,6 +543,14 @@ __global__ __launch_bounds__(256) void wgrad_reduce(WgRedArgs r) {
     if (is_cs) r.cs[idx] = v;
     else r.vec[idx] = v * r.vscale;
   }
+}
+
+template <bool VA, bool VB, bool F32>
+static void wg_launch(bool vec, bool same, dim3 grid, hipStream_t st, const WgKArgs& k) {
+  if (vec && same) hipLaunchKernelGGL((wgrad_kernel<VA, VB, F32, true, true>), grid, dim3(kWgThreads), 0, st, k);
+  else if (vec) hipLaunchKernelGGL((wgrad_kernel<VA, VB, F32, true, false>), grid, dim3(kWgThreads), 0, st, k);
+  else if (same) hipLaunchKernelGGL((wgrad_kernel<VA, VB, F32, false, true>), grid, dim3(kWgThreads), 0, st, k);
+  else hipLaunchKernelGGL((wgrad_kernel<VA, VB, F32, false, false>), grid, dim3(kWgThreads), 0, st, k);
 }
 
 struct WgPlan {
@@ -621,16 +642,20 @@ int nr_wgrad(const NrWgrad* w, void* stream) {
     ProfScope prof("wgrad", (double)w->npairs * w->P * (w->m + w->n) * 4.0, st);
     const dim3 grid((unsigned)(p.S * p.nmt * p.nnt));
     // S % 8 == 0 needs the grid padded to whole XCD rounds of the mapping (it already is: S * NT)
+    const bool vec = k.avec != nullptr;
+    // one lane-offset geometry for both pairs (a single pair trivially)
+    const int bits0 = w->blocked & (NR_WG_BLK_A0 | NR_WG_BLK_B0), bits1 = (w->blocked >> 1) & (NR_WG_BLK_A0 | NR_WG_BLK_B0);
+    const bool same = w->npairs == 1 || (w->lda[0] == w->lda[1] && w->ldb[0] == w->ldb[1] && bits0 == bits1);
     if (w->fp32) {
-      if (va && vb) hipLaunchKernelGGL((wgrad_kernel<true, true, true>), grid, dim3(kWgThreads), 0, st, k);
-      else if (va) hipLaunchKernelGGL((wgrad_kernel<true, false, true>), grid, dim3(kWgThreads), 0, st, k);
-      else if (vb) hipLaunchKernelGGL((wgrad_kernel<false, true, true>), grid, dim3(kWgThreads), 0, st, k);
-      else hipLaunchKernelGGL((wgrad_kernel<false, false, true>), grid, dim3(kWgThreads), 0, st, k);
+      if (va && vb) wg_launch<true, true, true>(vec, same, grid, st, k);
+      else if (va) wg_launch<true, false, true>(vec, same, grid, st, k);
+      else if (vb) wg_launch<false, true, true>(vec, same, grid, st, k);
+      else wg_launch<false, false, true>(vec, same, grid, st, k);
     } else {
-      if (va && vb) hipLaunchKernelGGL((wgrad_kernel<true, true>), grid, dim3(kWgThreads), 0, st, k);
-      else if (va) hipLaunchKernelGGL((wgrad_kernel<true, false>), grid, dim3(kWgThreads), 0, st, k);
-      else if (vb) hipLaunchKernelGGL((wgrad_kernel<false, true>), grid, dim3(kWgThreads), 0, st, k);
-      else hipLaunchKernelGGL((wgrad_kernel<false, false>), grid, dim3(kWgThreads), 0, st, k);
+      if (va && vb) wg_launch<true, true, false>(vec, same, grid, st, k);
+      else if (va) wg_launch<true, false, false>(vec, same, grid, st, k);
+      else if (vb) wg_launch<false, true, false>(vec, same, grid, st, k);
+      else wg_launch<false, false, false>(vec, same, grid, st, k);
     }
     NR_HIP_CHECK(hipGetLastError());
   }

@@ -98,7 +98,11 @@ VARIANTS = {
     'tgdrain': ['-DNR_TG_DRAIN=1'],
     # nr_wgrad slice count from $NR_WGRAD_SLICES (tools/wgrad_bench.py)
     'wg_slices_env': ['-DNR_WG_EXP_SLICES_ENV'],
+    # r05: nr_wgrad.hip built with -fno-slp-vectorize (VARIANT_FILE_FLAGS; valid results)
+    'wgnoslp': [],
 }
+# flags for one source file of a variant only
+VARIANT_FILE_FLAGS = {'wgnoslp': {'nr_wgrad.hip': ['-fno-slp-vectorize']}}
 
 
 def one(name):
@@ -106,7 +110,9 @@ def one(name):
     objs = []
     for src in B._sources():
         obj = os.path.join(out_dir, f'{name}_{os.path.basename(src)}.o')
-        subprocess.check_call([B.HIPCC] + B.flags_for(src) + ['-DNR_VARIANT_BUILD'] + VARIANTS[name] + ['-c', src, '-o', obj])
+        extra = VARIANT_FILE_FLAGS.get(name, {}).get(os.path.basename(src), [])
+        subprocess.check_call([B.HIPCC] + B.flags_for(src) + ['-DNR_VARIANT_BUILD'] + VARIANTS[name] + extra +
+                              ['-c', src, '-o', obj])
         objs.append(obj)
     lib = os.path.join(out_dir, f'libnrhip_{name}.so')
     subprocess.check_call([B.HIPCC, '-shared', '-fPIC', f'--offload-arch={B.ARCH}', '-o', lib] + objs)

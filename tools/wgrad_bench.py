@@ -13,9 +13,16 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--points', type=int, default=65536)
+    ap.add_argument('--no-blas', action='store_true', help='skip the hipBLASLt comparison')
+    ap.add_argument('--blocked', action='store_true',
+                    help='operands read as 16 x 16 blocked (the training step layout; timing only)')
+    args = ap.parse_args()
     from neurecon_amd.training import _wg, _wgrad, _wgrad2
     g = torch.Generator().manual_seed(3)
-    P = 65536
+    P = args.points
     a1, b1, a2, b2 = (torch.randn(P, 256, generator=g).cuda() for _ in range(4))
     cs = torch.empty(256, device='cuda')
 
@@ -30,13 +37,17 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps * 1e3
-    for name, fn in (('nr_wgrad 1 pair', lambda: _wg([(a1, b1)], colsum=cs)),
-                     ('nr_wgrad 2 pairs', lambda: _wg([(a1, b1), (a2, b2)], colsum=cs)),
+    from neurecon_amd import _lib as L
+    blk = (L.WG_BLK_A0 | L.WG_BLK_A1 | L.WG_BLK_B0 | L.WG_BLK_B1) if args.blocked else 0
+    for name, fn in (('nr_wgrad 1 pair', lambda: _wg([(a1, b1)], colsum=cs, blocked=blk)),
+                     ('nr_wgrad 2 pairs', lambda: _wg([(a1, b1), (a2, b2)], colsum=cs, blocked=blk)),
                      ('hipBLASLt 1 pair', lambda: _wgrad(a1, b1)),
                      ('hipBLASLt 2 pairs', lambda: _wgrad2(a1, b1, a2, b2))):
+        if args.no_blas and 'BLAS' in name:
+            continue
         us = t(fn)
         npairs = 2 if '2' in name else 1
-        print(f'{name}: {us:.1f} us, {npairs * 2 * P * 256 * 4 / us / 1e6:.2f} TB/s of operands '
+        print(f'P={P}{" blocked" if blk else ""} {name}: {us:.1f} us, {npairs * 2 * P * 256 * 4 / us / 1e6:.2f} TB/s of operands '
               f'(NR_WGRAD_SLICES={os.environ.get("NR_WGRAD_SLICES", "-")})', flush=True)
 
 
