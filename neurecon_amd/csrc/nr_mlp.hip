@@ -3181,6 +3181,9 @@ __device__ __forceinline__ uint32_t tg_elem(bool blk, uint32_t p, uint32_t ld, u
 #ifndef NR_TG_DRAIN
 #define NR_TG_DRAIN 0
 #endif
+#ifndef NR_TG_COLD_WAIT  // load_seg's scalar path ends in a compiler-visible vmcnt(0) (see there)
+#define NR_TG_COLD_WAIT 1
+#endif
 template <int KB, int KB2, int NBO, int NB2, int MODE>
 __global__ __attribute__((amdgpu_flat_work_group_size(kT4, kT4), amdgpu_waves_per_eu(kWPE, kWPE)))
 void tgemm_kernel(TGemmArgs a) {
@@ -3260,12 +3263,32 @@ void tgemm_kernel(TGemmArgs a) {
             if (col + 1 < n) v.y = e[1];
             if (col + 2 < n) v.z = e[2];
             if (col + 3 < n) v.w = e[3];
+#if NR_TG_COLD_WAIT
+            // a compiler-visible vmcnt(0) on this (partial-block / unaligned) path: otherwise its loads
+            // stay "maybe in flight" where the paths merge, and the compiler drains every load and store
+            // in flight at each tile start of every launch (the previous tile's stores included)
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
           }
           X[b0 + b] = v;
         }
       };
-      load_seg(a.x1, a.ld1, a.n1, 0, KB1, blk1, b_first);
-      if constexpr (KB2 > 0) load_seg(a.x2, a.ld2, a.n2, KB1, KB2, (a.blocked & NR_BLK_X2) != 0);
+#if NR_TG_COLD_WAIT
+      if constexpr (NPF == KB1 && KB2 == 0) {
+        // the prefetch covers every input block: the loads below run on the cold path only (the first
+        // tile, or inputs the prefetch cannot take), which ends in its own compiler-visible vmcnt(0) --
+        // so on the prefetched path the compiler has no load of its own to wait for before the split
+        // (it waited vmcnt(0) there, draining the previous tile's epilogue stores at every tile start)
+        if (!have_pf) {
+          load_seg(a.x1, a.ld1, a.n1, 0, KB1, blk1, 0);
+          __builtin_amdgcn_s_waitcnt(0x0F70);
+        }
+      } else
+#endif
+      {
+        load_seg(a.x1, a.ld1, a.n1, 0, KB1, blk1, b_first);
+        if constexpr (KB2 > 0) load_seg(a.x2, a.ld2, a.n2, KB1, KB2, (a.blocked & NR_BLK_X2) != 0);
+      }
       float m = 0.0f;
 #pragma unroll
       for (int b = 0; b < KB; b += 2) m = amax8(m, X[b], X[b + 1]);
