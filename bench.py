@@ -404,13 +404,12 @@ def train_roofline(kstats, dt, steps, census=None):
     return out
 
 
-def frame_d_setup(dev, precision, workspace_gb=None):
-    """config (d): NeuS + NeRF++ (N_outside=32), full 800x600 frame of the config-(d) camera (H=600,
-    W=800, f=800, camera at distance 2), rays sharded over the ranks; the frame's maps are
-    all-gathered (RCCL) inside the timed step (SURVEY §8e)."""
+def frame_d_inputs(dev, precision, workspace_gb=None):
+    """config (d)'s model, rays [1, 480000, 3] and volume_render kwargs (frame_d_setup; also the
+    full-frame test, tests/test_gpu_frame.py)."""
     import numpy as np
-    from neurecon_amd import dist as nd, rend_util
-    from neurecon_amd.frameworks.neus import NeuS, volume_render
+    from neurecon_amd import rend_util
+    from neurecon_amd.frameworks.neus import NeuS
     torch.manual_seed(0)
     surf = dict(use_siren=False, embed_multires=6, radius_init=0.5, geometric_init=True, D=8, W=256, skips=[4],
                 precision=precision)
@@ -430,11 +429,21 @@ def frame_d_setup(dev, precision, workspace_gb=None):
     kw = dict(obj_bounding_radius=1.0, batched=True, calc_normal=True, detailed_output=False, perturb=False,
               N_samples=64, N_importance=64, N_outside=32, upsample_algo='official_solution', N_upsample_iters=4,
               max_workspace_gb=workspace_gb)
+    return model, ro, rd, kw, H * W
+
+
+def frame_d_setup(dev, precision, workspace_gb=None):
+    """config (d): NeuS + NeRF++ (N_outside=32), full 800x600 frame of the config-(d) camera (H=600,
+    W=800, f=800, camera at distance 2), rays sharded over the ranks; the frame's maps are
+    all-gathered (RCCL) inside the timed step (SURVEY §8e)."""
+    from neurecon_amd import dist as nd
+    from neurecon_amd.frameworks.neus import volume_render
+    model, ro, rd, kw, n = frame_d_inputs(dev, precision, workspace_gb)
 
     def step():
         with torch.no_grad():
             return nd.render_sharded(volume_render, ro, rd, model, gather=True, **kw)
-    return step, H * W
+    return step, n
 
 
 def train_setup(dev, precision, n_rays, world, adam='nr', nerfpp=False):

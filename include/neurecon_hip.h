@@ -217,17 +217,17 @@ typedef struct {
    * every sample when drawn. */
   int no_defer;
   /* Memory bound of the render (neus.py:384-397: the reference's `rayschunk` loop is the caller's
-   * memory bound).  Rays per internal chunk <= max(max_chunk_rays, NR_MIN_CHUNK_RAYS) (the
-   * caller's rayschunk is a hint: a 256-ray validation chunk would leave the per-ray kernels a few
-   * CUs; <= 0: no bound), and the chunk is sized so that nr_neus_workspace_bytes() <=
-   * max_workspace_bytes (0: NR_DEFAULT_WORKSPACE_BYTES), down to one 16-ray chunk: the workspace
-   * budget is the memory bound. */
+   * memory bound).  With max_workspace_bytes 0, rays per internal chunk <= max(max_chunk_rays,
+   * NR_MIN_CHUNK_RAYS) (the caller's rayschunk is a hint: a 256-ray validation chunk would leave the
+   * per-ray kernels a few CUs); with an explicit max_workspace_bytes, <= max_chunk_rays exactly
+   * (<= 0: no bound).  Either way the chunk is sized so that nr_neus_workspace_bytes() <=
+   * max_workspace_bytes (0: NR_DEFAULT_WORKSPACE_BYTES), down to one 16-ray chunk. */
   int64_t max_chunk_rays;
   size_t max_workspace_bytes;
 } NrNeusArgs;
 
 #define NR_DEFAULT_WORKSPACE_BYTES ((size_t)4 << 30) /* 4 GiB */
-#define NR_MIN_CHUNK_RAYS 4096 /* floor of max_chunk_rays */
+#define NR_MIN_CHUNK_RAYS 4096 /* floor of max_chunk_rays when max_workspace_bytes is 0 */
 
 size_t nr_neus_workspace_bytes(const NrNeusArgs* a);
 int nr_neus_render(const NrNeusArgs* a, void* stream);
@@ -789,6 +789,13 @@ int nr_profile_enable(int on);
  * recorded launch costs two event markers (and, for compacted launches, a count copy) on the stream */
 int nr_profile_filter(const char* prefix);
 int nr_profile_read(NrKernelStat* out, int max, int* n_out);
+
+/* Kernel selection (no reference counterpart; a tuning switch of this library): on != 0 routes the
+ * f16x3 softplus SDF nets' forward-only evaluations (nr_sdf_forward without nablas or feature, the
+ * UNISURF / root-finding march, sphere tracing, the mesh grid, VolSDF's no-grad sampling) to the
+ * v_mfma_f32_32x32x16_f16 kernel (one wave per SIMD, nr_sdf5.hip) instead of the 16x16x32 one.
+ * Both meet the same bars; their results differ by rounding.  Returns the previous setting. */
+int nr_sdf5_enable(int on);
 
 #ifdef __cplusplus
 }

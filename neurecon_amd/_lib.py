@@ -256,6 +256,7 @@ _SIGS = {
     'nr_wgrad_workspace_bytes': (_c_sz, [_c_i64, _c_i, _c_i, _c_i]),
     'nr_wgrad': (_c_i, [ctypes.POINTER(NrWgrad), _c_p]),
     'nr_profile_enable': (_c_i, [_c_i]),
+    'nr_sdf5_enable': (_c_i, [_c_i]),
     'nr_profile_filter': (_c_i, [ctypes.c_char_p]),
     'nr_profile_read': (_c_i, [ctypes.POINTER(NrKernelStat), _c_i, ctypes.POINTER(_c_i)]),
 }
@@ -284,6 +285,8 @@ def lib():
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
+            if os.environ.get('NR_SDF5') is not None:  # kernel selection (nr_sdf5_enable), for A/B runs
+                L.nr_sdf5_enable(int(os.environ['NR_SDF5']))
             _lib = L
     return _lib
 

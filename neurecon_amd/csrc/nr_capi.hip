@@ -76,6 +76,10 @@ SdfLayout sdf_layout(const NrSdfDesc& d) {
   off = align256(off + 256 * 4);
   L.misc_off = (uint32_t)off;
   off = align256(off + 16);
+  if (L.prec == NR_PREC_F16X3 && !L.siren) {  // the ops again in the 32x32x16 layout (nr_sdf5.hip)
+    L.l32_off = (uint32_t)off;
+    off = align256(off + L.scale_off);
+  }
   L.total = (uint32_t)off;
   return L;
 }
@@ -429,15 +433,19 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   return NR_OK;
 }
 
-// rays per chunk: at most 16384, the caller's max_chunk_rays (its rayschunk) as a hint floored at
-// NR_MIN_CHUNK_RAYS (the reference's validation rayschunk of 256 would leave the per-ray kernels a
-// few CUs; memory is bounded by the workspace budget), and as many as keep the workspace within
+// rays per chunk: at most 16384, the caller's max_chunk_rays (its rayschunk) -- with no explicit
+// workspace budget a hint floored at NR_MIN_CHUNK_RAYS (the reference's validation rayschunk of 256
+// would leave the per-ray kernels a few CUs; memory is bounded by the default budget), exact when the
+// caller also set max_workspace_bytes -- and as many as keep the workspace within
 // max_workspace_bytes (the plan is affine in the chunk's ray count); deferred chunks (8 KB of slabs
 // per sample) are a multiple of 16 rays, so that every launch starts a tile
 static int64_t neus_chunk_rays(const NrNeusArgs* a) {
   const int64_t n = a->n_rays > 0 ? a->n_rays : 1;
   int64_t cap = 16384;
-  if (a->max_chunk_rays > 0) cap = std::min(cap, std::max<int64_t>(a->max_chunk_rays, NR_MIN_CHUNK_RAYS));
+  // the floor applies to a caller that left the memory bound to the library (max_workspace_bytes 0); one
+  // that set a workspace budget gets its max_chunk_rays exactly, as the reference's rayschunk loop
+  if (a->max_chunk_rays > 0)
+    cap = std::min(cap, a->max_workspace_bytes ? a->max_chunk_rays : std::max<int64_t>(a->max_chunk_rays, NR_MIN_CHUNK_RAYS));
   const size_t budget = a->max_workspace_bytes ? a->max_workspace_bytes : NR_DEFAULT_WORKSPACE_BYTES;
   const bool defer = neus_deferred(*a, 16);
   NrNeusArgs q = *a;  // plan sizes with deferral decided as for a 16-ray-multiple chunk
@@ -804,6 +812,13 @@ int nr_sdf_pack(const NrSdfDesc* d, const float* const* W, const float* const* b
   char* dst[kSdfOps];
   for (int i = 0; i < kSdfOps; ++i) dst[i] = P + L.op_off[i];
   if ((rc = launch_pack_ops(ops, dst, kSdfOps, st))) return rc;
+  if (L.l32_off) {  // the 32x32x16 copy of the forward ops (same scales and bounds, rewritten identically)
+    for (int i = 0; i <= F8; ++i) {
+      ops[i].l32 = 1;
+      dst[i] = P + L.l32_off + L.op_off[i];
+    }
+    if ((rc = launch_pack_ops(ops, dst, F8 + 1, st))) return rc;
+  }
   if ((rc = launch_pack_vec(W[8], 0, 256, 256, P + L.w8row0_off, st))) return rc;
   if ((rc = launch_pack_vec(b[8], 0, 1, 4, P + L.misc_off, st))) return rc;
   return NR_OK;

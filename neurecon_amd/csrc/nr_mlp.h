@@ -54,6 +54,8 @@ struct SdfLayout {
   uint32_t bound_off;          // [kSdfOps][2] max row L1 norm, max |bias| per op (f16x3 operand scales)
   uint32_t w8row0_off;         // sdf row of the last layer [256]
   uint32_t misc_off;           // [0] = sdf bias
+  uint32_t l32_off;            // f16x3 softplus nets: the ops again in the 32x32x16 layout (nr_sdf5.hip),
+                               // at l32_off + op_off[i]; 0: none
   uint32_t total;
   int prec;
   int siren;                   // op_off / op_bytes indexed by SirenOp
@@ -127,6 +129,7 @@ struct PackOp {
   const float* bias2;  //   ... and its bias
   int64_t wn2;
   int ld2;
+  int l32;             // f16x3: the 32x32x16 A layout of nr_sdf5.hip instead of the 16x16x32 one
 };
 
 int launch_pack_op(const PackOp& op, char* dst, hipStream_t stream);
@@ -138,6 +141,10 @@ int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t
                const int* P_dev = nullptr, int P_mult = 0);  // P_dev: device count, P_eff = min(P, *P_dev * P_mult)
 // deferred sample nablas (sdf4_kernel STAGE 1 / 2): stage 1 = sdf + slabs per 16-point tile into
 // `slabs` (P/16 x kSlabColBytes); stage 2 = nablas of the tiles tiles[0 .. *n_tiles) from their slabs
+// SDF forward (sdf only) on the 32x32x16 kernel (nr_sdf5.hip): needs L.l32_off
+int launch_sdf5_fwd(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, int nfreq,
+                    hipStream_t stream, const int* P_dev, int P_mult);
+extern int g_sdf5;  // route launch_sdf's forward-only f16x3 launches to it (nr_sdf5_enable)
 int launch_sdf_deferred(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,
                         int nfreq, float4* slabs, const int* tiles, const int* n_tiles, int stage, hipStream_t stream);
 int launch_nerf(const NerfLayout& L, const void* packed, const float* x4, const float* vdir, int64_t vdiv,

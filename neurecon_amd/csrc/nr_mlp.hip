@@ -3634,6 +3634,23 @@ __device__ __forceinline__ void pack_word(const PackOp& op, uint32_t* __restrict
     const int r = w & 3, lane = (w >> 2) & 63, t = w >> 8;
     const int b = t % KB, obl = t / KB;
     dst[e] = __float_as_uint(pack_src(op, 2 * c + obl, lane & 15, b, 4 * (lane >> 4) + r));
+  } else if (op.l32) {  // [s][hl][lane][8 halves], s = 16-feature k-step (nr_sdf5.hip): lane (r, h) element
+                        // el = W[row 32 c + r][16 s + 8 (el >> 2) + 4 h + (el & 3)]
+    const int q = w & 3, lane = (w >> 2) & 63, hl = (w >> 8) & 1, s = w >> 9;
+    const float sc = wscale(op);
+    const int row = lane & 31;
+    uint32_t word = 0;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int el = 2 * q + hh;
+      const int fi = 8 * (el >> 2) + 4 * (lane >> 5) + (el & 3);
+      const float v = pack_src(op, 2 * c + (row >> 4), row & 15, s, fi) * sc;
+      const _Float16 hi = (_Float16)v;
+      const _Float16 lo = (_Float16)(v - (float)hi);
+      const _Float16 out = hl ? lo : hi;
+      word |= (uint32_t)__builtin_bit_cast(uint16_t, out) << (16 * hh);
+    }
+    dst[e] = word;
   } else {  // [obl][s][hl][lane][8 halves]; word = halves (2q, 2q+1)
     const int q = w & 3, lane = (w >> 2) & 63, hl = (w >> 8) & 1, t = w >> 9;
     const int NS = KB / 2, s = t % NS, obl = t / NS;
@@ -3773,6 +3790,8 @@ int launch_pack_vec(const float* src, int off, int nvalid, int n, char* dst, hip
   return NR_OK;
 }
 
+int g_sdf5 = 0;
+
 static int grid_for(int64_t P) {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -3784,6 +3803,8 @@ int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t
                float* feature, int nfreq, void* ws, size_t ws_bytes, hipStream_t stream, const int* P_dev,
                int P_mult) {
   if (P <= 0) return NR_OK;
+  if (g_sdf5 && !nabla && !feature && L.prec == NR_PREC_F16X3 && !L.siren && L.l32_off)
+    return launch_sdf5_fwd(L, packed, pts, P, sdf, nfreq, stream, P_dev, P_mult);
   const int grid = grid_for(P);
   SdfKArgs a{(const char*)packed, L, pts, P, sdf, nabla, feature, (float4*)ws, nfreq, P_dev, P_mult, nullptr, nullptr,
              nullptr};

@@ -7,6 +7,7 @@ launches of a few workgroups each (~45 us each, latency bound); this one launch 
 4096 elements of every tensor (profiles/r05: 90 -> ~6 us per step).  amsgrad, maximize, sparse,
 non-fp32 or CPU parameters are not supported: they raise rather than fall back."""
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _lib as L
 
@@ -25,8 +26,10 @@ class Adam(torch.optim.Optimizer):
         if amsgrad or maximize:
             raise NotImplementedError('neurecon_amd.optim.Adam: amsgrad / maximize are not implemented '
                                       '(use torch.optim.Adam)')
+        # the param_group keys of torch.optim.Adam, so either optimizer loads the other's state_dict
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
-                                      maximize=False))
+                                      maximize=False, foreach=None, capturable=False, differentiable=False,
+                                      fused=None, decoupled_weight_decay=False))
 
     @staticmethod
     def _check(p):
@@ -73,4 +76,10 @@ class Adam(torch.optim.Optimizer):
                     L.check(L.lib().nr_adam_step(arr, len(part), step, float(group['lr']), float(b1), float(b2),
                                                  float(group['eps']), float(group['weight_decay']),
                                                  L.stream_of(part[0].device)))
+                    # the launch wrote through raw pointers: bump every written tensor's version counter as
+                    # torch's in-place ops do, so caches keyed on (data_ptr, _version) -- the packed weights
+                    # of base._version_key -- see the update and repack
+                    for p in part:
+                        st = self.state[p]
+                        increment_version([p, st['exp_avg'], st['exp_avg_sq']])
         return loss

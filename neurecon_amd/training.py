@@ -391,6 +391,8 @@ class NeRFFn(torch.autograd.Function):
         dev = xe.device
         P = xe.shape[0]
         xe, ve = xe.contiguous(), ve.contiguous()
+        if xe.data_ptr() % 16:  # a contiguous view at an unaligned offset: the kernel reads 16-B rows
+            xe = xe.clone()
         desc, pk, _ = _nerf_packs(net, Ws, bs, dev)
         H = [torch.empty(P, 256, device=dev) for _ in range(8)]
         feat = torch.empty(P, 256, device=dev)

@@ -467,7 +467,8 @@ def test_neus_workspace_bound_by_rayschunk(N_outside):
     tools/render_view.py:529) is a hint floored at NR_MIN_CHUNK_RAYS (4096: a 256-ray chunk leaves the
     per-ray kernels a few CUs); the memory bound is the workspace budget, 4 GiB by default
     (NR_DEFAULT_WORKSPACE_BYTES): renders with rayschunk=256, the default, a 0.5 GiB and a 16 GiB budget
-    are bit-identical, and the peak device memory of each is reported."""
+    are bit-identical, and the peak device memory of each is reported.  With an
+    explicit budget set, rayschunk is honoured exactly (256-ray chunks), bit-identical too."""
     from oracle import rays as orays
     from neurecon_amd.frameworks.neus import volume_render
     from neurecon_amd import _lib
@@ -482,7 +483,8 @@ def test_neus_workspace_bound_by_rayschunk(N_outside):
     o, d = ro.cuda(), rd.cuda()
     outs = []
     for name, extra in (('rayschunk=256', dict(rayschunk=256)), ('default (4 GiB)', {}),
-                        ('0.5 GiB budget', dict(max_workspace_gb=0.5)), ('16 GiB budget', dict(max_workspace_gb=16))):
+                        ('0.5 GiB budget', dict(max_workspace_gb=0.5)), ('16 GiB budget', dict(max_workspace_gb=16)),
+                        ('rayschunk=256 exact (4 GiB budget set)', dict(rayschunk=256, max_workspace_gb=4))):
         _lib._WS.clear()
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
@@ -497,6 +499,8 @@ def test_neus_workspace_bound_by_rayschunk(N_outside):
             assert peak <= 4.25, peak
         if name.startswith('0.5'):
             assert peak <= 0.75, peak
+        if 'exact' in name:  # 256-ray chunks: ~a sixteenth of the 4096-ray chunk's workspace
+            assert peak <= 1.0, peak
         outs.append([rgb, depth, ex['mask_volume'], ex['normals_volume']])
     _lib._WS.clear()
     for other in outs[1:]:

@@ -705,5 +705,62 @@ def test_adam_matches_torch_adam(weight_decay):
                start=4)
     for x, y in zip(a, b):
         assert float((x - y).abs().max()) / (float(y.abs().max()) + 1e-30) <= 2e-6
+    # ... and the other way: nr_adam_step's state continues on torch.optim.Adam
+    ref, orm = run(lambda g: Adam(g, **kw), 4)
+    sd = orm.state_dict()
+    assert sd['param_groups'][0].keys() == torch.optim.Adam(ref[:1]).state_dict()['param_groups'][0].keys()
+    a, _ = run(lambda g: torch.optim.Adam(g, **kw), 2, state=([p.detach() for p in ref], copy.deepcopy(sd)), start=4)
+    b, _ = run(lambda g: Adam(g, **kw), 2, state=([p.detach() for p in ref], copy.deepcopy(sd)), start=4)
+    for x, y in zip(a, b):
+        assert float((x - y).abs().max()) / (float(y.abs().max()) + 1e-30) <= 2e-6
+    # the launch writes through raw pointers: every updated tensor's version counter moves, as with torch's
+    # in-place update (the packed-weight caches are keyed on it)
+    v0 = [p._version for p in mine]
+    for p, g in zip(mine, grads[7]):
+        p.grad = g.clone()
+    om.step()
+    assert all(p._version > v for p, v in zip(mine, v0))
     with pytest.raises(NotImplementedError):
         Adam(mine, amsgrad=True)
+
+
+@pytest.mark.parametrize('precision', ['f16x3', 'fp32'])
+def test_neus_training_with_nr_adam_matches_torch_adam(golden, precision):
+    """Three NeuS training steps (Trainer.forward + backward + optimizer step, fixed rays) with
+    neurecon_amd.optim.Adam against the same steps with torch.optim.Adam: every step's loss and the
+    parameters after it agree within the two updates' rounding.  Pins that the packed-weight caches
+    (render pack of the no-grad sampler, training pack, fp32 packs; keyed on the parameters' version
+    counters) follow nr_adam_step's raw-pointer update: with stale packs the second and third steps'
+    losses would be computed from the step-0 weights."""
+    from neurecon_amd.frameworks.neus import Trainer
+    from neurecon_amd.optim import Adam
+    g = golden('neus_train')
+    H, W = int(g['H']), int(g['W'])
+    T = lambda a: torch.from_numpy(np.asarray(a)).cuda()
+    results = []
+    for make in (lambda ps: torch.optim.Adam(ps, lr=1e-3), lambda ps: Adam(ps, lr=1e-3)):
+        m = neus_model(wg.neus_state(seed=int(g['seed'])), precision=precision)
+        m.train()
+        trainer = Trainer(m, device_ids=[0])
+        opt = make(list(m.parameters()))
+        losses = []
+        for it in range(3):
+            opt.zero_grad(set_to_none=True)
+            ret = trainer.forward(_args(), None, {'intrinsics': T(g['K']), 'c2w': T(g['c2w']),
+                                                  'object_mask': T(g['target_mask'])},
+                                  {'rgb': T(g['target_rgb'])}, _kw(H, W), it, device='cuda')
+            loss = torch.mean(ret['losses']['total'])
+            loss.backward()
+            opt.step()
+            losses.append(float(loss))
+        torch.cuda.synchronize()
+        results.append((losses, [p.detach().clone() for p in m.parameters()]))
+    (l_ref, p_ref), (l_nr, p_nr) = results
+    print(precision, 'losses torch', l_ref, 'nr_adam', l_nr)
+    # the steps must move the loss by far more than the tolerance, or the check would not see stale packs
+    assert min(abs(l_ref[1] - l_ref[0]), abs(l_ref[2] - l_ref[1])) > 1e-3 * abs(l_ref[0]), l_ref
+    for a, b in zip(l_nr, l_ref):
+        assert abs(a - b) <= 2e-5 * abs(b), (l_nr, l_ref)
+    for a, b in zip(p_nr, p_ref):
+        sc = float(b.abs().max()) + 1e-30
+        assert float((a - b).abs().max()) <= 2e-5 * sc
