@@ -790,11 +790,13 @@ int nr_profile_enable(int on);
 int nr_profile_filter(const char* prefix);
 int nr_profile_read(NrKernelStat* out, int max, int* n_out);
 
-/* Kernel selection (no reference counterpart; a tuning switch of this library): on != 0 routes the
- * f16x3 softplus SDF nets' forward-only evaluations (nr_sdf_forward without nablas or feature, the
- * UNISURF / root-finding march, sphere tracing, the mesh grid, VolSDF's no-grad sampling) to the
- * v_mfma_f32_32x32x16_f16 kernel (one wave per SIMD, nr_sdf5.hip) instead of the 16x16x32 one.
- * Both meet the same bars; their results differ by rounding.  Returns the previous setting. */
+/* Kernel selection experiment (no reference counterpart): on != 0 routes the f16x3
+ * softplus SDF nets' forward-only evaluations (nr_sdf_forward without nablas or feature, the UNISURF /
+ * root-finding march, sphere tracing, the mesh grid, VolSDF's no-grad sampling) to the
+ * v_mfma_f32_32x32x16_f16 kernel (one wave per SIMD, nr_sdf5.hip) instead of the 16x16x32 one; both
+ * meet the same bars, their results differ by rounding.  Measured 3 % slower, so off by default.
+ * Needs the process started with $NR_SDF5 set (the packs then carry the 32x32x16 layout as well;
+ * nr_sdf_packed_bytes grows): returns -1 otherwise, else the previous setting. */
 int nr_sdf5_enable(int on);
 
 #ifdef __cplusplus

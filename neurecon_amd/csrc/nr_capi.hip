@@ -76,7 +76,7 @@ SdfLayout sdf_layout(const NrSdfDesc& d) {
   off = align256(off + 256 * 4);
   L.misc_off = (uint32_t)off;
   off = align256(off + 16);
-  if (L.prec == NR_PREC_F16X3 && !L.siren) {  // the ops again in the 32x32x16 layout (nr_sdf5.hip)
+  if (g_sdf5_pack && L.prec == NR_PREC_F16X3 && !L.siren) {  // the ops again in the 32x32x16 layout (nr_sdf5.hip)
     L.l32_off = (uint32_t)off;
     off = align256(off + L.scale_off);
   }

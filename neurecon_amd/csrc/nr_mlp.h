@@ -139,12 +139,13 @@ int launch_pack_vec(const float* src, int off, int nvalid, int n, char* dst, hip
 int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,
                float* feature, int nfreq, void* ws, size_t ws_bytes, hipStream_t stream,
                const int* P_dev = nullptr, int P_mult = 0);  // P_dev: device count, P_eff = min(P, *P_dev * P_mult)
-// deferred sample nablas (sdf4_kernel STAGE 1 / 2): stage 1 = sdf + slabs per 16-point tile into
-// `slabs` (P/16 x kSlabColBytes); stage 2 = nablas of the tiles tiles[0 .. *n_tiles) from their slabs
 // SDF forward (sdf only) on the 32x32x16 kernel (nr_sdf5.hip): needs L.l32_off
 int launch_sdf5_fwd(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, int nfreq,
                     hipStream_t stream, const int* P_dev, int P_mult);
-extern int g_sdf5;  // route launch_sdf's forward-only f16x3 launches to it (nr_sdf5_enable)
+extern int g_sdf5;             // route launch_sdf's forward-only f16x3 launches to it (nr_sdf5_enable)
+extern const int g_sdf5_pack;  // $NR_SDF5 set at load: the layout carries the 32x32x16 copy
+// deferred sample nablas (sdf4_kernel STAGE 1 / 2): stage 1 = sdf + slabs per 16-point tile into
+// `slabs` (P/16 x kSlabColBytes); stage 2 = nablas of the tiles tiles[0 .. *n_tiles) from their slabs
 int launch_sdf_deferred(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,
                         int nfreq, float4* slabs, const int* tiles, const int* n_tiles, int stage, hipStream_t stream);
 int launch_nerf(const NerfLayout& L, const void* packed, const float* x4, const float* vdir, int64_t vdiv,

@@ -3791,6 +3791,13 @@ int launch_pack_vec(const float* src, int off, int nvalid, int n, char* dst, hip
 }
 
 int g_sdf5 = 0;
+// the 32x32x16 copy of the ops is laid out and packed only in processes started with NR_SDF5 set (a
+// process-wide constant, so every pack and launch of the process agrees on the layout): the experiment
+// costs nothing elsewhere (training repacks every optimizer step)
+const int g_sdf5_pack = [] {
+  const char* e = getenv("NR_SDF5");
+  return (e && *e) ? 1 : 0;
+}();
 
 static int grid_for(int64_t P) {
   int dev = 0, cus = 256;

@@ -24,6 +24,7 @@
 //    as the 16x16x32 pack (2 KB per input block + the 1 KB bias slot).
 #include "nr_common.h"
 #include "nr_mlp.h"
+#include <type_traits>
 
 namespace nr {
 namespace s5 {
@@ -96,8 +97,11 @@ __device__ __forceinline__ void dma_piece(const char* sbase, uint32_t voff, uint
 // (the last run shifted back to end at the chunk's end: overlapping pieces write identical bytes), and a
 // wave issues its run piece by piece inside the chunk's k-step regions (beside the MFMAs), not as a
 // burst at the chunk start: with one wave per SIMD nothing else would issue MFMAs meanwhile.
-template <int CBMAX>
+// V: experiment bits (nr_sdf5_enable(1 + V)): 1 fragments two k-steps ahead; timing only (results
+// invalid): 2 no epilogue, 4 no weight DMA, 8 no chunk barrier
+template <int CBMAX, int V>
 struct Ring {
+  static constexpr int kV = V;
   char* lds;
   int cur;   // slot of the chunk being computed
   int prev;  // pieces this wave issued in the previous chunk iteration
@@ -136,7 +140,7 @@ struct Ring {
   __device__ __forceinline__ void flip(int n) {
     wait_vmcnt(n + prev);
     prev = n;
-    __syncthreads();
+    if constexpr (!(V & 8)) __syncthreads();
     cur = cur == kRing - 1 ? 0 : cur + 1;
   }
 };
@@ -176,9 +180,11 @@ __device__ __forceinline__ float max_halves(float m) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
-__device__ __forceinline__ float partner(float v) {  // the value of lane l ^ 32
+// v(lane r) + v(lane r + 32) in every lane of the pair (v_permlane32_swap of v with itself returns
+// the low half's values in r[0] and the high half's in r[1], in all 64 lanes)
+__device__ __forceinline__ float sum_halves(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return (threadIdx.x & 32) ? __uint_as_float(r[1]) : __uint_as_float(r[0]);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
 // positional encoding (models/base.py:14-81), as nr_mlp.hip's embed_feature
@@ -192,6 +198,15 @@ __device__ __noinline__ float embed_feature5(int f, float x0, float x1, float x2
   return m < 3 ? sinf(v) : cosf(v);
 }
 
+// compile-time loop: f(std::integral_constant<int, I>{}) for I = 0 .. N-1
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
 __device__ __forceinline__ f16x8 frag(const float4* __restrict__ A, int i, int lane) {
   return __builtin_bit_cast(f16x8, A[i * 64 + lane]);
 }
@@ -199,23 +214,30 @@ __device__ __forceinline__ f16x8 frag(const float4* __restrict__ A, int i, int l
 // One chunk's products: acc += A[32 rows x 16 KB] · B, three f16 products per k-step (lo·hi, hi·lo,
 // hi·hi, the small terms first), fragments read one k-step ahead; stage(s) is VALU work (the previous
 // chunk's epilogue, DMA pieces) placed in k-step s's scheduling region beside its MFMAs.
-template <int KB, int NB, class Stage>
+template <int KB, bool PF2, int NB, class Stage>
 __device__ __forceinline__ void mma5(const float4* __restrict__ A, const f16x8 (&bh)[NB], const f16x8 (&bl)[NB],
                                      f32x16& acc, int lane, Stage&& stage) {
   static_assert(KB <= NB, "operand k-steps");
-  f16x8 nh = frag(A, 0, lane), nl = frag(A, 1, lane);
+  constexpr int D = PF2 ? 2 : 1;  // k-steps of fragment prefetch
+  f16x8 fh[D + 1], fl[D + 1];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (d < KB) {
+      fh[d] = frag(A, 2 * d, lane);
+      fl[d] = frag(A, 2 * d + 1, lane);
+    }
 #pragma unroll
   for (int s = 0; s < KB; ++s) {
-    const f16x8 h = nh, l = nl;
-    if (s + 1 < KB) {
-      nh = frag(A, 2 * (s + 1), lane);
-      nl = frag(A, 2 * (s + 1) + 1, lane);
+    const f16x8 h = fh[s % (D + 1)], l = fl[s % (D + 1)];
+    if (s + D < KB) {
+      fh[(s + D) % (D + 1)] = frag(A, 2 * (s + D), lane);
+      fl[(s + D) % (D + 1)] = frag(A, 2 * (s + D) + 1, lane);
     }
     stage(s);
     acc = mfma32(l, bh[s], acc);
     acc = mfma32(h, bl[s], acc);
     acc = mfma32(h, bh[s], acc);
-    if (s + 1 < KB) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    if (s + D < KB) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -242,43 +264,33 @@ __device__ __forceinline__ void op5(R& ring, const char* __restrict__ op, const 
   static_assert(NCH >= 2, "ops of >= 2 chunks");
   const int h = lane >> 5;
   Z5 zq;
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
+  static_for<0, NCH>([&](auto ci) {
+    constexpr int c = decltype(ci)::value;
     const char* opc = op;
     const char* nxc = nxt;
     asm volatile("" : "+s"(opc), "+s"(nxc));
-    // this iteration's DMA: chunk c + LA of this op, or of the next op
-    const char* dsrc = nullptr;
-    int dkind = 0, npend = 0;
-    if (c + LA < NCH) {
-      dsrc = opc + (c + LA) * CB;
-      dkind = 1;
-      npend = R::template npw<CB>();
-    } else if (nxc) {
-      dsrc = nxc + (c + LA - NCH) * NXT_CB;
-      dkind = 2;
-      npend = R::template npw<NXT_CB>();
-    }
+    // this iteration's DMA: chunk c + LA of this op, or of the next op (with no next op, harmless bytes
+    // of this op into the free slot: the piece count, and with it every wait, stays a constant)
+    constexpr bool OWN = c + LA < NCH;
+    constexpr int DB = OWN ? CB : NXT_CB;
+    const char* dsrc = OWN ? opc + (c + LA) * CB : (nxc ? nxc + (c + LA - NCH) * NXT_CB : opc);
+    constexpr int npend = R::template npw<DB>();
     const int slot = ring.ahead_slot();
     const float4* A = ring.buf();
     f32x16 acc = {};
-    mma5<KB>(A, bh, bl, acc, lane, [&](int s) {
-      {
-        constexpr int N1 = R::template npw<CB>(), N2 = R::template npw<NXT_CB>();
-        if (dkind == 1) {
+    mma5<KB, (R::kV & 1) != 0>(A, bh, bl, acc, lane, [&](int s) {
+      if constexpr (!(R::kV & 4)) {
 #pragma unroll
-          for (int j = 0; j < N1; ++j)
-            if (1 + j * (KB - 1) / N1 == s) ring.template piece<CB>(dsrc, slot, j);
-        } else if (dkind == 2) {
-#pragma unroll
-          for (int j = 0; j < N2; ++j)
-            if (1 + j * (KB - 1) / N2 == s) ring.template piece<NXT_CB>(dsrc, slot, j);
-        }
+        for (int j = 0; j < npend; ++j)
+          if (1 + j * (KB - 1) / npend == s) ring.template piece<DB>(dsrc, slot, j);
       }
-      if (c > 0) {
+      if constexpr (R::kV & 2) {
+        if (s == 0) asm volatile("" : : "a"(zq.acc));
+      } else if constexpr (c > 0) {
+        constexpr int NST = std::decay_t<Epi>::kStages;
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (e * KB / 8 == s) epi(c - 1, zq, e);
+        for (int e = 0; e < NST; ++e)
+          if (e * KB / NST == s) epi(c - 1, zq, e);
       }
     });
     zq.acc = acc;
@@ -292,9 +304,13 @@ __device__ __forceinline__ void op5(R& ring, const char* __restrict__ op, const 
       for (int q = 0; q < 4; ++q) zq.aux[q] = A[2 * KB * 64 + 16 + 2 * q + h];
     }
     ring.flip(npend);
-  }
+  });
+  if constexpr (R::kV & 2) {
+    asm volatile("" : : "a"(zq.acc));
+  } else {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) epi(NCH - 1, zq, e);
+    for (int e = 0; e < std::decay_t<Epi>::kStages; ++e) epi(NCH - 1, zq, e);
+  }
 }
 
 __device__ __forceinline__ float f4(const float4& v, int r) { return r == 0 ? v.x : (r == 1 ? v.y : (r == 2 ? v.z : v.w)); }
@@ -312,53 +328,49 @@ struct FwdEpi5 {
   float& mrun;
   float& sdf_part;
   float t[16], e[16], m[16];
+  // kStages stages of roughly equal issue cost (~48-64 cycles: 16 plain VALU or 8 transcendentals),
+  // two halves of 8 values each, spread over the chunk's k-step regions by op5
+  static constexpr int kStages = 11;
   __device__ __forceinline__ void operator()(int c, const Z5& z, int st) {
-    if (st == 0) {
+    if (st <= 1) {  // A: pre-activations t (100 log2(e) z) and the exp2 argument, half st
+      const int i0 = 8 * st;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
+      for (int k = 0; k < 8; ++k) {
+        const int i = i0 + k;
         t[i] = __builtin_fmaf(z.acc[i], z.inv, f4(z.b[i >> 2], i & 3));
         e[i] = fminf(t[i], 126.0f);
       }
-    } else if (st == 1) {
+    } else if (st <= 3) {  // B: 2^t
+      const int i0 = 8 * (st - 2);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) e[i] = __builtin_amdgcn_exp2f(e[i]);
-    } else if (st == 2) {
+      for (int k = 0; k < 8; ++k) e[i0 + k] = __builtin_amdgcn_exp2f(e[i0 + k]);
+    } else if (st == 4) {  // C: 1 + 2^t
 #pragma unroll
       for (int i = 0; i < 16; ++i) e[i] = e[i] + 1.0f;
+    } else if (st <= 6) {  // D: L = log2(1 + 2^t)
+      const int i0 = 8 * (st - 5);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) e[i] = __builtin_amdgcn_logf(e[i]);
-    } else if (st == 3) {
+      for (int k = 0; k < 8; ++k) e[i0 + k] = __builtin_amdgcn_logf(e[i0 + k]);
+    } else if (st <= 8) {  // E: max(L, t) and the running max (softplus ops) / nothing (F7)
+      const int i0 = 8 * (st - 7);
 #pragma unroll
-      for (int i = 8; i < 16; ++i) e[i] = __builtin_amdgcn_logf(e[i]);
-    } else if (st == 4) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) m[i] = fmaxf(e[i], t[i]);
-    } else if (st == 5) {
+      for (int k = 0; k < 8; ++k) m[i0 + k] = fmaxf(e[i0 + k], t[i0 + k]);
       if constexpr (!LAST) {
         float r = mrun;
 #pragma unroll
-        for (int i = 0; i < 16; i += 2) r = __builtin_fmaxf(r, __builtin_fmaxf(m[i], m[i + 1]));
+        for (int k = 0; k < 8; k += 2) r = __builtin_fmaxf(r, __builtin_fmaxf(m[i0 + k], m[i0 + k + 1]));
         mrun = r;
       }
-    } else if (st == 6) {
+    } else {  // F: k-step 2c + half of the next operand / the sdf row's dot product (F7)
+      const int i0 = 8 * (st - 9);
       if constexpr (LAST) {
         float sp = sdf_part;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) sp = __builtin_fmaf(m[i] * kC2, f4(z.aux[i >> 2], i & 3), sp);
+        for (int k = 0; k < 8; ++k) sp = __builtin_fmaf(m[i0 + k] * kC2, f4(z.aux[(i0 + k) >> 2], k & 3), sp);
         sdf_part = sp;
       } else {
-        const float v[8] = {m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7]};
-        split8a(v, sc * kC2, oh[2 * c], ol[2 * c]);
-      }
-    } else {
-      if constexpr (LAST) {
-        float sp = sdf_part;
-#pragma unroll
-        for (int i = 8; i < 16; ++i) sp = __builtin_fmaf(m[i] * kC2, f4(z.aux[i >> 2], i & 3), sp);
-        sdf_part = sp;
-      } else {
-        const float v[8] = {m[8], m[9], m[10], m[11], m[12], m[13], m[14], m[15]};
-        split8a(v, sc * kC2, oh[2 * c + 1], ol[2 * c + 1]);
+        const float v[8] = {m[i0], m[i0 + 1], m[i0 + 2], m[i0 + 3], m[i0 + 4], m[i0 + 5], m[i0 + 6], m[i0 + 7]};
+        split8a(v, sc * kC2, oh[2 * c + (st - 9)], ol[2 * c + (st - 9)]);
       }
     }
   }
@@ -376,11 +388,12 @@ struct Sdf5Args {
 };
 
 // SDF forward (sdf only), persistent over 128-point tiles
+template <int V>
 __global__ __attribute__((amdgpu_flat_work_group_size(kT, kT), amdgpu_waves_per_eu(1, 1)))
 void sdf5_fwd_kernel(Sdf5Args a) {
   constexpr int C4 = cbytes(4), C16 = cbytes(16), C18 = cbytes(18);
   __shared__ __attribute__((aligned(16))) char smem[kRing * C18];
-  Ring<C18> ring{smem, 0, 0};
+  Ring<C18, V> ring{smem, 0, 0};
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, h = lane >> 5;
   const char* W = a.packed;
@@ -476,7 +489,7 @@ void sdf5_fwd_kernel(Sdf5Args a) {
     // F7: softplus and the sdf row (aux = W8[0, :]) as a running dot product
     op5<16, 16, C4, true, true>(ring, OP(F7), has_next ? OP(F0) : nullptr, Vh, Vl, xinv,
                                 FwdEpi5<18, true>{Uh, Ul, 1.0f, mrun, sdf_part}, lane);
-    const float sdf = (h == 0 ? sdf_part + partner(sdf_part) : partner(sdf_part) + sdf_part) + b8;
+    const float sdf = sum_halves(sdf_part) + b8;
     if (valid && h == 0) a.sdf[p] = sdf;
   }
   wait_vmcnt(0);
@@ -494,7 +507,14 @@ int launch_sdf5_fwd(const SdfLayout& L, const void* packed, const float* pts, in
   const int grid = (int)(need < cus ? need : cus);
   s5::Sdf5Args a{(const char*)packed + L.l32_off, L, pts, P, sdf, nfreq, P_dev, P_mult};
   ProfScope prof("sdf_fwd", (double)P, stream, P_dev, P_mult);
-  hipLaunchKernelGGL(s5::sdf5_fwd_kernel, dim3(grid), dim3(s5::kT), 0, stream, a);
+  switch (g_sdf5) {
+    case 2: hipLaunchKernelGGL(s5::sdf5_fwd_kernel<1>, dim3(grid), dim3(s5::kT), 0, stream, a); break;
+    case 3: hipLaunchKernelGGL(s5::sdf5_fwd_kernel<2>, dim3(grid), dim3(s5::kT), 0, stream, a); break;
+    case 4: hipLaunchKernelGGL(s5::sdf5_fwd_kernel<4>, dim3(grid), dim3(s5::kT), 0, stream, a); break;
+    case 5: hipLaunchKernelGGL(s5::sdf5_fwd_kernel<8>, dim3(grid), dim3(s5::kT), 0, stream, a); break;
+    case 6: hipLaunchKernelGGL(s5::sdf5_fwd_kernel<14>, dim3(grid), dim3(s5::kT), 0, stream, a); break;
+    default: hipLaunchKernelGGL(s5::sdf5_fwd_kernel<0>, dim3(grid), dim3(s5::kT), 0, stream, a); break;
+  }
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;
 }
@@ -503,6 +523,10 @@ int launch_sdf5_fwd(const SdfLayout& L, const void* packed, const float* pts, in
 
 extern "C" int nr_sdf5_enable(int on) {
   const int was = nr::g_sdf5;
-  nr::g_sdf5 = on ? 1 : 0;
+  if (on > 0 && !nr::g_sdf5_pack) {
+    nr::set_error("nr_sdf5_enable: start the process with NR_SDF5 set (the packs then carry the 32x32x16 layout)");
+    return -1;
+  }
+  nr::g_sdf5 = on < 0 ? 0 : on;  // 1: the kernel; 2..6: experiment variants (tools/sdf5_ab.py)
   return was;
 }

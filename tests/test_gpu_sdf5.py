@@ -1,0 +1,65 @@
+"""The 32x32x16 SDF forward kernel (nr_sdf5.hip, opt-in experiment: nr_sdf5_enable) against the reference
+golden and the oracle, in a child process started with NR_SDF5=1 (the load-time switch that adds the
+32x32x16 copy of the ops to the packs).  Same bar as the 16x16x32 kernel's forward
+(test_gpu_parity.py::test_sdf_net_vs_golden / test_sdf_net_ragged_sizes): sdf within 1e-5 relative +
+1e-6 of the reference, at the golden points and at ragged sizes (P = 1, 17, 129, 1000, 70001)."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+CHILD = r'''
+import sys, torch
+sys.path[:0] = [{here!r}, {golden!r}, {root!r}]
+import numpy as np
+import weightgen as wg
+from helpers import neus_model, report, to_gpu
+from oracle.nets import SDFNet
+from neurecon_amd import _lib as L
+lib = L.lib()
+assert lib.nr_sdf5_enable(1) == 0
+g = dict(np.load({golden_path!r}))
+m = neus_model(wg.neus_state(seed=int(g['seed'])))
+with torch.no_grad():
+    s = m.implicit_surface.forward(to_gpu(g['pts']))
+assert report('sdf5 sdf vs golden', s, g['sdf_nograd'], 1e-5, 1e-6)[0].all()
+sd = wg.neus_state(seed=11)
+m = neus_model(sd)
+orc = SDFNet(sd)
+torch.manual_seed(0)
+for P in (1, 17, 129, 1000, 70001):
+    x = torch.randn(P, 3) * 0.7
+    ref = orc.sdf(x)
+    with torch.no_grad():
+        s5 = m.implicit_surface.forward(x.cuda())
+        lib.nr_sdf5_enable(0)
+        s4 = m.implicit_surface.forward(x.cuda())
+        lib.nr_sdf5_enable(1)
+    assert report(f'sdf5 P={{P}}', s5, ref, 1e-5, 1e-6)[0].all()
+    d = float((s5 - s4).abs().max())
+    print(f'P={{P}}: |sdf5 - sdf4| max {{d:.2e}}')
+    assert d <= 4e-6
+print('SDF5 OK')
+'''
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+
+
+def test_sdf5_forward_vs_golden_and_oracle():
+    code = CHILD.format(here=HERE, golden=os.path.join(HERE, 'golden'), root=ROOT,
+                        golden_path=os.path.join(HERE, 'golden', 'sdf_net.npz'))
+    env = dict(os.environ, NR_SDF5='1')
+    r = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, text=True, timeout=300)
+    print(r.stdout[-3000:], r.stderr[-3000:])
+    assert r.returncode == 0 and 'SDF5 OK' in r.stdout
