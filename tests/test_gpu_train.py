@@ -761,6 +761,11 @@ def test_neus_training_with_nr_adam_matches_torch_adam(golden, precision):
     assert min(abs(l_ref[1] - l_ref[0]), abs(l_ref[2] - l_ref[1])) > 1e-3 * abs(l_ref[0]), l_ref
     for a, b in zip(l_nr, l_ref):
         assert abs(a - b) <= 2e-5 * abs(b), (l_nr, l_ref)
+    # parameters: Adam moves an element by up to ~lr per step whatever its gradient, and where a gradient
+    # is near 0 (|g| ~ sqrt(v)) the two updates' rounding moves its step by a visible part of lr; the
+    # bar is 2 % of the largest displacement (3 lr) per element and 0.1 % on average
+    lr, steps = 1e-3, 3
     for a, b in zip(p_nr, p_ref):
-        sc = float(b.abs().max()) + 1e-30
-        assert float((a - b).abs().max()) <= 2e-5 * sc
+        d = (a - b).abs()
+        assert float(d.max()) <= 0.02 * lr * steps and float(d.mean()) <= 1e-3 * lr * steps, \
+            (float(d.max()), float(d.mean()))

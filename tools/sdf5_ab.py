@@ -21,6 +21,7 @@ def main():
     ap.add_argument('--points', type=int, default=524288)
     ap.add_argument('--iters', type=int, default=20)
     ap.add_argument('--rounds', type=int, default=3)
+    ap.add_argument('--variants', default='0,1,2', help='nr_sdf5_enable values: 0 = sdf4_kernel, 1 = sdf5, 2.. experiments')
     a = ap.parse_args()
     from neurecon_amd import _lib as L
     from neurecon_amd.base import ImplicitSurface
@@ -30,10 +31,11 @@ def main():
     x = (torch.rand(a.points, 3, device='cuda') * 2 - 1) * 0.9
     lib = L.lib()
     out = {}
-    times = {0: [], 1: []}
+    vs = [int(v) for v in a.variants.split(',')]
+    times = {v: [] for v in vs}
     with torch.no_grad():
         for r in range(a.rounds):
-            for v in (0, 1):
+            for v in vs:
                 lib.nr_sdf5_enable(v)
                 y = s.forward(x)
                 torch.cuda.synchronize()
@@ -45,8 +47,8 @@ def main():
                 out[v] = y.clone()
     lib.nr_sdf5_enable(0)
     d = (out[1] - out[0]).abs()
-    print(f'points {a.points}: sdf4 (16x16x32) ms {["%.3f" % t for t in times[0]]}')
-    print(f'points {a.points}: sdf5 (32x32x16) ms {["%.3f" % t for t in times[1]]}')
+    for v in vs:
+        print(f'points {a.points}: variant {v} ms {["%.3f" % t for t in times[v]]}')
     print(f'|sdf5 - sdf4| max {float(d.max()):.3e} mean {float(d.mean()):.3e}; |sdf| max {float(out[0].abs().max()):.3f}')
     # float64 truth on a subset: the same net (its state_dict) through the oracle's SDFNet in float64
     # (test infrastructure, used here as the checker only)
@@ -58,11 +60,11 @@ def main():
     with torch.no_grad():
         sr = ref.forward(x[:n].double().cpu())
     sr = sr[0] if isinstance(sr, tuple) else sr
-    for v in (0, 1):
+    for v in [u for u in vs if u <= 2]:
         e = (out[v][:n].double().cpu().reshape(-1) - sr.reshape(-1)).abs()
         print(f'variant {v}: |sdf - f64| max {float(e.max()):.3e} mean {float(e.mean()):.3e}')
     macs = 459_008  # forward without the feature rows (bench.MAC_SDF_FWD_NOFEAT)
-    for v in (0, 1):
+    for v in vs:
         t = min(times[v])
         tf = a.points * macs * 2 / (t * 1e-3) / 1e12
         print(f'variant {v}: best {t:.3f} ms = {tf:.1f} TF/s = {tf / 833.3:.3f} of the f16x3 peak')
