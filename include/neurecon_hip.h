@@ -772,6 +772,15 @@ typedef struct {
 size_t nr_wgrad_workspace_bytes(int64_t P, int m, int n, int npairs);
 int nr_wgrad(const NrWgrad* w, void* stream);
 
+/* Layer products of the fp32 / SIREN nets' training step (nn.Linear forward, models/base.py:118-129,
+ * 243-263, SirenLayer base.py:84-115, RadianceNet base.py:372-391, and their autograd -- torch.addmm /
+ * mm in the reference): C[M, N] (row stride ldc) = A[M, K] (lda) op(B) (+ bias[N], may be NULL),
+ * op(B) = B^T for B [N, K] (ldb) with trans_b != 0 (A W^T), else B [K, N] (ldb); K > 0.  Exact fp32
+ * products accumulated in fp64 (v_mfma_f64_16x16x4_f64) and rounded once, the bias added last; acc32
+ * != 0: accumulated in fp32 in k order instead (v_mfma_f32_16x16x4_f32, an fmaf chain per element). */
+int nr_gemm32(const float* A, int64_t lda, const float* B, int64_t ldb, int trans_b, const float* bias, float* C,
+              int64_t ldc, int64_t M, int N, int K, int acc32, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Opt-in kernel timing (diagnostics / bench roofline).  While enabled, every kernel launch of
  * the library is bracketed by hipEvents on its stream; nr_profile_read() waits for them and

@@ -256,6 +256,7 @@ _SIGS = {
     'nr_wgrad_workspace_bytes': (_c_sz, [_c_i64, _c_i, _c_i, _c_i]),
     'nr_wgrad': (_c_i, [ctypes.POINTER(NrWgrad), _c_p]),
     'nr_profile_enable': (_c_i, [_c_i]),
+    'nr_gemm32': (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_i, _c_p, _c_p, _c_i64, _c_i64, _c_i, _c_i, _c_i, _c_p]),
     'nr_sdf5_enable': (_c_i, [_c_i]),
     'nr_profile_filter': (_c_i, [ctypes.c_char_p]),
     'nr_profile_read': (_c_i, [ctypes.POINTER(NrKernelStat), _c_i, ctypes.POINTER(_c_i)]),

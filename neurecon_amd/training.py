@@ -3,9 +3,10 @@ backward run on libnrhip.so.  f16x3 nets (the default precision; softplus SDF ne
 radiance nets) run every layer product on the hand-written training GEMM (nr_train_gemm: f16x3 MFMA
 over the render pack's weight stream, the elementwise step of the recipe fused into its epilogue);
 the weight gradients run on nr_wgrad (hand-written MFMA, f16x3 products).  fp32-precision and SIREN
-nets keep the reference-exact path: torch.addmm / mm on hipBLASLt (fp32) for the layer products, the
-elementwise kernels of nr_train.hip between them, and nr_wgrad with exact fp32 products (fixed-order
-reduction) for the weight gradients.
+nets keep the reference-exact path: exact fp32 layer products on nr_gemm32 (r06, hand-written
+v_mfma_f32_16x16x4_f32, k-order fmaf chains; torch.addmm / mm on hipBLASLt through r05), the elementwise
+kernels of nr_train.hip between them, and nr_wgrad with exact fp32 products (fixed-order reduction) for
+the weight gradients.
 
 What the reference differentiates (models/frameworks/neus.py:284-485, models/base.py:265-282):
   * ImplicitSurface.forward_with_nablas with create_graph=True: sdf, nablas = d sdf / d x and the
@@ -129,6 +130,23 @@ def _colsum(a):
     return out
 
 
+def _mm(a, w, bias=None, trans=False, acc32=False):
+    """a @ w.t() + bias (trans: nn.Linear's addmm) or a @ w on nr_gemm32: exact fp32 products accumulated
+    in fp64 and rounded once (acc32: an fp32 fmaf chain in k order), the bias added last; a [P, K] with
+    unit column stride (any row stride), w [N, K] (trans) or [K, N] contiguous"""
+    if a.stride(1) != 1:
+        a = a.contiguous()
+    w = w.contiguous()
+    P, K = a.shape
+    N = w.shape[0] if trans else w.shape[1]
+    assert w.shape[1 if trans else 0] == K
+    out = torch.empty(P, N, device=a.device)
+    L.check(L.lib().nr_gemm32(L.ptr(a), a.stride(0), L.ptr(w), w.stride(0), int(trans),
+                              L.ptr(bias.contiguous()) if bias is not None else None, L.ptr(out), N, P, N, K, int(acc32),
+                              _st(a)))
+    return out
+
+
 def _mul(a, b):
     out = torch.empty_like(a)
     L.check(L.lib().nr_mul(L.ptr(a), L.ptr(b), a.numel(), L.ptr(out), _st(a)))
@@ -151,12 +169,12 @@ class SdfNabla(torch.autograd.Function):
         h = h0
         for l in range(D):
             hi = torch.cat([h, h0], -1).div_(math.sqrt(2)) if l in skips else h  # base.py:250
-            z = torch.addmm(bs[l], hi, Ws[l].t())
+            z = _mm(hi, Ws[l], bs[l], trans=True)
             h, s = _sine30(z) if siren else _softplus(z)
             hin.append(hi)
             ss.append(s)
         hin.append(h)
-        out = torch.addmm(bs[D], h, Ws[D].t())
+        out = _mm(h, Ws[D], bs[D], trans=True)
         sdf = out[:, 0].contiguous()
         feat = out[:, 1:].contiguous() if want_feat else None
         # nabla chain: g_l = d sdf / d h_l, delta_l = s_l * g_l
@@ -167,7 +185,7 @@ class SdfNabla(torch.autograd.Function):
         for l in range(D - 1, -1, -1):
             gs[l] = g.contiguous()
             delta = deltas[l] = _mul(ss[l], gs[l])  # kept: the backward's tangent adjoint
-            gin = delta @ Ws[l]
+            gin = _mm(delta, Ws[l])
             if l in skips:
                 n_prev = Ws[l - 1].shape[0]
                 e_skip = _cols(gin, n_prev, gin.shape[1] - n_prev, scale=_ISQ2)
@@ -215,7 +233,7 @@ class SdfNabla(torch.autograd.Function):
             hd = hd0
             for l in range(D):
                 hdi = torch.cat([hd, hd0], -1).div_(math.sqrt(2)) if l in skips else hd
-                zd = hdi @ Ws[l].t()
+                zd = _mm(hdi, Ws[l], trans=True)
                 hdins[l], zdots[l] = hdi, zd
                 hd = _mul(ss[l], zd)
             hdins[D] = hd
@@ -225,7 +243,7 @@ class SdfNabla(torch.autograd.Function):
         db[D] = _colsum(ob)
         if tangent:  # d(g_nab . nabla) / d W_D[0, :] = sum_p hdot_{D-1}
             dW[D][0] += _colsum(hdins[D])
-        hbar = ob @ Ws[D]
+        hbar = _mm(ob, Ws[D])
         for l in range(D - 1, -1, -1):
             n = ss[l].shape[1]
             zbar = torch.empty(P, n, device=dev)
@@ -243,7 +261,7 @@ class SdfNabla(torch.autograd.Function):
                 dW[l] = _wgrad(zbar, hin[l])
             db[l] = _colsum(zbar)
             if l > 0:
-                hb = zbar @ Ws[l]
+                hb = _mm(zbar, Ws[l])
                 hbar = _cols(hb, 0, Ws[l - 1].shape[0], scale=_ISQ2) if l in skips else hb
         return (None, None, *dW, *db)
 
@@ -269,14 +287,14 @@ class RadianceFn(torch.autograd.Function):
         ss = []
         h = inp
         for l in range(D):
-            h = torch.addmm(bs[l], h, Ws[l].t())
+            h = _mm(h, Ws[l], bs[l], trans=True)
             if siren:
                 h, s = _sine30(h)
                 ss.append(s)
             else:
                 L.check(L.lib().nr_activation(L.ptr(h), None, h.numel(), 0, _st(x)))
             hs.append(h)
-        y = torch.addmm(bs[D], h, Ws[D].t())
+        y = _mm(h, Ws[D], bs[D], trans=True)
         L.check(L.lib().nr_activation(L.ptr(y), None, y.numel(), 2, _st(x)))
         ctx.cfg = (D, nv, nn_, wf, siren)
         ctx.save_for_backward(y, *Ws, *hs, *ss)
@@ -295,7 +313,7 @@ class RadianceFn(torch.autograd.Function):
         dW, db = [None] * (D + 1), [None] * (D + 1)
         for l in range(D, -1, -1):
             dW[l], db[l] = _wgb(g, hs[l])
-            g = g @ Ws[l]
+            g = _mm(g, Ws[l])
             if l > 0:
                 if siren:
                     g = _mul(ss[l - 1], g)

@@ -193,25 +193,31 @@ def test_neus_train_step_random_batch_vs_oracle(precision):
         a, b = float(losses[k]), float(ref_losses[k])
         print(f'{precision} {k}: gpu {a:.8f} oracle {b:.8f} f64 {float(ref["f64"][0][k]):.10f}')
         assert abs(a - b) <= 1e-5 * abs(b) + 1e-7
-    worst_gpu, worst_o32, n_tight = 0.0, 0.0, 0
+    worst_gpu, worst_o32, n_tight, worst_cpu_ratio = 0.0, 0.0, 0, 0.0
     for k, t64 in g64.items():
         mine, o32 = grads[k].double(), g32[k]
         scale = float(t64.abs().max()) + 1e-30
         e_gpu, e_o32 = (mine - t64).abs(), (o32 - t64).abs()
-        env = max([float(e_o32.max())] + [float((g[k] - t64).abs().max()) for g in g32x])
+        env_cpu = max([float(e_o32.max())] + [float((g[k] - t64).abs().max()) for g in g32x[:2]])
         e_gpu_oracle = float((g32x[2][k] - t64).abs().max())
+        env = max(env_cpu, e_gpu_oracle)
+        worst_cpu_ratio = max(worst_cpu_ratio, float(e_gpu.max()) / (env_cpu + 1e-5 * scale))
         worst_gpu, worst_o32 = max(worst_gpu, float(e_gpu.max()) / scale), max(worst_o32, env / scale)
         o32_meets = bool((e_o32 <= 1e-4 * t64.abs() + 1e-5 * scale).all())
-        print(f'{precision} {k}: |gpu-f64| max {float(e_gpu.max()) / scale:.2e}, fp32 envelope (4 variants) '
-              f'{env / scale:.2e} (the oracle in fp32 on the GPU: {e_gpu_oracle / scale:.2e}; of the tensor scale '
+        print(f'{precision} {k}: |gpu-f64| max {float(e_gpu.max()) / scale:.2e}, CPU fp32 envelope (3 variants) '
+              f'{env_cpu / scale:.2e}, the oracle in fp32 on the GPU {e_gpu_oracle / scale:.2e} (of the tensor scale '
               f'{scale:.3e}); oracle32 meets 1e-5: {o32_meets}')
         # r05: the fp32 mode's weight gradients run on nr_wgrad's exact-fp32 fixed-order reduction (r04:
         # hipBLASLt split-K, 1.43x the envelope on layers 0 / 4): the single-envelope bar holds in both modes
-        assert bool((e_gpu <= env + 1e-5 * scale).all()), (k, float(e_gpu.max()) / scale, env / scale)
+        # r06: the fp32 mode's layer products accumulate in fp64 (nr_gemm32; the fp32 rounding of those
+        # products was the excess, tools/train_error_probe.py): held to the three CPU fp32 variants alone
+        e_bar = env_cpu if precision == 'fp32' else env
+        assert bool((e_gpu <= e_bar + 1e-5 * scale).all()), (k, float(e_gpu.max()) / scale, e_bar / scale)
         if o32_meets:
             n_tight += 1
             s32 = float(o32.abs().max()) + 1e-30
             assert bool(((mine - o32).abs() <= 1e-4 * o32.abs() + 1e-5 * s32).all()), k
     print(f'{precision}: 512-ray batch, worst |gpu - f64| {worst_gpu:.3e}, worst |oracle32 - f64| {worst_o32:.3e} '
           f'(of the tensor scale); 1e-5 bar vs the fp32 oracle held on {n_tight} / {len(g64)} tensors '
-          f'(the rest: the fp32 oracle itself misses it against float64)')
+          f'(the rest: the fp32 oracle itself misses it against float64); worst |gpu - f64| / (E_cpu + 1e-5 scale) '
+          f'{worst_cpu_ratio:.3f}')

@@ -761,11 +761,13 @@ def test_neus_training_with_nr_adam_matches_torch_adam(golden, precision):
     assert min(abs(l_ref[1] - l_ref[0]), abs(l_ref[2] - l_ref[1])) > 1e-3 * abs(l_ref[0]), l_ref
     for a, b in zip(l_nr, l_ref):
         assert abs(a - b) <= 2e-5 * abs(b), (l_nr, l_ref)
-    # parameters: Adam moves an element by up to ~lr per step whatever its gradient, and where a gradient
-    # is near 0 (|g| ~ sqrt(v)) the two updates' rounding moves its step by a visible part of lr; the
-    # bar is 2 % of the largest displacement (3 lr) per element and 0.1 % on average
+    # parameters: Adam moves an element by ~lr per step whatever its gradient's size, so an element whose
+    # gradient is within rounding of 0 can step the other way in one run (a 2 lr difference); the bar:
+    # at most 0.1 % of a tensor's elements more than 2 % of the largest displacement (3 lr) apart, and
+    # 0.1 % of it on average
     lr, steps = 1e-3, 3
     for a, b in zip(p_nr, p_ref):
         d = (a - b).abs()
-        assert float(d.max()) <= 0.02 * lr * steps and float(d.mean()) <= 1e-3 * lr * steps, \
-            (float(d.max()), float(d.mean()))
+        far = int((d > 0.02 * lr * steps).sum())
+        assert far <= max(1, 1e-3 * d.numel()) and float(d.mean()) <= 1e-3 * lr * steps, \
+            (far, d.numel(), float(d.max()), float(d.mean()))
