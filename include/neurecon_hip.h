@@ -714,12 +714,17 @@ int nr_radiance_train_fwd32(const NrRadDesc* d, const void* packed, const float*
  *                        (16-byte aligned) and v_emb [P][27] from nr_nerf_train_input; outputs the 8 ReLU
  *                        activations h[0..7] [P][256], the feature [P][256], the view branch's ReLU output
  *                        hv [P][128], sigma [P] and rgb [P][3] in one launch
- *   nr_nerf_train_pack   the backward's transposed fp32 ops (views^T, feature^T, W7^T .. W1^T) and the
- *                        rgb / alpha rows; W / b as nr_nerf_pack's 12 layers (biases unused)
+ *   nr_nerf_train_pack   the backward's transposed ops (views^T, feature^T, W7^T .. W1^T) and the rgb /
+ *                        alpha rows, in d->precision (r06: NR_PREC_F16X3 packs them for the f16x3
+ *                        products below); W / b as nr_nerf_pack's 12 layers (biases unused)
  *   nr_nerf_train_bwd32  the data gradients in one launch: g3 = g_rgb * sigmoid' [P][3], ghv = (g3 Wr) *
  *                        [hv > 0] [P][128], g_feat = Wv[:, :256]^T ghv [P][256], gz[7] = (Wf^T g_feat +
  *                        g_sigma Wa) * [h7 > 0], gz[i-1] = (W_i^T gz[i])[h columns] * [h_{i-1} > 0]; g_rgb /
- *                        g_sigma may be null (zero).  The weight gradients are nr_wgrad products of these. */
+ *                        g_sigma may be null (zero).  The products are exact fp32 for d->precision
+ *                        NR_PREC_FP32, f16x3 for NR_PREC_F16X3 (the backward is linear in the forward's
+ *                        stored ReLU masks, so no decision depends on their rounding); `train_packed` must
+ *                        come from nr_nerf_train_pack with the same precision.  The weight gradients are
+ *                        nr_wgrad products of these. */
 int nr_nerf_train_fwd32(const NrNerfDesc* d, const void* packed, const float* x_emb, const float* v_emb, int64_t P,
                         float* const* h, float* feat, float* hv, float* sigma, float* rgb, void* stream);
 size_t nr_nerf_train_packed_bytes(const NrNerfDesc* d);

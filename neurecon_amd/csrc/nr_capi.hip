@@ -985,7 +985,7 @@ int nr_nerf_train_pack(const NrNerfDesc* d, const float* const* W, const float* 
   const NerfBwdLayout B = nerf_bwd_layout();
   char* P = (char*)packed;
   float* wmax = (float*)(P + B.scale_off);
-  const int prec = NR_PREC_FP32, in0 = 84, inv = 27;
+  const int prec = d->precision == NR_PREC_F16X3 ? NR_PREC_F16X3 : NR_PREC_FP32, in0 = 84, inv = 27;
   PackOp ops[kNerfBwdOps];
   // views_linears[0]^T restricted to the feature columns: [128][256 + 27] -> out 256 (feature), in 128
   ops[NBV] = mkop(W[9], nullptr, 128, 256 + inv, 1, seg(16, 0, 256), none(), seg(8, 0, 128), none(), 1.0f, prec,
@@ -1034,7 +1034,7 @@ int nr_nerf_train_bwd32(const NrNerfDesc* d, const void* train_packed, const flo
              "nr_nerf_train_bwd32: null argument");
   for (int i = 0; i < 8; ++i) NR_REQUIRE(h[i] && gz[i], NR_ERR_ARG, "nr_nerf_train_bwd32: null layer pointer");
   return launch_nerf_train32_bwd(nerf_bwd_layout(), train_packed, rgb, hv, h, g_rgb, g_sigma, P, g3, ghv, g_feat, gz,
-                                 (hipStream_t)stream);
+                                 (hipStream_t)stream, d->precision == NR_PREC_F16X3);
 }
 
 // ---- training layer GEMMs (nr_mlp.hip tgemm_kernel) ---------------------------------------------

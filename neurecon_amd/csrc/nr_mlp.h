@@ -92,7 +92,7 @@ struct NerfLayout {
   int prec;
 };
 
-// NeRF++ training pack (nr_nerf_train_pack, fp32): the transposed ops of the backward data gradients,
+// NeRF++ training pack (nr_nerf_train_pack, fp32 or f16x3): the transposed ops of the backward data gradients,
 // chained by nerf_train32_bwd_kernel: views (Wv[:, :256]^T: 128 -> 256), feature (Wf^T), then W7^T ..
 // W1^T (W5^T restricted to its h columns 84..339); Wr [3][128] and Wa [256] for the VALU heads
 enum NerfBwdOp { NBV, NBF, NB7, NB6, NB5, NB4, NB3, NB2, NB1, kNerfBwdOps };
@@ -133,7 +133,7 @@ struct PackOp {
 };
 
 int launch_pack_op(const PackOp& op, char* dst, hipStream_t stream);
-// the ops of one pack call, batched (two launches per 8 ops)
+// the ops of one pack call, batched (three launches per 8 ops)
 int launch_pack_ops(const PackOp* ops, char* const* dst, int nops, hipStream_t stream);
 int launch_pack_vec(const float* src, int off, int nvalid, int n, char* dst, hipStream_t stream);
 int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,
@@ -164,7 +164,8 @@ int launch_nerf_train32_fwd(const NerfLayout& L, const void* packed, const float
                             float* const* h, float* feat, float* hv, float* sigma, float* rgb, hipStream_t stream);
 int launch_nerf_train32_bwd(const NerfBwdLayout& B, const void* packed, const float* rgb, const float* hv,
                             const float* const* h, const float* g_rgb, const float* g_sigma, int64_t P, float* g3,
-                            float* ghv, float* g_feat, float* const* gz, hipStream_t stream);
+                            float* ghv, float* g_feat, float* const* gz, hipStream_t stream,
+                            bool f16x3 = false);
 SdfLayout sdf_layout(const NrSdfDesc& d);
 RadLayout rad_layout(const NrRadDesc& d);
 int check_sdf_desc(const NrSdfDesc* d);

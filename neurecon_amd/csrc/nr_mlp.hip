@@ -2756,6 +2756,7 @@ struct NerfTrainBwdArgs {
   float* gz[8];          // [P][256]
 };
 
+template <int P>
 __global__ __launch_bounds__(kThreads) void nerf_train32_bwd_kernel(NerfTrainBwdArgs a) {
   constexpr int CB = chunk_bytes(16);
   __shared__ __attribute__((aligned(16))) char smem[kRing * CB];
@@ -2768,7 +2769,7 @@ __global__ __launch_bounds__(kThreads) void nerf_train32_bwd_kernel(NerfTrainBwd
   auto OPB = [&](int i) { return (int)L.op_bytes[i]; };
   const float* wr = (const float*)(W + L.wr_off);  // [3][128]
   const float* wa = (const float*)(W + L.wa_off);  // [256]
-  constexpr int F32 = NR_PREC_FP32;
+  constexpr int F32 = P;  // the products' precision (the name kept from the fp32-only kernel)
   const float4 E0[1] = {make_float4(0.f, 0.f, 0.f, 0.f)};  // no second input segment
 
   ws.start(OP(NBV), OPB(NBV), OP(NBV) + OPB(NBV), OPB(NBV));
@@ -3672,7 +3673,7 @@ __device__ __forceinline__ void pack_word(const PackOp& op, uint32_t* __restrict
 
 // Packing runs every optimizer step in training (the no-grad sampler's render pack and the training
 // pack follow the weights), for up to 17 ops per network: the ops of one pack call go in batches of
-// kPackBatch through two launches -- pack_prep_kernel (one workgroup per op: max |W * scale| for the
+// kPackBatch through three launches -- pack_rows_kernel and pack_final_kernel (max |W * scale| for the
 // f16x3 weight scale, and the op's bound) and pack_ops_kernel (one thread per packed word, blockIdx.y =
 // op) -- instead of two memsets and three launches per op.
 constexpr int kPackBatch = 8;
@@ -3690,33 +3691,82 @@ __global__ void pack_ops_kernel(PackBatch pb) {
   pack_word(pb.op[o], pb.dst[o], e);
 }
 
-// One workgroup (16 waves) per op:
+// The op's scales and bounds, in two launches over many workgroups (r06; r05 ran one 16-wave
+// workgroup per op, ~60 us per batch of 8 ops: every optimizer step of training repacks 3-4 nets):
 //   *wmax    = max |W * scale| (and of W2) -- f16x3 ops
 //   bound[0] = max over packed output rows of sum_k |W * scale| (row L1 norm of the op's effective
 //              matrix, x 1.0001: margin for the summation's rounding), bound[1] = max |bias|
-// A row's KB x 16 inputs are strided over the lanes of one wave, then wave-summed; the maxima are
-// order-independent, so every op packs bit for bit as one launch per op did.
-__global__ __launch_bounds__(1024) void pack_prep_kernel(PackBatch pb) {
-  const PackOp& op = pb.op[blockIdx.x];
-  __shared__ float red[3][16];
+// pack_rows_kernel (grid: row groups of 16 x ops): one wave per packed output row sums its KB x 16
+// inputs (lanes strided over them, then wave-summed: the r05 kernel's order, so every op packs bit for
+// bit as before), and each workgroup takes a slice of W (and W2) for the max; the partials go to words
+// 128..255 of the op's packed bias slots, which pack_ops_kernel rewrites (to 0) afterwards.
+// pack_final_kernel (one workgroup per op) reduces them: maxima are order-independent.
+constexpr int kPackRowsPerWG = 16;
+__device__ __forceinline__ uint32_t* pack_part(const PackBatch& pb, int o, int chunk, int word) {
+  const PackOp& op = pb.op[o];
+  const int KB = op.in[0].nblk + op.in[1].nblk;
+  return pb.dst[o] + (int64_t)chunk * (2 * KB + 1) * 256 + 2 * KB * 256 + word;
+}
+__global__ __launch_bounds__(1024) void pack_rows_kernel(PackBatch pb) {
+  const int o = blockIdx.y, grp = blockIdx.x;
+  const PackOp& op = pb.op[o];
+  const int NBO = op.out[0].nblk + op.out[1].nblk;
+  const int R = NBO * 16, G = (R + kPackRowsPerWG - 1) / kPackRowsPerWG;
+  if (grp >= G) return;
+  __shared__ float red[2][16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float m = 0.0f, best = 0.0f, bb = 0.0f;
-  if (op.prec == NR_PREC_F16X3) {
-    for (int64_t i = threadIdx.x; i < op.wn; i += 1024) m = fmaxf(m, fabsf(op.W[i] * op.scale));
-    if (op.W2)
-      for (int64_t i = threadIdx.x; i < op.wn2; i += 1024) m = fmaxf(m, fabsf(op.W2[i] * op.scale));
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  }
   if (op.bound) {
-    const int KB = op.in[0].nblk + op.in[1].nblk;
-    const int NBO = op.out[0].nblk + op.out[1].nblk;
-    for (int r = wave; r < NBO * 16; r += 16) {
+    const int r = grp * kPackRowsPerWG + wave;
+    if (r < R) {
+      const int KB = op.in[0].nblk + op.in[1].nblk;
       const int ob = r >> 4, i = r & 15;
       float sr = 0.0f;
       for (int e = lane; e < KB * 16; e += 64) sr += fabsf(pack_src(op, ob, i, e >> 4, e & 15));
-      for (int o = 32; o > 0; o >>= 1) sr += __shfl_xor(sr, o);
-      best = fmaxf(best, sr * 1.0001f);
+      for (int off = 32; off > 0; off >>= 1) sr += __shfl_xor(sr, off);
+      if (lane == 0) *pack_part(pb, o, r >> 5, 128 + (r & 31)) = __float_as_uint(sr * 1.0001f);
+    }
+  }
+  if (op.prec == NR_PREC_F16X3) {  // this group's slice of W (and W2)
+    float m = 0.0f, m2 = 0.0f;
+    const int64_t a0 = op.wn * grp / G, a1 = op.wn * (grp + 1) / G;
+    for (int64_t i = a0 + threadIdx.x; i < a1; i += 1024) m = fmaxf(m, fabsf(op.W[i] * op.scale));
+    if (op.W2) {
+      const int64_t b0 = op.wn2 * grp / G, b1 = op.wn2 * (grp + 1) / G;
+      for (int64_t i = b0 + threadIdx.x; i < b1; i += 1024) m2 = fmaxf(m2, fabsf(op.W2[i] * op.scale));
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      m = fmaxf(m, __shfl_xor(m, off));
+      m2 = fmaxf(m2, __shfl_xor(m2, off));
+    }
+    if (lane == 0) {
+      red[0][wave] = m;
+      red[1][wave] = m2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float a = 0.0f, b = 0.0f;
+      for (int w = 0; w < 16; ++w) {
+        a = fmaxf(a, red[0][w]);
+        b = fmaxf(b, red[1][w]);
+      }
+      // G <= 18 groups: chunk 0's words 192.. and 224..
+      *pack_part(pb, o, 0, 192 + grp) = __float_as_uint(fmaxf(a, b));
+    }
+  }
+}
+__global__ __launch_bounds__(256) void pack_final_kernel(PackBatch pb) {
+  const int o = blockIdx.x;
+  const PackOp& op = pb.op[o];
+  const int NBO = op.out[0].nblk + op.out[1].nblk;
+  const int R = NBO * 16, G = (R + kPackRowsPerWG - 1) / kPackRowsPerWG;
+  __shared__ float red[3][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float best = 0.0f, bb = 0.0f, m = 0.0f;
+  if (op.bound) {
+    for (int r = threadIdx.x; r < R; r += 256) {
+      best = fmaxf(best, __uint_as_float(*pack_part(pb, o, r >> 5, 128 + (r & 31))));
       if (op.bias) {
+        const int ob = r >> 4, i = r & 15;
         int ob_loc = ob;
         for (int q = 0; q < 2; ++q) {
           if (ob_loc < op.out[q].nblk) {
@@ -3729,6 +3779,12 @@ __global__ __launch_bounds__(1024) void pack_prep_kernel(PackBatch pb) {
       }
     }
   }
+  if (op.prec == NR_PREC_F16X3 && threadIdx.x < G) m = __uint_as_float(*pack_part(pb, o, 0, 192 + threadIdx.x));
+  for (int off = 32; off > 0; off >>= 1) {
+    best = fmaxf(best, __shfl_xor(best, off));
+    bb = fmaxf(bb, __shfl_xor(bb, off));
+    m = fmaxf(m, __shfl_xor(m, off));
+  }
   if (lane == 0) {
     red[0][wave] = m;
     red[1][wave] = best;
@@ -3737,7 +3793,7 @@ __global__ __launch_bounds__(1024) void pack_prep_kernel(PackBatch pb) {
   __syncthreads();
   if (threadIdx.x == 0) {
     float a = 0.0f, b = 0.0f, c = 0.0f;
-    for (int w = 0; w < 16; ++w) {
+    for (int w = 0; w < 4; ++w) {
       a = fmaxf(a, red[0][w]);
       b = fmaxf(b, red[1][w]);
       c = fmaxf(c, red[2][w]);
@@ -3774,7 +3830,13 @@ int launch_pack_ops(const PackOp* ops, char* const* dst, int nops, hipStream_t s
       pb.n[i] = (int64_t)(NBO / 2) * (2 * KB + 1) * 256;
       nmax = std::max(nmax, pb.n[i]);
     }
-    hipLaunchKernelGGL(pack_prep_kernel, dim3(nb), dim3(1024), 0, stream, pb);
+    int gmax = 1;
+    for (int i = 0; i < nb; ++i)
+      gmax = std::max(gmax, ((pb.op[i].out[0].nblk + pb.op[i].out[1].nblk) * 16 + kPackRowsPerWG - 1) / kPackRowsPerWG);
+    NR_REQUIRE(gmax <= 32, NR_ERR_UNSUPPORTED, "pack: more than 512 output rows in one op");
+    hipLaunchKernelGGL(pack_rows_kernel, dim3(gmax, nb), dim3(1024), 0, stream, pb);
+    NR_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(pack_final_kernel, dim3(nb), dim3(256), 0, stream, pb);
     NR_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(pack_ops_kernel, dim3((unsigned)((nmax + 255) / 256), nb), dim3(256), 0, stream, pb);
     NR_HIP_CHECK(hipGetLastError());
@@ -3902,7 +3964,8 @@ int launch_nerf_train32_fwd(const NerfLayout& L, const void* packed, const float
 
 int launch_nerf_train32_bwd(const NerfBwdLayout& B, const void* packed, const float* rgb, const float* hv,
                             const float* const* h, const float* g_rgb, const float* g_sigma, int64_t P, float* g3,
-                            float* ghv, float* g_feat, float* const* gz, hipStream_t stream) {
+                            float* ghv, float* g_feat, float* const* gz, hipStream_t stream,
+                            bool f16x3) {
   if (P <= 0) return NR_OK;
   NerfTrainBwdArgs a{};
   a.packed = (const char*)packed;
@@ -3918,7 +3981,8 @@ int launch_nerf_train32_bwd(const NerfBwdLayout& B, const void* packed, const fl
   a.g_feat = g_feat;
   for (int i = 0; i < 8; ++i) a.gz[i] = gz[i];
   ProfScope prof("nerf_train32_bwd", (double)P, stream);
-  hipLaunchKernelGGL(nerf_train32_bwd_kernel, dim3(grid_for(P)), dim3(kThreads), 0, stream, a);
+  if (f16x3) hipLaunchKernelGGL(nerf_train32_bwd_kernel<NR_PREC_F16X3>, dim3(grid_for(P)), dim3(kThreads), 0, stream, a);
+  else hipLaunchKernelGGL(nerf_train32_bwd_kernel<NR_PREC_FP32>, dim3(grid_for(P)), dim3(kThreads), 0, stream, a);
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;
 }

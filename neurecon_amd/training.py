@@ -367,24 +367,29 @@ class NeuSComposite(torch.autograd.Function):
 
 
 def _nerf_packs(net, Ws, bs, device):
-    """(fp32 desc, the fp32 render pack, the training pack) of a NeRF++ net built from the step's
-    weights (12 layers: pts_linears 0..7, feature, views, alpha, rgb), cached per parameter version"""
+    """(fp32 desc, the fp32 render pack, the training desc, the training pack) of a NeRF++ net built from
+    the step's weights (12 layers: pts_linears 0..7, feature, views, alpha, rgb), cached per parameter
+    version.  The forward runs on the fp32 pack whatever the net's precision (its ReLU decisions must be
+    the reference's); the training pack (the backward's transposed ops) is in the net's precision: the
+    backward is linear in the stored masks, so an f16x3 net runs it on f16x3 products (r06)"""
     from .base import _version_key, _ptr_array
     key = _version_key(net, 'nerf_train32', device)
     c = getattr(net, '_nr_train32_cache', None)
     if c is not None and c[0] == key:
-        return c[1], c[2], c[3]
+        return c[1], c[2], c[3], c[4]
     lib = L.lib()
     desc = net.nr_desc()
     desc.precision = L.PREC_FP32
+    tdesc = net.nr_desc()
+    tdesc.precision = L.PREC_F16X3 if getattr(net, 'precision', 'fp32') == 'f16x3' else L.PREC_FP32
     W = [w.detach().float().contiguous() for w in Ws]
     b = [x.detach().float().contiguous() for x in bs]
     pk = torch.empty(lib.nr_nerf_packed_bytes(ctypes.byref(desc)), dtype=torch.uint8, device=device)
     L.check(lib.nr_nerf_pack(ctypes.byref(desc), _ptr_array(W), _ptr_array(b), L.ptr(pk), L.stream_of(device)))
-    tp = torch.empty(lib.nr_nerf_train_packed_bytes(ctypes.byref(desc)), dtype=torch.uint8, device=device)
-    L.check(lib.nr_nerf_train_pack(ctypes.byref(desc), _ptr_array(W), _ptr_array(b), L.ptr(tp), L.stream_of(device)))
-    net._nr_train32_cache = (key, desc, pk, tp, W, b)
-    return desc, pk, tp
+    tp = torch.empty(lib.nr_nerf_train_packed_bytes(ctypes.byref(tdesc)), dtype=torch.uint8, device=device)
+    L.check(lib.nr_nerf_train_pack(ctypes.byref(tdesc), _ptr_array(W), _ptr_array(b), L.ptr(tp), L.stream_of(device)))
+    net._nr_train32_cache = (key, desc, pk, tdesc, tp, W, b)
+    return desc, pk, tdesc, tp
 
 
 def _ptrs(ts):
@@ -398,8 +403,9 @@ class NeRFFn(torch.autograd.Function):
     on the rays and the no-grad depths).  Returns sigma [P], rgb [P,3]; gradients reach every parameter.
     r05: the forward is one launch of nr_nerf_train_fwd32 (exact fp32 products, the layers chained in
     registers, every activation the backward needs stored) and the backward's data gradients one launch
-    of nr_nerf_train_bwd32 (the transposed fp32 ops chained, each layer's ReLU mask applied and its
-    pre-activation gradient stored), in place of 23 hipBLASLt GEMMs and 13 activation launches; the
+    of nr_nerf_train_bwd32 (the transposed ops chained, each layer's ReLU mask applied and its
+    pre-activation gradient stored; r06: f16x3 products for f16x3 nets, exact fp32 for fp32 nets), in
+    place of 23 hipBLASLt GEMMs and 13 activation launches; the
     weight gradients are nr_wgrad products (exact fp32 for fp32 nets, f16x3 otherwise), the skip
     layer's and the views layer's per input column block (no [P, 340] / [P, 283] concatenations)."""
 
@@ -411,7 +417,7 @@ class NeRFFn(torch.autograd.Function):
         xe, ve = xe.contiguous(), ve.contiguous()
         if xe.data_ptr() % 16:  # a contiguous view at an unaligned offset: the kernel reads 16-B rows
             xe = xe.clone()
-        desc, pk, _ = _nerf_packs(net, Ws, bs, dev)
+        desc, pk, _, _ = _nerf_packs(net, Ws, bs, dev)
         H = [torch.empty(P, 256, device=dev) for _ in range(8)]
         feat = torch.empty(P, 256, device=dev)
         hv = torch.empty(P, 128, device=dev)
@@ -434,14 +440,14 @@ class NeRFFn(torch.autograd.Function):
         dev = rgb.device
         P = rgb.shape[0]
         nx = xe.shape[1]
-        desc, _, tp = _nerf_packs(ctx.net, Ws, bs, dev)
+        _, _, tdesc, tp = _nerf_packs(ctx.net, Ws, bs, dev)
         g3 = torch.empty(P, 3, device=dev)
         ghv = torch.empty(P, 128, device=dev)
         g_feat = torch.empty(P, 256, device=dev)
         GZ = [torch.empty(P, 256, device=dev) for _ in range(8)]
         g_rgb = None if g_rgb is None else g_rgb.contiguous()
         gs = torch.zeros(P, device=dev) if g_sigma is None else g_sigma.reshape(P).contiguous()
-        L.check(L.lib().nr_nerf_train_bwd32(ctypes.byref(desc), L.ptr(tp), L.ptr(rgb), L.ptr(hv), _ptrs(H),
+        L.check(L.lib().nr_nerf_train_bwd32(ctypes.byref(tdesc), L.ptr(tp), L.ptr(rgb), L.ptr(hv), _ptrs(H),
                                             None if g_rgb is None else L.ptr(g_rgb), L.ptr(gs), P, L.ptr(g3),
                                             L.ptr(ghv), L.ptr(g_feat), _ptrs(GZ), _st(rgb)))
         f32 = ctx.fp32  # weight gradients on nr_wgrad: exact fp32 products (fp32 nets) or f16x3

@@ -51,6 +51,10 @@ def main():
     for w in a.which.split(','):
         if w == 'neus32':
             fn = bench.train_setup(dev, 'fp32', 512, 1)
+        elif w == 'neus16':
+            fn = bench.train_setup(dev, 'f16x3', 512, 1)
+        elif w == 'nerfpp16':
+            fn = bench.train_setup(dev, 'f16x3', 512, 1, nerfpp=True)
         elif w == 'siren32':
             fn = siren_step('fp32')
         elif w == 'siren16':
