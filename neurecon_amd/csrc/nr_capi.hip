@@ -624,6 +624,7 @@ static int unisurf_chunk(const NrUnisurfArgs& a, const UniPlan& pl, int64_t ray0
   c.pts_m = F(pl.o_ptsm); c.sm = F(pl.o_sm); c.sec = F(pl.o_sec); c.pts_s = F(pl.o_ptss); c.ss = F(pl.o_ss);
   c.d_all = F(pl.o_dall); c.pts_f = F(pl.o_ptsf); c.sdf_f = F(pl.o_sdff); c.nab_f = F(pl.o_nabf);
   c.feat_f = F(pl.o_featf); c.nrm_f = F(pl.o_nrmf); c.rad_f = F(pl.o_radf); c.wss = (double*)(ws + pl.o_wss);
+  c.wsp = (double*)(ws + pl.o_wsp);
   c.netchunk = a.netchunk;
   const bool sharded = a.normal_mode == 1 && a.shard_row_rays > 0;
   if (a.normal_mode == 1) {
@@ -676,7 +677,10 @@ static int unisurf_chunk(const NrUnisurfArgs& a, const UniPlan& pl, int64_t ray0
                        st)))
     return rc;
   if (a.normal_mode == 1) {
-    hipLaunchKernelGGL(uni_window_ss, dim3((unsigned)c.nw_row, (unsigned)(R / nloc)), dim3(256), 0, st, c);
+    hipLaunchKernelGGL(uni_window_ss_part, dim3((unsigned)c.nw_row, (unsigned)(R / nloc), kWinSlices), dim3(256), 0,
+                       st, c);
+    NR_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(uni_window_ss_sum, dim3((unsigned)c.nw_row, (unsigned)(R / nloc)), dim3(64), 0, st, c);
     NR_HIP_CHECK(hipGetLastError());
     if (sharded) {  // every rank's partial sums -> the sums of the whole batch (collective, stream-ordered)
       const int rr = a.window_reduce(a.window_user);

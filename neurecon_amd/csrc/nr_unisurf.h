@@ -28,6 +28,7 @@ struct UniChunk {
   // index (ray - k*rc_rays) * P + s inside that chunk.  The chunk's R rays are `rows` batch rows of
   // nloc rays each, starting at row-relative ray row_ray0 (a multi-GPU shard, or an internal chunk).
   double* wss;       // [rows][nw_row][3] sum of squares of the nablas per window
+  double* wsp;       // [rows][nw_row][kWinSlices][3] partial sums (uni_window_ss_part)
   int64_t netchunk;  // points per F.normalize window
   int64_t rc_rays;   // the reference's rayschunk (clipped to the row)
   int64_t row_rays;  // rays per batch row of the whole (unsharded) batch
@@ -52,11 +53,12 @@ struct UniOut {
 // sign change (uni_root only reads up to there), so later chunks run on the device-compacted rays
 // still without one.  Same values at every step uni_root reads: the maps are bit-identical.
 constexpr int kMarchK = 32;
+constexpr int kWinSlices = 64;  // blocks per F.normalize window in its sum of squares
 
 struct UniPlan {
   int64_t Rc;
   size_t o_ro, o_rd, o_near, o_far, o_thr, o_ptsm, o_sm, o_sec, o_ptss, o_ss, o_dall, o_ptsf, o_sdff, o_nabf;
-  size_t o_featf, o_nrmf, o_radf, o_wss, o_mlp;
+  size_t o_featf, o_nrmf, o_radf, o_wss, o_wsp, o_mlp;
   size_t o_act0, o_act1, o_acnt, o_ptsc, o_sc;  // chunked march: active lists, counts, compacted points / sdf
   size_t total;
   int64_t max_windows;
@@ -87,7 +89,8 @@ __global__ void rf_finish(UniChunk c, int64_t ray0, float* d_out, float* pts, ui
                           int fill_inf);
 __global__ void uni_secant(UniChunk c, int last);
 __global__ void uni_samples(UniChunk c, UniOut o);
-__global__ void uni_window_ss(UniChunk c);  // grid (nw_row, rows)
+__global__ void uni_window_ss_part(UniChunk c);  // grid (nw_row, rows, kWinSlices), 256 threads
+__global__ void uni_window_ss_sum(UniChunk c);   // grid (nw_row, rows), 64 threads
 __global__ void uni_normalize(UniChunk c, int mode);
 __global__ void uni_composite(UniChunk c, UniOut o, int calc_normal, int white_bkgd);
 

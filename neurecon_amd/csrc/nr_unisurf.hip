@@ -288,18 +288,30 @@ __device__ __forceinline__ int64_t uni_window(const UniChunk& c, int64_t rg, int
 }
 
 // sum of squares of every nabla component over the part of each F.normalize window that lies in
-// this chunk (one block per (window, batch row); windows the chunk does not touch get zeros)
-__global__ void uni_window_ss(UniChunk c) {
-  __shared__ double red[3][256];
-  const int64_t w = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+// this chunk, in two deterministic stages (r06; r05 ran one 256-thread block per window, 0.55 ms for
+// config (e)'s single 393 k-point window): uni_window_ss_part sums slice g of the window's points in each
+// of kWinSlices blocks (grid: windows x rows x slices; a block tree-reduces its threads' fp64 sums),
+// uni_window_ss_sum adds the slices' partials in slice order.  Windows the chunk does not touch get
+// zeros.
+__device__ __forceinline__ void uni_window_range(const UniChunk& c, int64_t w, int64_t& k0, int64_t& q0, int64_t& q1) {
   const int64_t P = c.P, k = w / c.nw_full, j = w % c.nw_full;
-  const int64_t k0 = k * c.rc_rays;  // first ray of reference chunk k
+  k0 = k * c.rc_rays;  // first ray of reference chunk k
   const int64_t rays_k = min(c.rc_rays, c.row_rays - k0);
-  int64_t q0 = j * c.netchunk, q1 = min((j + 1) * c.netchunk, rays_k * P);
+  q0 = j * c.netchunk;
+  q1 = min((j + 1) * c.netchunk, rays_k * P);
   q0 = max(q0, (c.row_ray0 - k0) * P);           // points of this chunk's rays only
   q1 = min(q1, (c.row_ray0 + c.nloc - k0) * P);
+}
+__global__ void uni_window_ss_part(UniChunk c) {
+  __shared__ double red[3][256];
+  const int64_t w = blockIdx.x, b = blockIdx.y, g = blockIdx.z, t = threadIdx.x;
+  const int64_t P = c.P;
+  int64_t k0, q0, q1;
+  uni_window_range(c, w, k0, q0, q1);
+  const int64_t len = q1 > q0 ? q1 - q0 : 0;
+  const int64_t qa = q0 + len * g / kWinSlices, qb = q0 + len * (g + 1) / kWinSlices;
   double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-  for (int64_t q = q0 + t; q < q1; q += blockDim.x) {
+  for (int64_t q = qa + t; q < qb; q += blockDim.x) {
     const int64_t rl = k0 + q / P - c.row_ray0, s = q % P;  // ray within this chunk's row
     const int64_t p = s * c.R + b * c.nloc + rl;            // sample-major point index
     const double x = c.nab_f[p * 3 + 0], y = c.nab_f[p * 3 + 1], z = c.nab_f[p * 3 + 2];
@@ -320,11 +332,20 @@ __global__ void uni_window_ss(UniChunk c) {
     __syncthreads();
   }
   if (t == 0) {
-    double* o = c.wss + (b * c.nw_row + w) * 3;
+    double* o = c.wsp + ((b * c.nw_row + w) * kWinSlices + g) * 3;
     o[0] = red[0][0];
     o[1] = red[1][0];
     o[2] = red[2][0];
   }
+}
+__global__ void uni_window_ss_sum(UniChunk c) {
+  const int64_t w = blockIdx.x, b = blockIdx.y;
+  const int t = threadIdx.x;
+  if (t >= 3) return;
+  const double* pp = c.wsp + (b * c.nw_row + w) * kWinSlices * 3 + t;
+  double acc = 0.0;
+  for (int g = 0; g < kWinSlices; ++g) acc += pp[g * 3];
+  c.wss[(b * c.nw_row + w) * 3 + t] = acc;
 }
 
 // normals fed to the radiance net: F.normalize(nablas) (unisurf.py:36). mode 0: per point (an
@@ -481,6 +502,10 @@ UniPlan unisurf_plan(const NrUnisurfArgs& a, int64_t Rc) {
   p.o_nrmf = take((size_t)P * Rc * 3);
   p.o_radf = take((size_t)P * Rc * 3);
   p.o_wss = take((size_t)p.max_windows * 6);
+  // a multi-GPU shard renders all its batch rows in one chunk (nr_unisurf_render), internal chunks one row
+  const int64_t nloc = a.rays_per_batch > 0 ? a.rays_per_batch : (a.n_rays > 0 ? a.n_rays : 1);
+  const int64_t rows = (a.normal_mode == 1 && a.shard_row_rays > 0) ? (a.n_rays + nloc - 1) / nloc : 1;
+  p.o_wsp = take((size_t)(rows > 0 ? rows : 1) * p.max_windows * kWinSlices * 6);
   p.o_act0 = take(Rc);
   p.o_act1 = take(Rc);
   p.o_acnt = take(2);
