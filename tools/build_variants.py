@@ -14,6 +14,8 @@ from neurecon_amd import build as B  # noqa: E402
 
 VARIANTS = {
     'base': [],
+    # NOT for tgemm_kernel: its counted vmcnt waits include the DMA pieces, so without them asm loads
+    # land after their registers are reused (r06: an illegal address, profiles/r06/tgemm_nodma_bound.txt)
     'nodma': ['-DNR_EXP_NO_DMA'],
     'noestore': ['-DNR_EXP_NO_ESTORE'],
     'noeload': ['-DNR_EXP_NO_ELOAD'],
