@@ -804,7 +804,7 @@ int nr_profile_enable(int on);
 int nr_profile_filter(const char* prefix);
 int nr_profile_read(NrKernelStat* out, int max, int* n_out);
 
-/* Kernel selection experiment (no reference counterpart; DESIGN.md §7): on != 0 routes the f16x3
+/* Kernel selection experiment (no reference counterpart; DESIGN.md §2.5): on != 0 routes the f16x3
  * softplus SDF nets' forward-only evaluations (nr_sdf_forward without nablas or feature, the UNISURF /
  * root-finding march, sphere tracing, the mesh grid, VolSDF's no-grad sampling) to the
  * v_mfma_f32_32x32x16_f16 kernel (one wave per SIMD, nr_sdf5.hip) instead of the 16x16x32 one; both
