@@ -53,10 +53,10 @@ RAY_FLOP_REF = 704.8e6
 RAY_FLOP = 2.0 * (255 * (MAC_SDF_FWD + MAC_SDF_BWD) + 127 * MAC_RAD)
 # HBM-side bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc passes of this bench,
 # tools/gpu_pmc.sh); counters cannot be read live, so the latest committed summary is reported.
-PMC_SUMMARY = {'f16x3': 'profiles/r05/f16x3_pmc_summary.json'}  # tools/gpu_final_r05.sh PROFILES=1 (PMC passes of the default bench)
+PMC_SUMMARY = {'f16x3': 'profiles/r06/f16x3_pmc_summary.json'}  # tools/gpu_final_r06.sh PROFILES=1 (PMC passes of the default bench)
 # matrix-pipe occupancy and effective clock per nabla launch type (rocprofv3 GRBM_GUI_ACTIVE and
 # SQ_VALU_MFMA_BUSY_CYCLES passes of this bench, tools/gpu_mfma_r05.sh -> tools/mfma_summary.py)
-MFMA_SUMMARY = 'profiles/r05/mfma_summary.json'
+MFMA_SUMMARY = 'profiles/r06/mfma_summary.json'
 MFMA_KERNEL = {'sdf_nabla_fwd': 'void nr::sdf4_kernel<true, false, 1>(nr::SdfKArgs)',
                'sdf_nabla_bwd': 'void nr::sdf4_kernel<true, false, 2>(nr::SdfKArgs)',
                'sdf_nabla_feat': 'void nr::sdf4_kernel<true, true, 0>(nr::SdfKArgs)'}
@@ -353,7 +353,7 @@ def mfma_evidence(per_type):
 HBM_PEAK_TBPS = 8.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
-TRAIN_PMC_SUMMARY = 'profiles/r05/train_pmc_summary.json'  # tools/gpu_final_r05.sh PROFILES=1 (PMC passes of --workload train)
+TRAIN_PMC_SUMMARY = 'profiles/r06/train_pmc_summary.json'  # tools/gpu_final_r06.sh PROFILES=1 (PMC passes of --workload train)
 
 
 def train_pmc_traffic(prefix):
