@@ -150,6 +150,7 @@ extern "C" int nr_gemm32(const float* A, int64_t lda, const float* B, int64_t ld
   NR_REQUIRE(A && B && C && M >= 0 && N >= 0 && K >= 0, NR_ERR_ARG, "nr_gemm32: null argument or negative size");
   NR_REQUIRE(lda >= K && ldc >= N && ldb >= (trans_b ? K : N), NR_ERR_ARG, "nr_gemm32: leading dimension too small");
   NR_REQUIRE(K > 0, NR_ERR_ARG, "nr_gemm32: K must be positive");
+  NR_REQUIRE((M + g32::TM - 1) / g32::TM <= 65535, NR_ERR_ARG, "nr_gemm32: M above 65535 row tiles (split the rows)");
   if (M == 0 || N == 0) return NR_OK;
   g32::Args a{A, lda, B, ldb, trans_b, bias, C, ldc, M, N, K};
   ProfScope prof("gemm32", (double)M * N * K, (hipStream_t)stream);

@@ -175,6 +175,26 @@ def test_r05_training_entries_reject_bad_arguments(lib):
     assert rc == -1 and 'ld_small' in lib.nr_last_error().decode()
 
 
+def test_r06_entries_reject_bad_arguments(lib):
+    """nr_gemm32 checks its sizes and leading dimensions before any HIP call (fake device pointers);
+    nr_sdf5_enable refuses without NR_SDF5 at load (the packs would lack the 32x32x16 layout)"""
+    A, B, C = 0x1000, 0x2000, 0x3000
+    assert lib.nr_gemm32(None, 8, B, 8, 0, None, C, 8, 16, 8, 8, 0, None) == -1
+    assert 'null argument' in lib.nr_last_error().decode()
+    assert lib.nr_gemm32(A, 4, B, 8, 0, None, C, 8, 16, 8, 8, 0, None) == -1      # lda < K
+    assert 'leading dimension' in lib.nr_last_error().decode()
+    assert lib.nr_gemm32(A, 8, B, 4, 1, None, C, 8, 16, 8, 8, 0, None) == -1      # transposed B: ldb < K
+    assert lib.nr_gemm32(A, 8, B, 8, 0, None, C, 4, 16, 8, 8, 0, None) == -1      # ldc < N
+    assert lib.nr_gemm32(A, 0, B, 8, 0, None, C, 8, 16, 8, 0, 0, None) == -1      # K = 0
+    assert 'K must be positive' in lib.nr_last_error().decode()
+    assert lib.nr_gemm32(A, 8, B, 8, 0, None, C, 8, 128 * 65536, 8, 8, 0, None) == -1
+    assert 'row tiles' in lib.nr_last_error().decode()
+    assert lib.nr_gemm32(A, 8, B, 8, 0, None, C, 8, 0, 8, 8, 0, None) == 0        # empty: no launch
+    if not os.environ.get('NR_SDF5'):
+        assert lib.nr_sdf5_enable(1) == -1 and 'NR_SDF5' in lib.nr_last_error().decode()
+        assert lib.nr_sdf5_enable(0) == 0
+
+
 def test_adam_step_rejects_bad_arguments(lib):
     """nr_adam_step checks its table and hyper-parameters before any HIP call"""
     from neurecon_amd import _lib
