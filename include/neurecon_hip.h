@@ -809,7 +809,7 @@ int nr_profile_read(NrKernelStat* out, int max, int* n_out);
  * root-finding march, sphere tracing, the mesh grid, VolSDF's no-grad sampling) to the
  * v_mfma_f32_32x32x16_f16 kernel (one wave per SIMD, nr_sdf5.hip) instead of the 16x16x32 one; both
  * meet the same bars, their results differ by rounding.  Measured 3 % slower, so off by default.
- * Needs the process started with $NR_SDF5 set (the packs then carry the 32x32x16 layout as well;
+ * Needs the process started with $NR_SDF5 set to a nonzero integer (the packs then carry the 32x32x16 layout as well;
  * nr_sdf_packed_bytes grows): returns -1 otherwise, else the previous setting. */
 int nr_sdf5_enable(int on);
 

@@ -272,6 +272,14 @@ class NrError(RuntimeError):
     pass
 
 
+
+def _env_int(name):
+    """integer value of an environment switch (unset, empty or not a number: 0)"""
+    try:
+        return int(os.environ.get(name, '') or 0)
+    except ValueError:
+        return 0
+
 def lib():
     """Load libnrhip.so (raises if absent: the HIP path is the only path)."""
     global _lib
@@ -286,8 +294,8 @@ def lib():
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
-            if os.environ.get('NR_SDF5') is not None:  # kernel selection (nr_sdf5_enable), for A/B runs
-                L.nr_sdf5_enable(int(os.environ['NR_SDF5']))
+            if _env_int('NR_SDF5'):  # kernel selection (nr_sdf5_enable), for A/B runs
+                L.nr_sdf5_enable(_env_int('NR_SDF5'))
             _lib = L
     return _lib
 

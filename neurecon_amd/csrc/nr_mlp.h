@@ -143,7 +143,7 @@ int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t
 int launch_sdf5_fwd(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, int nfreq,
                     hipStream_t stream, const int* P_dev, int P_mult);
 extern int g_sdf5;             // route launch_sdf's forward-only f16x3 launches to it (nr_sdf5_enable)
-extern const int g_sdf5_pack;  // $NR_SDF5 set at load: the layout carries the 32x32x16 copy
+extern const int g_sdf5_pack;  // $NR_SDF5 (a nonzero integer) at load: the layout carries the 32x32x16 copy
 // deferred sample nablas (sdf4_kernel STAGE 1 / 2): stage 1 = sdf + slabs per 16-point tile into
 // `slabs` (P/16 x kSlabColBytes); stage 2 = nablas of the tiles tiles[0 .. *n_tiles) from their slabs
 int launch_sdf_deferred(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,

@@ -17,6 +17,7 @@
 //  * Everything per point (embedding, nabla chain rule through sin/cos, sdf row dot product,
 //    sigmoid head) is VALU work in the same kernel.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 #include "nr_common.h"
 #include "nr_mlp.h"
@@ -3857,8 +3858,8 @@ int g_sdf5 = 0;
 // process-wide constant, so every pack and launch of the process agrees on the layout): the experiment
 // costs nothing elsewhere (training repacks every optimizer step)
 const int g_sdf5_pack = [] {
-  const char* e = getenv("NR_SDF5");
-  return (e && *e) ? 1 : 0;
+  const char* e = getenv("NR_SDF5");  // a nonzero integer (NR_SDF5=0 or empty: off, no second layout)
+  return (e && atoi(e) != 0) ? 1 : 0;
 }();
 
 static int grid_for(int64_t P) {

@@ -175,6 +175,11 @@ def test_r05_training_entries_reject_bad_arguments(lib):
     assert rc == -1 and 'ld_small' in lib.nr_last_error().decode()
 
 
+def _lib_env_int(name):
+    from neurecon_amd import _lib
+    return _lib._env_int(name)
+
+
 def test_r06_entries_reject_bad_arguments(lib):
     """nr_gemm32 checks its sizes and leading dimensions before any HIP call (fake device pointers);
     nr_sdf5_enable refuses without NR_SDF5 at load (the packs would lack the 32x32x16 layout)"""
@@ -190,7 +195,7 @@ def test_r06_entries_reject_bad_arguments(lib):
     assert lib.nr_gemm32(A, 8, B, 8, 0, None, C, 8, 128 * 65536, 8, 8, 0, None) == -1
     assert 'row tiles' in lib.nr_last_error().decode()
     assert lib.nr_gemm32(A, 8, B, 8, 0, None, C, 8, 0, 8, 8, 0, None) == 0        # empty: no launch
-    if not os.environ.get('NR_SDF5'):
+    if not _lib_env_int('NR_SDF5'):
         assert lib.nr_sdf5_enable(1) == -1 and 'NR_SDF5' in lib.nr_last_error().decode()
         assert lib.nr_sdf5_enable(0) == 0
 
