@@ -967,10 +967,13 @@ constexpr int kSlabRing = 3;
 // slab ring shares the LDS (reverse passes); 4 in the forward-only launches, whose LDS holds the
 // weight ring alone (a 37 KB chunk x 4 = 148 KB): three chunks in flight instead of two against the
 // L2 latency of the stream
-template <int CBMAX, int RING = 3>
+// NW: waves of the workgroup (kW4; 4 in the narrow forward-only launches, sdf4_kernel), every one of
+// them a loader when NW != kW4
+template <int CBMAX, int RING = 3, int NW = kW4>
 struct WStream4 {
   static_assert(RING == 3 || RING == 4, "weight ring depth");
   static constexpr int kRingN = RING;
+  static constexpr int kLd = NW == kW4 ? kLoad : NW;  // loader waves
   char* lds;
   char* slab;  // kSlabRing x kSlab4
   int cur;     // ring slot of the chunk being computed
@@ -982,12 +985,12 @@ struct WStream4 {
   __device__ __forceinline__ static int nextr(int i) { return i == RING - 1 ? 0 : i + 1; }
   // the slot chunk c + RING - 1 goes into: the one chunk c - 1 left (every wave is past it)
   __device__ __forceinline__ int ahead_slot() const { return cur == 0 ? RING - 1 : cur - 1; }
-  // BYTES/1 KB pieces; every loader wave (the last kLoad of the workgroup) issues ceil(pieces/kLoad)
+  // BYTES/1 KB pieces; every loader wave (the last kLd of the workgroup) issues ceil(pieces/kLd)
   // (a wave past the end repeats the last piece: identical bytes to the same LDS address) so the
   // count is one constant in every loader wave
   template <int BYTES>
-  __device__ __forceinline__ static constexpr int pieces() { return (BYTES / 1024 + kLoad - 1) / kLoad; }
-  __device__ __forceinline__ static int loader() { return wave_id() - (kW4 - kLoad); }  // < 0: no DMA
+  __device__ __forceinline__ static constexpr int pieces() { return (BYTES / 1024 + kLd - 1) / kLd; }
+  __device__ __forceinline__ static int loader() { return wave_id() - (NW - kLd); }  // < 0: no DMA
   template <int BYTES>
   __device__ __forceinline__ static int npieces() { return loader() >= 0 ? pieces<BYTES>() : 0; }
   // Each wave moves a contiguous run of NPW pieces (the last wave's run is shifted back to end at
@@ -1649,10 +1652,18 @@ struct NoPre4 {
 // pair (NABLA, no feature): STAGE 1 runs the forward and leaves each 16-point tile's slabs (softplus
 // log2 terms, d sdf / d z7) in a.slabs at the tile's index; STAGE 2 runs only the reverse pass, on the
 // 16-point tiles of the device list a.tiles[0 .. *a.n_tiles) (nablas of those points).
-template <bool NABLA, bool FEAT, int STAGE>
-__global__ __attribute__((amdgpu_flat_work_group_size(kT4, kT4), amdgpu_waves_per_eu(kWPE, kWPE)))
+template <bool NABLA, bool FEAT, int STAGE_>
+__global__ __attribute__((amdgpu_flat_work_group_size(STAGE_ == 3 ? 256 : kT4, STAGE_ == 3 ? 256 : kT4),
+                          amdgpu_waves_per_eu(kWPE, kWPE)))
 void sdf4_kernel(SdfKArgs a) {
+  // STAGE_ 3: the forward of a small launch (launch_sdf: at most 64 points per CU) on 64-point tiles of 4
+  // waves, one per SIMD -- twice the CUs of 128-point tiles, half the matrix work per CU and chunk (each
+  // workgroup streams the whole net once per tile either way); otherwise STAGE 0, the same per-point code
+  constexpr int STAGE = STAGE_ == 3 ? 0 : STAGE_;
+  constexpr int NW = STAGE_ == 3 ? 4 : kW4;  // waves per workgroup
+  static_assert(STAGE_ != 3 || (!NABLA && !FEAT && kW4 == 8), "narrow tiles: forward-only launches");
   static_assert(STAGE == 0 || (NABLA && !FEAT && kNC == 1), "deferred nablas: 16-point waves, no feature");
+  constexpr int PPW = 16 * kNC * NW;  // points per workgroup tile
   constexpr int CB = chunk_bytes(18);  // largest SDF op chunk (F4: 14 + 4 input blocks)
   constexpr int C16 = chunk_bytes(16), C4 = chunk_bytes(4), C14 = chunk_bytes(14), C18 = chunk_bytes(18);
   // launches with a reverse pass share the LDS with the slab ring (3 weight slots); forward-only
@@ -1662,7 +1673,7 @@ void sdf4_kernel(SdfKArgs a) {
   constexpr int RING = SLABS ? 3 : NR_FWD_RING;
   __shared__ __attribute__((aligned(16))) char smem[RING * CB + (SLABS ? kSlabRing * kSlab4 : 0)];
   static_assert(RING * CB + (SLABS ? kSlabRing * kSlab4 : 0) <= 160 * 1024, "LDS budget");
-  WStream4<CB, RING> ws{smem, SLABS ? smem + RING * CB : nullptr, 0, 0, 0, 0};
+  WStream4<CB, RING, NW> ws{smem, SLABS ? smem + RING * CB : nullptr, 0, 0, 0, 0};
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int j = lane & 15, g = lane >> 4;
   const char* W = a.packed;
@@ -1707,8 +1718,8 @@ void sdf4_kernel(SdfKArgs a) {
   // STAGE 2 walks the tile list, 8 tiles (one per wave) per workgroup iteration
   const int64_t Pn = STAGE == 2 ? (int64_t)(*a.n_tiles) * kPointsPerWG / kW4
                                 : (a.P_dev ? min(a.P, (int64_t)(*a.P_dev) * a.P_mult) : a.P);
-  for (int64_t base = (int64_t)blockIdx.x * kPointsPerWG; base < Pn; base += (int64_t)gridDim.x * kPointsPerWG) {
-    const bool has_next = base + (int64_t)gridDim.x * kPointsPerWG < Pn;
+  for (int64_t base = (int64_t)blockIdx.x * PPW; base < Pn; base += (int64_t)gridDim.x * PPW) {
+    const bool has_next = base + (int64_t)gridDim.x * PPW < Pn;
     int64_t p0 = base + wave * 16 * kNC;  // this wave's first point
     if constexpr (STAGE == 2) {  // this wave's tile (the last one again past the list's end: nothing stored)
       const int64_t ti = min(p0 / 16, (int64_t)(*a.n_tiles) - 1);
@@ -1996,6 +2007,7 @@ void sdf4_kernel(SdfKArgs a) {
       g_nr_stamps[(blockIdx.x * kW4 + wave) * kStampPh + i] = stamp_lds()[wave * kStampPh + i];
 #endif
 }
+
 
 // =============================================================================================
 // SIREN SDF kernel (base.py:84-115 SirenLayer, ImplicitSurface(use_siren=True) with
@@ -3862,10 +3874,15 @@ const int g_sdf5_pack = [] {
   return (e && atoi(e) != 0) ? 1 : 0;
 }();
 
-static int grid_for(int64_t P) {
+static int cu_count() {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int64_t need = (P + kPointsPerWG - 1) / kPointsPerWG;
+  return cus;
+}
+
+static int grid_for(int64_t P, int ppw = kPointsPerWG) {
+  const int cus = cu_count();
+  const int64_t need = (P + ppw - 1) / ppw;
   return (int)(need < cus ? (need > 0 ? need : 1) : cus);
 }
 
@@ -3906,6 +3923,8 @@ int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t
   } else {
     if (L.prec == NR_PREC_F16X3) {
       if (feature) hipLaunchKernelGGL((sdf4_kernel<false, true, 0>), dim3(grid), dim3(kT4), 0, stream, a);
+      else if (kW4 == 8 && P <= (int64_t)64 * cu_count())  // a few thousand points: 64-point tiles on all CUs
+        hipLaunchKernelGGL((sdf4_kernel<false, false, 3>), dim3(grid_for(P, 64)), dim3(256), 0, stream, a);
       else hipLaunchKernelGGL((sdf4_kernel<false, false, 0>), dim3(grid), dim3(kT4), 0, stream, a);
     }
     else hipLaunchKernelGGL((sdf_kernel<NR_PREC_FP32, false>), dim3(grid), dim3(kThreads), 0, stream, a);

@@ -59,6 +59,28 @@ def test_sdf_net_ragged_sizes():
         assert report(f'h P={P}', h, ref_h, 1e-5, 1e-6)[0].all()
 
 
+def test_sdf_forward_narrow_tiles_bit_identical():
+    """launch_sdf runs forward-only launches of at most 64 points per CU on 64-point tiles (sdf4_kernel
+    STAGE 3: 4 waves, one per SIMD) and larger ones on 128-point tiles: the same per-point code, so every
+    point's sdf is bit-identical between the two (ragged sizes, the size limit itself, an offset slice),
+    and the narrow launches meet the oracle bar"""
+    from oracle.nets import SDFNet
+    sd = wg.neus_state(seed=11)
+    m = neus_model(sd)
+    orc = SDFNet(sd)
+    torch.manual_seed(1)
+    lim = 64 * torch.cuda.get_device_properties(0).multi_processor_count
+    x = torch.randn(lim + 4096, 3) * 0.7
+    xg = x.cuda()
+    with torch.no_grad():
+        wide = m.implicit_surface.forward(xg)  # more than 64 points per CU: 128-point tiles
+        for p0, n in ((0, 1), (5, 17), (100, 129), (1000, 1000), (0, lim), (lim - 4096, 4096)):
+            narrow = m.implicit_surface.forward(xg[p0:p0 + n].contiguous())
+            assert torch.equal(narrow, wide[p0:p0 + n]), (p0, n, float((narrow - wide[p0:p0 + n]).abs().max()))
+        s = m.implicit_surface.forward(xg[:2000].contiguous())
+    assert report('sdf narrow tiles P=2000', s, orc.sdf(x[:2000]), 1e-5, 1e-6)[0].all()
+
+
 def test_radiance_vs_golden(golden):
     g = golden('radiance')
     m = neus_model(wg.neus_state(seed=int(g['seed_neus'])))
