@@ -133,7 +133,7 @@ struct PackOp {
 };
 
 int launch_pack_op(const PackOp& op, char* dst, hipStream_t stream);
-// the ops of one pack call, batched (three launches per 8 ops)
+// the ops of one pack call, batched (three launches per 20 ops)
 int launch_pack_ops(const PackOp* ops, char* const* dst, int nops, hipStream_t stream);
 int launch_pack_vec(const float* src, int off, int nvalid, int n, char* dst, hipStream_t stream);
 int launch_sdf(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,

@@ -3689,12 +3689,13 @@ __device__ __forceinline__ void pack_word(const PackOp& op, uint32_t* __restrict
 // kPackBatch through three launches -- pack_rows_kernel and pack_final_kernel (max |W * scale| for the
 // f16x3 weight scale, and the op's bound) and pack_ops_kernel (one thread per packed word, blockIdx.y =
 // op) -- instead of two memsets and three launches per op.
-constexpr int kPackBatch = 8;
+constexpr int kPackBatch = 20;  // a whole SDF pack (17 ops) in one batch: three launches per pack call
 struct PackBatch {
   PackOp op[kPackBatch];
   uint32_t* dst[kPackBatch];
   int64_t n[kPackBatch];  // packed words of op i
 };
+static_assert(sizeof(PackBatch) <= 4096, "kernel argument size");
 
 // one thread per 32-bit word of the packed op
 __global__ void pack_ops_kernel(PackBatch pb) {
