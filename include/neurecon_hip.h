@@ -197,7 +197,8 @@ typedef struct {
   const float* t_out_rand;
   const float* s_dev; /* optional device scalar s (overrides `s`): no host round trip per call */
   /* sample_only = 1 (training, neus.py:206-279 under torch.no_grad): stop after the upsampling and
-   * write the sorted sample depths d_all_out [n_rays, S]; rgb / depth / acc may then be NULL.  The
+   * write the sorted sample depths d_all_out [n_rays, S]; rgb / depth / acc and rad_packed (the radiance
+   * net is not evaluated; `rad` still describes it) may then be NULL.  The
    * differentiable part of the step (SDF + nablas, radiance, compositing) runs through the
    * nr_train entry points below. */
   int sample_only;
@@ -367,7 +368,7 @@ typedef struct {
   /* training (unisurf.py:140-211 under torch.no_grad in neurecon_amd's training render): d_all_out
    * [n_rays, P] receives each ray's sorted sample depths d_all (unisurf.py:201); sample_only != 0 stops
    * after the sampling (root finding + interval / free-space samples; surface_points / mask_surface /
-   * depth_surface are still written when given) -- rgb / depth / acc may then be NULL */
+   * depth_surface are still written when given) -- rgb / depth / acc and rad_packed may then be NULL */
   float* d_all_out;
   int sample_only;
   /* full_march != 0: the root-finding march evaluates every step of every ray in one launch (the

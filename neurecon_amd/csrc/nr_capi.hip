@@ -710,8 +710,8 @@ static int check_unisurf(const NrUnisurfArgs* a) {
              NR_ERR_ARG, "nr_unisurf_render: null ray or output pointer");
   NR_REQUIRE(!a->sample_only || a->shard_row_rays <= 0, NR_ERR_ARG,
              "nr_unisurf_render: sample_only is not a sharded render");
-  NR_REQUIRE(a->sdf_packed && a->rad_packed && a->t_march && a->t_query && a->t_free, NR_ERR_ARG,
-             "nr_unisurf_render: null argument");
+  NR_REQUIRE(a->sdf_packed && a->rad && (a->rad_packed || a->sample_only) && a->t_march && a->t_query && a->t_free,
+             NR_ERR_ARG, "nr_unisurf_render: null argument");
   NR_REQUIRE(a->n_rays <= 0 || a->sample_only || !a->calc_normal || a->normals, NR_ERR_ARG,
              "nr_unisurf_render: calc_normal needs normals output");
   NR_REQUIRE(a->N_steps >= 2 && a->N_secant_steps >= 0 && a->N_query >= 1 && a->N_freespace >= 1, NR_ERR_ARG,
@@ -1175,7 +1175,8 @@ int nr_neus_render(const NrNeusArgs* a, void* stream) {
   NR_REQUIRE(a->n_rays <= 0 || (a->rays_o && a->rays_d && (a->sample_only ? a->d_all_out != nullptr
                                                                             : (a->rgb && a->depth && a->acc))),
              NR_ERR_ARG, "nr_neus_render: null ray or output pointer");
-  NR_REQUIRE(a->sdf_packed && a->rad_packed && a->t_coarse, NR_ERR_ARG, "nr_neus_render: null argument");
+  NR_REQUIRE(a->sdf_packed && a->rad && (a->rad_packed || a->sample_only) && a->t_coarse, NR_ERR_ARG,
+             "nr_neus_render: null argument");
   NR_REQUIRE(a->N_samples >= 2, NR_ERR_ARG, "nr_neus_render: N_samples must be >= 2");
   NR_REQUIRE(a->n_rays <= 0 || a->sample_only || !a->calc_normal || a->normals, NR_ERR_ARG,
              "nr_neus_render: calc_normal needs normals output");

@@ -232,12 +232,12 @@ def _sample_depths(ro, rd, model, dev, obj_bounding_radius, batched, B, rayschun
     n_up = N_importance if direct else (N_importance // N_upsample_iters if N_upsample_iters > 0 else 0)
     S = N_samples + (N_importance if direct else N_upsample_iters * n_up)
     sdf_desc, sdf_packed = model.implicit_surface.nr_packed(dev)
-    rad_desc, rad_packed = model.radiance_net.nr_packed(dev)
+    rad_desc = model.radiance_net.nr_desc()  # the sample pass never evaluates the radiance net: no pack
     d_all = torch.empty(n, S, device=dev)
     a = L.NrNeusArgs()
     a.rays_o, a.rays_d, a.n_rays = L.ptr(ro), L.ptr(rd), n
     a.sdf, a.sdf_packed = ctypes.pointer(sdf_desc), L.ptr(sdf_packed)
-    a.rad, a.rad_packed = ctypes.pointer(rad_desc), L.ptr(rad_packed)
+    a.rad, a.rad_packed = ctypes.pointer(rad_desc), None
     a.obj_bounding_radius = float(obj_bounding_radius)
     a.near_bypass = float('nan') if near_bypass is None else float(near_bypass)
     a.far_bypass = float('nan') if far_bypass is None else float(far_bypass)

@@ -980,7 +980,7 @@ class RadianceTG(torch.autograd.Function):
         dev = rgb.device
         st = L.stream_of(dev)
         P = rgb.shape[0]
-        desc, _ = net.nr_packed(dev)
+        desc = net.nr_desc()  # the layout only (no render pack)
         info = _op_info('rad', desc, 10)
         tp = _train_pack(net, 'rad', saved[6:11], [l.bias for l in net.layers], dev)  # the forward's effective weights
         tb = tp.data_ptr()
