@@ -301,19 +301,23 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   }
   if (c.n_iters > 0 && (rc = merge(c.S - n_up))) return rc;
   if (defer) {  // nablas of the tiles holding a sample of non-zero interval weight; the rest stay 0
-    const int64_t nslot = (int64_t)c.S * R, ntile = nslot / 16;
+    const int64_t nslot = (int64_t)c.S * R;
+    // per sample slot (compacted reverse pass) when the slab offsets fit 32 bits, else per 16-slot tile
+    const bool pts_list = nslot <= kDeferredCompactMax;
+    const int64_t nflag = pts_list ? nslot : nslot / 16;
+    c.tshift = pts_list ? 0 : 4;
     NR_HIP_CHECK(hipMemsetAsync(c.nraw, 0, (size_t)nslot * 3 * sizeof(float), st));
     if (a.calc_normal && a.N_outside == 0) {  // normals_volume is the only reader of the sample nablas here
       // (with NeRF++ the flags need the background's alphas: after the background net, below)
-      NR_HIP_CHECK(hipMemsetAsync(c.tflag, 0, (size_t)ntile * sizeof(int), st));
+      NR_HIP_CHECK(hipMemsetAsync(c.tflag, 0, (size_t)nflag * sizeof(int), st));
       NR_HIP_CHECK(hipMemsetAsync(c.tcnt, 0, sizeof(int), st));
       const int64_t nq = (int64_t)(c.S - 1) * R;
       hipLaunchKernelGGL(neus_sample_need, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, c, a.s_dev, a.s);
       NR_HIP_CHECK(hipGetLastError());
-      hipLaunchKernelGGL(neus_tile_list, dim3((unsigned)((ntile + 1023) / 1024)), dim3(1024), 0, st, c, ntile);
+      hipLaunchKernelGGL(neus_tile_list, dim3((unsigned)((nflag + 1023) / 1024)), dim3(1024), 0, st, c, nflag);
       NR_HIP_CHECK(hipGetLastError());
       if ((rc = launch_sdf_deferred(SL, a.sdf_packed, c.pts, nslot, nullptr, c.nraw, a.sdf->multires, c.slabs, c.tiles,
-                                    c.tcnt, 2, st)))
+                                    c.tcnt, pts_list ? 4 : 2, st)))
         return rc;
     }
   }
@@ -391,18 +395,21 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
       hipLaunchKernelGGL(neus_outside_scatter, g1, dim3(256), 0, st, slot, sigc, radc, Po, c.sig_o, c.rad_o);
       NR_HIP_CHECK(hipGetLastError());
     }
-    if (defer) {  // deferred sample nablas: tiles holding a sample whose (inside or background) alpha != 0
-      const int64_t nslot = (int64_t)c.S * R, ntile = nslot / 16;
+    if (defer) {  // deferred sample nablas: samples (or tiles) whose (inside or background) alpha != 0
+      const int64_t nslot = (int64_t)c.S * R;
+      const bool pts_list = nslot <= kDeferredCompactMax;
+      const int64_t nflag = pts_list ? nslot : nslot / 16;
+      c.tshift = pts_list ? 0 : 4;
       if (a.calc_normal) {
-        NR_HIP_CHECK(hipMemsetAsync(c.tflag, 0, (size_t)ntile * sizeof(int), st));
+        NR_HIP_CHECK(hipMemsetAsync(c.tflag, 0, (size_t)nflag * sizeof(int), st));
         NR_HIP_CHECK(hipMemsetAsync(c.tcnt, 0, sizeof(int), st));
         hipLaunchKernelGGL(neus_sample_need_outside, dim3((unsigned)((nslot + 255) / 256)), dim3(256), 0, st, c,
                            a.s_dev, a.s);
         NR_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(neus_tile_list, dim3((unsigned)((ntile + 1023) / 1024)), dim3(1024), 0, st, c, ntile);
+        hipLaunchKernelGGL(neus_tile_list, dim3((unsigned)((nflag + 1023) / 1024)), dim3(1024), 0, st, c, nflag);
         NR_HIP_CHECK(hipGetLastError());
         if ((rc = launch_sdf_deferred(SL, a.sdf_packed, c.pts, nslot, nullptr, c.nraw, a.sdf->multires, c.slabs,
-                                      c.tiles, c.tcnt, 2, st)))
+                                      c.tiles, c.tcnt, pts_list ? 4 : 2, st)))
           return rc;
       }
       hipLaunchKernelGGL(neus_gather_nablas, dim3((unsigned)((nslot + 255) / 256)), dim3(256), 0, st, c);
@@ -1051,7 +1058,7 @@ static int softplus_net(const NrSdfDesc* d) {
   int rc = check_sdf_desc(d);
   if (rc) return rc;
   NR_REQUIRE(!d->siren && d->precision == NR_PREC_F16X3, NR_ERR_UNSUPPORTED,
-             "training GEMMs: f16x3 softplus SDF nets only (SIREN / fp32 nets train on hipBLASLt)");
+             "training GEMMs: f16x3 softplus SDF nets only (SIREN / fp32 nets train on nr_gemm32)");
   return NR_OK;
 }
 

@@ -1095,12 +1095,16 @@ struct WStream4 {
   // Staged two chunk-iterations before the epilogue that reads it.  Returns the DMA instructions issued.
   // e: byte base of the layer's slab (24-bit codes, kSlab24Chunk per column and chunk)
   __device__ __forceinline__ int stage_slab(const float4* e, int c) {
+    return stage_slab(e, c, (threadIdx.x & 63) * kSlabVB);
+  }
+  // voff: this lane's byte offset from e (lane x kSlabVB; the compacted reverse pass gathers each lane's
+  // codes from its point's own tile)
+  __device__ __forceinline__ int stage_slab(const float4* e, int c, uint32_t voff) {
 #ifdef NR_EXP_NO_ELOAD  // timing experiment: softplus' slab not read back
     return 0;
 #endif
     // global: 768 B per piece (64 lanes x 12 B); LDS: 1 KB per piece (lane stride 16 B), so each piece
     // gets its own global base and M0 (the instruction offset would step both by the same amount)
-    const uint32_t voff = (threadIdx.x & 63) * kSlabVB;
     const char* g = uniform_ptr((const char*)e + kNC * kSlab24Chunk * c);
     const uint32_t base =
         __builtin_amdgcn_readfirstlane(lds_u32(slab) + (uint32_t)(es * kSlab4 + wave_id() * kSlabW));
@@ -1612,6 +1616,7 @@ struct BwdEpi4 {
   float (&mrun)[kNC];
   Pend4& pd;
   int lane;
+  int plane;  // this lane's float4 index in the parked embedding gradients (lane; compacted: its point's)
   float4 y[kNC][2];
   __device__ __forceinline__ void operator()(int c, const Z4& zz, int st) {
     if (2 * c < NMAIN) {
@@ -1639,7 +1644,7 @@ struct BwdEpi4 {
         pd.v[q] = zz.z[q][0];
         pd.v[kNC + q] = zz.z[q][1];
       }
-      pend_chunk(pd, park, park_blk + 2 * c - NMAIN, lane, false);
+      pend_chunk(pd, park, park_blk + 2 * c - NMAIN, plane, false);
     }
   }
 };
@@ -1659,7 +1664,10 @@ void sdf4_kernel(SdfKArgs a) {
   // STAGE_ 3: the forward of a small launch (launch_sdf: at most 64 points per CU) on 64-point tiles of 4
   // waves, one per SIMD -- twice the CUs of 128-point tiles, half the matrix work per CU and chunk (each
   // workgroup streams the whole net once per tile either way); otherwise STAGE 0, the same per-point code
-  constexpr int STAGE = STAGE_ == 3 ? 0 : STAGE_;
+  // STAGE_ 4: STAGE 2 over a device list of points instead of tiles (each wave 16 listed points, every
+  // lane reading its point's slab codes from that point's own tile)
+  constexpr int STAGE = STAGE_ == 3 ? 0 : (STAGE_ == 4 ? 2 : STAGE_);
+  constexpr bool COMPACT = STAGE_ == 4;
   constexpr int NW = STAGE_ == 3 ? 4 : kW4;  // waves per workgroup
   static_assert(STAGE_ != 3 || (!NABLA && !FEAT && kW4 == 8), "narrow tiles: forward-only launches");
   static_assert(STAGE == 0 || (NABLA && !FEAT && kNC == 1), "deferred nablas: 16-point waves, no feature");
@@ -1716,12 +1724,23 @@ void sdf4_kernel(SdfKArgs a) {
   const float kSpSlack = 0.0070f;  // softplus(z) <= max(z, 0) + ln2/100
 
   // STAGE 2 walks the tile list, 8 tiles (one per wave) per workgroup iteration
-  const int64_t Pn = STAGE == 2 ? (int64_t)(*a.n_tiles) * kPointsPerWG / kW4
-                                : (a.P_dev ? min(a.P, (int64_t)(*a.P_dev) * a.P_mult) : a.P);
+  const int64_t Pn = COMPACT      ? ((int64_t)(*a.n_tiles) + 15) / 16 * 16
+                     : STAGE == 2 ? (int64_t)(*a.n_tiles) * kPointsPerWG / kW4
+                                  : (a.P_dev ? min(a.P, (int64_t)(*a.P_dev) * a.P_mult) : a.P);
   for (int64_t base = (int64_t)blockIdx.x * PPW; base < Pn; base += (int64_t)gridDim.x * PPW) {
     const bool has_next = base + (int64_t)gridDim.x * PPW < Pn;
     int64_t p0 = base + wave * 16 * kNC;  // this wave's first point
-    if constexpr (STAGE == 2) {  // this wave's tile (the last one again past the list's end: nothing stored)
+    int plane = lane;                      // float4 index of this lane's slab-7 / parked entries
+    uint32_t soff = 0;                     // byte offset of this lane's slab codes (COMPACT)
+    int64_t pl = 0;                        // this lane's listed point (COMPACT)
+    if constexpr (COMPACT) {  // list entries [p0, p0 + 16): one point per lane j (the last again past the end)
+      const int64_t n = *a.n_tiles;
+      pl = a.tiles[min(p0 + j, n - 1)];
+      const uint32_t ts = (uint32_t)(pl >> 4), js = (uint32_t)(pl & 15);
+      plane = (int)(ts * (uint32_t)(kSlabColBytes / 16) + js + 16u * (uint32_t)g);
+      soff = ts * (uint32_t)kSlabColBytes + (js + 16u * (uint32_t)g) * (uint32_t)kSlabVB;
+      escr = uniform_ptr(a.slabs);
+    } else if constexpr (STAGE == 2) {  // this wave's tile (the last one again past the list's end: nothing stored)
       const int64_t ti = min(p0 / 16, (int64_t)(*a.n_tiles) - 1);
       const int64_t tile = a.tiles[ti];
       escr = uniform_ptr((float4*)((char*)a.slabs + (size_t)tile * kSlabColBytes));
@@ -1736,8 +1755,13 @@ void sdf4_kernel(SdfKArgs a) {
 #pragma unroll
     for (int q = 0; q < kNC; ++q) {
       const int64_t p = p0 + 16 * q + j;
-      valid[q] = p < Pv;
-      pq[q] = valid[q] ? p : Pv - 1;
+      if constexpr (COMPACT) {
+        valid[q] = p < (int64_t)(*a.n_tiles);
+        pq[q] = pl;
+      } else {
+        valid[q] = p < Pv;
+        pq[q] = valid[q] ? p : Pv - 1;
+      }
       xs[q][0] = a.pts[pq[q] * 3 + 0];
       xs[q][1] = a.pts[pq[q] * 3 + 1];
       xs[q][2] = a.pts[pq[q] * 3 + 2];
@@ -1920,7 +1944,7 @@ void sdf4_kernel(SdfKArgs a) {
       for (int q = 0; q < kNC; ++q) {  // d sdf / d z7 from slab 7, split with the exact max scale
         float4 G[16];
 #pragma unroll
-        for (int b = 0; b < 16; ++b) G[b] = fromf(*((const gf4*)g7 + (kNC * b + q) * 64 + lane));
+        for (int b = 0; b < 16; ++b) G[b] = fromf(*((const gf4*)g7 + (kNC * b + q) * 64 + (COMPACT ? plane : lane)));
         float m = 0.0f;
 #pragma unroll
         for (int b = 0; b < 16; b += 2) m = amax8(m, G[b], G[b + 1]);
@@ -1936,7 +1960,8 @@ void sdf4_kernel(SdfKArgs a) {
       // two chunk-iterations ahead of the epilogue that reads it: chunk c+1's slab goes out right after
       // chunk c's weight DMA, the next op's chunk 0 during this op's last chunk); output chunks >=
       // NMAIN/2 are embedding gradients, parked in fp32
-      ws.stage_slab(slab(6), 0);  // B7's chunk 0 (consumed in B7's second iteration)
+      if constexpr (COMPACT) ws.stage_slab(slab(6), 0, soff);  // B7's chunk 0 (consumed in B7's second iteration)
+      else ws.stage_slab(slab(6), 0);
       auto bwd = [&](auto kb_tag, auto nbo_tag, auto nmain_tag, auto nxt_tag, int opi, const char* nxt,
                      f16x8(&ih)[kNC][12], f16x8(&il)[kNC][12], f16x8(&oh)[kNC][12], f16x8(&ol)[kNC][12], int lcur,
                      int park_blk, int lnext) {
@@ -1945,11 +1970,16 @@ void sdf4_kernel(SdfKArgs a) {
         float sc[kNC];
         next_scales(KBo, 0.0f, zero2, sc);
         auto pre = [&](int c) -> int {
-          if (2 * (c + 1) < NMAIN) return ws.stage_slab(slab(lcur), c + 1);
-          if (c + 1 == NBOo / 2 && lnext >= 0) return ws.stage_slab(slab(lnext), 0);
+          if constexpr (COMPACT) {
+            if (2 * (c + 1) < NMAIN) return ws.stage_slab(slab(lcur), c + 1, soff);
+            if (c + 1 == NBOo / 2 && lnext >= 0) return ws.stage_slab(slab(lnext), 0, soff);
+          } else {
+            if (2 * (c + 1) < NMAIN) return ws.stage_slab(slab(lcur), c + 1);
+            if (c + 1 == NBOo / 2 && lnext >= 0) return ws.stage_slab(slab(lnext), 0);
+          }
           return 0;
         };
-        BwdEpi4<NMAIN, decltype(ws)> epi{oh, ol, sc, ws, park, park_blk, mrun, pd, lane};
+        BwdEpi4<NMAIN, decltype(ws)> epi{oh, ol, sc, ws, park, park_blk, mrun, pd, lane, COMPACT ? plane : lane};
         op4<KBo, NBOo, NXC, false, false>(ws, OP(opi), nxt, ih, il, xinv, pd, pre, epi, lane);
         finish(sc);
       };
@@ -1979,8 +2009,8 @@ void sdf4_kernel(SdfKArgs a) {
         float n0 = 0.f, n1 = 0.f, n2 = 0.f;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          const float4 u = fromf(*((const gf4*)park + (kNC * b + q) * 64 + lane));
-          const float4 v = fromf(*((const gf4*)park + (kNC * (4 + b) + q) * 64 + lane));
+          const float4 u = fromf(*((const gf4*)park + (kNC * b + q) * 64 + (COMPACT ? plane : lane)));
+          const float4 v = fromf(*((const gf4*)park + (kNC * (4 + b) + q) * 64 + (COMPACT ? plane : lane)));
           const int f = 16 * b + 4 * g;
           embed_backward(f + 0, fadd(v.x, u.x), xs[q][0], xs[q][1], xs[q][2], a.nfreq, n0, n1, n2);
           embed_backward(f + 1, fadd(v.y, u.y), xs[q][0], xs[q][1], xs[q][2], a.nfreq, n0, n1, n2);
@@ -1991,7 +2021,7 @@ void sdf4_kernel(SdfKArgs a) {
         n1 = wave_sum4(n1);
         n2 = wave_sum4(n2);
         if (valid[q] && g == 0) {
-          const int64_t p = p0 + 16 * q + j;
+          const int64_t p = COMPACT ? pq[q] : p0 + 16 * q + j;
           a.nabla[p * 3 + 0] = n0;
           a.nabla[p * 3 + 1] = n1;
           a.nabla[p * 3 + 2] = n2;
@@ -3942,9 +3972,13 @@ int launch_sdf_deferred(const SdfLayout& L, const void* packed, const float* pts
   if (stage == 1) {
     ProfScope prof("sdf_nabla_fwd", (double)P, stream);
     hipLaunchKernelGGL((sdf4_kernel<true, false, 1>), dim3(grid_for(P)), dim3(kT4), 0, stream, a);
-  } else {
+  } else if (stage == 2) {
     ProfScope prof("sdf_nabla_bwd", (double)P, stream, n_tiles, 16);
     hipLaunchKernelGGL((sdf4_kernel<true, false, 2>), dim3(grid_for(P)), dim3(kT4), 0, stream, a);
+  } else {  // 4: `tiles` lists sample slots (the per-lane 32-bit slab offsets: P < kDeferredCompactMax)
+    NR_REQUIRE(stage == 4 && P <= kDeferredCompactMax, NR_ERR_ARG, "deferred nablas: bad stage");
+    ProfScope prof("sdf_nabla_bwd", (double)P, stream, n_tiles, 1);
+    hipLaunchKernelGGL((sdf4_kernel<true, false, 4>), dim3(grid_for(P)), dim3(kT4), 0, stream, a);
   }
   NR_HIP_CHECK(hipGetLastError());
   return NR_OK;

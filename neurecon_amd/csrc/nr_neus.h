@@ -25,8 +25,10 @@ struct NeusChunk {
   // deferred sample nablas (official_solution, no detailed outputs): the sample launches leave each
   // 16-slot tile's slabs in `slabs` (sdf4_kernel STAGE 1); the tiles holding a sample whose interval
   // weight can be non-zero are flagged (tflag), listed (tiles / tcnt) and get their nablas in one
-  // reverse-pass launch (STAGE 2); the rest of nraw stays 0 (those samples are weighted by exactly 0)
-  float4* slabs; int* tflag; int* tiles; int* tcnt;
+  // reverse-pass launch (STAGE 2); the rest of nraw stays 0 (those samples are weighted by exactly 0).
+  // tshift 0: the flags and the list are per sample slot, and the reverse pass runs on the listed
+  // samples alone (STAGE 4, sdf4_kernel); 4: per 16-slot tile
+  float4* slabs; int* tflag; int* tiles; int* tcnt; int tshift;
   float* sdf_m; float* nab_m; float* feat_m; float* rad_m;
   // NeRF++ background (N_out = 0: none); M = S-1+N_out samples, sample-major
   int N_out;

@@ -646,7 +646,7 @@ __global__ void neus_sample_need(NeusChunk c, const float* __restrict__ s_dev, f
   const float cp = sigmoidf_ref(fmul(c.sdf_f[(int64_t)i * R + r], s_inv));
   const float cn = sigmoidf_ref(fmul(c.sdf_f[(int64_t)(i + 1) * R + r], s_inv));
   const float alpha = fmaxf(fdiv(fsub(cp, cn), fadd(cp, 1e-10f)), 0.0f);
-  if (!(alpha == 0.0f)) c.tflag[((int64_t)c.idv[q] * R + r) >> 4] = 1;
+  if (!(alpha == 0.0f)) c.tflag[((int64_t)c.idv[q] * R + r) >> c.tshift] = 1;
 }
 
 // the same with the NeRF++ background (neus_composite_outside): sample k < S weights its unit nabla by
@@ -678,10 +678,10 @@ __global__ void neus_sample_need_outside(NeusChunk c, const float* __restrict__ 
     const float dist = k + 1 < M ? fsub(c.d_out[q + R], dk) : 1e10f;
     alpha = fsub(1.0f, expf(fmul(-softplus1(c.sig_o[q]), dist)));
   }
-  if (!(alpha == 0.0f)) c.tflag[((int64_t)c.idv[q] * R + r) >> 4] = 1;
+  if (!(alpha == 0.0f)) c.tflag[((int64_t)c.idv[q] * R + r) >> c.tshift] = 1;
 }
 
-// flagged tiles -> list (any order: each tile's nablas depend on that tile alone)
+// flagged tiles (or sample slots, tshift 0) -> list (any order: each point's nabla depends on that point alone)
 __global__ void neus_tile_list(NeusChunk c, int64_t n_tiles) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool need = t < n_tiles && c.tflag[t] != 0;
@@ -1044,8 +1044,10 @@ NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc) {
   p.o_idv2 = take((size_t)S * Rc);
   const size_t tiles = neus_deferred(a, Rc) ? ((size_t)S * Rc + 15) / 16 : 1;
   p.o_slabs = take(neus_deferred(a, Rc) ? tiles * (kSlabColBytes / 4) : 1);  // 100 KB per 16-slot tile
-  p.o_tflag = take(tiles);
-  p.o_tiles = take(tiles);
+  // flags and list per sample slot (the compacted reverse pass) or per tile (chunks past kDeferredCompactMax)
+  const size_t slots = neus_deferred(a, Rc) ? (size_t)S * Rc : 1;
+  p.o_tflag = take(slots);
+  p.o_tiles = take(slots);
   p.o_tcnt = take(1);
   p.o_mlp = off;
   p.total = off + nr_mlp_workspace_bytes(1);
