@@ -58,7 +58,7 @@ PMC_SUMMARY = {'f16x3': 'profiles/r06/f16x3_pmc_summary.json'}  # tools/gpu_fina
 # SQ_VALU_MFMA_BUSY_CYCLES passes of this bench, tools/gpu_mfma_r05.sh -> tools/mfma_summary.py)
 MFMA_SUMMARY = 'profiles/r06/mfma_summary.json'
 MFMA_KERNEL = {'sdf_nabla_fwd': 'void nr::sdf4_kernel<true, false, 1>(nr::SdfKArgs)',
-               'sdf_nabla_bwd': 'void nr::sdf4_kernel<true, false, 2>(nr::SdfKArgs)',
+               'sdf_nabla_bwd': 'void nr::sdf4_kernel<true, false, 4>(nr::SdfKArgs)',  # r06: the compacted pass
                'sdf_nabla_feat': 'void nr::sdf4_kernel<true, true, 0>(nr::SdfKArgs)'}
 # device kernels behind each merged library kernel name (sdf_nabla = samples + mid-points launches)
 PMC_KERNEL = {('sdf_nabla', 'f16x3'): ('void nr::sdf4_kernel<true, false>(nr::SdfKArgs)',       # r02 names
@@ -66,7 +66,9 @@ PMC_KERNEL = {('sdf_nabla', 'f16x3'): ('void nr::sdf4_kernel<true, false>(nr::Sd
                                        # r03: deferred sample nablas (forward + slabs, reverse pass), mid-points
                                        'void nr::sdf4_kernel<true, false, 1>(nr::SdfKArgs)',
                                        'void nr::sdf4_kernel<true, false, 2>(nr::SdfKArgs)',
-                                       'void nr::sdf4_kernel<true, true, 0>(nr::SdfKArgs)'),
+                                       'void nr::sdf4_kernel<true, true, 0>(nr::SdfKArgs)',
+                                       # r06: the reverse pass over listed samples (chunks <= 671 072 slots)
+                                       'void nr::sdf4_kernel<true, false, 4>(nr::SdfKArgs)'),
               ('sdf_nabla', 'fp32'): ('void nr::sdf_kernel<0, true>(nr::SdfKArgs)',)}
 
 
@@ -231,8 +233,8 @@ def eager_gpu_baseline(dev, n_rays, reps=3):
 # without the geometry feature skip its 256 rows of the last layer
 KERNEL_MAC = {'sdf_fwd': MAC_SDF_FWD_NOFEAT, 'sdf_feat': MAC_SDF_FWD, 'sdf_nabla': MAC_SDF_FWD_NOFEAT + MAC_SDF_BWD,
               'sdf_nabla_feat': MAC_SDF_FWD + MAC_SDF_BWD, 'radiance': MAC_RAD, 'nerf': MAC_NERF,
-              # deferred sample nablas: forward of every sample, reverse pass of the 16-point tiles whose
-              # samples have non-zero weight (units = tile points)
+              # deferred sample nablas: forward of every sample, reverse pass of the samples of non-zero
+              # weight (units = listed samples; r03-r05 and chunks past 671 072 slots: their 16-point tiles)
               'sdf_nabla_fwd': MAC_SDF_FWD_NOFEAT, 'sdf_nabla_bwd': MAC_SDF_BWD,
               # training GEMMs report MACs (padded 16x16 blocks) as their units
               'train_gemm': 1}
