@@ -302,22 +302,19 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
   if (c.n_iters > 0 && (rc = merge(c.S - n_up))) return rc;
   if (defer) {  // nablas of the tiles holding a sample of non-zero interval weight; the rest stay 0
     const int64_t nslot = (int64_t)c.S * R;
-    // per sample slot (compacted reverse pass) when the slab offsets fit 32 bits, else per 16-slot tile
-    const bool pts_list = nslot <= kDeferredCompactMax;
-    const int64_t nflag = pts_list ? nslot : nslot / 16;
-    c.tshift = pts_list ? 0 : 4;
+    c.tshift = 0;  // flags per sample slot, the reverse pass on the listed samples (sdf4_kernel STAGE 4)
     NR_HIP_CHECK(hipMemsetAsync(c.nraw, 0, (size_t)nslot * 3 * sizeof(float), st));
     if (a.calc_normal && a.N_outside == 0) {  // normals_volume is the only reader of the sample nablas here
       // (with NeRF++ the flags need the background's alphas: after the background net, below)
-      NR_HIP_CHECK(hipMemsetAsync(c.tflag, 0, (size_t)nflag * sizeof(int), st));
+      NR_HIP_CHECK(hipMemsetAsync(c.tflag, 0, (size_t)nslot * sizeof(int), st));
       NR_HIP_CHECK(hipMemsetAsync(c.tcnt, 0, sizeof(int), st));
       const int64_t nq = (int64_t)(c.S - 1) * R;
       hipLaunchKernelGGL(neus_sample_need, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, c, a.s_dev, a.s);
       NR_HIP_CHECK(hipGetLastError());
-      hipLaunchKernelGGL(neus_tile_list, dim3((unsigned)((nflag + 1023) / 1024)), dim3(1024), 0, st, c, nflag);
+      hipLaunchKernelGGL(neus_point_list, dim3((unsigned)((nslot + 1023) / 1024)), dim3(1024), 0, st, c, nslot);
       NR_HIP_CHECK(hipGetLastError());
       if ((rc = launch_sdf_deferred(SL, a.sdf_packed, c.pts, nslot, nullptr, c.nraw, a.sdf->multires, c.slabs, c.tiles,
-                                    c.tcnt, pts_list ? 4 : 2, st)))
+                                    c.tcnt, 4, st)))
         return rc;
     }
   }
@@ -397,19 +394,17 @@ static int neus_chunk(const NrNeusArgs& a, const NeusPlan& pl, int64_t ray0, int
     }
     if (defer) {  // deferred sample nablas: samples (or tiles) whose (inside or background) alpha != 0
       const int64_t nslot = (int64_t)c.S * R;
-      const bool pts_list = nslot <= kDeferredCompactMax;
-      const int64_t nflag = pts_list ? nslot : nslot / 16;
-      c.tshift = pts_list ? 0 : 4;
+      c.tshift = 0;
       if (a.calc_normal) {
-        NR_HIP_CHECK(hipMemsetAsync(c.tflag, 0, (size_t)nflag * sizeof(int), st));
+        NR_HIP_CHECK(hipMemsetAsync(c.tflag, 0, (size_t)nslot * sizeof(int), st));
         NR_HIP_CHECK(hipMemsetAsync(c.tcnt, 0, sizeof(int), st));
         hipLaunchKernelGGL(neus_sample_need_outside, dim3((unsigned)((nslot + 255) / 256)), dim3(256), 0, st, c,
                            a.s_dev, a.s);
         NR_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(neus_tile_list, dim3((unsigned)((nflag + 1023) / 1024)), dim3(1024), 0, st, c, nflag);
+        hipLaunchKernelGGL(neus_point_list, dim3((unsigned)((nslot + 1023) / 1024)), dim3(1024), 0, st, c, nslot);
         NR_HIP_CHECK(hipGetLastError());
         if ((rc = launch_sdf_deferred(SL, a.sdf_packed, c.pts, nslot, nullptr, c.nraw, a.sdf->multires, c.slabs,
-                                      c.tiles, c.tcnt, pts_list ? 4 : 2, st)))
+                                      c.tiles, c.tcnt, 4, st)))
           return rc;
       }
       hipLaunchKernelGGL(neus_gather_nablas, dim3((unsigned)((nslot + 255) / 256)), dim3(256), 0, st, c);

@@ -146,9 +146,8 @@ extern int g_sdf5;             // route launch_sdf's forward-only f16x3 launches
 extern const int g_sdf5_pack;  // $NR_SDF5 (a nonzero integer) at load: the layout carries the 32x32x16 copy
 // deferred sample nablas (sdf4_kernel STAGE 1 / 2): stage 1 = sdf + slabs per 16-point tile into
 // `slabs` (P/16 x kSlabColBytes); stage 2 = nablas of the tiles tiles[0 .. *n_tiles) from their slabs;
-// stage 4 = nablas of the points tiles[0 .. *n_tiles) (P <= kDeferredCompactMax: the kernel addresses a
-// lane's slab codes with 32-bit byte offsets)
-constexpr int64_t kDeferredCompactMax = ((int64_t)1 << 32) / kSlabColBytes * 16 - 16;
+// stage 4 = nablas of the points tiles[0 .. *n_tiles) (neus_point_list's layout: 16-aligned segments of
+// slots within one 1024-slot range, padded with -1)
 int launch_sdf_deferred(const SdfLayout& L, const void* packed, const float* pts, int64_t P, float* sdf, float* nabla,
                         int nfreq, float4* slabs, const int* tiles, const int* n_tiles, int stage, hipStream_t stream);
 int launch_nerf(const NerfLayout& L, const void* packed, const float* x4, const float* vdir, int64_t vdiv,

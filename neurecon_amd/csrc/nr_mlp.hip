@@ -1733,13 +1733,20 @@ void sdf4_kernel(SdfKArgs a) {
     int plane = lane;                      // float4 index of this lane's slab-7 / parked entries
     uint32_t soff = 0;                     // byte offset of this lane's slab codes (COMPACT)
     int64_t pl = 0;                        // this lane's listed point (COMPACT)
-    if constexpr (COMPACT) {  // list entries [p0, p0 + 16): one point per lane j (the last again past the end)
+    bool listed = true;
+    if constexpr (COMPACT) {  // list entries [p0, p0 + 16): one slot per lane j, -1 = padding (invalid)
+      // neus_point_list: the 16 entries of a wave are one segment's, in slot order, the first one a slot,
+      // all within 64 tiles of it -- which is the wave's slab base (past the list's end: the last wave's)
       const int64_t n = *a.n_tiles;
-      pl = a.tiles[min(p0 + j, n - 1)];
-      const uint32_t ts = (uint32_t)(pl >> 4), js = (uint32_t)(pl & 15);
-      plane = (int)(ts * (uint32_t)(kSlabColBytes / 16) + js + 16u * (uint32_t)g);
-      soff = ts * (uint32_t)kSlabColBytes + (js + 16u * (uint32_t)g) * (uint32_t)kSlabVB;
-      escr = uniform_ptr(a.slabs);
+      const int64_t w0 = p0 < n ? p0 : n - 16;
+      const int e = a.tiles[w0 + j];
+      const int e0 = __builtin_amdgcn_readfirstlane(a.tiles[w0]);
+      listed = p0 < n && e >= 0;
+      pl = e >= 0 ? e : e0;
+      const uint32_t rt = (uint32_t)((pl >> 4) - (e0 >> 4)), js = (uint32_t)(pl & 15);  // rt < 64
+      plane = (int)(rt * (uint32_t)(kSlabColBytes / 16) + js + 16u * (uint32_t)g);
+      soff = rt * (uint32_t)kSlabColBytes + (js + 16u * (uint32_t)g) * (uint32_t)kSlabVB;
+      escr = uniform_ptr((float4*)((char*)a.slabs + (size_t)(e0 >> 4) * kSlabColBytes));
     } else if constexpr (STAGE == 2) {  // this wave's tile (the last one again past the list's end: nothing stored)
       const int64_t ti = min(p0 / 16, (int64_t)(*a.n_tiles) - 1);
       const int64_t tile = a.tiles[ti];
@@ -1756,7 +1763,7 @@ void sdf4_kernel(SdfKArgs a) {
     for (int q = 0; q < kNC; ++q) {
       const int64_t p = p0 + 16 * q + j;
       if constexpr (COMPACT) {
-        valid[q] = p < (int64_t)(*a.n_tiles);
+        valid[q] = listed;
         pq[q] = pl;
       } else {
         valid[q] = p < Pv;
@@ -3975,8 +3982,8 @@ int launch_sdf_deferred(const SdfLayout& L, const void* packed, const float* pts
   } else if (stage == 2) {
     ProfScope prof("sdf_nabla_bwd", (double)P, stream, n_tiles, 16);
     hipLaunchKernelGGL((sdf4_kernel<true, false, 2>), dim3(grid_for(P)), dim3(kT4), 0, stream, a);
-  } else {  // 4: `tiles` lists sample slots (the per-lane 32-bit slab offsets: P < kDeferredCompactMax)
-    NR_REQUIRE(stage == 4 && P <= kDeferredCompactMax, NR_ERR_ARG, "deferred nablas: bad stage");
+  } else {  // 4: `tiles` lists sample slots (neus_point_list); the units count its padding too
+    NR_REQUIRE(stage == 4, NR_ERR_ARG, "deferred nablas: bad stage");
     ProfScope prof("sdf_nabla_bwd", (double)P, stream, n_tiles, 1);
     hipLaunchKernelGGL((sdf4_kernel<true, false, 4>), dim3(grid_for(P)), dim3(kT4), 0, stream, a);
   }

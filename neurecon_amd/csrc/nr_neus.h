@@ -26,8 +26,9 @@ struct NeusChunk {
   // 16-slot tile's slabs in `slabs` (sdf4_kernel STAGE 1); the tiles holding a sample whose interval
   // weight can be non-zero are flagged (tflag), listed (tiles / tcnt) and get their nablas in one
   // reverse-pass launch (STAGE 2); the rest of nraw stays 0 (those samples are weighted by exactly 0).
-  // tshift 0: the flags and the list are per sample slot, and the reverse pass runs on the listed
-  // samples alone (STAGE 4, sdf4_kernel); 4: per 16-slot tile
+  // tshift 0: the flags are per sample slot, the list (neus_point_list) holds the flagged slots in
+  // 16-aligned segments, and the reverse pass runs on the listed samples alone (STAGE 4, sdf4_kernel);
+  // 4: flags and list per 16-slot tile (STAGE 2)
   float4* slabs; int* tflag; int* tiles; int* tcnt; int tshift;
   float* sdf_m; float* nab_m; float* feat_m; float* rad_m;
   // NeRF++ background (N_out = 0: none); M = S-1+N_out samples, sample-major
@@ -68,6 +69,7 @@ bool neus_deferred(const NrNeusArgs& a, int64_t R);
 int neus_total_samples(const NrNeusArgs& a);
 __global__ void neus_sample_need(NeusChunk c, const float* s_dev, float s_val);
 __global__ void neus_tile_list(NeusChunk c, int64_t n_tiles);
+__global__ void neus_point_list(NeusChunk c, int64_t n_slots);
 __global__ void neus_sample_need_outside(NeusChunk c, const float* s_dev, float s_val);
 __global__ void neus_gather_nablas(NeusChunk c);
 

@@ -681,7 +681,36 @@ __global__ void neus_sample_need_outside(NeusChunk c, const float* __restrict__ 
   if (!(alpha == 0.0f)) c.tflag[((int64_t)c.idv[q] * R + r) >> c.tshift] = 1;
 }
 
-// flagged tiles (or sample slots, tshift 0) -> list (any order: each point's nabla depends on that point alone)
+// flagged sample slots -> list for the compacted reverse pass (sdf4_kernel STAGE 4): each 1024-slot
+// workgroup appends its flagged slots in slot order as one segment padded with -1 to a multiple of 16
+// entries (one atomic per workgroup), so the 16 entries a wave takes come from one 1024-slot range:
+// within 64 tiles of the segment's first entry (the kernel's per-lane slab offsets stay small)
+__global__ __launch_bounds__(1024) void neus_point_list(NeusChunk c, int64_t n_slots) {
+  __shared__ int wcnt[16];
+  __shared__ int bbase, btot;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool need = t < n_slots && c.tflag[t] != 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint64_t bal = __ballot(need);
+  if (lane == 0) wcnt[w] = __popcll(bal);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int i = 0; i < nw; ++i) {
+      const int v = wcnt[i];
+      wcnt[i] = s;
+      s += v;
+    }
+    btot = s;
+    bbase = s ? atomicAdd(c.tcnt, (s + 15) & ~15) : 0;
+  }
+  __syncthreads();
+  if (need) c.tiles[(int64_t)bbase + wcnt[w] + __popcll(bal & ((1ull << lane) - 1ull))] = (int)t;
+  const int pad = ((btot + 15) & ~15) - btot;
+  if ((int)threadIdx.x < pad) c.tiles[(int64_t)bbase + btot + threadIdx.x] = -1;
+}
+
+// flagged tiles -> list (any order: each tile's nablas depend on that tile alone)
 __global__ void neus_tile_list(NeusChunk c, int64_t n_tiles) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool need = t < n_tiles && c.tflag[t] != 0;
@@ -1044,10 +1073,10 @@ NeusPlan neus_plan(const NrNeusArgs& a, int64_t Rc) {
   p.o_idv2 = take((size_t)S * Rc);
   const size_t tiles = neus_deferred(a, Rc) ? ((size_t)S * Rc + 15) / 16 : 1;
   p.o_slabs = take(neus_deferred(a, Rc) ? tiles * (kSlabColBytes / 4) : 1);  // 100 KB per 16-slot tile
-  // flags and list per sample slot (the compacted reverse pass) or per tile (chunks past kDeferredCompactMax)
+  // flags per sample slot; the list (neus_point_list) pads each 1024-slot segment to 16 entries
   const size_t slots = neus_deferred(a, Rc) ? (size_t)S * Rc : 1;
   p.o_tflag = take(slots);
-  p.o_tiles = take(slots);
+  p.o_tiles = take(slots + 16 * ((slots + 1023) / 1024));
   p.o_tcnt = take(1);
   p.o_mlp = off;
   p.total = off + nr_mlp_workspace_bytes(1);
