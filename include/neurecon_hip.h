@@ -211,8 +211,8 @@ typedef struct {
   int no_mid_skip;
   /* Deferred sample nablas (official_solution render without the per-sample nablas / radiance outputs,
    * f16x3 softplus net, chunks of a multiple of 16 rays; with NeRF++ too, flagged after the background
-   * net): the sample launches leave their reverse-pass state per 16-sample tile and only the tiles
-   * holding a sample of non-zero interval weight run the reverse pass; the other samples' nablas are
+   * net): the sample launches leave their reverse-pass state per 16-sample tile and only the samples
+   * of non-zero interval weight run the reverse pass (listed one by one); the other samples' nablas are
    * weighted by exactly 0 in normals_volume (neus.py:364-368).  Maps bit-identical; the workspace then
    * holds 8 KB per sample of a chunk (sized by max_workspace_bytes below).  no_defer != 0: nablas at
    * every sample when drawn. */
